@@ -1,0 +1,283 @@
+#!/usr/bin/env python3
+"""Headline benchmark: output tokens/s + p50 TTFT of streaming /v1/chat/completions on a
+random-init Llama-3-8B-Instruct GGUF (Q4_K_M mix) -- BASELINE.json's metric and config.
+
+One "step" = one wave of `--concurrency` concurrent streaming chat completions per GPU,
+each with a synthetic ~`--prompt-len`-token user message and `--max-tokens` generated
+tokens (ignore_eos, temperature 0, mirostat 0 -- SURVEY §6 / BASELINE.md).  W untimed
+warm-up waves, then exactly K timed waves bracketed by barrier + synchronize.
+
+Multi-GPU (torchrun, one process per GPU): data-parallel engine replicas (weak scaling:
+fixed per-GPU load), aggregate tokens/s = sum over ranks / max wall time over ranks.
+
+--mode http   : requests go through the real gateway (FastAPI app served by uvicorn on
+                127.0.0.1, aiohttp SSE client) -> gateway -> engine (default)
+--mode engine : requests are fed to the engine directly (no HTTP), for kernel work
+"""
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "output tokens/sec + p50 TTFT, /v1/chat/completions Llama-3-8B GGUF, 1/2/4/8 GPU"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--concurrency", type=int, default=int(os.environ.get("BENCH_CONCURRENCY", 64)))
+    ap.add_argument("--prompt-len", type=int, default=128)
+    ap.add_argument("--max-tokens", type=int, default=256)
+    ap.add_argument("--preset", default=os.environ.get("BENCH_PRESET", "llama3-8b"))
+    ap.add_argument("--mode", default=os.environ.get("BENCH_MODE", "http"), choices=["http", "engine"])
+    ap.add_argument("--context", type=int, default=2048)
+    ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--cache-dir", default=os.environ.get("LOCALAI_AMD_CACHE", "/tmp/localai_amd_cache"))
+    return ap.parse_args()
+
+
+def user_messages(tok, n, plen, seed=0):
+    import random
+    rnd = random.Random(seed)
+    words = ["the", "model", "server", "token", "request", "graph", "kernel", "memory", "stream", "batch",
+             "latency", "context", "python", "value", "system", "answer", "question", "data", "quick", "brown"]
+    out = []
+    for i in range(n):
+        ws = []
+        while len(tok.encode(" ".join(ws), add_bos=False)) < plen - 24:
+            ws.extend(rnd.choice(words) for _ in range(8))
+        out.append(f"Request {i}: " + " ".join(ws))
+    return out
+
+
+def percentile(xs, p):
+    xs = sorted(xs)
+    if not xs:
+        return 0.0
+    k = (len(xs) - 1) * p / 100.0
+    f = int(k)
+    c = min(f + 1, len(xs) - 1)
+    return xs[f] + (xs[c] - xs[f]) * (k - f)
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    dev = f"cuda:{local}"
+
+    from localai_amd.models import synth
+
+    os.makedirs(args.cache_dir, exist_ok=True)
+    path = os.path.join(args.cache_dir, f"{args.preset}.gguf")
+    t_gen = time.time()
+    if rank == 0 and not os.path.exists(path):
+        synth.write_model(path + f".partial{os.getpid()}", args.preset)
+        os.replace(path + f".partial{os.getpid()}", path)
+    if world > 1:
+        dist.barrier()
+    t_gen = time.time() - t_gen
+
+    from localai_amd.engine.llm_engine import EngineConfig, LLMEngine
+
+    t0 = time.time()
+    cfg = EngineConfig(model_path=path, device=dev, context_size=args.context,
+                       max_num_seqs=max(args.concurrency, 1), max_batched_tokens=max(8192, args.prompt_len * 8),
+                       use_graphs=not args.no_graphs,
+                       max_kv_tokens=args.concurrency * (args.prompt_len + args.max_tokens + 64) + 4096)
+    eng = LLMEngine(cfg)
+    t_load = time.time() - t0
+    t0 = time.time()
+    eng.warmup()
+    t_capture = time.time() - t0
+
+    msgs = user_messages(eng.tokenizer, args.concurrency, args.prompt_len, seed=rank)
+    if args.mode == "http":
+        runner = HttpRunner(eng, args)
+    else:
+        runner = EngineRunner(eng, args)
+
+    def wave(w):
+        return runner.wave([m + f" (wave {w})" for m in msgs])
+
+    for w in range(args.warmup):
+        wave(-1 - w)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ttfts, tokens = [], 0
+    for s in range(args.steps):
+        tt, nt = wave(s)
+        ttfts += tt
+        tokens += nt
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+
+    all_ttft, tot_tokens, max_el = ttfts, tokens, elapsed
+    if world > 1:
+        el = torch.tensor([elapsed], device=dev)
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        nt = torch.tensor([float(tokens)], device=dev)
+        dist.all_reduce(nt)
+        gathered = [None] * world
+        dist.all_gather_object(gathered, ttfts)
+        all_ttft = [x for g in gathered for x in g]
+        max_el, tot_tokens = float(el.item()), int(nt.item())
+    runner.close()
+    if rank == 0:
+        value = tot_tokens / max_el
+        seq = args.prompt_len + args.max_tokens
+        out = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "tokens/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(max_el / args.steps * 1000, 2),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic",
+            "p50_ttft_ms": round(percentile(all_ttft, 50) * 1000, 2),
+            "p90_ttft_ms": round(percentile(all_ttft, 90) * 1000, 2),
+            "config": {"model": "Llama-3-8B-Instruct GGUF Q4_K_M (random-init)" if args.preset == "llama3-8b"
+                       else args.preset, "global_batch": args.concurrency * world, "seq_len": seq,
+                       "prompt_tokens": args.prompt_len, "max_tokens": args.max_tokens,
+                       "parallelism": f"dp{world}", "endpoint": "/v1/chat/completions (stream)",
+                       "mode": args.mode, "sampling": "greedy, mirostat 0, ignore_eos"},
+            "setup_s": {"model_gen": round(t_gen, 1), "load": round(t_load, 1), "graph_capture": round(t_capture, 1)},
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+class EngineRunner:
+    """Feeds chat-templated prompts straight into the engine (no HTTP)."""
+
+    def __init__(self, eng, args):
+        self.eng, self.args = eng, args
+        from localai_amd.engine.sampling_params import SamplingParams
+        self.SP = SamplingParams
+
+    def wave(self, contents):
+        eng = self.eng
+        ttft, ntok = [], [0]
+        done = [0]
+        lock = threading.Lock()
+        t_start = {}
+        for i, c in enumerate(contents):
+            prompt = ("<|begin_of_text|><|start_header_id|>user<|end_header_id|>\n\n" + c +
+                      "<|eot_id|>\n<|start_header_id|>assistant<|end_header_id|>")
+            first = [True]
+            t0 = time.perf_counter()
+
+            def cb(ev, first=first, t0=t0):
+                with lock:
+                    if first[0] and (ev.text or ev.finished):
+                        first[0] = False
+                        ttft.append(time.perf_counter() - t0)
+                    if ev.finished:
+                        ntok[0] += ev.completion_tokens
+                        done[0] += 1
+
+            eng.add_request(prompt, self.SP(max_tokens=self.args.max_tokens, temperature=0.0, ignore_eos=True,
+                                            mirostat=0, repeat_penalty=1.0), cb)
+        while done[0] < len(contents):
+            eng.step()
+        return ttft, ntok[0]
+
+    def close(self):
+        pass
+
+
+class HttpRunner:
+    """Real gateway over HTTP: uvicorn serving the FastAPI app, aiohttp SSE clients."""
+
+    def __init__(self, eng, args):
+        import asyncio
+        import socket
+        from localai_amd.gateway.app import create_app_for_engine
+        self.args = args
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        self.port = s.getsockname()[1]
+        s.close()
+        self.app, self.model_name = create_app_for_engine(eng, name="llama3-8b-instruct")
+        import uvicorn
+        cfg = uvicorn.Config(self.app, host="127.0.0.1", port=self.port, log_level="warning", loop="asyncio",
+                             http="h11", access_log=False)
+        self.server = uvicorn.Server(cfg)
+        self.th = threading.Thread(target=self.server.run, daemon=True)
+        self.th.start()
+        for _ in range(600):
+            if self.server.started:
+                break
+            time.sleep(0.05)
+        self.loop = asyncio.new_event_loop()
+
+    def wave(self, contents):
+        return self.loop.run_until_complete(self._wave(contents))
+
+    async def _wave(self, contents):
+        import asyncio
+        import aiohttp
+        url = f"http://127.0.0.1:{self.port}/v1/chat/completions"
+        conn = aiohttp.TCPConnector(limit=0)
+        timeout = aiohttp.ClientTimeout(total=3600)
+        async with aiohttp.ClientSession(connector=conn, timeout=timeout) as sess:
+            async def one(c):
+                body = {"model": self.model_name, "stream": True, "max_tokens": self.args.max_tokens,
+                        "temperature": 0, "ignore_eos": True, "mirostat": 0,
+                        "messages": [{"role": "user", "content": c}]}
+                t0 = time.perf_counter()
+                ttft = None
+                ntok = 0
+                async with sess.post(url, json=body) as resp:
+                    resp.raise_for_status()
+                    async for raw in resp.content:
+                        line = raw.strip()
+                        if not line.startswith(b"data:"):
+                            continue
+                        data = line[5:].strip()
+                        if data == b"[DONE]":
+                            break
+                        ev = json.loads(data)
+                        ch = ev.get("choices") or [{}]
+                        delta = ch[0].get("delta") or {}
+                        if ttft is None and delta.get("content"):
+                            ttft = time.perf_counter() - t0
+                        if ev.get("usage"):
+                            ntok = ev["usage"].get("completion_tokens", ntok)
+                return (ttft if ttft is not None else time.perf_counter() - t0), ntok
+            res = await asyncio.gather(*[one(c) for c in contents])
+        return [r[0] for r in res], sum(r[1] for r in res)
+
+    def close(self):
+        self.server.should_exit = True
+        self.th.join(timeout=10)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,420 @@
+"""Decoder-only transformer families served by the engine: llama (Llama-2/3, Mistral),
+llama+MoE (Mixtral), phi2.
+
+Replaces the llama.cpp graph the reference's backend drives through llama_decode
+(`backend/cpp/llama/grpc-server.cpp:1910`, [external]).  The forward pass is a fixed
+sequence of our gfx950 kernels (ops/csrc):
+
+  embed(K1) -> [ add_norm(K2+K14) -> QKV skinny/hipBLASLt GEMM (K5/K6) -> rope_kv (K9+K10)
+             -> paged attention (K12) -> O GEMM -> add_norm -> gate|up GEMM -> act (K13)
+             -> down GEMM ] x L -> add_norm -> lm_head GEMM -> on-device sampler (K22)
+
+Tensor parallelism (one process per GPU, RCCL over xGMI via torch.distributed "nccl"):
+column-parallel QKV / gate|up (heads and FFN columns split), row-parallel O / down
+(K split along 256-aligned super-blocks), one all-reduce after each row-parallel GEMM,
+vocab-parallel lm_head + all-gather.  Experts (Mixtral) are split the same way
+(TP-within-expert).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from .. import ops
+from ..gguf import GGML_BLOCK, GGMLType, GGUFReader, dequantize
+from .hparams import HParams
+
+
+@dataclass
+class TPInfo:
+    rank: int = 0
+    world: int = 1
+    group: object = None
+
+    def all_reduce(self, t: torch.Tensor):
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.all_reduce(t, group=self.group)
+        return t
+
+    def all_gather_cols(self, t: torch.Tensor) -> torch.Tensor:
+        if self.world == 1:
+            return t
+        import torch.distributed as dist
+        parts = [torch.empty_like(t) for _ in range(self.world)]
+        dist.all_gather(parts, t.contiguous(), group=self.group)
+        return torch.cat(parts, -1)
+
+
+@dataclass
+class ForwardBatch:
+    tokens: torch.Tensor                 # [T] i32
+    pos: torch.Tensor                    # [T] i32
+    slots: torch.Tensor                  # [T] i32  (-1: no KV write)
+    decode: bool
+    block_tables: torch.Tensor           # [nseq, maxb] i32
+    seq_lens: Optional[torch.Tensor] = None   # decode: [B] i32 (keys incl. the new one)
+    max_len: int = 0                          # decode: upper bound of seq_lens
+    cu_q: Optional[torch.Tensor] = None       # prefill: [nseq+1] i32
+    ctx_lens: Optional[torch.Tensor] = None   # prefill: [nseq] i32
+    tiles: Optional[torch.Tensor] = None      # prefill: attention work tiles
+    logits_idx: Optional[torch.Tensor] = None  # rows to project to logits (None: all)
+
+
+class KVCache:
+    """Per-layer paged K/V pools: [num_blocks, Hkv_local, block_size, head_dim] bf16."""
+
+    def __init__(self, n_layer: int, num_blocks: int, n_kv: int, block_size: int, head_dim: int, device,
+                 dtype=torch.bfloat16):
+        self.num_blocks, self.block_size = num_blocks, block_size
+        self.k = [torch.zeros(num_blocks, n_kv, block_size, head_dim, dtype=dtype, device=device)
+                  for _ in range(n_layer)]
+        self.v = [torch.zeros(num_blocks, n_kv, block_size, head_dim, dtype=dtype, device=device)
+                  for _ in range(n_layer)]
+
+    @staticmethod
+    def bytes_per_block(n_layer, n_kv, block_size, head_dim, dtype_bytes=2):
+        return 2 * n_layer * n_kv * block_size * head_dim * dtype_bytes
+
+
+@dataclass
+class Layer:
+    attn_norm: torch.Tensor
+    attn_norm_b: Optional[torch.Tensor]
+    qkv: List[ops.QWeight]
+    qkv_bias: Optional[torch.Tensor]
+    wo: ops.QWeight
+    wo_bias: Optional[torch.Tensor]
+    ffn_norm: Optional[torch.Tensor]
+    ffn_norm_b: Optional[torch.Tensor]
+    gate_up: List[ops.QWeight]
+    up_bias: Optional[torch.Tensor]
+    down: Optional[ops.QWeight]
+    down_bias: Optional[torch.Tensor]
+    router: Optional[torch.Tensor] = None            # [E, D] f32 (MoE)
+    experts: Optional[List[tuple]] = None            # [(gate_up list, down)] per expert
+
+
+def _raw2d(t, rows: Optional[slice] = None, cols: Optional[slice] = None):
+    """Slice a GGUF tensor's raw bytes as a 2-D [N, K] matrix by rows and/or column blocks."""
+    N, K = t.shape[-2], t.shape[-1]
+    bs, bb = GGML_BLOCK[t.ggml_type]
+    a = t.data.reshape(-1, K // bs, bb)
+    if rows is not None:
+        a = a[rows]
+    n = a.shape[0]
+    k = K
+    if cols is not None:
+        b0, b1 = cols.start // bs, cols.stop // bs
+        a = a[:, b0:b1]
+        k = cols.stop - cols.start
+    return np.ascontiguousarray(a).reshape(-1), (n, k)
+
+
+class DecoderModel:
+    def __init__(self, reader: GGUFReader, device: torch.device, tp: Optional[TPInfo] = None,
+                 max_pos: Optional[int] = None, rope_overrides: Optional[dict] = None):
+        self.hp = hp = HParams.from_gguf(reader)
+        self.device = device
+        self.tp = tp = tp or TPInfo()
+        W, R = tp.world, tp.rank
+        if hp.n_head % W or hp.n_head_kv % W:
+            raise ValueError(f"TP={W} must divide heads ({hp.n_head}/{hp.n_head_kv})")
+        self.Hq, self.Hkv, self.Dh = hp.n_head // W, hp.n_head_kv // W, hp.head_dim
+        self.F = hp.n_ff // W
+        self.rot = hp.rope_dim or hp.head_dim
+        self.scale = 1.0 / math.sqrt(hp.head_dim)
+        self.norm_mode = 0 if hp.norm_type == "rms" else 1
+        T = reader.tensors
+        dev = device
+        def f32(name):
+            if name not in T:
+                return None
+            t = T[name]
+            arr = dequantize(t.data, t.ggml_type, t.shape).reshape(-1).astype(np.float32)
+            return torch.from_numpy(arr).to(dev)
+
+        def qw(name, rows=None, cols=None):
+            t = T[name]
+            raw, shape = _raw2d(t, rows, cols)
+            return ops.QWeight.from_raw(raw, t.ggml_type, shape, dev)
+
+        def sl(n_total, part=None):
+            n = n_total // W
+            return slice(R * n, (R + 1) * n)
+
+        def vec_slice(v, s):
+            return None if v is None else v[s].contiguous()
+
+        qd, kvd = hp.q_dim, hp.kv_dim
+        self.tok_embd = qw("token_embd.weight")
+        self.layers: List[Layer] = []
+        for i in range(hp.n_layer):
+            b = f"blk.{i}."
+            qs, ks = sl(qd), sl(kvd)
+            if hp.arch == "phi2":
+                qkv_name = b + "attn_qkv.weight"
+                qkv = [qw(qkv_name, rows=slice(qs.start, qs.stop)),
+                       qw(qkv_name, rows=slice(qd + ks.start, qd + ks.stop)),
+                       qw(qkv_name, rows=slice(qd + kvd + ks.start, qd + kvd + ks.stop))]
+                qb = f32(b + "attn_qkv.bias")
+                qkv_bias = None if qb is None else torch.cat([qb[qs], qb[qd + ks.start:qd + ks.stop],
+                                                              qb[qd + kvd + ks.start:qd + kvd + ks.stop]])
+            else:
+                qkv = [qw(b + "attn_q.weight", rows=qs), qw(b + "attn_k.weight", rows=ks),
+                       qw(b + "attn_v.weight", rows=ks)]
+                qkv_bias = None
+                if b + "attn_q.bias" in T:
+                    qkv_bias = torch.cat([f32(b + "attn_q.bias")[qs], f32(b + "attn_k.bias")[ks],
+                                          f32(b + "attn_v.bias")[ks]])
+            fused = ops.concat_rows(qkv)
+            if fused is not None:
+                qkv = [fused]
+            wo = qw(b + "attn_output.weight", cols=sl(qd))
+            wo_b = f32(b + "attn_output.bias")
+            if wo_b is not None and R != 0:
+                wo_b = torch.zeros_like(wo_b)  # bias added once across TP ranks
+            fs = sl(hp.n_ff)
+            router = experts = None
+            gate_up, down, up_b, down_b = [], None, None, None
+            if hp.n_expert:
+                router = torch.from_numpy(np.frombuffer(T[b + "ffn_gate_inp.weight"].data, dtype=np.float32)
+                                          .reshape(hp.n_expert, hp.n_embd).copy()).to(dev)
+                experts = []
+                for e in range(hp.n_expert):
+                    ge = self._expert_slice(T[b + "ffn_gate_exps.weight"], e, rows=fs)
+                    ue = self._expert_slice(T[b + "ffn_up_exps.weight"], e, rows=fs)
+                    de = self._expert_slice(T[b + "ffn_down_exps.weight"], e, cols=sl(hp.n_ff))
+                    gu = ops.concat_rows([ge, ue])
+                    experts.append(([gu] if gu is not None else [ge, ue], de))
+            elif hp.arch == "phi2":
+                gate_up = [qw(b + "ffn_up.weight", rows=fs)]
+                up_b = vec_slice(f32(b + "ffn_up.bias"), fs)
+                down = qw(b + "ffn_down.weight", cols=fs)
+                down_b = f32(b + "ffn_down.bias")
+                if down_b is not None and R != 0:
+                    down_b = torch.zeros_like(down_b)
+            else:
+                g, u = qw(b + "ffn_gate.weight", rows=fs), qw(b + "ffn_up.weight", rows=fs)
+                gu = ops.concat_rows([g, u])
+                gate_up = [gu] if gu is not None else [g, u]
+                down = qw(b + "ffn_down.weight", cols=fs)
+            self.layers.append(Layer(
+                attn_norm=f32(b + "attn_norm.weight"), attn_norm_b=f32(b + "attn_norm.bias"),
+                qkv=qkv, qkv_bias=qkv_bias, wo=wo, wo_bias=wo_b,
+                ffn_norm=f32(b + "ffn_norm.weight"), ffn_norm_b=f32(b + "ffn_norm.bias"),
+                gate_up=gate_up, up_bias=up_b, down=down, down_bias=down_b,
+                router=router, experts=experts))
+        self.out_norm = f32("output_norm.weight")
+        self.out_norm_b = f32("output_norm.bias")
+        vs = sl(hp.n_vocab)
+        self.vocab_local = vs.stop - vs.start
+        if hp.n_vocab % W:
+            raise ValueError("TP must divide the vocabulary")
+        out_name = "output.weight" if "output.weight" in T else "token_embd.weight"
+        self.output = qw(out_name, rows=vs)
+        ob = f32("output.bias")
+        self.out_bias = None if ob is None else ob[vs].contiguous()
+        rope_freqs = f32("rope_freqs.weight")
+        self.max_pos = max_pos or hp.n_ctx_train
+        ro = rope_overrides or {}
+        theta = ro.get("freq_base") or hp.rope_theta
+        fscale = ro.get("freq_scale") or hp.rope_freq_scale
+        self.cos_sin = ops.rope_cos_sin(self.max_pos, self.rot, theta, dev, freq_scale=fscale,
+                                        freq_factors=rope_freqs, rope_type=ro.get("type", hp.rope_scaling),
+                                        yarn=ro.get("yarn"))
+
+    def _expert_slice(self, t, e, rows=None, cols=None):
+        E = t.shape[0]
+        N, K = t.shape[1], t.shape[2]
+        bs, bb = GGML_BLOCK[t.ggml_type]
+        per = N * K // bs * bb
+        sub = type("T", (), {})()
+        sub.shape, sub.ggml_type = (N, K), t.ggml_type
+        sub.data = t.data[e * per:(e + 1) * per]
+        raw, shape = _raw2d(sub, rows, cols)
+        return ops.QWeight.from_raw(raw, t.ggml_type, shape, self.device)
+
+    # --------------------------------------------------------------------------- forward
+    def new_kv_cache(self, num_blocks: int, block_size: int) -> KVCache:
+        return KVCache(self.hp.n_layer, num_blocks, self.Hkv, block_size, self.Dh, self.device)
+
+    def _row_parallel_out(self, p: ops.Partial, bias) -> ops.Partial:
+        if self.tp.world == 1:
+            return ops.Partial(p.t, bias)
+        dense = ops.reduce(p)
+        self.tp.all_reduce(dense)
+        return ops.Partial(dense.unsqueeze(0), bias)
+
+    def _mlp(self, L: Layer, xn: torch.Tensor) -> ops.Partial:
+        hp = self.hp
+        if L.experts is not None:
+            return self._moe(L, xn)
+        gu = ops.linear_multi(xn, L.gate_up, bias=L.up_bias)
+        h = ops.act(gu, self.F, ops.ACT_SWIGLU if hp.act == "swiglu" else ops.ACT_GELU)
+        d = ops.linear(h, L.down)
+        return self._row_parallel_out(d, L.down_bias)
+
+    def _moe(self, L: Layer, xn: torch.Tensor) -> ops.Partial:
+        """Mixtral sparse MoE: softmax router, top-k, renormalised weights (K16/K18), per-expert
+        quantised GEMMs on the routed rows (K17), weighted scatter-add."""
+        hp = self.hp
+        T = xn.shape[0]
+        logits = xn.float() @ L.router.t()                       # [T, E]
+        w, idx = torch.topk(torch.softmax(logits, -1), hp.n_expert_used, -1)
+        w = w / w.sum(-1, keepdim=True)
+        out = torch.zeros(T, hp.n_embd, dtype=torch.float32, device=xn.device)
+        flat_e = idx.reshape(-1)
+        flat_t = torch.arange(T, device=xn.device).repeat_interleave(hp.n_expert_used)
+        flat_w = w.reshape(-1)
+        for e, (gate_up, down) in enumerate(L.experts):
+            sel = (flat_e == e).nonzero(as_tuple=True)[0]
+            if sel.numel() == 0:
+                continue
+            rows = flat_t[sel]
+            xe = xn.index_select(0, rows).contiguous()
+            gu = ops.linear_multi(xe, gate_up)
+            h = ops.act(gu, self.F, ops.ACT_SWIGLU)
+            d = ops.reduce(ops.linear(h, down))
+            out.index_add_(0, rows, d * flat_w[sel].unsqueeze(1))
+        self.tp.all_reduce(out)
+        return ops.Partial(out.unsqueeze(0))
+
+    def forward(self, fb: ForwardBatch, kv: KVCache, attn_workspace=None, return_hidden: bool = False) -> torch.Tensor:
+        """Returns fp32 logits [R, V] for the rows selected by fb.logits_idx (or, with
+        return_hidden, the final-norm hidden states [T, D])."""
+        hp = self.hp
+        eps, nm = hp.norm_eps, self.norm_mode
+        T = fb.tokens.shape[0]
+        res = ops.embed(fb.tokens, self.tok_embd)
+        L0 = self.layers[0]
+        xn = ops.add_norm(res, None, L0.attn_norm, L0.attn_norm_b, eps, nm)
+        n = len(self.layers)
+        for i, L in enumerate(self.layers):
+            qkv = ops.linear_multi(xn, L.qkv, bias=L.qkv_bias)
+            q = ops.rope_kv(qkv, fb.pos, fb.slots, self.cos_sin, self.Hq, self.Hkv, self.Dh, self.rot, hp.rope_mode,
+                            kv.k[i], kv.v[i], kv.block_size)
+            if fb.decode:
+                a = ops.attn_decode(q, kv.k[i], kv.v[i], fb.block_tables, fb.seq_lens, self.scale, fb.max_len,
+                                    workspace=attn_workspace)
+            else:
+                a = ops.attn_prefill(q, kv.k[i], kv.v[i], fb.cu_q, fb.ctx_lens, fb.block_tables, self.scale,
+                                     tiles=fb.tiles)
+            o = self._row_parallel_out(ops.linear(a.view(T, self.Hq * self.Dh), L.wo), L.wo_bias)
+            nxt = self.layers[i + 1] if i + 1 < n else None
+            nw = nxt.attn_norm if nxt is not None else self.out_norm
+            nb = nxt.attn_norm_b if nxt is not None else self.out_norm_b
+            if hp.parallel_residual:
+                f = self._mlp(L, xn)
+                ops.add_norm(res, o, nw, nb, eps, nm, want_out=False)
+                xn = ops.add_norm(res, f, nw, nb, eps, nm)
+            else:
+                xn = ops.add_norm(res, o, L.ffn_norm, L.ffn_norm_b, eps, nm)
+                f = self._mlp(L, xn)
+                xn = ops.add_norm(res, f, nw, nb, eps, nm)
+        if return_hidden:
+            return xn
+        rows = xn if fb.logits_idx is None else xn.index_select(0, fb.logits_idx)
+        lp = ops.linear(rows.contiguous(), self.output, bias=self.out_bias)
+        if lp.S == 1 and lp.bias is None:
+            logits = lp.t[0]
+        else:
+            logits = ops.reduce(lp)
+        return self.tp.all_gather_cols(logits)
+
+    def reference_logits(self, tokens: Sequence[int]) -> torch.Tensor:
+        """Plain fp32 PyTorch forward of one sequence (no paging): the numerics oracle for the
+        GPU engine and for the TP tests.  Uses dequantised weights."""
+        hp = self.hp
+        dev = torch.device("cpu")
+        t = torch.tensor(tokens, dtype=torch.long)
+        Tn = len(tokens)
+        x = self.tok_embd.dequant_f32().to(dev)[t] if self.tok_embd.ref is not None else \
+            self.tok_embd.materialize_bf16().float().cpu()[t]
+
+        def deq(w):
+            return (w.ref if w.ref is not None else w.materialize_bf16().float()).cpu()
+
+        def norm(x, w, b):
+            if self.norm_mode == 0:
+                return x * torch.rsqrt(x.pow(2).mean(-1, keepdim=True) + hp.norm_eps) * w.cpu()
+            mu = x.mean(-1, keepdim=True)
+            y = (x - mu) * torch.rsqrt((x - mu).pow(2).mean(-1, keepdim=True) + hp.norm_eps) * w.cpu()
+            return y + b.cpu() if b is not None else y
+
+        cs = self.cos_sin.cpu()[:Tn]
+        c, s = cs[..., 0], cs[..., 1]
+
+        def rope(h):
+            h = h.clone()
+            r = self.rot
+            if hp.rope_mode == 0:
+                x0, x1 = h[..., 0:r:2].clone(), h[..., 1:r:2].clone()
+                h[..., 0:r:2] = x0 * c[:, None] - x1 * s[:, None]
+                h[..., 1:r:2] = x0 * s[:, None] + x1 * c[:, None]
+            else:
+                hf = r // 2
+                x0, x1 = h[..., :hf].clone(), h[..., hf:r].clone()
+                h[..., :hf] = x0 * c[:, None] - x1 * s[:, None]
+                h[..., hf:r] = x0 * s[:, None] + x1 * c[:, None]
+            return h
+
+        Hq, Hkv, Dh = self.Hq, self.Hkv, self.Dh
+        mask = torch.triu(torch.full((Tn, Tn), float("-inf")), 1)
+        for L in self.layers:
+            h = norm(x, L.attn_norm, L.attn_norm_b)
+            qkv = torch.cat([h @ deq(w).t() for w in L.qkv], -1)
+            if L.qkv_bias is not None:
+                qkv = qkv + L.qkv_bias.cpu()
+            q = rope(qkv[:, :Hq * Dh].view(Tn, Hq, Dh))
+            k = rope(qkv[:, Hq * Dh:(Hq + Hkv) * Dh].view(Tn, Hkv, Dh))
+            v = qkv[:, (Hq + Hkv) * Dh:].view(Tn, Hkv, Dh)
+            G = Hq // Hkv
+            k = k.repeat_interleave(G, 1)
+            v = v.repeat_interleave(G, 1)
+            att = torch.einsum("qhd,khd->hqk", q, k) * self.scale + mask
+            a = torch.einsum("hqk,khd->qhd", torch.softmax(att, -1), v).reshape(Tn, Hq * Dh)
+            o = a @ deq(L.wo).t()
+            if L.wo_bias is not None:
+                o = o + L.wo_bias.cpu()
+
+            def mlp(hin):
+                if L.experts is not None:
+                    lg = hin @ L.router.cpu().t()
+                    w, idx = torch.topk(torch.softmax(lg, -1), hp.n_expert_used, -1)
+                    w = w / w.sum(-1, keepdim=True)
+                    out = torch.zeros_like(hin)
+                    for tt in range(Tn):
+                        for j in range(hp.n_expert_used):
+                            gu_w, dw = L.experts[int(idx[tt, j])]
+                            gu = torch.cat([hin[tt:tt + 1] @ deq(ww).t() for ww in gu_w], -1)
+                            ff = gu.shape[-1] // 2
+                            hh = torch.nn.functional.silu(gu[:, :ff]) * gu[:, ff:]
+                            out[tt] += w[tt, j] * (hh @ deq(dw).t())[0]
+                    return out
+                gu = torch.cat([hin @ deq(w).t() for w in L.gate_up], -1)
+                if L.up_bias is not None:
+                    gu = gu + L.up_bias.cpu()
+                if hp.act == "swiglu":
+                    hh = torch.nn.functional.silu(gu[:, :self.F]) * gu[:, self.F:]
+                else:
+                    hh = torch.nn.functional.gelu(gu, approximate="tanh")
+                d = hh @ deq(L.down).t()
+                if L.down_bias is not None:
+                    d = d + L.down_bias.cpu()
+                return d
+
+            if hp.parallel_residual:
+                x = x + o + mlp(h)
+            else:
+                x = x + o
+                x = x + mlp(norm(x, L.ffn_norm, L.ffn_norm_b))
+        x = norm(x, self.out_norm, self.out_norm_b)
+        lg = x @ deq(self.output).t()
+        if self.out_bias is not None:
+            lg = lg + self.out_bias.cpu()
+        return lg

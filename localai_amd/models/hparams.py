@@ -1,0 +1,89 @@
+"""Model hyper-parameters read from GGUF metadata (llama.cpp's llm_load_hparams equivalent)."""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Optional
+
+
+@dataclass
+class HParams:
+    arch: str
+    n_layer: int
+    n_embd: int
+    n_head: int
+    n_head_kv: int
+    head_dim: int
+    n_ff: int
+    n_vocab: int
+    n_ctx_train: int = 4096
+    rope_theta: float = 10000.0
+    rope_dim: int = 0                 # rotary dims (partial rotary for phi-2)
+    rope_mode: int = 0                # 0 = NORM (llama), 1 = NEOX (phi2, qwen2, ...)
+    rope_scaling: str = "none"
+    rope_freq_scale: float = 1.0
+    rope_orig_ctx: int = 0
+    norm_eps: float = 1e-5
+    norm_type: str = "rms"            # "rms" | "layer"
+    n_expert: int = 0
+    n_expert_used: int = 0
+    parallel_residual: bool = False   # phi-2: h = x + attn(ln x) + mlp(ln x)
+    act: str = "swiglu"               # "swiglu" | "gelu"
+    tied_embeddings: bool = False
+    name: str = ""
+
+    @property
+    def q_dim(self) -> int:
+        return self.n_head * self.head_dim
+
+    @property
+    def kv_dim(self) -> int:
+        return self.n_head_kv * self.head_dim
+
+    @staticmethod
+    def from_gguf(r) -> "HParams":
+        a = r.architecture
+        g = lambda k, d=None: r.kv.get(f"{a}.{k}", d)  # noqa: E731
+        n_embd = int(g("embedding_length"))
+        n_head = int(g("attention.head_count"))
+        n_head_kv = int(g("attention.head_count_kv", n_head))
+        head_dim = int(g("attention.key_length", n_embd // n_head))
+        tokens = r.kv.get("tokenizer.ggml.tokens") or []
+        n_vocab = int(g("vocab_size", len(tokens)))
+        if "token_embd.weight" in r.tensors:
+            n_vocab = r.tensors["token_embd.weight"].shape[0]
+        rope_dim = int(g("rope.dimension_count", head_dim))
+        neox_archs = {"phi2", "phi3", "qwen2", "qwen2moe", "gptneox", "stablelm", "gemma", "gemma2", "falcon"}
+        eps = g("attention.layer_norm_rms_epsilon")
+        norm_type = "rms"
+        if eps is None:
+            eps = g("attention.layer_norm_epsilon", 1e-5)
+            norm_type = "layer"
+        n_ff = g("feed_forward_length")
+        if isinstance(n_ff, list):
+            n_ff = n_ff[0]
+        hp = HParams(
+            arch=a,
+            n_layer=int(g("block_count")),
+            n_embd=n_embd,
+            n_head=n_head,
+            n_head_kv=n_head_kv,
+            head_dim=head_dim,
+            n_ff=int(n_ff),
+            n_vocab=n_vocab,
+            n_ctx_train=int(g("context_length", 4096)),
+            rope_theta=float(g("rope.freq_base", 10000.0)),
+            rope_dim=rope_dim,
+            rope_mode=1 if a in neox_archs else 0,
+            rope_scaling=str(g("rope.scaling.type", "none")),
+            rope_freq_scale=1.0 / float(g("rope.scaling.factor", 1.0) or 1.0),
+            rope_orig_ctx=int(g("rope.scaling.original_context_length", 0) or 0),
+            norm_eps=float(eps),
+            norm_type=norm_type,
+            n_expert=int(g("expert_count", 0) or 0),
+            n_expert_used=int(g("expert_used_count", 0) or 0),
+            parallel_residual=a == "phi2",
+            act="gelu" if a in ("phi2", "gptneox", "falcon") else "swiglu",
+            tied_embeddings="output.weight" not in r.tensors,
+            name=str(r.kv.get("general.name", "")),
+        )
+        return hp

@@ -1,0 +1,289 @@
+"""Random-init GGUF models of the BASELINE architectures (no network: no real checkpoints).
+
+Presets reproduce the public hyper-parameters and llama.cpp's Q4_K_M tensor-type mix
+(`use_more_bits` layers get Q6_K for attn_v / ffn_down, output is Q6_K), so the engine
+streams exactly the bytes a real Llama-3-8B-Instruct-Q4_K_M.gguf would make it stream.
+Quantised tensors are written as random *valid* blocks (fast: O(bytes)); small test
+models can instead quantise real float weights for exact reference checks.
+
+The tokenizer is a byte-level BPE trained offline on Python sources (assets/bpe32k.json.gz),
+padded to the preset vocabulary with unreachable filler tokens plus the preset's special
+tokens (Llama-3's <|begin_of_text|> ... <|eot_id|> at 128000+).
+"""
+from __future__ import annotations
+
+import gzip
+import json
+import os
+from dataclasses import dataclass, field, replace
+from pathlib import Path
+from typing import Dict, List, Optional
+
+import numpy as np
+
+from ..gguf import (GGMLType, GGUFValueType, GGUFWriter, quantize, random_q4_k_blocks, random_q6_k_blocks,
+                    random_q8_0_blocks)
+
+ASSETS = Path(__file__).resolve().parent.parent / "assets"
+
+LLAMA3_TEMPLATE = ("{% set loop_messages = messages %}{% for message in loop_messages %}{% set content = "
+                   "'<|start_header_id|>' + message['role'] + '<|end_header_id|>\n\n'+ message['content'] | trim + "
+                   "'<|eot_id|>' %}{% if loop.index0 == 0 %}{% set content = bos_token + content %}{% endif %}"
+                   "{{ content }}{% endfor %}{% if add_generation_prompt %}{{ '<|start_header_id|>assistant"
+                   "<|end_header_id|>\n\n' }}{% endif %}")
+
+
+@dataclass
+class Preset:
+    arch: str = "llama"
+    n_layer: int = 32
+    n_embd: int = 4096
+    n_head: int = 32
+    n_head_kv: int = 8
+    n_ff: int = 14336
+    n_vocab: int = 128256
+    ctx: int = 8192
+    rope_theta: float = 500000.0
+    eps: float = 1e-5
+    n_expert: int = 0
+    n_expert_used: int = 0
+    rope_dim: Optional[int] = None
+    qtype: str = "Q4_K_M"            # Q4_K_M | Q4_K | Q8_0 | F16 | F32
+    tokenizer: str = "llama3"        # llama3 | mistral | phi2
+    name: str = "synthetic"
+
+
+PRESETS: Dict[str, Preset] = {
+    "llama3-8b": Preset(name="Meta-Llama-3-8B-Instruct (random-init)"),
+    "llama3-70b": Preset(n_layer=80, n_embd=8192, n_head=64, n_head_kv=8, n_ff=28672,
+                         name="Meta-Llama-3-70B-Instruct (random-init)"),
+    "mixtral-8x7b": Preset(n_layer=32, n_embd=4096, n_head=32, n_head_kv=8, n_ff=14336, n_vocab=32000,
+                           ctx=32768, rope_theta=1e6, n_expert=8, n_expert_used=2, tokenizer="mistral",
+                           name="Mixtral-8x7B-Instruct-v0.1 (random-init)"),
+    "mistral-7b": Preset(n_vocab=32000, ctx=32768, rope_theta=1e6, tokenizer="mistral",
+                         name="Mistral-7B-Instruct (random-init)"),
+    "phi2": Preset(arch="phi2", n_layer=32, n_embd=2560, n_head=32, n_head_kv=32, n_ff=10240, n_vocab=51200,
+                   ctx=2048, rope_theta=10000.0, rope_dim=32, tokenizer="phi2", name="phi-2 (random-init)"),
+    # small shapes for tests (CPU reference runs) -- K dims multiples of 256 so every kernel path is used
+    "tiny-llama": Preset(n_layer=2, n_embd=256, n_head=4, n_head_kv=2, n_ff=512, n_vocab=32256, ctx=512,
+                         qtype="Q4_K", name="tiny-llama"),
+    "tiny-llama-q8": Preset(n_layer=2, n_embd=256, n_head=4, n_head_kv=2, n_ff=512, n_vocab=32256, ctx=512,
+                            qtype="Q8_0", name="tiny-llama-q8"),
+    "tiny-mixtral": Preset(n_layer=2, n_embd=256, n_head=4, n_head_kv=2, n_ff=512, n_vocab=32256, ctx=512,
+                           n_expert=4, n_expert_used=2, qtype="Q4_K", name="tiny-mixtral"),
+    "tiny-phi2": Preset(arch="phi2", n_layer=2, n_embd=256, n_head=4, n_head_kv=4, n_ff=512, n_vocab=32256,
+                        ctx=512, rope_theta=10000.0, rope_dim=32, qtype="Q8_0", tokenizer="phi2", name="tiny-phi2"),
+}
+
+
+def _bpe_asset():
+    with gzip.open(ASSETS / "bpe32k.json.gz", "rt") as f:
+        return json.load(f)
+
+
+LLAMA3_SPECIAL = {0: "<|begin_of_text|>", 1: "<|end_of_text|>", 6: "<|start_header_id|>",
+                  7: "<|end_header_id|>", 9: "<|eot_id|>"}
+
+
+def build_vocab(p: Preset):
+    """-> (model, tokens, types, merges, bos, eos, extra kv)"""
+    a = _bpe_asset()
+    base, merges = a["tokens"], a["merges"]
+    if p.tokenizer == "mistral":
+        # SentencePiece-style vocab: <unk> <s> </s>, byte tokens, then pieces; scores favour frequent merges
+        toks = ["<unk>", "<s>", "</s>"] + [f"<0x{i:02X}>" for i in range(256)]
+        types = [2, 3, 3] + [6] * 256
+        from ..tokenizer import unicode_to_bytes
+        u2b = unicode_to_bytes()
+        seen = set(toks)
+        for t in base:
+            try:
+                s = bytes(u2b[c] for c in t).decode("utf-8")
+            except (KeyError, UnicodeDecodeError):
+                continue
+            s = s.replace(" ", "▁")
+            if s in seen or not s:
+                continue
+            seen.add(s)
+            toks.append(s)
+            types.append(1)
+            if len(toks) >= p.n_vocab:
+                break
+        i = 0
+        while len(toks) < p.n_vocab:
+            toks.append(f"▁filler{i}")
+            types.append(1)
+            i += 1
+        scores = [0.0] * 259 + [-float(i) for i in range(len(toks) - 259)]
+        return "llama", toks, types, None, scores, 1, 2, {"tokenizer.ggml.add_bos_token": True}
+    n_special = 256 if p.tokenizer == "llama3" else 1
+    n_normal = p.n_vocab - n_special
+    toks = list(base[:n_normal])
+    i = 0
+    while len(toks) < n_normal:
+        toks.append(f"Ġfill{i}")
+        i += 1
+    types = [1] * n_normal
+    if p.tokenizer == "llama3":
+        for k in range(256):
+            toks.append(LLAMA3_SPECIAL.get(k, f"<|reserved_special_token_{k}|>"))
+            types.append(3)
+        bos, eos = n_normal + 0, n_normal + 9
+        extra = {"tokenizer.ggml.pre": "llama-bpe", "tokenizer.chat_template": LLAMA3_TEMPLATE,
+                 "tokenizer.ggml.add_bos_token": True, "tokenizer.ggml.eot_token_id": n_normal + 9}
+    else:  # phi2: <|endoftext|> is bos = eos
+        toks.append("<|endoftext|>")
+        types.append(3)
+        bos = eos = n_normal
+        extra = {"tokenizer.ggml.pre": "phi-2", "tokenizer.ggml.add_bos_token": False}
+    return "gpt2", toks, types, merges, None, bos, eos, extra
+
+
+def _more_bits(i: int, n: int) -> bool:
+    return i < n // 8 or i >= 7 * n // 8 or (i - n // 8) % 3 == 2
+
+
+def _tensor_types(p: Preset, name: str, layer: int) -> int:
+    if name.endswith("norm.weight") or name.endswith(".bias") or name == "rope_freqs.weight" or \
+            name.endswith("ffn_gate_inp.weight"):
+        return GGMLType.F32
+    q = p.qtype
+    if q == "F32":
+        return GGMLType.F32
+    if q == "F16":
+        return GGMLType.F16
+    if q == "Q8_0":
+        return GGMLType.Q8_0
+    if q == "Q4_K":
+        return GGMLType.Q6_K if name == "output.weight" else GGMLType.Q4_K
+    # Q4_K_M
+    if name == "output.weight":
+        return GGMLType.Q6_K
+    if name.endswith("attn_v.weight") and _more_bits(layer, p.n_layer):
+        return GGMLType.Q6_K
+    if (name.endswith("ffn_down.weight") or name.endswith("ffn_down_exps.weight")) and _more_bits(layer, p.n_layer):
+        return GGMLType.Q6_K
+    return GGMLType.Q4_K
+
+
+def tensor_list(p: Preset):
+    """(name, shape, layer) for every tensor of the preset, torch/numpy order."""
+    d, hd = p.n_embd, p.n_embd // p.n_head
+    qd, kvd = p.n_head * hd, p.n_head_kv * hd
+    out = [("token_embd.weight", (p.n_vocab, d), -1)]
+    for i in range(p.n_layer):
+        b = f"blk.{i}."
+        if p.arch == "phi2":
+            out += [(b + "attn_norm.weight", (d,), i), (b + "attn_norm.bias", (d,), i),
+                    (b + "attn_qkv.weight", (qd + 2 * kvd, d), i), (b + "attn_qkv.bias", (qd + 2 * kvd,), i),
+                    (b + "attn_output.weight", (d, qd), i), (b + "attn_output.bias", (d,), i),
+                    (b + "ffn_up.weight", (p.n_ff, d), i), (b + "ffn_up.bias", (p.n_ff,), i),
+                    (b + "ffn_down.weight", (d, p.n_ff), i), (b + "ffn_down.bias", (d,), i)]
+            continue
+        out += [(b + "attn_norm.weight", (d,), i), (b + "attn_q.weight", (qd, d), i),
+                (b + "attn_k.weight", (kvd, d), i), (b + "attn_v.weight", (kvd, d), i),
+                (b + "attn_output.weight", (d, qd), i), (b + "ffn_norm.weight", (d,), i)]
+        if p.n_expert:
+            E = p.n_expert
+            out += [(b + "ffn_gate_inp.weight", (E, d), i), (b + "ffn_gate_exps.weight", (E, p.n_ff, d), i),
+                    (b + "ffn_up_exps.weight", (E, p.n_ff, d), i), (b + "ffn_down_exps.weight", (E, d, p.n_ff), i)]
+        else:
+            out += [(b + "ffn_gate.weight", (p.n_ff, d), i), (b + "ffn_up.weight", (p.n_ff, d), i),
+                    (b + "ffn_down.weight", (d, p.n_ff), i)]
+    out.append(("output_norm.weight", (d,), -1))
+    if p.arch == "phi2":
+        out.append(("output_norm.bias", (d,), -1))
+        out.append(("output.bias", (p.n_vocab,), -1))
+    out.append(("output.weight", (p.n_vocab, d), -1))
+    return out
+
+
+def write_model(path: str, preset: str | Preset, seed: int = 0, exact: bool = False, std: float = 0.02,
+                **overrides) -> str:
+    """Write a random-init GGUF.  exact=True quantises real float weights (slow; tests only)."""
+    p = PRESETS[preset] if isinstance(preset, str) else preset
+    if overrides:
+        p = replace(p, **overrides)
+    model, toks, types, merges, scores, bos, eos, extra = build_vocab(p)
+    w = GGUFWriter(path, p.arch)
+    a = p.arch
+    hd = p.n_embd // p.n_head
+    w.add_string("general.name", p.name)
+    w.add_uint32("general.file_type", 15 if p.qtype == "Q4_K_M" else 7)
+    w.add_uint32(f"{a}.context_length", p.ctx)
+    w.add_uint32(f"{a}.embedding_length", p.n_embd)
+    w.add_uint32(f"{a}.block_count", p.n_layer)
+    w.add_uint32(f"{a}.feed_forward_length", p.n_ff)
+    w.add_uint32(f"{a}.attention.head_count", p.n_head)
+    w.add_uint32(f"{a}.attention.head_count_kv", p.n_head_kv)
+    w.add_float32(f"{a}.rope.freq_base", p.rope_theta)
+    w.add_uint32(f"{a}.rope.dimension_count", p.rope_dim or hd)
+    if a == "phi2":
+        w.add_float32(f"{a}.attention.layer_norm_epsilon", p.eps)
+    else:
+        w.add_float32(f"{a}.attention.layer_norm_rms_epsilon", p.eps)
+        w.add_uint32(f"{a}.vocab_size", p.n_vocab)
+    if p.n_expert:
+        w.add_uint32(f"{a}.expert_count", p.n_expert)
+        w.add_uint32(f"{a}.expert_used_count", p.n_expert_used)
+    w.add_string("tokenizer.ggml.model", model)
+    w.add_array("tokenizer.ggml.tokens", toks, GGUFValueType.STRING)
+    w.add_array("tokenizer.ggml.token_type", types, GGUFValueType.INT32)
+    if merges is not None:
+        w.add_array("tokenizer.ggml.merges", merges, GGUFValueType.STRING)
+    if scores is not None:
+        w.add_array("tokenizer.ggml.scores", scores, GGUFValueType.FLOAT32)
+    w.add_uint32("tokenizer.ggml.bos_token_id", bos)
+    w.add_uint32("tokenizer.ggml.eos_token_id", eos)
+    for k, v in extra.items():
+        if isinstance(v, bool):
+            w.add_bool(k, v)
+        elif isinstance(v, int):
+            w.add_uint32(k, v)
+        else:
+            w.add_string(k, v)
+
+    rng_master = np.random.default_rng(seed)
+    for name, shape, layer in tensor_list(p):
+        t = _tensor_types(p, name, layer)
+        tseed = int(rng_master.integers(0, 2 ** 31))
+        n = int(np.prod(shape))
+
+        def payload(shape=shape, t=t, tseed=tseed, name=name, n=n):
+            rng = np.random.default_rng(tseed)
+            if name.endswith("norm.weight"):
+                return (1.0 + 0.1 * rng.standard_normal(n)).astype(np.float32)
+            if name.endswith(".bias"):
+                return (0.02 * rng.standard_normal(n)).astype(np.float32)
+            if name.endswith("ffn_gate_inp.weight"):
+                return (std * rng.standard_normal(n)).astype(np.float32)
+            sd = std
+            if name == "token_embd.weight":
+                sd = 1.0  # embeddings feed an RMSNorm; unit scale keeps activations O(1)
+            if exact or t in (GGMLType.F32, GGMLType.F16, GGMLType.BF16):
+                x = (sd * rng.standard_normal(n)).astype(np.float32)
+                return quantize(x, t)
+            if t == GGMLType.Q4_K:
+                return random_q4_k_blocks(rng, n // 256, sd)
+            if t == GGMLType.Q6_K:
+                return random_q6_k_blocks(rng, n // 256, sd)
+            if t == GGMLType.Q8_0:
+                return random_q8_0_blocks(rng, n // 32, sd)
+            raise NotImplementedError(t)
+
+        w.add_tensor(name, shape, t, payload)
+    w.write()
+    return path
+
+
+def ensure_model(preset: str, cache_dir: Optional[str] = None, **kw) -> str:
+    cache_dir = cache_dir or os.environ.get("LOCALAI_AMD_CACHE", os.path.join(os.path.expanduser("~"), ".cache",
+                                                                               "localai_amd"))
+    os.makedirs(cache_dir, exist_ok=True)
+    tag = "-".join(f"{k}{v}" for k, v in sorted(kw.items()))
+    path = os.path.join(cache_dir, f"{preset}{'-' + tag if tag else ''}.gguf")
+    if not os.path.exists(path):
+        tmp = path + ".partial"
+        write_model(tmp, preset, **kw)
+        os.replace(tmp, path)
+    return path

@@ -1,0 +1,689 @@
+"""Operator layer: HIP (gfx950) kernels via a C ABI, plus fp32 PyTorch references.
+
+Dispatch rule: a tensor on a GPU runs the hand-written HIP kernel from
+`_la_kernels.so` -- there is NO silent eager fallback on the GPU (a missing library
+raises).  CPU tensors run the PyTorch reference, which is also the numerics oracle
+for the GPU tests (tests/test_kernels_gpu.py).
+
+Every wrapper validates shapes/dtypes/contiguity on the host before launching, so a
+bad call fails in Python instead of faulting the device.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import os
+import threading
+from dataclasses import dataclass
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from ..gguf import GGMLType, dequantize
+
+_LIB = None
+_LIB_LOCK = threading.Lock()
+
+FMT_Q8_0, FMT_Q4_K, FMT_Q6_K, FMT_BF16 = 8, 12, 14, 30
+
+
+def lib():
+    """Load (building if needed) the kernel library.  Raises if unavailable."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    with _LIB_LOCK:
+        if _LIB is not None:
+            return _LIB
+        from . import _build
+        path = _build.LIB
+        if not path.exists() or os.environ.get("LOCALAI_AMD_REBUILD"):
+            _build.build()
+        L = ctypes.CDLL(str(path))
+        P, I, F, LNG = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_long
+        sig = {
+            "la_qgemm_skinny": [I, P, P, P, P, I, I, P, I, I, I, P, I, LNG, P],
+            "la_add_norm": [P, P, LNG, I, P, I, P, P, P, I, I, F, I, P, P],
+            "la_rope_kv": [P, LNG, I, P, P, P, P, I, I, I, I, I, I, P, P, P, I, P],
+            "la_act": [P, LNG, I, P, P, I, I, I, P],
+            "la_reduce_slabs": [P, LNG, I, P, I, I, P, P, P],
+            "la_embed": [I, P, P, P, P, I, I, P, I, P, F, P],
+            "la_dequant": [I, P, P, P, P, I, I, P, P],
+            "la_attn_decode": [P, P, P, P, I, P, I, I, I, I, I, F, I, P, P, P, P],
+            "la_attn_prefill": [P, P, P, P, I, P, P, P, I, I, I, I, I, F, P, P],
+            "la_sample": [P, LNG, I, I, P, P, P, P, P],
+            "la_penalties": [P, LNG, I, P, I, P, P, I, P, P],
+            "la_sample_row_bytes": [],
+        }
+        for name, args in sig.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = I
+        _LIB = L
+        return L
+
+
+def hip_available() -> bool:
+    try:
+        lib()
+        return True
+    except Exception:
+        return False
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def _check(rc: int, name: str):
+    if rc != 0:
+        raise RuntimeError(f"{name} failed with code {rc}")
+
+
+# ---------------------------------------------------------------------------------------
+# Quantised weights
+# ---------------------------------------------------------------------------------------
+
+@dataclass
+class QWeight:
+    """A [N, K] matrix in a runtime layout (see csrc/qweight.h)."""
+    fmt: int
+    N: int
+    K: int
+    planes: Tuple[Optional[torch.Tensor], ...]   # p0..p3 device planes (GPU path)
+    ref: Optional[torch.Tensor] = None            # fp32 [N, K] (CPU path / oracle)
+    bf16: Optional[torch.Tensor] = None           # optional HBM-resident bf16 copy (prefill GEMMs)
+
+    @property
+    def device(self) -> torch.device:
+        t = self.planes[0] if self.planes and self.planes[0] is not None else self.ref
+        return t.device
+
+    @property
+    def nbytes(self) -> int:
+        return sum(p.numel() * p.element_size() for p in self.planes if p is not None)
+
+    @staticmethod
+    def from_raw(raw: np.ndarray, ggml_type: int, shape: Tuple[int, int], device: torch.device,
+                 keep_ref: bool = False) -> "QWeight":
+        """raw: uint8 GGUF payload of a [N, K] tensor."""
+        N, K = int(shape[0]), int(shape[1])
+        t = int(ggml_type)
+        if device.type != "cuda":
+            ref = torch.from_numpy(dequantize(raw, t, (N, K)).astype(np.float32))
+            fmt = {GGMLType.Q4_K: FMT_Q4_K, GGMLType.Q6_K: FMT_Q6_K, GGMLType.Q8_0: FMT_Q8_0}.get(t, FMT_BF16)
+            return QWeight(fmt, N, K, (None, None, None, None), ref=ref)
+        ref = torch.from_numpy(dequantize(raw, t, (N, K)).astype(np.float32)) if keep_ref else None
+        src = torch.from_numpy(np.ascontiguousarray(raw)).to(device, non_blocking=False)
+        if t == GGMLType.Q4_K and K % 256 == 0:
+            b = src.view(N, K // 256, 144)
+            qs = b[:, :, 16:].contiguous().view(N, K // 2)
+            hdr = b[:, :, :16].contiguous().view(N, K // 256 * 16)
+            return QWeight(FMT_Q4_K, N, K, (qs, hdr, None, None), ref=ref)
+        if t == GGMLType.Q6_K and K % 256 == 0:
+            b = src.view(N, K // 256, 210)
+            ql = b[:, :, :128].contiguous().view(N, K // 2)
+            qh = b[:, :, 128:192].contiguous().view(N, K // 4)
+            sc = b[:, :, 192:208].contiguous().view(N, K // 16)
+            d = b[:, :, 208:210].contiguous().view(N, K // 256 * 2)
+            return QWeight(FMT_Q6_K, N, K, (ql, qh, sc, d), ref=ref)
+        if t == GGMLType.Q8_0 and K % 256 == 0:
+            b = src.view(N, K // 32, 34)
+            d = b[:, :, :2].contiguous().view(N, K // 32 * 2)
+            qs = b[:, :, 2:].contiguous().view(N, K)
+            return QWeight(FMT_Q8_0, N, K, (qs, d, None, None), ref=ref)
+        # anything else: materialise bf16 (dequantised on the host once)
+        w = torch.from_numpy(dequantize(raw, t, (N, K)).astype(np.float32)).to(device).to(torch.bfloat16)
+        return QWeight(FMT_BF16, N, K, (w.view(torch.uint8).view(N, K * 2), None, None, None), ref=ref)
+
+    @staticmethod
+    def from_float(w: torch.Tensor) -> "QWeight":
+        """Dense bf16 weight (used for tensors stored as F16/F32 or built in memory)."""
+        N, K = w.shape
+        if w.device.type != "cuda":
+            return QWeight(FMT_BF16, N, K, (None, None, None, None), ref=w.float())
+        wb = w.to(torch.bfloat16).contiguous()
+        return QWeight(FMT_BF16, N, K, (wb.view(torch.uint8).view(N, K * 2), None, None, None))
+
+    def ptrs(self):
+        return [_ptr(p) for p in self.planes]
+
+    def materialize_bf16(self) -> torch.Tensor:
+        """HBM-resident bf16 copy for the large-M (prefill) GEMM path."""
+        if self.bf16 is None:
+            if self.device.type != "cuda":
+                self.bf16 = self.ref.to(torch.bfloat16)
+            elif self.fmt == FMT_BF16:
+                self.bf16 = self.planes[0].view(torch.bfloat16).view(self.N, self.K)
+            else:
+                out = torch.empty(self.N, self.K, dtype=torch.bfloat16, device=self.device)
+                _check(lib().la_dequant(self.fmt, *self.ptrs(), self.N, self.K, out.data_ptr(), _stream()),
+                       "la_dequant")
+                self.bf16 = out
+        return self.bf16
+
+    def dequant_f32(self) -> torch.Tensor:
+        if self.ref is not None:
+            return self.ref
+        return self.materialize_bf16().float()
+
+    def shard(self, dim: int, rank: int, world: int) -> "QWeight":
+        """Row (dim=0) or column (dim=1) shard for tensor parallelism.  Column shards
+        must stay aligned to 256-wide super-blocks."""
+        if world == 1:
+            return self
+        if dim == 0:
+            n = self.N // world
+            sl = slice(rank * n, (rank + 1) * n)
+            planes = tuple(None if p is None else p[sl].contiguous() for p in self.planes)
+            ref = None if self.ref is None else self.ref[sl].contiguous()
+            return QWeight(self.fmt, n, self.K, planes, ref=ref)
+        k = self.K // world
+        if k % 256:
+            raise ValueError(f"column shard {k} not a multiple of 256")
+        ref = None if self.ref is None else self.ref[:, rank * k:(rank + 1) * k].contiguous()
+        planes = []
+        for p in self.planes:
+            if p is None:
+                planes.append(None)
+                continue
+            per_row = p.shape[1]
+            c = per_row // world
+            planes.append(p[:, rank * c:(rank + 1) * c].contiguous())
+        return QWeight(self.fmt, self.N, k, tuple(planes), ref=ref)
+
+
+def concat_rows(ws: Sequence[QWeight]) -> Optional[QWeight]:
+    """Fuse weights with equal format and K along N (QKV, gate|up).  None if impossible."""
+    if not ws or len({(w.fmt, w.K) for w in ws}) != 1:
+        return None
+    w0 = ws[0]
+    planes = []
+    for i in range(4):
+        ps = [w.planes[i] for w in ws]
+        planes.append(None if ps[0] is None else torch.cat(ps, 0))
+    ref = None if w0.ref is None else torch.cat([w.ref for w in ws], 0)
+    return QWeight(w0.fmt, sum(w.N for w in ws), w0.K, tuple(planes), ref=ref)
+
+
+# ---------------------------------------------------------------------------------------
+# Partial results: S fp32 split-K slabs [S, M, N] or one bf16/fp32 [M, N] matrix
+# ---------------------------------------------------------------------------------------
+
+@dataclass
+class Partial:
+    t: torch.Tensor              # [S, M, N] f32 or [M, N] bf16/f32
+    bias: Optional[torch.Tensor] = None
+
+    @property
+    def S(self) -> int:
+        return self.t.shape[0] if self.t.dim() == 3 else 0
+
+    @property
+    def M(self) -> int:
+        return self.t.shape[-2]
+
+    @property
+    def N(self) -> int:
+        return self.t.shape[-1]
+
+    def src_args(self):
+        if self.t.dim() == 3:
+            assert self.t.dtype == torch.float32
+            return (self.t.data_ptr(), self.t.shape[1] * self.t.shape[2], self.t.shape[0], _ptr(self.bias))
+        assert self.t.dtype == torch.bfloat16, "single-matrix sources must be bf16"
+        return (self.t.data_ptr(), 0, 0, _ptr(self.bias))
+
+    def dense(self) -> torch.Tensor:
+        x = self.t.float().sum(0) if self.t.dim() == 3 else self.t.float()
+        if self.bias is not None:
+            x = x + self.bias.float()
+        return x
+
+    def cols(self, a: int, b: int) -> "Partial":
+        t = self.t[..., a:b].contiguous()
+        bias = None if self.bias is None else self.bias[a:b]
+        return Partial(t, bias)
+
+
+def pick_splits(N: int, K: int, M: int) -> int:
+    """Split-K so the skinny GEMM launches >= ~2 workgroups per CU (256 CUs)."""
+    nsb = K // 256
+    nblk = (N + 63) // 64
+    want = max(1, math.ceil(512 / nblk))
+    best = 1
+    for s in range(1, nsb + 1):
+        if nsb % s == 0:
+            best = s
+            if s >= want:
+                break
+    # the consumer reads S slabs: keep the slab traffic below the weight traffic
+    while best > 1 and best * M * N * 4 * 2 > N * K // 2:
+        cands = [s for s in range(1, best) if nsb % s == 0]
+        best = cands[-1] if cands else 1
+    return best
+
+
+SKINNY_MAX_M = 64
+
+
+def linear(x: torch.Tensor, w: QWeight, bias: Optional[torch.Tensor] = None,
+           out_slabs: Optional[torch.Tensor] = None, force: Optional[str] = None) -> Partial:
+    """y = x @ W^T.  x: [M, K] bf16.  GPU: M <= 64 -> skinny MFMA kernel on the quantised
+    weights; larger M -> hipBLASLt on the HBM-resident bf16 copy."""
+    return linear_multi(x, [w], bias, out_slabs, force)
+
+
+def linear_multi(x: torch.Tensor, ws: Sequence[QWeight], bias: Optional[torch.Tensor] = None,
+                 out_slabs: Optional[torch.Tensor] = None, force: Optional[str] = None) -> Partial:
+    """y = x @ [W0; W1; ...]^T written side by side into ONE partial (e.g. Q4_K q|k with a
+    Q6_K v), so the consumer sees a single fused QKV / gate|up output."""
+    M, K = x.shape
+    for w in ws:
+        if K != w.K:
+            raise ValueError(f"linear: x has K={K}, weight has K={w.K}")
+    Ntot = sum(w.N for w in ws)
+    if not x.is_cuda:
+        y = torch.cat([x.float() @ w.dequant_f32().t() for w in ws], -1)
+        return Partial(y.to(torch.bfloat16) if force == "bf16" else y.unsqueeze(0), bias)
+    if x.dtype != torch.bfloat16 or not x.is_contiguous():
+        raise ValueError("linear: x must be contiguous bf16")
+    skinny_ok = all(w.K % 256 == 0 for w in ws)
+    use_skinny = (M <= SKINNY_MAX_M and skinny_ok) if force is None else force == "skinny"
+    if use_skinny:
+        S = min(pick_splits(w.N, w.K, M) for w in ws)
+        nsb = K // 256
+        while nsb % S:
+            S -= 1
+        out = out_slabs
+        if out is None or out.shape != (S, M, Ntot):
+            out = torch.empty(S, M, Ntot, dtype=torch.float32, device=x.device)
+        col = 0
+        for w in ws:
+            dst = out.data_ptr() + col * 4
+            _check(lib().la_qgemm_skinny(w.fmt, *w.ptrs(), w.N, w.K, x.data_ptr(), K, M, S, dst, Ntot,
+                                         M * Ntot, _stream()), "la_qgemm_skinny")
+            col += w.N
+        return Partial(out, bias)
+    if len(ws) == 1:
+        return Partial(torch.matmul(x, ws[0].materialize_bf16().t()), bias)
+    y = torch.empty(M, Ntot, dtype=torch.bfloat16, device=x.device)
+    col = 0
+    for w in ws:
+        torch.matmul(x, w.materialize_bf16().t(), out=y[:, col:col + w.N])
+        col += w.N
+    return Partial(y, bias)
+
+
+# ---------------------------------------------------------------------------------------
+# Fused elementwise
+# ---------------------------------------------------------------------------------------
+
+def add_norm(residual: torch.Tensor, add: Optional[Partial], weight: torch.Tensor,
+             bias: Optional[torch.Tensor], eps: float, mode: int = 0,
+             out: Optional[torch.Tensor] = None, want_out: bool = True) -> Optional[torch.Tensor]:
+    """residual[T,D] (fp32, updated in place) += add;  return norm(residual)*w(+b) as bf16."""
+    T, D = residual.shape
+    if add is not None and (add.M != T or add.N != D):
+        raise ValueError(f"add_norm: add {tuple(add.t.shape)} vs residual {T}x{D}")
+    if not residual.is_cuda:
+        if add is not None:
+            residual += add.dense()
+        if not want_out:
+            return None
+        x = residual
+        if mode == 0:
+            y = x * torch.rsqrt(x.pow(2).mean(-1, keepdim=True) + eps) * weight
+        else:
+            mu = x.mean(-1, keepdim=True)
+            var = (x - mu).pow(2).mean(-1, keepdim=True)
+            y = (x - mu) * torch.rsqrt(var + eps) * weight
+            if bias is not None:
+                y = y + bias
+        return y.to(torch.bfloat16)
+    assert residual.dtype == torch.float32 and residual.is_contiguous()
+    if want_out and out is None:
+        out = torch.empty(T, D, dtype=torch.bfloat16, device=residual.device)
+    a = add.src_args() if add is not None else (None, 0, 0, None)
+    _check(lib().la_add_norm(residual.data_ptr(), a[0], a[1], a[2], a[3], int(add is not None),
+                             weight.data_ptr(), _ptr(bias), _ptr(out) if want_out else None, T, D,
+                             float(eps), mode, None, _stream()), "la_add_norm")
+    return out if want_out else None
+
+
+def rope_cos_sin(max_pos: int, rot_dim: int, theta: float, device, freq_scale: float = 1.0,
+                 freq_factors: Optional[torch.Tensor] = None, rope_type: str = "none",
+                 yarn: Optional[dict] = None) -> torch.Tensor:
+    """[max_pos, rot/2, 2] (cos, sin) table, fp32, computed in float64 on the host."""
+    half = rot_dim // 2
+    inv = 1.0 / (theta ** (np.arange(0, half, dtype=np.float64) * 2.0 / rot_dim))
+    if freq_factors is not None:
+        inv = inv / freq_factors.detach().cpu().double().numpy()[:half]
+    mscale = 1.0
+    if rope_type == "yarn" and yarn:
+        # YaRN (ggml rope_yarn): blend interpolated/extrapolated frequencies by ramp
+        orig = yarn.get("orig_ctx", 4096)
+        bf, bs = yarn.get("beta_fast", 32.0), yarn.get("beta_slow", 1.0)
+        ext = yarn.get("ext_factor", 1.0)
+        def corr_dim(nrot):
+            return rot_dim * math.log(orig / (nrot * 2 * math.pi)) / (2 * math.log(theta))
+        lo = max(0.0, math.floor(corr_dim(bf)))
+        hi = min(rot_dim - 1.0, math.ceil(corr_dim(bs)))
+        i = np.arange(half, dtype=np.float64)
+        ramp = np.clip((i - lo) / max(0.001, hi - lo), 0, 1)
+        mix = (1 - ramp) * ext
+        inv = inv * freq_scale * (1 - mix) + inv * mix
+        mscale = yarn.get("attn_factor", 1.0) * (1.0 + 0.1 * math.log(1.0 / freq_scale)) if freq_scale < 1 else \
+            yarn.get("attn_factor", 1.0)
+    else:
+        inv = inv * freq_scale
+    pos = np.arange(max_pos, dtype=np.float64)
+    ang = np.outer(pos, inv)
+    cs = np.stack([np.cos(ang) * mscale, np.sin(ang) * mscale], -1).astype(np.float32)
+    return torch.from_numpy(cs).to(device)
+
+
+def rope_kv(qkv: Partial, pos: torch.Tensor, slots: Optional[torch.Tensor], cos_sin: torch.Tensor,
+            Hq: int, Hkv: int, Dh: int, rot: int, mode: int, k_cache: torch.Tensor, v_cache: torch.Tensor,
+            block_size: int, q_out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Rotate q,k; write k,v into the paged cache at `slots`; return q [T,Hq,Dh] bf16."""
+    T = qkv.M
+    W = (Hq + 2 * Hkv) * Dh
+    if qkv.N != W:
+        raise ValueError(f"rope_kv: qkv width {qkv.N} != {W}")
+    if not qkv.t.is_cuda:
+        x = qkv.dense().view(T, Hq + 2 * Hkv, Dh)
+        cs = cos_sin[pos.long()]  # [T, rot/2, 2]
+        c, s = cs[..., 0], cs[..., 1]
+
+        def rot_fn(h):
+            h = h.clone()
+            if mode == 0:
+                x0, x1 = h[..., 0:rot:2].clone(), h[..., 1:rot:2].clone()
+                h[..., 0:rot:2] = x0 * c[:, None] - x1 * s[:, None]
+                h[..., 1:rot:2] = x0 * s[:, None] + x1 * c[:, None]
+            else:
+                half = rot // 2
+                x0, x1 = h[..., :half].clone(), h[..., half:rot].clone()
+                h[..., :half] = x0 * c[:, None] - x1 * s[:, None]
+                h[..., half:rot] = x0 * s[:, None] + x1 * c[:, None]
+            return h
+        q = rot_fn(x[:, :Hq]).to(torch.bfloat16)
+        k = rot_fn(x[:, Hq:Hq + Hkv]).to(k_cache.dtype)
+        v = x[:, Hq + Hkv:].to(v_cache.dtype)
+        if slots is not None:
+            sl = slots.long()
+            ok = sl >= 0
+            blk, off = sl[ok] // block_size, sl[ok] % block_size
+            k_cache[blk, :, off] = k[ok]
+            v_cache[blk, :, off] = v[ok]
+        if q_out is not None:
+            q_out.copy_(q)
+            return q_out
+        return q
+    if q_out is None:
+        q_out = torch.empty(T, Hq, Dh, dtype=torch.bfloat16, device=qkv.t.device)
+    a = qkv.src_args()
+    _check(lib().la_rope_kv(a[0], a[1], a[2], a[3], pos.data_ptr(), _ptr(slots), cos_sin.data_ptr(), T, Hq, Hkv,
+                            Dh, rot, mode, q_out.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), block_size,
+                            _stream()), "la_rope_kv")
+    return q_out
+
+
+ACT_SWIGLU, ACT_GELU, ACT_GELU_QUICK = 0, 1, 2
+
+
+def act(src: Partial, F: int, mode: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    T = src.M
+    if not src.t.is_cuda:
+        x = src.dense()
+        if mode == ACT_SWIGLU:
+            y = torch.nn.functional.silu(x[:, :F]) * x[:, F:2 * F]
+        elif mode == ACT_GELU:
+            y = torch.nn.functional.gelu(x, approximate="tanh")
+        else:
+            y = x * torch.sigmoid(1.702 * x)
+        return y.to(torch.bfloat16)
+    if out is None:
+        out = torch.empty(T, F, dtype=torch.bfloat16, device=src.t.device)
+    a = src.src_args()
+    _check(lib().la_act(a[0], a[1], a[2], a[3], out.data_ptr(), T, F, mode, _stream()), "la_act")
+    return out
+
+
+def reduce(src: Partial, dtype=torch.float32) -> torch.Tensor:
+    if not src.t.is_cuda:
+        return src.dense().to(dtype)
+    T, N = src.M, src.N
+    out = torch.empty(T, N, dtype=dtype, device=src.t.device)
+    a = src.src_args()
+    f32 = out.data_ptr() if dtype == torch.float32 else None
+    b16 = out.data_ptr() if dtype == torch.bfloat16 else None
+    _check(lib().la_reduce_slabs(a[0], a[1], a[2], a[3], T, N, f32, b16, _stream()), "la_reduce_slabs")
+    return out
+
+
+def embed(tokens: torch.Tensor, w: QWeight, scale: float = 1.0, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    T = tokens.shape[0]
+    if not tokens.is_cuda:
+        return w.dequant_f32()[tokens.long()] * scale
+    if out is None:
+        out = torch.empty(T, w.K, dtype=torch.float32, device=tokens.device)
+    assert tokens.dtype == torch.int32
+    _check(lib().la_embed(w.fmt, *w.ptrs(), w.N, w.K, tokens.data_ptr(), T, out.data_ptr(), float(scale),
+                          _stream()), "la_embed")
+    return out
+
+
+# ---------------------------------------------------------------------------------------
+# Attention
+# ---------------------------------------------------------------------------------------
+
+DEC_PS = 256
+
+
+def attn_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, block_tables: torch.Tensor,
+                seq_lens: torch.Tensor, scale: float, max_seq_len: int, out: Optional[torch.Tensor] = None,
+                workspace: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:
+    """q [B,Hq,Dh] bf16; caches [nblk,Hkv,BS,Dh]; block_tables [B,maxb] i32; seq_lens [B] i32."""
+    B, Hq, Dh = q.shape
+    nblk, Hkv, BS, Dh2 = k_cache.shape
+    if Dh2 != Dh or Hq % Hkv:
+        raise ValueError("attn_decode: head shape mismatch")
+    if not q.is_cuda:
+        return _attn_ref_decode(q, k_cache, v_cache, block_tables, seq_lens, scale)
+    P = max(1, (max_seq_len + DEC_PS - 1) // DEC_PS)
+    if out is None:
+        out = torch.empty(B, Hq, Dh, dtype=torch.bfloat16, device=q.device)
+    if workspace is None or workspace[0].numel() < B * Hq * P * Dh:
+        po = torch.empty(B * Hq * P * Dh, dtype=torch.float32, device=q.device)
+        pml = torch.empty(B * Hq * P * 2, dtype=torch.float32, device=q.device)
+    else:
+        po, pml = workspace
+    _check(lib().la_attn_decode(q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr(),
+                                block_tables.shape[1], seq_lens.data_ptr(), B, Hq, Hkv, Dh, BS, float(scale), P,
+                                out.data_ptr(), po.data_ptr(), pml.data_ptr(), _stream()), "la_attn_decode")
+    return out
+
+
+def _gather_kv(cache, bt_row, L):
+    BS = cache.shape[2]
+    nb = (L + BS - 1) // BS
+    blocks = cache[bt_row[:nb].long()]                  # [nb, Hkv, BS, Dh]
+    return blocks.permute(1, 0, 2, 3).reshape(cache.shape[1], nb * BS, cache.shape[3])[:, :L]
+
+
+def _attn_ref_decode(q, kc, vc, bt, sl, scale):
+    B, Hq, Dh = q.shape
+    Hkv = kc.shape[1]
+    G = Hq // Hkv
+    out = torch.empty_like(q)
+    for b in range(B):
+        L = int(sl[b])
+        k = _gather_kv(kc, bt[b], L).float()
+        v = _gather_kv(vc, bt[b], L).float()
+        qq = q[b].float().view(Hkv, G, Dh)
+        s = torch.einsum("hgd,hld->hgl", qq, k) * scale
+        p = torch.softmax(s, -1)
+        out[b] = torch.einsum("hgl,hld->hgd", p, v).reshape(Hq, Dh).to(q.dtype)
+    return out
+
+
+PF_QT = 64
+
+
+def prefill_tiles(q_lens: Sequence[int], device) -> torch.Tensor:
+    tiles = []
+    for s, ql in enumerate(q_lens):
+        for r in range(0, ql, PF_QT):
+            tiles.append((s, r))
+    return torch.tensor(tiles, dtype=torch.int32, device=device).view(-1, 2)
+
+
+def attn_prefill(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, cu_q: torch.Tensor,
+                 ctx_lens: torch.Tensor, block_tables: torch.Tensor, scale: float,
+                 tiles: Optional[torch.Tensor] = None, q_lens: Optional[Sequence[int]] = None,
+                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Causal attention for new tokens. q [T,Hq,Dh]; cu_q [nseq+1]; ctx_lens [nseq] (cached+new)."""
+    T, Hq, Dh = q.shape
+    Hkv = k_cache.shape[1]
+    if not q.is_cuda:
+        return _attn_ref_prefill(q, k_cache, v_cache, cu_q, ctx_lens, block_tables, scale)
+    if tiles is None:
+        cq = cu_q.cpu().tolist()
+        tiles = prefill_tiles([cq[i + 1] - cq[i] for i in range(len(cq) - 1)], q.device)
+    if out is None:
+        out = torch.empty(T, Hq, Dh, dtype=torch.bfloat16, device=q.device)
+    _check(lib().la_attn_prefill(q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), tiles.data_ptr(),
+                                 tiles.shape[0], cu_q.data_ptr(), ctx_lens.data_ptr(), block_tables.data_ptr(),
+                                 block_tables.shape[1], Hq, Hkv, Dh, k_cache.shape[2], float(scale),
+                                 out.data_ptr(), _stream()), "la_attn_prefill")
+    return out
+
+
+def _attn_ref_prefill(q, kc, vc, cu_q, ctx_lens, bt, scale):
+    T, Hq, Dh = q.shape
+    Hkv = kc.shape[1]
+    G = Hq // Hkv
+    out = torch.empty_like(q)
+    cq = cu_q.tolist()
+    for s in range(len(cq) - 1):
+        a, b = cq[s], cq[s + 1]
+        ql = b - a
+        if ql == 0:
+            continue
+        L = int(ctx_lens[s])
+        k = _gather_kv(kc, bt[s], L).float().repeat_interleave(G, 0)   # [Hq, L, Dh]
+        v = _gather_kv(vc, bt[s], L).float().repeat_interleave(G, 0)
+        qq = q[a:b].float().transpose(0, 1)                              # [Hq, ql, Dh]
+        sc = torch.einsum("hqd,hld->hql", qq, k) * scale
+        qpos = torch.arange(L - ql, L).view(-1, 1)
+        kpos = torch.arange(L).view(1, -1)
+        sc = sc.masked_fill(kpos > qpos, float("-inf"))
+        p = torch.softmax(sc, -1)
+        out[a:b] = torch.einsum("hql,hld->hqd", p, v).transpose(0, 1).to(q.dtype)
+    return out
+
+
+# ---------------------------------------------------------------------------------------
+# Sampling
+# ---------------------------------------------------------------------------------------
+
+SAMPLE_ROW_DTYPE = np.dtype([("temp", "<f4"), ("top_p", "<f4"), ("min_p", "<f4"), ("typical_p", "<f4"),
+                             ("tfs_z", "<f4"), ("tau", "<f4"), ("eta", "<f4"), ("top_k", "<i4"),
+                             ("mirostat", "<i4"), ("pad", "<i4"), ("seed", "<u8"), ("counter", "<u8")])
+
+
+def sample(logits: torch.Tensor, params: np.ndarray, mu: Optional[torch.Tensor] = None,
+           params_dev: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """logits [B, V] f32; params: structured array (SAMPLE_ROW_DTYPE) of length B."""
+    B, V = logits.shape
+    assert params.dtype == SAMPLE_ROW_DTYPE and len(params) == B
+    if not logits.is_cuda:
+        return sample_ref(logits, params, mu)
+    if logits.dtype != torch.float32 or logits.stride(1) != 1:
+        raise ValueError("sample: logits must be f32 with unit column stride")
+    if params_dev is None:
+        params_dev = torch.from_numpy(params.view(np.uint8).copy()).to(logits.device, non_blocking=True)
+    if mu is None:
+        mu = torch.zeros(B, dtype=torch.float32, device=logits.device)
+    if out is None:
+        out = torch.empty(B, dtype=torch.int32, device=logits.device)
+    _check(lib().la_sample(logits.data_ptr(), logits.stride(0), B, V, params_dev.data_ptr(), mu.data_ptr(),
+                           out.data_ptr(), None, _stream()), "la_sample")
+    return out
+
+
+def sample_ref(logits: torch.Tensor, params: np.ndarray, mu: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Host reference of the sampler chain (same semantics, torch RNG)."""
+    B, V = logits.shape
+    out = torch.empty(B, dtype=torch.int32)
+    for b in range(B):
+        p = params[b]
+        l = logits[b].float().cpu()
+        if p["temp"] <= 0:
+            out[b] = int(torch.argmax(l))
+            continue
+        g = torch.Generator().manual_seed(int(p["seed"]) ^ int(p["counter"]))
+        if p["mirostat"] == 2:
+            pr = torch.softmax(l / float(p["temp"]), -1)
+            m = float(mu[b]) if mu is not None else 2 * float(p["tau"])
+            keep = pr >= 2.0 ** (-m)
+            keep[torch.argmax(pr)] = True
+            q = torch.where(keep, pr, torch.zeros_like(pr))
+            q = q / q.sum()
+            t = int(torch.multinomial(q, 1, generator=g))
+            if mu is not None:
+                mu[b] = m - float(p["eta"]) * (-math.log2(float(q[t])) - float(p["tau"]))
+            out[b] = t
+            continue
+        vals, idx = torch.sort(l, descending=True, stable=True)
+        k = int(p["top_k"])
+        if 0 < k < V:
+            vals, idx = vals[:k], idx[:k]
+        pr = torch.softmax(vals, -1)
+        n = len(vals)
+        if p["top_p"] < 1:
+            cs = torch.cumsum(pr, 0)
+            hit = torch.nonzero(cs >= float(p["top_p"]))
+            if len(hit):
+                n = min(n, int(hit[0]) + 1)
+        if p["min_p"] > 0:
+            keepm = int((vals >= vals[0] + math.log(float(p["min_p"]))).sum())
+            n = min(n, max(1, keepm))
+        vals, idx = vals[:n], idx[:n]
+        q = torch.softmax(vals / float(p["temp"]), -1)
+        out[b] = int(idx[int(torch.multinomial(q, 1, generator=g))])
+    return out
+
+
+def penalties(logits: torch.Tensor, hist: torch.Tensor, hist_len: torch.Tensor, pen: torch.Tensor,
+              nl_token: int = -1, penalize_nl: Optional[torch.Tensor] = None):
+    """In-place repeat/frequency/presence penalties.  hist [B, L] i32 (-1 padded); pen [B,3]."""
+    B = logits.shape[0]
+    if not logits.is_cuda:
+        for b in range(B):
+            L = int(hist_len[b])
+            rp, fp, pp = (float(x) for x in pen[b])
+            toks = hist[b, :L].tolist()
+            for t in set(toks):
+                if t < 0:
+                    continue
+                if t == nl_token and penalize_nl is not None and not bool(penalize_nl[b]):
+                    continue
+                c = toks.count(t)
+                v = float(logits[b, t])
+                if rp != 1:
+                    v = v / rp if v > 0 else v * rp
+                v -= c * fp + (pp if c > 0 else 0)
+                logits[b, t] = v
+        return logits
+    _check(lib().la_penalties(logits.data_ptr(), logits.stride(0), B, hist.data_ptr(), hist.stride(0),
+                              hist_len.data_ptr(), pen.data_ptr(), nl_token, _ptr(penalize_nl), _stream()),
+           "la_penalties")
+    return logits

@@ -1,0 +1,333 @@
+// Memory-bound fused kernels: residual-add + RMSNorm/LayerNorm, RoPE + paged-KV append,
+// gated activations, embedding gather with dequant, weight materialisation.
+// Replaces ggml-cuda norm.cu / rope.cu / cpy.cu / unary.cu / binbcast.cu / getrows.cu
+// ([external]).
+//
+// Every kernel that consumes a GEMM output takes a `Src`: either S fp32 split-K slabs
+// (summed here, in the prologue -- the skinny GEMM never reduces) or one bf16 matrix
+// (the hipBLASLt prefill path).  All loads are 16-byte vectors (guide §6 G13).
+#include "qweight.h"
+
+namespace la {
+
+struct Src {
+  const void* p;
+  long slab;   // elements between split-K slabs
+  int S;       // number of fp32 slabs; 0 => p is a single bf16 matrix
+  const float* bias;  // optional per-column bias (length = row width), may be null
+};
+
+LA_DEV void load4(const Src& s, long idx, int col, float v[4]) {
+  if (s.S == 0) {
+    const bf16x4 b = *(const bf16x4*)((const bf16*)s.p + idx);
+    v[0] = (float)b[0]; v[1] = (float)b[1]; v[2] = (float)b[2]; v[3] = (float)b[3];
+  } else {
+    const float* f = (const float*)s.p + idx;
+    float4 a = *(const float4*)f;
+    for (int i = 1; i < s.S; ++i) {
+      const float4 b = *(const float4*)(f + (long)i * s.slab);
+      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    }
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  }
+  if (s.bias) {
+    const float4 b = *(const float4*)(s.bias + col);
+    v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// residual[t] += sum(src[t]) (optional);  out[t] = norm(residual[t]) * w (+ b)
+// mode 0 = RMSNorm, 1 = LayerNorm.  One 256-thread workgroup per row, row cached in VGPRs.
+constexpr int NORM_T = 256;
+constexpr int NORM_MAXV = 8;  // float4 per thread => D <= 8192
+
+__global__ __launch_bounds__(NORM_T) void add_norm_kernel(float* __restrict__ residual, Src add, int has_add,
+                                                          const float* __restrict__ w, const float* __restrict__ b,
+                                                          bf16* __restrict__ out, int D, float eps, int mode,
+                                                          float* __restrict__ out_f32) {
+  __shared__ float red[NORM_T / 64];
+  const int t = blockIdx.x;
+  const int nv = D >> 2;
+  float* rrow = residual + (long)t * D;
+  float v[NORM_MAXV][4];
+  float s1 = 0.f;
+#pragma unroll
+  for (int i = 0; i < NORM_MAXV; ++i) {
+    const int c = threadIdx.x + i * NORM_T;
+    if (c < nv) {
+      float4 r = *(const float4*)(rrow + 4 * c);
+      v[i][0] = r.x; v[i][1] = r.y; v[i][2] = r.z; v[i][3] = r.w;
+      if (has_add) {
+        float a[4];
+        load4(add, (long)t * D + 4 * c, 4 * c, a);
+        v[i][0] += a[0]; v[i][1] += a[1]; v[i][2] += a[2]; v[i][3] += a[3];
+        *(float4*)(rrow + 4 * c) = make_float4(v[i][0], v[i][1], v[i][2], v[i][3]);
+      }
+      s1 += (mode == 0) ? (v[i][0] * v[i][0] + v[i][1] * v[i][1] + v[i][2] * v[i][2] + v[i][3] * v[i][3])
+                        : (v[i][0] + v[i][1] + v[i][2] + v[i][3]);
+    }
+  }
+  float mean = 0.f, rstd;
+  if (mode == 0) {
+    const float ss = block_sum<NORM_T>(s1, red);
+    rstd = rsqrtf(ss / (float)D + eps);
+  } else {
+    mean = block_sum<NORM_T>(s1, red) / (float)D;
+    float s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NORM_MAXV; ++i) {
+      const int c = threadIdx.x + i * NORM_T;
+      if (c < nv) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { const float d = v[i][j] - mean; s2 += d * d; }
+      }
+    }
+    rstd = rsqrtf(block_sum<NORM_T>(s2, red) / (float)D + eps);
+  }
+  if (!out) return;
+#pragma unroll
+  for (int i = 0; i < NORM_MAXV; ++i) {
+    const int c = threadIdx.x + i * NORM_T;
+    if (c < nv) {
+      const float4 ww = *(const float4*)(w + 4 * c);
+      float4 bb = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (b) bb = *(const float4*)(b + 4 * c);
+      float o[4] = {(v[i][0] - mean) * rstd * ww.x + bb.x, (v[i][1] - mean) * rstd * ww.y + bb.y,
+                    (v[i][2] - mean) * rstd * ww.z + bb.z, (v[i][3] - mean) * rstd * ww.w + bb.w};
+      bf16x4 ob = {(bf16)o[0], (bf16)o[1], (bf16)o[2], (bf16)o[3]};
+      *(bf16x4*)(out + (long)t * D + 4 * c) = ob;
+      if (out_f32) *(float4*)(out_f32 + (long)t * D + 4 * c) = make_float4(o[0], o[1], o[2], o[3]);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// RoPE on q,k + append k,v into the paged cache.
+// qkv row layout: [Hq*Dh | Hkv*Dh | Hkv*Dh].  Cache: [num_blocks][Hkv][BS][Dh] bf16.
+// cos_sin: [max_pos][rot/2][2] f32 (host-precomputed table: guide App. B "trig tables").
+// mode 0 = NORM (adjacent pairs, llama/mistral GGUF), 1 = NEOX (half-split, phi-2).
+__global__ __launch_bounds__(256) void rope_kv_kernel(Src qkv, const int* __restrict__ pos,
+                                                      const int* __restrict__ slots,
+                                                      const float* __restrict__ cos_sin, int Hq, int Hkv,
+                                                      int Dh, int rot, int mode, bf16* __restrict__ q_out,
+                                                      bf16* __restrict__ kc, bf16* __restrict__ vc, int BS) {
+  const int t = blockIdx.x;
+  const int W = (Hq + 2 * Hkv) * Dh;
+  const int p = pos[t];
+  const int slot = slots ? slots[t] : -1;
+  const long row = (long)t * W;
+  const float* cs = cos_sin + (long)p * rot;  // rot/2 pairs x (cos, sin)
+  // work unit = 4 consecutive elements of one head (Dh % 4 == 0)
+  const int units = W >> 2;
+  for (int u = threadIdx.x; u < units; u += blockDim.x) {
+    const int col = u * 4;
+    const int head = col / Dh, d0 = col - head * Dh;
+    float v[4];
+    load4(qkv, row + col, col, v);
+    bf16* dst;
+    if (head < Hq) {
+      dst = q_out + ((long)t * Hq + head) * Dh + d0;
+    } else if (head < Hq + Hkv) {
+      if (slot < 0) continue;
+      const int kh = head - Hq, blk = slot / BS, off = slot - blk * BS;
+      dst = kc + (((long)blk * Hkv + kh) * BS + off) * Dh + d0;
+    } else {
+      if (slot < 0) continue;
+      const int vh = head - Hq - Hkv, blk = slot / BS, off = slot - blk * BS;
+      dst = vc + (((long)blk * Hkv + vh) * BS + off) * Dh + d0;
+      bf16x4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+      *(bf16x4*)dst = o;
+      continue;
+    }
+    if (mode == 0) {
+      // pairs (d0,d0+1), (d0+2,d0+3)
+#pragma unroll
+      for (int j = 0; j < 4; j += 2) {
+        const int pi = (d0 + j) >> 1;
+        if (d0 + j < rot) {
+          const float c = cs[2 * pi], s = cs[2 * pi + 1];
+          const float x0 = v[j], x1 = v[j + 1];
+          v[j] = x0 * c - x1 * s;
+          v[j + 1] = x0 * s + x1 * c;
+        }
+      }
+    } else {
+      // NEOX: pair (i, i + rot/2) for i < rot/2.  Each unit of the first half handles both halves.
+      const int half = rot >> 1;
+      if (d0 < half) {
+        float w2[4];
+        load4(qkv, row + col + half, col + half, w2);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int pi = d0 + j;
+          const float c = cs[2 * pi], s = cs[2 * pi + 1];
+          const float x0 = v[j], x1 = w2[j];
+          v[j] = x0 * c - x1 * s;
+          w2[j] = x0 * s + x1 * c;
+        }
+        bf16x4 o2 = {(bf16)w2[0], (bf16)w2[1], (bf16)w2[2], (bf16)w2[3]};
+        *(bf16x4*)(dst + half) = o2;
+      } else if (d0 < rot) {
+        continue;  // written by its partner unit
+      }
+    }
+    bf16x4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+    *(bf16x4*)dst = o;
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Activations.  mode 0: SwiGLU  out[t][i] = silu(x[t][i]) * x[t][F+i]   (src width 2F)
+//               mode 1: GELU(tanh) out[t][i] = gelu(x[t][i])             (src width F)
+//               mode 2: GELU-quick (CLIP)  x * sigmoid(1.702 x)
+__global__ __launch_bounds__(256) void act_kernel(Src src, bf16* __restrict__ out, int F, int mode) {
+  const int t = blockIdx.y;
+  const int c = (blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (c >= F) return;
+  const int W = (mode == 0) ? 2 * F : F;
+  float a[4];
+  load4(src, (long)t * W + c, c, a);
+  float o[4];
+  if (mode == 0) {
+    float b[4];
+    load4(src, (long)t * W + F + c, F + c, b);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = silu(a[j]) * b[j];
+  } else if (mode == 1) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float x = a[j];
+      o[j] = 0.5f * x * (1.f + tanhf(0.7978845608f * (x + 0.044715f * x * x * x)));
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = a[j] / (1.f + __expf(-1.702f * a[j]));
+  }
+  bf16x4 ob = {(bf16)o[0], (bf16)o[1], (bf16)o[2], (bf16)o[3]};
+  *(bf16x4*)(out + (long)t * F + c) = ob;
+}
+
+// sum split-K slabs (+bias) -> f32 or bf16 matrix [T][N]
+__global__ __launch_bounds__(256) void reduce_slabs_kernel(Src src, int N, float* __restrict__ out_f32,
+                                                           bf16* __restrict__ out_bf16) {
+  const int t = blockIdx.y;
+  const int c = (blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (c >= N) return;
+  float a[4];
+  load4(src, (long)t * N + c, c, a);
+  if (out_f32) *(float4*)(out_f32 + (long)t * N + c) = make_float4(a[0], a[1], a[2], a[3]);
+  if (out_bf16) {
+    bf16x4 ob = {(bf16)a[0], (bf16)a[1], (bf16)a[2], (bf16)a[3]};
+    *(bf16x4*)(out_bf16 + (long)t * N + c) = ob;
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Embedding gather with on-the-fly dequant: out[t][:] = W[tok[t]][:] * scale   (f32 out)
+template <int FMT>
+__global__ __launch_bounds__(256) void embed_kernel(QW w, const int* __restrict__ tok, float* __restrict__ out,
+                                                    float scale) {
+  const int t = blockIdx.x;
+  const int n = tok[t];
+  for (int k = threadIdx.x * 8; k < w.K; k += blockDim.x * 8) {
+    float v[8];
+    deq8_natural<FMT>(w, n, k, v);
+    float* o = out + (long)t * w.K + k;
+    *(float4*)o = make_float4(v[0] * scale, v[1] * scale, v[2] * scale, v[3] * scale);
+    *(float4*)(o + 4) = make_float4(v[4] * scale, v[5] * scale, v[6] * scale, v[7] * scale);
+  }
+}
+
+// W (any format) -> bf16 [N][K]   (prefill path keeps an HBM-resident bf16 copy)
+template <int FMT>
+__global__ __launch_bounds__(256) void dequant_kernel(QW w, bf16* __restrict__ out, long total8) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total8) return;
+  const int kc = w.K >> 3;
+  const int n = (int)(i / kc), k = (int)(i - (long)n * kc) * 8;
+  float v[8];
+  deq8_natural<FMT>(w, n, k, v);
+  bf16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = (bf16)v[j];
+  *(bf16x8*)(out + (long)n * w.K + k) = o;
+}
+
+}  // namespace la
+
+// C ABI ------------------------------------------------------------------------------
+using la::Src;
+
+extern "C" int la_add_norm(void* residual, const void* add_p, long add_slab, int add_S, const void* add_bias,
+                           int has_add, const void* w, const void* b, void* out, int T, int D, float eps,
+                           int mode, void* out_f32, void* stream) {
+  if ((D & 3) || D > la::NORM_T * la::NORM_MAXV * 4) return -1;
+  Src s{add_p, add_slab, add_S, (const float*)add_bias};
+  hipLaunchKernelGGL(la::add_norm_kernel, dim3(T), dim3(la::NORM_T), 0, (hipStream_t)stream, (float*)residual, s,
+                     has_add, (const float*)w, (const float*)b, (bf16*)out, D, eps, mode, (float*)out_f32);
+  return (int)hipGetLastError();
+}
+
+extern "C" int la_rope_kv(const void* qkv_p, long slab, int S, const void* bias, const int* pos, const int* slots,
+                          const float* cos_sin, int T, int Hq, int Hkv, int Dh, int rot, int mode, void* q_out,
+                          void* kc, void* vc, int BS, void* stream) {
+  if ((Dh & 3) || (rot & 3) || rot > Dh) return -1;
+  Src s{qkv_p, slab, S, (const float*)bias};
+  hipLaunchKernelGGL(la::rope_kv_kernel, dim3(T), dim3(256), 0, (hipStream_t)stream, s, pos, slots, cos_sin, Hq,
+                     Hkv, Dh, rot, mode, (bf16*)q_out, (bf16*)kc, (bf16*)vc, BS);
+  return (int)hipGetLastError();
+}
+
+extern "C" int la_act(const void* p, long slab, int S, const void* bias, void* out, int T, int F, int mode,
+                      void* stream) {
+  if (F & 3) return -1;
+  Src s{p, slab, S, (const float*)bias};
+  dim3 grid((F / 4 + 255) / 256, T);
+  hipLaunchKernelGGL(la::act_kernel, grid, dim3(256), 0, (hipStream_t)stream, s, (bf16*)out, F, mode);
+  return (int)hipGetLastError();
+}
+
+extern "C" int la_reduce_slabs(const void* p, long slab, int S, const void* bias, int T, int N, void* out_f32,
+                               void* out_bf16, void* stream) {
+  if (N & 3) return -1;
+  Src s{p, slab, S, (const float*)bias};
+  dim3 grid((N / 4 + 255) / 256, T);
+  hipLaunchKernelGGL(la::reduce_slabs_kernel, grid, dim3(256), 0, (hipStream_t)stream, s, N, (float*)out_f32,
+                     (bf16*)out_bf16);
+  return (int)hipGetLastError();
+}
+
+extern "C" int la_embed(int fmt, const void* p0, const void* p1, const void* p2, const void* p3, int N, int K,
+                        const int* tok, int T, void* out, float scale, void* stream) {
+  using namespace la;
+  if (K & 7) return -1;
+  QW w{(const uint8_t*)p0, (const uint8_t*)p1, (const uint8_t*)p2, (const uint8_t*)p3, N, K};
+  hipStream_t st = (hipStream_t)stream;
+  switch (fmt) {
+    case FMT_Q4_K: hipLaunchKernelGGL(embed_kernel<FMT_Q4_K>, dim3(T), dim3(256), 0, st, w, tok, (float*)out, scale); break;
+    case FMT_Q6_K: hipLaunchKernelGGL(embed_kernel<FMT_Q6_K>, dim3(T), dim3(256), 0, st, w, tok, (float*)out, scale); break;
+    case FMT_Q8_0: hipLaunchKernelGGL(embed_kernel<FMT_Q8_0>, dim3(T), dim3(256), 0, st, w, tok, (float*)out, scale); break;
+    case FMT_BF16: hipLaunchKernelGGL(embed_kernel<FMT_BF16>, dim3(T), dim3(256), 0, st, w, tok, (float*)out, scale); break;
+    default: return -2;
+  }
+  return (int)hipGetLastError();
+}
+
+extern "C" int la_dequant(int fmt, const void* p0, const void* p1, const void* p2, const void* p3, int N, int K,
+                          void* out, void* stream) {
+  using namespace la;
+  if (K & 7) return -1;
+  QW w{(const uint8_t*)p0, (const uint8_t*)p1, (const uint8_t*)p2, (const uint8_t*)p3, N, K};
+  const long total8 = (long)N * (K >> 3);
+  dim3 grid((unsigned)((total8 + 255) / 256));
+  hipStream_t st = (hipStream_t)stream;
+  switch (fmt) {
+    case FMT_Q4_K: hipLaunchKernelGGL(dequant_kernel<FMT_Q4_K>, grid, dim3(256), 0, st, w, (bf16*)out, total8); break;
+    case FMT_Q6_K: hipLaunchKernelGGL(dequant_kernel<FMT_Q6_K>, grid, dim3(256), 0, st, w, (bf16*)out, total8); break;
+    case FMT_Q8_0: hipLaunchKernelGGL(dequant_kernel<FMT_Q8_0>, grid, dim3(256), 0, st, w, (bf16*)out, total8); break;
+    case FMT_BF16: hipLaunchKernelGGL(dequant_kernel<FMT_BF16>, grid, dim3(256), 0, st, w, (bf16*)out, total8); break;
+    default: return -2;
+  }
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,400 @@
+// On-device sampling: the whole llama.cpp sampler chain runs on the GPU,
+// one workgroup per sequence, and only the chosen token ids (4 B/row) go back to the host
+// instead of the 513 KB logits row the reference copies every step.
+//
+// Chain semantics follow llama.cpp @ d5cb868 common/sampling.cpp [external] as driven by
+// LocalAI's grpc-server.cpp (params_parse / parse_options):
+//   logit_bias -> penalties (repeat/frequency/presence over last-n)   [la_penalties]
+//   mirostat == 0 : top_k -> tail-free(z) -> typical(p) -> top_p -> min_p -> temperature -> dist
+//   mirostat == 2 : temperature -> mirostat_v2(tau, eta)  (mu state kept on device)
+//   temperature <= 0 : greedy argmax
+// Philox4x32-10 keyed by (seed, per-row counter) supplies the uniform draw.
+#include "common.h"
+
+namespace la {
+
+struct SampleRow {
+  float temp, top_p, min_p, typical_p, tfs_z, tau, eta;
+  int top_k, mirostat, pad;
+  unsigned long long seed, counter;
+};
+
+constexpr int SMP_T = 1024;
+constexpr int CAP = 1024;
+
+LA_DEV uint32_t fkey(float f) {  // order-preserving float -> uint
+  const uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+LA_DEV void philox(uint64_t seed, uint64_t ctr, uint32_t out[4]) {
+  uint32_t c0 = (uint32_t)ctr, c1 = (uint32_t)(ctr >> 32), c2 = 0x9E3779B9u, c3 = 0x85EBCA6Bu;
+  uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0, n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+    c1 = (uint32_t)p1; c3 = (uint32_t)p0; c0 = n0; c2 = n2;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+  out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+struct SmpShared {
+  float cval[CAP];
+  int cidx[CAP];
+  float fred[SMP_T / 64];
+  int ired[SMP_T / 64];
+  unsigned hist[256];
+  float scan[SMP_T];
+  int tok2[CAP];
+  int count;
+  int sel;
+  uint32_t prefix;
+  int kleft;
+};
+
+// block-wide (max, argmax) with lowest-index tie break
+LA_DEV void block_argmax(float& v, int& i, SmpShared& sh) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(v, o, 64);
+    const int oi = __shfl_xor(i, o, 64);
+    if (ov > v || (ov == v && oi < i)) { v = ov; i = oi; }
+  }
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) { sh.fred[w] = v; sh.ired[w] = i; }
+  __syncthreads();
+  v = sh.fred[0]; i = sh.ired[0];
+  for (int k = 1; k < SMP_T / 64; ++k)
+    if (sh.fred[k] > v || (sh.fred[k] == v && sh.ired[k] < i)) { v = sh.fred[k]; i = sh.ired[k]; }
+}
+
+// k-th largest key (1-based) among row keys via 4-pass 8-bit radix select
+LA_DEV uint32_t radix_kth(const float* row, int V, int k, SmpShared& sh) {
+  uint32_t prefix = 0, mask = 0;
+  int kleft = k;
+  for (int shift = 24; shift >= 0; shift -= 8) {
+    for (int i = threadIdx.x; i < 256; i += SMP_T) sh.hist[i] = 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < V; i += SMP_T) {
+      const uint32_t key = fkey(row[i]);
+      if ((key & mask) == prefix) atomicAdd(&sh.hist[(key >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int acc = 0, d = 255;
+      for (; d > 0; --d) {
+        if (acc + (int)sh.hist[d] >= kleft) break;
+        acc += sh.hist[d];
+      }
+      sh.kleft = kleft - acc;
+      sh.prefix = prefix | ((uint32_t)d << shift);
+    }
+    __syncthreads();
+    prefix = sh.prefix;
+    kleft = sh.kleft;
+    mask |= 255u << shift;
+    __syncthreads();
+  }
+  return prefix;
+}
+
+// bitonic sort of sh.cval/cidx[0..n) descending by value (n padded to pow2 with -inf)
+LA_DEV void block_sort_desc(SmpShared& sh, int n) {
+  int P = 1;
+  while (P < n) P <<= 1;
+  for (int i = n + threadIdx.x; i < P; i += SMP_T) { sh.cval[i] = -INFINITY; sh.cidx[i] = 0x7fffffff; }
+  __syncthreads();
+  for (int k = 2; k <= P; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < P; i += SMP_T) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const bool desc = ((i & k) == 0);
+          const float a = sh.cval[i], b = sh.cval[ixj];
+          const bool a_first = (a > b) || (a == b && sh.cidx[i] < sh.cidx[ixj]);
+          if (desc ? !a_first : a_first) {
+            sh.cval[i] = b; sh.cval[ixj] = a;
+            const int t = sh.cidx[i]; sh.cidx[i] = sh.cidx[ixj]; sh.cidx[ixj] = t;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+__global__ __launch_bounds__(SMP_T) void sample_kernel(const float* __restrict__ logits, long ld, int V,
+                                                       const SampleRow* __restrict__ params, float* __restrict__ mu,
+                                                       int* __restrict__ out_tok, float* __restrict__ out_p) {
+  __shared__ SmpShared sh;
+  const int b = blockIdx.x;
+  const float* row = logits + (long)b * ld;
+  const SampleRow P = params[b];
+
+  // max / argmax
+  float mv = -INFINITY;
+  int mi = 0x7fffffff;
+  for (int i = threadIdx.x; i < V; i += SMP_T) {
+    const float v = row[i];
+    if (v > mv) { mv = v; mi = i; }
+  }
+  block_argmax(mv, mi, sh);
+  if (P.temp <= 0.f) {
+    if (threadIdx.x == 0) { out_tok[b] = mi; if (out_p) out_p[b] = 1.f; }
+    return;
+  }
+  uint32_t rnd[4];
+  philox(P.seed, P.counter, rnd);
+  const float u01 = ((rnd[0] >> 8) + 0.5f) * (1.0f / 16777216.0f);
+
+  if (P.mirostat == 2) {
+    // temperature, then keep p >= 2^-mu (prefix of the sorted list), renormalise, sample
+    const float invT = 1.f / P.temp;
+    float z = 0.f;
+    for (int i = threadIdx.x; i < V; i += SMP_T) z += __expf((row[i] - mv) * invT);
+    z = block_sum<SMP_T>(z, sh.fred);
+    const float m = mu[b];
+    const float thr = exp2f(-m) * z;  // unnormalised mass threshold
+    // contiguous chunk per thread for an ordered prefix scan
+    const int C = (V + SMP_T - 1) / SMP_T;
+    const int lo = threadIdx.x * C, hi = min(V, lo + C);
+    float part = 0.f;
+    for (int i = lo; i < hi; ++i) {
+      const float e = __expf((row[i] - mv) * invT);
+      if (e >= thr || i == mi) part += e;
+    }
+    sh.scan[threadIdx.x] = part;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float acc = 0.f;
+      for (int i = 0; i < SMP_T; ++i) { const float t = sh.scan[i]; sh.scan[i] = acc; acc += t; }
+      sh.fred[0] = acc;
+      sh.sel = mi;
+    }
+    __syncthreads();
+    const float zk = sh.fred[0];
+    const float target = u01 * zk;
+    float acc = sh.scan[threadIdx.x];
+    if (target >= acc && target < acc + part) {
+      for (int i = lo; i < hi; ++i) {
+        const float e = __expf((row[i] - mv) * invT);
+        if (!(e >= thr || i == mi)) continue;
+        acc += e;
+        if (target < acc) { sh.sel = i; break; }
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const int s = sh.sel;
+      const float ps = __expf((row[s] - mv) * invT) / zk;
+      out_tok[b] = s;
+      if (out_p) out_p[b] = ps;
+      mu[b] = m - P.eta * (-log2f(ps) - P.tau);
+    }
+    return;
+  }
+
+  // ---------------- standard chain
+  int k = P.top_k;
+  if (k <= 0 || k > V) k = V;
+  // threshold for top-k, and candidate prefilter by min_p (valid: min_p is relative to the max)
+  uint32_t key_k = 0;
+  if (k < V) key_k = radix_kth(row, V, k, sh);
+  // Z over the top-k set (top_p normalisation in llama.cpp is over the post-top-k list)
+  float zk = 0.f;
+  int cnt = 0;
+  for (int i = threadIdx.x; i < V; i += SMP_T) {
+    const float v = row[i];
+    if (k == V || fkey(v) >= key_k) zk += __expf(v - mv);
+  }
+  zk = block_sum<SMP_T>(zk, sh.fred);
+  float thr = -INFINITY;
+  if (P.min_p > 0.f && P.min_p <= 1.f) thr = mv + logf(P.min_p);
+  // count candidates; if > CAP raise the threshold to the CAP-th largest
+  for (int i = threadIdx.x; i < V; i += SMP_T) {
+    const float v = row[i];
+    if ((k == V || fkey(v) >= key_k) && v >= thr) ++cnt;
+  }
+  cnt = (int)block_sum<SMP_T>((float)cnt, sh.fred);
+  uint32_t key_c = 0;
+  bool capped = false;
+  if (cnt > CAP) { key_c = radix_kth(row, V, CAP, sh); capped = true; }
+  if (threadIdx.x == 0) sh.count = 0;
+  __syncthreads();
+  for (int i = threadIdx.x; i < V; i += SMP_T) {
+    const float v = row[i];
+    const uint32_t kk = fkey(v);
+    if ((k == V || kk >= key_k) && v >= thr && (!capped || kk >= key_c)) {
+      const int slot = atomicAdd(&sh.count, 1);
+      if (slot < CAP) { sh.cval[slot] = v; sh.cidx[slot] = i; }
+    }
+  }
+  __syncthreads();
+  int n = min(sh.count, CAP);
+  block_sort_desc(sh, n);
+  if (n > k) n = k;
+
+  if (threadIdx.x == 0) {
+    // tail-free sampling
+    if (P.tfs_z < 1.f && n > 2) {
+      float z = 0.f;
+      for (int i = 0; i < n; ++i) z += __expf(sh.cval[i] - mv);
+      // second derivatives of the sorted probabilities
+      float sum2 = 0.f;
+      for (int i = 0; i < n - 2; ++i) {
+        const float p0 = __expf(sh.cval[i] - mv) / z, p1 = __expf(sh.cval[i + 1] - mv) / z,
+                    p2 = __expf(sh.cval[i + 2] - mv) / z;
+        sum2 += fabsf((p0 - p1) - (p1 - p2));
+      }
+      int last = n;
+      if (sum2 > 0.f) {
+        float cum = 0.f;
+        for (int i = 0; i < n - 2; ++i) {
+          const float p0 = __expf(sh.cval[i] - mv) / z, p1 = __expf(sh.cval[i + 1] - mv) / z,
+                      p2 = __expf(sh.cval[i + 2] - mv) / z;
+          cum += fabsf((p0 - p1) - (p1 - p2)) / sum2;
+          if (cum > P.tfs_z) { last = i + 1; break; }
+        }
+      }
+      n = max(1, last);
+    }
+    sh.count = n;
+  }
+  __syncthreads();
+  n = sh.count;
+
+  // locally typical sampling: re-sort by |surprise - entropy| ascending, keep until mass >= p
+  if (P.typical_p < 1.f && n > 1) {
+    if (threadIdx.x == 0) {
+      float z = 0.f, H = 0.f;
+      for (int i = 0; i < n; ++i) z += __expf(sh.cval[i] - mv);
+      for (int i = 0; i < n; ++i) { const float p = __expf(sh.cval[i] - mv) / z; H -= p * logf(p); }
+      sh.fred[0] = z; sh.fred[1] = H;
+    }
+    __syncthreads();
+    const float z = sh.fred[0], H = sh.fred[1];
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += SMP_T) {
+      const float p = __expf(sh.cval[i] - mv) / z;
+      sh.scan[i] = sh.cval[i];   // logit of slot i
+      sh.tok2[i] = sh.cidx[i];   // token of slot i
+      sh.cval[i] = -fabsf(-logf(p) - H);
+      sh.cidx[i] = i;
+    }
+    __syncthreads();
+    block_sort_desc(sh, n);
+    if (threadIdx.x == 0) {
+      float cum = 0.f;
+      int last = n;
+      for (int i = 0; i < n; ++i) {
+        cum += __expf(sh.scan[sh.cidx[i]] - mv) / z;
+        if (cum >= P.typical_p) { last = i + 1; break; }
+      }
+      for (int i = 0; i < last; ++i) {
+        const int slot = sh.cidx[i];
+        sh.cval[i] = sh.scan[slot];
+        sh.cidx[i] = sh.tok2[slot];
+      }
+      sh.count = last;
+    }
+    __syncthreads();
+    n = sh.count;
+    block_sort_desc(sh, n);  // back to logit order for top_p
+    if (threadIdx.x == 0) {
+      float z2 = 0.f;
+      for (int i = 0; i < n; ++i) z2 += __expf(sh.cval[i] - mv);
+      sh.fred[0] = z2;
+    }
+    __syncthreads();
+    zk = sh.fred[0];
+  } else if (P.tfs_z < 1.f) {
+    // tail-free renormalises over its kept prefix
+    if (threadIdx.x == 0) {
+      float z2 = 0.f;
+      for (int i = 0; i < n; ++i) z2 += __expf(sh.cval[i] - mv);
+      sh.fred[0] = z2;
+    }
+    __syncthreads();
+    zk = sh.fred[0];
+  }
+
+  if (threadIdx.x == 0) {
+    // top_p over the current list (normalised by zk), then min_p (already prefiltered), then temperature
+    if (P.top_p < 1.f) {
+      float cum = 0.f;
+      int last = n;
+      for (int i = 0; i < n; ++i) {
+        cum += __expf(sh.cval[i] - mv) / zk;
+        if (cum >= P.top_p) { last = i + 1; break; }
+      }
+      n = last;
+    }
+    const float invT = 1.f / P.temp;
+    const float m0 = sh.cval[0];
+    float z = 0.f;
+    for (int i = 0; i < n; ++i) z += __expf((sh.cval[i] - m0) * invT);
+    const float target = u01 * z;
+    float acc = 0.f;
+    int sel = n - 1;
+    for (int i = 0; i < n; ++i) {
+      acc += __expf((sh.cval[i] - m0) * invT);
+      if (target < acc) { sel = i; break; }
+    }
+    out_tok[b] = sh.cidx[sel];
+    if (out_p) out_p[b] = __expf((sh.cval[sel] - m0) * invT) / z;
+  }
+}
+
+// penalties over the last-n window (llama_sampler_penalties): every distinct token t in the
+// window gets  l = l>0 ? l/rp : l*rp ;  l -= count*freq + (count>0)*presence
+__global__ __launch_bounds__(256) void penalties_kernel(float* __restrict__ logits, long ld,
+                                                        const int* __restrict__ hist, int hist_ld,
+                                                        const int* __restrict__ hist_len,
+                                                        const float* __restrict__ pen /* [B][3] */, int nl_token,
+                                                        const int* __restrict__ penalize_nl) {
+  const int b = blockIdx.x;
+  const int L = hist_len[b];
+  const float rp = pen[3 * b], fp = pen[3 * b + 1], pp = pen[3 * b + 2];
+  if (L <= 0 || (rp == 1.f && fp == 0.f && pp == 0.f)) return;
+  const int* h = hist + (long)b * hist_ld;
+  float* row = logits + (long)b * ld;
+  for (int i = threadIdx.x; i < L; i += blockDim.x) {
+    const int t = h[i];
+    if (t < 0) continue;
+    bool first = true;
+    int cnt = 0;
+    for (int j = 0; j < L; ++j) {
+      if (h[j] == t) {
+        if (j < i) { first = false; break; }
+        ++cnt;
+      }
+    }
+    if (!first) continue;
+    if (t == nl_token && penalize_nl && !penalize_nl[b]) continue;
+    float l = row[t];
+    if (rp != 1.f) l = (l > 0.f) ? l / rp : l * rp;
+    l -= (float)cnt * fp + (cnt > 0 ? pp : 0.f);
+    row[t] = l;
+  }
+}
+
+}  // namespace la
+
+extern "C" int la_sample(const float* logits, long ld, int B, int V, const void* params, float* mu, int* out_tok,
+                         float* out_p, void* stream) {
+  hipLaunchKernelGGL(la::sample_kernel, dim3(B), dim3(la::SMP_T), 0, (hipStream_t)stream, logits, ld, V,
+                     (const la::SampleRow*)params, mu, out_tok, out_p);
+  return (int)hipGetLastError();
+}
+
+extern "C" int la_penalties(float* logits, long ld, int B, const int* hist, int hist_ld, const int* hist_len,
+                            const float* pen, int nl_token, const int* penalize_nl, void* stream) {
+  hipLaunchKernelGGL(la::penalties_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, logits, ld, hist, hist_ld,
+                     hist_len, pen, nl_token, penalize_nl);
+  return (int)hipGetLastError();
+}
+
+extern "C" int la_sample_row_bytes() { return (int)sizeof(la::SampleRow); }

@@ -1,0 +1,238 @@
+"""Numerics of every HIP kernel against a plain PyTorch fp32 reference of the same op."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from localai_amd import ops
+from localai_amd.gguf import GGMLType, quantize
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+def _qw(N, K, t, seed=0, std=0.05):
+    rng = np.random.default_rng(seed)
+    w = rng.standard_normal((N, K)).astype(np.float32) * std
+    raw = quantize(w, t)
+    return ops.QWeight.from_raw(raw, t, (N, K), DEV, keep_ref=True)
+
+
+def test_library_loads():
+    assert ops.hip_available()
+    assert ops.lib().la_sample_row_bytes() == ops.SAMPLE_ROW_DTYPE.itemsize
+
+
+@pytest.mark.parametrize("t", [GGMLType.Q4_K, GGMLType.Q6_K, GGMLType.Q8_0, GGMLType.F16])
+@pytest.mark.parametrize("M", [1, 5, 16, 33, 64])
+def test_skinny_gemm(t, M):
+    N, K = 320, 1024
+    w = _qw(N, K, t)
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    y = ops.linear(x, w, force="skinny").dense()
+    ref = x.float().cpu() @ w.ref.t()
+    err = (y.cpu() - ref).abs().max().item()
+    assert err < 2e-2 * max(1.0, ref.abs().max().item()), err
+
+
+def test_skinny_gemm_splits_and_tail():
+    # N not a multiple of 64, K = 14 super-blocks (split-K by 7 / 14)
+    N, K, M = 200, 3584, 3
+    w = _qw(N, K, GGMLType.Q4_K, seed=3)
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    for S in (1, 2, 7, 14):
+        out = torch.empty(S, M, N, dtype=torch.float32, device=DEV)
+        rc = ops.lib().la_qgemm_skinny(w.fmt, *w.ptrs(), N, K, x.data_ptr(), K, M, S, out.data_ptr(), N, M * N,
+                                       ops._stream())
+        assert rc == 0
+        ref = x.float().cpu() @ w.ref.t()
+        assert (out.sum(0).cpu() - ref).abs().max().item() < 2e-2
+
+
+@pytest.mark.parametrize("M", [3, 100])
+def test_linear_multi_mixed_formats(M):
+    K = 512
+    ws = [_qw(128, K, GGMLType.Q4_K, seed=4), _qw(64, K, GGMLType.Q4_K, seed=5), _qw(64, K, GGMLType.Q6_K, seed=6)]
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    y = ops.linear_multi(x, ws).dense().cpu()
+    ref = torch.cat([x.float().cpu() @ w.ref.t() for w in ws], -1)
+    assert (y - ref).abs().max().item() < 5e-2
+
+
+def test_dequant_and_large_m_linear():
+    w = _qw(256, 512, GGMLType.Q4_K, seed=1)
+    wb = w.materialize_bf16().float().cpu()
+    assert (wb - w.ref).abs().max().item() < 1e-2
+    x = torch.randn(300, 512, device=DEV).to(torch.bfloat16)
+    y = ops.linear(x, w).dense().cpu()
+    ref = x.float().cpu() @ w.ref.t()
+    assert (y - ref).abs().max().item() < 5e-2
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_add_norm(mode):
+    T, D = 7, 4096
+    res = torch.randn(T, D, device=DEV)
+    add = torch.randn(3, T, D, device=DEV)
+    w = torch.rand(D, device=DEV) + 0.5
+    b = torch.randn(D, device=DEV) if mode == 1 else None
+    r_ref = res.cpu().clone()
+    out = ops.add_norm(res, ops.Partial(add), w, b, 1e-5, mode)
+    out_ref = ops.add_norm(r_ref, ops.Partial(add.cpu()), w.cpu(), None if b is None else b.cpu(), 1e-5, mode)
+    assert (res.cpu() - r_ref).abs().max().item() < 1e-4
+    assert (out.float().cpu() - out_ref.float()).abs().max().item() < 3e-2
+
+
+@pytest.mark.parametrize("mode,Dh,rot", [(0, 128, 128), (1, 80, 32), (1, 64, 64)])
+def test_rope_kv(mode, Dh, rot):
+    T, Hq, Hkv, BS, nblk = 5, 8, 2, 16, 6
+    qkv = torch.randn(2, T, (Hq + 2 * Hkv) * Dh, device=DEV)
+    pos = torch.tensor([0, 3, 7, 100, 5], dtype=torch.int32, device=DEV)
+    slots = torch.tensor([0, 17, 33, 50, -1], dtype=torch.int32, device=DEV)
+    cs = ops.rope_cos_sin(256, rot, 10000.0, DEV)
+    kc = torch.zeros(nblk, Hkv, BS, Dh, dtype=torch.bfloat16, device=DEV)
+    vc = torch.zeros_like(kc)
+    kr, vr = kc.cpu().clone(), vc.cpu().clone()
+    q = ops.rope_kv(ops.Partial(qkv), pos, slots, cs, Hq, Hkv, Dh, rot, mode, kc, vc, BS)
+    qr = ops.rope_kv(ops.Partial(qkv.cpu()), pos.cpu(), slots.cpu(), cs.cpu(), Hq, Hkv, Dh, rot, mode, kr, vr, BS)
+    assert (q.float().cpu() - qr.float()).abs().max().item() < 3e-2
+    assert (kc.float().cpu() - kr.float()).abs().max().item() < 3e-2
+    assert (vc.float().cpu() - vr.float()).abs().max().item() < 3e-2
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_act(mode):
+    T, F = 9, 1024
+    W = 2 * F if mode == 0 else F
+    x = torch.randn(2, T, W, device=DEV) * 3
+    y = ops.act(ops.Partial(x), F, mode)
+    yr = ops.act(ops.Partial(x.cpu()), F, mode)
+    assert (y.float().cpu() - yr.float()).abs().max().item() < 5e-2
+
+
+@pytest.mark.parametrize("t", [GGMLType.Q4_K, GGMLType.Q6_K, GGMLType.Q8_0])
+def test_embed(t):
+    w = _qw(100, 512, t)
+    tok = torch.tensor([0, 5, 99, 5], dtype=torch.int32, device=DEV)
+    e = ops.embed(tok, w, 2.0)
+    assert (e.cpu() - w.ref[tok.cpu().long()] * 2).abs().max().item() < 1e-5
+
+
+def _paged_setup(lens, Hkv, Dh, BS, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    maxb = max((l + BS - 1) // BS for l in lens)
+    nblk = sum((l + BS - 1) // BS for l in lens) + 3
+    kc = torch.randn(nblk, Hkv, BS, Dh, generator=g).to(torch.bfloat16)
+    vc = torch.randn(nblk, Hkv, BS, Dh, generator=g).to(torch.bfloat16)
+    perm = torch.randperm(nblk, generator=g)
+    bt = torch.zeros(len(lens), maxb, dtype=torch.int32)
+    c = 0
+    for i, l in enumerate(lens):
+        nb = (l + BS - 1) // BS
+        bt[i, :nb] = perm[c:c + nb]
+        c += nb
+    return kc, vc, bt
+
+
+@pytest.mark.parametrize("Hq,Hkv,Dh", [(32, 8, 128), (32, 32, 80), (8, 1, 64)])
+def test_attn_decode(Hq, Hkv, Dh):
+    lens = [1, 37, 300, 1025]
+    BS = 32
+    kc, vc, bt = _paged_setup(lens, Hkv, Dh, BS)
+    q = torch.randn(len(lens), Hq, Dh).to(torch.bfloat16)
+    sl = torch.tensor(lens, dtype=torch.int32)
+    scale = 1 / math.sqrt(Dh)
+    ref = ops.attn_decode(q, kc, vc, bt, sl, scale, max(lens))
+    out = ops.attn_decode(q.to(DEV), kc.to(DEV), vc.to(DEV), bt.to(DEV), sl.to(DEV), scale, max(lens))
+    assert (out.float().cpu() - ref.float()).abs().max().item() < 2e-2
+
+
+@pytest.mark.parametrize("Hq,Hkv,Dh", [(32, 8, 128), (32, 32, 80)])
+def test_attn_prefill(Hq, Hkv, Dh):
+    # (new tokens, total context) per sequence: plain prefill, prefix-cached, chunked
+    qlens = [70, 5, 33]
+    ctx = [70, 41, 200]
+    BS = 32
+    kc, vc, bt = _paged_setup(ctx, Hkv, Dh, BS, seed=1)
+    T = sum(qlens)
+    q = torch.randn(T, Hq, Dh).to(torch.bfloat16)
+    cu = torch.tensor([0] + list(np.cumsum(qlens)), dtype=torch.int32)
+    cl = torch.tensor(ctx, dtype=torch.int32)
+    scale = 1 / math.sqrt(Dh)
+    ref = ops.attn_prefill(q, kc, vc, cu, cl, bt, scale)
+    out = ops.attn_prefill(q.to(DEV), kc.to(DEV), vc.to(DEV), cu.to(DEV), cl.to(DEV), bt.to(DEV), scale)
+    assert (out.float().cpu() - ref.float()).abs().max().item() < 3e-2
+
+
+def _params(B, **kw):
+    p = np.zeros(B, dtype=ops.SAMPLE_ROW_DTYPE)
+    p["temp"] = kw.get("temp", 0.0)
+    p["top_p"] = kw.get("top_p", 1.0)
+    p["min_p"] = kw.get("min_p", 0.0)
+    p["typical_p"] = 1.0
+    p["tfs_z"] = 1.0
+    p["top_k"] = kw.get("top_k", 0)
+    p["mirostat"] = kw.get("mirostat", 0)
+    p["tau"] = 5.0
+    p["eta"] = 0.1
+    p["seed"] = np.arange(B) + 1
+    p["counter"] = 0
+    return p
+
+
+def test_sample_greedy():
+    B, V = 6, 128256
+    l = torch.randn(B, V, device=DEV)
+    t = ops.sample(l, _params(B))
+    assert torch.equal(t.cpu().long(), l.argmax(-1).cpu())
+
+
+def test_sample_topk1_equals_greedy():
+    B, V = 4, 32000
+    l = torch.randn(B, V, device=DEV)
+    t = ops.sample(l, _params(B, temp=0.8, top_k=1))
+    assert torch.equal(t.cpu().long(), l.argmax(-1).cpu())
+
+
+def test_sample_respects_topk_topp():
+    B, V = 256, 5000
+    l = torch.randn(B, V, device=DEV) * 3
+    p = _params(B, temp=1.0, top_k=40, top_p=0.9, min_p=0.05)
+    for c in range(3):
+        p["counter"] = c
+        t = ops.sample(l, p).cpu().long()
+        top40 = torch.topk(l.cpu(), 40, -1).indices
+        assert all(int(t[b]) in set(top40[b].tolist()) for b in range(B))
+
+
+def test_sample_distribution():
+    # temperature sampling over 4 tokens must follow softmax
+    B, V = 4096, 4
+    base = torch.tensor([2.0, 1.0, 0.0, -1.0])
+    l = base.repeat(B, 1).to(DEV)
+    p = _params(B, temp=1.0)
+    t = ops.sample(l, p).cpu()
+    freq = torch.bincount(t.long(), minlength=4).float() / B
+    assert (freq - torch.softmax(base, 0)).abs().max().item() < 0.03
+
+
+def test_sample_mirostat():
+    B, V = 8, 32000
+    l = torch.randn(B, V, device=DEV) * 4
+    mu = torch.full((B,), 10.0, device=DEV)
+    p = _params(B, temp=1.0, mirostat=2)
+    t = ops.sample(l, p, mu=mu).cpu()
+    assert ((t >= 0) & (t < V)).all()
+    assert not torch.allclose(mu.cpu(), torch.full((B,), 10.0))
+
+
+def test_penalties():
+    B, V = 3, 1000
+    l = torch.randn(B, V)
+    hist = torch.tensor([[1, 2, 2, -1], [5, 5, 5, 5], [7, -1, -1, -1]], dtype=torch.int32)
+    hl = torch.tensor([3, 4, 1], dtype=torch.int32)
+    pen = torch.tensor([[1.1, 0.1, 0.2]] * 3)
+    ref = ops.penalties(l.clone(), hist, hl, pen)
+    out = ops.penalties(l.to(DEV), hist.to(DEV), hl.to(DEV), pen.to(DEV))
+    assert (out.cpu() - ref).abs().max().item() < 1e-5
