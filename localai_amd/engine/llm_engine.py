@@ -361,7 +361,7 @@ class LLMEngine:
         }
         fb = ForwardBatch(tokens=st["tokens"], pos=st["pos"], slots=st["slots"], decode=True, block_tables=st["bt"],
                           seq_lens=st["lens"], max_len=self.ctx)
-        ws_P = max(1, (self.ctx + ops.DEC_PS - 1) // ops.DEC_PS)
+        ws_P, _ = ops.decode_partitions(Bp, self.model.Hkv, self.ctx)
         ws = (torch.empty(Bp * self.model.Hq * ws_P * self.model.Dh, dtype=torch.float32, device=dev),
               torch.empty(Bp * self.model.Hq * ws_P * 2, dtype=torch.float32, device=dev))
         s = torch.cuda.Stream(device=dev)

@@ -66,14 +66,16 @@ class ForwardBatch:
 
 
 class KVCache:
-    """Per-layer paged K/V pools: [num_blocks, Hkv_local, block_size, head_dim] bf16."""
+    """Per-layer paged K/V pools: K [num_blocks, Hkv_local, block_size, head_dim], V transposed
+    [num_blocks, Hkv_local, head_dim, block_size] (bf16)."""
 
     def __init__(self, n_layer: int, num_blocks: int, n_kv: int, block_size: int, head_dim: int, device,
                  dtype=torch.bfloat16):
         self.num_blocks, self.block_size = num_blocks, block_size
         self.k = [torch.zeros(num_blocks, n_kv, block_size, head_dim, dtype=dtype, device=device)
                   for _ in range(n_layer)]
-        self.v = [torch.zeros(num_blocks, n_kv, block_size, head_dim, dtype=dtype, device=device)
+        # V pages are stored transposed ([head_dim][block_size]) -- see ops/csrc/attention.hip
+        self.v = [torch.zeros(num_blocks, n_kv, head_dim, block_size, dtype=dtype, device=device)
                   for _ in range(n_layer)]
 
     @staticmethod

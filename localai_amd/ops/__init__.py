@@ -50,7 +50,7 @@ def lib():
             "la_reduce_slabs": [P, LNG, I, P, I, I, P, P, P],
             "la_embed": [I, P, P, P, P, I, I, P, I, P, F, P],
             "la_dequant": [I, P, P, P, P, I, I, P, P],
-            "la_attn_decode": [P, P, P, P, I, P, I, I, I, I, I, F, I, P, P, P, P],
+            "la_attn_decode": [P, P, P, P, I, P, I, I, I, I, I, F, I, I, P, P, P, P],
             "la_attn_prefill": [P, P, P, P, I, P, P, P, I, I, I, I, I, F, P, P],
             "la_sample": [P, LNG, I, I, P, P, P, P, P],
             "la_penalties": [P, LNG, I, P, I, P, P, I, P, P],
@@ -421,7 +421,7 @@ def rope_kv(qkv: Partial, pos: torch.Tensor, slots: Optional[torch.Tensor], cos_
             ok = sl >= 0
             blk, off = sl[ok] // block_size, sl[ok] % block_size
             k_cache[blk, :, off] = k[ok]
-            v_cache[blk, :, off] = v[ok]
+            v_cache[blk, :, :, off] = v[ok]
         if q_out is not None:
             q_out.copy_(q)
             return q_out
@@ -484,34 +484,49 @@ def embed(tokens: torch.Tensor, w: QWeight, scale: float = 1.0, out: Optional[to
 # Attention
 # ---------------------------------------------------------------------------------------
 
-DEC_PS = 256
+DEC_TARGET_WAVES = 4096  # ~16 waves per CU over 256 CUs
+
+
+def decode_partitions(B: int, Hkv: int, max_len: int) -> Tuple[int, int]:
+    """Split-KV partitioning for attn_decode: (P, PS).  Enough partitions to put ~16 waves on
+    every CU; each workgroup (4 waves) covers PS keys (multiple of 128)."""
+    max_len = max(1, max_len)
+    P = max(1, min(-(-DEC_TARGET_WAVES // (B * Hkv * 4)), -(-max_len // 128)))
+    PS = -(-(-(-max_len // P)) // 128) * 128
+    P = -(-max_len // PS)
+    return P, PS
 
 
 def attn_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, block_tables: torch.Tensor,
                 seq_lens: torch.Tensor, scale: float, max_seq_len: int, out: Optional[torch.Tensor] = None,
                 workspace: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:
-    """q [B,Hq,Dh] bf16; caches [nblk,Hkv,BS,Dh]; block_tables [B,maxb] i32; seq_lens [B] i32."""
+    """q [B,Hq,Dh] bf16; K cache [nblk,Hkv,BS,Dh]; V cache (transposed pages) [nblk,Hkv,Dh,BS];
+    block_tables [B,maxb] i32; seq_lens [B] i32."""
     B, Hq, Dh = q.shape
     nblk, Hkv, BS, Dh2 = k_cache.shape
-    if Dh2 != Dh or Hq % Hkv:
-        raise ValueError("attn_decode: head shape mismatch")
+    if Dh2 != Dh or Hq % Hkv or tuple(v_cache.shape) != (nblk, Hkv, Dh, BS):
+        raise ValueError("attn_decode: head/cache shape mismatch")
     if not q.is_cuda:
         return _attn_ref_decode(q, k_cache, v_cache, block_tables, seq_lens, scale)
-    P = max(1, (max_seq_len + DEC_PS - 1) // DEC_PS)
+    P, PS = decode_partitions(B, Hkv, max_seq_len)
     if out is None:
         out = torch.empty(B, Hq, Dh, dtype=torch.bfloat16, device=q.device)
-    if workspace is None or workspace[0].numel() < B * Hq * P * Dh:
-        po = torch.empty(B * Hq * P * Dh, dtype=torch.float32, device=q.device)
-        pml = torch.empty(B * Hq * P * 2, dtype=torch.float32, device=q.device)
+    need = B * Hq * P * Dh
+    if workspace is None or workspace[0].numel() < need or workspace[1].numel() < B * Hq * P * 2:
+        po = torch.empty(max(1, need), dtype=torch.float32, device=q.device)
+        pml = torch.empty(max(1, B * Hq * P * 2), dtype=torch.float32, device=q.device)
     else:
         po, pml = workspace
     _check(lib().la_attn_decode(q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr(),
-                                block_tables.shape[1], seq_lens.data_ptr(), B, Hq, Hkv, Dh, BS, float(scale), P,
+                                block_tables.shape[1], seq_lens.data_ptr(), B, Hq, Hkv, Dh, BS, float(scale), P, PS,
                                 out.data_ptr(), po.data_ptr(), pml.data_ptr(), _stream()), "la_attn_decode")
     return out
 
 
-def _gather_kv(cache, bt_row, L):
+def _gather_kv(cache, bt_row, L, transposed=False):
+    """-> [Hkv, L, Dh] from K pages [nblk,Hkv,BS,Dh] or transposed V pages [nblk,Hkv,Dh,BS]."""
+    if transposed:
+        cache = cache.transpose(2, 3)
     BS = cache.shape[2]
     nb = (L + BS - 1) // BS
     blocks = cache[bt_row[:nb].long()]                  # [nb, Hkv, BS, Dh]
@@ -526,7 +541,7 @@ def _attn_ref_decode(q, kc, vc, bt, sl, scale):
     for b in range(B):
         L = int(sl[b])
         k = _gather_kv(kc, bt[b], L).float()
-        v = _gather_kv(vc, bt[b], L).float()
+        v = _gather_kv(vc, bt[b], L, transposed=True).float()
         qq = q[b].float().view(Hkv, G, Dh)
         s = torch.einsum("hgd,hld->hgl", qq, k) * scale
         p = torch.softmax(s, -1)
@@ -579,7 +594,7 @@ def _attn_ref_prefill(q, kc, vc, cu_q, ctx_lens, bt, scale):
             continue
         L = int(ctx_lens[s])
         k = _gather_kv(kc, bt[s], L).float().repeat_interleave(G, 0)   # [Hq, L, Dh]
-        v = _gather_kv(vc, bt[s], L).float().repeat_interleave(G, 0)
+        v = _gather_kv(vc, bt[s], L, transposed=True).float().repeat_interleave(G, 0)
         qq = q[a:b].float().transpose(0, 1)                              # [Hq, ql, Dh]
         sc = torch.einsum("hqd,hld->hql", qq, k) * scale
         qpos = torch.arange(L - ql, L).view(-1, 1)

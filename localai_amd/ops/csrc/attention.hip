@@ -1,8 +1,9 @@
 // Paged attention for the engine (replaces ggml-cuda fattn*.cu / softmax.cu / the KQ,KQV
 // batched GEMMs of the non-FA path; SURVEY §2.8 K7, K11, K12, K15 [external]).
 //
-// KV cache layout (per layer): K, V each [num_blocks][Hkv][BS][Dh] bf16, so one page of one
-// kv-head is BS*Dh*2 contiguous bytes (8 KiB at BS=32, Dh=128).
+// KV cache layout (per layer): K [num_blocks][Hkv][BS][Dh] and V^T [num_blocks][Hkv][Dh][BS] bf16:
+// one page of one kv-head is BS*Dh*2 contiguous bytes (8 KiB at BS=32, Dh=128); V is stored
+// transposed inside the page so the PV MFMA's B operand (8 keys at one d) is a vector load.
 //
 // * attn_decode: one query row per sequence.  Workgroup = (partition of <=PS keys, kv head,
 //   sequence); the G = Hq/Hkv query heads sharing a kv head are packed so K/V are read from
@@ -15,147 +16,180 @@
 namespace la {
 
 // ----------------------------------------------------------------------------- decode
+// MFMA flash-decoding.  Per wave: one (sequence, kv-head) and a strided set of 32-key tiles.
+//   S^T[16 keys x 16 heads] = K[16 keys x Dh] . Q^T[Dh x 16 heads]   (keys on MFMA rows)
+//   -> lane l holds the scores of head l&15 for keys 4(l>>4)+i, so the running max needs only
+//      two cross-lane shuffles (xor 16, 32) and P is already the lane's A-operand fragment;
+//   O[16 heads x Dh] += P[16 heads x 32 keys] . V[32 keys x Dh]
+//   -> V is stored transposed per page ([Dh][BS]) so the B fragment (8 keys at one d) is a
+//      contiguous 8-byte load; no LDS staging, no transposes.
+// The 4 waves of a workgroup split one partition's tiles and merge through LDS; partitions
+// (flash-decoding split-KV) are merged by attn_decode_combine_kernel.  Scores live in the
+// log2 domain (scale * log2 e folded in) so every exponential is one v_exp_f32.
 constexpr int DEC_T = 256;
-constexpr int DEC_PS = 256;  // keys per partition
 
-template <int DH, int G>
+template <int DH>
 __global__ __launch_bounds__(DEC_T) void attn_decode_kernel(
     const bf16* __restrict__ q, const bf16* __restrict__ kc, const bf16* __restrict__ vc,
-    const int* __restrict__ block_tables, int max_blocks, const int* __restrict__ seq_lens, int Hkv, int BS,
-    float scale, bf16* __restrict__ out, float* __restrict__ part_o, float* __restrict__ part_ml, int P) {
-  constexpr int NC = DH / 8;  // 16-byte chunks per row
-  static_assert(NC <= 16, "head dim <= 128");
-  __shared__ float qs[G][DH];
-  __shared__ float sc[G][DEC_PS];
-  __shared__ float red[DEC_T / 64][G][DH];
-  __shared__ float stat[G][2];
+    const int* __restrict__ block_tables, int max_blocks, const int* __restrict__ seq_lens, int Hkv, int G,
+    int BS, float scale_log2, int PS, bf16* __restrict__ out, float* __restrict__ part_o,
+    float* __restrict__ part_ml, int P) {
+  constexpr int KC = (DH + 31) / 32;  // 32-wide k chunks of the QK^T product
+  constexpr int ND = DH / 16;         // 16-wide d tiles of the PV product
+  __shared__ float ow[4][16][DH];
+  __shared__ float mw[4][16], lw[4][16];
 
   const int p = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
   const int Hq = Hkv * G;
   const int L = seq_lens[b];
-  const int t0 = p * DEC_PS;
+  const int t0 = p * PS;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 15, g = lane >> 4;
   if (t0 >= L) {
-    // empty partition: publish a neutral partial
-    if (P > 1 && threadIdx.x < G) {
-      const int h = kvh * G + threadIdx.x;
-      float* ml = part_ml + (((long)b * Hq + h) * P + p) * 2;
-      ml[0] = -INFINITY;
-      ml[1] = 0.f;
-    }
     if (P > 1) {
-      for (int i = threadIdx.x; i < G * DH; i += DEC_T) {
+      for (int i = tid; i < G * DH; i += DEC_T) {
         const int h = kvh * G + i / DH;
         part_o[(((long)b * Hq + h) * P + p) * DH + (i % DH)] = 0.f;
+      }
+      if (tid < G) {
+        float* ml = part_ml + (((long)b * Hq + kvh * G + tid) * P + p) * 2;
+        ml[0] = -INFINITY;
+        ml[1] = 0.f;
       }
     }
     return;
   }
-  const int t1 = min(L, t0 + DEC_PS);
+  const int kend = min(L, t0 + PS);
   const int* bt = block_tables + (long)b * max_blocks;
 
-  for (int i = threadIdx.x; i < G * DH; i += DEC_T) {
-    const int h = i / DH, d = i % DH;
-    qs[h][d] = (float)q[((long)b * Hq + kvh * G + h) * DH + d] * scale;
+  // Q^T fragments: lane holds Q[head r][d = 32c + 8g .. +8]
+  bf16x8 qf[KC];
+#pragma unroll
+  for (int c = 0; c < KC; ++c) {
+    const int d = 32 * c + 8 * g;
+    bf16x8 v = {};
+    if (r < G && d < DH) v = *(const bf16x8*)(q + ((long)b * Hq + kvh * G + r) * DH + d);
+    qf[c] = v;
   }
-  __syncthreads();
 
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int grp = lane >> 4, c = lane & 15;  // 4 token-groups per wave, 16 lanes each
-  const int gid = wave * 4 + grp;             // 0..15
+  f32x4 o[ND];
+#pragma unroll
+  for (int i = 0; i < ND; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, lsum = 0.f;
 
-  // ---- scores
-  for (int t = t0 + gid; t < t1; t += 16) {
-    const int blk = bt[t / BS], off = t % BS;
-    float s[G];
+  for (int kb = t0 + 32 * wave; kb < kend; kb += 32 * 4) {
+    float s[2][4];
+    uint32_t vmask[2];
+    int blk[2], off[2];
 #pragma unroll
-    for (int h = 0; h < G; ++h) s[h] = 0.f;
-    if (c < NC) {
-      const bf16x8 kv = *(const bf16x8*)(kc + (((long)blk * Hkv + kvh) * BS + off) * DH + 8 * c);
+    for (int t = 0; t < 2; ++t) {
+      const int key0 = kb + 16 * t;
+      vmask[t] = 0;
+      if (key0 >= kend) {
+        blk[t] = 0; off[t] = 0;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float kf = (float)kv[j];
+        for (int i = 0; i < 4; ++i) s[t][i] = -INFINITY;
+        continue;
+      }
+      blk[t] = bt[key0 / BS];
+      off[t] = key0 % BS;
+      const bf16* krow = kc + (((long)blk[t] * Hkv + kvh) * BS + off[t] + r) * DH;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int h = 0; h < G; ++h) s[h] = fmaf(qs[h][8 * c + j], kf, s[h]);
+      for (int c = 0; c < KC; ++c) {
+        const int d = 32 * c + 8 * g;
+        bf16x8 a = {};
+        if (d < DH) a = *(const bf16x8*)(krow + d);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, qf[c], acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const bool ok = key0 + 4 * g + i < kend;
+        s[t][i] = ok ? acc[i] * scale_log2 : -INFINITY;
+        vmask[t] |= ok ? (1u << i) : 0u;
       }
     }
+    // online softmax for head r over this 32-key tile
+    float mx = fmaxf(fmaxf(fmaxf(s[0][0], s[0][1]), fmaxf(s[0][2], s[0][3])),
+                     fmaxf(fmaxf(s[1][0], s[1][1]), fmaxf(s[1][2], s[1][3])));
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mnew = fmaxf(m, mx);
+    const float msafe = (mnew == -INFINITY) ? 0.f : mnew;
+    const float alpha = exp2f(m - msafe);
+    bf16x8 pa;
+    float ps = 0.f;
 #pragma unroll
-    for (int h = 0; h < G; ++h) s[h] = group_sum<16>(s[h]);
-    if (c == 0) {
+    for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int h = 0; h < G; ++h) sc[h][t - t0] = s[h];
-    }
-  }
-  __syncthreads();
-
-  // ---- softmax per head (wave w handles heads w, w+4, ...)
-  const int n = t1 - t0;
-  for (int h = wave; h < G; h += DEC_T / 64) {
-    float m = -INFINITY;
-    for (int i = lane; i < n; i += 64) m = fmaxf(m, sc[h][i]);
-    m = wave_max(m);
-    float l = 0.f;
-    for (int i = lane; i < n; i += 64) {
-      const float e = __expf(sc[h][i] - m);
-      sc[h][i] = e;
-      l += e;
-    }
-    l = wave_sum(l);
-    if (lane == 0) {
-      stat[h][0] = m;
-      stat[h][1] = l;
-    }
-  }
-  __syncthreads();
-
-  // ---- P.V : lane chunk c owns d in [8c, 8c+8)
-  float acc[G][8];
-#pragma unroll
-  for (int h = 0; h < G; ++h)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[h][j] = 0.f;
-  if (c < NC) {
-    for (int t = t0 + gid; t < t1; t += 16) {
-      const int blk = bt[t / BS], off = t % BS;
-      const bf16x8 vv = *(const bf16x8*)(vc + (((long)blk * Hkv + kvh) * BS + off) * DH + 8 * c);
-#pragma unroll
-      for (int h = 0; h < G; ++h) {
-        const float pr = sc[h][t - t0];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc[h][j] = fmaf(pr, (float)vv[j], acc[h][j]);
+      for (int i = 0; i < 4; ++i) {
+        const float e = exp2f(s[t][i] - msafe);
+        ps += e;
+        pa[4 * t + i] = (bf16)e;
       }
+    lsum = lsum * alpha + ps;
+    m = mnew;
+    // O rows are heads 4g+i: fetch each row's alpha from the lane that owns that head
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float f = __shfl(alpha, 4 * g + i, 64);
+#pragma unroll
+      for (int nd = 0; nd < ND; ++nd) o[nd][i] *= f;
+    }
+    // PV: B fragment = V[keys 4g..4g+3 of sub-tile 0, 4g..4g+3 of sub-tile 1][d = 16nd + r]
+#pragma unroll
+    for (int nd = 0; nd < ND; ++nd) {
+      const int d = 16 * nd + r;
+      bf16x8 vb;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        bf16x4 v4 = {};
+        if (vmask[t]) {
+          v4 = *(const bf16x4*)(vc + (((long)blk[t] * Hkv + kvh) * DH + d) * BS + off[t] + 4 * g);
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (!(vmask[t] & (1u << i))) v4[i] = (bf16)0.f;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) vb[4 * t + i] = v4[i];
+      }
+      o[nd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, vb, o[nd], 0, 0, 0);
     }
   }
-  // reduce over the 4 token groups of the wave (lanes c, c+16, c+32, c+48)
-#pragma unroll
-  for (int h = 0; h < G; ++h)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float v = acc[h][j];
-      v += __shfl_xor(v, 16, 64);
-      v += __shfl_xor(v, 32, 64);
-      acc[h][j] = v;
-    }
-  if (grp == 0 && c < NC) {
-#pragma unroll
-    for (int h = 0; h < G; ++h)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) red[wave][h][8 * c + j] = acc[h][j];
+  // wave totals: lsum over the 4 lane groups (same head r)
+  lsum += __shfl_xor(lsum, 16, 64);
+  lsum += __shfl_xor(lsum, 32, 64);
+  if (g == 0) {
+    mw[wave][r] = m;
+    lw[wave][r] = lsum;
   }
+#pragma unroll
+  for (int nd = 0; nd < ND; ++nd)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ow[wave][4 * g + i][16 * nd + r] = o[nd][i];
   __syncthreads();
-  for (int i = threadIdx.x; i < G * DH; i += DEC_T) {
+  for (int i = tid; i < G * DH; i += DEC_T) {
     const int h = i / DH, d = i % DH;
-    float v = 0.f;
+    float M = -INFINITY;
 #pragma unroll
-    for (int w = 0; w < DEC_T / 64; ++w) v += red[w][h][d];
+    for (int w = 0; w < 4; ++w) M = fmaxf(M, mw[w][h]);
+    const float Ms = (M == -INFINITY) ? 0.f : M;
+    float num = 0.f, den = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const float f = exp2f(mw[w][h] - Ms);
+      num += f * ow[w][h][d];
+      den += f * lw[w][h];
+    }
     const int hq = kvh * G + h;
     if (P == 1) {
-      out[((long)b * Hq + hq) * DH + d] = (bf16)(v / stat[h][1]);
+      out[((long)b * Hq + hq) * DH + d] = (bf16)(den > 0.f ? num / den : 0.f);
     } else {
-      part_o[(((long)b * Hq + hq) * P + p) * DH + d] = v;
+      part_o[(((long)b * Hq + hq) * P + p) * DH + d] = num;
       if (d == 0) {
         float* ml = part_ml + (((long)b * Hq + hq) * P + p) * 2;
-        ml[0] = stat[h][0];
-        ml[1] = stat[h][1];
+        ml[0] = M;
+        ml[1] = den;
       }
     }
   }
@@ -168,18 +202,13 @@ __global__ __launch_bounds__(128) void attn_decode_combine_kernel(const float* _
   const long base = ((long)b * Hq + hq) * P;
   float M = -INFINITY;
   for (int i = 0; i < P; ++i) M = fmaxf(M, part_ml[(base + i) * 2]);
+  const float Ms = (M == -INFINITY) ? 0.f : M;
   float den = 0.f;
-  for (int i = 0; i < P; ++i) {
-    const float m = part_ml[(base + i) * 2];
-    if (m > -INFINITY) den += __expf(m - M) * part_ml[(base + i) * 2 + 1];
-  }
+  for (int i = 0; i < P; ++i) den += exp2f(part_ml[(base + i) * 2] - Ms) * part_ml[(base + i) * 2 + 1];
   for (int d = threadIdx.x; d < DH; d += blockDim.x) {
     float num = 0.f;
-    for (int i = 0; i < P; ++i) {
-      const float m = part_ml[(base + i) * 2];
-      if (m > -INFINITY) num += __expf(m - M) * part_o[(base + i) * DH + d];
-    }
-    out[((long)b * Hq + hq) * DH + d] = (bf16)(num / den);
+    for (int i = 0; i < P; ++i) num += exp2f(part_ml[(base + i) * 2] - Ms) * part_o[(base + i) * DH + d];
+    out[((long)b * Hq + hq) * DH + d] = (bf16)(den > 0.f ? num / den : 0.f);
   }
 }
 
@@ -240,20 +269,31 @@ __global__ __launch_bounds__(PF_T) void attn_prefill_kernel(
 
   for (int k0 = 0; k0 < kend; k0 += PF_KT) {
     __syncthreads();
-    // stage K tile rows and V^T tile: PF_KT keys x DP dims, 16-byte chunks
+    // stage the K tile (row-major) and the V^T tile ([d][key], copied from the transposed cache)
     for (int cidx = tid; cidx < PF_KT * (DP / 8); cidx += PF_T) {
       const int kr = cidx / (DP / 8), d = (cidx % (DP / 8)) * 8;
       const int key = k0 + kr;
-      bf16x8 kv = {}, vv = {};
+      bf16x8 kv = {};
       if (key < kend && d < DH) {
         const int blk = bt[key / BS], off = key % BS;
-        const long base = (((long)blk * Hkv + kvh) * BS + off) * DH + d;
-        kv = *(const bf16x8*)(kc + base);
-        vv = *(const bf16x8*)(vc + base);
+        kv = *(const bf16x8*)(kc + (((long)blk * Hkv + kvh) * BS + off) * DH + d);
       }
       *(bf16x8*)(ks + kr * KS + d) = kv;
+    }
+    for (int cidx = tid; cidx < DP * (PF_KT / 8); cidx += PF_T) {
+      const int d = cidx / (PF_KT / 8), q8 = (cidx % (PF_KT / 8)) * 8;
+      const int key = k0 + q8;
+      bf16x8 vv = {};
+      if (key < kend && d < DH) {
+        const int blk = bt[key / BS], off = key % BS;
+        vv = *(const bf16x8*)(vc + (((long)blk * Hkv + kvh) * DH + d) * BS + off);
+        if (key + 8 > kend) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) vt[(d + j) * VS + kr] = vv[j];
+          for (int j = 0; j < 8; ++j)
+            if (key + j >= kend) vv[j] = (bf16)0.f;
+        }
+      }
+      *(bf16x8*)(vt + d * VS + q8) = vv;
     }
     __syncthreads();
 
@@ -320,46 +360,27 @@ __global__ __launch_bounds__(PF_T) void attn_prefill_kernel(
 }  // namespace la
 
 // C ABI ------------------------------------------------------------------------------------
-template <int DH, int G>
-static void dec_launch(dim3 grid, hipStream_t st, const void* q, const void* kc, const void* vc, const int* bt,
-                       int maxb, const int* sl, int Hkv, int BS, float scale, void* out, float* po, float* pml,
-                       int P) {
-  hipLaunchKernelGGL((la::attn_decode_kernel<DH, G>), grid, dim3(la::DEC_T), 0, st, (const bf16*)q,
-                     (const bf16*)kc, (const bf16*)vc, bt, maxb, sl, Hkv, BS, scale, (bf16*)out, po, pml, P);
-}
-
-template <int DH>
-static int dec_dispatch_g(int G, dim3 grid, hipStream_t st, const void* q, const void* kc, const void* vc,
-                          const int* bt, int maxb, const int* sl, int Hkv, int BS, float scale, void* out, float* po,
-                          float* pml, int P) {
-  switch (G) {
-    case 1: dec_launch<DH, 1>(grid, st, q, kc, vc, bt, maxb, sl, Hkv, BS, scale, out, po, pml, P); break;
-    case 2: dec_launch<DH, 2>(grid, st, q, kc, vc, bt, maxb, sl, Hkv, BS, scale, out, po, pml, P); break;
-    case 4: dec_launch<DH, 4>(grid, st, q, kc, vc, bt, maxb, sl, Hkv, BS, scale, out, po, pml, P); break;
-    case 8: dec_launch<DH, 8>(grid, st, q, kc, vc, bt, maxb, sl, Hkv, BS, scale, out, po, pml, P); break;
-    default: return -3;
-  }
-  return 0;
-}
-
 extern "C" int la_attn_decode(const void* q, const void* kc, const void* vc, const int* block_tables, int max_blocks,
-                              const int* seq_lens, int B, int Hq, int Hkv, int Dh, int BS, float scale, int P,
+                              const int* seq_lens, int B, int Hq, int Hkv, int Dh, int BS, float scale, int P, int PS,
                               void* out, void* part_o, void* part_ml, void* stream) {
-  if (Hq % Hkv) return -1;
+  if (Hq % Hkv || Hq / Hkv > 16 || (BS % 16) || (PS % 128) || P < 1) return -1;
   const int G = Hq / Hkv;
   hipStream_t st = (hipStream_t)stream;
   dim3 grid(P, Hkv, B);
   float* po = (float*)part_o;
   float* pml = (float*)part_ml;
-  int rc;
+  const float sl2 = scale * 1.4426950408889634f;
+#define DEC(D)                                                                                                     \
+  hipLaunchKernelGGL(la::attn_decode_kernel<D>, grid, dim3(la::DEC_T), 0, st, (const bf16*)q, (const bf16*)kc,     \
+                     (const bf16*)vc, block_tables, max_blocks, seq_lens, Hkv, G, BS, sl2, PS, (bf16*)out, po, pml, P)
   switch (Dh) {
-    case 64: rc = dec_dispatch_g<64>(G, grid, st, q, kc, vc, block_tables, max_blocks, seq_lens, Hkv, BS, scale, out, po, pml, P); break;
-    case 80: rc = dec_dispatch_g<80>(G, grid, st, q, kc, vc, block_tables, max_blocks, seq_lens, Hkv, BS, scale, out, po, pml, P); break;
-    case 96: rc = dec_dispatch_g<96>(G, grid, st, q, kc, vc, block_tables, max_blocks, seq_lens, Hkv, BS, scale, out, po, pml, P); break;
-    case 128: rc = dec_dispatch_g<128>(G, grid, st, q, kc, vc, block_tables, max_blocks, seq_lens, Hkv, BS, scale, out, po, pml, P); break;
+    case 64: DEC(64); break;
+    case 80: DEC(80); break;
+    case 96: DEC(96); break;
+    case 128: DEC(128); break;
     default: return -2;
   }
-  if (rc) return rc;
+#undef DEC
   if (P > 1)
     hipLaunchKernelGGL(la::attn_decode_combine_kernel, dim3(Hq, B), dim3(128), 0, st, po, pml, P, Dh, (bf16*)out);
   return (int)hipGetLastError();

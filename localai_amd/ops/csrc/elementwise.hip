@@ -104,7 +104,8 @@ __global__ __launch_bounds__(NORM_T) void add_norm_kernel(float* __restrict__ re
 
 // ------------------------------------------------------------------------------------
 // RoPE on q,k + append k,v into the paged cache.
-// qkv row layout: [Hq*Dh | Hkv*Dh | Hkv*Dh].  Cache: [num_blocks][Hkv][BS][Dh] bf16.
+// qkv row layout: [Hq*Dh | Hkv*Dh | Hkv*Dh].  K cache [num_blocks][Hkv][BS][Dh], V cache transposed
+// per page: [num_blocks][Hkv][Dh][BS] (bf16).
 // cos_sin: [max_pos][rot/2][2] f32 (host-precomputed table: guide App. B "trig tables").
 // mode 0 = NORM (adjacent pairs, llama/mistral GGUF), 1 = NEOX (half-split, phi-2).
 __global__ __launch_bounds__(256) void rope_kv_kernel(Src qkv, const int* __restrict__ pos,
@@ -135,9 +136,9 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(Src qkv, const int* __rest
     } else {
       if (slot < 0) continue;
       const int vh = head - Hq - Hkv, blk = slot / BS, off = slot - blk * BS;
-      dst = vc + (((long)blk * Hkv + vh) * BS + off) * Dh + d0;
-      bf16x4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
-      *(bf16x4*)dst = o;
+      dst = vc + (((long)blk * Hkv + vh) * Dh + d0) * BS + off;  // V^T page layout [Dh][BS]
+#pragma unroll
+      for (int j = 0; j < 4; ++j) dst[(long)j * BS] = (bf16)v[j];
       continue;
     }
     if (mode == 0) {

@@ -92,7 +92,7 @@ def test_rope_kv(mode, Dh, rot):
     slots = torch.tensor([0, 17, 33, 50, -1], dtype=torch.int32, device=DEV)
     cs = ops.rope_cos_sin(256, rot, 10000.0, DEV)
     kc = torch.zeros(nblk, Hkv, BS, Dh, dtype=torch.bfloat16, device=DEV)
-    vc = torch.zeros_like(kc)
+    vc = torch.zeros(nblk, Hkv, Dh, BS, dtype=torch.bfloat16, device=DEV)
     kr, vr = kc.cpu().clone(), vc.cpu().clone()
     q = ops.rope_kv(ops.Partial(qkv), pos, slots, cs, Hq, Hkv, Dh, rot, mode, kc, vc, BS)
     qr = ops.rope_kv(ops.Partial(qkv.cpu()), pos.cpu(), slots.cpu(), cs.cpu(), Hq, Hkv, Dh, rot, mode, kr, vr, BS)
@@ -124,7 +124,7 @@ def _paged_setup(lens, Hkv, Dh, BS, seed=0):
     maxb = max((l + BS - 1) // BS for l in lens)
     nblk = sum((l + BS - 1) // BS for l in lens) + 3
     kc = torch.randn(nblk, Hkv, BS, Dh, generator=g).to(torch.bfloat16)
-    vc = torch.randn(nblk, Hkv, BS, Dh, generator=g).to(torch.bfloat16)
+    vc = torch.randn(nblk, Hkv, Dh, BS, generator=g).to(torch.bfloat16)  # transposed V pages
     perm = torch.randperm(nblk, generator=g)
     bt = torch.zeros(len(lens), maxb, dtype=torch.int32)
     c = 0
@@ -135,16 +135,28 @@ def _paged_setup(lens, Hkv, Dh, BS, seed=0):
     return kc, vc, bt
 
 
-@pytest.mark.parametrize("Hq,Hkv,Dh", [(32, 8, 128), (32, 32, 80), (8, 1, 64)])
-def test_attn_decode(Hq, Hkv, Dh):
+@pytest.mark.parametrize("Hq,Hkv,Dh,BS", [(32, 8, 128, 32), (32, 32, 80, 32), (8, 1, 64, 16), (64, 8, 128, 32),
+                                         (16, 1, 96, 64)])
+def test_attn_decode(Hq, Hkv, Dh, BS):
     lens = [1, 37, 300, 1025]
-    BS = 32
     kc, vc, bt = _paged_setup(lens, Hkv, Dh, BS)
     q = torch.randn(len(lens), Hq, Dh).to(torch.bfloat16)
     sl = torch.tensor(lens, dtype=torch.int32)
     scale = 1 / math.sqrt(Dh)
     ref = ops.attn_decode(q, kc, vc, bt, sl, scale, max(lens))
-    out = ops.attn_decode(q.to(DEV), kc.to(DEV), vc.to(DEV), bt.to(DEV), sl.to(DEV), scale, max(lens))
+    for ml in (max(lens), 4096):  # exact bound and the graph-capture bound (many empty partitions)
+        out = ops.attn_decode(q.to(DEV), kc.to(DEV), vc.to(DEV), bt.to(DEV), sl.to(DEV), scale, ml)
+        assert (out.float().cpu() - ref.float()).abs().max().item() < 2e-2
+
+
+def test_attn_decode_batch1_long():
+    Hq, Hkv, Dh, BS = 32, 8, 128, 32
+    lens = [3000]
+    kc, vc, bt = _paged_setup(lens, Hkv, Dh, BS, seed=7)
+    q = torch.randn(1, Hq, Dh).to(torch.bfloat16)
+    sl = torch.tensor(lens, dtype=torch.int32)
+    ref = ops.attn_decode(q, kc, vc, bt, sl, 0.088, 3000)
+    out = ops.attn_decode(q.to(DEV), kc.to(DEV), vc.to(DEV), bt.to(DEV), sl.to(DEV), 0.088, 3000)
     assert (out.float().cpu() - ref.float()).abs().max().item() < 2e-2
 
 
