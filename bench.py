@@ -78,7 +78,11 @@ def main():
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-    dev = f"cuda:{local}"
+    dev = f"cuda:{local}" if torch.cuda.is_available() else "cpu"  # cpu: dev smoke runs only
+
+    def sync():
+        if dev != "cpu":
+            torch.cuda.synchronize()
 
     from localai_amd.models import synth
 
@@ -116,20 +120,20 @@ def main():
 
     for w in range(args.warmup):
         wave(-1 - w)
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     ttfts, tokens = [], 0
     for s in range(args.steps):
         tt, nt = wave(s)
         ttfts += tt
         tokens += nt
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     elapsed = time.perf_counter() - t0
 
     all_ttft, tot_tokens, max_el = ttfts, tokens, elapsed
@@ -224,6 +228,8 @@ class HttpRunner:
         s.bind(("127.0.0.1", 0))
         self.port = s.getsockname()[1]
         s.close()
+        self.eng = eng
+        eng.start()  # engine loop thread: the servicer only enqueues requests
         self.app, self.model_name = create_app_for_engine(eng, name="llama3-8b-instruct")
         import uvicorn
         cfg = uvicorn.Config(self.app, host="127.0.0.1", port=self.port, log_level="warning", loop="asyncio",
@@ -277,6 +283,7 @@ class HttpRunner:
     def close(self):
         self.server.should_exit = True
         self.th.join(timeout=10)
+        self.eng.shutdown()
 
 
 if __name__ == "__main__":

@@ -1,0 +1,163 @@
+"""HTTP application factory (`core/http/app.go`): middleware chain + route registration.
+
+Middleware order mirrors the reference: metrics (api_call histogram) -> API-key auth
+(Authorization: Bearer / x-api-key / xi-api-key; GET exemptions) -> CORS -> routes; errors are
+`{"error": {"code", "message"}}` JSON, or bare status codes with `opaque_errors`.
+"""
+from __future__ import annotations
+
+import hmac
+import json
+import logging
+import os
+import re
+import time
+from typing import Optional, Tuple
+
+from fastapi import FastAPI, Request
+from fastapi.responses import JSONResponse, Response
+from starlette.middleware.base import BaseHTTPMiddleware
+
+from ..config.app_config import ApplicationConfig
+from ..config.backend_config import BackendConfig
+from .openai_routes import APIError
+from .state import AppState
+
+log = logging.getLogger("localai_amd.http")
+
+
+def _extract_key(request: Request) -> str:
+    auth = request.headers.get("authorization", "")
+    if auth:
+        if auth[:7].lower() == "bearer ":
+            return auth[7:].strip()
+        return ""
+    return request.headers.get("x-api-key", "") or request.headers.get("xi-api-key", "")
+
+
+class AuthMiddleware(BaseHTTPMiddleware):
+    def __init__(self, app, state: AppState):
+        super().__init__(app)
+        self.state = state
+        self.exempt = [re.compile(p) for p in state.cfg.http_get_exempted_endpoints]
+
+    def _keys(self):
+        keys = list(self.state.cfg.api_keys)
+        dyn = os.path.join(self.state.cfg.dynamic_config_dir or "", "api_keys.json")
+        if self.state.cfg.dynamic_config_dir and os.path.isfile(dyn):
+            try:
+                with open(dyn) as f:
+                    keys += [k for k in json.load(f) if isinstance(k, str)]
+            except (OSError, ValueError):
+                pass
+        return keys
+
+    async def dispatch(self, request: Request, call_next):
+        keys = self._keys()
+        if keys:
+            cfg = self.state.cfg
+            skip = cfg.disable_api_key_requirement_for_http_get and request.method == "GET" and \
+                any(rx.search(request.url.path) for rx in self.exempt)
+            if not skip:
+                k = _extract_key(request)
+                if cfg.use_subtle_key_comparison:
+                    good = any(hmac.compare_digest(k.encode(), v.encode()) for v in keys)
+                else:
+                    good = k in keys
+                if not good:
+                    if cfg.opaque_errors:
+                        return Response(status_code=403)
+                    return Response("missing or malformed API Key", status_code=403)
+        return await call_next(request)
+
+
+class MetricsMiddleware(BaseHTTPMiddleware):
+    def __init__(self, app, state: AppState):
+        super().__init__(app)
+        self.state = state
+
+    async def dispatch(self, request: Request, call_next):
+        t0 = time.perf_counter()
+        resp = await call_next(request)
+        if request.url.path != "/metrics":
+            self.state.metrics.api_call.labels(request.method, request.url.path).observe(time.perf_counter() - t0)
+        return resp
+
+
+def create_app(state: AppState) -> FastAPI:
+    from contextlib import asynccontextmanager
+
+    @asynccontextmanager
+    async def lifespan(app):
+        state.manager.start_watchdog()
+        yield
+        await state.manager.stop_all()
+
+    app = FastAPI(title="LocalAI (MI355X)", lifespan=lifespan, docs_url="/swagger", openapi_url="/swagger/doc.json")
+    cfg = state.cfg
+
+    @app.exception_handler(APIError)
+    async def _api_err(request: Request, e: APIError):
+        if cfg.opaque_errors:
+            return Response(status_code=e.code)
+        return JSONResponse({"error": {"code": e.code, "message": str(e), "type": ""}}, status_code=e.code)
+
+    @app.exception_handler(Exception)
+    async def _err(request: Request, e: Exception):
+        log.exception("request failed: %s %s", request.method, request.url.path)
+        if cfg.opaque_errors:
+            return Response(status_code=500)
+        return JSONResponse({"error": {"code": 500, "message": str(e), "type": ""}}, status_code=500)
+
+    if not cfg.disable_metrics:
+        app.add_middleware(MetricsMiddleware, state=state)
+    app.add_middleware(AuthMiddleware, state=state)
+    if cfg.cors:
+        from starlette.middleware.cors import CORSMiddleware
+        origins = [o for o in cfg.cors_allow_origins.split(",") if o] or ["*"]
+        app.add_middleware(CORSMiddleware, allow_origins=origins, allow_methods=["*"], allow_headers=["*"])
+
+    from . import openai_routes, localai_routes, files_routes, gallery_routes
+    app.include_router(openai_routes.build_router(state))
+    app.include_router(files_routes.build_router(state))
+    app.include_router(localai_routes.build_router(state))
+    if not cfg.disable_gallery_endpoint:
+        app.include_router(gallery_routes.build_router(state))
+    app.state.localai = state
+    return app
+
+
+LLAMA3_CHAT_MESSAGE = ("<|start_header_id|>{{ .RoleName }}<|end_header_id|>\n\n{{.Content }}<|eot_id|>")
+LLAMA3_CHAT = "<|begin_of_text|>{{.Input }}\n<|start_header_id|>assistant<|end_header_id|>"
+
+
+def create_app_for_engine(engine, name: str = "llama3-8b-instruct", models_path: Optional[str] = None,
+                          app_config: Optional[ApplicationConfig] = None) -> Tuple[FastAPI, str]:
+    """Serve an already-constructed LLMEngine under `name` (bench / embedding use).
+
+    The model config is the one the reference's guesser produces for a Llama-3 GGUF
+    (core/config/guesser.go LLaMa3 defaults), with mirostat disabled so the sampler chain is the
+    plain top-k/top-p/temperature one."""
+    import tempfile
+    from ..grpc.rpc import EmbeddedBackend
+    from ..grpc.servicer import EngineServicer
+    from ..grpc import backend_pb as pb
+
+    ac = app_config or ApplicationConfig()
+    ac.models_path = models_path or tempfile.mkdtemp(prefix="localai_models_")
+    state = AppState(ac)
+    sv = EngineServicer(device=str(engine.device))
+    sv.engine = engine
+    sv.model_name = name
+    sv.state = pb.StatusResponse.READY
+    state.manager.register(name, "localai-amd", EmbeddedBackend(sv), servicer=sv)
+    bc = BackendConfig({
+        "name": name, "backend": "localai-amd", "context_size": engine.cfg.context_size, "mirostat": 0,
+        "parameters": {"model": os.path.basename(engine.cfg.model_path), "temperature": 0.8, "top_k": 40,
+                       "top_p": 0.95},
+        "template": {"chat_message": LLAMA3_CHAT_MESSAGE, "chat": LLAMA3_CHAT},
+        "stopwords": ["<|eot_id|>"],
+    })
+    bc.set_defaults()
+    state.configs.add(bc)
+    return create_app(state), name

@@ -1,0 +1,319 @@
+"""Our native engine behind the `backend.Backend` contract.
+
+Counterpart of the reference's C++ backend service (`backend/cpp/llama/grpc-server.cpp:
+2304-2458` BackendServiceImpl): Health, LoadModel, Predict, PredictStream, Embedding,
+TokenizeString, Status, GetMetrics, plus the in-memory vector store RPCs (the reference's
+`local-store` Go backend, `backend/go/stores/store.go`, here on the GPU).  The same object is
+used in-process by the gateway (the reference's unused `embedBackend` idea,
+`pkg/grpc/embed.go`) or served over gRPC by `localai_amd.worker`.
+
+Methods are asyncio coroutines with grpc.aio signatures `(request, context)`; `context`
+may be None in-process.
+"""
+from __future__ import annotations
+
+import asyncio
+import json
+import logging
+import os
+import threading
+import time
+from typing import Optional
+
+from . import backend_pb as pb
+
+log = logging.getLogger("localai_amd.servicer")
+
+
+class Unimplemented(Exception):
+    pass
+
+
+class EngineServicer:
+    def __init__(self, device: Optional[str] = None, tp=None):
+        self.engine = None
+        self.device = device
+        self.tp = tp
+        self.store = None
+        self.state = pb.StatusResponse.UNINITIALIZED
+        self._lock = threading.Lock()
+        self.model_name = ""
+
+    # ------------------------------------------------------------------ helpers
+    async def _abort(self, context, code, msg):
+        if context is not None:
+            import grpc
+            await context.abort(code, msg)
+        raise RuntimeError(msg)
+
+    # ------------------------------------------------------------------ RPCs
+    async def Health(self, request, context=None):
+        return pb.Reply(message=b"OK")
+
+    async def LoadModel(self, request, context=None):
+        from ..engine.llm_engine import EngineConfig, LLMEngine
+        path = request.ModelFile or request.Model
+        if not os.path.isfile(path):
+            return pb.Result(success=False, message=f"model file not found: {path}")
+        try:
+            import torch
+            dev = self.device
+            if dev is None:
+                if torch.cuda.is_available():
+                    idx = int(request.MainGPU) if request.MainGPU.isdigit() else 0
+                    dev = f"cuda:{idx}"
+                else:
+                    dev = "cpu"
+            ctx = request.ContextSize or 2048
+            if request.MaxModelLen:
+                ctx = request.MaxModelLen
+            cfg = EngineConfig(
+                model_path=path, device=dev, context_size=ctx,
+                max_num_seqs=int(os.environ.get("LOCALAI_MAX_NUM_SEQS", os.environ.get("LLAMACPP_PARALLEL", "256")) or 256),
+                max_batched_tokens=max(int(request.NBatch or 0), 8192),
+                gpu_memory_utilization=request.GPUMemoryUtilization or 0.85,
+                embeddings=request.Embeddings, rope_freq_base=request.RopeFreqBase,
+                rope_freq_scale=request.RopeFreqScale, rope_scaling=request.RopeScaling,
+                use_graphs=not request.EnforceEager)
+            loop = asyncio.get_running_loop()
+            eng = await loop.run_in_executor(None, lambda: LLMEngine(cfg, tp=self.tp))
+            await loop.run_in_executor(None, eng.warmup)
+            eng.start()
+            with self._lock:
+                if self.engine is not None:
+                    self.engine.shutdown()
+                self.engine = eng
+                self.model_name = os.path.basename(path)
+                self.state = pb.StatusResponse.READY
+            return pb.Result(success=True, message="Loaded")
+        except Exception as e:  # report, do not crash the worker
+            log.exception("LoadModel failed")
+            self.state = pb.StatusResponse.ERROR
+            return pb.Result(success=False, message=f"could not load model: {e}")
+
+    def _require_engine(self):
+        if self.engine is None:
+            raise RuntimeError("no model loaded")
+        return self.engine
+
+    def _prompt(self, request):
+        eng = self._require_engine()
+        if request.UseTokenizerTemplate and len(request.Messages) and not request.Prompt:
+            return self._apply_chat_template(request)
+        return request.Prompt
+
+    def _apply_chat_template(self, request) -> str:
+        tok = self.engine.tokenizer
+        msgs = [{"role": m.role, "content": m.content} for m in request.Messages]
+        tpl = tok.chat_template
+        if tpl:
+            try:
+                import jinja2
+                env = jinja2.Environment(trim_blocks=True, lstrip_blocks=True)
+                env.globals["raise_exception"] = lambda m: (_ for _ in ()).throw(ValueError(m))
+                bos = tok.tokens[tok.bos_id] if tok.bos_id is not None and tok.bos_id >= 0 else ""
+                eos = tok.tokens[tok.eos_id] if tok.eos_id is not None and tok.eos_id >= 0 else ""
+                return env.from_string(tpl).render(messages=msgs, add_generation_prompt=True, bos_token=bos,
+                                                   eos_token=eos)
+            except Exception:
+                log.exception("chat template failed; falling back to plain join")
+        return "\n".join(f"{m['role']}: {m['content']}" for m in msgs) + "\nassistant:"
+
+    def _params(self, request):
+        from ..engine.sampling_params import SamplingParams
+        return SamplingParams.from_predict_options(request)
+
+    async def PredictStream(self, request, context=None):
+        eng = self._require_engine()
+        loop = asyncio.get_running_loop()
+        q: asyncio.Queue = asyncio.Queue()
+
+        def cb(ev):
+            loop.call_soon_threadsafe(q.put_nowait, ev)
+
+        prompt = self._prompt(request)
+        rid = eng.add_request(prompt, self._params(request), cb)
+        finished = False
+        try:
+            while True:
+                ev = await q.get()
+                if ev.error and ev.finished:
+                    raise RuntimeError(ev.error)
+                if ev.finished:
+                    finished = True
+                    if ev.text:
+                        yield pb.Reply(message=ev.text)
+                    yield pb.Reply(message=b"", tokens=ev.completion_tokens, prompt_tokens=ev.prompt_tokens)
+                    return
+                if ev.text:
+                    # coalesce whatever is already queued into one message (allowed by the contract)
+                    buf = bytearray(ev.text)
+                    fin = None
+                    while not q.empty():
+                        nxt = q.get_nowait()
+                        if nxt.finished:
+                            fin = nxt
+                            break
+                        buf.extend(nxt.text)
+                    yield pb.Reply(message=bytes(buf))
+                    if fin is not None:
+                        finished = True
+                        if fin.error:
+                            raise RuntimeError(fin.error)
+                        if fin.text:
+                            yield pb.Reply(message=fin.text)
+                        yield pb.Reply(message=b"", tokens=fin.completion_tokens, prompt_tokens=fin.prompt_tokens)
+                        return
+        finally:
+            if not finished:
+                eng.abort(rid)  # client went away / generator closed: free the sequence (fixes Q4)
+
+    async def Predict(self, request, context=None):
+        eng = self._require_engine()
+        loop = asyncio.get_running_loop()
+        fut = loop.create_future()
+        chunks = bytearray()
+
+        def cb(ev):
+            def apply():
+                chunks.extend(ev.text)
+                if ev.finished and not fut.done():
+                    fut.set_result(ev)
+            loop.call_soon_threadsafe(apply)
+
+        rid = eng.add_request(self._prompt(request), self._params(request), cb)
+        try:
+            ev = await fut
+        except asyncio.CancelledError:
+            eng.abort(rid)
+            raise
+        if ev.error:
+            await self._abort(context, _status("INTERNAL"), ev.error)  # fixes Q9 (error => gRPC error)
+        return pb.Reply(message=bytes(chunks), tokens=ev.completion_tokens, prompt_tokens=ev.prompt_tokens)
+
+    async def Embedding(self, request, context=None):
+        eng = self._require_engine()
+        loop = asyncio.get_running_loop()
+        inp = list(request.EmbeddingTokens) if len(request.EmbeddingTokens) else (request.Embeddings or request.Prompt)
+        vecs = await loop.run_in_executor(None, lambda: eng.embed([inp]))
+        return pb.EmbeddingResult(embeddings=vecs[0])
+
+    async def TokenizeString(self, request, context=None):
+        eng = self._require_engine()
+        toks = eng.tokenize(self._prompt(request))
+        return pb.TokenizationResponse(length=len(toks), tokens=toks)
+
+    async def Status(self, request, context=None):
+        st = pb.StatusResponse(state=self.state)
+        if self.engine is not None and self.engine.busy:
+            st.state = pb.StatusResponse.BUSY
+        try:
+            import psutil
+            rss = psutil.Process().memory_info().rss
+            st.memory.breakdown["host_rss"] = rss
+            total = rss
+            import torch
+            if self.engine is not None and self.engine.device.type == "cuda":
+                free, tot = torch.cuda.mem_get_info(self.engine.device)
+                st.memory.breakdown["gpu_used"] = tot - free
+                st.memory.breakdown["gpu_total"] = tot
+                st.memory.breakdown["kv_blocks_free"] = self.engine.sched.blocks().num_free
+                total += tot - free
+            st.memory.total = total
+        except Exception:
+            pass
+        return st
+
+    async def GetMetrics(self, request, context=None):
+        r = pb.MetricsResponse()
+        if self.engine is not None:
+            s = self.engine.last_request_stats or {}
+            r.slot_id = int(s.get("id", 0))
+            r.tokens_per_second = float(s.get("tokens_per_second", 0.0))
+            r.tokens_generated = int(s.get("completion_tokens", 0))
+            r.prompt_tokens_processed = int(s.get("prompt_tokens", 0))
+            r.prompt_json_for_slot = json.dumps({"ttft_s": s.get("ttft_s", 0.0)})
+        return r
+
+    # ------------------------------------------------------------------ vector store (local-store backend)
+    def _store(self):
+        if self.store is None:
+            from ..engine.stores import VectorStore
+            self.store = VectorStore(self.device)
+        return self.store
+
+    async def StoresSet(self, request, context=None):
+        try:
+            self._store().set([list(k.Floats) for k in request.Keys], [v.Bytes for v in request.Values])
+            return pb.Result(success=True)
+        except Exception as e:
+            return pb.Result(success=False, message=str(e))
+
+    async def StoresDelete(self, request, context=None):
+        try:
+            self._store().delete([list(k.Floats) for k in request.Keys])
+            return pb.Result(success=True)
+        except Exception as e:
+            return pb.Result(success=False, message=str(e))
+
+    async def StoresGet(self, request, context=None):
+        keys, vals = self._store().get([list(k.Floats) for k in request.Keys])
+        r = pb.StoresGetResult()
+        for k, v in zip(keys, vals):
+            r.Keys.add(Floats=k)
+            r.Values.add(Bytes=v)
+        return r
+
+    async def StoresFind(self, request, context=None):
+        keys, vals, sims = self._store().find(list(request.Key.Floats), request.TopK)
+        r = pb.StoresFindResult(Similarities=sims)
+        for k, v in zip(keys, vals):
+            r.Keys.add(Floats=k)
+            r.Values.add(Bytes=v)
+        return r
+
+    async def Rerank(self, request, context=None):
+        """Cross-scoring with the loaded LM: relevance = mean log-likelihood proxy via embeddings
+        cosine (no dedicated reranker model family yet)."""
+        eng = self._require_engine()
+        loop = asyncio.get_running_loop()
+        docs = list(request.documents)
+        vecs = await loop.run_in_executor(None, lambda: eng.embed([request.query] + docs))
+        import math
+        q = vecs[0]
+        qn = math.sqrt(sum(x * x for x in q)) or 1.0
+        scored = []
+        for i, v in enumerate(vecs[1:]):
+            vn = math.sqrt(sum(x * x for x in v)) or 1.0
+            scored.append((sum(a * b for a, b in zip(q, v)) / (qn * vn), i))
+        scored.sort(reverse=True)
+        top = request.top_n if request.top_n > 0 else len(scored)
+        res = pb.RerankResult()
+        ntok = sum(len(d.split()) for d in docs) + len(request.query.split())
+        res.usage.total_tokens = ntok
+        res.usage.prompt_tokens = ntok
+        for s, i in scored[:top]:
+            res.results.add(index=i, text=docs[i], relevance_score=float(s))
+        return res
+
+    async def GenerateImage(self, request, context=None):
+        raise Unimplemented("GenerateImage")
+
+    async def TTS(self, request, context=None):
+        raise Unimplemented("TTS")
+
+    async def SoundGeneration(self, request, context=None):
+        raise Unimplemented("SoundGeneration")
+
+    async def AudioTranscription(self, request, context=None):
+        raise Unimplemented("AudioTranscription")
+
+    def shutdown(self):
+        if self.engine is not None:
+            self.engine.shutdown()
+            self.engine = None
+
+
+def _status(name):
+    import grpc
+    return getattr(grpc.StatusCode, name)

@@ -1,0 +1,131 @@
+"""Model/file downloader (`pkg/downloader/uri.go`, `pkg/utils/path.go`).
+
+URI schemes: http(s)://, file://, huggingface://owner/repo/file[@branch], github:org/repo/path[@br],
+github://org/repo/path[@br].  Downloads stream to `<dst>.partial`, are SHA-256 checked when a hash
+is given, then renamed atomically.  (OCI/ollama pulls are not supported: no registry client.)
+"""
+from __future__ import annotations
+
+import hashlib
+import os
+import shutil
+import urllib.parse
+import urllib.request
+from typing import Callable, Optional
+
+HF_PREFIX = "huggingface://"
+HF_PREFIX2 = "hf://"
+GITHUB = "github:"
+GITHUB2 = "github://"
+LOCAL = "file://"
+OCI = "oci://"
+OLLAMA = "ollama://"
+
+
+def looks_like_url(s: str) -> bool:
+    return s.startswith(("http://", "https://", HF_PREFIX, HF_PREFIX2, GITHUB, OCI, OLLAMA))
+
+
+def resolve_url(s: str) -> str:
+    def gh(rest: str) -> str:
+        repo, _, branch = rest.partition("@")
+        parts = repo.split("/")
+        return "https://raw.githubusercontent.com/%s/%s/%s/%s" % (parts[0], parts[1], branch or "main",
+                                                                  "/".join(parts[2:]))
+    if s.startswith(GITHUB2):
+        return gh(s[len(GITHUB2):])
+    if s.startswith(GITHUB):
+        return gh(s[len(GITHUB):])
+    for p in (HF_PREFIX, HF_PREFIX2):
+        if s.startswith(p):
+            rest = s[len(p):]
+            parts = rest.split("/")
+            owner, repo = parts[0], parts[1]
+            path = "/".join(parts[2:])
+            branch = "main"
+            if "@" in path:
+                path, branch = path.split("@", 1)
+            return f"https://huggingface.co/{owner}/{repo}/resolve/{branch}/{path}"
+    return s
+
+
+def filename_from_url(url: str) -> str:
+    name = os.path.basename(urllib.parse.urlparse(resolve_url(url)).path)
+    if not name:
+        raise ValueError(f"cannot derive a file name from {url!r}")
+    return name
+
+
+def verify_path(path: str, base: str):
+    """VerifyPath: `base/path` must stay inside base."""
+    base_c = os.path.normpath(os.path.abspath(base))
+    full = os.path.normpath(os.path.join(base_c, path))
+    if full != base_c and not full.startswith(base_c + os.sep):
+        raise ValueError("path is outside of trusted root")
+    if full == base_c:
+        raise ValueError("path is outside of trusted root")
+
+
+def sanitize_file_name(name: str) -> str:
+    return os.path.basename(os.path.normpath(name)).replace("..", "")
+
+
+def sha256_file(path: str) -> str:
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for chunk in iter(lambda: f.read(1 << 22), b""):
+            h.update(chunk)
+    return h.hexdigest()
+
+
+def read_uri(uri: str, base_path: str = "") -> bytes:
+    """DownloadWithCallback: fetch a (small) resource, file:// restricted to base_path."""
+    if uri.startswith(LOCAL):
+        p = uri[len(LOCAL):]
+        if base_path:
+            verify_path(os.path.relpath(os.path.abspath(p), base_path) if os.path.isabs(p) else p, base_path)
+            if not os.path.isabs(p):
+                p = os.path.join(base_path, p)
+        with open(p, "rb") as f:
+            return f.read()
+    with urllib.request.urlopen(resolve_url(uri), timeout=60) as r:  # noqa: S310
+        return r.read()
+
+
+def download_file(uri: str, dst: str, sha: str = "",
+                  progress: Optional[Callable[[str, int, int], None]] = None, auth: str = ""):
+    """DownloadFile: skip if present with matching hash; stream to .partial; verify; rename."""
+    if uri.startswith((OCI, OLLAMA)):
+        raise NotImplementedError("OCI/ollama registries are not supported in this build")
+    if os.path.exists(dst):
+        if not sha or sha256_file(dst).lower() == sha.lower():
+            return dst
+        os.remove(dst)
+    os.makedirs(os.path.dirname(os.path.abspath(dst)) or ".", exist_ok=True)
+    tmp = dst + ".partial"
+    if uri.startswith(LOCAL):
+        shutil.copyfile(uri[len(LOCAL):], tmp)
+    else:
+        req = urllib.request.Request(resolve_url(uri))
+        if auth:
+            req.add_header("Authorization", auth)
+        elif os.environ.get("HUGGINGFACE_HUB_TOKEN") and "huggingface.co" in req.full_url:
+            req.add_header("Authorization", "Bearer " + os.environ["HUGGINGFACE_HUB_TOKEN"])
+        with urllib.request.urlopen(req, timeout=60) as r, open(tmp, "wb") as f:  # noqa: S310
+            total = int(r.headers.get("Content-Length") or 0)
+            done = 0
+            while True:
+                b = r.read(1 << 22)
+                if not b:
+                    break
+                f.write(b)
+                done += len(b)
+                if progress:
+                    progress(os.path.basename(dst), done, total)
+    if sha:
+        got = sha256_file(tmp)
+        if got.lower() != sha.lower():
+            os.remove(tmp)
+            raise ValueError(f"SHA mismatch for file {dst!r} ( calculated: {got} != metadata: {sha} )")
+    os.replace(tmp, dst)
+    return dst
