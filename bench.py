@@ -10,8 +10,9 @@ warm-up waves, then exactly K timed waves bracketed by barrier + synchronize.
 Multi-GPU (torchrun, one process per GPU): data-parallel engine replicas (weak scaling:
 fixed per-GPU load), aggregate tokens/s = sum over ranks / max wall time over ranks.
 
---mode http   : requests go through the real gateway (FastAPI app served by uvicorn on
-                127.0.0.1, aiohttp SSE client) -> gateway -> engine (default)
+--mode http   : requests go through the real gateway (FastAPI app on the native C++ HTTP
+                server, or uvicorn with --server uvicorn) from out-of-process aiohttp SSE
+                clients (localai_amd/utils/loadgen.py) -> gateway -> engine (default)
 --mode engine : requests are fed to the engine directly (no HTTP), for kernel work
 """
 import argparse
@@ -39,6 +40,9 @@ def parse():
     ap.add_argument("--mode", default=os.environ.get("BENCH_MODE", "http"), choices=["http", "engine"])
     ap.add_argument("--context", type=int, default=2048)
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--server", default=os.environ.get("BENCH_SERVER", "native"), choices=["native", "uvicorn"])
+    ap.add_argument("--clients", type=int, default=int(os.environ.get("BENCH_CLIENTS", 4)),
+                    help="load-generator processes (separate from the server process)")
     ap.add_argument("--cache-dir", default=os.environ.get("LOCALAI_AMD_CACHE", "/tmp/localai_amd_cache"))
     return ap.parse_args()
 
@@ -69,6 +73,12 @@ def percentile(xs, p):
 
 def main():
     args = parse()
+    loadgen = None
+    if args.mode == "http":
+        # client processes are started before this process touches the GPU (no fork/exec
+        # from a GPU-initialised process)
+        from localai_amd.utils.loadgen import LoadGen
+        loadgen = LoadGen(args.clients)
     import torch
     import torch.distributed as dist
 
@@ -111,7 +121,7 @@ def main():
 
     msgs = user_messages(eng.tokenizer, args.concurrency, args.prompt_len, seed=rank)
     if args.mode == "http":
-        runner = HttpRunner(eng, args)
+        runner = HttpRunner(eng, args, loadgen)
     else:
         runner = EngineRunner(eng, args)
 
@@ -217,10 +227,10 @@ class EngineRunner:
 
 
 class HttpRunner:
-    """Real gateway over HTTP: uvicorn serving the FastAPI app, aiohttp SSE clients."""
+    """Real gateway over HTTP: the FastAPI app on the native server (or uvicorn), driven by
+    out-of-process aiohttp SSE clients."""
 
-    def __init__(self, eng, args):
-        import asyncio
+    def __init__(self, eng, args, loadgen):
         import socket
         from localai_amd.gateway.app import create_app_for_engine
         self.args = args
@@ -231,57 +241,34 @@ class HttpRunner:
         self.eng = eng
         eng.start()  # engine loop thread: the servicer only enqueues requests
         self.app, self.model_name = create_app_for_engine(eng, name="llama3-8b-instruct")
-        import uvicorn
-        cfg = uvicorn.Config(self.app, host="127.0.0.1", port=self.port, log_level="warning", loop="asyncio",
-                             http="h11", access_log=False)
-        self.server = uvicorn.Server(cfg)
+        if args.server == "native":
+            from localai_amd.gateway.native_server import NativeHTTPServer
+            self.server = NativeHTTPServer(self.app, "127.0.0.1", 0)
+            self.port = self.server.port
+        else:
+            import uvicorn
+            cfg = uvicorn.Config(self.app, host="127.0.0.1", port=self.port, log_level="warning", loop="asyncio",
+                                 http="h11", access_log=False)
+            self.server = uvicorn.Server(cfg)
         self.th = threading.Thread(target=self.server.run, daemon=True)
         self.th.start()
         for _ in range(600):
             if self.server.started:
                 break
             time.sleep(0.05)
-        self.loop = asyncio.new_event_loop()
+        self.lg = loadgen
+        self.url = f"http://127.0.0.1:{self.port}/v1/chat/completions"
 
     def wave(self, contents):
-        return self.loop.run_until_complete(self._wave(contents))
-
-    async def _wave(self, contents):
-        import asyncio
-        import aiohttp
-        url = f"http://127.0.0.1:{self.port}/v1/chat/completions"
-        conn = aiohttp.TCPConnector(limit=0)
-        timeout = aiohttp.ClientTimeout(total=3600)
-        async with aiohttp.ClientSession(connector=conn, timeout=timeout) as sess:
-            async def one(c):
-                body = {"model": self.model_name, "stream": True, "max_tokens": self.args.max_tokens,
-                        "temperature": 0, "ignore_eos": True, "mirostat": 0,
-                        "messages": [{"role": "user", "content": c}]}
-                t0 = time.perf_counter()
-                ttft = None
-                ntok = 0
-                async with sess.post(url, json=body) as resp:
-                    resp.raise_for_status()
-                    async for raw in resp.content:
-                        line = raw.strip()
-                        if not line.startswith(b"data:"):
-                            continue
-                        data = line[5:].strip()
-                        if data == b"[DONE]":
-                            break
-                        ev = json.loads(data)
-                        ch = ev.get("choices") or [{}]
-                        delta = ch[0].get("delta") or {}
-                        if ttft is None and delta.get("content"):
-                            ttft = time.perf_counter() - t0
-                        if ev.get("usage"):
-                            ntok = ev["usage"].get("completion_tokens", ntok)
-                return (ttft if ttft is not None else time.perf_counter() - t0), ntok
-            res = await asyncio.gather(*[one(c) for c in contents])
-        return [r[0] for r in res], sum(r[1] for r in res)
+        return self.lg.wave(self.url, self.model_name, contents, self.args.max_tokens,
+                            extra={"temperature": 0, "ignore_eos": True, "mirostat": 0})
 
     def close(self):
-        self.server.should_exit = True
+        self.lg.close()
+        if hasattr(self.server, "shutdown"):
+            self.server.shutdown()
+        else:
+            self.server.should_exit = True
         self.th.join(timeout=10)
         self.eng.shutdown()
 

@@ -79,6 +79,7 @@ class Request:
     n_gen: int = 0
     mu: float = 0.0
     cancelled: bool = False
+    sink: object = None
 
 
 class LLMEngine:
@@ -161,7 +162,11 @@ class LLMEngine:
         return self.tokenizer.encode(text, add_bos=add_bos)
 
     def add_request(self, prompt, params: SamplingParams, callback: Callable[[Event], None],
-                    req_id: Optional[int] = None) -> int:
+                    req_id: Optional[int] = None, sink=None) -> int:
+        """Queue a generation.  `callback(Event)` gets every text delta and the final event;
+        with a native `sink` (native/_la_http SseSink) text deltas go straight to
+        `sink.push(text, n_generated)` (no Python Event per token) and only the final event
+        reaches `callback`."""
         toks = self.tokenize(prompt) if isinstance(prompt, str) else list(prompt)
         if not toks:
             toks = [self.tokenizer.bos_id if self.tokenizer.bos_id >= 0 else 0]
@@ -171,6 +176,9 @@ class LLMEngine:
         stops = list(params.stop)
         r = Request(rid, toks, params, callback, n_prompt=len(toks), mu=2.0 * params.mirostat_tau)
         r.stream = core.TextStream(self.vocab, stops)
+        r.sink = sink
+        if sink is not None:
+            sink.set_prompt_tokens(r.n_prompt)
         self._inbox.put(r)
         self._wake.set()
         return rid
@@ -496,20 +504,28 @@ class LLMEngine:
         text, stopped = r.stream.push(tok)
         if stopped:
             if text:
-                r.callback(Event(text=text, token=tok))
+                self._emit(r, text, tok)
             self._finish(r, "stop", flush=False)
             return
         if p.max_tokens > 0 and r.n_gen >= p.max_tokens:
             if text:
-                r.callback(Event(text=text, token=tok))
+                self._emit(r, text, tok)
             self._finish(r, "length")
             return
         if self.sched.n_tokens(r.id) >= self.ctx:
             if text:
-                r.callback(Event(text=text, token=tok))
+                self._emit(r, text, tok)
             self._finish(r, "length")
             return
+        if not self._emit(r, text, tok):
+            self._finish(r, "abort")  # the client went away
+
+    def _emit(self, r: Request, text: bytes, tok: int) -> bool:
+        sink = r.sink
+        if sink is not None:
+            return sink.push(text, r.n_gen) if text else True
         r.callback(Event(text=text, token=tok))
+        return True
 
     def _finish(self, r: Request, reason: str, flush: bool = True, error: str = ""):
         if r.done:

@@ -377,6 +377,8 @@ def parse_json(s: str) -> List[dict]:
             obj, end = dec.raw_decode(s, off)
             if isinstance(obj, dict):
                 objs.append(obj)
+            elif isinstance(obj, list):  # parallel calls: [ {...}, {...} ]
+                objs.extend(o for o in obj if isinstance(o, dict))
             off = max(end, off + 1)
         except json.JSONDecodeError as e:
             off = max(e.pos, off + 1)

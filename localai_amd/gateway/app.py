@@ -16,7 +16,6 @@ from typing import Optional, Tuple
 
 from fastapi import FastAPI, Request
 from fastapi.responses import JSONResponse, Response
-from starlette.middleware.base import BaseHTTPMiddleware
 
 from ..config.app_config import ApplicationConfig
 from ..config.backend_config import BackendConfig
@@ -35,16 +34,19 @@ def _extract_key(request: Request) -> str:
     return request.headers.get("x-api-key", "") or request.headers.get("xi-api-key", "")
 
 
-class AuthMiddleware(BaseHTTPMiddleware):
+class AuthMiddleware:
+    """API-key check as a plain ASGI middleware (no per-chunk body re-streaming)."""
+
     def __init__(self, app, state: AppState):
-        super().__init__(app)
+        self.app = app
         self.state = state
         self.exempt = [re.compile(p) for p in state.cfg.http_get_exempted_endpoints]
 
     def _keys(self):
         keys = list(self.state.cfg.api_keys)
-        dyn = os.path.join(self.state.cfg.dynamic_config_dir or "", "api_keys.json")
-        if self.state.cfg.dynamic_config_dir and os.path.isfile(dyn):
+        d = self.state.cfg.dynamic_config_dir
+        dyn = os.path.join(d or "", "api_keys.json")
+        if d and os.path.isfile(dyn):
             try:
                 with open(dyn) as f:
                     keys += [k for k in json.load(f) if isinstance(k, str)]
@@ -52,10 +54,13 @@ class AuthMiddleware(BaseHTTPMiddleware):
                 pass
         return keys
 
-    async def dispatch(self, request: Request, call_next):
+    async def __call__(self, scope, receive, send):
+        if scope["type"] != "http":
+            return await self.app(scope, receive, send)
         keys = self._keys()
         if keys:
             cfg = self.state.cfg
+            request = Request(scope)
             skip = cfg.disable_api_key_requirement_for_http_get and request.method == "GET" and \
                 any(rx.search(request.url.path) for rx in self.exempt)
             if not skip:
@@ -65,23 +70,32 @@ class AuthMiddleware(BaseHTTPMiddleware):
                 else:
                     good = k in keys
                 if not good:
-                    if cfg.opaque_errors:
-                        return Response(status_code=403)
-                    return Response("missing or malformed API Key", status_code=403)
-        return await call_next(request)
+                    resp = Response(status_code=403) if cfg.opaque_errors else \
+                        Response("missing or malformed API Key", status_code=403)
+                    return await resp(scope, receive, send)
+        return await self.app(scope, receive, send)
 
 
-class MetricsMiddleware(BaseHTTPMiddleware):
+class MetricsMiddleware:
+    """api_call{method,path} histogram (time to response start, like fiber's middleware)."""
+
     def __init__(self, app, state: AppState):
-        super().__init__(app)
+        self.app = app
         self.state = state
 
-    async def dispatch(self, request: Request, call_next):
+    async def __call__(self, scope, receive, send):
+        if scope["type"] != "http" or scope.get("path") == "/metrics":
+            return await self.app(scope, receive, send)
         t0 = time.perf_counter()
-        resp = await call_next(request)
-        if request.url.path != "/metrics":
-            self.state.metrics.api_call.labels(request.method, request.url.path).observe(time.perf_counter() - t0)
-        return resp
+        done = False
+
+        async def send_wrap(msg):
+            nonlocal done
+            if not done and msg["type"] == "http.response.start":
+                done = True
+                self.state.metrics.api_call.labels(scope["method"], scope["path"]).observe(time.perf_counter() - t0)
+            await send(msg)
+        return await self.app(scope, receive, send_wrap)
 
 
 def create_app(state: AppState) -> FastAPI:

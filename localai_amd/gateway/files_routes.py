@@ -16,6 +16,7 @@ from fastapi import APIRouter, Request
 from fastapi.responses import JSONResponse, PlainTextResponse, Response
 
 from ..utils.downloader import sanitize_file_name
+from ..utils.multipart import read_form
 
 FILES_JSON = "uploadedFiles.json"
 ASSISTANTS_JSON = "assistants.json"
@@ -70,7 +71,7 @@ def build_router(state) -> APIRouter:
 
     # ------------------------------------------------------------------ files
     async def upload(request: Request):
-        form = await request.form()
+        form = await read_form(request)
         up = form.get("file")
         if up is None:
             return _err(400, "file is required")

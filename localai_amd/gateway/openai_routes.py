@@ -6,6 +6,7 @@ framing `data: {json}\\n\\n` ... `data: [DONE]` as in chat.go:463-508; token-gra
 """
 from __future__ import annotations
 
+import asyncio
 import json
 import logging
 import time
@@ -201,6 +202,11 @@ def build_router(state) -> APIRouter:
         model_out = req.get("model", model)
         headers = {"X-Correlation-ID": req["_correlation_id"]}
 
+        if req.get("stream") and not should_use_fn:
+            h = await _native_stream(request, state, cfg, req, pred_input, cid, created, model_out, "chat")
+            if h is not None:
+                return h
+
         if req.get("stream"):
             async def gen_plain():
                 first = {"id": cid, "created": created, "model": model_out, "object": "chat.completion.chunk",
@@ -333,6 +339,9 @@ def build_router(state) -> APIRouter:
             if len(cfg.prompt_strings) > 1:
                 raise APIError("cannot handle more than 1 `PromptStrings` when Streaming", 400)
             pred_input = apply_tpl(cfg.prompt_strings[0] if cfg.prompt_strings else "")
+            h = await _native_stream(request, state, cfg, req, pred_input, cid, created, model_out, "completion")
+            if h is not None:
+                return h
 
             async def gen():
                 usage = TokenUsage()
@@ -450,7 +459,8 @@ def build_router(state) -> APIRouter:
         from ..grpc import backend_pb as pb
         import os
         import tempfile
-        form = await request.form()
+        from ..utils.multipart import read_form
+        form = await read_form(request)
         model = model_from_context(request, state, form.get("model", ""), True)
         cfg = merge_request_with_config(state, model, {})
         up = form.get("file")
@@ -501,6 +511,73 @@ def build_router(state) -> APIRouter:
 
     r.add_api_route("/v1/images/generations", images, methods=["POST"])
     return r
+
+
+async def _native_stream(request, state, cfg, req, pred_input: str, cid: str, created: int, model_out: str,
+                         kind: str):
+    """Token streaming without the event loop: bind a native SseSink (native/http_server.cpp) to
+    the connection and hand it to the in-process engine.  Only the final event comes back to
+    Python (once per request).  Returns None when not applicable (uvicorn, out-of-process or
+    external backend), so the generic async-generator path is used instead."""
+    nc = request.scope.get("localai.native")
+    if nc is None:
+        return None
+    lm = await state.manager.load(cfg)
+    sv = lm.servicer
+    eng = getattr(sv, "engine", None) if sv is not None else None
+    if eng is None:
+        return None
+    from ..native import http
+    from .inference import predict_options
+    from .native_server import NativeHandledResponse
+    po = predict_options(cfg, pred_input, req.get("messages"))
+    prompt = sv._prompt(po)
+    params = sv._params(po)
+    obj = "chat.completion.chunk" if kind == "chat" else "text_completion"
+    base = 'data: {"id":%s,"created":%d,"model":%s,"object":"%s","choices":[{"index":0,"finish_reason":' % (
+        json.dumps(cid), created, json.dumps(model_out, ensure_ascii=False), obj)
+    if kind == "chat":
+        head, mid = base + 'null,"delta":{"content":"', '"}}],"usage":'
+        fin_body = ',"delta":{"content":""}}],"usage":'
+    else:
+        head, mid = base + 'null,"text":"', '"}],"usage":'
+        fin_body = ',"text":""}],"usage":'
+    srv, conn = nc.srv, nc.conn
+    srv.stream_start(conn, 200, [("content-type", "text/event-stream"), ("cache-control", "no-cache"),
+                                 ("connection", "keep-alive"), ("x-correlation-id", req["_correlation_id"])])
+    if kind == "chat":
+        srv.stream_write(conn, (base + 'null,"delta":{"role":"assistant","content":""}}]}\n\n').encode())
+    sink = http().SseSink(srv, conn, head.encode(), mid.encode(), b"}\n\n", 0)
+    nc.handled = True
+    loop = asyncio.get_running_loop()
+    mid_ = lm.id
+    metrics = state.metrics
+    state.manager.mark_busy(mid_, True)
+    t0 = time.perf_counter()
+
+    def on_final(ev):  # engine thread, once per request
+        if ev.text:
+            sink.push(ev.text, ev.completion_tokens)
+        if ev.error:
+            err = json.dumps({"error": {"message": ev.error, "type": "server_error", "code": 500}})
+            sink.finish(f"data: {err}\n\ndata: [DONE]\n\n".encode())
+        else:
+            usage = json.dumps({"prompt_tokens": ev.prompt_tokens, "completion_tokens": ev.completion_tokens,
+                                "total_tokens": ev.prompt_tokens + ev.completion_tokens}, separators=(",", ":"))
+            reason = "length" if ev.finish_reason == "length" else "stop"
+            sink.finish(f'{base}"{reason}"{fin_body}{usage}}}\n\ndata: [DONE]\n\n'.encode())
+        metrics.requests.labels(mid_, kind).inc()
+        metrics.out_tokens.labels(mid_).inc(ev.completion_tokens)
+        metrics.prompt_tokens.labels(mid_).inc(ev.prompt_tokens)
+        tt = sink.ttft
+        if tt >= 0:
+            metrics.ttft.labels(mid_).observe(tt)
+            if ev.completion_tokens > 1:
+                metrics.itl.labels(mid_).observe((time.perf_counter() - t0 - tt) / (ev.completion_tokens - 1))
+        loop.call_soon_threadsafe(state.manager.mark_busy, mid_, False)
+
+    eng.add_request(prompt, params, on_final, sink=sink)
+    return NativeHandledResponse()
 
 
 async def handle_question(state, cfg, req, calls, result: str, prompt: str) -> str:

@@ -29,6 +29,67 @@ class Unimplemented(Exception):
     pass
 
 
+class _Pump:
+    """Moves engine-thread events onto the event loop with ONE loop wake-up per burst (the
+    engine emits a whole decode step of events at once) instead of one per token."""
+
+    def __init__(self, loop):
+        import collections
+        self.loop = loop
+        self.dq = collections.deque()
+        self.pending = False
+
+    def push(self, ch, ev):
+        self.dq.append((ch, ev))
+        if not self.pending:
+            self.pending = True
+            self.loop.call_soon_threadsafe(self._drain)
+
+    def _drain(self):
+        self.pending = False
+        dq = self.dq
+        while dq:
+            ch, ev = dq.popleft()
+            ch._deliver(ev)
+
+
+_PUMPS = {}
+
+
+def _pump_for(loop) -> _Pump:
+    p = _PUMPS.get(id(loop))
+    if p is None or p.loop is not loop:
+        p = _PUMPS[id(loop)] = _Pump(loop)
+    return p
+
+
+class _Channel:
+    """Single-consumer event channel fed by a _Pump."""
+    __slots__ = ("pump", "items", "waiter")
+
+    def __init__(self, pump: _Pump):
+        self.pump = pump
+        self.items = []
+        self.waiter = None
+
+    def put(self, ev):  # engine thread
+        self.pump.push(self, ev)
+
+    def _deliver(self, ev):  # loop thread
+        self.items.append(ev)
+        w = self.waiter
+        if w is not None and not w.done():
+            w.set_result(None)
+
+    async def get_all(self):
+        while not self.items:
+            self.waiter = self.pump.loop.create_future()
+            await self.waiter
+            self.waiter = None
+        out, self.items = self.items, []
+        return out
+
+
 class EngineServicer:
     def __init__(self, device: Optional[str] = None, tp=None):
         self.engine = None
@@ -125,45 +186,29 @@ class EngineServicer:
 
     async def PredictStream(self, request, context=None):
         eng = self._require_engine()
-        loop = asyncio.get_running_loop()
-        q: asyncio.Queue = asyncio.Queue()
-
-        def cb(ev):
-            loop.call_soon_threadsafe(q.put_nowait, ev)
-
-        prompt = self._prompt(request)
-        rid = eng.add_request(prompt, self._params(request), cb)
+        ch = _Channel(_pump_for(asyncio.get_running_loop()))
+        rid = eng.add_request(self._prompt(request), self._params(request), ch.put)
         finished = False
         try:
             while True:
-                ev = await q.get()
-                if ev.error and ev.finished:
-                    raise RuntimeError(ev.error)
-                if ev.finished:
+                evs = await ch.get_all()
+                buf = bytearray()
+                fin = None
+                for ev in evs:  # coalesce everything already produced into one message
+                    buf += ev.text
+                    if ev.finished:
+                        fin = ev
+                        break
+                if fin is not None:
                     finished = True
-                    if ev.text:
-                        yield pb.Reply(message=ev.text)
-                    yield pb.Reply(message=b"", tokens=ev.completion_tokens, prompt_tokens=ev.prompt_tokens)
+                    if fin.error:
+                        raise RuntimeError(fin.error)
+                    if buf:
+                        yield pb.Reply(message=bytes(buf))
+                    yield pb.Reply(message=b"", tokens=fin.completion_tokens, prompt_tokens=fin.prompt_tokens)
                     return
-                if ev.text:
-                    # coalesce whatever is already queued into one message (allowed by the contract)
-                    buf = bytearray(ev.text)
-                    fin = None
-                    while not q.empty():
-                        nxt = q.get_nowait()
-                        if nxt.finished:
-                            fin = nxt
-                            break
-                        buf.extend(nxt.text)
+                if buf:
                     yield pb.Reply(message=bytes(buf))
-                    if fin is not None:
-                        finished = True
-                        if fin.error:
-                            raise RuntimeError(fin.error)
-                        if fin.text:
-                            yield pb.Reply(message=fin.text)
-                        yield pb.Reply(message=b"", tokens=fin.completion_tokens, prompt_tokens=fin.prompt_tokens)
-                        return
         finally:
             if not finished:
                 eng.abort(rid)  # client went away / generator closed: free the sequence (fixes Q4)

@@ -1,8 +1,18 @@
-"""Native (C++/pybind11) engine core.  Built in-tree on first import."""
+"""Native (C++/pybind11) runtime: engine core (scheduler, paged-KV manager, detokenizing
+stop matcher) and the HTTP/1.1 front end with SSE token sinks.  Built in-tree on first import."""
 from . import _build
 
 try:
     from . import _la_core as core  # noqa: F401
 except ImportError:
-    _build.build()
+    _build.build_module("_la_core")
     from . import _la_core as core  # noqa: F401
+
+
+def http():
+    try:
+        from . import _la_http
+    except ImportError:
+        _build.build_module("_la_http")
+        from . import _la_http
+    return _la_http

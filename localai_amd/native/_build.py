@@ -9,21 +9,30 @@ import sysconfig
 from pathlib import Path
 
 HERE = Path(__file__).resolve().parent
-SRCS = sorted(HERE.glob("*.cpp"))
 EXT = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+# module name -> sources
+MODULES = {"_la_core": ["engine_core.cpp"], "_la_http": ["http_server.cpp"]}
 LIB = HERE / f"_la_core{EXT}"
 
 
-def _digest() -> str:
+def _digest(srcs) -> str:
     h = hashlib.sha256()
-    for p in SRCS:
+    for p in srcs:
         h.update(p.read_bytes())
     return h.hexdigest()[:16]
 
 
 def build(force: bool = False, verbose: bool = False, sanitize: bool = False) -> Path:
-    stamp = HERE / "_la_core.stamp"
-    dig = _digest() + ("-asan" if sanitize else "")
+    for name in MODULES:
+        build_module(name, force, verbose, sanitize)
+    return LIB
+
+
+def build_module(name: str, force: bool = False, verbose: bool = False, sanitize: bool = False) -> Path:
+    SRCS = [HERE / s for s in MODULES[name]]
+    LIB = HERE / f"{name}{EXT}"
+    stamp = HERE / f"{name}.stamp"
+    dig = _digest(SRCS) + ("-asan" if sanitize else "")
     if not force and LIB.exists() and stamp.exists() and stamp.read_text().strip() == dig:
         return LIB
     import pybind11
@@ -33,7 +42,7 @@ def build(force: bool = False, verbose: bool = False, sanitize: bool = False) ->
     if sanitize:
         flags += ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-g"]
     tmp = str(LIB) + ".tmp"
-    cmd = [cxx, *flags, *map(str, SRCS), "-o", tmp]
+    cmd = [cxx, *flags, *map(str, SRCS), "-o", tmp, "-lpthread"]
     if verbose:
         print(" ".join(cmd), flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)

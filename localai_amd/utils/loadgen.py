@@ -1,0 +1,111 @@
+"""Streaming chat-completions load generator, run as separate client processes so the
+measuring client never shares a GIL with the server under test.
+
+    python -m localai_amd.utils.loadgen        (reads one JSON job per stdin line)
+
+job  = {"url", "model", "contents": [...], "max_tokens", "extra": {...}}
+reply= {"ttft": [s...], "tokens": n, "errors": k}   (one JSON line per job)
+"""
+from __future__ import annotations
+
+import asyncio
+import json
+import os
+import subprocess
+import sys
+import time
+from typing import List, Tuple
+
+
+async def _wave(job) -> dict:
+    import aiohttp
+    conn = aiohttp.TCPConnector(limit=0)
+    timeout = aiohttp.ClientTimeout(total=3600)
+    errors = 0
+    async with aiohttp.ClientSession(connector=conn, timeout=timeout) as sess:
+        async def one(c):
+            nonlocal errors
+            body = {"model": job["model"], "stream": True, "max_tokens": job["max_tokens"],
+                    "messages": [{"role": "user", "content": c}], **job.get("extra", {})}
+            t0 = time.perf_counter()
+            ttft = None
+            ntok = 0
+            try:
+                async with sess.post(job["url"], json=body) as resp:
+                    resp.raise_for_status()
+                    async for raw in resp.content:
+                        if not raw.startswith(b"data:"):
+                            continue
+                        data = raw[5:].strip()
+                        if data == b"[DONE]":
+                            break
+                        if ttft is None and b'"content":""' not in data and b'"content"' in data:
+                            ttft = time.perf_counter() - t0
+                        u = data.rfind(b'"completion_tokens":')
+                        if u >= 0:
+                            e = u + 20
+                            while data[e:e + 1].isdigit():
+                                e += 1
+                            ntok = int(data[u + 20:e])
+            except Exception:
+                errors += 1
+            return (ttft if ttft is not None else time.perf_counter() - t0), ntok
+        res = await asyncio.gather(*[one(c) for c in job["contents"]])
+    return {"ttft": [r[0] for r in res], "tokens": sum(r[1] for r in res), "errors": errors}
+
+
+def _main():
+    for line in sys.stdin:
+        line = line.strip()
+        if not line:
+            continue
+        job = json.loads(line)
+        if job.get("quit"):
+            break
+        out = asyncio.run(_wave(job))
+        sys.stdout.write(json.dumps(out) + "\n")
+        sys.stdout.flush()
+
+
+class LoadGen:
+    """Pool of client processes; a wave's requests are split round-robin across them."""
+
+    def __init__(self, n_procs: int = 2):
+        env = dict(os.environ)
+        root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        env["PYTHONPATH"] = root + os.pathsep + env.get("PYTHONPATH", "")
+        env["CUDA_VISIBLE_DEVICES"] = ""  # clients never touch the GPU
+        env["HIP_VISIBLE_DEVICES"] = ""
+        self.procs = [subprocess.Popen([sys.executable, "-m", "localai_amd.utils.loadgen"], stdin=subprocess.PIPE,
+                                       stdout=subprocess.PIPE, env=env, text=True, bufsize=1)
+                      for _ in range(max(1, n_procs))]
+
+    def wave(self, url: str, model: str, contents: List[str], max_tokens: int, extra=None) -> Tuple[list, int]:
+        n = len(self.procs)
+        parts = [contents[i::n] for i in range(n)]
+        for p, part in zip(self.procs, parts):
+            p.stdin.write(json.dumps({"url": url, "model": model, "contents": part, "max_tokens": max_tokens,
+                                      "extra": extra or {}}) + "\n")
+            p.stdin.flush()
+        ttft, tokens, errors = [], 0, 0
+        for p, part in zip(self.procs, parts):
+            r = json.loads(p.stdout.readline())
+            ttft += r["ttft"]
+            tokens += r["tokens"]
+            errors += r["errors"]
+        if errors:
+            raise RuntimeError(f"{errors} streaming requests failed")
+        return ttft, tokens
+
+    def close(self):
+        for p in self.procs:
+            try:
+                p.stdin.write(json.dumps({"quit": True}) + "\n")
+                p.stdin.flush()
+                p.wait(10)
+            except Exception:
+                p.kill()
+
+
+if __name__ == "__main__":
+    _main()

@@ -25,3 +25,12 @@ def pytest_collection_modifyitems(config, items):
     for it in items:
         if "gpu" in it.keywords:
             it.add_marker(skip)
+
+
+@pytest.fixture(scope="session")
+def tiny_model_path(tmp_path_factory):
+    """A tiny random-init Llama GGUF (exactly quantised) shared by the CPU engine tests."""
+    from localai_amd.models import synth
+    p = tmp_path_factory.mktemp("models") / "tiny-llama.gguf"
+    synth.write_model(str(p), "tiny-llama", exact=True)
+    return str(p)

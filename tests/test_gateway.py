@@ -1,0 +1,201 @@
+"""HTTP gateway end-to-end on CPU: tiny random Llama on the CPU engine, served through both the
+native C++ HTTP server (SSE sinks) and Starlette's TestClient.  Mirrors the reference's
+core/http/app_test.go coverage (models list, chat/completions/edits/embeddings, streaming,
+stores, tokenize, metrics, auth)."""
+import json
+import threading
+import time
+import urllib.request
+
+import pytest
+
+from localai_amd.config.app_config import ApplicationConfig
+
+
+@pytest.fixture(scope="module")
+def engine(tiny_model_path):
+    from localai_amd.engine.llm_engine import EngineConfig, LLMEngine
+    eng = LLMEngine(EngineConfig(model_path=tiny_model_path, device="cpu", context_size=512, max_num_seqs=8,
+                                 use_graphs=False))
+    eng.start()
+    yield eng
+    eng.shutdown()
+
+
+def _app_config(tmp_path_factory, **kw):
+    d = tmp_path_factory.mktemp("localai")
+    return ApplicationConfig(upload_dir=str(d / "upload"), config_dir=str(d / "config"),
+                             image_dir=str(d / "images"), audio_dir=str(d / "audio"), **kw)
+
+
+@pytest.fixture(scope="module")
+def client(engine, tmp_path_factory):
+    from fastapi.testclient import TestClient
+    from localai_amd.gateway.app import create_app_for_engine
+    app, name = create_app_for_engine(engine, name="tiny", app_config=_app_config(tmp_path_factory))
+    with TestClient(app) as c:
+        c.model_name = name
+        yield c
+
+
+@pytest.fixture(scope="module")
+def native(engine, tmp_path_factory):
+    from localai_amd.gateway.app import create_app_for_engine
+    from localai_amd.gateway.native_server import NativeHTTPServer
+    app, name = create_app_for_engine(engine, name="tiny", app_config=_app_config(tmp_path_factory))
+    srv = NativeHTTPServer(app, "127.0.0.1", 0)
+    th = threading.Thread(target=srv.run, daemon=True)
+    th.start()
+    t0 = time.time()
+    while not srv.started and time.time() - t0 < 30:
+        time.sleep(0.02)
+    yield f"http://127.0.0.1:{srv.port}", name
+    srv.shutdown()
+    th.join(10)
+
+
+def _post(url, body, headers=None):
+    req = urllib.request.Request(url, data=json.dumps(body).encode(),
+                                 headers={"content-type": "application/json", **(headers or {})})
+    with urllib.request.urlopen(req, timeout=60) as r:
+        return r.status, r.read()
+
+
+def _sse(raw: bytes):
+    evs = []
+    for line in raw.decode().split("\n"):
+        if line.startswith("data: "):
+            d = line[6:]
+            evs.append(d if d == "[DONE]" else json.loads(d))
+    return evs
+
+
+def test_models_and_health(client):
+    assert client.get("/healthz").status_code == 200
+    assert client.get("/readyz").status_code == 200
+    ids = [m["id"] for m in client.get("/v1/models").json()["data"]]
+    assert client.model_name in ids
+    assert client.get("/version").json()["version"]
+
+
+def test_chat_completion_greedy_is_deterministic(client):
+    body = {"model": client.model_name, "messages": [{"role": "user", "content": "hello"}], "max_tokens": 6,
+            "temperature": 0, "ignore_eos": True}
+    a = client.post("/v1/chat/completions", json=body).json()
+    b = client.post("/chat/completions", json=body).json()
+    assert a["object"] == "chat.completion"
+    assert a["choices"][0]["message"]["content"] == b["choices"][0]["message"]["content"]
+    assert a["usage"]["completion_tokens"] == 6
+    assert a["usage"]["prompt_tokens"] > 0
+
+
+def test_completion_and_edit(client):
+    r = client.post("/v1/completions", json={"model": client.model_name, "prompt": "abc", "max_tokens": 3,
+                                             "ignore_eos": True}).json()
+    assert r["object"] == "text_completion" and r["usage"]["completion_tokens"] == 3
+    r = client.post(f"/v1/engines/{client.model_name}/completions", json={"prompt": "x", "max_tokens": 2,
+                                                                          "ignore_eos": True})
+    assert r.status_code == 200
+    r = client.post("/v1/edits", json={"model": client.model_name, "input": "abc", "instruction": "fix",
+                                       "max_tokens": 2, "ignore_eos": True}).json()
+    assert r["object"] == "edit" and len(r["choices"]) == 1
+
+
+def test_streaming_uvicorn_path(client):
+    body = {"model": client.model_name, "messages": [{"role": "user", "content": "hi"}], "max_tokens": 5,
+            "stream": True, "ignore_eos": True, "temperature": 0}
+    with client.stream("POST", "/v1/chat/completions", json=body) as r:
+        raw = b"".join(r.iter_bytes())
+    evs = _sse(raw)
+    assert evs[-1] == "[DONE]"
+    assert evs[-2]["choices"][0]["finish_reason"] in ("stop", "length")
+    assert evs[-2]["usage"]["completion_tokens"] == 5
+
+
+def test_native_server_streaming_matches_nonstreaming(native):
+    base, name = native
+    msgs = [{"role": "user", "content": "stream me"}]
+    st, raw = _post(base + "/v1/chat/completions", {"model": name, "messages": msgs, "max_tokens": 7,
+                                                    "temperature": 0, "ignore_eos": True})
+    full = json.loads(raw)["choices"][0]["message"]["content"]
+    st, raw = _post(base + "/v1/chat/completions", {"model": name, "messages": msgs, "max_tokens": 7,
+                                                    "temperature": 0, "ignore_eos": True, "stream": True})
+    evs = _sse(raw)
+    assert evs[0]["choices"][0]["delta"]["role"] == "assistant"
+    text = "".join(e["choices"][0]["delta"].get("content", "") for e in evs[1:-1])
+    assert text == full
+    assert evs[-2]["choices"][0]["finish_reason"] == "length"
+    assert evs[-2]["usage"]["completion_tokens"] == 7
+    # completions endpoint streaming through the native sink
+    st, raw = _post(base + "/v1/completions", {"model": name, "prompt": "abc", "max_tokens": 4, "stream": True,
+                                               "ignore_eos": True})
+    evs = _sse(raw)
+    assert evs[-1] == "[DONE]" and evs[-2]["usage"]["completion_tokens"] == 4
+
+
+def test_native_server_keepalive_and_errors(native):
+    base, name = native
+    import http.client
+    host, port = base[len("http://"):].split(":")
+    c = http.client.HTTPConnection(host, int(port), timeout=30)
+    for _ in range(3):  # several requests on one keep-alive connection
+        c.request("GET", "/v1/models")
+        r = c.getresponse()
+        assert r.status == 200 and json.loads(r.read())["data"]
+    c.request("GET", "/does-not-exist")
+    r = c.getresponse()
+    r.read()
+    assert r.status == 404
+    c.close()
+
+
+def test_embeddings_tokenize_rerank(client):
+    r = client.post("/v1/embeddings", json={"model": client.model_name, "input": ["hello", "world"]}).json()
+    assert len(r["data"]) == 2 and len(r["data"][0]["embedding"]) > 0
+    t = client.post("/v1/tokenize", json={"model": client.model_name, "content": "hello world"}).json()
+    assert len(t["tokens"]) >= 2
+    rr = client.post("/v1/rerank", json={"model": client.model_name, "query": "q", "documents": ["a", "b", "c"],
+                                         "top_n": 2}).json()
+    assert len(rr["results"]) == 2
+
+
+def test_stores_roundtrip(client):
+    assert client.post("/stores/set", json={"keys": [[1, 0, 0], [0, 1, 0], [0, 0, 1]],
+                                            "values": ["x", "y", "z"]}).status_code == 200
+    f = client.post("/stores/find", json={"key": [0.9, 0.1, 0], "topk": 2}).json()
+    assert f["values"] == ["x", "y"] and f["similarities"][0] > f["similarities"][1]
+    assert client.post("/stores/delete", json={"keys": [[1, 0, 0]]}).status_code == 200
+    g = client.post("/stores/get", json={"keys": [[1, 0, 0], [0, 0, 1]]}).json()
+    assert g["values"] == ["z"]
+
+
+def test_metrics_endpoint(client):
+    txt = client.get("/metrics").text
+    assert "api_call" in txt and "localai_output_tokens_total" in txt
+
+
+def test_api_key_auth(engine, tmp_path_factory):
+    from fastapi.testclient import TestClient
+    from localai_amd.gateway.app import create_app_for_engine
+    ac = _app_config(tmp_path_factory, api_keys=["sekrit"])
+    app, name = create_app_for_engine(engine, name="tiny", app_config=ac)
+    with TestClient(app) as c:
+        assert c.get("/v1/models").status_code == 403
+        assert c.get("/v1/models", headers={"Authorization": "Bearer sekrit"}).status_code == 200
+        assert c.get("/v1/models", headers={"x-api-key": "sekrit"}).status_code == 200
+        assert c.get("/v1/models", headers={"Authorization": "Bearer nope"}).status_code == 403
+
+
+def test_files_and_assistants(client, tmp_path):
+    r = client.post("/v1/files", files={"file": ("a.txt", b"hello")}, data={"purpose": "fine-tune"})
+    assert r.status_code == 200, r.text
+    fid = r.json()["id"]
+    assert any(f["id"] == fid for f in client.get("/v1/files").json()["data"])
+    assert client.get(f"/v1/files/{fid}/content").content == b"hello"
+    a = client.post("/v1/assistants", json={"model": client.model_name, "name": "helper"}).json()
+    assert a["object"] == "assistant"
+    af = client.post(f"/v1/assistants/{a['id']}/files", json={"file_id": fid}).json()
+    assert af["assistant_id"] == a["id"]
+    assert client.delete(f"/v1/assistants/{a['id']}/files/{fid}").json()["deleted"]
+    assert client.delete(f"/v1/assistants/{a['id']}").json()["deleted"]
+    assert client.delete(f"/v1/files/{fid}").json()["deleted"]
