@@ -25,7 +25,7 @@ import numpy as np
 import torch
 
 from .. import ops
-from ..gguf import GGML_BLOCK, GGMLType, GGUFReader, dequantize
+from ..gguf import GGML_BLOCK, GGMLType, GGUFReader, dequantize, quantize
 from .hparams import HParams
 
 
@@ -102,9 +102,17 @@ class Layer:
 
 
 def _raw2d(t, rows: Optional[slice] = None, cols: Optional[slice] = None):
-    """Slice a GGUF tensor's raw bytes as a 2-D [N, K] matrix by rows and/or column blocks."""
+    """Slice a GGUF tensor's raw bytes as a 2-D [N, K] matrix by rows and/or column blocks.
+    A column shard that does not fall on quant-block boundaries (small models at high TP
+    degree) is dequantised and returned as BF16."""
     N, K = t.shape[-2], t.shape[-1]
     bs, bb = GGML_BLOCK[t.ggml_type]
+    if cols is not None and (cols.start % bs or cols.stop % bs):
+        w = dequantize(t.data, t.ggml_type, (N, K))
+        if rows is not None:
+            w = w[rows]
+        w = np.ascontiguousarray(w[:, cols])
+        return quantize(w, GGMLType.BF16), w.shape, GGMLType.BF16
     a = t.data.reshape(-1, K // bs, bb)
     if rows is not None:
         a = a[rows]
@@ -114,7 +122,7 @@ def _raw2d(t, rows: Optional[slice] = None, cols: Optional[slice] = None):
         b0, b1 = cols.start // bs, cols.stop // bs
         a = a[:, b0:b1]
         k = cols.stop - cols.start
-    return np.ascontiguousarray(a).reshape(-1), (n, k)
+    return np.ascontiguousarray(a).reshape(-1), (n, k), t.ggml_type
 
 
 class DecoderModel:
@@ -141,9 +149,8 @@ class DecoderModel:
             return torch.from_numpy(arr).to(dev)
 
         def qw(name, rows=None, cols=None):
-            t = T[name]
-            raw, shape = _raw2d(t, rows, cols)
-            return ops.QWeight.from_raw(raw, t.ggml_type, shape, dev)
+            raw, shape, gt = _raw2d(T[name], rows, cols)
+            return ops.QWeight.from_raw(raw, gt, shape, dev)
 
         def sl(n_total, part=None):
             n = n_total // W
@@ -238,8 +245,8 @@ class DecoderModel:
         sub = type("T", (), {})()
         sub.shape, sub.ggml_type = (N, K), t.ggml_type
         sub.data = t.data[e * per:(e + 1) * per]
-        raw, shape = _raw2d(sub, rows, cols)
-        return ops.QWeight.from_raw(raw, t.ggml_type, shape, self.device)
+        raw, shape, gt = _raw2d(sub, rows, cols)
+        return ops.QWeight.from_raw(raw, gt, shape, self.device)
 
     # --------------------------------------------------------------------------- forward
     def new_kv_cache(self, num_blocks: int, block_size: int) -> KVCache:
