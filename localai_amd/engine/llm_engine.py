@@ -52,6 +52,8 @@ class EngineConfig:
     rope_freq_base: float = 0.0
     rope_freq_scale: float = 0.0
     rope_scaling: str = ""
+    decode_steps: int = 8             # device-resident decode steps per host round trip (graphs only)
+    bias_capacity: int = 16           # logit-bias / EOS-ban entries per sequence inside the graph
 
 
 @dataclass
@@ -261,7 +263,8 @@ class LLMEngine:
         if not self.requests:
             return False
         self.busy = True
-        plan = self.sched.schedule()
+        K = self._lookahead()
+        plan = self.sched.schedule(K)
         did = False
         p_ids = plan["p_ids"]
         if len(p_ids):
@@ -272,7 +275,7 @@ class LLMEngine:
         d_ids = plan["d_ids"]
         if len(d_ids):
             t0 = time.perf_counter()
-            self._run_decode(plan)
+            self._run_decode(plan, K)
             self.metrics["decode_s"] += time.perf_counter() - t0
             did = True
         self.metrics["steps"] += 1
@@ -328,61 +331,175 @@ class LLMEngine:
         seqs = [int(ids[i]) for i in range(len(ids)) if last[i]]
         self._sample_and_emit(seqs, logits)
 
-    def _run_decode(self, plan):
+    # ------------------------------------------------------------------ decode
+    def _needs_host_sampling(self, r: Request) -> bool:
+        p = r.params
+        return (p.repeat_penalty != 1.0 or p.frequency_penalty != 0.0 or p.presence_penalty != 0.0
+                or p.mirostat == 1 or bool(p.grammar) or len(p.logit_bias) + len(self.tokenizer.eog) >
+                self.cfg.bias_capacity)
+
+    def _lookahead(self) -> int:
+        """Decode steps to run on the device before coming back to the host."""
+        K = self.cfg.decode_steps
+        if K <= 1 or not (self.cfg.use_graphs and self.device.type == "cuda"):
+            return 1
+        s = self.sched
+        if s.num_waiting > 0 and s.num_running < self.cfg.max_num_seqs:
+            return 1  # admit new prompts promptly
+        rem_tok, rem_ctx = 1, K
+        for r in self.requests.values():
+            if r.n_gen == 0 or self._needs_host_sampling(r):
+                return 1  # prefill in flight, or a host-side sampler feature
+            n = r.n_prompt + r.n_gen
+            rem_ctx = min(rem_ctx, self.ctx - n)
+            mt = r.params.max_tokens
+            rem_tok = max(rem_tok, (mt - r.n_gen) if mt > 0 else K)
+        return max(1, min(K, rem_ctx, rem_tok))
+
+    def _run_decode(self, plan, K: int = 1):
         ids = [int(x) for x in plan["d_ids"]]
         B = len(ids)
         tok, pos, slots, lens, bt = plan["d_tokens"], plan["d_pos"], plan["d_slots"], plan["d_lens"], plan["d_bt"]
         Bp = len(tok)
-        if self.cfg.use_graphs and self.device.type == "cuda":
-            logits = self._decode_graph(Bp, tok, pos, slots, lens, bt)
-        else:
+        if not (self.cfg.use_graphs and self.device.type == "cuda"):
             fb = ForwardBatch(tokens=self._dev(tok), pos=self._dev(pos), slots=self._dev(slots), decode=True,
                               block_tables=self._dev(bt), seq_lens=self._dev(lens), max_len=int(plan["d_maxlen"]))
             logits = self.model.forward(fb, self.kv)
-        self._sample_and_emit(ids, logits[:B])
-
-    def _decode_graph(self, Bp, tok, pos, slots, lens, bt):
+            self._sample_and_emit(ids, logits[:B])
+            return
+        reqs = [self.requests[i] for i in ids]
         g = self._graphs.get(Bp)
         if g is None:
-            g = self._capture(Bp)
-            self._graphs[Bp] = g
+            g = self._graphs[Bp] = self._capture(Bp)
         graph, st, logits = g
-        st["tokens"].copy_(torch.from_numpy(tok), non_blocking=True)
-        st["pos"].copy_(torch.from_numpy(pos), non_blocking=True)
-        st["slots"].copy_(torch.from_numpy(slots), non_blocking=True)
-        st["lens"].copy_(torch.from_numpy(lens), non_blocking=True)
+        device_sampling = not any(self._needs_host_sampling(r) for r in reqs)
+        self._upload_step_inputs(st, reqs, Bp, tok, pos, slots, lens, bt, device_sampling)
+        if not device_sampling:  # penalties / mirostat v1 / grammar: one step, host-driven sampling
+            graph.replay()
+            self._sample_and_emit(ids, logits[:B])
+            return
+        for _ in range(K):
+            graph.replay()
+        hist = st["hist"][:K, :B].cpu().numpy()  # the only sync per K steps
+        if any(r.params.mirostat == 2 for r in reqs):
+            muh = st["mu"][:B].cpu().numpy()
+            for j, r in enumerate(reqs):
+                r.mu = float(muh[j])
+        now = time.perf_counter()
+        for j, r in enumerate(reqs):
+            if r.done:
+                continue
+            acc = []
+            for k in range(K):
+                t = int(hist[k, j])
+                acc.append(t)
+                self._on_token(r, t, now, append=False)
+                if r.done:
+                    break
+            if not r.done:
+                self.sched.append_run(r.id, acc)
+
+    def _upload_step_inputs(self, st, reqs, Bp, tok, pos, slots, lens, bt, device_sampling: bool):
+        B = len(reqs)
+        h = st["host"]  # one pinned staging block -> one H2D copy per run
+        h["tokens"][:] = torch.from_numpy(tok)
+        h["pos"][:] = torch.from_numpy(pos)
+        h["slots"][:] = torch.from_numpy(slots)
+        h["lens"][:] = torch.from_numpy(lens)
         nb = bt.shape[1]
-        st["bt_host"][:, :nb] = torch.from_numpy(bt)
-        st["bt"].copy_(st["bt_host"], non_blocking=True)
-        graph.replay()
-        return logits
+        h["bt"][:, :nb] = torch.from_numpy(bt)
+        h["step"][0] = 0
+        n_bias = 0
+        if device_sampling:
+            prm = st["prm_np"]
+            prm[:] = 0  # padding rows: greedy
+            for j, r in enumerate(reqs):
+                p = r.params
+                prm[j] = (p.temperature, p.top_p, p.min_p, p.typical_p, p.tfs_z, p.mirostat_tau, p.mirostat_eta,
+                          p.top_k, 2 if p.mirostat == 2 else 0, 0, p.seed & 0xFFFFFFFFFFFFFFFF, r.n_gen)
+            h["prm"][:] = torch.from_numpy(prm.view(np.uint8))
+            rows, cols, vals = st["bias_np"]
+            for j, r in enumerate(reqs):
+                for t, b in r.params.logit_bias.items():
+                    if 0 <= t < self.hp.n_vocab:
+                        rows[n_bias], cols[n_bias], vals[n_bias] = j, t, b
+                        n_bias += 1
+                if r.params.ignore_eos:
+                    for t in self.tokenizer.eog:
+                        rows[n_bias], cols[n_bias], vals[n_bias] = j, t, -math.inf
+                        n_bias += 1
+            h["bias_rows"][:] = torch.from_numpy(rows)
+            h["bias_cols"][:] = torch.from_numpy(cols)
+            h["bias_vals"][:] = torch.from_numpy(vals)
+            mu = np.zeros(Bp, dtype=np.float32)
+            for j, r in enumerate(reqs):
+                mu[j] = r.mu
+            h["mu"][:] = torch.from_numpy(mu)
+        h["bias_n"][0] = n_bias
+        st["dev_block"].copy_(st["host_block"], non_blocking=True)
 
     def _capture(self, Bp: int):
+        """One hipGraph per padded batch size: forward + logit bias + sampler + advance."""
         dev = self.device
-        st = {
-            "tokens": torch.zeros(Bp, dtype=torch.int32, device=dev),
-            "pos": torch.zeros(Bp, dtype=torch.int32, device=dev),
-            "slots": torch.full((Bp,), -1, dtype=torch.int32, device=dev),
-            "lens": torch.ones(Bp, dtype=torch.int32, device=dev),
-            "bt": torch.zeros(Bp, self.max_blocks, dtype=torch.int32, device=dev),
-            "bt_host": torch.zeros(Bp, self.max_blocks, dtype=torch.int32).pin_memory(),
-        }
+        MB = self.max_blocks
+        cap = max(1, Bp * self.cfg.bias_capacity)
+        K = max(1, self.cfg.decode_steps)
+        # all per-run inputs live in one int32 block (uploaded with a single copy)
+        prm_words = Bp * ops.SAMPLE_ROW_DTYPE.itemsize // 4
+        layout = [("tokens", Bp), ("pos", Bp), ("slots", Bp), ("lens", Bp), ("bt", Bp * MB), ("step", 1),
+                  ("prm", prm_words), ("bias_rows", cap), ("bias_cols", cap), ("bias_vals", cap), ("bias_n", 1),
+                  ("mu", Bp)]
+        total = sum(n for _, n in layout)
+        host_block = torch.zeros(total, dtype=torch.int32).pin_memory()
+        dev_block = torch.zeros(total, dtype=torch.int32, device=dev)
+        host, st, o = {}, {}, 0
+        for name, n in layout:
+            hv, dv = host_block[o:o + n], dev_block[o:o + n]
+            if name == "bt":
+                hv, dv = hv.view(Bp, MB), dv.view(Bp, MB)
+            elif name in ("bias_vals", "mu"):
+                hv, dv = hv.view(torch.float32), dv.view(torch.float32)
+            elif name == "prm":
+                hv, dv = hv.view(torch.uint8), dv.view(torch.uint8)
+            host[name], st[name] = hv, dv
+            o += n
+        st["slots"].fill_(-1)
+        st["lens"].fill_(1)
+        st["host"], st["host_block"], st["dev_block"] = host, host_block, dev_block
+        st["prm_np"] = np.zeros(Bp, dtype=ops.SAMPLE_ROW_DTYPE)
+        st["bias_np"] = (np.zeros(cap, np.int32), np.zeros(cap, np.int32), np.zeros(cap, np.float32))
+        st["next"] = torch.zeros(Bp, dtype=torch.int32, device=dev)
+        st["hist"] = torch.zeros(K, Bp, dtype=torch.int32, device=dev)
         fb = ForwardBatch(tokens=st["tokens"], pos=st["pos"], slots=st["slots"], decode=True, block_tables=st["bt"],
                           seq_lens=st["lens"], max_len=self.ctx)
         ws_P, _ = ops.decode_partitions(Bp, self.model.Hkv, self.ctx)
         ws = (torch.empty(Bp * self.model.Hq * ws_P * self.model.Dh, dtype=torch.float32, device=dev),
               torch.empty(Bp * self.model.Hq * ws_P * 2, dtype=torch.float32, device=dev))
+        bs = self.cfg.block_size
+
+        def body():
+            lg = self.model.forward(fb, self.kv, attn_workspace=ws)
+            ops.logit_bias(lg, st["bias_rows"], st["bias_cols"], st["bias_vals"], st["bias_n"])
+            ops.sample(lg, st["prm_np"], mu=st["mu"], params_dev=st["prm"], out=st["next"])
+            ops.decode_advance(st["next"], st["tokens"], st["pos"], st["lens"], st["slots"], st["bt"], bs,
+                               st["hist"], st["step"], st["prm"])
+            return lg
+
         s = torch.cuda.Stream(device=dev)
         s.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(s):
             for _ in range(2):  # warm up allocator / kernels outside the graph
-                self.model.forward(fb, self.kv, attn_workspace=ws)
+                body()
+                st["slots"].fill_(-1)
+                st["pos"].zero_()
+                st["lens"].fill_(1)
+                st["step"].zero_()
         torch.cuda.current_stream(dev).wait_stream(s)
         if self._graph_pool is None:
             self._graph_pool = torch.cuda.graph_pool_handle()
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph, pool=self._graph_pool):
-            logits = self.model.forward(fb, self.kv, attn_workspace=ws)
+            logits = body()
         st["ws"] = ws
         return graph, st, logits
 
@@ -489,10 +606,11 @@ class LLMEngine:
             out.append(int(idx[c]))
         return np.array(out, dtype=np.int32)
 
-    def _on_token(self, r: Request, tok: int, now: float):
+    def _on_token(self, r: Request, tok: int, now: float, append: bool = True):
         if r.done:
             return
-        self.sched.append(r.id, tok)
+        if append:
+            self.sched.append(r.id, tok)
         r.n_gen += 1
         self.metrics["gen_tokens"] += 1
         if r.first_token_t == 0.0:
@@ -512,7 +630,7 @@ class LLMEngine:
                 self._emit(r, text, tok)
             self._finish(r, "length")
             return
-        if self.sched.n_tokens(r.id) >= self.ctx:
+        if r.n_prompt + r.n_gen >= self.ctx:
             if text:
                 self._emit(r, text, tok)
             self._finish(r, "length")

@@ -272,6 +272,16 @@ class Scheduler {
     s.n_gen++;
   }
 
+  // After a multi-step decode run: `toks` were generated on the device; every one but the last
+  // already has its KV written.
+  void append_run(int64_t id, const std::vector<int32_t>& toks) {
+    SeqInfo& s = seqs_.at(id);
+    for (int32_t t : toks) s.toks.push_back(t);
+    s.n_gen += (int)toks.size();
+    s.n_computed = (int)s.toks.size() - 1;
+    bm_.commit(id, s.toks, s.n_computed);
+  }
+
   int num_waiting() const { return (int)waiting_.size(); }
   int num_running() const { return (int)running_.size(); }
   bool has(int64_t id) const { return seqs_.count(id) > 0; }
@@ -279,7 +289,10 @@ class Scheduler {
   int n_tokens(int64_t id) const { return (int)seqs_.at(id).toks.size(); }
   std::vector<int32_t> tokens(int64_t id) const { return seqs_.at(id).toks; }
 
-  py::dict schedule() {
+  // lookahead > 1 reserves KV slots for that many decode steps (device-resident multi-step
+  // decode: the host comes back only after `lookahead` tokens per sequence).
+  py::dict schedule(int lookahead = 1) {
+    if (lookahead < 1) lookahead = 1;
     std::vector<int64_t> preempted;
     // ---- 1. decode: every running sequence whose prompt is fully computed
     std::vector<int64_t> dec;
@@ -292,7 +305,7 @@ class Scheduler {
       SeqInfo& s = seqs_.at(id);
       if (s.n_computed >= (int)s.toks.size() - 1 && s.n_computed >= s.n_prompt) {
         // needs one new slot for token toks.back() at position toks.size()-1
-        while (!bm_.ensure(id, (int)s.toks.size())) {
+        while (!bm_.ensure(id, (int)s.toks.size() + lookahead - 1)) {
           // preempt youngest running sequence (recompute later)
           const int64_t victim = running_.back();
           preempt(victim);
@@ -397,7 +410,7 @@ class Scheduler {
       if (pad_ > 0 && B > 0) Bp = bucket(B);
       int maxb = 1, maxlen = 1;
       for (int64_t id : dec) {
-        const int n = (int)seqs_.at(id).toks.size();
+        const int n = (int)seqs_.at(id).toks.size() + lookahead - 1;
         maxb = std::max(maxb, bm_.blocks_for(n));
         maxlen = std::max(maxlen, n);
       }
@@ -618,7 +631,8 @@ PYBIND11_MODULE(_la_core, m) {
       .def("add", &Scheduler::add)
       .def("finish", &Scheduler::finish)
       .def("append", &Scheduler::append)
-      .def("schedule", &Scheduler::schedule)
+      .def("schedule", &Scheduler::schedule, py::arg("lookahead") = 1)
+      .def("append_run", &Scheduler::append_run)
       .def("has", &Scheduler::has)
       .def("n_gen", &Scheduler::n_gen)
       .def("n_tokens", &Scheduler::n_tokens)

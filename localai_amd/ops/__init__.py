@@ -55,6 +55,8 @@ def lib():
             "la_sample": [P, LNG, I, I, P, P, P, P, P],
             "la_penalties": [P, LNG, I, P, I, P, P, I, P, P],
             "la_sample_row_bytes": [],
+            "la_logit_bias": [P, LNG, P, P, P, P, I, P],
+            "la_decode_advance": [P, P, P, P, P, P, I, I, I, P, I, P, P, P],
         }
         for name, args in sig.items():
             fn = getattr(L, name)
@@ -675,6 +677,43 @@ def sample_ref(logits: torch.Tensor, params: np.ndarray, mu: Optional[torch.Tens
         q = torch.softmax(vals / float(p["temp"]), -1)
         out[b] = int(idx[int(torch.multinomial(q, 1, generator=g))])
     return out
+
+
+def logit_bias(logits: torch.Tensor, rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor,
+               count: torch.Tensor):
+    """In place: logits[rows[i], cols[i]] += vals[i] for i < count[0] (graph-capturable: the
+    entry count lives on the device)."""
+    cap = rows.shape[0]
+    if not logits.is_cuda:
+        n = int(count[0])
+        logits.index_put_((rows[:n].long(), cols[:n].long()), vals[:n].to(logits.dtype), accumulate=True)
+        return logits
+    _check(lib().la_logit_bias(logits.data_ptr(), logits.stride(0), rows.data_ptr(), cols.data_ptr(),
+                               vals.data_ptr(), count.data_ptr(), cap, _stream()), "la_logit_bias")
+    return logits
+
+
+def decode_advance(next_tok, tok, pos, lens, slots, bt, block_size: int, hist, step, prm_dev):
+    """Feed sampled tokens back as the next decode inputs (see csrc/decode_loop.hip)."""
+    B = tok.shape[0]
+    if not tok.is_cuda:
+        s = int(step[0])
+        if s < hist.shape[0]:
+            hist[s] = next_tok
+        live = slots >= 0
+        tok[live] = next_tok[live]
+        pos[live] += 1
+        lens[live] = pos[live] + 1
+        p = pos[live].long()
+        slots[live] = (bt[live, p // block_size] * block_size + (p % block_size)).to(slots.dtype)
+        rows = prm_dev.numpy().view(SAMPLE_ROW_DTYPE)
+        rows["counter"][live.numpy()] += 1
+        step[0] = s + 1
+        return
+    _check(lib().la_decode_advance(next_tok.data_ptr(), tok.data_ptr(), pos.data_ptr(), lens.data_ptr(),
+                                   slots.data_ptr(), bt.data_ptr(), bt.stride(0), block_size, B, hist.data_ptr(),
+                                   hist.shape[0], step.data_ptr(), prm_dev.data_ptr(), _stream()),
+           "la_decode_advance")
 
 
 def penalties(logits: torch.Tensor, hist: torch.Tensor, hist_len: torch.Tensor, pen: torch.Tensor,

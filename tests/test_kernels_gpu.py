@@ -248,3 +248,45 @@ def test_penalties():
     ref = ops.penalties(l.clone(), hist, hl, pen)
     out = ops.penalties(l.to(DEV), hist.to(DEV), hl.to(DEV), pen.to(DEV))
     assert (out.cpu() - ref).abs().max().item() < 1e-5
+
+
+def test_logit_bias_kernel():
+    B, V, cap = 4, 1000, 32
+    lg = torch.randn(B, V, device=DEV)
+    ref = lg.clone().cpu()
+    rows = torch.zeros(cap, dtype=torch.int32)
+    cols = torch.zeros(cap, dtype=torch.int32)
+    vals = torch.zeros(cap, dtype=torch.float32)
+    ent = [(0, 5, 1.5), (3, 999, -math.inf), (1, 0, -2.0), (1, 0, 0.5)]
+    for i, (r, c, v) in enumerate(ent):
+        rows[i], cols[i], vals[i] = r, c, v
+        ref[r, c] += v
+    cnt = torch.tensor([len(ent)], dtype=torch.int32)
+    ops.logit_bias(lg, rows.to(DEV), cols.to(DEV), vals.to(DEV), cnt.to(DEV))
+    assert torch.equal(lg.cpu(), ref)
+
+
+def test_decode_advance_kernel():
+    B, MB, BS, K = 5, 4, 16, 3
+    bt = torch.randint(0, 100, (B, MB), dtype=torch.int32)
+    pos = torch.tensor([3, 15, 31, 0, 7], dtype=torch.int32)
+    slots = (bt[torch.arange(B), pos.long() // BS] * BS + pos % BS).to(torch.int32)
+    slots[3] = -1  # padding row
+    lens = pos + 1
+    tok = torch.zeros(B, dtype=torch.int32)
+    prm = np.zeros(B, dtype=ops.SAMPLE_ROW_DTYPE)
+    prm["counter"] = [10, 11, 12, 13, 14]
+    nxt = torch.tensor([7, 8, 9, 10, 11], dtype=torch.int32)
+    hist = torch.zeros(K, B, dtype=torch.int32)
+    step = torch.zeros(1, dtype=torch.int32)
+    st_cpu = [x.clone() for x in (tok, pos, lens, slots, hist, step)]
+    prm_cpu = torch.from_numpy(prm.view(np.uint8).copy())
+    ops.decode_advance(nxt, *st_cpu[:4], bt, BS, st_cpu[4], st_cpu[5], prm_cpu)
+    g = [x.to(DEV) for x in (tok, pos, lens, slots, hist, step)]
+    prm_dev = torch.from_numpy(prm.view(np.uint8).copy()).to(DEV)
+    ops.decode_advance(nxt.to(DEV), *g[:4], bt.to(DEV), BS, g[4], g[5], prm_dev)
+    for a, b in zip(g, st_cpu):
+        assert torch.equal(a.cpu(), b)
+    assert np.array_equal(prm_dev.cpu().numpy().view(ops.SAMPLE_ROW_DTYPE)["counter"],
+                          prm_cpu.numpy().view(ops.SAMPLE_ROW_DTYPE)["counter"])
+    assert int(g[5].item()) == 1 and list(g[4][0].cpu()) == [7, 8, 9, 10, 11]
