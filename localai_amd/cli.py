@@ -1,0 +1,274 @@
+"""`local-ai`-compatible command line (`main.go`, `core/cli/*`).
+
+    python -m localai_amd run [MODEL_URLS...] [--models-path DIR] [--address :8080] ...
+    python -m localai_amd models list|install NAME
+    python -m localai_amd tts TEXT --model M [--backend B] [--voice V] [--output-file F]
+    python -m localai_amd sound-generation TEXT --model M ...
+    python -m localai_amd transcript FILE --model M [--language L]
+    python -m localai_amd util gguf-info FILE | usecase-heuristic FILE
+    python -m localai_amd worker tp --model FILE ...   (tensor-parallel worker group, RCCL)
+
+Every `run` flag mirrors the reference flag name and its LOCALAI_* / legacy env variable
+(core/cli/run.go:19-73); flags win over env, env over defaults.  `.env` / `localai.env`
+files are read like the reference entrypoint (main.go:20-60).
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import logging
+import os
+import sys
+from typing import List, Optional
+
+from .config.app_config import ApplicationConfig, parse_duration
+
+ENV_FILES = [".env", "localai.env", os.path.expanduser("~/.config/localai.env"), "/etc/localai.env"]
+
+
+def load_env_files():
+    for p in ENV_FILES:
+        try:
+            with open(p) as f:
+                for line in f:
+                    line = line.strip()
+                    if not line or line.startswith("#") or "=" not in line:
+                        continue
+                    k, v = line.split("=", 1)
+                    k = k.strip().removeprefix("export ").strip()
+                    v = v.strip().strip('"').strip("'")
+                    os.environ.setdefault(k, v)
+        except OSError:
+            continue
+
+
+# (flag, ApplicationConfig field, kind)
+RUN_FLAGS = [
+    ("--models-path", "models_path", str), ("--backend-assets-path", "backend_assets_path", str),
+    ("--image-path", "image_dir", str), ("--audio-path", "audio_dir", str), ("--upload-path", "upload_dir", str),
+    ("--config-path", "config_dir", str), ("--localai-config-dir", "dynamic_config_dir", str),
+    ("--localai-config-dir-poll-interval", "dynamic_config_poll_interval", "duration"),
+    ("--models-config-file", "models_config_file", str), ("--galleries", "galleries", "json"),
+    ("--autoload-galleries", "autoload_galleries", bool), ("--remote-library", "remote_library", str),
+    ("--preload-models", "preload_models", str), ("--models", "model_urls", "list"),
+    ("--preload-models-config", "preload_models_from_path", str), ("--f16", "f16", bool),
+    ("--threads", "threads", int), ("--context-size", "context_size", int), ("--address", "address", str),
+    ("--cors", "cors", bool), ("--cors-allow-origins", "cors_allow_origins", str), ("--csrf", "csrf", bool),
+    ("--upload-limit", "upload_limit_mb", int), ("--api-keys", "api_keys", "list"),
+    ("--disable-webui", "disable_webui", bool), ("--disable-predownload-scan", "disable_predownload_scan", bool),
+    ("--opaque-errors", "opaque_errors", bool), ("--use-subtle-key-comparison", "use_subtle_key_comparison", bool),
+    ("--disable-api-key-requirement-for-http-get", "disable_api_key_requirement_for_http_get", bool),
+    ("--http-get-exempted-endpoints", "http_get_exempted_endpoints", "list"), ("--p2p", "p2p", bool),
+    ("--p2ptoken", "p2p_token", str), ("--p2p-network-id", "p2p_network_id", str),
+    ("--parallel-requests", "parallel_backend_requests", bool),
+    ("--single-active-backend", "single_active_backend", bool),
+    ("--preload-backend-only", "preload_backend_only", bool),
+    ("--external-grpc-backends", "external_grpc_backends", "backends"),
+    ("--enable-watchdog-idle", "watchdog_idle", bool), ("--watchdog-idle-timeout", "watchdog_idle_timeout", "duration"),
+    ("--enable-watchdog-busy", "watchdog_busy", bool), ("--watchdog-busy-timeout", "watchdog_busy_timeout", "duration"),
+    ("--federated", "federated", bool), ("--disable-gallery-endpoint", "disable_gallery_endpoint", bool),
+    ("--load-to-memory", "load_to_memory", "list"), ("--engine-mode", "engine_mode", str),
+]
+
+
+def _convert(kind, v):
+    if kind is bool:
+        return True if v is True else str(v).lower() in ("1", "true", "yes", "on")
+    if kind is int:
+        return int(v)
+    if kind == "duration":
+        return parse_duration(v)
+    if kind == "json":
+        return json.loads(v)
+    if kind == "list":
+        return [x for x in (v if isinstance(v, list) else str(v).split(",")) if x]
+    if kind == "backends":
+        out = {}
+        for item in (v if isinstance(v, list) else str(v).split(",")):
+            name, _, uri = item.partition(":")
+            if name and uri:
+                out[name] = uri
+        return out
+    return v
+
+
+def add_run_flags(p: argparse.ArgumentParser):
+    p.add_argument("models_args", nargs="*", help="model configuration URLs / gallery names to load")
+    for flag, field, kind in RUN_FLAGS:
+        if kind is bool:
+            p.add_argument(flag, dest=field, nargs="?", const=True, default=None)
+        else:
+            p.add_argument(flag, dest=field, default=None)
+    p.add_argument("--http-server", default="native", choices=["native", "uvicorn"])
+    p.add_argument("--log-level", default=os.environ.get("LOCALAI_LOG_LEVEL", "info"))
+
+
+def app_config_from_args(a) -> ApplicationConfig:
+    cfg = ApplicationConfig.from_env()
+    for flag, field, kind in RUN_FLAGS:
+        v = getattr(a, field, None)
+        if v is not None:
+            setattr(cfg, field, _convert(kind, v))
+    if getattr(a, "models_args", None):
+        cfg.model_urls = list(cfg.model_urls) + list(a.models_args)
+    return cfg
+
+
+def parse_address(addr: str):
+    host, _, port = addr.rpartition(":")
+    return (host or "0.0.0.0"), int(port or 8080)
+
+
+def cmd_run(a) -> int:
+    from .startup import run_server, startup
+    cfg = app_config_from_args(a)
+    state = startup(cfg)
+    if cfg.preload_backend_only:
+        from .startup import load_to_memory
+        asyncio.run(load_to_memory(state))
+        return 0
+    host, port = parse_address(cfg.address)
+    run_server(state, host, port, a.http_server)
+    return 0
+
+
+def cmd_models(a) -> int:
+    from . import gallery as gal
+    cfg = ApplicationConfig.from_env()
+    if a.models_path:
+        cfg.models_path = a.models_path
+    if a.galleries:
+        cfg.galleries = json.loads(a.galleries)
+    if a.action == "list":
+        for m in gal.available_models(cfg.galleries, cfg.models_path):
+            print(f"{'*' if m.installed else ' '} {m.id()}")
+        return 0
+    for name in a.names:
+        gal.install_from_gallery(cfg.galleries, name, cfg.models_path, gal.GalleryModel())
+        print(f"installed {name}")
+    return 0
+
+
+async def _one_shot(cfg: ApplicationConfig, model: str, backend: str, rpc: str, req):
+    from .startup import startup
+    state = startup(cfg)
+    bc = state.config_for(model)
+    if backend:
+        bc.backend = backend
+    lm = await state.manager.load(bc)
+    try:
+        return await getattr(lm.handle, rpc)(req)
+    finally:
+        await state.manager.stop_all()
+
+
+def cmd_tts(a) -> int:
+    from .grpc import backend_pb as pb
+    cfg = ApplicationConfig.from_env(models_path=a.models_path or ApplicationConfig.from_env().models_path)
+    out = os.path.abspath(a.output_file or "tts.wav")
+    res = asyncio.run(_one_shot(cfg, a.model, a.backend, "TTS",
+                                pb.TTSRequest(text=" ".join(a.text), model=a.model, dst=out, voice=a.voice or "",
+                                              language=a.language or "")))
+    print(out if res.success else res.message)
+    return 0 if res.success else 1
+
+
+def cmd_sound(a) -> int:
+    from .grpc import backend_pb as pb
+    cfg = ApplicationConfig.from_env(models_path=a.models_path or ApplicationConfig.from_env().models_path)
+    out = os.path.abspath(a.output_file or "sound.wav")
+    kw = {"text": " ".join(a.text), "model": a.model, "dst": out}
+    if a.duration:
+        kw["duration"] = float(a.duration)
+    res = asyncio.run(_one_shot(cfg, a.model, a.backend, "SoundGeneration", pb.SoundGenerationRequest(**kw)))
+    print(out if res.success else res.message)
+    return 0 if res.success else 1
+
+
+def cmd_transcript(a) -> int:
+    from .grpc import backend_pb as pb
+    cfg = ApplicationConfig.from_env(models_path=a.models_path or ApplicationConfig.from_env().models_path)
+    res = asyncio.run(_one_shot(cfg, a.model, a.backend, "AudioTranscription",
+                                pb.TranscriptRequest(dst=os.path.abspath(a.filename), language=a.language or "",
+                                                     threads=int(a.threads or 4))))
+    for s in res.segments:
+        print(s.text)
+    return 0
+
+
+def cmd_util(a) -> int:
+    from .gguf import gguf_info
+    if a.action == "gguf-info":
+        info = gguf_info(a.file)
+        print(json.dumps(info, indent=2, default=str))
+        return 0
+    if a.action == "usecase-heuristic":
+        from .config.backend_config import USECASE_FLAGS
+        from .config.loader import BackendConfigLoader
+        ld = BackendConfigLoader(os.path.dirname(os.path.abspath(a.file)))
+        ld.load_backend_config(a.file)
+        for c in ld.all():
+            flags = [n for n, f in USECASE_FLAGS.items() if f and c.guess_usecases(f)]
+            print(f"{c.name}: {', '.join(flags) or 'none'}")
+        return 0
+    return 2
+
+
+def cmd_worker(a) -> int:
+    from .parallel.worker import main as worker_main
+    return worker_main(a.rest)
+
+
+def build_parser() -> argparse.ArgumentParser:
+    ap = argparse.ArgumentParser("local-ai", description="LocalAI-compatible server, MI355X-native engine")
+    ap.add_argument("--log-level", default=None)
+    sub = ap.add_subparsers(dest="cmd")
+    add_run_flags(sub.add_parser("run", help="start the API server"))
+    m = sub.add_parser("models", help="gallery models")
+    m.add_argument("action", choices=["list", "install"])
+    m.add_argument("names", nargs="*")
+    m.add_argument("--models-path", default=None)
+    m.add_argument("--galleries", default=None)
+    for name, fn in (("tts", cmd_tts), ("sound-generation", cmd_sound)):
+        t = sub.add_parser(name)
+        t.add_argument("text", nargs="+")
+        t.add_argument("--model", "-m", required=True)
+        t.add_argument("--backend", "-b", default="")
+        t.add_argument("--voice", default="")
+        t.add_argument("--language", default="")
+        t.add_argument("--duration", default=None)
+        t.add_argument("--output-file", default=None)
+        t.add_argument("--models-path", default=None)
+        t.set_defaults(fn=fn)
+    t = sub.add_parser("transcript")
+    t.add_argument("filename")
+    t.add_argument("--model", "-m", required=True)
+    t.add_argument("--backend", "-b", default="")
+    t.add_argument("--language", default="")
+    t.add_argument("--threads", default=None)
+    t.add_argument("--models-path", default=None)
+    u = sub.add_parser("util")
+    u.add_argument("action", choices=["gguf-info", "usecase-heuristic"])
+    u.add_argument("file")
+    w = sub.add_parser("worker", help="tensor-parallel engine worker group (replaces llama-cpp-rpc workers)")
+    w.add_argument("rest", nargs=argparse.REMAINDER)
+    return ap
+
+
+def main(argv: Optional[List[str]] = None) -> int:
+    load_env_files()
+    ap = build_parser()
+    a = ap.parse_args(argv)
+    lvl = (getattr(a, "log_level", None) or os.environ.get("LOCALAI_LOG_LEVEL", "info")).upper()
+    logging.basicConfig(level=getattr(logging, lvl, logging.INFO), format="%(asctime)s %(levelname)s %(name)s %(message)s")
+    if a.cmd is None:
+        ap.print_help()
+        return 2
+    fn = {"run": cmd_run, "models": cmd_models, "transcript": cmd_transcript, "util": cmd_util,
+          "worker": cmd_worker}.get(a.cmd) or getattr(a, "fn", None)
+    return fn(a)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

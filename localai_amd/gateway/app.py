@@ -43,16 +43,8 @@ class AuthMiddleware:
         self.exempt = [re.compile(p) for p in state.cfg.http_get_exempted_endpoints]
 
     def _keys(self):
-        keys = list(self.state.cfg.api_keys)
-        d = self.state.cfg.dynamic_config_dir
-        dyn = os.path.join(d or "", "api_keys.json")
-        if d and os.path.isfile(dyn):
-            try:
-                with open(dyn) as f:
-                    keys += [k for k in json.load(f) if isinstance(k, str)]
-            except (OSError, ValueError):
-                pass
-        return keys
+        # static keys + dynamic api_keys.json (kept current by startup.ConfigWatcher)
+        return self.state.cfg.api_keys
 
     async def __call__(self, scope, receive, send):
         if scope["type"] != "http":

@@ -23,7 +23,7 @@ __global__ void __launch_bounds__(256) logit_bias_kernel(float* __restrict__ log
                                                          int cap) {
   const int n = min(*count, cap);
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
-    logits[(long)rows[i] * ld + cols[i]] += vals[i];
+    atomicAdd(&logits[(long)rows[i] * ld + cols[i]], vals[i]);  // entries may repeat a (row, col)
 }
 
 // One workgroup: rows are independent; thread 0 bumps the step counter after all rows read it.
