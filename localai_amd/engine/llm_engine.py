@@ -472,9 +472,8 @@ class LLMEngine:
         st["hist"] = torch.zeros(K, Bp, dtype=torch.int32, device=dev)
         fb = ForwardBatch(tokens=st["tokens"], pos=st["pos"], slots=st["slots"], decode=True, block_tables=st["bt"],
                           seq_lens=st["lens"], max_len=self.ctx)
-        ws_P, _ = ops.decode_partitions(Bp, self.model.Hkv, self.ctx)
-        ws = (torch.empty(Bp * self.model.Hq * ws_P * self.model.Dh, dtype=torch.float32, device=dev),
-              torch.empty(Bp * self.model.Hq * ws_P * 2, dtype=torch.float32, device=dev))
+        ws = ops.decode_workspace(Bp, self.model.Hq, self.model.Hkv, self.model.Dh, self.ctx, dev,
+                                  self.cfg.block_size)
         bs = self.cfg.block_size
 
         def body():

@@ -50,7 +50,7 @@ def lib():
             "la_reduce_slabs": [P, LNG, I, P, I, I, P, P, P],
             "la_embed": [I, P, P, P, P, I, I, P, I, P, F, P],
             "la_dequant": [I, P, P, P, P, I, I, P, P],
-            "la_attn_decode": [P, P, P, P, I, P, I, I, I, I, I, F, I, I, P, P, P, P],
+            "la_attn_decode": [P, P, P, P, I, P, I, I, I, I, I, F, I, I, P, P, P, P, P],
             "la_attn_prefill": [P, P, P, P, I, P, P, P, I, I, I, I, I, F, P, P],
             "la_sample": [P, LNG, I, I, P, P, P, P, P],
             "la_penalties": [P, LNG, I, P, I, P, P, I, P, P],
@@ -254,16 +254,19 @@ class Partial:
 
 
 def pick_splits(N: int, K: int, M: int) -> int:
-    """Split-K so the skinny GEMM launches >= ~2 workgroups per CU (256 CUs)."""
+    """Split-K for the skinny GEMM: about 2 workgroups per CU (256 CUs), but every split keeps
+    >= 4 super-blocks so each lane streams a full chunk of weight fragments (4 in flight)."""
     nsb = K // 256
     nblk = (N + 63) // 64
-    want = max(1, math.ceil(512 / nblk))
     best = 1
     for s in range(1, nsb + 1):
-        if nsb % s == 0:
-            best = s
-            if s >= want:
-                break
+        if nsb % s:
+            continue
+        if s > 1 and nsb // s < 4:
+            break
+        best = s
+        if nblk * s >= 512:
+            break
     # the consumer reads S slabs: keep the slab traffic below the weight traffic
     while best > 1 and best * M * N * 4 * 2 > N * K // 2:
         cands = [s for s in range(1, best) if nsb % s == 0]
@@ -489,19 +492,29 @@ def embed(tokens: torch.Tensor, w: QWeight, scale: float = 1.0, out: Optional[to
 DEC_TARGET_WAVES = 4096  # ~16 waves per CU over 256 CUs
 
 
-def decode_partitions(B: int, Hkv: int, max_len: int) -> Tuple[int, int]:
+def decode_partitions(B: int, Hkv: int, max_len: int, block_size: int = 32) -> Tuple[int, int]:
     """Split-KV partitioning for attn_decode: (P, PS).  Enough partitions to put ~16 waves on
-    every CU; each workgroup (4 waves) covers PS keys (multiple of 128)."""
+    every CU; each workgroup (4 waves) covers PS keys (multiple of 128, at most 2048 pages so
+    the partition's block-table slice fits the kernel's LDS stage)."""
     max_len = max(1, max_len)
-    P = max(1, min(-(-DEC_TARGET_WAVES // (B * Hkv * 4)), -(-max_len // 128)))
+    P = max(1, min(-(-DEC_TARGET_WAVES // (B * Hkv * 4)), -(-max_len // 128), 64))
+    P = max(P, -(-max_len // (2048 * block_size)))
     PS = -(-(-(-max_len // P)) // 128) * 128
     P = -(-max_len // PS)
     return P, PS
 
 
+def decode_workspace(B: int, Hq: int, Hkv: int, Dh: int, max_len: int, device, block_size: int = 32):
+    """Persistent buffers for attn_decode (split-KV partials + self-resetting merge tickets)."""
+    P, _ = decode_partitions(B, Hkv, max_len, block_size)
+    return (torch.empty(max(1, B * Hq * P * Dh), dtype=torch.float32, device=device),
+            torch.empty(max(1, B * Hq * P * 2), dtype=torch.float32, device=device),
+            torch.zeros(max(1, B * Hkv), dtype=torch.int32, device=device))
+
+
 def attn_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, block_tables: torch.Tensor,
                 seq_lens: torch.Tensor, scale: float, max_seq_len: int, out: Optional[torch.Tensor] = None,
-                workspace: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:
+                workspace: Optional[Tuple[torch.Tensor, ...]] = None) -> torch.Tensor:
     """q [B,Hq,Dh] bf16; K cache [nblk,Hkv,BS,Dh]; V cache (transposed pages) [nblk,Hkv,Dh,BS];
     block_tables [B,maxb] i32; seq_lens [B] i32."""
     B, Hq, Dh = q.shape
@@ -510,18 +523,17 @@ def attn_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, b
         raise ValueError("attn_decode: head/cache shape mismatch")
     if not q.is_cuda:
         return _attn_ref_decode(q, k_cache, v_cache, block_tables, seq_lens, scale)
-    P, PS = decode_partitions(B, Hkv, max_seq_len)
+    P, PS = decode_partitions(B, Hkv, max_seq_len, BS)
     if out is None:
         out = torch.empty(B, Hq, Dh, dtype=torch.bfloat16, device=q.device)
-    need = B * Hq * P * Dh
-    if workspace is None or workspace[0].numel() < need or workspace[1].numel() < B * Hq * P * 2:
-        po = torch.empty(max(1, need), dtype=torch.float32, device=q.device)
-        pml = torch.empty(max(1, B * Hq * P * 2), dtype=torch.float32, device=q.device)
-    else:
-        po, pml = workspace
+    if (workspace is None or len(workspace) < 3 or workspace[0].numel() < B * Hq * P * Dh
+            or workspace[1].numel() < B * Hq * P * 2 or workspace[2].numel() < B * Hkv):
+        workspace = decode_workspace(B, Hq, Hkv, Dh, max_seq_len, q.device, BS)
+    po, pml, tk = workspace[:3]
     _check(lib().la_attn_decode(q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr(),
                                 block_tables.shape[1], seq_lens.data_ptr(), B, Hq, Hkv, Dh, BS, float(scale), P, PS,
-                                out.data_ptr(), po.data_ptr(), pml.data_ptr(), _stream()), "la_attn_decode")
+                                out.data_ptr(), po.data_ptr(), pml.data_ptr(), tk.data_ptr(), _stream()),
+           "la_attn_decode")
     return out
 
 

@@ -16,51 +16,61 @@
 namespace la {
 
 // ----------------------------------------------------------------------------- decode
-// MFMA flash-decoding.  Per wave: one (sequence, kv-head) and a strided set of 32-key tiles.
+// MFMA flash-decoding.  Workgroup = (partition of <= PS keys, kv head, sequence), 4 waves; wave w
+// takes the partition's 32-key tiles w, w+4, ...
 //   S^T[16 keys x 16 heads] = K[16 keys x Dh] . Q^T[Dh x 16 heads]   (keys on MFMA rows)
 //   -> lane l holds the scores of head l&15 for keys 4(l>>4)+i, so the running max needs only
 //      two cross-lane shuffles (xor 16, 32) and P is already the lane's A-operand fragment;
 //   O[16 heads x Dh] += P[16 heads x 32 keys] . V[32 keys x Dh]
-//   -> V is stored transposed per page ([Dh][BS]) so the B fragment (8 keys at one d) is a
+//   -> V is stored transposed per page ([Dh][BS]) so the B fragment (4 keys at one d) is a
 //      contiguous 8-byte load; no LDS staging, no transposes.
-// The 4 waves of a workgroup split one partition's tiles and merge through LDS; partitions
-// (flash-decoding split-KV) are merged by attn_decode_combine_kernel.  Scores live in the
-// log2 domain (scale * log2 e folded in) so every exponential is one v_exp_f32.
+// Latency structure (decode attention is latency-bound: a few KB per wave):
+//   * the partition's block-table slice is staged in LDS once (no bt -> K/V load chains);
+//   * every K and V load of tile i+1 is issued before tile i is computed (register double
+//     buffer); keys past the sequence end are clamped to a valid key and masked in the scores,
+//     so no load sits behind a branch;
+//   * split-KV partials are merged IN the kernel by the last-arriving partition (agent-scope
+//     release/acquire ticket per (sequence, kv head); the ticket resets itself for the next
+//     launch / graph replay), so there is no separate combine launch.
+// Scores live in the log2 domain (scale * log2 e folded in): every exponential is one v_exp_f32.
 constexpr int DEC_T = 256;
+constexpr int DEC_MAXBT = 2048;  // block-table entries of one partition staged in LDS
+
+template <int DH, int GT>
+struct DecShared {
+  float ow[4][GT][DH];
+  float mw[4][16], lw[4][16];
+  int bt[DEC_MAXBT];
+  int last;
+};
 
 template <int DH>
+struct DecTile {
+  bf16x8 k[2][(DH + 31) / 32];
+  bf16x4 v[2][DH / 16];
+};
+
+template <int DH, int GT>
 __global__ __launch_bounds__(DEC_T) void attn_decode_kernel(
     const bf16* __restrict__ q, const bf16* __restrict__ kc, const bf16* __restrict__ vc,
     const int* __restrict__ block_tables, int max_blocks, const int* __restrict__ seq_lens, int Hkv, int G,
     int BS, float scale_log2, int PS, bf16* __restrict__ out, float* __restrict__ part_o,
-    float* __restrict__ part_ml, int P) {
+    float* __restrict__ part_ml, int P, int* __restrict__ tickets) {
   constexpr int KC = (DH + 31) / 32;  // 32-wide k chunks of the QK^T product
   constexpr int ND = DH / 16;         // 16-wide d tiles of the PV product
-  __shared__ float ow[4][16][DH];
-  __shared__ float mw[4][16], lw[4][16];
+  __shared__ DecShared<DH, GT> sh;
 
   const int p = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
   const int Hq = Hkv * G;
   const int L = seq_lens[b];
   const int t0 = p * PS;
+  if (t0 >= L) return;  // empty partition: the combiner only waits for ceil(L / PS) of them
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 15, g = lane >> 4;
-  if (t0 >= L) {
-    if (P > 1) {
-      for (int i = tid; i < G * DH; i += DEC_T) {
-        const int h = kvh * G + i / DH;
-        part_o[(((long)b * Hq + h) * P + p) * DH + (i % DH)] = 0.f;
-      }
-      if (tid < G) {
-        float* ml = part_ml + (((long)b * Hq + kvh * G + tid) * P + p) * 2;
-        ml[0] = -INFINITY;
-        ml[1] = 0.f;
-      }
-    }
-    return;
-  }
   const int kend = min(L, t0 + PS);
-  const int* bt = block_tables + (long)b * max_blocks;
+  const int nbt = (kend - t0 + BS - 1) / BS;
+  const int* bt = block_tables + (long)b * max_blocks + t0 / BS;
+  for (int i = tid; i < nbt; i += DEC_T) sh.bt[i] = bt[i];
 
   // Q^T fragments: lane holds Q[head r][d = 32c + 8g .. +8]
   bf16x8 qf[KC];
@@ -71,118 +81,124 @@ __global__ __launch_bounds__(DEC_T) void attn_decode_kernel(
     if (r < G && d < DH) v = *(const bf16x8*)(q + ((long)b * Hq + kvh * G + r) * DH + d);
     qf[c] = v;
   }
+  __syncthreads();
+
+  const long head_off = (long)kvh * BS * DH;  // inside a page: [Hkv][BS][Dh] / [Hkv][Dh][BS]
+  auto load_tile = [&](int kb, DecTile<DH>& T) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      // K rows: key kb + 16t + r;  V^T: keys kb + 16t + 4g .. +3 (all clamped to a real key)
+      const int kk = min(kb + 16 * t + r, kend - 1);
+      const int kv = min(kb + 16 * t + 4 * g, kend - 1) & ~3;
+      const long pk = (long)sh.bt[(kk - t0) / BS] * Hkv * BS * DH + head_off;
+      const long pv = (long)sh.bt[(kv - t0) / BS] * Hkv * BS * DH + head_off;
+      const bf16* krow = kc + pk + (long)(kk % BS) * DH;
+#pragma unroll
+      for (int c = 0; c < KC; ++c) {
+        const int d = min(32 * c + 8 * g, DH - 8);
+        T.k[t][c] = *(const bf16x8*)(krow + d);
+      }
+#pragma unroll
+      for (int nd = 0; nd < ND; ++nd) {
+        const int d = 16 * nd + r;
+        T.v[t][nd] = *(const bf16x4*)(vc + pv + (long)d * BS + (kv % BS));
+      }
+    }
+  };
 
   f32x4 o[ND];
 #pragma unroll
   for (int i = 0; i < ND; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m = -INFINITY, lsum = 0.f;
 
-  for (int kb = t0 + 32 * wave; kb < kend; kb += 32 * 4) {
-    float s[2][4];
-    uint32_t vmask[2];
-    int blk[2], off[2];
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const int key0 = kb + 16 * t;
-      vmask[t] = 0;
-      if (key0 >= kend) {
-        blk[t] = 0; off[t] = 0;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) s[t][i] = -INFINITY;
-        continue;
-      }
-      blk[t] = bt[key0 / BS];
-      off[t] = key0 % BS;
-      const bf16* krow = kc + (((long)blk[t] * Hkv + kvh) * BS + off[t] + r) * DH;
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int c = 0; c < KC; ++c) {
-        const int d = 32 * c + 8 * g;
-        bf16x8 a = {};
-        if (d < DH) a = *(const bf16x8*)(krow + d);
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, qf[c], acc, 0, 0, 0);
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const bool ok = key0 + 4 * g + i < kend;
-        s[t][i] = ok ? acc[i] * scale_log2 : -INFINITY;
-        vmask[t] |= ok ? (1u << i) : 0u;
-      }
-    }
-    // online softmax for head r over this 32-key tile
-    float mx = fmaxf(fmaxf(fmaxf(s[0][0], s[0][1]), fmaxf(s[0][2], s[0][3])),
-                     fmaxf(fmaxf(s[1][0], s[1][1]), fmaxf(s[1][2], s[1][3])));
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float mnew = fmaxf(m, mx);
-    const float msafe = (mnew == -INFINITY) ? 0.f : mnew;
-    const float alpha = exp2f(m - msafe);
-    bf16x8 pa;
-    float ps = 0.f;
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float e = exp2f(s[t][i] - msafe);
-        ps += e;
-        pa[4 * t + i] = (bf16)e;
-      }
-    lsum = lsum * alpha + ps;
-    m = mnew;
-    // O rows are heads 4g+i: fetch each row's alpha from the lane that owns that head
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float f = __shfl(alpha, 4 * g + i, 64);
-#pragma unroll
-      for (int nd = 0; nd < ND; ++nd) o[nd][i] *= f;
-    }
-    // PV: B fragment = V[keys 4g..4g+3 of sub-tile 0, 4g..4g+3 of sub-tile 1][d = 16nd + r]
-#pragma unroll
-    for (int nd = 0; nd < ND; ++nd) {
-      const int d = 16 * nd + r;
-      bf16x8 vb;
+  int kb = t0 + 32 * wave;
+  if (kb < kend) {
+    DecTile<DH> cur, nxt;
+    load_tile(kb, cur);
+    for (; kb < kend; kb += 128) {
+      if (kb + 128 < kend) load_tile(kb + 128, nxt);
+      float s[2][4];
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
-        bf16x4 v4 = {};
-        if (vmask[t]) {
-          v4 = *(const bf16x4*)(vc + (((long)blk[t] * Hkv + kvh) * DH + d) * BS + off[t] + 4 * g);
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int i = 0; i < 4; ++i)
-            if (!(vmask[t] & (1u << i))) v4[i] = (bf16)0.f;
+        for (int c = 0; c < KC; ++c) {
+          bf16x8 a = cur.k[t][c];
+          if (32 * c + 8 * g >= DH) a = bf16x8{};  // Dh % 32 != 0: zero the tail chunk
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, qf[c], acc, 0, 0, 0);
         }
 #pragma unroll
-        for (int i = 0; i < 4; ++i) vb[4 * t + i] = v4[i];
+        for (int i = 0; i < 4; ++i) s[t][i] = (kb + 16 * t + 4 * g + i < kend) ? acc[i] * scale_log2 : -INFINITY;
       }
-      o[nd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, vb, o[nd], 0, 0, 0);
+      // online softmax for head r over this 32-key tile
+      float mx = fmaxf(fmaxf(fmaxf(s[0][0], s[0][1]), fmaxf(s[0][2], s[0][3])),
+                       fmaxf(fmaxf(s[1][0], s[1][1]), fmaxf(s[1][2], s[1][3])));
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mnew = fmaxf(m, mx);
+      const float msafe = (mnew == -INFINITY) ? 0.f : mnew;
+      const float alpha = exp2f(m - msafe);
+      bf16x8 pa;
+      float ps = 0.f;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float e = exp2f(s[t][i] - msafe);
+          ps += e;
+          pa[4 * t + i] = (bf16)e;
+        }
+      lsum = lsum * alpha + ps;
+      m = mnew;
+      // O rows are heads 4g+i: fetch each row's alpha from the lane that owns that head
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float f = __shfl(alpha, 4 * g + i, 64);
+#pragma unroll
+        for (int nd = 0; nd < ND; ++nd) o[nd][i] *= f;
+      }
+#pragma unroll
+      for (int nd = 0; nd < ND; ++nd) {
+        bf16x8 vb;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          vb[i] = cur.v[0][nd][i];
+          vb[4 + i] = cur.v[1][nd][i];
+        }
+        o[nd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, vb, o[nd], 0, 0, 0);
+      }
+      cur = nxt;
     }
   }
   // wave totals: lsum over the 4 lane groups (same head r)
   lsum += __shfl_xor(lsum, 16, 64);
   lsum += __shfl_xor(lsum, 32, 64);
   if (g == 0) {
-    mw[wave][r] = m;
-    lw[wave][r] = lsum;
+    sh.mw[wave][r] = m;
+    sh.lw[wave][r] = lsum;
   }
 #pragma unroll
   for (int nd = 0; nd < ND; ++nd)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) ow[wave][4 * g + i][16 * nd + r] = o[nd][i];
+    for (int i = 0; i < 4; ++i)
+      if (4 * g + i < GT) sh.ow[wave][min(4 * g + i, GT - 1)][16 * nd + r] = o[nd][i];
   __syncthreads();
+  const int np = (L + PS - 1) / PS;  // partitions holding keys of this sequence
   for (int i = tid; i < G * DH; i += DEC_T) {
     const int h = i / DH, d = i % DH;
     float M = -INFINITY;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) M = fmaxf(M, mw[w][h]);
+    for (int w = 0; w < 4; ++w) M = fmaxf(M, sh.mw[w][h]);
     const float Ms = (M == -INFINITY) ? 0.f : M;
     float num = 0.f, den = 0.f;
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
-      const float f = exp2f(mw[w][h] - Ms);
-      num += f * ow[w][h][d];
-      den += f * lw[w][h];
+      const float f = exp2f(sh.mw[w][h] - Ms);
+      num += f * sh.ow[w][h][d];
+      den += f * sh.lw[w][h];
     }
     const int hq = kvh * G + h;
-    if (P == 1) {
+    if (np == 1) {
       out[((long)b * Hq + hq) * DH + d] = (bf16)(den > 0.f ? num / den : 0.f);
     } else {
       part_o[(((long)b * Hq + hq) * P + p) * DH + d] = num;
@@ -193,22 +209,56 @@ __global__ __launch_bounds__(DEC_T) void attn_decode_kernel(
       }
     }
   }
-}
-
-__global__ __launch_bounds__(128) void attn_decode_combine_kernel(const float* __restrict__ part_o,
-                                                                  const float* __restrict__ part_ml, int P, int DH,
-                                                                  bf16* __restrict__ out) {
-  const int hq = blockIdx.x, b = blockIdx.y, Hq = gridDim.x;
-  const long base = ((long)b * Hq + hq) * P;
-  float M = -INFINITY;
-  for (int i = 0; i < P; ++i) M = fmaxf(M, part_ml[(base + i) * 2]);
-  const float Ms = (M == -INFINITY) ? 0.f : M;
-  float den = 0.f;
-  for (int i = 0; i < P; ++i) den += exp2f(part_ml[(base + i) * 2] - Ms) * part_ml[(base + i) * 2 + 1];
-  for (int d = threadIdx.x; d < DH; d += blockDim.x) {
+  if (np == 1) return;
+  // ---- split-KV merge by the last-arriving partition of (b, kvh)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int* tk = tickets + (long)b * Hkv + kvh;
+    const int prev = __hip_atomic_fetch_add(tk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = (prev == np - 1);
+    if (last) {
+      *tk = 0;  // self-resetting ticket (next launch / graph replay starts from 0)
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    sh.last = last;
+  }
+  __syncthreads();
+  if (!sh.last) return;
+  // merge weights per (partition, head) staged in LDS (reuses the wave-merge arrays), then every
+  // (head, d) output sums its np partials with independent, unrolled loads
+  float* wts = &sh.ow[0][0][0];  // [np][G] weights, then [G] 1/den
+  const long hb = ((long)b * Hq + kvh * G) * P;
+  if (tid < G) {
+    const long base = hb + (long)tid * P;
+    float M = -INFINITY;
+    for (int j = 0; j < np; ++j) M = fmaxf(M, part_ml[(base + j) * 2]);
+    const float Ms = (M == -INFINITY) ? 0.f : M;
+    float den = 0.f;
+    for (int j = 0; j < np; ++j) {
+      const float f = exp2f(part_ml[(base + j) * 2] - Ms);
+      wts[j * G + tid] = f;
+      den += f * part_ml[(base + j) * 2 + 1];
+    }
+    wts[np * G + tid] = den > 0.f ? 1.f / den : 0.f;
+  }
+  __syncthreads();
+  for (int i = tid; i < G * DH; i += DEC_T) {
+    const int h = i / DH, d = i % DH;
+    const float* po = part_o + (hb + (long)h * P) * DH + d;
     float num = 0.f;
-    for (int i = 0; i < P; ++i) num += exp2f(part_ml[(base + i) * 2] - Ms) * part_o[(base + i) * DH + d];
-    out[((long)b * Hq + hq) * DH + d] = (bf16)(den > 0.f ? num / den : 0.f);
+    for (int j0 = 0; j0 < np; j0 += 8) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = po[(long)min(j0 + j, np - 1) * DH];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (j0 + j < np) num += wts[(j0 + j) * G + h] * v[j];
+    }
+    out[((long)b * Hq + kvh * G + h) * DH + d] = (bf16)(num * wts[np * G + h]);
   }
 }
 
@@ -362,27 +412,36 @@ __global__ __launch_bounds__(PF_T) void attn_prefill_kernel(
 // C ABI ------------------------------------------------------------------------------------
 extern "C" int la_attn_decode(const void* q, const void* kc, const void* vc, const int* block_tables, int max_blocks,
                               const int* seq_lens, int B, int Hq, int Hkv, int Dh, int BS, float scale, int P, int PS,
-                              void* out, void* part_o, void* part_ml, void* stream) {
-  if (Hq % Hkv || Hq / Hkv > 16 || (BS % 16) || (PS % 128) || P < 1) return -1;
+                              void* out, void* part_o, void* part_ml, void* tickets, void* stream) {
+  if (Hq % Hkv || Hq / Hkv > 16 || (BS % 16) || (128 % BS && BS % 128) || (PS % 128) || P < 1 ||
+      PS / BS > la::DEC_MAXBT || P > 64 || (P > 1 && !tickets))
+    return -1;
   const int G = Hq / Hkv;
   hipStream_t st = (hipStream_t)stream;
   dim3 grid(P, Hkv, B);
   float* po = (float*)part_o;
   float* pml = (float*)part_ml;
+  int* tk = (int*)tickets;
   const float sl2 = scale * 1.4426950408889634f;
-#define DEC(D)                                                                                                     \
-  hipLaunchKernelGGL(la::attn_decode_kernel<D>, grid, dim3(la::DEC_T), 0, st, (const bf16*)q, (const bf16*)kc,     \
-                     (const bf16*)vc, block_tables, max_blocks, seq_lens, Hkv, G, BS, sl2, PS, (bf16*)out, po, pml, P)
+#define DEC(D, GT)                                                                                                 \
+  hipLaunchKernelGGL((la::attn_decode_kernel<D, GT>), grid, dim3(la::DEC_T), 0, st, (const bf16*)q,              \
+                     (const bf16*)kc, (const bf16*)vc, block_tables, max_blocks, seq_lens, Hkv, G, BS, sl2, PS,  \
+                     (bf16*)out, po, pml, P, tk)
+#define DEC_G(D)                          \
+  if (G == 1) DEC(D, 1);                  \
+  else if (G == 2) DEC(D, 2);             \
+  else if (G <= 4) DEC(D, 4);             \
+  else if (G <= 8) DEC(D, 8);             \
+  else DEC(D, 16);
   switch (Dh) {
-    case 64: DEC(64); break;
-    case 80: DEC(80); break;
-    case 96: DEC(96); break;
-    case 128: DEC(128); break;
+    case 64: DEC_G(64); break;
+    case 80: DEC_G(80); break;
+    case 96: DEC_G(96); break;
+    case 128: DEC_G(128); break;
     default: return -2;
   }
+#undef DEC_G
 #undef DEC
-  if (P > 1)
-    hipLaunchKernelGGL(la::attn_decode_combine_kernel, dim3(Hq, B), dim3(128), 0, st, po, pml, P, Dh, (bf16*)out);
   return (int)hipGetLastError();
 }
 

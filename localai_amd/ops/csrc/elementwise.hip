@@ -17,16 +17,41 @@ struct Src {
   const float* bias;  // optional per-column bias (length = row width), may be null
 };
 
+// Sum of up to SMAX slabs with every load issued before the first add: the slab index is
+// clamped (duplicate loads hit L2) and masked, never branched on, so hipcc keeps all the
+// loads in flight instead of waiting vmcnt(0) per slab (guide §5 trap (c)).
+template <int SMAX>
+LA_DEV float4 sum_slabs(const float* f, long slab, int S) {
+  float4 b[SMAX];
+#pragma unroll
+  for (int i = 0; i < SMAX; ++i) b[i] = *(const float4*)(f + (long)min(i, S - 1) * slab);
+  float4 a = b[0];
+#pragma unroll
+  for (int i = 1; i < SMAX; ++i) {
+    const float m = (i < S) ? 1.f : 0.f;
+    a.x = fmaf(m, b[i].x, a.x); a.y = fmaf(m, b[i].y, a.y);
+    a.z = fmaf(m, b[i].z, a.z); a.w = fmaf(m, b[i].w, a.w);
+  }
+  return a;
+}
+
 LA_DEV void load4(const Src& s, long idx, int col, float v[4]) {
   if (s.S == 0) {
     const bf16x4 b = *(const bf16x4*)((const bf16*)s.p + idx);
     v[0] = (float)b[0]; v[1] = (float)b[1]; v[2] = (float)b[2]; v[3] = (float)b[3];
   } else {
     const float* f = (const float*)s.p + idx;
-    float4 a = *(const float4*)f;
-    for (int i = 1; i < s.S; ++i) {
-      const float4 b = *(const float4*)(f + (long)i * s.slab);
-      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    float4 a;
+    if (s.S == 1) a = *(const float4*)f;
+    else if (s.S <= 2) a = sum_slabs<2>(f, s.slab, s.S);
+    else if (s.S <= 4) a = sum_slabs<4>(f, s.slab, s.S);
+    else if (s.S <= 8) a = sum_slabs<8>(f, s.slab, s.S);
+    else {
+      a = sum_slabs<8>(f, s.slab, min(s.S, 8));
+      for (int i0 = 8; i0 < s.S; i0 += 8) {
+        const float4 c = sum_slabs<8>(f + (long)i0 * s.slab, s.slab, min(s.S - i0, 8));
+        a.x += c.x; a.y += c.y; a.z += c.z; a.w += c.w;
+      }
     }
     v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
   }
@@ -42,6 +67,9 @@ LA_DEV void load4(const Src& s, long idx, int col, float v[4]) {
 constexpr int NORM_T = 256;
 constexpr int NORM_MAXV = 8;  // float4 per thread => D <= 8192
 
+// IT = ceil(D/4 / NORM_T) float4 chunks per thread, a compile-time count so every load of
+// the row (and of all its split-K slabs) is issued before the first use.
+template <int IT>
 __global__ __launch_bounds__(NORM_T) void add_norm_kernel(float* __restrict__ residual, Src add, int has_add,
                                                           const float* __restrict__ w, const float* __restrict__ b,
                                                           bf16* __restrict__ out, int D, float eps, int mode,
@@ -50,20 +78,24 @@ __global__ __launch_bounds__(NORM_T) void add_norm_kernel(float* __restrict__ re
   const int t = blockIdx.x;
   const int nv = D >> 2;
   float* rrow = residual + (long)t * D;
-  float v[NORM_MAXV][4];
+  float v[IT][4];
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int c = min(threadIdx.x + i * NORM_T, nv - 1);  // clamped: loads never branch
+    const float4 r = *(const float4*)(rrow + 4 * c);
+    v[i][0] = r.x; v[i][1] = r.y; v[i][2] = r.z; v[i][3] = r.w;
+    if (has_add) {
+      float a[4];
+      load4(add, (long)t * D + 4 * c, 4 * c, a);
+      v[i][0] += a[0]; v[i][1] += a[1]; v[i][2] += a[2]; v[i][3] += a[3];
+    }
+  }
   float s1 = 0.f;
 #pragma unroll
-  for (int i = 0; i < NORM_MAXV; ++i) {
+  for (int i = 0; i < IT; ++i) {
     const int c = threadIdx.x + i * NORM_T;
     if (c < nv) {
-      float4 r = *(const float4*)(rrow + 4 * c);
-      v[i][0] = r.x; v[i][1] = r.y; v[i][2] = r.z; v[i][3] = r.w;
-      if (has_add) {
-        float a[4];
-        load4(add, (long)t * D + 4 * c, 4 * c, a);
-        v[i][0] += a[0]; v[i][1] += a[1]; v[i][2] += a[2]; v[i][3] += a[3];
-        *(float4*)(rrow + 4 * c) = make_float4(v[i][0], v[i][1], v[i][2], v[i][3]);
-      }
+      if (has_add) *(float4*)(rrow + 4 * c) = make_float4(v[i][0], v[i][1], v[i][2], v[i][3]);
       s1 += (mode == 0) ? (v[i][0] * v[i][0] + v[i][1] * v[i][1] + v[i][2] * v[i][2] + v[i][3] * v[i][3])
                         : (v[i][0] + v[i][1] + v[i][2] + v[i][3]);
     }
@@ -76,7 +108,7 @@ __global__ __launch_bounds__(NORM_T) void add_norm_kernel(float* __restrict__ re
     mean = block_sum<NORM_T>(s1, red) / (float)D;
     float s2 = 0.f;
 #pragma unroll
-    for (int i = 0; i < NORM_MAXV; ++i) {
+    for (int i = 0; i < IT; ++i) {
       const int c = threadIdx.x + i * NORM_T;
       if (c < nv) {
 #pragma unroll
@@ -87,7 +119,7 @@ __global__ __launch_bounds__(NORM_T) void add_norm_kernel(float* __restrict__ re
   }
   if (!out) return;
 #pragma unroll
-  for (int i = 0; i < NORM_MAXV; ++i) {
+  for (int i = 0; i < IT; ++i) {
     const int c = threadIdx.x + i * NORM_T;
     if (c < nv) {
       const float4 ww = *(const float4*)(w + 4 * c);
@@ -121,7 +153,9 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(Src qkv, const int* __rest
   const float* cs = cos_sin + (long)p * rot;  // rot/2 pairs x (cos, sin)
   // work unit = 4 consecutive elements of one head (Dh % 4 == 0)
   const int units = W >> 2;
-  for (int u = threadIdx.x; u < units; u += blockDim.x) {
+  // one thread per 4-element unit; grid.y spreads a row over several workgroups so a
+  // single decode token still fills more than one CU
+  for (int u = blockIdx.y * blockDim.x + threadIdx.x; u < units; u += blockDim.x * gridDim.y) {
     const int col = u * 4;
     const int head = col / Dh, d0 = col - head * Dh;
     float v[4];
@@ -265,8 +299,19 @@ extern "C" int la_add_norm(void* residual, const void* add_p, long add_slab, int
                            int mode, void* out_f32, void* stream) {
   if ((D & 3) || D > la::NORM_T * la::NORM_MAXV * 4) return -1;
   Src s{add_p, add_slab, add_S, (const float*)add_bias};
-  hipLaunchKernelGGL(la::add_norm_kernel, dim3(T), dim3(la::NORM_T), 0, (hipStream_t)stream, (float*)residual, s,
-                     has_add, (const float*)w, (const float*)b, (bf16*)out, D, eps, mode, (float*)out_f32);
+  const int it = (D / 4 + la::NORM_T - 1) / la::NORM_T;
+#define LA_NORM_CASE(I)                                                                                     \
+  case I:                                                                                                   \
+    hipLaunchKernelGGL(la::add_norm_kernel<I>, dim3(T), dim3(la::NORM_T), 0, (hipStream_t)stream,          \
+                       (float*)residual, s, has_add, (const float*)w, (const float*)b, (bf16*)out, D, eps,  \
+                       mode, (float*)out_f32);                                                            \
+    break;
+  switch (it) {
+    LA_NORM_CASE(1) LA_NORM_CASE(2) LA_NORM_CASE(3) LA_NORM_CASE(4)
+    LA_NORM_CASE(5) LA_NORM_CASE(6) LA_NORM_CASE(7) LA_NORM_CASE(8)
+    default: return -1;
+  }
+#undef LA_NORM_CASE
   return (int)hipGetLastError();
 }
 
@@ -275,7 +320,9 @@ extern "C" int la_rope_kv(const void* qkv_p, long slab, int S, const void* bias,
                           void* kc, void* vc, int BS, void* stream) {
   if ((Dh & 3) || (rot & 3) || rot > Dh) return -1;
   Src s{qkv_p, slab, S, (const float*)bias};
-  hipLaunchKernelGGL(la::rope_kv_kernel, dim3(T), dim3(256), 0, (hipStream_t)stream, s, pos, slots, cos_sin, Hq,
+  const int units = (Hq + 2 * Hkv) * Dh / 4;
+  hipLaunchKernelGGL(la::rope_kv_kernel, dim3(T, (units + 255) / 256), dim3(256), 0, (hipStream_t)stream, s, pos,
+                     slots, cos_sin, Hq,
                      Hkv, Dh, rot, mode, (bf16*)q_out, (bf16*)kc, (bf16*)vc, BS);
   return (int)hipGetLastError();
 }
