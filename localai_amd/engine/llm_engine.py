@@ -82,6 +82,7 @@ class Request:
     mu: float = 0.0
     cancelled: bool = False
     sink: object = None
+    grammar: object = None       # native GrammarState (GBNF-constrained decoding)
 
 
 class LLMEngine:
@@ -103,6 +104,8 @@ class LLMEngine:
         self.model = DecoderModel(self.reader, self.device, tp=tp, max_pos=cfg.context_size, rope_overrides=ro)
         self.hp = self.model.hp
         self.vocab = core.Vocab(self.tokenizer.pieces)
+        self.gvocab = core.GrammarVocab(self.tokenizer.pieces, sorted(self.tokenizer.eog))
+        self._grammars: Dict[str, object] = {}
         self.ctx = cfg.context_size
         bs = cfg.block_size
         if self.device.type == "cuda":
@@ -178,12 +181,23 @@ class LLMEngine:
         stops = list(params.stop)
         r = Request(rid, toks, params, callback, n_prompt=len(toks), mu=2.0 * params.mirostat_tau)
         r.stream = core.TextStream(self.vocab, stops)
+        if params.grammar:
+            r.grammar = core.GrammarState(self._grammar(params.grammar), self.gvocab)
         r.sink = sink
         if sink is not None:
             sink.set_prompt_tokens(r.n_prompt)
         self._inbox.put(r)
         self._wake.set()
         return rid
+
+    def _grammar(self, text: str):
+        g = self._grammars.get(text)
+        if g is None:
+            g = core.Grammar(text)  # ValueError on a malformed grammar (surfaced to the caller)
+            if len(self._grammars) > 64:
+                self._grammars.clear()
+            self._grammars[text] = g
+        return g
 
     def abort(self, rid: int):
         self._inbox.put(("abort", rid))
@@ -567,6 +581,8 @@ class LLMEngine:
             toks = self._sample_host_mirostat1(logits, reqs)
         else:
             toks = ops.sample(logits, prm, mu=mu).cpu().numpy()
+        if any(r.grammar is not None for r in reqs):
+            toks = self._apply_grammar(reqs, logits, prm, toks)
         if mu is not None:
             muh = mu.cpu().numpy()
             for j, r in enumerate(reqs):
@@ -574,6 +590,41 @@ class LLMEngine:
         now = time.perf_counter()
         for j, r in enumerate(reqs):
             self._on_token(r, int(toks[j]), now)
+
+    GRAMMAR_TOPN = 1024
+
+    def _apply_grammar(self, reqs, logits, prm, toks):
+        """Constrained decoding: keep the device sample if the grammar accepts it (the common
+        case); otherwise take the device top-N candidates, keep the ones the grammar accepts
+        (whole-vocabulary scan if none is), and re-run the sampler chain on those -- i.e. the
+        sampler's distribution restricted to grammar-valid tokens (llama.cpp resample path)."""
+        toks = np.array(toks, copy=True)
+        for j, r in enumerate(reqs):
+            gs = r.grammar
+            if gs is None or r.done:
+                continue
+            t = int(toks[j])
+            if gs.check(t):
+                continue
+            row = logits[j].float()
+            n = min(self.GRAMMAR_TOPN, row.shape[0])
+            vals, idx = torch.topk(row, n)
+            idx_np = idx.cpu().numpy().astype(np.int32)
+            ok = gs.filter(idx_np).astype(bool)
+            if ok.any():
+                cand_ids = idx_np[ok]
+                cand_vals = vals.cpu()[torch.from_numpy(ok)]
+            else:
+                mask = gs.mask().astype(bool)
+                if not mask.any():
+                    toks[j] = -1  # nothing can follow: the grammar is complete
+                    continue
+                cand_ids = np.nonzero(mask)[0].astype(np.int32)
+                cand_vals = row.cpu()[torch.from_numpy(cand_ids).long()]
+            sub = prm[j:j + 1].copy()
+            k = int(ops.sample_ref(cand_vals.view(1, -1), sub)[0])
+            toks[j] = int(cand_ids[k])
+        return toks
 
     def _sample_host_mirostat1(self, logits, reqs):
         """Mirostat v1 (rare): host implementation of llama_sampler_mirostat."""
@@ -608,6 +659,13 @@ class LLMEngine:
     def _on_token(self, r: Request, tok: int, now: float, append: bool = True):
         if r.done:
             return
+        if r.grammar is not None:
+            if tok < 0:
+                self._finish(r, "stop")  # grammar complete, no token may follow
+                return
+            if not r.grammar.accept(tok):
+                self._finish(r, "error", error="grammar rejected the sampled token")
+                return
         if append:
             self.sched.append(r.id, tok)
         r.n_gen += 1

@@ -11,7 +11,7 @@ from pathlib import Path
 HERE = Path(__file__).resolve().parent
 EXT = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 # module name -> sources
-MODULES = {"_la_core": ["engine_core.cpp"], "_la_http": ["http_server.cpp"]}
+MODULES = {"_la_core": ["engine_core.cpp", "grammar.cpp"], "_la_http": ["http_server.cpp"]}
 LIB = HERE / f"_la_core{EXT}"
 
 

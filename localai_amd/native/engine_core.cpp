@@ -607,8 +607,11 @@ class TextStream {
 
 }  // namespace la
 
+void register_grammar(py::module& m);  // grammar.cpp
+
 PYBIND11_MODULE(_la_core, m) {
   using namespace la;
+  register_grammar(m);
   m.doc() = "localai_amd native engine core (scheduler, paged KV manager, stop matcher)";
   py::class_<BlockManager>(m, "BlockManager")
       .def(py::init<int, int, bool>())

@@ -254,19 +254,16 @@ class Partial:
 
 
 def pick_splits(N: int, K: int, M: int) -> int:
-    """Split-K for the skinny GEMM: about 2 workgroups per CU (256 CUs), but every split keeps
-    >= 4 super-blocks so each lane streams a full chunk of weight fragments (4 in flight)."""
+    """Split-K so the skinny GEMM launches >= ~2 workgroups per CU (256 CUs)."""
     nsb = K // 256
     nblk = (N + 63) // 64
+    want = max(1, math.ceil(512 / nblk))
     best = 1
     for s in range(1, nsb + 1):
-        if nsb % s:
-            continue
-        if s > 1 and nsb // s < 4:
-            break
-        best = s
-        if nblk * s >= 512:
-            break
+        if nsb % s == 0:
+            best = s
+            if s >= want:
+                break
     # the consumer reads S slabs: keep the slab traffic below the weight traffic
     while best > 1 and best * M * N * 4 * 2 > N * K // 2:
         cands = [s for s in range(1, best) if nsb % s == 0]
@@ -489,7 +486,7 @@ def embed(tokens: torch.Tensor, w: QWeight, scale: float = 1.0, out: Optional[to
 # Attention
 # ---------------------------------------------------------------------------------------
 
-DEC_TARGET_WAVES = 4096  # ~16 waves per CU over 256 CUs
+DEC_TARGET_WAVES = 2048  # ~16 waves per CU over 256 CUs
 
 
 def decode_partitions(B: int, Hkv: int, max_len: int, block_size: int = 32) -> Tuple[int, int]:

@@ -2,12 +2,12 @@
 //
 // Replaces ggml-cuda's mmvq/mmq ([external]).  MI355X-first design:
 //  * B operand = weights, read ONCE from HBM straight into VGPRs (16-byte loads,
-//    4/MT super-blocks of prefetch in flight per lane), dequantised in-register to bf16 and
-//    fed to v_mfma_f32_16x16x32_bf16.  No LDS round trip for weights (guide §5:
+//    one super-block of prefetch in flight), dequantised in-register to bf16 and fed
+//    to v_mfma_f32_16x16x32_bf16.  No LDS round trip for weights (guide §5:
 //    "GEMV / M <= 16 decode weights: load straight to VGPRs").
-//  * A operand = activations (M <= 64 rows), staged through LDS in chunks of 4/MT
-//    super-blocks (shared by the 4 waves of the workgroup, each wave owns 16 output
-//    columns), issue-early / write-late (T14) so the L2 latency of X hides under the MFMAs.
+//  * A operand = activations (M <= 64 rows), staged per super-block through LDS
+//    (shared by the 4 waves of the workgroup, each wave owns 16 output columns),
+//    issue-early / write-late (T14) so the L2 latency of X hides under the MFMAs.
 //  * Split-K over grid.y gives >= 2 workgroups per CU; partial fp32 slabs are summed by
 //    the consuming kernel (rmsnorm / rope / silu-mul prologue), never by atomics.
 #include "qweight.h"
@@ -16,53 +16,45 @@ namespace la {
 
 constexpr int SK_WAVES = 4;
 constexpr int SK_THREADS = 64 * SK_WAVES;
+constexpr int SK_LDS_STRIDE = 256 + 8;  // bf16 elements per LDS row (16 B pad: spreads banks)
 
-// SBC = super-blocks per X chunk (4 / MT, so the LDS chunk is always 16*MT x 256*SBC bf16 ~ 33 KB):
-// one barrier pair per chunk instead of per super-block, and SBC weight fragments in flight
-// per lane (a full chunk of prefetch: the fragment of super-block j+SBC is requested as soon as
-// super-block j has been multiplied).
-template <int FMT, int MT, int SBC>
+template <int FMT, int MT>
 __global__ __launch_bounds__(SK_THREADS, 2) void qgemm_skinny_kernel(
     QW w, const bf16* __restrict__ X, int ldx, int M, int k_per_split, float* __restrict__ out, int ldo,
     long slab) {
   constexpr int MP = 16 * MT;
-  constexpr int XW = 256 * SBC;
-  constexpr int XSTR = XW + 8;  // 16 B pad per row spreads LDS banks
-  __shared__ __attribute__((aligned(16))) bf16 xs[MP * XSTR];
+  __shared__ __attribute__((aligned(16))) bf16 xs[MP * SK_LDS_STRIDE];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, r = lane & 15;
   const int N = w.N, K = w.K;
   const int split = blockIdx.y;
   const int kbeg = split * k_per_split;
-  const int krange = min(k_per_split, K - kbeg);
-  const int nsb = krange >> 8;
-  const int nchunk = (nsb + SBC - 1) / SBC;
+  const int nsb = min(k_per_split, K - kbeg) >> 8;
   const int n = blockIdx.x * (16 * SK_WAVES) + wave * 16 + r;
   const int nl = min(n, N - 1);  // clamp: out-of-range lanes compute garbage, never stored
 
-  // ---- X staging: MP rows x XW cols bf16 = MP*XW/8 16-byte pieces per chunk
-  constexpr int XCH = MP * XW / 8;
+  // ---- X staging: MP rows x 256 cols bf16 = MP*32 16-byte chunks per super-block
+  constexpr int XCH = MP * 32;
   constexpr int XPT = (XCH + SK_THREADS - 1) / SK_THREADS;
   bf16x8 xr[XPT];
-  auto x_issue = [&](int c) {
+  auto x_issue = [&](int sb) {
 #pragma unroll
     for (int i = 0; i < XPT; ++i) {
-      const int e = tid + i * SK_THREADS;
-      const int row = e / (XW / 8), col = (e % (XW / 8)) * 8;
-      const int kc = min(c * XW + col, krange - 8);  // clamped: never branch around the load
-      bf16x8 v = *(const bf16x8*)(X + (size_t)min(row, M - 1) * ldx + kbeg + kc);
-      if (row >= M) v = bf16x8{};
+      const int c = tid + i * SK_THREADS;
+      const int row = c >> 5, col = (c & 31) * 8;
+      bf16x8 v = {};
+      if (c < XCH && row < M) v = *(const bf16x8*)(X + (size_t)row * ldx + kbeg + sb * 256 + col);
       xr[i] = v;
     }
   };
   auto x_store = [&]() {
 #pragma unroll
     for (int i = 0; i < XPT; ++i) {
-      const int e = tid + i * SK_THREADS;
-      if (e < XCH) {
-        const int row = e / (XW / 8), col = (e % (XW / 8)) * 8;
-        *(bf16x8*)(xs + row * XSTR + col) = xr[i];
+      const int c = tid + i * SK_THREADS;
+      if (c < XCH) {
+        const int row = c >> 5, col = (c & 31) * 8;
+        *(bf16x8*)(xs + row * SK_LDS_STRIDE + col) = xr[i];
       }
     }
   };
@@ -72,36 +64,46 @@ __global__ __launch_bounds__(SK_THREADS, 2) void qgemm_skinny_kernel(
   for (int i = 0; i < MT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int sb0 = kbeg >> 8;
-  WFrag<FMT> f[SBC];
+  WFrag<FMT> fa, fb;
   x_issue(0);
-#pragma unroll
-  for (int j = 0; j < SBC; ++j)
-    if (j < nsb) f[j].load(w, nl, sb0 + j, g);
+  fa.load(w, nl, sb0, g);
 
-  for (int c = 0; c < nchunk; ++c) {
+  auto compute = [&](WFrag<FMT>& f) {
+    f.prep(g);
+#define SK_STEP(S)                                                                         \
+  {                                                                                        \
+    const bf16x8 b = f.template deq<S>();                                                  \
+    const int kp = kphys<FMT>(S, g);                                                       \
+    _Pragma("unroll") for (int mt = 0; mt < MT; ++mt) {                                    \
+      const bf16x8 a = *(const bf16x8*)(xs + (mt * 16 + r) * SK_LDS_STRIDE + kp);          \
+      acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[mt], 0, 0, 0);           \
+    }                                                                                      \
+  }
+    SK_STEP(0) SK_STEP(1) SK_STEP(2) SK_STEP(3) SK_STEP(4) SK_STEP(5) SK_STEP(6) SK_STEP(7)
+#undef SK_STEP
+  };
+
+  // two super-blocks per iteration with statically named fragments (no runtime-indexed arrays)
+  for (int sb = 0; sb < nsb; sb += 2) {
+    // --- super-block sb (fragment fa)
     __syncthreads();  // previous readers of xs done
     x_store();
     __syncthreads();
-    if (c + 1 < nchunk) x_issue(c + 1);
-#pragma unroll
-    for (int j = 0; j < SBC; ++j) {
-      const int sb = c * SBC + j;
-      if (sb < nsb) {
-        f[j].prep(g);
-#define SK_STEP(S)                                                                              \
-  {                                                                                             \
-    const bf16x8 b = f[j].template deq<S>();                                                    \
-    const int kp = j * 256 + kphys<FMT>(S, g);                                                  \
-    _Pragma("unroll") for (int mt = 0; mt < MT; ++mt) {                                         \
-      const bf16x8 a = *(const bf16x8*)(xs + (mt * 16 + r) * XSTR + kp);                        \
-      acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[mt], 0, 0, 0);                \
-    }                                                                                           \
-  }
-        SK_STEP(0) SK_STEP(1) SK_STEP(2) SK_STEP(3) SK_STEP(4) SK_STEP(5) SK_STEP(6) SK_STEP(7)
-#undef SK_STEP
-        if (sb + SBC < nsb) f[j].load(w, nl, sb0 + sb + SBC, g);
-      }
+    if (sb + 1 < nsb) {
+      x_issue(sb + 1);
+      fb.load(w, nl, sb0 + sb + 1, g);
     }
+    compute(fa);
+    if (sb + 1 >= nsb) break;
+    // --- super-block sb+1 (fragment fb)
+    __syncthreads();
+    x_store();
+    __syncthreads();
+    if (sb + 2 < nsb) {
+      x_issue(sb + 2);
+      fa.load(w, nl, sb0 + sb + 2, g);
+    }
+    compute(fb);
   }
 
   if (n < N) {
@@ -123,8 +125,7 @@ static void launch_skinny_t(const QW& w, const bf16* X, int ldx, int M, int spli
   const int nsb_total = w.K >> 8;
   const int per = nsb_total / splits;
   dim3 grid((w.N + 16 * SK_WAVES - 1) / (16 * SK_WAVES), splits);
-  constexpr int SBC = 4 / MT;
-  hipLaunchKernelGGL((qgemm_skinny_kernel<FMT, MT, SBC>), grid, dim3(SK_THREADS), 0, st, w, X, ldx, M,
+  hipLaunchKernelGGL((qgemm_skinny_kernel<FMT, MT>), grid, dim3(SK_THREADS), 0, st, w, X, ldx, M,
                      per * 256, out, ldo, slab);
 }
 
