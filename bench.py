@@ -33,7 +33,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--concurrency", type=int, default=int(os.environ.get("BENCH_CONCURRENCY", 64)))
+    ap.add_argument("--concurrency", type=int, default=int(os.environ.get("BENCH_CONCURRENCY", 256)))
     ap.add_argument("--prompt-len", type=int, default=128)
     ap.add_argument("--max-tokens", type=int, default=256)
     ap.add_argument("--preset", default=os.environ.get("BENCH_PRESET", "llama3-8b"))
