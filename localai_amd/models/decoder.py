@@ -99,6 +99,8 @@ class Layer:
     down_bias: Optional[torch.Tensor]
     router: Optional[torch.Tensor] = None            # [E, D] f32 (MoE)
     experts: Optional[List[tuple]] = None            # [(gate_up list, down)] per expert
+    moe_gu: Optional[object] = None                  # ops.MoEWeights (fused gate|up of every expert)
+    moe_down: Optional[object] = None                # ops.MoEWeights
 
 
 def _raw2d(t, rows: Optional[slice] = None, cols: Optional[slice] = None):
@@ -191,8 +193,7 @@ class DecoderModel:
             router = experts = None
             gate_up, down, up_b, down_b = [], None, None, None
             if hp.n_expert:
-                router = torch.from_numpy(np.frombuffer(T[b + "ffn_gate_inp.weight"].data, dtype=np.float32)
-                                          .reshape(hp.n_expert, hp.n_embd).copy()).to(dev)
+                router = f32(b + "ffn_gate_inp.weight").view(hp.n_expert, hp.n_embd)
                 experts = []
                 for e in range(hp.n_expert):
                     ge = self._expert_slice(T[b + "ffn_gate_exps.weight"], e, rows=fs)
@@ -212,12 +213,19 @@ class DecoderModel:
                 gu = ops.concat_rows([g, u])
                 gate_up = [gu] if gu is not None else [g, u]
                 down = qw(b + "ffn_down.weight", cols=fs)
+            moe_gu = moe_down = None
+            if experts and all(len(gu) == 1 for gu, _ in experts):
+                try:
+                    moe_gu = ops.MoEWeights([gu[0] for gu, _ in experts])
+                    moe_down = ops.MoEWeights([d for _, d in experts])
+                except ValueError:
+                    moe_gu = moe_down = None
             self.layers.append(Layer(
                 attn_norm=f32(b + "attn_norm.weight"), attn_norm_b=f32(b + "attn_norm.bias"),
                 qkv=qkv, qkv_bias=qkv_bias, wo=wo, wo_bias=wo_b,
                 ffn_norm=f32(b + "ffn_norm.weight"), ffn_norm_b=f32(b + "ffn_norm.bias"),
                 gate_up=gate_up, up_bias=up_b, down=down, down_bias=down_b,
-                router=router, experts=experts))
+                router=router, experts=experts, moe_gu=moe_gu, moe_down=moe_down))
         self.out_norm = f32("output_norm.weight")
         self.out_norm_b = f32("output_norm.bias")
         vs = sl(hp.n_vocab)
@@ -276,6 +284,16 @@ class DecoderModel:
         logits = xn.float() @ L.router.t()                       # [T, E]
         w, idx = torch.topk(torch.softmax(logits, -1), hp.n_expert_used, -1)
         w = w / w.sum(-1, keepdim=True)
+        if L.moe_gu is not None and T <= 64 and xn.is_cuda:
+            # graph-capturable grouped path: device routing, one weight stream per active expert,
+            # routing-weighted outputs land as extra slabs summed by the next kernel
+            k = hp.n_expert_used
+            order, off = ops.moe_route(idx.to(torch.int32), hp.n_expert)
+            gu = ops.moe_linear(xn, L.moe_gu, order, off, k, T)
+            h = ops.act(gu, self.F, ops.ACT_SWIGLU)
+            d = ops.moe_linear(h, L.moe_down, order, off, k, T, down=True,
+                               wts=w.reshape(-1).float().contiguous())
+            return self._row_parallel_out(d, None)
         out = torch.zeros(T, hp.n_embd, dtype=torch.float32, device=xn.device)
         flat_e = idx.reshape(-1)
         flat_t = torch.arange(T, device=xn.device).repeat_interleave(hp.n_expert_used)

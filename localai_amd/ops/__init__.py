@@ -56,6 +56,9 @@ def lib():
             "la_penalties": [P, LNG, I, P, I, P, P, I, P, P],
             "la_sample_row_bytes": [],
             "la_logit_bias": [P, LNG, P, P, P, P, I, P],
+            "la_moe_route": [P, I, I, I, P, P, P],
+            "la_moe_gemm": [I, I, P, I, I, I, P, P, I, P, I, I, I, P, P, I, LNG, I, P],
+            "la_qw_size": [],
             "la_decode_advance": [P, P, P, P, P, P, I, I, I, P, I, P, P, P],
         }
         for name, args in sig.items():
@@ -723,6 +726,92 @@ def decode_advance(next_tok, tok, pos, lens, slots, bt, block_size: int, hist, s
                                    slots.data_ptr(), bt.data_ptr(), bt.stride(0), block_size, B, hist.data_ptr(),
                                    hist.shape[0], step.data_ptr(), prm_dev.data_ptr(), _stream()),
            "la_decode_advance")
+
+
+# ---------------------------------------------------------------------------------------
+# Mixture of experts (decode-sized batches; csrc/moe.hip)
+# ---------------------------------------------------------------------------------------
+
+class MoEWeights:
+    """E experts of one projection (same format / shape) + their QW descriptors on the device."""
+
+    def __init__(self, experts: Sequence[QWeight]):
+        if not experts or len({(w.fmt, w.N, w.K) for w in experts}) != 1:
+            raise ValueError("MoEWeights: experts must share format and shape")
+        self.experts = list(experts)
+        self.E, self.N, self.K, self.fmt = len(experts), experts[0].N, experts[0].K, experts[0].fmt
+        self.desc = None
+        p0 = experts[0].planes[0]
+        if p0 is not None and p0.device.type == "cuda":
+            dev = p0.device
+            qw = np.zeros(self.E, dtype=[("p", "<u8", 4), ("N", "<i4"), ("K", "<i4")])
+            assert qw.dtype.itemsize == lib().la_qw_size()
+            for e, w in enumerate(experts):
+                qw[e]["p"] = [_ptr(p) or 0 for p in w.planes]
+                qw[e]["N"], qw[e]["K"] = w.N, w.K
+            self.desc = torch.from_numpy(qw.view(np.uint8).copy()).to(dev)
+
+
+def moe_route(ids: torch.Tensor, E: int, order: Optional[torch.Tensor] = None, off: Optional[torch.Tensor] = None):
+    """ids [T, topk] int32 -> (order [T*topk] pair ids grouped by expert, off [E+1])."""
+    T, topk = ids.shape
+    if order is None:
+        order = torch.empty(T * topk, dtype=torch.int32, device=ids.device)
+    if off is None:
+        off = torch.empty(E + 1, dtype=torch.int32, device=ids.device)
+    if not ids.is_cuda:
+        flat = ids.reshape(-1).long()
+        perm = torch.sort(flat, stable=True).indices
+        order.copy_(perm.to(torch.int32))
+        cnt = torch.bincount(flat, minlength=E)
+        off.copy_(torch.cat([torch.zeros(1, dtype=torch.long), cnt.cumsum(0)]).to(torch.int32))
+        return order, off
+    ids = ids.contiguous().to(torch.int32)
+    _check(lib().la_moe_route(ids.data_ptr(), T, topk, E, order.data_ptr(), off.data_ptr(), _stream()), "la_moe_route")
+    return order, off
+
+
+def moe_linear(x: torch.Tensor, mw: MoEWeights, order: torch.Tensor, off: torch.Tensor, topk: int, T: int,
+               down: bool = False, wts: Optional[torch.Tensor] = None) -> Partial:
+    """Grouped expert GEMM.  gate/up (down=False): x [T, K] -> Partial [S, T*topk, N] (row = pair).
+    down (down=True): x [T*topk, K] (row = pair) -> Partial [S*topk, T, N], each slab scaled by
+    the routing weight, so summing the slabs performs the weighted top-k combine."""
+    if not x.is_cuda:
+        P = T * topk
+        flat_e = torch.empty(P, dtype=torch.long)
+        offs = off.tolist()
+        for e in range(mw.E):
+            flat_e[order[offs[e]:offs[e + 1]].long()] = e
+        if down:
+            out = torch.zeros(topk, T, mw.N)
+            for p in range(P):
+                t, slot = divmod(p, topk)
+                out[slot, t] = (x[p].float() @ mw.experts[int(flat_e[p])].dequant_f32().t()) * float(wts[p])
+        else:
+            out = torch.zeros(1, P, mw.N)
+            for p in range(P):
+                out[0, p] = x[p // topk].float() @ mw.experts[int(flat_e[p])].dequant_f32().t()
+        return Partial(out)
+    if x.dtype != torch.bfloat16 or not x.is_contiguous():
+        raise ValueError("moe_linear: x must be contiguous bf16")
+    maxM = T  # a token picks an expert at most once
+    if maxM > 64:
+        raise ValueError("moe_linear: grouped decode path supports T <= 64")
+    S = pick_splits(mw.N, mw.K, maxM)
+    nsb = mw.K // 256
+    while nsb % S:
+        S -= 1
+    P = T * topk
+    if down:
+        out = torch.empty(S * topk, T, mw.N, dtype=torch.float32, device=x.device)
+        slab = T * mw.N
+    else:
+        out = torch.empty(S, P, mw.N, dtype=torch.float32, device=x.device)
+        slab = P * mw.N
+    _check(lib().la_moe_gemm(mw.fmt, 1 if down else 0, mw.desc.data_ptr(), mw.N, mw.K, mw.E, order.data_ptr(),
+                             off.data_ptr(), topk, x.data_ptr(), x.shape[1], maxM, S,
+                             _ptr(wts) if down else None, out.data_ptr(), mw.N, slab, T, _stream()), "la_moe_gemm")
+    return Partial(out)
 
 
 def penalties(logits: torch.Tensor, hist: torch.Tensor, hist_len: torch.Tensor, pen: torch.Tensor,

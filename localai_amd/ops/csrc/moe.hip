@@ -1,0 +1,199 @@
+// Mixture-of-experts for decode-sized batches (ggml MUL_MAT_ID [external]),
+// graph-capturable: routing, grouping and the expert GEMMs never leave the device.
+//
+//  moe_route   : one workgroup; from top-k expert ids [T][topk] build a pair list grouped by expert
+//                (order[], off[E+1]; pair p = t*topk + slot), deterministic (stable by pair id).
+//  grouped GEMM: the skinny quantised GEMM with blockIdx.z = expert.  The expert's QW descriptor
+//                comes from a device array; its rows are gathered through order[] (so each expert's
+//                weights stream from HBM once per step however many tokens picked it).  Two output
+//                modes:
+//                  GATE_UP: out[split][pair][n]                      (X row = token of the pair)
+//                  DOWN   : out[split*topk + slot][token][n] * w[pair]  (X row = pair)
+//                DOWN writes the routing-weighted expert outputs as extra split-K slabs, so the
+//                next kernel's slab-sum prologue (add_norm) performs the top-k combine for free.
+#include "qweight.h"
+
+namespace la {
+
+constexpr int MOE_WAVES = 4;
+constexpr int MOE_THREADS = 64 * MOE_WAVES;
+constexpr int MOE_LDS_STRIDE = 256 + 8;
+
+__global__ __launch_bounds__(256) void moe_route_kernel(const int* __restrict__ ids, int T, int topk, int E,
+                                                        int* __restrict__ order, int* __restrict__ off) {
+  __shared__ int cnt[256];
+  __shared__ int base[257];
+  const int P = T * topk;
+  for (int e = threadIdx.x; e < E; e += blockDim.x) cnt[e] = 0;
+  __syncthreads();
+  for (int p = threadIdx.x; p < P; p += blockDim.x) atomicAdd(&cnt[min(max(ids[p], 0), E - 1)], 1);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    base[0] = 0;
+    for (int e = 0; e < E; ++e) base[e + 1] = base[e] + cnt[e];
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e <= E; e += blockDim.x) off[e] = base[e];
+  // stable placement: expert e's pairs in increasing pair order (one thread per expert)
+  for (int e = threadIdx.x; e < E; e += blockDim.x) {
+    int o = base[e];
+    for (int p = 0; p < P; ++p)
+      if (min(max(ids[p], 0), E - 1) == e) order[o++] = p;
+  }
+}
+
+template <int FMT, int MT, bool DOWN>
+__global__ __launch_bounds__(MOE_THREADS, 2) void moe_gemm_kernel(
+    const QW* __restrict__ qws, const int* __restrict__ order, const int* __restrict__ off, int topk,
+    const bf16* __restrict__ X, int ldx, int k_per_split, const float* __restrict__ wts, float* __restrict__ out,
+    int ldo, long slab, int T) {
+  constexpr int MP = 16 * MT;
+  __shared__ __attribute__((aligned(16))) bf16 xs[MP * MOE_LDS_STRIDE];
+  __shared__ int prow[MP];
+
+  const int e = blockIdx.z;
+  const int o0 = off[e];
+  const int M = min(off[e + 1] - o0, MP);
+  if (M <= 0) return;
+  const QW w = qws[e];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, r = lane & 15;
+  const int N = w.N, K = w.K;
+  const int split = blockIdx.y;
+  const int kbeg = split * k_per_split;
+  const int nsb = min(k_per_split, K - kbeg) >> 8;
+  const int n = blockIdx.x * (16 * MOE_WAVES) + wave * 16 + r;
+  const int nl = min(n, N - 1);
+  if (tid < MP) prow[tid] = tid < M ? order[o0 + tid] : 0;
+  __syncthreads();
+
+  constexpr int XCH = MP * 32;
+  constexpr int XPT = (XCH + MOE_THREADS - 1) / MOE_THREADS;
+  bf16x8 xr[XPT];
+  auto x_issue = [&](int sb) {
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) {
+      const int c = tid + i * MOE_THREADS;
+      const int row = min(c >> 5, MP - 1), col = (c & 31) * 8;
+      const int p = prow[row];
+      const int xrow = DOWN ? p : p / topk;
+      bf16x8 v = *(const bf16x8*)(X + (size_t)xrow * ldx + kbeg + sb * 256 + col);
+      if (row >= M) v = bf16x8{};
+      xr[i] = v;
+    }
+  };
+  auto x_store = [&]() {
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) {
+      const int c = tid + i * MOE_THREADS;
+      if (c < XCH) *(bf16x8*)(xs + (c >> 5) * MOE_LDS_STRIDE + (c & 31) * 8) = xr[i];
+    }
+  };
+
+  f32x4 acc[MT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int sb0 = kbeg >> 8;
+  WFrag<FMT> fa, fb;
+  x_issue(0);
+  fa.load(w, nl, sb0, g);
+  auto compute = [&](WFrag<FMT>& f) {
+    f.prep(g);
+#define MOE_STEP(S)                                                                          \
+  {                                                                                          \
+    const bf16x8 b = f.template deq<S>();                                                    \
+    const int kp = kphys<FMT>(S, g);                                                         \
+    _Pragma("unroll") for (int mt = 0; mt < MT; ++mt) {                                      \
+      const bf16x8 a = *(const bf16x8*)(xs + (mt * 16 + r) * MOE_LDS_STRIDE + kp);           \
+      acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[mt], 0, 0, 0);             \
+    }                                                                                        \
+  }
+    MOE_STEP(0) MOE_STEP(1) MOE_STEP(2) MOE_STEP(3) MOE_STEP(4) MOE_STEP(5) MOE_STEP(6) MOE_STEP(7)
+#undef MOE_STEP
+  };
+  for (int sb = 0; sb < nsb; sb += 2) {
+    __syncthreads();
+    x_store();
+    __syncthreads();
+    if (sb + 1 < nsb) {
+      x_issue(sb + 1);
+      fb.load(w, nl, sb0 + sb + 1, g);
+    }
+    compute(fa);
+    if (sb + 1 >= nsb) break;
+    __syncthreads();
+    x_store();
+    __syncthreads();
+    if (sb + 2 < nsb) {
+      x_issue(sb + 2);
+      fa.load(w, nl, sb0 + sb + 2, g);
+    }
+    compute(fb);
+  }
+  if (n >= N) return;
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = mt * 16 + 4 * g + i;
+      if (m >= M) continue;
+      const int p = prow[m];
+      if (DOWN) {
+        const int t = p / topk, slot = p - t * topk;
+        out[((size_t)split * topk + slot) * slab + (size_t)t * ldo + n] = acc[mt][i] * wts[p];
+      } else {
+        out[(size_t)split * slab + (size_t)p * ldo + n] = acc[mt][i];
+      }
+    }
+  }
+}
+
+template <int FMT, bool DOWN>
+static void launch_moe(const QW* qws, int N, int K, int E, const int* order, const int* off, int topk,
+                       const bf16* X, int ldx, int maxM, int splits, const float* wts, float* out, int ldo, long slab,
+                       int T, hipStream_t st) {
+  const int per = (K >> 8) / splits;
+  dim3 grid((N + 16 * MOE_WAVES - 1) / (16 * MOE_WAVES), splits, E);
+#define MOE_L(MT)                                                                                            \
+  hipLaunchKernelGGL((moe_gemm_kernel<FMT, MT, DOWN>), grid, dim3(MOE_THREADS), 0, st, qws, order, off, topk, X, \
+                     ldx, per * 256, wts, out, ldo, slab, T)
+  if (maxM <= 16) MOE_L(1);
+  else if (maxM <= 32) MOE_L(2);
+  else MOE_L(4);
+#undef MOE_L
+}
+
+}  // namespace la
+
+extern "C" int la_moe_route(const int* ids, int T, int topk, int E, int* order, int* off, void* stream) {
+  if (E > 256 || E < 1) return -1;
+  hipLaunchKernelGGL(la::moe_route_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, ids, T, topk, E, order, off);
+  return (int)hipGetLastError();
+}
+
+// qws: device array of E QW descriptors (all experts share fmt, N, K).  maxM = max rows per expert
+// (<= T for GATE_UP / DOWN since a token picks an expert at most once) must be <= 64.
+extern "C" int la_moe_gemm(int fmt, int down, const void* qws, int N, int K, int E, const int* order, const int* off,
+                           int topk, const void* X, int ldx, int maxM, int splits, const float* wts, void* out,
+                           int ldo, long slab, int T, void* stream) {
+  using namespace la;
+  if (maxM < 1 || maxM > 64 || (K & 255) || splits < 1 || ((K >> 8) % splits) || ldo < N) return -1;
+  hipStream_t st = (hipStream_t)stream;
+  const QW* q = (const QW*)qws;
+  const bf16* x = (const bf16*)X;
+  float* o = (float*)out;
+#define MOE_F(F)                                                                                     \
+  if (down) launch_moe<F, true>(q, N, K, E, order, off, topk, x, ldx, maxM, splits, wts, o, ldo, slab, T, st); \
+  else launch_moe<F, false>(q, N, K, E, order, off, topk, x, ldx, maxM, splits, wts, o, ldo, slab, T, st);
+  switch (fmt) {
+    case FMT_Q4_K: MOE_F(FMT_Q4_K) break;
+    case FMT_Q6_K: MOE_F(FMT_Q6_K) break;
+    case FMT_Q8_0: MOE_F(FMT_Q8_0) break;
+    case FMT_BF16: MOE_F(FMT_BF16) break;
+    default: return -2;
+  }
+#undef MOE_F
+  return (int)hipGetLastError();
+}
+
+extern "C" int la_qw_size() { return (int)sizeof(la::QW); }

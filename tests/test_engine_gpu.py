@@ -54,3 +54,19 @@ def test_engine_greedy_matches_reference_first_token(tiny_model_path):
     first = eng.tokenize(prompt + res["text"])[len(ids)]
     top = torch.topk(ref, 2)
     assert first == int(top.indices[0]) or float(top.values[0] - ref[first]) < 0.05
+
+
+def test_mixtral_moe_graph_decode(tmp_path):
+    from localai_amd.models import synth
+    p = str(tmp_path / "tiny-mixtral.gguf")
+    synth.write_model(p, "tiny-mixtral", exact=True)
+    a = _run(_eng(p, 1), ["mixture", "of experts"], max_tokens=10, temperature=0.0, ignore_eos=True)
+    b = _run(_eng(p, 8), ["mixture", "of experts"], max_tokens=10, temperature=0.0, ignore_eos=True)
+    assert [x[1] for x in a] == [10, 10] and a == b
+    eng = _eng(p, 8)
+    ids = eng.tokenize("mixture")
+    ref = eng.model.reference_logits(ids)[-1]
+    res = eng.generate("mixture", SamplingParams(max_tokens=2, temperature=0.0, ignore_eos=True))
+    first = eng.tokenize("mixture" + res["text"])[len(ids)]
+    top = torch.topk(ref, 2)
+    assert first == int(top.indices[0]) or float(top.values[0] - ref[first]) < 0.05

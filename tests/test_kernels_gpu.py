@@ -290,3 +290,31 @@ def test_decode_advance_kernel():
     assert np.array_equal(prm_dev.cpu().numpy().view(ops.SAMPLE_ROW_DTYPE)["counter"],
                           prm_cpu.numpy().view(ops.SAMPLE_ROW_DTYPE)["counter"])
     assert int(g[5].item()) == 1 and list(g[4][0].cpu()) == [7, 8, 9, 10, 11]
+
+
+@pytest.mark.parametrize("T", [1, 5, 33])
+def test_moe_grouped_gemm(T):
+    E, topk, D, F = 8, 2, 512, 768
+    gu = [_qw(2 * F, D, GGMLType.Q4_K, seed=10 + e) for e in range(E)]
+    dn = [_qw(D, F, GGMLType.Q6_K, seed=30 + e) for e in range(E)]
+    mg, md = ops.MoEWeights(gu), ops.MoEWeights(dn)
+    x = torch.randn(T, D, device=DEV).to(torch.bfloat16)
+    ids = torch.stack([torch.randperm(E)[:topk] for _ in range(T)]).to(torch.int32).to(DEV)
+    wts = torch.rand(T, topk, device=DEV)
+    order, off = ops.moe_route(ids, E)
+    o = order.cpu().tolist()
+    assert sorted(o) == list(range(T * topk))
+    y = ops.moe_linear(x, mg, order, off, topk, T).dense()          # [T*topk, 2F]
+    idc = ids.cpu()
+    for p in range(T * topk):
+        e = int(idc.view(-1)[p])
+        ref = x[p // topk].float().cpu() @ gu[e].ref.t()
+        assert (y[p].cpu() - ref).abs().max() < 2e-2 * max(1.0, ref.abs().max())
+    h = torch.randn(T * topk, F, device=DEV).to(torch.bfloat16)
+    z = ops.moe_linear(h, md, order, off, topk, T, down=True, wts=wts.reshape(-1).contiguous()).dense()  # [T, D]
+    ref = torch.zeros(T, D)
+    for p in range(T * topk):
+        t, slot = divmod(p, topk)
+        e = int(idc.view(-1)[p])
+        ref[t] += float(wts.view(-1)[p]) * (h[p].float().cpu() @ dn[e].ref.t())
+    assert (z.cpu() - ref).abs().max() < 2e-2 * max(1.0, ref.abs().max())
