@@ -217,7 +217,10 @@ def cmd_util(a) -> int:
 
 def cmd_worker(a) -> int:
     from .parallel.worker import main as worker_main
-    return worker_main(a.rest)
+    rest = list(a.rest)
+    if rest and rest[0] in ("tp", "llama-cpp-rpc", "p2p-llama-cpp-rpc"):  # reference command names
+        rest = rest[1:]
+    return worker_main(rest)
 
 
 def build_parser() -> argparse.ArgumentParser:

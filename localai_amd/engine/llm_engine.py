@@ -14,6 +14,7 @@ Decode steps replay per-batch-size HIP graphs (torch.cuda.CUDAGraph == hipGraph 
 """
 from __future__ import annotations
 
+import dataclasses
 import logging
 import math
 import os
@@ -85,9 +86,21 @@ class Request:
     grammar: object = None       # native GrammarState (GBNF-constrained decoding)
 
 
+def _noop_callback(ev):  # follower ranks: the leader talks to the client
+    pass
+
+
 class LLMEngine:
-    def __init__(self, cfg: EngineConfig, tp: Optional[TPInfo] = None):
+    def __init__(self, cfg: EngineConfig, tp: Optional[TPInfo] = None, ctrl_group=None):
+        """tp: tensor-parallel rank info (one engine per GPU, identical schedulers on every rank).
+        ctrl_group: a gloo process group the leader (rank 0) uses to broadcast new requests /
+        aborts to the followers each step; required when tp.world > 1."""
         self.cfg = cfg
+        self.tp = tp or TPInfo()
+        self.leader = self.tp.rank == 0
+        self.ctrl = ctrl_group
+        if self.tp.world > 1 and ctrl_group is None:
+            raise ValueError("tensor-parallel engines need a control process group")
         self.device = torch.device(cfg.device)
         if self.device.type == "cuda":
             torch.cuda.set_device(self.device)
@@ -244,6 +257,15 @@ class LLMEngine:
             self._thread.start()
 
     def shutdown(self):
+        if self.tp.world > 1 and self.leader and not self._stop:
+            self._inbox.put(("stop",))  # followers leave run_follower() after this broadcast
+            self._wake.set()
+            if self._thread is not None:
+                self._thread.join(timeout=30)
+                self._thread = None
+            else:
+                self._drain_inbox()
+            return
         self._stop = True
         self._wake.set()
         if self._thread is not None:
@@ -274,7 +296,7 @@ class LLMEngine:
 
     def step(self) -> bool:
         self._drain_inbox()
-        if not self.requests:
+        if not self.requests or self._stop:
             return False
         self.busy = True
         K = self._lookahead()
@@ -297,28 +319,75 @@ class LLMEngine:
         return did or bool(self.requests)
 
     def _drain_inbox(self):
-        while True:
-            try:
-                item = self._inbox.get_nowait()
-            except queue.Empty:
-                break
-            if isinstance(item, tuple) and item[0] == "embed":
-                self._run_embed_job(item[1])
-                continue
-            if isinstance(item, tuple) and item[0] == "abort":
-                r = self.requests.get(item[1])
-                if r is not None:
-                    r.cancelled = True
-                    self._finish(r, "cancelled")
-                continue
-            r: Request = item
-            if len(r.prompt) >= self.ctx:
-                r.callback(Event(finished=True, finish_reason="error", error="prompt exceeds context"))
-                continue
-            self.requests[r.id] = r
-            max_new = r.params.max_tokens if r.params.max_tokens > 0 else self.ctx
-            self.sched.add(r.id, r.prompt, max_new)
-            self.metrics["requests"] += 1
+        items = []
+        if self.leader:
+            while True:
+                try:
+                    items.append(self._inbox.get_nowait())
+                except queue.Empty:
+                    break
+        if self.tp.world > 1:
+            # replicated scheduling: every rank applies the leader's new work in the same order,
+            # so all ranks build identical batches and sample identical tokens
+            import torch.distributed as dist
+            box = [[self._to_wire(it) for it in items] if self.leader else None]
+            dist.broadcast_object_list(box, src=0, group=self.ctrl)
+            if not self.leader:
+                items = [self._from_wire(w) for w in box[0]]
+        for item in items:
+            self._apply(item)
+
+    @staticmethod
+    def _to_wire(item):
+        if isinstance(item, tuple):
+            if item[0] == "embed":
+                return ("embed", item[1]["texts"], item[1]["pool"])
+            return item
+        r: Request = item
+        return ("req", r.id, list(r.prompt), dataclasses.asdict(r.params))
+
+    def _from_wire(self, w):
+        kind = w[0]
+        if kind == "req":
+            _, rid, prompt, prm = w
+            params = SamplingParams(**prm)
+            r = Request(rid, prompt, params, _noop_callback, n_prompt=len(prompt), mu=2.0 * params.mirostat_tau)
+            r.stream = core.TextStream(self.vocab, list(params.stop))
+            if params.grammar:
+                r.grammar = core.GrammarState(self._grammar(params.grammar), self.gvocab)
+            return r
+        if kind == "embed":
+            return ("embed", {"texts": w[1], "pool": w[2], "done": threading.Event()})
+        return w
+
+    def _apply(self, item):
+        if isinstance(item, tuple) and item[0] == "stop":
+            self._stop = True
+            return
+        if isinstance(item, tuple) and item[0] == "embed":
+            self._run_embed_job(item[1])
+            return
+        if isinstance(item, tuple) and item[0] == "abort":
+            r = self.requests.get(item[1])
+            if r is not None:
+                r.cancelled = True
+                self._finish(r, "cancelled")
+            return
+        r: Request = item
+        if len(r.prompt) >= self.ctx:
+            r.callback(Event(finished=True, finish_reason="error", error="prompt exceeds context"))
+            return
+        self.requests[r.id] = r
+        max_new = r.params.max_tokens if r.params.max_tokens > 0 else self.ctx
+        self.sched.add(r.id, r.prompt, max_new)
+        self.metrics["requests"] += 1
+
+    def run_follower(self):
+        """Non-leader tensor-parallel rank: mirror the leader's steps until it broadcasts stop."""
+        if self.device.type == "cuda":
+            torch.cuda.set_device(self.device)
+        while not self._stop:
+            self.step()
 
     def _dev(self, a: np.ndarray) -> torch.Tensor:
         t = torch.from_numpy(np.ascontiguousarray(a))

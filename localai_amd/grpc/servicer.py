@@ -116,6 +116,8 @@ class EngineServicer:
         path = request.ModelFile or request.Model
         if not os.path.isfile(path):
             return pb.Result(success=False, message=f"model file not found: {path}")
+        if self.engine is not None and getattr(self, "loaded_path", "") == os.path.abspath(path):
+            return pb.Result(success=True, message="Loaded")  # pre-loaded (tensor-parallel worker group)
         try:
             import torch
             dev = self.device
@@ -144,6 +146,7 @@ class EngineServicer:
                 if self.engine is not None:
                     self.engine.shutdown()
                 self.engine = eng
+                self.loaded_path = os.path.abspath(path)
                 self.model_name = os.path.basename(path)
                 self.state = pb.StatusResponse.READY
             return pb.Result(success=True, message="Loaded")
