@@ -15,10 +15,12 @@ Decode steps replay per-batch-size HIP graphs (torch.cuda.CUDAGraph == hipGraph 
 from __future__ import annotations
 
 import dataclasses
+import hashlib
 import logging
 import math
 import os
 import queue
+import re
 import threading
 import time
 from dataclasses import dataclass, field
@@ -54,6 +56,7 @@ class EngineConfig:
     rope_freq_scale: float = 0.0
     rope_scaling: str = ""
     decode_steps: int = 8             # device-resident decode steps per host round trip (graphs only)
+    mmproj: str = ""                  # LLaVA vision tower + projector GGUF (images in prompts)
     bias_capacity: int = 16           # logit-bias / EOS-ban entries per sequence inside the graph
 
 
@@ -84,6 +87,8 @@ class Request:
     cancelled: bool = False
     sink: object = None
     grammar: object = None       # native GrammarState (GBNF-constrained decoding)
+    mm_pos: object = None        # {prompt position: row of mm_emb} for image-embedding positions
+    mm_emb: object = None        # [rows, n_embd] f32 projected image embeddings (device)
 
 
 def _noop_callback(ev):  # follower ranks: the leader talks to the client
@@ -119,6 +124,12 @@ class LLMEngine:
         self.vocab = core.Vocab(self.tokenizer.pieces)
         self.gvocab = core.GrammarVocab(self.tokenizer.pieces, sorted(self.tokenizer.eog))
         self._grammars: Dict[str, object] = {}
+        self.clip = None
+        if cfg.mmproj:
+            from ..models.clip import ClipVision
+            self.clip = ClipVision(cfg.mmproj, self.device)
+            if self.clip.out_dim != self.hp.n_embd:
+                raise ValueError(f"mmproj projects to {self.clip.out_dim}, the LLM embeds {self.hp.n_embd}")
         self.ctx = cfg.context_size
         bs = cfg.block_size
         if self.device.type == "cuda":
@@ -180,16 +191,22 @@ class LLMEngine:
         return self.tokenizer.encode(text, add_bos=add_bos)
 
     def add_request(self, prompt, params: SamplingParams, callback: Callable[[Event], None],
-                    req_id: Optional[int] = None, sink=None) -> int:
+                    req_id: Optional[int] = None, sink=None, images: Optional[Sequence] = None) -> int:
         """Queue a generation.  `callback(Event)` gets every text delta and the final event;
         with a native `sink` (native/_la_http SseSink) text deltas go straight to
         `sink.push(text, n_generated)` (no Python Event per token) and only the final event
         reaches `callback`."""
+        rid = req_id if req_id is not None else self.new_id()
+        if images and self.clip is not None and isinstance(prompt, str):
+            # the vision tower runs on the engine thread (single GPU stream owner)
+            params.resolved_seed()
+            self._inbox.put(("mm", rid, prompt, list(images), params, callback, sink))
+            self._wake.set()
+            return rid
         toks = self.tokenize(prompt) if isinstance(prompt, str) else list(prompt)
         if not toks:
             toks = [self.tokenizer.bos_id if self.tokenizer.bos_id >= 0 else 0]
         toks = self._truncate(toks, params.n_keep)
-        rid = req_id if req_id is not None else self.new_id()
         params.resolved_seed()
         stops = list(params.stop)
         r = Request(rid, toks, params, callback, n_prompt=len(toks), mu=2.0 * params.mirostat_tau)
@@ -342,6 +359,9 @@ class LLMEngine:
         if isinstance(item, tuple):
             if item[0] == "embed":
                 return ("embed", item[1]["texts"], item[1]["pool"])
+            if item[0] == "mm":
+                _, rid, prompt, images, params, _cb, _sink = item
+                return ("mm", rid, prompt, images, dataclasses.asdict(params))
             return item
         r: Request = item
         return ("req", r.id, list(r.prompt), dataclasses.asdict(r.params))
@@ -358,12 +378,22 @@ class LLMEngine:
             return r
         if kind == "embed":
             return ("embed", {"texts": w[1], "pool": w[2], "done": threading.Event()})
+        if kind == "mm":
+            _, rid, prompt, images, prm = w
+            return ("mm", rid, prompt, images, SamplingParams(**prm), _noop_callback, None)
         return w
 
     def _apply(self, item):
         if isinstance(item, tuple) and item[0] == "stop":
             self._stop = True
             return
+        if isinstance(item, tuple) and item[0] == "mm":
+            try:
+                item = self._build_mm_request(*item[1:])
+            except Exception as e:  # bad image / too long: report to the caller
+                log.exception("multimodal request failed")
+                item[5](Event(finished=True, finish_reason="error", error=f"image processing failed: {e}"))
+                return
         if isinstance(item, tuple) and item[0] == "embed":
             self._run_embed_job(item[1])
             return
@@ -381,6 +411,52 @@ class LLMEngine:
         max_new = r.params.max_tokens if r.params.max_tokens > 0 else self.ctx
         self.sched.add(r.id, r.prompt, max_new)
         self.metrics["requests"] += 1
+
+    IMG_MARK = re.compile(r"\[img-(\d+)\]")
+
+    def _build_mm_request(self, rid, prompt, images, params, callback, sink) -> Request:
+        """Tokenise around `[img-N]` markers (LocalAI's multimodal template) and splice the
+        projected CLIP embeddings of image N in.  Image positions carry placeholder token ids
+        above the vocabulary, derived from the image hash so prefix caching never matches two
+        different images."""
+        V = self.hp.n_vocab
+        embs = [self.clip.embed_image(im) for im in images]
+        parts = self.IMG_MARK.split(prompt)
+        used = {int(parts[i]) for i in range(1, len(parts), 2)}
+        seq: List = [("img", i) for i in range(len(embs)) if i not in used]  # unreferenced: up front
+        for i, ptxt in enumerate(parts):
+            if i % 2 == 0:
+                if ptxt:
+                    seq.append(("txt", ptxt))
+            elif int(ptxt) < len(embs):
+                seq.append(("img", int(ptxt)))
+        toks: List[int] = []
+        if self.tokenizer.add_bos and self.tokenizer.bos_id >= 0:
+            toks.append(self.tokenizer.bos_id)
+        rows, mm_pos = [], {}
+        for kind, v in seq:
+            if kind == "txt":
+                toks += self.tokenize(v, add_bos=False)
+                continue
+            e = embs[v]
+            data = images[v].encode() if isinstance(images[v], str) else bytes(images[v])
+            base = V + (int(hashlib.sha1(data).hexdigest()[:8], 16) % (1 << 18)) * 4096
+            for j in range(e.shape[0]):
+                mm_pos[len(toks)] = len(rows) + j
+                toks.append(base + (j % 4096))
+            rows.append(e)
+        if len(toks) >= self.ctx:
+            raise ValueError(f"prompt with images is {len(toks)} tokens, context is {self.ctx}")
+        r = Request(rid, toks, params, callback, n_prompt=len(toks), mu=2.0 * params.mirostat_tau)
+        r.stream = core.TextStream(self.vocab, list(params.stop))
+        if params.grammar:
+            r.grammar = core.GrammarState(self._grammar(params.grammar), self.gvocab)
+        r.sink = sink
+        if sink is not None:
+            sink.set_prompt_tokens(r.n_prompt)
+        r.mm_pos = mm_pos
+        r.mm_emb = torch.cat(rows, 0).float() if rows else None
+        return r
 
     def run_follower(self):
         """Non-leader tensor-parallel rank: mirror the leader's steps until it broadcasts stop."""
@@ -401,11 +477,31 @@ class LLMEngine:
         last = plan["p_last"]
         qlens = plan["p_qlen"]
         rows = [int(cu[i + 1]) - 1 for i in range(len(ids)) if last[i]]
+        tokens = plan["p_tokens"]
+        inj_idx = inj_rows = None
+        if self.clip is not None and (tokens >= self.hp.n_vocab).any():
+            tokens = tokens.copy()
+            pos = plan["p_pos"]
+            idx, chunks = [], []
+            for i, sid in enumerate(ids):
+                r = self.requests[int(sid)]
+                a, b = int(cu[i]), int(cu[i + 1])
+                if r.mm_pos is None:
+                    continue
+                sel = [(t, r.mm_pos[int(pos[t])]) for t in range(a, b) if int(pos[t]) in r.mm_pos]
+                if sel:
+                    idx += [t for t, _ in sel]
+                    chunks.append(r.mm_emb[torch.tensor([k for _, k in sel], device=r.mm_emb.device)])
+            tokens[tokens >= self.hp.n_vocab] = 0
+            if idx:
+                inj_idx = torch.tensor(idx, dtype=torch.long, device=self.device)
+                inj_rows = torch.cat(chunks, 0).to(self.device, torch.float32)
         fb = ForwardBatch(
-            tokens=self._dev(plan["p_tokens"]), pos=self._dev(plan["p_pos"]), slots=self._dev(plan["p_slots"]),
+            tokens=self._dev(tokens), pos=self._dev(plan["p_pos"]), slots=self._dev(plan["p_slots"]),
             decode=False, block_tables=self._dev(plan["p_bt"]), cu_q=self._dev(cu), ctx_lens=self._dev(plan["p_ctx"]),
             tiles=ops.prefill_tiles(qlens.tolist(), self.device) if self.device.type == "cuda" else None,
-            logits_idx=self._dev(np.array(rows, dtype=np.int64)) if rows else None)
+            logits_idx=self._dev(np.array(rows, dtype=np.int64)) if rows else None,
+            inject_idx=inj_idx, inject_rows=inj_rows)
         self.metrics["prompt_tokens"] += int(cu[-1])
         if not rows:
             self.model.forward(fb, self.kv)  # intermediate chunk: KV only

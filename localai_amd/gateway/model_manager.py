@@ -181,6 +181,9 @@ class ModelManager:
         opts = grpc_model_options(cfg, self.app, self.models_path)
         if not os.path.isfile(opts.ModelFile):
             raise RuntimeError(f"could not load model: model file {opts.ModelFile} not found")
+        tp = int(cfg.raw.get("tensor_parallel_size") or 0)
+        if tp > 1:
+            return await self._start_tp_group(mid, cfg, opts, tp)
         if self.app.engine_mode == "process":
             port = free_port()
             addr = f"127.0.0.1:{port}"
@@ -203,6 +206,30 @@ class ModelManager:
         if not res.success:
             raise RuntimeError(res.message)
         return LoadedModel(mid, "localai-amd", EmbeddedBackend(sv), servicer=sv)
+
+    async def _start_tp_group(self, mid: str, cfg: BackendConfig, opts, tp: int) -> LoadedModel:
+        """tensor_parallel_size > 1: one process per GPU via torch.distributed.run (RCCL over xGMI);
+        rank 0 serves backend.proto and the gateway talks to it like any other backend."""
+        port, mport = free_port(), free_port()
+        addr = f"127.0.0.1:{port}"
+        ctx = int(cfg.raw.get("context_size") or opts.ContextSize or 4096)
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={tp}",
+               "--master-addr", "127.0.0.1", "--master-port", str(mport), "-m", "localai_amd.parallel.worker",
+               "--model", opts.ModelFile, "--addr", addr, "--context", str(ctx),
+               "--max-num-seqs", os.environ.get("LOCALAI_MAX_NUM_SEQS", "256")]
+        if opts.EnforceEager:
+            cmd.append("--eager")
+        proc = subprocess.Popen(cmd, env=dict(os.environ))
+        h = GRPCBackend(addr)
+        g = dict(cfg.raw.get("grpc") or {})
+        g.setdefault("attempts", 300)  # sharded load of a 70B model takes a while
+        cfg.raw["grpc"] = g
+        await self._wait_healthy(h, cfg, proc)
+        res = await h.LoadModel(opts, timeout=3600)
+        if not res.success:
+            proc.terminate()
+            raise RuntimeError(f"could not load model: {res.message}")
+        return LoadedModel(mid, f"localai-amd-tp{tp}", h, process=proc, addr=addr)
 
     async def _wait_healthy(self, h: GRPCBackend, cfg: BackendConfig, proc=None):
         g = cfg.raw.get("grpc") or {}

@@ -525,8 +525,8 @@ async def _native_stream(request, state, cfg, req, pred_input: str, cid: str, cr
     lm = await state.manager.load(cfg)
     sv = lm.servicer
     eng = getattr(sv, "engine", None) if sv is not None else None
-    if eng is None:
-        return None
+    if eng is None or (getattr(eng, "clip", None) is not None and any(m.get("_images") for m in req.get("messages") or [])):
+        return None  # images go through the generic path (the servicer hands them to the engine)
     from ..native import http
     from .inference import predict_options
     from .native_server import NativeHandledResponse

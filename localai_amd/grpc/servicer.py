@@ -137,7 +137,8 @@ class EngineServicer:
                 gpu_memory_utilization=request.GPUMemoryUtilization or 0.85,
                 embeddings=request.Embeddings, rope_freq_base=request.RopeFreqBase,
                 rope_freq_scale=request.RopeFreqScale, rope_scaling=request.RopeScaling,
-                use_graphs=not request.EnforceEager)
+                use_graphs=not request.EnforceEager,
+                mmproj=self._mmproj_path(request, path))
             loop = asyncio.get_running_loop()
             eng = await loop.run_in_executor(None, lambda: LLMEngine(cfg, tp=self.tp))
             await loop.run_in_executor(None, eng.warmup)
@@ -154,6 +155,20 @@ class EngineServicer:
             log.exception("LoadModel failed")
             self.state = pb.StatusResponse.ERROR
             return pb.Result(success=False, message=f"could not load model: {e}")
+
+    @staticmethod
+    def _mmproj_path(request, model_path: str) -> str:
+        mm = request.MMProj
+        if not mm:
+            return ""
+        return mm if os.path.isabs(mm) else os.path.join(os.path.dirname(model_path), mm)
+
+    def _images(self, request):
+        imgs = list(request.Images)
+        if imgs and getattr(self.engine, "clip", None) is None:
+            log.warning("request has %d image(s) but the model has no mmproj; ignoring them", len(imgs))
+            return None
+        return imgs or None
 
     def _require_engine(self):
         if self.engine is None:
@@ -190,7 +205,7 @@ class EngineServicer:
     async def PredictStream(self, request, context=None):
         eng = self._require_engine()
         ch = _Channel(_pump_for(asyncio.get_running_loop()))
-        rid = eng.add_request(self._prompt(request), self._params(request), ch.put)
+        rid = eng.add_request(self._prompt(request), self._params(request), ch.put, images=self._images(request))
         finished = False
         try:
             while True:
@@ -229,7 +244,7 @@ class EngineServicer:
                     fut.set_result(ev)
             loop.call_soon_threadsafe(apply)
 
-        rid = eng.add_request(self._prompt(request), self._params(request), cb)
+        rid = eng.add_request(self._prompt(request), self._params(request), cb, images=self._images(request))
         try:
             ev = await fut
         except asyncio.CancelledError:

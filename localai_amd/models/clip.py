@@ -1,0 +1,200 @@
+"""CLIP ViT image encoder + LLaVA projector, loaded from a llama.cpp `mmproj` GGUF (the reference
+reaches this through grpc-server.cpp -> llava/clip.cpp).
+
+Preprocessing (PIL decode -> resize -> center crop / pad -> normalise) runs on the host; the ViT
+runs on the device in bf16: patch embedding as one GEMM over unfolded patches (im2col), fused
+QKV, SDPA attention, LayerNorm / quick-GELU, the two-layer GELU projector into the LLM's
+embedding space.  LLaVA-1.5 (one 336^2 tile -> 576 embeddings) and LLaVA-1.6 "anyres"
+(grid tiles + a base tile, spatial unpadding, image_newline rows) layouts are supported.
+"""
+from __future__ import annotations
+
+import base64
+import io
+import math
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from ..gguf import GGUFReader, dequantize
+
+DEFAULT_MEAN = (0.48145466, 0.4578275, 0.40821073)
+DEFAULT_STD = (0.26862954, 0.26130258, 0.27577711)
+
+
+def decode_image(data) -> "PIL.Image.Image":
+    from PIL import Image
+    if isinstance(data, str):
+        if data.startswith("data:"):
+            data = data.split(",", 1)[1]
+        data = base64.b64decode(data)
+    return Image.open(io.BytesIO(data)).convert("RGB")
+
+
+class ClipVision:
+    def __init__(self, path: str, device: torch.device, dtype=torch.bfloat16):
+        r = GGUFReader(path)
+        kv = r.kv
+        self.device, self.dtype = device, dtype
+        self.image_size = int(kv.get("clip.vision.image_size", 336))
+        self.patch = int(kv.get("clip.vision.patch_size", 14))
+        self.dim = int(kv.get("clip.vision.embedding_length", 1024))
+        self.heads = int(kv.get("clip.vision.attention.head_count", 16))
+        self.eps = float(kv.get("clip.vision.attention.layer_norm_epsilon", 1e-5))
+        self.n_layer = int(kv.get("clip.vision.block_count", 23))
+        self.mean = tuple(float(x) for x in kv.get("clip.vision.image_mean", DEFAULT_MEAN))
+        self.std = tuple(float(x) for x in kv.get("clip.vision.image_std", DEFAULT_STD))
+        self.use_gelu = bool(kv.get("clip.use_gelu", False))
+        self.merge = str(kv.get("clip.vision.mm_patch_merge_type", "flat"))
+        pins = kv.get("clip.vision.image_grid_pinpoints", None)
+        self.pinpoints = [(int(pins[i]), int(pins[i + 1])) for i in range(0, len(pins), 2)] if pins else []
+        T = r.tensors
+
+        def t(name, required=True):
+            if name not in T:
+                if required:
+                    raise KeyError(f"mmproj: missing tensor {name}")
+                return None
+            x = T[name]
+            a = dequantize(x.data, x.ggml_type, x.shape).reshape(x.shape)
+            return torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).to(device)
+
+        D = self.dim
+        pe = t("v.patch_embd.weight")                       # [D, 3, p, p]
+        self.patch_w = pe.reshape(D, -1).to(dtype)          # im2col GEMM weight [D, 3*p*p]
+        self.patch_b = t("v.patch_embd.bias", False)
+        self.cls = t("v.class_embd")
+        self.pos = t("v.position_embd.weight")
+        self.pre_ln = (t("v.pre_ln.weight", False), t("v.pre_ln.bias", False))
+        self.post_ln = (t("v.post_ln.weight", False), t("v.post_ln.bias", False))
+        self.layers = []
+        for i in range(self.n_layer):
+            b = f"v.blk.{i}."
+            qkv_w = torch.cat([t(b + "attn_q.weight"), t(b + "attn_k.weight"), t(b + "attn_v.weight")], 0)
+            qkv_b = torch.cat([t(b + "attn_q.bias"), t(b + "attn_k.bias"), t(b + "attn_v.bias")], 0)
+            f1, f2 = t(b + "ffn_down.weight"), t(b + "ffn_up.weight")  # llama.cpp naming: down = fc1
+            f1b, f2b = t(b + "ffn_down.bias"), t(b + "ffn_up.bias")
+            if f1.shape[1] != D:  # other converters name them the natural way round
+                f1, f2, f1b, f2b = f2, f1, f2b, f1b
+            self.layers.append(dict(
+                ln1=(t(b + "ln1.weight"), t(b + "ln1.bias")), ln2=(t(b + "ln2.weight"), t(b + "ln2.bias")),
+                qkv_w=qkv_w.to(dtype), qkv_b=qkv_b, o_w=t(b + "attn_out.weight").to(dtype), o_b=t(b + "attn_out.bias"),
+                f1_w=f1.to(dtype), f1_b=f1b, f2_w=f2.to(dtype), f2_b=f2b))
+        self.mm0 = (t("mm.0.weight").to(dtype), t("mm.0.bias"))
+        self.mm2 = (t("mm.2.weight").to(dtype), t("mm.2.bias"))
+        self.out_dim = self.mm2[0].shape[0]
+        self.newline = t("model.image_newline", False)
+        self.grid = self.image_size // self.patch
+        self.n_patches = self.grid * self.grid
+
+    # ------------------------------------------------------------------ preprocessing
+    def _norm(self, img) -> torch.Tensor:
+        a = torch.from_numpy(np.asarray(img, dtype=np.float32) / 255.0).permute(2, 0, 1)
+        m = torch.tensor(self.mean).view(3, 1, 1)
+        s = torch.tensor(self.std).view(3, 1, 1)
+        return (a - m) / s
+
+    def _resize_square(self, img):
+        """CLIP: shortest side -> image_size (bicubic), center crop."""
+        from PIL import Image
+        S = self.image_size
+        w, h = img.size
+        sc = S / min(w, h)
+        img = img.resize((max(S, round(w * sc)), max(S, round(h * sc))), Image.BICUBIC)
+        w, h = img.size
+        l, tp = (w - S) // 2, (h - S) // 2
+        return img.crop((l, tp, l + S, tp + S))
+
+    def _best_resolution(self, w: int, h: int) -> Tuple[int, int]:
+        best, best_eff, best_waste = None, -1, float("inf")
+        for pw, ph in self.pinpoints:
+            sc = min(pw / w, ph / h)
+            dw, dh = int(w * sc), int(h * sc)
+            eff = min(dw * dh, w * h)
+            waste = pw * ph - eff
+            if eff > best_eff or (eff == best_eff and waste < best_waste):
+                best, best_eff, best_waste = (pw, ph), eff, waste
+        return best
+
+    def preprocess(self, data) -> Tuple[torch.Tensor, Optional[Tuple[int, int, int, int]]]:
+        """-> (tiles [n, 3, S, S], anyres layout (grid_w, grid_h, orig_w, orig_h) or None)."""
+        img = decode_image(data)
+        if not self.pinpoints or self.merge == "flat":
+            return self._norm(self._resize_square(img)).unsqueeze(0), None
+        from PIL import Image
+        w, h = img.size
+        bw, bh = self._best_resolution(w, h)
+        sc = min(bw / w, bh / h)
+        nw, nh = max(1, int(w * sc)), max(1, int(h * sc))
+        canvas = Image.new("RGB", (bw, bh), tuple(int(255 * m) for m in self.mean))
+        canvas.paste(img.resize((nw, nh), Image.BICUBIC), ((bw - nw) // 2, (bh - nh) // 2))
+        S = self.image_size
+        tiles = [self._norm(img.resize((S, S), Image.BICUBIC))]  # base image first
+        for y in range(0, bh, S):
+            for x in range(0, bw, S):
+                tiles.append(self._norm(canvas.crop((x, y, x + S, y + S))))
+        return torch.stack(tiles), (bw // S, bh // S, w, h)
+
+    # ------------------------------------------------------------------ encoder
+    @torch.inference_mode()
+    def encode_tiles(self, pix: torch.Tensor) -> torch.Tensor:
+        """pixels [n, 3, S, S] -> projected patch embeddings [n, n_patches, out_dim] (f32)."""
+        n = pix.shape[0]
+        D, P, H = self.dim, self.patch, self.heads
+        x = pix.to(self.device, torch.float32)
+        cols = F.unfold(x, kernel_size=P, stride=P).transpose(1, 2)           # [n, np, 3*P*P]
+        h = (cols.to(self.dtype) @ self.patch_w.t()).float()                  # im2col patch GEMM
+        if self.patch_b is not None:
+            h = h + self.patch_b
+        h = torch.cat([self.cls.view(1, 1, D).expand(n, 1, D), h], 1) + self.pos[: h.shape[1] + 1]
+        if self.pre_ln[0] is not None:
+            h = F.layer_norm(h, (D,), self.pre_ln[0], self.pre_ln[1], self.eps)
+        L = h.shape[1]
+        for ly in self.layers:
+            res = h
+            a = F.layer_norm(h, (D,), ly["ln1"][0], ly["ln1"][1], self.eps)
+            qkv = (a.to(self.dtype) @ ly["qkv_w"].t()).float() + ly["qkv_b"]
+            q, k, v = qkv.view(n, L, 3, H, D // H).permute(2, 0, 3, 1, 4).to(self.dtype)
+            o = F.scaled_dot_product_attention(q, k, v)                        # non-causal
+            o = o.transpose(1, 2).reshape(n, L, D)
+            h = res + (o @ ly["o_w"].t()).float() + ly["o_b"]
+            res = h
+            a = F.layer_norm(h, (D,), ly["ln2"][0], ly["ln2"][1], self.eps)
+            f = (a.to(self.dtype) @ ly["f1_w"].t()).float() + ly["f1_b"]
+            f = F.gelu(f) if self.use_gelu else f * torch.sigmoid(1.702 * f)
+            h = res + (f.to(self.dtype) @ ly["f2_w"].t()).float() + ly["f2_b"]
+        if self.post_ln[0] is not None:
+            h = F.layer_norm(h, (D,), self.post_ln[0], self.post_ln[1], self.eps)
+        h = h[:, 1:]                                                           # drop CLS
+        y = (h.to(self.dtype) @ self.mm0[0].t()).float() + self.mm0[1]
+        y = F.gelu(y)
+        y = (y.to(self.dtype) @ self.mm2[0].t()).float() + self.mm2[1]
+        return y
+
+    def embed_image(self, data) -> torch.Tensor:
+        """One image -> [n_tokens, out_dim] f32 rows to splice into the prompt."""
+        tiles, layout = self.preprocess(data)
+        e = self.encode_tiles(tiles)
+        if layout is None:
+            return e[0]
+        gw, gh, ow, oh = layout
+        g = self.grid
+        base, rest = e[0], e[1:]                                               # [np, C]
+        C = e.shape[-1]
+        feat = rest.view(gh, gw, g, g, C).permute(0, 2, 1, 3, 4).reshape(gh * g, gw * g, C)
+        # spatial unpad: drop the padding rows / cols the letterboxing added
+        cur_h, cur_w = feat.shape[0], feat.shape[1]
+        if ow / oh > cur_w / cur_h:
+            nh = int(oh * cur_w / ow)
+            pad = (cur_h - nh) // 2
+            feat = feat[pad:pad + nh]
+        else:
+            nw = int(ow * cur_h / oh)
+            pad = (cur_w - nw) // 2
+            feat = feat[:, pad:pad + nw]
+        if self.newline is not None:
+            nl = self.newline.view(1, 1, C).expand(feat.shape[0], 1, C)
+            feat = torch.cat([feat, nl], 1)
+        return torch.cat([base, feat.reshape(-1, C)], 0)

@@ -63,6 +63,8 @@ class ForwardBatch:
     ctx_lens: Optional[torch.Tensor] = None   # prefill: [nseq] i32
     tiles: Optional[torch.Tensor] = None      # prefill: attention work tiles
     logits_idx: Optional[torch.Tensor] = None  # rows to project to logits (None: all)
+    inject_idx: Optional[torch.Tensor] = None  # prefill rows whose embedding is given (images)
+    inject_rows: Optional[torch.Tensor] = None  # [n, n_embd] f32
 
 
 class KVCache:
@@ -318,6 +320,8 @@ class DecoderModel:
         eps, nm = hp.norm_eps, self.norm_mode
         T = fb.tokens.shape[0]
         res = ops.embed(fb.tokens, self.tok_embd)
+        if fb.inject_idx is not None:
+            res.index_copy_(0, fb.inject_idx, fb.inject_rows.to(res.dtype))
         L0 = self.layers[0]
         xn = ops.add_norm(res, None, L0.attn_norm, L0.attn_norm_b, eps, nm)
         n = len(self.layers)

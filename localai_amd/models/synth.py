@@ -287,3 +287,54 @@ def ensure_model(preset: str, cache_dir: Optional[str] = None, **kw) -> str:
         write_model(tmp, preset, **kw)
         os.replace(tmp, path)
     return path
+
+
+def write_mmproj(path: str, out_dim: int, dim: int = 1024, n_layer: int = 23, heads: int = 16, ffn: int = 4096,
+                 image_size: int = 336, patch: int = 14, seed: int = 0, std: float = 0.02,
+                 pinpoints: Optional[List[int]] = None) -> str:
+    """Random-init llama.cpp-style LLaVA mmproj GGUF (CLIP ViT-L/14 layout + mlp2x_gelu projector).
+    Defaults are the LLaVA-1.5/1.6 vision tower; tests pass tiny dims."""
+    w = GGUFWriter(path, "clip")
+    w.add_bool("clip.has_vision_encoder", True)
+    w.add_bool("clip.has_llava_projector", True)
+    w.add_string("clip.projector_type", "mlp")
+    w.add_uint32("clip.vision.image_size", image_size)
+    w.add_uint32("clip.vision.patch_size", patch)
+    w.add_uint32("clip.vision.embedding_length", dim)
+    w.add_uint32("clip.vision.feed_forward_length", ffn)
+    w.add_uint32("clip.vision.projection_dim", out_dim)
+    w.add_uint32("clip.vision.attention.head_count", heads)
+    w.add_float32("clip.vision.attention.layer_norm_epsilon", 1e-5)
+    w.add_uint32("clip.vision.block_count", n_layer)
+    w.add_array("clip.vision.image_mean", [0.48145466, 0.4578275, 0.40821073], GGUFValueType.FLOAT32)
+    w.add_array("clip.vision.image_std", [0.26862954, 0.26130258, 0.27577711], GGUFValueType.FLOAT32)
+    w.add_bool("clip.use_gelu", False)
+    if pinpoints:
+        w.add_array("clip.vision.image_grid_pinpoints", pinpoints, GGUFValueType.INT32)
+        w.add_string("clip.vision.mm_patch_merge_type", "spatial_unpad")
+    rng = np.random.default_rng(seed)
+    npatch = (image_size // patch) ** 2
+    tensors = [("v.patch_embd.weight", (dim, 3, patch, patch)), ("v.class_embd", (dim,)),
+               ("v.position_embd.weight", (npatch + 1, dim)), ("v.pre_ln.weight", (dim,)), ("v.pre_ln.bias", (dim,))]
+    for i in range(n_layer):
+        b = f"v.blk.{i}."
+        for nm in ("attn_q", "attn_k", "attn_v", "attn_out"):
+            tensors += [(b + nm + ".weight", (dim, dim)), (b + nm + ".bias", (dim,))]
+        tensors += [(b + "ln1.weight", (dim,)), (b + "ln1.bias", (dim,)), (b + "ln2.weight", (dim,)),
+                    (b + "ln2.bias", (dim,)), (b + "ffn_down.weight", (ffn, dim)), (b + "ffn_down.bias", (ffn,)),
+                    (b + "ffn_up.weight", (dim, ffn)), (b + "ffn_up.bias", (dim,))]
+    tensors += [("mm.0.weight", (out_dim, dim)), ("mm.0.bias", (out_dim,)), ("mm.2.weight", (out_dim, out_dim)),
+                ("mm.2.bias", (out_dim,))]
+    if pinpoints:
+        tensors.append(("model.image_newline", (out_dim,)))
+    for name, shape in tensors:
+        n = int(np.prod(shape))
+        if name.endswith(("ln1.weight", "ln2.weight", "pre_ln.weight")):
+            a = (1.0 + 0.05 * rng.standard_normal(n)).astype(np.float32)
+        else:
+            a = (std * rng.standard_normal(n)).astype(np.float32)
+        big = len(shape) >= 2 and n >= 1 << 16
+        t = GGMLType.F16 if big else GGMLType.F32
+        w.add_tensor(name, shape, t, quantize(a, t))
+    w.write()
+    return path

@@ -114,3 +114,58 @@ def test_model_families_generate(preset, tmp_path):
     ids = e.tokenize("hello")
     ref = e.model.reference_logits(ids)[-1]
     assert torch.isfinite(ref).all()
+
+
+def _png(color, size=40):
+    import io
+    from PIL import Image
+    img = Image.new("RGB", (size, size + 8), color)
+    for x in range(0, size, 3):
+        img.putpixel((x, x % size), (255 - color[0], 30, 200))
+    b = io.BytesIO()
+    img.save(b, format="PNG")
+    return b.getvalue()
+
+
+def test_llava_image_prompt(tiny_model_path, tmp_path):
+    import base64
+    from localai_amd.gguf import GGUFReader
+    n_embd = int(GGUFReader(tiny_model_path).kv["llama.embedding_length"])
+    mm = synth.write_mmproj(str(tmp_path / "mmproj.gguf"), out_dim=n_embd, dim=64, n_layer=2, heads=4, ffn=128,
+                            image_size=28, patch=14)
+    e = _engine(tiny_model_path, mmproj=mm)
+    assert e.clip is not None and e.clip.n_patches == 4
+    sp = dict(max_tokens=4, temperature=0.0, ignore_eos=True)
+    out = {}
+
+    def run(images, prompt="[img-0]What is in the image?"):
+        got = {}
+
+        def cb(ev):
+            if ev.finished:
+                got.update(n_prompt=ev.prompt_tokens, n=ev.completion_tokens, err=ev.error)
+        e.add_request(prompt, SamplingParams(**sp), cb, images=images)
+        while not got:
+            e.step()
+        return got
+    text_only = len(e.tokenize("What is in the image?"))
+    a = run([base64.b64encode(_png((200, 10, 10))).decode()])
+    assert a["err"] == "" and a["n"] == 4
+    assert a["n_prompt"] == text_only + 4            # 2x2 patches spliced in front of the text
+    b = run([_png((10, 200, 10))], prompt="What is in the image?")  # unreferenced image goes first
+    assert b["n_prompt"] == text_only + 4
+    emb = e.clip.embed_image(_png((1, 2, 3)))
+    assert emb.shape == (4, n_embd) and torch.isfinite(emb).all()
+
+
+def test_llava16_anyres_layout(tiny_model_path, tmp_path):
+    from localai_amd.gguf import GGUFReader
+    n_embd = int(GGUFReader(tiny_model_path).kv["llama.embedding_length"])
+    mm = synth.write_mmproj(str(tmp_path / "mmproj16.gguf"), out_dim=n_embd, dim=64, n_layer=1, heads=4, ffn=128,
+                            image_size=28, patch=14, pinpoints=[28, 56, 56, 28, 56, 56])
+    from localai_amd.models.clip import ClipVision
+    cv = ClipVision(mm, torch.device("cpu"))
+    tiles, layout = cv.preprocess(_png((90, 90, 90), size=50))
+    assert layout is not None and tiles.shape[0] == 1 + layout[0] * layout[1]
+    emb = cv.embed_image(_png((90, 90, 90), size=50))
+    assert emb.shape[1] == n_embd and emb.shape[0] > 4 and torch.isfinite(emb).all()

@@ -70,3 +70,28 @@ def test_mixtral_moe_graph_decode(tmp_path):
     first = eng.tokenize("mixture" + res["text"])[len(ids)]
     top = torch.topk(ref, 2)
     assert first == int(top.indices[0]) or float(top.values[0] - ref[first]) < 0.05
+
+
+def test_llava_on_gpu(tiny_model_path, tmp_path):
+    import io
+    from PIL import Image
+    from localai_amd.gguf import GGUFReader
+    from localai_amd.models import synth
+    n_embd = int(GGUFReader(tiny_model_path).kv["llama.embedding_length"])
+    mm = synth.write_mmproj(str(tmp_path / "mmproj.gguf"), out_dim=n_embd, dim=128, n_layer=2, heads=4, ffn=256,
+                            image_size=56, patch=14)
+    eng = LLMEngine(EngineConfig(model_path=tiny_model_path, device="cuda:0", context_size=256, max_num_seqs=4,
+                                 mmproj=mm))
+    buf = io.BytesIO()
+    Image.new("RGB", (64, 48), (120, 30, 200)).save(buf, format="PNG")
+    got = {}
+
+    def cb(ev):
+        if ev.finished:
+            got.update(n_prompt=ev.prompt_tokens, n=ev.completion_tokens, err=ev.error)
+    eng.add_request("[img-0] describe", SamplingParams(max_tokens=6, temperature=0.0, ignore_eos=True), cb,
+                    images=[buf.getvalue()])
+    while not got:
+        eng.step()
+    assert got["err"] == "" and got["n"] == 6
+    assert got["n_prompt"] == len(eng.tokenize(" describe")) + 16
