@@ -215,6 +215,17 @@ def cmd_util(a) -> int:
     return 2
 
 
+def cmd_federated(a) -> int:
+    from .gateway.federated import FederatedBalancer, create_federated_app
+    from .gateway.native_server import NativeHTTPServer
+    workers = [w for w in (a.workers or os.environ.get("LOCALAI_FEDERATED_WORKERS", "")).split(",") if w]
+    app = create_federated_app(FederatedBalancer(workers, "random" if a.random_worker else "least-used",
+                                                 a.target_worker or ""))
+    host, port = parse_address(a.address)
+    NativeHTTPServer(app, host, port).run()
+    return 0
+
+
 def cmd_worker(a) -> int:
     from .parallel.worker import main as worker_main
     rest = list(a.rest)
@@ -254,6 +265,11 @@ def build_parser() -> argparse.ArgumentParser:
     u = sub.add_parser("util")
     u.add_argument("action", choices=["gguf-info", "usecase-heuristic"])
     u.add_argument("file")
+    f = sub.add_parser("federated", help="request-level load balancer over LocalAI instances")
+    f.add_argument("--address", default=os.environ.get("LOCALAI_ADDRESS", ":8080"))
+    f.add_argument("--workers", default="", help="comma-separated worker base URLs")
+    f.add_argument("--random-worker", action="store_true")
+    f.add_argument("--target-worker", default="")
     w = sub.add_parser("worker", help="tensor-parallel engine worker group (replaces llama-cpp-rpc workers)")
     w.add_argument("rest", nargs=argparse.REMAINDER)
     return ap
@@ -269,7 +285,7 @@ def main(argv: Optional[List[str]] = None) -> int:
         ap.print_help()
         return 2
     fn = {"run": cmd_run, "models": cmd_models, "transcript": cmd_transcript, "util": cmd_util,
-          "worker": cmd_worker}.get(a.cmd) or getattr(a, "fn", None)
+          "worker": cmd_worker, "federated": cmd_federated}.get(a.cmd) or getattr(a, "fn", None)
     return fn(a)
 
 

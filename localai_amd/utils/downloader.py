@@ -83,9 +83,13 @@ def read_uri(uri: str, base_path: str = "") -> bytes:
     if uri.startswith(LOCAL):
         p = uri[len(LOCAL):]
         if base_path:
-            verify_path(os.path.relpath(os.path.abspath(p), base_path) if os.path.isabs(p) else p, base_path)
+            # like the reference: a file:// resource must resolve (symlinks included) inside base_path
             if not os.path.isabs(p):
                 p = os.path.join(base_path, p)
+            real, root = os.path.realpath(p), os.path.realpath(base_path)
+            if not real.startswith(root + os.sep):
+                raise ValueError("path is outside of trusted root")
+            p = real
         with open(p, "rb") as f:
             return f.read()
     with urllib.request.urlopen(resolve_url(uri), timeout=60) as r:  # noqa: S310
