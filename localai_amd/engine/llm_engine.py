@@ -123,6 +123,7 @@ class LLMEngine:
         self.hp = self.model.hp
         self.vocab = core.Vocab(self.tokenizer.pieces)
         self.gvocab = core.GrammarVocab(self.tokenizer.pieces, sorted(self.tokenizer.eog))
+        self._eog_list = sorted(self.tokenizer.eog)
         self._grammars: Dict[str, object] = {}
         self.clip = None
         if cfg.mmproj:
@@ -564,19 +565,37 @@ class LLMEngine:
             muh = st["mu"][:B].cpu().numpy()
             for j, r in enumerate(reqs):
                 r.mu = float(muh[j])
+        self._emit_run(reqs, hist, K)
+
+    _REASONS = {1: ("stop", True), 2: ("stop", False), 3: ("length", True), 4: ("abort", True)}
+
+    def _emit_run(self, reqs: List[Request], hist: np.ndarray, K: int):
+        """Hand a [K, B] block of device-sampled tokens to the native emitter (detokenise, stop
+        strings, EOS / length limits, SSE writes), then update Python-side request state once
+        per row."""
+        B = len(reqs)
+        st = np.zeros((B, 5), dtype=np.int32)
+        for j, r in enumerate(reqs):
+            st[j] = (r.n_gen, r.params.max_tokens, r.n_prompt, 1 if r.params.ignore_eos else 0, 0 if r.done else 1)
+        n_acc, reason, texts = core.emit_run(hist, K, B, [r.stream for r in reqs], [r.sink for r in reqs], st,
+                                             self._eog_list, self.ctx)
         now = time.perf_counter()
         for j, r in enumerate(reqs):
-            if r.done:
+            n = int(n_acc[j])
+            if r.done or n == 0:
                 continue
-            acc = []
-            for k in range(K):
-                t = int(hist[k, j])
-                acc.append(t)
-                self._on_token(r, t, now, append=False)
-                if r.done:
-                    break
-            if not r.done:
-                self.sched.append_run(r.id, acc)
+            if r.first_token_t == 0.0:
+                r.first_token_t = now
+            r.n_gen += n
+            self.metrics["gen_tokens"] += n
+            if texts[j]:
+                r.callback(Event(text=texts[j], token=-1))
+            rs = int(reason[j])
+            if rs == 0:
+                self.sched.append_run(r.id, hist[:n, j].tolist())
+            else:
+                why, flush = self._REASONS[rs]
+                self._finish(r, why, flush=flush)
 
     def _upload_step_inputs(self, st, reqs, Bp, tok, pos, slots, lens, bt, device_sampling: bool):
         B = len(reqs)

@@ -10,9 +10,6 @@ except ImportError:
 
 
 def http():
-    try:
-        from . import _la_http
-    except ImportError:
-        _build.build_module("_la_http")
-        from . import _la_http
-    return _la_http
+    """The HTTP server / SSE sink classes (compiled into the same module as the engine core, so
+    the engine's native token emitter can drive the sinks directly)."""
+    return core

@@ -11,7 +11,8 @@ from pathlib import Path
 HERE = Path(__file__).resolve().parent
 EXT = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 # module name -> sources
-MODULES = {"_la_core": ["engine_core.cpp", "grammar.cpp"], "_la_http": ["http_server.cpp"]}
+MODULES = {"_la_core": ["engine_core.cpp", "grammar.cpp", "http_server.cpp"]}
+HEADERS = ["text_stream.h"]
 LIB = HERE / f"_la_core{EXT}"
 
 
@@ -32,7 +33,7 @@ def build_module(name: str, force: bool = False, verbose: bool = False, sanitize
     SRCS = [HERE / s for s in MODULES[name]]
     LIB = HERE / f"{name}{EXT}"
     stamp = HERE / f"{name}.stamp"
-    dig = _digest(SRCS) + ("-asan" if sanitize else "")
+    dig = _digest(SRCS + [HERE / h for h in HEADERS]) + ("-asan" if sanitize else "")
     if not force and LIB.exists() and stamp.exists() and stamp.read_text().strip() == dig:
         return LIB
     import pybind11

@@ -20,8 +20,11 @@
 #include <sys/socket.h>
 #include <unistd.h>
 
+#include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
+
+#include "text_stream.h"
 
 #include <atomic>
 #include <chrono>
@@ -629,6 +632,27 @@ class SseSink {
     return srv_->stream_write(conn_, s);
   }
 
+  // Several tokens at once (one SSE event each, one socket write): n_gen[i] is the completion
+  // count after piece i.
+  bool push_many(const std::vector<std::string>& pieces, const std::vector<int>& n_gen) {
+    if (done_) return false;
+    std::string s;
+    for (size_t i = 0; i < pieces.size(); ++i) {
+      ntok_ = n_gen[i];
+      const std::string& text = pieces[i];
+      if (text.empty()) continue;
+      if (t_first_ == 0) t_first_ = now_s();
+      s += head_;
+      json_escape_append(s, text.data(), text.size());
+      s += mid_;
+      s += "{\"prompt_tokens\":" + std::to_string(prompt_) + ",\"completion_tokens\":" + std::to_string(ntok_) +
+           ",\"total_tokens\":" + std::to_string(prompt_ + ntok_) + "}";
+      s += tail_;
+    }
+    if (s.empty()) return srv_->is_open(conn_);
+    return srv_->stream_write(conn_, s);
+  }
+
   // Raw final bytes (final chunk + [DONE]) and end of the chunked body.
   bool finish(const std::string& raw) {
     if (done_) return false;
@@ -650,11 +674,70 @@ class SseSink {
   bool done_ = false;
 };
 
+// Post-process one device-resident multi-step decode run for every row in C++ (the per-token
+// Python path cost ~4 us x rows x steps on the engine thread): detokenise with stop-string
+// hold-back, apply EOS / max_tokens / context limits, and write each streaming row's new SSE
+// events with a single socket write.  reason: 0 running, 1 eos, 2 stop string, 3 length,
+// 4 client gone.
+py::tuple emit_run(py::array_t<int32_t, py::array::c_style | py::array::forcecast> hist, int K, int B,
+                   py::list streams, py::list sinks, py::array_t<int32_t, py::array::c_style | py::array::forcecast> st,
+                   std::vector<int32_t> eog, int ctx) {
+  const int ld = (int)hist.shape(1);
+  const int32_t* H = hist.data();
+  const int32_t* S = st.data();
+  std::vector<la::TextStream*> ts(B, nullptr);
+  std::vector<SseSink*> sk(B, nullptr);
+  for (int b = 0; b < B; ++b) {
+    if (!streams[b].is_none()) ts[b] = streams[b].cast<la::TextStream*>();
+    if (!sinks[b].is_none()) sk[b] = sinks[b].cast<SseSink*>();
+  }
+  std::vector<int> nacc(B, 0), reason(B, 0);
+  std::vector<std::string> texts(B);
+  {
+    py::gil_scoped_release rel;
+    std::vector<std::string> pieces;
+    std::vector<int> ngen;
+    for (int b = 0; b < B; ++b) {
+      const int32_t* row = S + 5 * b;
+      int n_gen = row[0];
+      const int max_tokens = row[1], n_prompt = row[2], ignore_eos = row[3], active = row[4];
+      if (!active || !ts[b]) continue;
+      pieces.clear();
+      ngen.clear();
+      int rs = 0, acc = 0;
+      for (int k = 0; k < K; ++k) {
+        const int32_t tok = H[(long)k * ld + b];
+        ++n_gen;
+        ++acc;
+        if (!ignore_eos && std::find(eog.begin(), eog.end(), tok) != eog.end()) {
+          rs = 1;
+          break;
+        }
+        auto r = ts[b]->push_raw(tok);
+        pieces.push_back(std::move(r.first));
+        ngen.push_back(n_gen);
+        if (r.second) { rs = 2; break; }
+        if (max_tokens > 0 && n_gen >= max_tokens) { rs = 3; break; }
+        if (n_prompt + n_gen >= ctx) { rs = 3; break; }
+      }
+      if (sk[b]) {
+        if (!sk[b]->push_many(pieces, ngen) && rs == 0) rs = 4;
+      } else {
+        for (auto& p : pieces) texts[b] += p;
+      }
+      nacc[b] = acc;
+      reason[b] = rs;
+    }
+  }
+  py::list out_texts;
+  for (int b = 0; b < B; ++b) out_texts.append(texts[b].empty() ? py::object(py::none()) : py::object(py::bytes(texts[b])));
+  return py::make_tuple(py::array_t<int32_t>(B, nacc.data()), py::array_t<int32_t>(B, reason.data()), out_texts);
+}
+
 }  // namespace lahttp
 
-PYBIND11_MODULE(_la_http, m) {
+void register_http(py::module& m) {
   using namespace lahttp;
-  m.doc() = "localai_amd native HTTP/1.1 server + SSE token sinks";
   py::class_<Server>(m, "Server")
       .def(py::init<const std::string&, int, int>(), py::arg("host"), py::arg("port"), py::arg("backlog") = 4096)
       .def_property_readonly("port", &Server::port)
@@ -674,11 +757,13 @@ PYBIND11_MODULE(_la_http, m) {
       .def(py::init<Server*, uint64_t, std::string, std::string, std::string, int>(), py::keep_alive<1, 2>())
       .def("push", &SseSink::push, py::arg("text"), py::arg("completion_tokens") = 0,
            py::call_guard<py::gil_scoped_release>())
+      .def("push_many", &SseSink::push_many, py::call_guard<py::gil_scoped_release>())
       .def("finish", &SseSink::finish, py::call_guard<py::gil_scoped_release>())
       .def("set_prompt_tokens", &SseSink::set_prompt_tokens)
       .def("open", &SseSink::open)
       .def_property_readonly("ttft", &SseSink::ttft)
       .def_property_readonly("tokens", &SseSink::tokens);
+  m.def("emit_run", &emit_run);
   m.def("json_escape", [](const std::string& s) {
     std::string o;
     json_escape_append(o, s.data(), s.size());

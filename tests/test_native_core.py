@@ -123,3 +123,33 @@ def test_vocab_decode(n):
     v = _vocab()
     ids = [1, 2] * n
     assert v.decode(ids) == b"Hello" * n
+
+
+def test_emit_run_matches_python_semantics():
+    """Native multi-step token emitter vs. the per-token Python rules (EOS, stop strings with
+    hold-back, max_tokens, context limit)."""
+    pieces = [b"", b"Hel", b"lo", b" wor", b"ld", b"<eot>", b"ST", b"OP", b"!"]
+    v = core.Vocab(pieces)
+    K, B = 6, 5
+    hist = np.array([[1, 1, 1, 1, 1],
+                     [2, 2, 6, 2, 2],
+                     [3, 5, 7, 3, 3],
+                     [4, 3, 8, 4, 4],
+                     [8, 4, 8, 8, 8],
+                     [8, 8, 8, 8, 8]], dtype=np.int32)
+    streams = [core.TextStream(v, ["STOP"] if j == 2 else []) for j in range(B)]
+    # n_gen, max_tokens, n_prompt, ignore_eos, active
+    st = np.array([[0, -1, 3, 0, 1],      # runs all 6 tokens
+                   [0, -1, 3, 0, 1],      # EOS at k=2
+                   [0, -1, 3, 0, 1],      # stop string STOP at k=2
+                   [2, 5, 3, 0, 1],       # max_tokens hit after 3 tokens
+                   [0, -1, 508, 0, 1]],   # context 512 hit after 4 tokens
+                  dtype=np.int32)
+    n_acc, reason, texts = core.emit_run(hist, K, B, streams, [None] * B, st, [5], 512)
+    assert list(n_acc) == [6, 3, 3, 3, 4]
+    assert list(reason) == [0, 1, 2, 3, 3]
+    assert texts[0] == b"Hello world!!"
+    assert texts[1] == b"Hello"
+    assert texts[2] is None or texts[2] == b"Hel"
+    assert texts[3] == b"Hello wor"
+    assert texts[4] == b"Hello world"
