@@ -130,6 +130,17 @@ class EngineServicer:
             ctx = request.ContextSize or 2048
             if request.MaxModelLen:
                 ctx = request.MaxModelLen
+            from ..gguf import GGUFReader
+            if GGUFReader(path).architecture in ("bert", "nomic-bert"):
+                # sentence-embedding encoder (bert-embeddings / sentencetransformers backends)
+                from ..models.bert import BertConfig, BertEmbedder
+                loop = asyncio.get_running_loop()
+                emb = await loop.run_in_executor(None, lambda: BertEmbedder(BertConfig(path, dev, ctx)))
+                with self._lock:
+                    self.engine, self.loaded_path = emb, os.path.abspath(path)
+                    self.model_name = os.path.basename(path)
+                    self.state = pb.StatusResponse.READY
+                return pb.Result(success=True, message="Loaded")
             cfg = EngineConfig(
                 model_path=path, device=dev, context_size=ctx,
                 max_num_seqs=int(os.environ.get("LOCALAI_MAX_NUM_SEQS", os.environ.get("LLAMACPP_PARALLEL", "256")) or 256),

@@ -338,3 +338,56 @@ def write_mmproj(path: str, out_dim: int, dim: int = 1024, n_layer: int = 23, he
         w.add_tensor(name, shape, t, quantize(a, t))
     w.write()
     return path
+
+
+def write_bert(path: str, dim: int = 384, n_layer: int = 6, heads: int = 12, ffn: int = 1536, ctx: int = 512,
+               seed: int = 0, std: float = 0.05, words: Optional[List[str]] = None) -> str:
+    """Random-init llama.cpp-style `bert` GGUF (all-MiniLM-L6-v2 geometry by default) with a small
+    WordPiece vocabulary (specials, U+2581-prefixed word pieces, bare continuation pieces)."""
+    words = words or ("the a an of to and in is it that for on with as was at by be this are from or have "
+                      "model server token request graph kernel memory stream batch hello world image text "
+                      "quick brown fox dog cat red green blue gpu fast slow").split()
+    toks = ["[PAD]", "[UNK]", "[CLS]", "[SEP]", "[MASK]"]
+    toks += ["▁" + c for c in ".,!?;:'\"()-"]
+    toks += ["▁" + w for w in words]
+    toks += list("abcdefghijklmnopqrstuvwxyz0123456789")
+    toks += ["▁" + c for c in "abcdefghijklmnopqrstuvwxyz0123456789"]
+    w = GGUFWriter(path, "bert")
+    w.add_string("general.name", "synthetic-minilm")
+    w.add_uint32("bert.context_length", ctx)
+    w.add_uint32("bert.embedding_length", dim)
+    w.add_uint32("bert.feed_forward_length", ffn)
+    w.add_uint32("bert.block_count", n_layer)
+    w.add_uint32("bert.attention.head_count", heads)
+    w.add_float32("bert.attention.layer_norm_epsilon", 1e-12)
+    w.add_bool("bert.attention.causal", False)
+    w.add_uint32("bert.pooling_type", 1)
+    w.add_string("tokenizer.ggml.model", "bert")
+    w.add_array("tokenizer.ggml.tokens", toks, GGUFValueType.STRING)
+    w.add_array("tokenizer.ggml.token_type", [3] * 5 + [1] * (len(toks) - 5), GGUFValueType.INT32)
+    w.add_uint32("tokenizer.ggml.unknown_token_id", 1)
+    w.add_uint32("tokenizer.ggml.cls_token_id", 2)
+    w.add_uint32("tokenizer.ggml.seperator_token_id", 3)
+    w.add_uint32("tokenizer.ggml.padding_token_id", 0)
+    rng = np.random.default_rng(seed)
+    V = len(toks)
+    tensors = [("token_embd.weight", (V, dim)), ("token_types.weight", (2, dim)), ("position_embd.weight", (ctx, dim)),
+               ("token_embd_norm.weight", (dim,)), ("token_embd_norm.bias", (dim,))]
+    for i in range(n_layer):
+        b = f"blk.{i}."
+        for nm in ("attn_q", "attn_k", "attn_v", "attn_output"):
+            tensors += [(b + nm + ".weight", (dim, dim)), (b + nm + ".bias", (dim,))]
+        tensors += [(b + "attn_output_norm.weight", (dim,)), (b + "attn_output_norm.bias", (dim,)),
+                    (b + "ffn_up.weight", (ffn, dim)), (b + "ffn_up.bias", (ffn,)),
+                    (b + "ffn_down.weight", (dim, ffn)), (b + "ffn_down.bias", (dim,)),
+                    (b + "layer_output_norm.weight", (dim,)), (b + "layer_output_norm.bias", (dim,))]
+    for name, shape in tensors:
+        n = int(np.prod(shape))
+        if name.endswith("norm.weight"):
+            a = (1.0 + 0.05 * rng.standard_normal(n)).astype(np.float32)
+        else:
+            a = (std * rng.standard_normal(n)).astype(np.float32)
+        t = GGMLType.F16 if len(shape) >= 2 else GGMLType.F32
+        w.add_tensor(name, shape, t, quantize(a, t))
+    w.write()
+    return path
