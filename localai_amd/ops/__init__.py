@@ -44,6 +44,7 @@ def lib():
         P, I, F, LNG = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_long
         sig = {
             "la_qgemm_skinny": [I, P, P, P, P, I, I, P, I, I, I, P, I, LNG, P],
+            "la_qgemm_mid": [I, P, P, P, P, I, I, P, I, I, I, P, I, LNG, P],
             "la_add_norm": [P, P, LNG, I, P, I, P, P, P, I, I, F, I, P, P],
             "la_rope_kv": [P, LNG, I, P, P, P, P, I, I, I, I, I, I, P, P, P, I, P],
             "la_act": [P, LNG, I, P, P, I, I, I, P],
@@ -275,6 +276,77 @@ def pick_splits(N: int, K: int, M: int) -> int:
 
 
 SKINNY_MAX_M = 64
+MID_MAX_M = 256          # 64 < M <= MID_MAX_M: quantised mid-M MFMA GEMM (gemm_mid.hip) or hipBLASLt
+MID_FMTS = (FMT_Q4_K, FMT_Q6_K, FMT_Q8_0)
+GEMM_AUTOTUNE = True
+# (M, K, ((fmt, N), ...)) -> ("mid", S) | ("blas", 0); filled by _autotune_mid at warm-up (eager
+# runs before each decode-graph capture), consulted during capture / replay.
+_GEMM_CHOICE: dict = {}
+
+
+def _mid_split_ok(K: int, S: int) -> bool:
+    ks = K // 64
+    return S >= 1 and -(-ks // S) * (S - 1) < ks
+
+
+def pick_mid_splits(N: int, K: int, M: int) -> int:
+    """Default split-K for the mid-M GEMM when no tuned choice exists: ~2 workgroups per CU,
+    every split >= 8 K-steps of 64, fp32 slab round trip kept below the weight bytes."""
+    tiles = ((N + 127) // 128) * ((M + 127) // 128)
+    ksteps = K // 64
+    s = max(1, min(ksteps // 8, round(512 / tiles)))
+    while s > 1 and s * M * N * 4 * 2 > N * K:
+        s -= 1
+    while s > 1 and not _mid_split_ok(K, s):
+        s -= 1
+    return s
+
+
+def _run_mid(x, ws, S, out, Ntot):
+    M, K = x.shape
+    col = 0
+    for w in ws:
+        _check(lib().la_qgemm_mid(w.fmt, *w.ptrs(), w.N, w.K, x.data_ptr(), K, M, S, out.data_ptr() + col * 4,
+                                  Ntot, M * Ntot, _stream()), "la_qgemm_mid")
+        col += w.N
+
+
+def _run_blas(x, ws, Ntot):
+    if len(ws) == 1:
+        return torch.matmul(x, ws[0].materialize_bf16().t())
+    y = torch.empty(x.shape[0], Ntot, dtype=torch.bfloat16, device=x.device)
+    col = 0
+    for w in ws:
+        torch.matmul(x, w.materialize_bf16().t(), out=y[:, col:col + w.N])
+        col += w.N
+    return y
+
+
+def _autotune_mid(x, ws, key, Ntot):
+    """Time hipBLASLt (bf16 copy) against the quantised mid-M kernel at a few split-K factors
+    and remember the winner.  The slab variant is charged for the extra fp32 bytes its
+    consumer reads (at ~4 TB/s)."""
+    M, K = x.shape
+    cands = [("blas", 0)] + [("mid", S) for S in (1, 2, 4, 8) if _mid_split_ok(K, S)]
+    outs = {S: torch.empty(S, M, Ntot, dtype=torch.float32, device=x.device) for _, S in cands if S}
+    best, best_t = ("blas", 0), float("inf")
+    for kind, S in cands:
+        fn = (lambda: _run_blas(x, ws, Ntot)) if kind == "blas" else (lambda S=S: _run_mid(x, ws, S, outs[S], Ntot))
+        for _ in range(2):
+            fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(5):
+            fn()
+        e1.record()
+        e1.synchronize()
+        t = e0.elapsed_time(e1) * 1000 / 5
+        if kind == "mid":
+            t += (S * M * Ntot * 4 - M * Ntot * 2) / 4e6
+        if t < best_t:
+            best, best_t = (kind, S), t
+    _GEMM_CHOICE[key] = best
+    return best
 
 
 def linear(x: torch.Tensor, w: QWeight, bias: Optional[torch.Tensor] = None,
@@ -300,6 +372,23 @@ def linear_multi(x: torch.Tensor, ws: Sequence[QWeight], bias: Optional[torch.Te
         raise ValueError("linear: x must be contiguous bf16")
     skinny_ok = all(w.K % 256 == 0 for w in ws)
     use_skinny = (M <= SKINNY_MAX_M and skinny_ok) if force is None else force == "skinny"
+    mid_ok = skinny_ok and all(w.fmt in MID_FMTS for w in ws)
+    S = 0
+    if force == "mid":
+        S = min(pick_mid_splits(w.N, w.K, M) for w in ws)
+    elif force is None and not use_skinny and M <= MID_MAX_M and mid_ok:
+        key = (M, K, tuple((w.fmt, w.N) for w in ws))
+        choice = _GEMM_CHOICE.get(key)
+        if choice is None and GEMM_AUTOTUNE and not torch.cuda.is_current_stream_capturing():
+            choice = _autotune_mid(x, ws, key, Ntot)
+        if choice is not None and choice[0] == "mid":
+            S = choice[1]
+    if S:
+        out = out_slabs
+        if out is None or out.shape != (S, M, Ntot):
+            out = torch.empty(S, M, Ntot, dtype=torch.float32, device=x.device)
+        _run_mid(x, ws, S, out, Ntot)
+        return Partial(out, bias)
     if use_skinny:
         S = min(pick_splits(w.N, w.K, M) for w in ws)
         nsb = K // 256
@@ -315,14 +404,7 @@ def linear_multi(x: torch.Tensor, ws: Sequence[QWeight], bias: Optional[torch.Te
                                          M * Ntot, _stream()), "la_qgemm_skinny")
             col += w.N
         return Partial(out, bias)
-    if len(ws) == 1:
-        return Partial(torch.matmul(x, ws[0].materialize_bf16().t()), bias)
-    y = torch.empty(M, Ntot, dtype=torch.bfloat16, device=x.device)
-    col = 0
-    for w in ws:
-        torch.matmul(x, w.materialize_bf16().t(), out=y[:, col:col + w.N])
-        col += w.N
-    return Partial(y, bias)
+    return Partial(_run_blas(x, ws, Ntot), bias)
 
 
 # ---------------------------------------------------------------------------------------

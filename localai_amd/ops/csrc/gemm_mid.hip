@@ -1,0 +1,303 @@
+// Quantised mid-M GEMM (batched decode, 64 < M <= a few hundred rows):
+//   out[s][m][n] = sum_{k in split s} X[m,k] * W[n,k]      (fp32 split-K slabs)
+//
+// Replaces the bf16 hipBLASLt call on a dequantised weight copy that the engine used
+// for 64 < M (SURVEY §2.8 K5/K6 mmq, [external]).  Why a second kernel next to the skinny
+// one: at M = 128..256 the in-register dequant of the skinny kernel (each wave dequantises
+// the fragments it multiplies) costs ~22 VALU ops per 8 weights, which only hides under
+// the MFMAs when ONE dequantised fragment feeds >= ~11 of them.  Here the weight tile is
+// dequantised ONCE per workgroup into LDS (16-weight units, 16-B raw loads) and shared by
+// all waves, like the activation tile:
+//   * tile BM (M) x 128 (N) x 64 (K) with BM = 128 (4 waves, 2x2) for M <= 128 and BM = 256
+//     (8 waves, 4x2) above, so the dequant cost per MFMA halves as M grows; each wave owns a
+//     64x64 output tile = 4x4 v_mfma_f32_16x16x32_bf16 accumulators;
+//   * both operands staged through padded LDS rows (row stride 144 B: the 16 rows a
+//     ds_read_b128 lane group touches land on 16 distinct 16-B bank slots);
+//   * a 3-deep register ring feeds a 2-buffer LDS pipeline: the raw quant bytes + X chunks
+//     of K-step t+3 are in flight while the MFMAs of step t run; dequant/LDS write after;
+//   * split-K over grid.y, M tiles over grid.z; the fp32 slabs are summed by the
+//     consuming kernel's prologue (same contract as the skinny GEMM).
+#include "qweight.h"
+
+namespace la {
+
+constexpr int MD_BN = 128, MD_BK = 64;
+constexpr int MD_LDS = MD_BK + 8;  // bf16 elements per LDS row
+
+// Raw bytes for one staging unit = 16 weights of row n at k = 64*ks + 16*q .. +16 (q = 0..3).
+// Addressing is split into a per-thread 32-bit offset (fixed for the whole K loop, set by
+// init) and a wave-uniform per-K-step base, so every staging load is a saddr+voffset
+// global_load with no per-step 64-bit address VALU work.
+template <int FMT> struct MidRaw;
+
+template <> struct MidRaw<FMT_Q4_K> {
+  struct Addr {
+    uint32_t qs, hdr;
+    int half;
+    LA_DEV void init(const QW& w, int n, int q) {
+      qs = (uint32_t)n * (w.K >> 1) + 16 * (q & 1);
+      hdr = (uint32_t)n * (w.K >> 8) * 16;
+      half = q >> 1;
+    }
+  };
+  u32x4 qs;
+  u32x4 hdr;
+  LA_DEV void load(const QW& w, const Addr& a, int ks) {
+    qs = *(const u32x4*)(w.p0 + 32 * ks + a.qs);
+    hdr = *(const u32x4*)(w.p1 + 16 * (ks >> 2) + a.hdr);
+  }
+  LA_DEV void deq(const Addr& ad, int ks, bf16x8 out[2]) const {
+    const int half = ad.half;
+    uint32_t sc, m;
+    q4k_scale_min(hdr.y, hdr.z, hdr.w, 2 * (ks & 3) + half, sc, m);
+    const float D = h2f(hdr.x & 0xFFFFu) * (float)sc, Mv = -h2f(hdr.x >> 16) * (float)m;
+    const uint32_t v[4] = {qs.x, qs.y, qs.z, qs.w};
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const uint32_t a = (v[2 * j] >> (4 * half)) & 0x0F0F0F0Fu, b = (v[2 * j + 1] >> (4 * half)) & 0x0F0F0F0Fu;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        out[j][i] = (bf16)fmaf(D, (float)((a >> (8 * i)) & 0xFFu), Mv);
+        out[j][i + 4] = (bf16)fmaf(D, (float)((b >> (8 * i)) & 0xFFu), Mv);
+      }
+    }
+  }
+};
+
+template <> struct MidRaw<FMT_Q6_K> {
+  struct Addr {
+    uint32_t ql, qh, sc, d;
+    int qhi;
+    LA_DEV void init(const QW& w, int n, int q) {
+      qhi = q >> 1;
+      ql = (uint32_t)n * (w.K >> 1) + 32 * qhi + 16 * (q & 1);
+      qh = (uint32_t)n * (w.K >> 2) + 16 * (q & 1);
+      sc = (uint32_t)n * (w.K >> 4) + 2 * qhi + (q & 1);
+      d = (uint32_t)n * (w.K >> 8) * 2;
+    }
+  };
+  u32x4 ql, qh;
+  int8_t sc;
+  uint16_t dbits;
+  LA_DEV void load(const QW& w, const Addr& a, int ks) {
+    // sb*128 + 64*hh == 64*(ks>>1);  sb*64 + 32*hh == 32*(ks>>1);  sb*16 + 8*hh + 4*(c&1) == 8*(ks>>1) + 4*(ks&1)
+    ql = *(const u32x4*)(w.p0 + 64 * (ks >> 1) + a.ql);
+    qh = *(const u32x4*)(w.p1 + 32 * (ks >> 1) + a.qh);
+    sc = *(const int8_t*)(w.p2 + 8 * (ks >> 1) + 4 * (ks & 1) + a.sc);
+    dbits = *(const uint16_t*)(w.p3 + 2 * (ks >> 2) + a.d);
+  }
+  LA_DEV void deq(const Addr& ad, int ks, bf16x8 out[2]) const {
+    const int qi = 2 * (ks & 1) + ad.qhi;
+    const int ls = 4 * (qi >> 1), hs = 2 * qi;
+    const float s = h2f(dbits) * (float)sc;
+    const uint32_t L[4] = {ql.x, ql.y, ql.z, ql.w};
+    const uint32_t H[4] = {qh.x, qh.y, qh.z, qh.w};
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const uint32_t lw = L[2 * j + (i >> 2)], hw = H[2 * j + (i >> 2)];
+        const int sh = 8 * (i & 3);
+        const int v = (int)(((lw >> (sh + ls)) & 0xFu) | (((hw >> (sh + hs)) & 3u) << 4)) - 32;
+        out[j][i] = (bf16)(s * (float)v);
+      }
+    }
+  }
+};
+
+template <> struct MidRaw<FMT_Q8_0> {
+  struct Addr {
+    uint32_t qs, d;
+    LA_DEV void init(const QW& w, int n, int q) {
+      qs = (uint32_t)n * w.K + 16 * q;
+      d = ((uint32_t)n * (w.K >> 5) + (q >> 1)) * 2;
+    }
+  };
+  u32x4 qs;
+  uint16_t dbits;
+  LA_DEV void load(const QW& w, const Addr& a, int ks) {
+    qs = *(const u32x4*)(w.p0 + 64 * ks + a.qs);
+    dbits = *(const uint16_t*)(w.p1 + 4 * ks + a.d);
+  }
+  LA_DEV void deq(const Addr&, int, bf16x8 out[2]) const {
+    const float d = h2f(dbits);
+    const uint32_t v[4] = {qs.x, qs.y, qs.z, qs.w};
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) out[j][i] = (bf16)(d * (float)(int8_t)((v[2 * j + (i >> 2)] >> (8 * (i & 3))) & 0xFFu));
+    }
+  }
+};
+
+// BM = 128 (4 waves, 2x2) or 256 (8 waves, 4x2); every wave owns a 64x64 output tile.
+template <int FMT, int BM>
+__global__ __launch_bounds__(2 * BM, 256 / BM) void qgemm_mid_kernel(QW w, const bf16* __restrict__ X, int ldx,
+                                                                    int M, int ksteps_per_split,
+                                                                    float* __restrict__ out, int ldo, long slab) {
+  constexpr int NT = 2 * BM;                    // threads
+  constexpr int XU = BM * MD_BK / 8 / NT;       // 16-B X chunks per thread per K-step (= 4)
+  constexpr int WU = MD_BN * 4 / NT;            // 16-weight W units per thread (2 or 1)
+  constexpr int BUF = (BM + MD_BN) * MD_LDS;    // bf16 per stage buffer
+  __shared__ __attribute__((aligned(16))) bf16 lds[2 * BUF];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int r = lane & 15, g = lane >> 4;
+  const int N = w.N;
+  const int n0 = blockIdx.x * MD_BN, m0 = blockIdx.z * BM;
+  const int total_ks = w.K / MD_BK;
+  const int ks0 = blockIdx.y * ksteps_per_split;
+  const int ks1 = min(total_ks, ks0 + ksteps_per_split);
+  if (ks0 >= ks1) return;  // uniform per block
+
+  // 3-deep register ring: the raw quant bytes + X chunks of K-step t+3 are issued while the
+  // MFMAs of step t run (HBM latency under load is ~2-3 K-steps of MFMA work).  Loads are
+  // never predicated (clamped instead) so hipcc emits counted vmcnt waits, not vmcnt(0).
+  struct Stage {
+    MidRaw<FMT> raw[WU];
+    bf16x8 xr[XU];
+  };
+  typename MidRaw<FMT>::Addr wad[WU];
+#pragma unroll
+  for (int u = 0; u < WU; ++u) {
+    const int id = tid + u * NT;
+    wad[u].init(w, min(n0 + (id >> 2), N - 1), id & 3);  // clamped rows: garbage, never stored
+  }
+  uint32_t xoff[XU];
+#pragma unroll
+  for (int i = 0; i < XU; ++i) {
+    const int c = tid + i * NT;
+    xoff[i] = (uint32_t)min(m0 + (c >> 3), M - 1) * ldx + (c & 7) * 8;  // rows >= M: never stored
+  }
+  auto issue = [&](Stage& S, int ks) {
+#pragma unroll
+    for (int u = 0; u < WU; ++u) S.raw[u].load(w, wad[u], ks);
+    const bf16* xk = X + ks * MD_BK;
+#pragma unroll
+    for (int i = 0; i < XU; ++i) S.xr[i] = *(const bf16x8*)(xk + xoff[i]);
+  };
+  auto commit = [&](const Stage& S, int ks, int buf) {
+    bf16* xs = lds + buf * BUF;
+    bf16* ws = xs + BM * MD_LDS;
+#pragma unroll
+    for (int i = 0; i < XU; ++i) {
+      const int c = tid + i * NT;
+      *(bf16x8*)(xs + (c >> 3) * MD_LDS + (c & 7) * 8) = S.xr[i];
+    }
+#pragma unroll
+    for (int u = 0; u < WU; ++u) {
+      const int id = tid + u * NT;
+      bf16x8 d[2];
+      S.raw[u].deq(wad[u], ks, d);
+      bf16* dst = ws + (id >> 2) * MD_LDS + 16 * (id & 3);
+      *(bf16x8*)dst = d[0];
+      *(bf16x8*)(dst + 8) = d[1];
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](int buf) {
+    const bf16* xs = lds + buf * BUF;
+    const bf16* ws = xs + BM * MD_LDS;
+#pragma unroll
+    for (int kk = 0; kk < MD_BK; kk += 32) {
+      bf16x8 a[4], b[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        a[t] = *(const bf16x8*)(xs + (wm * 64 + t * 16 + r) * MD_LDS + kk + 8 * g);
+        b[t] = *(const bf16x8*)(ws + (wn * 64 + t * 16 + r) * MD_LDS + kk + 8 * g);
+      }
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mt], b[nt], acc[mt][nt], 0, 0, 0);
+    }
+  };
+
+  const int last = ks1 - 1;
+  Stage s0, s1, s2;
+  issue(s0, ks0);
+  issue(s1, min(ks0 + 1, last));
+  issue(s2, min(ks0 + 2, last));
+  commit(s0, ks0, 0);
+  __syncthreads();
+  // step t: stage `fr` (already in LDS) refills with t+3; stage `nx` (t+1) is committed to LDS
+#define MID_STEP(KS, fr, nx, BUFI)                 \
+  {                                                \
+    issue(fr, min((KS) + 3, last));                \
+    compute(BUFI);                                 \
+    commit(nx, min((KS) + 1, last), (BUFI) ^ 1);   \
+    __syncthreads();                               \
+  }
+  int buf = 0;
+  for (int ks = ks0;; ks += 3) {
+    MID_STEP(ks, s0, s1, buf);
+    buf ^= 1;
+    if (ks + 1 >= ks1) break;
+    MID_STEP(ks + 1, s1, s2, buf);
+    buf ^= 1;
+    if (ks + 2 >= ks1) break;
+    MID_STEP(ks + 2, s2, s0, buf);
+    buf ^= 1;
+    if (ks + 3 >= ks1) break;
+  }
+#undef MID_STEP
+
+  float* o = out + (size_t)blockIdx.y * slab;
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) {
+    const int n = n0 + wn * 64 + nt * 16 + r;
+    if (n >= N) continue;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = m0 + wm * 64 + mt * 16 + 4 * g + i;
+        if (m < M) o[(size_t)m * ldo + n] = acc[mt][nt][i];
+      }
+    }
+  }
+}
+
+template <int FMT>
+static void launch_mid(const QW& w, const bf16* X, int ldx, int M, int splits, float* out, int ldo, long slab,
+                       hipStream_t st) {
+  const int total = w.K / MD_BK;
+  const int per = (total + splits - 1) / splits;
+  if (M <= 128) {
+    dim3 grid((w.N + MD_BN - 1) / MD_BN, splits, 1);
+    hipLaunchKernelGGL((qgemm_mid_kernel<FMT, 128>), grid, dim3(256), 0, st, w, X, ldx, M, per, out, ldo, slab);
+  } else {
+    dim3 grid((w.N + MD_BN - 1) / MD_BN, splits, (M + 255) / 256);
+    hipLaunchKernelGGL((qgemm_mid_kernel<FMT, 256>), grid, dim3(512), 0, st, w, X, ldx, M, per, out, ldo, slab);
+  }
+}
+
+}  // namespace la
+
+// C ABI ---------------------------------------------------------------------------
+// splits must satisfy ceil(K/64 / splits) * (splits-1) < K/64 so every slab is written.
+extern "C" int la_qgemm_mid(int fmt, const void* p0, const void* p1, const void* p2, const void* p3, int N, int K,
+                            const void* X, int ldx, int M, int splits, void* out, int ldo, long slab, void* stream) {
+  using namespace la;
+  if (M < 1 || (K & 255) || splits < 1 || ldo < N || ldx < K || slab < (long)M * ldo) return -1;
+  if ((long)N * K >= (1L << 31) || (long)M * ldx >= (1L << 31)) return -1;  // 32-bit staging offsets
+  const int total = K / MD_BK, per = (total + splits - 1) / splits;
+  if (per * (splits - 1) >= total) return -1;
+  QW w{(const uint8_t*)p0, (const uint8_t*)p1, (const uint8_t*)p2, (const uint8_t*)p3, N, K};
+  hipStream_t st = (hipStream_t)stream;
+  const bf16* x = (const bf16*)X;
+  float* o = (float*)out;
+  switch (fmt) {
+    case FMT_Q4_K: launch_mid<FMT_Q4_K>(w, x, ldx, M, splits, o, ldo, slab, st); break;
+    case FMT_Q6_K: launch_mid<FMT_Q6_K>(w, x, ldx, M, splits, o, ldo, slab, st); break;
+    case FMT_Q8_0: launch_mid<FMT_Q8_0>(w, x, ldx, M, splits, o, ldo, slab, st); break;
+    default: return -2;
+  }
+  return (int)hipGetLastError();
+}

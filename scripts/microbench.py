@@ -41,7 +41,20 @@ for M in (1, 8, 16, 32, 64):
         S = ops.pick_splits(w.N, w.K, M)
         res[f"skinny_{k}_M{M}"] = (round(us, 2), round(gbs, 1), S)
         print(f"skinny {k:8s} M={M:3d} S={S:2d} {us:8.2f} us  {gbs:7.1f} GB/s", flush=True)
-for M in (128, 256):
+for M in (96, 128, 256, 512):
+    for k, w in W.items():
+        x = torch.randn(M, w.K, device=dev).to(torch.bfloat16)
+        S0 = ops.pick_mid_splits(w.N, w.K, M)
+        best = None
+        for S in sorted({1, 2, 3, 4, 6, 8, S0}):
+            if -(-(w.K // 64) // S) * (S - 1) >= w.K // 64:
+                continue
+            out = torch.empty(S, M, w.N, dtype=torch.float32, device=dev)
+            us = timeit(lambda: ops.lib().la_qgemm_mid(w.fmt, *w.ptrs(), w.N, w.K, x.data_ptr(), w.K, M, S,
+                                                       out.data_ptr(), w.N, M * w.N, ops._stream()), iters=20)
+            tf = 2 * M * w.N * w.K / us / 1e6
+            res[f"mid_{k}_M{M}_S{S}"] = (round(us, 2), round(tf, 1))
+            print(f"mid {k:8s} M={M:3d} S={S:2d}{'*' if S == S0 else ' '} {us:8.2f} us  {tf:7.1f} TF/s", flush=True)
     for k, w in W.items():
         x = torch.randn(M, w.K, device=dev).to(torch.bfloat16)
         wb = w.materialize_bf16()
@@ -49,6 +62,8 @@ for M in (128, 256):
         tf = 2 * M * w.N * w.K / us / 1e6
         res[f"hipblaslt_{k}_M{M}"] = (round(us, 2), round(tf, 1))
         print(f"hipblaslt {k:8s} M={M:3d} {us:8.2f} us  {tf:7.1f} TF/s  {wb.numel()*2/us/1e3:7.1f} GB/s", flush=True)
+if os.environ.get("MB_ONLY_GEMM"):
+    sys.exit(0)
 # attention decode
 Hq, Hkv, Dh, BS = 32, 8, 128, 32
 for B, L in ((1, 384), (1, 4096), (64, 384), (256, 384), (64, 2048)):

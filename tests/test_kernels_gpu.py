@@ -50,6 +50,33 @@ def test_skinny_gemm_splits_and_tail():
         assert (out.sum(0).cpu() - ref).abs().max().item() < 2e-2
 
 
+@pytest.mark.parametrize("t", [GGMLType.Q4_K, GGMLType.Q6_K, GGMLType.Q8_0])
+@pytest.mark.parametrize("M", [65, 128, 200, 256, 300])
+def test_mid_gemm(t, M):
+    """Mid-M quantised MFMA GEMM (LDS-dequantised weight tiles) vs the fp32 reference; N not a
+    multiple of the 128-wide tile, M spanning several 128-row tiles."""
+    N, K = 200, 1536
+    w = _qw(N, K, t, seed=7)
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    y = ops.linear(x, w, force="mid").dense()
+    ref = x.float().cpu() @ w.ref.t()
+    err = (y.cpu() - ref).abs().max().item()
+    assert err < 2e-2 * max(1.0, ref.abs().max().item()), err
+
+
+def test_mid_gemm_splits():
+    N, K, M = 130, 2048, 150
+    w = _qw(N, K, GGMLType.Q4_K, seed=8)
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    ref = x.float().cpu() @ w.ref.t()
+    for S in (1, 3, 4, 8):
+        out = torch.full((S, M, N), float("nan"), dtype=torch.float32, device=DEV)
+        rc = ops.lib().la_qgemm_mid(w.fmt, *w.ptrs(), N, K, x.data_ptr(), K, M, S, out.data_ptr(), N, M * N,
+                                    ops._stream())
+        assert rc == 0
+        assert (out.sum(0).cpu() - ref).abs().max().item() < 3e-2
+
+
 @pytest.mark.parametrize("M", [3, 100])
 def test_linear_multi_mixed_formats(M):
     K = 512
