@@ -26,12 +26,25 @@ from .utils.downloader import download_file, filename_from_url, looks_like_url, 
 log = logging.getLogger("localai_amd.startup")
 
 
-def install_models(galleries: List[dict], models_path: str, models: List[str]) -> List[str]:
-    """InstallModels: URL -> download file; local YAML -> copy as <md5>.yaml; else gallery name."""
+def install_models(galleries: List[dict], models_path: str, models: List[str], library_url: str = "") -> List[str]:
+    """InstallModels: remote/embedded library name -> config or URL; URL -> download file; local
+    YAML -> copy as <md5>.yaml; else gallery name."""
+    from . import library
     errors = []
+    lib = {}
+    if library_url:
+        try:
+            lib = library.remote_library_shorteners(library_url, models_path)
+        except Exception as e:  # best effort, like the reference
+            log.warning("[startup] remote library %s: %s", library_url, e)
     for url in models:
         try:
-            if looks_like_url(url) and not url.startswith(("oci://", "ollama://")):
+            url = library.model_short_url(lib.get(url) or url)
+            if library.exists_in_library(url):
+                name = hashlib.md5(url.encode()).hexdigest()
+                with open(os.path.join(models_path, name + ".yaml"), "wb") as f:
+                    f.write(library.resolve_content(url))
+            elif looks_like_url(url) and not url.startswith(("oci://", "ollama://")):
                 fn = filename_from_url(url)
                 verify_path(fn, models_path)
                 dst = os.path.join(models_path, fn)
@@ -130,7 +143,7 @@ def startup(app: ApplicationConfig) -> AppState:
         if d:
             os.makedirs(d, exist_ok=True)
     if app.model_urls:
-        install_models(app.galleries, app.models_path, app.model_urls)
+        install_models(app.galleries, app.models_path, app.model_urls, app.remote_library)
     state = AppState(app)
     lo = state.load_options()
     state.configs.load_from_path(app.models_path, lo)

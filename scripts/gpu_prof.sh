@@ -1,8 +1,13 @@
+# rocprofv3 kernel profiles of the engine benches (C=1 and C=256, default max_tokens).
+# The raw traces stay on the box; only the markdown summaries come back.
 set -o pipefail
 R=$GRAFT_REPO_ROOT; cd $R && mkdir -p gpurun_out
 export LOCALAI_AMD_CACHE=/tmp/la_cache
-timeout -k 10 600 python bench.py --mode engine --steps 2 --warmup 1 --concurrency 128 > gpurun_out/bench_engine128.log 2>&1 && echo B128 && tail -1 gpurun_out/bench_engine128.log &&
-timeout -k 10 600 python bench.py --mode engine --steps 2 --warmup 1 --concurrency 256 > gpurun_out/bench_engine256.log 2>&1 && echo B256 && tail -1 gpurun_out/bench_engine256.log &&
-timeout -k 10 300 python bench.py --mode engine --steps 2 --warmup 1 --concurrency 1 --max-tokens 128 > gpurun_out/bench_engine1.log 2>&1 && echo B1 && tail -1 gpurun_out/bench_engine1.log &&
+P=/tmp/la_prof
 cd /tmp && export TMPDIR=/tmp &&
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof64 -o run --output-format csv -- python3 $R/bench.py --mode engine --steps 1 --warmup 0 --concurrency 64 --max-tokens 64 > $R/gpurun_out/prof64.log 2>&1 && echo PROF_OK
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $P/c256 -o run --output-format csv -- python3 $R/bench.py --mode engine --steps 1 --warmup 1 --concurrency 256 > $R/gpurun_out/prof_c256.log 2>&1 &&
+tail -1 $R/gpurun_out/prof_c256.log | cut -c1-400 &&
+python3 $R/scripts/prof_summary.py $P/c256 "Engine C=256, Llama-3-8B Q4_K_M" > $R/gpurun_out/prof_c256.md &&
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $P/c1 -o run --output-format csv -- python3 $R/bench.py --mode engine --steps 1 --warmup 1 --concurrency 1 > $R/gpurun_out/prof_c1.log 2>&1 &&
+tail -1 $R/gpurun_out/prof_c1.log | cut -c1-400 &&
+python3 $R/scripts/prof_summary.py $P/c1 "Engine C=1, Llama-3-8B Q4_K_M" > $R/gpurun_out/prof_c1.md && echo PROF_OK
