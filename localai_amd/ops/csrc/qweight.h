@@ -43,15 +43,18 @@ LA_DEV uint32_t byte_of12(uint32_t a, uint32_t b, uint32_t c, int i) {
   return (w >> (8 * (i & 3))) & 0xFFu;
 }
 
-// ggml get_scale_min_k4 on the 12 packed bytes (a,b,c little-endian dwords)
+// ggml get_scale_min_k4 on the 12 packed bytes (a,b,c little-endian dwords).  Branch-free:
+// j is per-lane in the GEMV kernels, and an exec-masked if/else there makes hipcc drain
+// the weight-load ring (vmcnt) around each arm.
 LA_DEV void q4k_scale_min(uint32_t a, uint32_t b, uint32_t c, int j, uint32_t& sc, uint32_t& m) {
-  if (j < 4) {
-    sc = byte_of12(a, b, c, j) & 63u;
-    m = byte_of12(a, b, c, j + 4) & 63u;
-  } else {
-    sc = (byte_of12(a, b, c, j + 4) & 0xFu) | ((byte_of12(a, b, c, j - 4) >> 6) << 4);
-    m = (byte_of12(a, b, c, j + 4) >> 4) | ((byte_of12(a, b, c, j) >> 6) << 4);
-  }
+  const bool lo = j < 4;
+  const uint32_t bj = byte_of12(a, b, c, j);                  // j < 4: scale byte
+  const uint32_t bj4 = byte_of12(a, b, c, j + 4);             // j < 4: min byte; j >= 4: low nibbles
+  const uint32_t bjm4 = byte_of12(a, b, c, lo ? j : j - 4);   // j >= 4: high bits of the scale
+  const uint32_t sc_hi = (bj4 & 0xFu) | ((bjm4 >> 6) << 4);
+  const uint32_t m_hi = (bj4 >> 4) | ((bj >> 6) << 4);
+  sc = lo ? (bj & 63u) : sc_hi;
+  m = lo ? (bj4 & 63u) : m_hi;
 }
 
 template <int FMT> struct WFrag;
