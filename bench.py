@@ -118,6 +118,10 @@ def main():
     t0 = time.time()
     eng.warmup()
     t_capture = time.time() - t0
+    if os.environ.get("BENCH_DUMP_GEMM") and rank == 0:
+        from localai_amd import ops
+        for k, v in sorted(ops._GEMM_CHOICE.items(), key=str):
+            print(f"gemm choice M={k[0]} K={k[1]} ws={k[2]} -> {v}", file=sys.stderr)
 
     msgs = user_messages(eng.tokenizer, args.concurrency, args.prompt_len, seed=rank)
     if args.mode == "http":

@@ -44,7 +44,7 @@ def lib():
         P, I, F, LNG = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_long
         sig = {
             "la_qgemm_skinny": [I, P, P, P, P, I, I, P, I, I, I, P, I, LNG, P],
-            "la_qgemm_mid": [I, P, P, P, P, I, I, P, I, I, I, P, I, LNG, P],
+            "la_qgemm_mid": [I, P, P, P, P, I, I, P, I, I, I, P, I, LNG, I, P],
             "la_add_norm": [P, P, LNG, I, P, I, P, P, P, I, I, F, I, P, P],
             "la_rope_kv": [P, LNG, I, P, P, P, P, I, I, I, I, I, I, P, P, P, I, P],
             "la_act": [P, LNG, I, P, P, I, I, I, P],
@@ -302,12 +302,12 @@ def pick_mid_splits(N: int, K: int, M: int) -> int:
     return s
 
 
-def _run_mid(x, ws, S, out, Ntot):
+def _run_mid(x, ws, S, out, Ntot, tile=0):
     M, K = x.shape
     col = 0
     for w in ws:
         _check(lib().la_qgemm_mid(w.fmt, *w.ptrs(), w.N, w.K, x.data_ptr(), K, M, S, out.data_ptr() + col * 4,
-                                  Ntot, M * Ntot, _stream()), "la_qgemm_mid")
+                                  Ntot, M * Ntot, tile, _stream()), "la_qgemm_mid")
         col += w.N
 
 
@@ -322,29 +322,47 @@ def _run_blas(x, ws, Ntot):
     return y
 
 
+_FLUSH: dict = {}
+
+
+def _cold_caches(device):
+    """Evict L2 and the 256 MiB Infinity Cache (write a 384 MiB scratch buffer), so a timed
+    GEMM reads its weights from HBM as it does in the engine, where every decode step streams
+    the whole model once."""
+    buf = _FLUSH.get(device)
+    if buf is None:
+        buf = _FLUSH[device] = torch.empty(384 << 20, dtype=torch.uint8, device=device)
+    buf.fill_(1)
+
+
 def _autotune_mid(x, ws, key, Ntot):
     """Time hipBLASLt (bf16 copy) against the quantised mid-M kernel at a few split-K factors
-    and remember the winner.  The slab variant is charged for the extra fp32 bytes its
-    consumer reads (at ~4 TB/s)."""
+    with COLD weights (caches flushed before every timed call: warm timings favour the 3.6x
+    larger bf16 copy), and remember the winner.  The slab variant is charged for the extra
+    fp32 bytes its consumer reads (at ~4 TB/s)."""
     M, K = x.shape
-    cands = [("blas", 0)] + [("mid", S) for S in (1, 2, 4, 8) if _mid_split_ok(K, S)]
-    outs = {S: torch.empty(S, M, Ntot, dtype=torch.float32, device=x.device) for _, S in cands if S}
-    best, best_t = ("blas", 0), float("inf")
-    for kind, S in cands:
-        fn = (lambda: _run_blas(x, ws, Ntot)) if kind == "blas" else (lambda S=S: _run_mid(x, ws, S, outs[S], Ntot))
-        for _ in range(2):
+    tiles = (22, 21) if M <= 128 else (42, 41, 22, 21)
+    cands = [("blas", 0, 0)] + [("mid", S, t) for t in tiles for S in (1, 2, 4, 8) if _mid_split_ok(K, S)]
+    outs = {S: torch.empty(S, M, Ntot, dtype=torch.float32, device=x.device) for _, S, _ in cands if S}
+    best, best_t = ("blas", 0, 0), float("inf")
+    for kind, S, t in cands:
+        fn = (lambda: _run_blas(x, ws, Ntot)) if kind == "blas" else \
+            (lambda S=S, t=t: _run_mid(x, ws, S, outs[S], Ntot, t))
+        fn()
+        ts = []
+        for _ in range(3):
+            _cold_caches(x.device)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
             fn()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(5):
-            fn()
-        e1.record()
-        e1.synchronize()
-        t = e0.elapsed_time(e1) * 1000 / 5
+            e1.record()
+            e1.synchronize()
+            ts.append(e0.elapsed_time(e1) * 1000)
+        tt = sorted(ts)[1]
         if kind == "mid":
-            t += (S * M * Ntot * 4 - M * Ntot * 2) / 4e6
-        if t < best_t:
-            best, best_t = (kind, S), t
+            tt += (S * M * Ntot * 4 - M * Ntot * 2) / 4e6
+        if tt < best_t:
+            best, best_t = (kind, S, t), tt
     _GEMM_CHOICE[key] = best
     return best
 
@@ -373,7 +391,7 @@ def linear_multi(x: torch.Tensor, ws: Sequence[QWeight], bias: Optional[torch.Te
     skinny_ok = all(w.K % 256 == 0 for w in ws)
     use_skinny = (M <= SKINNY_MAX_M and skinny_ok) if force is None else force == "skinny"
     mid_ok = skinny_ok and all(w.fmt in MID_FMTS for w in ws)
-    S = 0
+    S, tile = 0, 0
     if force == "mid":
         S = min(pick_mid_splits(w.N, w.K, M) for w in ws)
     elif force is None and not use_skinny and M <= MID_MAX_M and mid_ok:
@@ -382,12 +400,12 @@ def linear_multi(x: torch.Tensor, ws: Sequence[QWeight], bias: Optional[torch.Te
         if choice is None and GEMM_AUTOTUNE and not torch.cuda.is_current_stream_capturing():
             choice = _autotune_mid(x, ws, key, Ntot)
         if choice is not None and choice[0] == "mid":
-            S = choice[1]
+            S, tile = choice[1], choice[2]
     if S:
         out = out_slabs
         if out is None or out.shape != (S, M, Ntot):
             out = torch.empty(S, M, Ntot, dtype=torch.float32, device=x.device)
-        _run_mid(x, ws, S, out, Ntot)
+        _run_mid(x, ws, S, out, Ntot, tile)
         return Partial(out, bias)
     if use_skinny:
         S = min(pick_splits(w.N, w.K, M) for w in ws)

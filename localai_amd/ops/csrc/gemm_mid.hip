@@ -8,10 +8,11 @@
 // the MFMAs when ONE dequantised fragment feeds >= ~11 of them.  Here the weight tile is
 // dequantised ONCE per workgroup into LDS (16-weight units, 16-B raw loads) and shared by
 // all waves, like the activation tile:
-//   * tile BM (M) x 128 (N) x 64 (K) with BM = 128 (4 waves, 2x2) for M <= 128 and BM = 256
+//   * tile BM (M) x BN (N) x 64 (K), BM in {128, 256}, BN in {64, 128} (autotuned per shape);
+//     default BM = 128 (4 waves, 2x2) for M <= 128 and BM = 256
 //     (8 waves, 4x2) above, so the dequant cost per MFMA halves as M grows; each wave owns a
 //     64x64 output tile = 4x4 v_mfma_f32_16x16x32_bf16 accumulators;
-//   * both operands staged through padded LDS rows (row stride 144 B: the 16 rows a
+//   * both operands staged through padded LDS rows (row stride 160 B: the 16 rows a
 //     ds_read_b128 lane group touches land on 16 distinct 16-B bank slots);
 //   * a 3-deep register ring feeds a 2-buffer LDS pipeline: the raw quant bytes + X chunks
 //     of K-step t+3 are in flight while the MFMAs of step t run; dequant/LDS write after;
@@ -22,7 +23,7 @@
 namespace la {
 
 constexpr int MD_BN = 128, MD_BK = 64;
-constexpr int MD_LDS = MD_BK + 8;  // bf16 elements per LDS row
+constexpr int MD_LDS = MD_BK + 16;  // bf16 per LDS row: 160 B = 10 16-B slots, conflict-free ds_read_b128 for the (row r, k-chunk g) fragment pattern (stride 144 B was 2-way)
 
 // Raw bytes for one staging unit = 16 weights of row n at k = 64*ks + 16*q .. +16 (q = 0..3).
 // Addressing is split into a per-thread 32-bit offset (fixed for the whole K loop, set by
@@ -130,21 +131,25 @@ template <> struct MidRaw<FMT_Q8_0> {
   }
 };
 
-// BM = 128 (4 waves, 2x2) or 256 (8 waves, 4x2); every wave owns a 64x64 output tile.
-template <int FMT, int BM>
-__global__ __launch_bounds__(2 * BM, 256 / BM) void qgemm_mid_kernel(QW w, const bf16* __restrict__ X, int ldx,
-                                                                    int M, int ksteps_per_split,
-                                                                    float* __restrict__ out, int ldo, long slab) {
-  constexpr int NT = 2 * BM;                    // threads
-  constexpr int XU = BM * MD_BK / 8 / NT;       // 16-B X chunks per thread per K-step (= 4)
-  constexpr int WU = MD_BN * 4 / NT;            // 16-weight W units per thread (2 or 1)
-  constexpr int BUF = (BM + MD_BN) * MD_LDS;    // bf16 per stage buffer
+// Tile BM x BN, (BM/64) x (BN/64) waves; every wave owns a 64x64 output tile.  BN = 64 tiles
+// double the workgroup count of the small-N projections (o / down / qkv: N = 4096-6144) at
+// batch-decode M, where BN = 128 leaves most CUs idle.
+template <int FMT, int BM, int BN>
+__global__ __launch_bounds__((BM / 64) * (BN / 64) * 64) void qgemm_mid_kernel(
+    QW w, const bf16* __restrict__ X, int ldx, int M, int ksteps_per_split, float* __restrict__ out, int ldo,
+    long slab) {
+  constexpr int WN = BN / 64;                   // waves along N
+  constexpr int NT = (BM / 64) * WN * 64;       // threads
+  constexpr int XU = BM * MD_BK / 8 / NT;       // 16-B X chunks per thread per K-step
+  constexpr int WU = BN * 4 / NT;               // 16-weight W units per thread
+  static_assert(XU >= 1 && WU >= 1 && BM * MD_BK / 8 % NT == 0 && BN * 4 % NT == 0, "tile/thread mismatch");
+  constexpr int BUF = (BM + BN) * MD_LDS;       // bf16 per stage buffer
   __shared__ __attribute__((aligned(16))) bf16 lds[2 * BUF];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WN, wn = wave % WN;
   const int r = lane & 15, g = lane >> 4;
   const int N = w.N;
-  const int n0 = blockIdx.x * MD_BN, m0 = blockIdx.z * BM;
+  const int n0 = blockIdx.x * BN, m0 = blockIdx.z * BM;
   const int total_ks = w.K / MD_BK;
   const int ks0 = blockIdx.y * ksteps_per_split;
   const int ks1 = min(total_ks, ks0 + ksteps_per_split);
@@ -264,18 +269,30 @@ __global__ __launch_bounds__(2 * BM, 256 / BM) void qgemm_mid_kernel(QW w, const
   }
 }
 
+template <int FMT, int BM, int BN>
+static void launch_mid_t(const QW& w, const bf16* X, int ldx, int M, int per, int splits, float* out, int ldo,
+                         long slab, hipStream_t st) {
+  dim3 grid((w.N + BN - 1) / BN, splits, (M + BM - 1) / BM);
+  hipLaunchKernelGGL((qgemm_mid_kernel<FMT, BM, BN>), grid, dim3((BM / 64) * (BN / 64) * 64), 0, st, w, X, ldx, M,
+                     per, out, ldo, slab);
+}
+
+// tile: 0 = auto (BM by M, BN 128); else 10 * (BM / 64) + (BN / 64), e.g. 42 = 256 x 128, 41 = 256 x 64,
+// 22 = 128 x 128, 21 = 128 x 64
 template <int FMT>
-static void launch_mid(const QW& w, const bf16* X, int ldx, int M, int splits, float* out, int ldo, long slab,
-                       hipStream_t st) {
+static int launch_mid(const QW& w, const bf16* X, int ldx, int M, int splits, int tile, float* out, int ldo,
+                      long slab, hipStream_t st) {
   const int total = w.K / MD_BK;
   const int per = (total + splits - 1) / splits;
-  if (M <= 128) {
-    dim3 grid((w.N + MD_BN - 1) / MD_BN, splits, 1);
-    hipLaunchKernelGGL((qgemm_mid_kernel<FMT, 128>), grid, dim3(256), 0, st, w, X, ldx, M, per, out, ldo, slab);
-  } else {
-    dim3 grid((w.N + MD_BN - 1) / MD_BN, splits, (M + 255) / 256);
-    hipLaunchKernelGGL((qgemm_mid_kernel<FMT, 256>), grid, dim3(512), 0, st, w, X, ldx, M, per, out, ldo, slab);
+  if (tile == 0) tile = (M <= 128) ? 22 : 42;
+  switch (tile) {
+    case 42: launch_mid_t<FMT, 256, 128>(w, X, ldx, M, per, splits, out, ldo, slab, st); break;
+    case 41: launch_mid_t<FMT, 256, 64>(w, X, ldx, M, per, splits, out, ldo, slab, st); break;
+    case 22: launch_mid_t<FMT, 128, 128>(w, X, ldx, M, per, splits, out, ldo, slab, st); break;
+    case 21: launch_mid_t<FMT, 128, 64>(w, X, ldx, M, per, splits, out, ldo, slab, st); break;
+    default: return -1;
   }
+  return 0;
 }
 
 }  // namespace la
@@ -283,7 +300,8 @@ static void launch_mid(const QW& w, const bf16* X, int ldx, int M, int splits, f
 // C ABI ---------------------------------------------------------------------------
 // splits must satisfy ceil(K/64 / splits) * (splits-1) < K/64 so every slab is written.
 extern "C" int la_qgemm_mid(int fmt, const void* p0, const void* p1, const void* p2, const void* p3, int N, int K,
-                            const void* X, int ldx, int M, int splits, void* out, int ldo, long slab, void* stream) {
+                            const void* X, int ldx, int M, int splits, void* out, int ldo, long slab, int tile,
+                            void* stream) {
   using namespace la;
   if (M < 1 || (K & 255) || splits < 1 || ldo < N || ldx < K || slab < (long)M * ldo) return -1;
   if ((long)N * K >= (1L << 31) || (long)M * ldx >= (1L << 31)) return -1;  // 32-bit staging offsets
@@ -294,9 +312,9 @@ extern "C" int la_qgemm_mid(int fmt, const void* p0, const void* p1, const void*
   const bf16* x = (const bf16*)X;
   float* o = (float*)out;
   switch (fmt) {
-    case FMT_Q4_K: launch_mid<FMT_Q4_K>(w, x, ldx, M, splits, o, ldo, slab, st); break;
-    case FMT_Q6_K: launch_mid<FMT_Q6_K>(w, x, ldx, M, splits, o, ldo, slab, st); break;
-    case FMT_Q8_0: launch_mid<FMT_Q8_0>(w, x, ldx, M, splits, o, ldo, slab, st); break;
+    case FMT_Q4_K: if (launch_mid<FMT_Q4_K>(w, x, ldx, M, splits, tile, o, ldo, slab, st)) return -1; break;
+    case FMT_Q6_K: if (launch_mid<FMT_Q6_K>(w, x, ldx, M, splits, tile, o, ldo, slab, st)) return -1; break;
+    case FMT_Q8_0: if (launch_mid<FMT_Q8_0>(w, x, ldx, M, splits, tile, o, ldo, slab, st)) return -1; break;
     default: return -2;
   }
   return (int)hipGetLastError();

@@ -60,11 +60,13 @@ for name, fmt, N, K in SHAPES:
     wbf = [w.materialize_bf16() for w in ws[:max(2, -(-640 * 2**20 // (N * K * 2)))]]
     for M in Ms:
         x = (torch.randn(M, K, device=dev) * 0.5).to(torch.bfloat16)
+        outs = {S: torch.empty(S, M, N, dtype=torch.float32, device=dev) for S in (1, 2, 4, 8)}
         paths = []
         if M <= ops.SKINNY_MAX_M:
             paths.append("skinny")
         if M > 16:
-            paths += ["mid", "blas"]
+            paths += ["blas"] + [f"mid:{t}:{S}" for t in ((42, 41, 22, 21) if M > 128 else (22, 21))
+                                 for S in (1, 2, 4, 8) if ops._mid_split_ok(K, S)]
         for p in paths:
             cnt = [0]
 
@@ -73,6 +75,9 @@ for name, fmt, N, K in SHAPES:
                 cnt[0] += 1
                 if p == "blas":
                     return torch.matmul(x, wbf[i % len(wbf)].t())
+                if p.startswith("mid:"):
+                    _, t, S = p.split(":")
+                    return ops._run_mid(x, [ws[i % len(ws)]], int(S), outs[int(S)], N, int(t))
                 return ops.linear(x, ws[i % len(ws)], force=p)
             try:
                 us = timeit(fn, iters=max(20, 2 * len(ws)))

@@ -69,12 +69,13 @@ def test_mid_gemm_splits():
     w = _qw(N, K, GGMLType.Q4_K, seed=8)
     x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
     ref = x.float().cpu() @ w.ref.t()
-    for S in (1, 3, 4, 8):
-        out = torch.full((S, M, N), float("nan"), dtype=torch.float32, device=DEV)
-        rc = ops.lib().la_qgemm_mid(w.fmt, *w.ptrs(), N, K, x.data_ptr(), K, M, S, out.data_ptr(), N, M * N,
-                                    ops._stream())
-        assert rc == 0
-        assert (out.sum(0).cpu() - ref).abs().max().item() < 3e-2
+    for tile in (0, 42, 41, 22, 21):  # auto, 256x128, 256x64, 128x128, 128x64
+        for S in (1, 3, 4, 8):
+            out = torch.full((S, M, N), float("nan"), dtype=torch.float32, device=DEV)
+            rc = ops.lib().la_qgemm_mid(w.fmt, *w.ptrs(), N, K, x.data_ptr(), K, M, S, out.data_ptr(), N, M * N,
+                                        tile, ops._stream())
+            assert rc == 0
+            assert (out.sum(0).cpu() - ref).abs().max().item() < 3e-2, (tile, S)
 
 
 @pytest.mark.parametrize("M", [3, 100])
