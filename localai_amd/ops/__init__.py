@@ -326,13 +326,14 @@ _FLUSH: dict = {}
 
 
 def _cold_caches(device):
-    """Evict L2 and the 256 MiB Infinity Cache (write a 384 MiB scratch buffer), so a timed
-    GEMM reads its weights from HBM as it does in the engine, where every decode step streams
-    the whole model once."""
+    """Evict L2 and the 256 MiB Infinity Cache by READING a 384 MiB scratch buffer (a write
+    flush leaves dirty lines whose write-back then taxes the timed call), so a timed GEMM
+    reads its weights from HBM as it does in the engine, where every decode step streams the
+    whole model once."""
     buf = _FLUSH.get(device)
     if buf is None:
-        buf = _FLUSH[device] = torch.empty(384 << 20, dtype=torch.uint8, device=device)
-    buf.fill_(1)
+        buf = _FLUSH[device] = torch.ones(96 << 20, dtype=torch.float32, device=device)
+    buf.sum()
 
 
 def _autotune_mid(x, ws, key, Ntot):

@@ -63,25 +63,28 @@ LA_DEV void load4(const Src& s, long idx, int col, float v[4]) {
 
 // ------------------------------------------------------------------------------------
 // residual[t] += sum(src[t]) (optional);  out[t] = norm(residual[t]) * w (+ b)
-// mode 0 = RMSNorm, 1 = LayerNorm.  One 256-thread workgroup per row, row cached in VGPRs.
+// mode 0 = RMSNorm, 1 = LayerNorm.  One workgroup per row, row cached in VGPRs: 256 threads,
+// or 1024 when there are few rows (batch-1/-small decode: a single 256-thread workgroup
+// reading the row plus up to 8 split-K slabs (~150 KB) is latency-bound at ~6.6 us; 16 waves
+// keep 4x the loads in flight).
 constexpr int NORM_T = 256;
 constexpr int NORM_MAXV = 8;  // float4 per thread => D <= 8192
 
 // IT = ceil(D/4 / NORM_T) float4 chunks per thread, a compile-time count so every load of
 // the row (and of all its split-K slabs) is issued before the first use.
-template <int IT>
-__global__ __launch_bounds__(NORM_T) void add_norm_kernel(float* __restrict__ residual, Src add, int has_add,
-                                                          const float* __restrict__ w, const float* __restrict__ b,
-                                                          bf16* __restrict__ out, int D, float eps, int mode,
-                                                          float* __restrict__ out_f32) {
-  __shared__ float red[NORM_T / 64];
+template <int IT, int NT = NORM_T>
+__global__ __launch_bounds__(NT) void add_norm_kernel(float* __restrict__ residual, Src add, int has_add,
+                                                      const float* __restrict__ w, const float* __restrict__ b,
+                                                      bf16* __restrict__ out, int D, float eps, int mode,
+                                                      float* __restrict__ out_f32) {
+  __shared__ float red[NT / 64];
   const int t = blockIdx.x;
   const int nv = D >> 2;
   float* rrow = residual + (long)t * D;
   float v[IT][4];
 #pragma unroll
   for (int i = 0; i < IT; ++i) {
-    const int c = min(threadIdx.x + i * NORM_T, nv - 1);  // clamped: loads never branch
+    const int c = min(threadIdx.x + i * NT, nv - 1);  // clamped: loads never branch
     const float4 r = *(const float4*)(rrow + 4 * c);
     v[i][0] = r.x; v[i][1] = r.y; v[i][2] = r.z; v[i][3] = r.w;
     if (has_add) {
@@ -93,7 +96,7 @@ __global__ __launch_bounds__(NORM_T) void add_norm_kernel(float* __restrict__ re
   float s1 = 0.f;
 #pragma unroll
   for (int i = 0; i < IT; ++i) {
-    const int c = threadIdx.x + i * NORM_T;
+    const int c = threadIdx.x + i * NT;
     if (c < nv) {
       if (has_add) *(float4*)(rrow + 4 * c) = make_float4(v[i][0], v[i][1], v[i][2], v[i][3]);
       s1 += (mode == 0) ? (v[i][0] * v[i][0] + v[i][1] * v[i][1] + v[i][2] * v[i][2] + v[i][3] * v[i][3])
@@ -102,25 +105,25 @@ __global__ __launch_bounds__(NORM_T) void add_norm_kernel(float* __restrict__ re
   }
   float mean = 0.f, rstd;
   if (mode == 0) {
-    const float ss = block_sum<NORM_T>(s1, red);
+    const float ss = block_sum<NT>(s1, red);
     rstd = rsqrtf(ss / (float)D + eps);
   } else {
-    mean = block_sum<NORM_T>(s1, red) / (float)D;
+    mean = block_sum<NT>(s1, red) / (float)D;
     float s2 = 0.f;
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
-      const int c = threadIdx.x + i * NORM_T;
+      const int c = threadIdx.x + i * NT;
       if (c < nv) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) { const float d = v[i][j] - mean; s2 += d * d; }
       }
     }
-    rstd = rsqrtf(block_sum<NORM_T>(s2, red) / (float)D + eps);
+    rstd = rsqrtf(block_sum<NT>(s2, red) / (float)D + eps);
   }
   if (!out) return;
 #pragma unroll
   for (int i = 0; i < IT; ++i) {
-    const int c = threadIdx.x + i * NORM_T;
+    const int c = threadIdx.x + i * NT;
     if (c < nv) {
       const float4 ww = *(const float4*)(w + 4 * c);
       float4 bb = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -306,6 +309,18 @@ extern "C" int la_add_norm(void* residual, const void* add_p, long add_slab, int
                        (float*)residual, s, has_add, (const float*)w, (const float*)b, (bf16*)out, D, eps,  \
                        mode, (float*)out_f32);                                                            \
     break;
+  if (T <= 32 && D <= 1024 * 4 * 2) {
+    const int it4 = (D / 4 + 1023) / 1024;
+    if (it4 == 1)
+      hipLaunchKernelGGL((la::add_norm_kernel<1, 1024>), dim3(T), dim3(1024), 0, (hipStream_t)stream,
+                         (float*)residual, s, has_add, (const float*)w, (const float*)b, (bf16*)out, D, eps, mode,
+                         (float*)out_f32);
+    else
+      hipLaunchKernelGGL((la::add_norm_kernel<2, 1024>), dim3(T), dim3(1024), 0, (hipStream_t)stream,
+                         (float*)residual, s, has_add, (const float*)w, (const float*)b, (bf16*)out, D, eps, mode,
+                         (float*)out_f32);
+    return (int)hipGetLastError();
+  }
   switch (it) {
     LA_NORM_CASE(1) LA_NORM_CASE(2) LA_NORM_CASE(3) LA_NORM_CASE(4)
     LA_NORM_CASE(5) LA_NORM_CASE(6) LA_NORM_CASE(7) LA_NORM_CASE(8)

@@ -99,8 +99,8 @@ def test_dequant_and_large_m_linear():
 
 
 @pytest.mark.parametrize("mode", [0, 1])
-def test_add_norm(mode):
-    T, D = 7, 4096
+@pytest.mark.parametrize("T,D", [(7, 4096), (1, 2560), (40, 4096), (3, 8192)])
+def test_add_norm(mode, T, D):
     res = torch.randn(T, D, device=DEV)
     add = torch.randn(3, T, D, device=DEV)
     w = torch.rand(D, device=DEV) + 0.5
