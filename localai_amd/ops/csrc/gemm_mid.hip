@@ -14,8 +14,8 @@
 //     64x64 output tile = 4x4 v_mfma_f32_16x16x32_bf16 accumulators;
 //   * both operands staged through padded LDS rows (row stride 160 B: the 16 rows a
 //     ds_read_b128 lane group touches land on 16 distinct 16-B bank slots);
-//   * a 3-deep register ring feeds a 2-buffer LDS pipeline: the raw quant bytes + X chunks
-//     of K-step t+3 are in flight while the MFMAs of step t run; dequant/LDS write after;
+//   * a 4-deep register ring feeds a 2-buffer LDS pipeline: the raw quant bytes + X chunks
+//     of K-step t+4 are in flight while the MFMAs of step t run; dequant/LDS write after;
 //   * split-K over grid.y, M tiles over grid.z; the fp32 slabs are summed by the
 //     consuming kernel's prologue (same contract as the skinny GEMM).
 #include "qweight.h"
@@ -23,6 +23,9 @@
 namespace la {
 
 constexpr int MD_BN = 128, MD_BK = 64;
+#ifndef MID_DEPTH
+#define MID_DEPTH 4
+#endif
 constexpr int MD_LDS = MD_BK + 16;  // bf16 per LDS row: 160 B = 10 16-B slots, conflict-free ds_read_b128 for the (row r, k-chunk g) fragment pattern (stride 144 B was 2-way)
 
 // Raw bytes for one staging unit = 16 weights of row n at k = 64*ks + 16*q .. +16 (q = 0..3).
@@ -155,9 +158,8 @@ __global__ __launch_bounds__((BM / 64) * (BN / 64) * 64) void qgemm_mid_kernel(
   const int ks1 = min(total_ks, ks0 + ksteps_per_split);
   if (ks0 >= ks1) return;  // uniform per block
 
-  // 3-deep register ring: the raw quant bytes + X chunks of K-step t+3 are issued while the
-  // MFMAs of step t run (HBM latency under load is ~2-3 K-steps of MFMA work).  Loads are
-  // never predicated (clamped instead) so hipcc emits counted vmcnt waits, not vmcnt(0).
+  // Register ring stages: the raw quant bytes + X chunks of one K-step.  Loads are never
+  // predicated (clamped instead) so hipcc emits counted vmcnt waits, not vmcnt(0).
   struct Stage {
     MidRaw<FMT> raw[WU];
     bf16x8 xr[XU];
@@ -179,7 +181,9 @@ __global__ __launch_bounds__((BM / 64) * (BN / 64) * 64) void qgemm_mid_kernel(
     for (int u = 0; u < WU; ++u) S.raw[u].load(w, wad[u], ks);
     const bf16* xk = X + ks * MD_BK;
 #pragma unroll
-    for (int i = 0; i < XU; ++i) S.xr[i] = *(const bf16x8*)(xk + xoff[i]);
+    for (int i = 0; i < XU; ++i) {
+      S.xr[i] = *(const bf16x8*)(xk + xoff[i]);
+    }
   };
   auto commit = [&](const Stage& S, int ks, int buf) {
     bf16* xs = lds + buf * BUF;
@@ -224,34 +228,32 @@ __global__ __launch_bounds__((BM / 64) * (BN / 64) * 64) void qgemm_mid_kernel(
     }
   };
 
+  // D-deep ring (MID_DEPTH stages): vmcnt retires in issue order, so the X chunks (L2) and
+  // the raw weights (HBM) share one prefetch distance; at ~1 WG per CU the weight stream
+  // needs ~3-4 K-steps of loads in flight to cover HBM latency (measured: the ablated kernel
+  // with no MFMA/dequant/X still ran at 1 TB/s with a 3-deep ring).
+  constexpr int D = MID_DEPTH;
   const int last = ks1 - 1;
-  Stage s0, s1, s2;
-  issue(s0, ks0);
-  issue(s1, min(ks0 + 1, last));
-  issue(s2, min(ks0 + 2, last));
-  commit(s0, ks0, 0);
+  Stage st[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) issue(st[i], min(ks0 + i, last));
+  commit(st[0], ks0, 0);
   __syncthreads();
-  // step t: stage `fr` (already in LDS) refills with t+3; stage `nx` (t+1) is committed to LDS
-#define MID_STEP(KS, fr, nx, BUFI)                 \
-  {                                                \
-    issue(fr, min((KS) + 3, last));                \
-    compute(BUFI);                                 \
-    commit(nx, min((KS) + 1, last), (BUFI) ^ 1);   \
-    __syncthreads();                               \
+  const int nks = ks1 - ks0;
+  for (int j = 0; j < nks; j += D) {
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      // step t = j + i: buffer (t & 1) holds K-step t; slot i refills with t + D; slot i+1
+      // (K-step t + 1) is committed to the other buffer
+      const int t = j + i;
+      issue(st[i], min(ks0 + t + D, last));
+      compute(t & 1);
+      commit(st[(i + 1) % D], min(ks0 + t + 1, last), (t + 1) & 1);
+      __syncthreads();
+      if (t + 1 >= nks) break;
+    }
   }
-  int buf = 0;
-  for (int ks = ks0;; ks += 3) {
-    MID_STEP(ks, s0, s1, buf);
-    buf ^= 1;
-    if (ks + 1 >= ks1) break;
-    MID_STEP(ks + 1, s1, s2, buf);
-    buf ^= 1;
-    if (ks + 2 >= ks1) break;
-    MID_STEP(ks + 2, s2, s0, buf);
-    buf ^= 1;
-    if (ks + 3 >= ks1) break;
-  }
-#undef MID_STEP
+
 
   float* o = out + (size_t)blockIdx.y * slab;
 #pragma unroll
