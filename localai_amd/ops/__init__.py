@@ -45,6 +45,7 @@ def lib():
         sig = {
             "la_qgemm_skinny": [I, P, P, P, P, I, I, P, I, I, I, P, I, LNG, P],
             "la_qgemm_mid": [I, P, P, P, P, I, I, P, I, I, I, P, I, LNG, I, P],
+            "la_qgemm_ws": [I, P, P, P, P, I, I, P, I, I, I, P, I, LNG, P],
             "la_add_norm": [P, P, LNG, I, P, I, P, P, P, I, I, F, I, P, P],
             "la_rope_kv": [P, LNG, I, P, P, P, P, I, I, I, I, I, I, P, P, P, I, P],
             "la_act": [P, LNG, I, P, P, I, I, I, P],
@@ -311,6 +312,20 @@ def _run_mid(x, ws, S, out, Ntot, tile=0):
         col += w.N
 
 
+def _ws_ok(ws, K: int, S: int) -> bool:
+    """Warp-specialised LDS-DMA GEMM (gemm_ws.hip): Q4_K weights, equal K splits."""
+    return all(w.fmt == FMT_Q4_K for w in ws) and (K // 64) % S == 0
+
+
+def _run_ws(x, ws, S, out, Ntot):
+    M, K = x.shape
+    col = 0
+    for w in ws:
+        _check(lib().la_qgemm_ws(w.fmt, *w.ptrs(), w.N, w.K, x.data_ptr(), K, M, S, out.data_ptr() + col * 4,
+                                 Ntot, M * Ntot, _stream()), "la_qgemm_ws")
+        col += w.N
+
+
 def _run_blas(x, ws, Ntot):
     if len(ws) == 1:
         return torch.matmul(x, ws[0].materialize_bf16().t())
@@ -344,11 +359,17 @@ def _autotune_mid(x, ws, key, Ntot):
     M, K = x.shape
     tiles = (22, 21) if M <= 128 else (42, 41, 22, 21)
     cands = [("blas", 0, 0)] + [("mid", S, t) for t in tiles for S in (1, 2, 4, 8) if _mid_split_ok(K, S)]
+    if M > 128:
+        cands += [("ws", S, 0) for S in (1, 2, 4, 8) if _ws_ok(ws, K, S)]
     outs = {S: torch.empty(S, M, Ntot, dtype=torch.float32, device=x.device) for _, S, _ in cands if S}
     best, best_t = ("blas", 0, 0), float("inf")
     for kind, S, t in cands:
-        fn = (lambda: _run_blas(x, ws, Ntot)) if kind == "blas" else \
-            (lambda S=S, t=t: _run_mid(x, ws, S, outs[S], Ntot, t))
+        if kind == "blas":
+            fn = lambda: _run_blas(x, ws, Ntot)  # noqa: E731
+        elif kind == "ws":
+            fn = lambda S=S: _run_ws(x, ws, S, outs[S], Ntot)  # noqa: E731
+        else:
+            fn = lambda S=S, t=t: _run_mid(x, ws, S, outs[S], Ntot, t)  # noqa: E731
         fn()
         ts = []
         for _ in range(3):
@@ -360,7 +381,7 @@ def _autotune_mid(x, ws, key, Ntot):
             e1.synchronize()
             ts.append(e0.elapsed_time(e1) * 1000)
         tt = sorted(ts)[1]
-        if kind == "mid":
+        if kind != "blas":
             tt += (S * M * Ntot * 4 - M * Ntot * 2) / 4e6
         if tt < best_t:
             best, best_t = (kind, S, t), tt
@@ -392,7 +413,9 @@ def linear_multi(x: torch.Tensor, ws: Sequence[QWeight], bias: Optional[torch.Te
     skinny_ok = all(w.K % 256 == 0 for w in ws)
     use_skinny = (M <= SKINNY_MAX_M and skinny_ok) if force is None else force == "skinny"
     mid_ok = skinny_ok and all(w.fmt in MID_FMTS for w in ws)
-    S, tile = 0, 0
+    S, tile, use_ws = 0, 0, False
+    if force == "ws":
+        S, use_ws = 1, True
     if force == "mid":
         S = min(pick_mid_splits(w.N, w.K, M) for w in ws)
     elif force is None and not use_skinny and M <= MID_MAX_M and mid_ok:
@@ -400,13 +423,17 @@ def linear_multi(x: torch.Tensor, ws: Sequence[QWeight], bias: Optional[torch.Te
         choice = _GEMM_CHOICE.get(key)
         if choice is None and GEMM_AUTOTUNE and not torch.cuda.is_current_stream_capturing():
             choice = _autotune_mid(x, ws, key, Ntot)
-        if choice is not None and choice[0] == "mid":
+        if choice is not None and choice[0] in ("mid", "ws"):
             S, tile = choice[1], choice[2]
+            use_ws = choice[0] == "ws"
     if S:
         out = out_slabs
         if out is None or out.shape != (S, M, Ntot):
             out = torch.empty(S, M, Ntot, dtype=torch.float32, device=x.device)
-        _run_mid(x, ws, S, out, Ntot, tile)
+        if use_ws:
+            _run_ws(x, ws, S, out, Ntot)
+        else:
+            _run_mid(x, ws, S, out, Ntot, tile)
         return Partial(out, bias)
     if use_skinny:
         S = min(pick_splits(w.N, w.K, M) for w in ws)

@@ -67,6 +67,8 @@ for name, fmt, N, K in SHAPES:
         if M > 16:
             paths += ["blas"] + [f"mid:{t}:{S}" for t in ((42, 41, 22, 21) if M > 128 else (22, 21))
                                  for S in (1, 2, 4, 8) if ops._mid_split_ok(K, S)]
+            if M > 128 and fmt == "q4k":
+                paths += [f"ws:{S}" for S in (1, 2, 4, 8) if (K // 64) % S == 0]
         for p in paths:
             cnt = [0]
 
@@ -75,6 +77,9 @@ for name, fmt, N, K in SHAPES:
                 cnt[0] += 1
                 if p == "blas":
                     return torch.matmul(x, wbf[i % len(wbf)].t())
+                if p.startswith("ws:"):
+                    S = int(p.split(":")[1])
+                    return ops._run_ws(x, [ws[i % len(ws)]], S, outs[S], N)
                 if p.startswith("mid:"):
                     _, t, S = p.split(":")
                     return ops._run_mid(x, [ws[i % len(ws)]], int(S), outs[int(S)], N, int(t))

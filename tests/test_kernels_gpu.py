@@ -78,6 +78,30 @@ def test_mid_gemm_splits():
             assert (out.sum(0).cpu() - ref).abs().max().item() < 3e-2, (tile, S)
 
 
+@pytest.mark.parametrize("M", [1, 100, 256, 300])
+@pytest.mark.parametrize("K", [1024, 3584])
+def test_ws_gemm(M, K):
+    """Warp-specialised LDS-DMA Q4_K GEMM vs the fp32 reference: N off the 128 tile, several
+    M tiles, every equal split of the K-steps (repeated launches bit-identical)."""
+    N = 200
+    w = _qw(N, K, GGMLType.Q4_K, seed=9)
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    ref = x.float().cpu() @ w.ref.t()
+    for S in (1, 2, 4, 7):
+        if (K // 64) % S:
+            continue
+        out = torch.full((S, M, N), float("nan"), dtype=torch.float32, device=DEV)
+        rc = ops.lib().la_qgemm_ws(w.fmt, *w.ptrs(), N, K, x.data_ptr(), K, M, S, out.data_ptr(), N, M * N,
+                                   ops._stream())
+        assert rc == 0
+        y = out.sum(0).cpu()
+        assert (y - ref).abs().max().item() < 3e-2 * max(1.0, ref.abs().max().item()), S
+        out2 = torch.empty_like(out)
+        ops.lib().la_qgemm_ws(w.fmt, *w.ptrs(), N, K, x.data_ptr(), K, M, S, out2.data_ptr(), N, M * N,
+                              ops._stream())
+        assert torch.equal(out, out2)
+
+
 @pytest.mark.parametrize("M", [3, 100])
 def test_linear_multi_mixed_formats(M):
     K = 512
