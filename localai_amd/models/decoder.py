@@ -184,9 +184,7 @@ class DecoderModel:
                 if b + "attn_q.bias" in T:
                     qkv_bias = torch.cat([f32(b + "attn_q.bias")[qs], f32(b + "attn_k.bias")[ks],
                                           f32(b + "attn_v.bias")[ks]])
-            fused = ops.concat_rows(qkv)
-            if fused is not None:
-                qkv = [fused]
+            qkv = ops.fuse_runs(qkv)  # q|k|v, or q|k + v when v has its own format (Q4_K_M)
             wo = qw(b + "attn_output.weight", cols=sl(qd))
             wo_b = f32(b + "attn_output.bias")
             if wo_b is not None and R != 0:

@@ -218,6 +218,21 @@ def concat_rows(ws: Sequence[QWeight]) -> Optional[QWeight]:
     return QWeight(w0.fmt, sum(w.N for w in ws), w0.K, tuple(planes), ref=ref)
 
 
+def fuse_runs(ws: Sequence[QWeight]) -> List[QWeight]:
+    """Concatenate each run of consecutive weights that share format and K (one GEMM launch
+    per run); the output column order is unchanged."""
+    out: List[QWeight] = []
+    run: List[QWeight] = []
+    for w in ws:
+        if run and (w.fmt, w.K) != (run[0].fmt, run[0].K):
+            out.append(concat_rows(run) if len(run) > 1 else run[0])
+            run = []
+        run.append(w)
+    if run:
+        out.append(concat_rows(run) if len(run) > 1 else run[0])
+    return out
+
+
 # ---------------------------------------------------------------------------------------
 # Partial results: S fp32 split-K slabs [S, M, N] or one bf16/fp32 [M, N] matrix
 # ---------------------------------------------------------------------------------------
@@ -419,7 +434,9 @@ def linear_multi(x: torch.Tensor, ws: Sequence[QWeight], bias: Optional[torch.Te
     if force == "mid":
         S = min(pick_mid_splits(w.N, w.K, M) for w in ws)
     elif force is None and not use_skinny and M <= MID_MAX_M and mid_ok:
-        key = (M, K, tuple((w.fmt, w.N) for w in ws))
+        # one tuned choice per 32-row bucket: prefill chunk / decode batch sizes vary per step
+        # and must not re-run the (cache-flushing) autotune inside the serving loop
+        key = ((M + 31) // 32 * 32, K, tuple((w.fmt, w.N) for w in ws))
         choice = _GEMM_CHOICE.get(key)
         if choice is None and GEMM_AUTOTUNE and not torch.cuda.is_current_stream_capturing():
             choice = _autotune_mid(x, ws, key, Ntot)
