@@ -85,10 +85,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # BENCH_BACKEND=gloo rehearses the multi-rank path on fewer GPUs than ranks (ranks share
+    # devices round-robin); the real run is one rank per GPU over RCCL ("nccl")
+    backend = os.environ.get("BENCH_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    gpu = local % max(1, ndev)
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-    dev = f"cuda:{local}" if torch.cuda.is_available() else "cpu"  # cpu: dev smoke runs only
+        torch.cuda.set_device(gpu)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{gpu}"))
+        else:
+            dist.init_process_group(backend)
+    dev = f"cuda:{gpu}" if torch.cuda.is_available() else "cpu"  # cpu: dev smoke runs only
+    red_dev = dev if backend == "nccl" else "cpu"  # gloo reduces host tensors
 
     def sync():
         if dev != "cpu":
@@ -152,9 +161,9 @@ def main():
 
     all_ttft, tot_tokens, max_el = ttfts, tokens, elapsed
     if world > 1:
-        el = torch.tensor([elapsed], device=dev)
+        el = torch.tensor([elapsed], device=red_dev)
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
-        nt = torch.tensor([float(tokens)], device=dev)
+        nt = torch.tensor([float(tokens)], device=red_dev)
         dist.all_reduce(nt)
         gathered = [None] * world
         dist.all_gather_object(gathered, ttfts)
