@@ -123,10 +123,11 @@ def create_app(state: AppState) -> FastAPI:
         origins = [o for o in cfg.cors_allow_origins.split(",") if o] or ["*"]
         app.add_middleware(CORSMiddleware, allow_origins=origins, allow_methods=["*"], allow_headers=["*"])
 
-    from . import openai_routes, localai_routes, files_routes, gallery_routes
+    from . import openai_routes, localai_routes, files_routes, gallery_routes, webui
     app.include_router(openai_routes.build_router(state))
     app.include_router(files_routes.build_router(state))
     app.include_router(localai_routes.build_router(state))
+    app.include_router(webui.build_router(state))
     if not cfg.disable_gallery_endpoint:
         app.include_router(gallery_routes.build_router(state))
     app.state.localai = state

@@ -220,11 +220,4 @@ def build_router(state) -> APIRouter:
     r.add_api_route("/v1/text-to-speech/{voice_id}", tts_eleven, methods=["POST"])
     r.add_api_route("/v1/sound-generation", sound_generation, methods=["POST"])
 
-    # ---------------------------------------------------------------- welcome
-    async def welcome():
-        return JSONResponse({"version": __version__, "models": state.list_models(),
-                             "loaded": [m.id for m in state.manager.list_loaded()],
-                             "uptime_s": round(time.time() - state.start_time, 1)})
-
-    r.add_api_route("/", welcome, methods=["GET"])
     return r

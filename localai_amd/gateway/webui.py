@@ -1,0 +1,218 @@
+"""Built-in web UI (`core/http/routes/ui.go:87-432`, `core/http/views/*.html` -- behaviour, not
+assets): home page with the installed models, model gallery browser with install/delete and
+job progress, streaming chat, text-to-speech and text-to-image pages.
+
+Self-contained HTML + vanilla JS served by the gateway (no build step, no CDN: the server may
+run air-gapped).  Every page talks to the public REST API (/v1/chat/completions with SSE,
+/models/apply, /models/jobs/:uuid, /tts, /v1/images/generations), so the UI exercises exactly
+the endpoints clients use.  `/` keeps the JSON welcome document for API clients (Accept:
+application/json), like the reference's content negotiation.  Disabled by --disable-webui.
+"""
+from __future__ import annotations
+
+import html
+import time
+
+from fastapi import APIRouter, Request
+from fastapi.responses import HTMLResponse, JSONResponse
+
+from .. import __version__
+
+_CSS = """
+body{font-family:system-ui,sans-serif;margin:0;background:#0f1115;color:#e6e6e6}
+header{display:flex;gap:1.2em;align-items:center;padding:.7em 1.2em;background:#171a21;border-bottom:1px solid #2a2f3a}
+header b{color:#ff7a45}header a{color:#cfd6e4;text-decoration:none}header a:hover{color:#fff}
+main{max-width:980px;margin:1.2em auto;padding:0 1em}
+table{border-collapse:collapse;width:100%}td,th{border-bottom:1px solid #2a2f3a;padding:.45em;text-align:left}
+button,select,input,textarea{background:#1f2430;color:#e6e6e6;border:1px solid #39404f;border-radius:6px;padding:.45em .7em}
+button{cursor:pointer}button:hover{background:#2b3242}
+#log{white-space:pre-wrap;background:#151821;border:1px solid #2a2f3a;border-radius:8px;padding:1em;min-height:260px}
+.u{color:#8ab4ff}.a{color:#e6e6e6}.muted{color:#8a93a5;font-size:.9em}
+.row{display:flex;gap:.6em;margin:.8em 0}.row>*{flex:1}.row>button,.row>select{flex:0 0 auto}
+"""
+
+_NAV = ('<header><b>LocalAI · MI355X</b><a href="/">Home</a><a href="/browse">Models</a>'
+        '<a href="/chat/">Chat</a><a href="/tts/">TTS</a><a href="/text2image/">Text→Image</a>'
+        '<a href="/swagger">API</a></header>')
+
+
+def _page(title: str, body: str, script: str = "") -> HTMLResponse:
+    return HTMLResponse(f"<!doctype html><html><head><meta charset='utf-8'><title>{html.escape(title)}</title>"
+                        f"<style>{_CSS}</style></head><body>{_NAV}<main>{body}</main>"
+                        f"<script>{script}</script></body></html>")
+
+
+def _model_select(models, selected: str) -> str:
+    opts = "".join(f"<option{' selected' if m == selected else ''}>{html.escape(m)}</option>" for m in models)
+    return f"<select id='model'>{opts}</select>"
+
+
+_AUTH_JS = """
+const KEY = localStorage.getItem('localai_key') || '';
+function hdrs(){const h={'Content-Type':'application/json'}; if(KEY) h['Authorization']='Bearer '+KEY; return h;}
+"""
+
+_CHAT_JS = _AUTH_JS + """
+const log = document.getElementById('log'), inp = document.getElementById('msg');
+const history = [];
+function add(cls, text){const d=document.createElement('div'); d.className=cls; d.textContent=text; log.appendChild(d); return d;}
+async function send(){
+  const text = inp.value.trim(); if(!text) return; inp.value='';
+  history.push({role:'user', content:text}); add('u', '> '+text);
+  const out = add('a', ''); const t0 = performance.now(); let first = 0, n = 0;
+  const res = await fetch('/v1/chat/completions', {method:'POST', headers:hdrs(), body: JSON.stringify({
+    model: document.getElementById('model').value, messages: history, stream: true,
+    temperature: parseFloat(document.getElementById('temp').value)})});
+  if(!res.ok){out.textContent = 'error: ' + res.status + ' ' + await res.text(); return;}
+  const rd = res.body.getReader(), dec = new TextDecoder(); let buf = '', full = '';
+  for(;;){
+    const {value, done} = await rd.read(); if(done) break;
+    buf += dec.decode(value, {stream:true});
+    let i; while((i = buf.indexOf('\\n')) >= 0){
+      const line = buf.slice(0, i).trim(); buf = buf.slice(i + 1);
+      if(!line.startsWith('data:')) continue; const data = line.slice(5).trim();
+      if(data === '[DONE]') continue;
+      try{const j = JSON.parse(data); const d = (j.choices && j.choices[0].delta) || {};
+          if(d.content){ if(!first) first = performance.now(); n++; full += d.content; out.textContent = full; }}catch(e){}
+    }
+  }
+  history.push({role:'assistant', content: full});
+  const s = (performance.now() - t0) / 1000;
+  document.getElementById('stats').textContent =
+    `TTFT ${first ? ((first - t0)).toFixed(0) : '-'} ms · ${n} chunks · ${(n / Math.max(s, 1e-3)).toFixed(1)} chunks/s`;
+}
+inp.addEventListener('keydown', e => { if(e.key === 'Enter' && !e.shiftKey){ e.preventDefault(); send(); } });
+"""
+
+_BROWSE_JS = _AUTH_JS + """
+async function install(id){
+  const r = await fetch('/models/apply', {method:'POST', headers:hdrs(), body: JSON.stringify({id})});
+  const j = await r.json(); const cell = document.getElementById('st-' + CSS.escape(id));
+  if(!j.uuid){cell.textContent = 'error'; return;}
+  for(;;){
+    const s = await (await fetch('/models/jobs/' + j.uuid, {headers:hdrs()})).json();
+    cell.textContent = s.processed ? (s.error ? 'error: ' + s.error : 'installed') : (s.message || '') + ' ' + (s.progress ? s.progress.toFixed(0) + '%' : '');
+    if(s.processed) break; await new Promise(r => setTimeout(r, 1000));
+  }
+}
+async function remove(name){
+  await fetch('/models/delete/' + encodeURIComponent(name), {method:'POST', headers:hdrs()});
+  location.reload();
+}
+function filter(){const q = document.getElementById('q').value.toLowerCase();
+  for(const tr of document.querySelectorAll('tbody tr')) tr.style.display = tr.dataset.k.includes(q) ? '' : 'none';}
+"""
+
+_TTS_JS = _AUTH_JS + """
+async function speak(){
+  const r = await fetch('/tts', {method:'POST', headers:hdrs(), body: JSON.stringify({
+    model: document.getElementById('model').value, input: document.getElementById('txt').value})});
+  if(!r.ok){document.getElementById('st').textContent = 'error: ' + r.status + ' ' + await r.text(); return;}
+  const a = document.getElementById('audio'); a.src = URL.createObjectURL(await r.blob()); a.play();
+}
+"""
+
+_IMG_JS = _AUTH_JS + """
+async function gen(){
+  const st = document.getElementById('st'); st.textContent = 'generating...';
+  const r = await fetch('/v1/images/generations', {method:'POST', headers:hdrs(), body: JSON.stringify({
+    model: document.getElementById('model').value, prompt: document.getElementById('txt').value,
+    size: '512x512', response_format: 'b64_json'})});
+  if(!r.ok){st.textContent = 'error: ' + r.status + ' ' + await r.text(); return;}
+  const j = await r.json(); st.textContent = '';
+  document.getElementById('img').src = 'data:image/png;base64,' + j.data[0].b64_json;
+}
+"""
+
+
+def build_router(state) -> APIRouter:
+    r = APIRouter()
+
+    def models():
+        return state.list_models()
+
+    async def home(request: Request):
+        if state.cfg.disable_webui or "text/html" not in request.headers.get("accept", ""):
+            return JSONResponse({"version": __version__, "models": models(),
+                                 "loaded": [m.id for m in state.manager.list_loaded()],
+                                 "uptime_s": round(time.time() - state.start_time, 1)})
+        loaded = {m.id for m in state.manager.list_loaded()}
+        rows = "".join(
+            f"<tr><td>{html.escape(m)}</td><td>{'loaded' if m in loaded else ''}</td>"
+            f"<td><a href='/chat/{html.escape(m)}'>chat</a></td></tr>" for m in models())
+        body = (f"<h2>Installed models</h2><table><thead><tr><th>model</th><th>state</th><th></th></tr></thead>"
+                f"<tbody>{rows or '<tr><td colspan=3 class=muted>no models yet: install one from the gallery</td></tr>'}"
+                f"</tbody></table><p class=muted>version {html.escape(__version__)} · "
+                f"<a href='/metrics'>metrics</a> · <a href='/system'>system</a></p>")
+        return _page("LocalAI", body)
+
+    async def browse():
+        import asyncio
+
+        from .. import gallery as gal
+        try:
+            avail = [m.to_json() | {"id": m.id()} for m in await asyncio.to_thread(
+                gal.available_models, state.cfg.galleries, state.models_path)]
+            err = ""
+        except Exception as e:  # gallery unreachable (air-gapped): show installed only
+            avail, err = [], str(e)
+        installed = set(models())
+        rows = []
+        for m in avail:
+            gid = m.get("id") or f"{m.get('gallery', {}).get('name', '')}@{m.get('name', '')}"
+            name = m.get("name", gid)
+            key = (name + " " + " ".join(m.get("tags") or []) + " " + (m.get("description") or "")).lower()
+            act = (f"<button onclick=\"remove('{html.escape(name)}')\">delete</button>" if name in installed else
+                   f"<button onclick=\"install('{html.escape(gid)}')\">install</button>")
+            rows.append(f"<tr data-k='{html.escape(key)}'><td>{html.escape(name)}</td>"
+                        f"<td class=muted>{html.escape((m.get('description') or '')[:140])}</td>"
+                        f"<td>{act}</td><td id='st-{html.escape(gid)}'></td></tr>")
+        body = ("<h2>Model gallery</h2><div class=row><input id=q placeholder='search' oninput='filter()'></div>"
+                + (f"<p class=muted>gallery unavailable: {html.escape(err)}</p>" if err else "")
+                + "<table><thead><tr><th>model</th><th>description</th><th></th><th>status</th></tr></thead>"
+                + f"<tbody>{''.join(rows)}</tbody></table>")
+        return _page("Models", body, _BROWSE_JS)
+
+    async def chat(model: str = ""):
+        ms = models()
+        model = model or (ms[0] if ms else "")
+        body = (f"<h2>Chat</h2><div class=row>{_model_select(ms, model)}"
+                f"<input id=temp type=number step=0.1 value=0.7 title=temperature style='max-width:90px'></div>"
+                f"<div id=log></div><div class=row><textarea id=msg rows=3 placeholder='message (Enter to send)'>"
+                f"</textarea><button onclick='send()'>Send</button></div><div id=stats class=muted></div>")
+        return _page("Chat", body, _CHAT_JS)
+
+    async def chat_model(model: str):
+        return await chat(model)
+
+    async def tts(model: str = ""):
+        ms = models()
+        body = (f"<h2>Text to speech</h2><div class=row>{_model_select(ms, model or (ms[0] if ms else ''))}</div>"
+                f"<div class=row><textarea id=txt rows=3></textarea><button onclick='speak()'>Speak</button></div>"
+                f"<audio id=audio controls></audio><div id=st class=muted></div>")
+        return _page("TTS", body, _TTS_JS)
+
+    async def tts_model(model: str):
+        return await tts(model)
+
+    async def text2image(model: str = ""):
+        ms = models()
+        body = (f"<h2>Text to image</h2><div class=row>{_model_select(ms, model or (ms[0] if ms else ''))}</div>"
+                f"<div class=row><input id=txt placeholder=prompt><button onclick='gen()'>Generate</button></div>"
+                f"<div id=st class=muted></div><img id=img style='max-width:100%'>")
+        return _page("Text to image", body, _IMG_JS)
+
+    async def text2image_model(model: str):
+        return await text2image(model)
+
+    r.add_api_route("/", home, methods=["GET"])
+    if not state.cfg.disable_webui:
+        r.add_api_route("/browse", browse, methods=["GET"])
+        r.add_api_route("/chat/", chat, methods=["GET"])
+        r.add_api_route("/chat/{model}", chat_model, methods=["GET"])
+        r.add_api_route("/tts/", tts, methods=["GET"])
+        r.add_api_route("/tts/{model}", tts_model, methods=["GET"])
+        r.add_api_route("/text2image/", text2image, methods=["GET"])
+        r.add_api_route("/text2image/{model}", text2image_model, methods=["GET"])
+    return r
+

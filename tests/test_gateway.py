@@ -78,6 +78,19 @@ def test_models_and_health(client):
     assert client.get("/version").json()["version"]
 
 
+def test_web_ui_pages(client):
+    # API clients get the JSON welcome document, browsers the HTML UI
+    w = client.get("/").json()
+    assert client.model_name in w["models"]
+    page = client.get("/", headers={"accept": "text/html"})
+    assert page.status_code == 200 and "Installed models" in page.text and client.model_name in page.text
+    for path in ("/chat/", f"/chat/{client.model_name}", "/tts/", "/text2image/", "/browse"):
+        r = client.get(path, headers={"accept": "text/html"})
+        assert r.status_code == 200, path
+        assert "<main>" in r.text
+    assert "/v1/chat/completions" in client.get("/chat/").text  # the page streams through the public API
+
+
 def test_chat_completion_greedy_is_deterministic(client):
     body = {"model": client.model_name, "messages": [{"role": "user", "content": "hello"}], "max_tokens": 6,
             "temperature": 0, "ignore_eos": True}
