@@ -35,6 +35,7 @@ from ..models.decoder import DecoderModel, ForwardBatch, TPInfo
 from ..native import core
 from ..tokenizer import Tokenizer
 from .sampling_params import SamplingParams
+from ..utils.trace import get_tracer, roctx
 
 log = logging.getLogger("localai_amd.engine")
 
@@ -149,6 +150,7 @@ class LLMEngine:
         self._thread: Optional[threading.Thread] = None
         self._stop = False
         self._graphs: Dict[int, tuple] = {}
+        self.tracer = get_tracer()
         self._graph_pool = None
         self.metrics = {"prompt_tokens": 0, "gen_tokens": 0, "steps": 0, "prefill_s": 0.0, "decode_s": 0.0,
                         "requests": 0}
@@ -275,6 +277,8 @@ class LLMEngine:
             self._thread.start()
 
     def shutdown(self):
+        if self.tracer is not None:
+            self.tracer.flush()
         if self.tp.world > 1 and self.leader and not self._stop:
             self._inbox.put(("stop",))  # followers leave run_follower() after this broadcast
             self._wake.set()
@@ -320,18 +324,30 @@ class LLMEngine:
         K = self._lookahead()
         plan = self.sched.schedule(K)
         did = False
+        tr = self.tracer
         p_ids = plan["p_ids"]
         if len(p_ids):
             t0 = time.perf_counter()
-            self._run_prefill(plan)
-            self.metrics["prefill_s"] += time.perf_counter() - t0
+            with roctx("prefill"):
+                self._run_prefill(plan)
+            t1 = time.perf_counter()
+            self.metrics["prefill_s"] += t1 - t0
+            if tr is not None:
+                tr.complete("prefill", t0, t1, seqs=len(p_ids), tokens=int(plan["p_cu"][-1]))
             did = True
         d_ids = plan["d_ids"]
         if len(d_ids):
             t0 = time.perf_counter()
-            self._run_decode(plan, K)
-            self.metrics["decode_s"] += time.perf_counter() - t0
+            with roctx("decode"):
+                self._run_decode(plan, K)
+            t1 = time.perf_counter()
+            self.metrics["decode_s"] += t1 - t0
+            if tr is not None:
+                tr.complete("decode", t0, t1, batch=len(d_ids), device_steps=K)
             did = True
+        if tr is not None:
+            tr.counter("sequences", time.perf_counter(), running=self.sched.num_running,
+                       waiting=self.sched.num_waiting)
         self.metrics["steps"] += 1
         self.busy = bool(self.requests)
         return did or bool(self.requests)
@@ -412,6 +428,9 @@ class LLMEngine:
         max_new = r.params.max_tokens if r.params.max_tokens > 0 else self.ctx
         self.sched.add(r.id, r.prompt, max_new)
         self.metrics["requests"] += 1
+        if self.tracer is not None:
+            self.tracer.instant("arrival", r.arrival, cat="request", tid=1, id=r.id,
+                                correlation_id=r.params.correlation_id, prompt_tokens=r.n_prompt)
 
     IMG_MARK = re.compile(r"\[img-(\d+)\]")
 
@@ -586,6 +605,9 @@ class LLMEngine:
                 continue
             if r.first_token_t == 0.0:
                 r.first_token_t = now
+                if self.tracer is not None:
+                    self.tracer.instant("first_token", now, cat="request", tid=1, id=r.id,
+                                        correlation_id=r.params.correlation_id)
             r.n_gen += n
             self.metrics["gen_tokens"] += n
             if texts[j]:
@@ -856,6 +878,9 @@ class LLMEngine:
         self.metrics["gen_tokens"] += 1
         if r.first_token_t == 0.0:
             r.first_token_t = now
+            if self.tracer is not None:
+                self.tracer.instant("first_token", now, cat="request", tid=1, id=r.id,
+                                    correlation_id=r.params.correlation_id)
         p = r.params
         if self.tokenizer.is_eog(tok) and not p.ignore_eos:
             self._finish(r, "stop")
@@ -899,6 +924,14 @@ class LLMEngine:
         self.last_request_stats = {"id": r.id, "prompt_tokens": r.n_prompt, "completion_tokens": r.n_gen,
                                    "ttft_s": ttft, "gen_s": gen_s,
                                    "tokens_per_second": (r.n_gen - 1) / gen_s if gen_s > 0 and r.n_gen > 1 else 0.0}
+        if self.tracer is not None:
+            self.tracer.complete("request", r.arrival, end, cat="request", tid=1, id=r.id,
+                                 correlation_id=r.params.correlation_id, prompt_tokens=r.n_prompt,
+                                 completion_tokens=r.n_gen, ttft_ms=round(ttft * 1e3, 3), finish_reason=reason)
+        if log.isEnabledFor(logging.DEBUG):
+            log.debug("request %s [%s] done (%s): prompt %d tok, gen %d tok, ttft %.1f ms, %.1f tok/s",
+                      r.id, r.params.correlation_id, reason, r.n_prompt, r.n_gen, ttft * 1e3,
+                      self.last_request_stats["tokens_per_second"])
         try:
             r.callback(Event(text=tail, finished=True, finish_reason=reason, prompt_tokens=r.n_prompt,
                              completion_tokens=r.n_gen, error=error))

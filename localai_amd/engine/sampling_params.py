@@ -31,6 +31,7 @@ class SamplingParams:
     n_keep: int = 0
     grammar: str = ""
     n_probs: int = 0
+    correlation_id: str = ""          # X-Correlation-ID of the HTTP request (PredictOptions.CorrelationId)
 
     def resolved_seed(self) -> int:
         if self.seed is None or self.seed < 0:
@@ -60,6 +61,7 @@ class SamplingParams:
             stop=[s for s in po.StopPrompts if s],
             n_keep=int(po.NKeep),
             grammar=po.Grammar,
+            correlation_id=po.CorrelationId,
         )
         if po.LogitBias:
             import json

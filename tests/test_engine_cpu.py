@@ -169,3 +169,29 @@ def test_llava16_anyres_layout(tiny_model_path, tmp_path):
     assert layout is not None and tiles.shape[0] == 1 + layout[0] * layout[1]
     emb = cv.embed_image(_png((90, 90, 90), size=50))
     assert emb.shape[1] == n_embd and emb.shape[0] > 4 and torch.isfinite(emb).all()
+
+
+def test_engine_trace_timeline(tiny_model_path, tmp_path, monkeypatch):
+    """LOCALAI_AMD_TRACE: Chrome-trace timeline with prefill/decode steps, sequence counters and
+    per-request spans tagged with the correlation ID."""
+    import json
+
+    from localai_amd.utils import trace
+    out = tmp_path / "trace.json"
+    monkeypatch.setenv("LOCALAI_AMD_TRACE", str(out))
+    trace.reset_for_tests()
+    try:
+        e = _engine(tiny_model_path)
+        res = e.generate("trace me", SamplingParams(max_tokens=3, temperature=0.0, ignore_eos=True,
+                                                     correlation_id="cid-42"))
+        assert res["completion_tokens"] == 3
+        e.shutdown()
+    finally:
+        trace.reset_for_tests()
+    doc = json.loads(out.read_text())
+    names = [ev["name"] for ev in doc["traceEvents"]]
+    assert "prefill" in names and "decode" in names and "sequences" in names
+    req = [ev for ev in doc["traceEvents"] if ev["name"] == "request"]
+    assert len(req) == 1 and req[0]["args"]["correlation_id"] == "cid-42"
+    assert req[0]["args"]["completion_tokens"] == 3 and req[0]["dur"] > 0
+    assert any(ev["name"] == "first_token" and ev["args"]["correlation_id"] == "cid-42" for ev in doc["traceEvents"])
