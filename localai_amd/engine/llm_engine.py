@@ -34,7 +34,10 @@ from ..gguf import GGUFReader
 from ..models.decoder import DecoderModel, ForwardBatch, TPInfo
 from ..native import core
 from ..tokenizer import Tokenizer
+from .prompt_cache import PromptCacheFiles
 from .sampling_params import SamplingParams
+from .speculative import ngram_draft
+from ..utils import faults
 from ..utils.trace import get_tracer, roctx
 
 log = logging.getLogger("localai_amd.engine")
@@ -138,6 +141,8 @@ class LLMEngine:
             # prefill / big decode batches run hipBLASLt on bf16 copies: materialise before any graph capture
             self._materialize_bf16()
         num_blocks = self._num_kv_blocks()
+        if faults.hit("kv_alloc"):
+            raise faults.InjectedFault("hipMalloc failed for the KV cache (injected fault): out of memory")
         self.kv = self.model.new_kv_cache(num_blocks, bs)
         self.sched = core.Scheduler(num_blocks, bs, cfg.max_num_seqs, cfg.max_batched_tokens, self.ctx,
                                     cfg.prefix_cache, 1 if (cfg.use_graphs and self.device.type == "cuda") else 0)
@@ -149,11 +154,14 @@ class LLMEngine:
         self._wake = threading.Event()
         self._thread: Optional[threading.Thread] = None
         self._stop = False
+        self.healthy = True          # False after a fatal device error: the model manager respawns
+        self.fatal_error = ""
         self._graphs: Dict[int, tuple] = {}
         self.tracer = get_tracer()
+        self._pcache = PromptCacheFiles()
         self._graph_pool = None
         self.metrics = {"prompt_tokens": 0, "gen_tokens": 0, "steps": 0, "prefill_s": 0.0, "decode_s": 0.0,
-                        "requests": 0}
+                        "requests": 0, "spec_steps": 0, "spec_drafted": 0, "spec_accepted": 0}
         self.last_request_stats: dict = {}
         self.busy = False
 
@@ -200,6 +208,9 @@ class LLMEngine:
         `sink.push(text, n_generated)` (no Python Event per token) and only the final event
         reaches `callback`."""
         rid = req_id if req_id is not None else self.new_id()
+        if not self.healthy:  # dead device: refuse instead of queueing work nobody will run
+            callback(Event(finished=True, finish_reason="error", error=f"backend unhealthy: {self.fatal_error}"))
+            return rid
         if images and self.clip is not None and isinstance(prompt, str):
             # the vision tower runs on the engine thread (single GPU stream owner)
             params.resolved_seed()
@@ -304,9 +315,34 @@ class LLMEngine:
                 log.exception("engine step failed")
                 self._fail_all(str(e))
                 worked = False
+                if self._is_fatal(e):
+                    # a device fault leaves the GPU context unusable: stop taking work and let
+                    # the model manager's health check respawn the backend (pkg/model/loader.go
+                    # CheckIsLoaded semantics)
+                    self.healthy = False
+                    self.fatal_error = str(e)
+                    self._stop = True
+                    self._reject_inbox(str(e))
             if not worked:
                 self._wake.wait(0.05)
                 self._wake.clear()
+
+    @staticmethod
+    def _is_fatal(e: Exception) -> bool:
+        if isinstance(e, faults.InjectedFault):
+            return True
+        m = str(e).lower()
+        return any(k in m for k in ("hip error", "hiperror", "device-side", "illegal memory", "gpu hang",
+                                    "memory access fault", "unspecified launch failure"))
+
+    def _reject_inbox(self, msg: str):
+        while True:
+            try:
+                item = self._inbox.get_nowait()
+            except queue.Empty:
+                return
+            if isinstance(item, Request):
+                item.callback(Event(finished=True, finish_reason="error", error=msg))
 
     def _fail_all(self, msg: str):
         for rid in list(self.requests):
@@ -320,9 +356,12 @@ class LLMEngine:
         self._drain_inbox()
         if not self.requests or self._stop:
             return False
+        if faults.hit("engine_step"):
+            raise faults.InjectedFault("HIP error: memory access fault on the engine stream (injected fault)")
         self.busy = True
-        K = self._lookahead()
-        plan = self.sched.schedule(K)
+        spec_k = self._spec_k()
+        K = 1 + spec_k if spec_k else self._lookahead()
+        plan = self.sched.schedule(K)  # spec: reserves KV slots for the draft positions
         did = False
         tr = self.tracer
         p_ids = plan["p_ids"]
@@ -339,7 +378,10 @@ class LLMEngine:
         if len(d_ids):
             t0 = time.perf_counter()
             with roctx("decode"):
-                self._run_decode(plan, K)
+                if spec_k:
+                    self._run_spec(plan, spec_k)
+                else:
+                    self._run_decode(plan, K)
             t1 = time.perf_counter()
             self.metrics["decode_s"] += t1 - t0
             if tr is not None:
@@ -424,6 +466,10 @@ class LLMEngine:
         if len(r.prompt) >= self.ctx:
             r.callback(Event(finished=True, finish_reason="error", error="prompt exceeds context"))
             return
+        if r.params.prompt_cache_path and self.tp.world == 1:
+            n = self._pcache.ensure_loaded(self, r.params.prompt_cache_path)
+            if n:
+                log.info("prompt cache %s: %d tokens of KV restored", r.params.prompt_cache_path, n)
         self.requests[r.id] = r
         max_new = r.params.max_tokens if r.params.max_tokens > 0 else self.ctx
         self.sched.add(r.id, r.prompt, max_new)
@@ -554,6 +600,78 @@ class LLMEngine:
             mt = r.params.max_tokens
             rem_tok = max(rem_tok, (mt - r.n_gen) if mt > 0 else K)
         return max(1, min(K, rem_ctx, rem_tok))
+
+    SPEC_MAX_BATCH = 8   # speculation pays while decode streams weights (small batches)
+    SPEC_MAX_DRAFT = 16
+
+    def _spec_k(self) -> int:
+        """Draft length for an n-gram speculative step (engine/speculative.py), or 0: every
+        running request asked for it (n_draft) and is plain greedy, the batch is small, and no
+        prompt is still prefilling."""
+        if not self.requests or len(self.requests) > self.SPEC_MAX_BATCH or self.sched.num_waiting:
+            return 0
+        k = 0
+        for r in self.requests.values():
+            p = r.params
+            if (p.n_draft <= 0 or r.n_gen == 0 or r.grammar is not None or p.mirostat
+                    or not (p.temperature <= 0.0 or p.top_k == 1) or p.logit_bias or p.repeat_penalty != 1.0
+                    or p.frequency_penalty != 0.0 or p.presence_penalty != 0.0):
+                return 0
+            k = max(k, min(p.n_draft, self.SPEC_MAX_DRAFT))
+        return k
+
+    def _run_spec(self, plan, k: int):
+        """Verify n-gram drafts for every decoding sequence in ONE forward pass (the chunked-
+        prefill path: last token + draft at positions L-1 .. L-1+k), keep the longest prefix the
+        greedy argmax agrees with plus the model's own next token."""
+        ids = [int(x) for x in plan["d_ids"]]
+        reqs = [self.requests[i] for i in ids]
+        bm = self.sched.blocks()
+        toks, pos, slots, cu, ctxl, drafts, tabs = [], [], [], [0], [], [], []
+        for r in reqs:
+            seq = self.sched.tokens(r.id)
+            L = len(seq)
+            room = min(self.ctx - L, (r.params.max_tokens - r.n_gen) if r.params.max_tokens > 0 else self.ctx)
+            d = ngram_draft(seq, min(k, max(0, room - 1)))
+            for j, t in enumerate([seq[-1]] + d):
+                toks.append(t)
+                pos.append(L - 1 + j)
+                slots.append(bm.slot(r.id, L - 1 + j))
+            cu.append(len(toks))
+            ctxl.append(L + len(d))
+            drafts.append(d)
+            tabs.append(bm.table(r.id))
+        bt = np.zeros((len(reqs), max(len(t) for t in tabs)), dtype=np.int32)
+        for i, t in enumerate(tabs):
+            bt[i, :len(t)] = t
+        qlens = [cu[i + 1] - cu[i] for i in range(len(reqs))]
+        i32 = lambda a: self._dev(np.asarray(a, dtype=np.int32))  # noqa: E731
+        fb = ForwardBatch(tokens=i32(toks), pos=i32(pos), slots=i32(slots), decode=False, block_tables=self._dev(bt),
+                          cu_q=i32(cu), ctx_lens=i32(ctxl),
+                          tiles=ops.prefill_tiles(qlens, self.device) if self.device.type == "cuda" else None)
+        logits = self.model.forward(fb, self.kv)  # [T, V]: every position verifies one draft token
+        ban = [i for i, r in enumerate(reqs) if r.params.ignore_eos]
+        if ban and self._eog_list:
+            rows = torch.cat([torch.arange(cu[i], cu[i + 1]) for i in ban]).to(logits.device)
+            cols = torch.tensor(self._eog_list, device=logits.device)
+            logits[rows.unsqueeze(1), cols.unsqueeze(0)] = -math.inf
+        am = logits.argmax(-1).cpu().numpy()
+        now = time.perf_counter()
+        self.metrics["spec_steps"] += 1
+        for i, r in enumerate(reqs):
+            d, row = drafts[i], am[cu[i]:cu[i + 1]]
+            j = 0
+            while j < len(d) and int(row[j]) == d[j]:
+                j += 1
+            self.metrics["spec_drafted"] += len(d)
+            self.metrics["spec_accepted"] += j
+            out = d[:j] + [int(row[j])]
+            for t in out:
+                self._on_token(r, t, now, append=False)
+                if r.done:
+                    break
+            if not r.done:
+                self.sched.append_run(r.id, out)
 
     def _run_decode(self, plan, K: int = 1):
         ids = [int(x) for x in plan["d_ids"]]
@@ -916,6 +1034,15 @@ class LLMEngine:
             return
         r.done = True
         tail = r.stream.flush() if (flush and r.stream is not None) else b""
+        p = r.params
+        if p.prompt_cache_path and not p.prompt_cache_ro and r.n_gen > 0 and self.tp.world == 1 \
+                and self.sched.has(r.id):
+            try:
+                toks = self.sched.tokens(r.id)
+                keep = len(toks) - 1 if p.prompt_cache_all else r.n_prompt  # tokens whose KV exists
+                self._pcache.store(self, r.id, toks[:keep], p.prompt_cache_path)
+            except Exception:
+                log.exception("saving prompt cache %s", p.prompt_cache_path)
         self.sched.finish(r.id)
         self.requests.pop(r.id, None)
         end = time.perf_counter()

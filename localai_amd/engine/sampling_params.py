@@ -32,6 +32,10 @@ class SamplingParams:
     grammar: str = ""
     n_probs: int = 0
     correlation_id: str = ""          # X-Correlation-ID of the HTTP request (PredictOptions.CorrelationId)
+    n_draft: int = 0                  # speculative (n-gram) draft length for greedy requests
+    prompt_cache_path: str = ""       # persistent KV prefix file (engine/prompt_cache.py)
+    prompt_cache_all: bool = False    # also persist the generated tokens' KV
+    prompt_cache_ro: bool = False     # read the file, never write it
 
     def resolved_seed(self) -> int:
         if self.seed is None or self.seed < 0:
@@ -62,6 +66,10 @@ class SamplingParams:
             n_keep=int(po.NKeep),
             grammar=po.Grammar,
             correlation_id=po.CorrelationId,
+            n_draft=int(po.NDraft),
+            prompt_cache_path=po.PromptCachePath,
+            prompt_cache_all=bool(po.PromptCacheAll),
+            prompt_cache_ro=bool(po.PromptCacheRO),
         )
         if po.LogitBias:
             import json

@@ -166,10 +166,15 @@ def update_request_config(cfg: BackendConfig, req: dict):
         cfg.prompt_strings.extend(p for p in pr if isinstance(p, str))
 
 
-def predict_options(cfg: BackendConfig, prompt: str, messages: Optional[list] = None) -> pb.PredictOptions:
+def predict_options(cfg: BackendConfig, prompt: str, messages: Optional[list] = None,
+                    models_path: str = "") -> pb.PredictOptions:
     """gRPCPredictOpts (core/backend/options.go:180-229)."""
     P = cfg.raw["parameters"]
     r = cfg.raw
+    pc_path = ""
+    if r.get("prompt_cache_path"):  # options.go:181-190: relative to the models directory
+        pc_path = os.path.join(models_path, str(r["prompt_cache_path"]))
+        os.makedirs(os.path.dirname(pc_path) or ".", exist_ok=True)
     po = pb.PredictOptions(
         Prompt=prompt,
         Temperature=float(P.get("temperature") if P.get("temperature") is not None else 0.9),
@@ -179,6 +184,7 @@ def predict_options(cfg: BackendConfig, prompt: str, messages: Optional[list] = 
         Threads=int(r.get("threads") or 4),
         NDraft=int(r.get("n_draft") or 0),
         PromptCacheAll=bool(r.get("prompt_cache_all")), PromptCacheRO=bool(r.get("prompt_cache_ro")),
+        PromptCachePath=pc_path,
         F16KV=bool(r.get("f16")), DebugMode=bool(r.get("debug")), Grammar=str(r.get("grammar") or ""),
         NegativePromptScale=float(P.get("negative_prompt_scale") or 0),
         RopeFreqBase=float(P.get("rope_freq_base") or 0), RopeFreqScale=float(P.get("rope_freq_scale") or 0),
@@ -243,7 +249,7 @@ class Inference:
     async def stream(self, prompt: str) -> AsyncIterator[Tuple[str, TokenUsage, bool]]:
         """Yields (text_delta, usage, is_final).  Text deltas are whole UTF-8 sequences."""
         lm = await self._backend()
-        po = predict_options(self.cfg, prompt, self.req.get("messages"))
+        po = predict_options(self.cfg, prompt, self.req.get("messages"), self.state.models_path)
         self._media(po)
         mid = lm.id
         self.state.manager.mark_busy(mid, True)
@@ -285,7 +291,7 @@ class Inference:
 
     async def predict(self, prompt: str) -> Tuple[str, TokenUsage]:
         lm = await self._backend()
-        po = predict_options(self.cfg, prompt, self.req.get("messages"))
+        po = predict_options(self.cfg, prompt, self.req.get("messages"), self.state.models_path)
         self._media(po)
         self.state.manager.mark_busy(lm.id, True)
         t0 = time.perf_counter()

@@ -144,8 +144,16 @@ class ModelManager:
             log.warning("backend for %s died (rc=%s); respawning", lm.id, lm.process.returncode)
             self.models.pop(lm.id, None)
             return False
-        if isinstance(lm.handle, GRPCBackend) and not await lm.handle.health(timeout=120):
+        if hasattr(lm.handle, "health") and not await lm.handle.health(timeout=120):
+            log.warning("backend for %s is unhealthy; respawning", lm.id)
             self.models.pop(lm.id, None)
+            try:
+                if lm.servicer is not None and getattr(lm.servicer, "engine", None) is not None:
+                    lm.servicer.engine.shutdown()
+                if lm.process is not None:
+                    lm.process.kill()
+            except Exception:
+                log.exception("tearing down the unhealthy backend of %s", lm.id)
             return False
         return True
 

@@ -530,7 +530,8 @@ async def _native_stream(request, state, cfg, req, pred_input: str, cid: str, cr
     from ..native import http
     from .inference import predict_options
     from .native_server import NativeHandledResponse
-    po = predict_options(cfg, pred_input, req.get("messages"))
+    po = predict_options(cfg, pred_input, req.get("messages"), state.models_path)
+    po.CorrelationId = req.get("_correlation_id", "")
     prompt = sv._prompt(po)
     params = sv._params(po)
     obj = "chat.completion.chunk" if kind == "chat" else "text_completion"

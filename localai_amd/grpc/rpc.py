@@ -105,7 +105,8 @@ class EmbeddedBackend:
         return call
 
     async def health(self, timeout: float = 5.0) -> bool:
-        return True
+        res = await self.servicer.Health(pb.HealthMessage(), None)
+        return res.message == b"OK"
 
     async def close(self):
         pass

@@ -21,6 +21,7 @@ import time
 from typing import Optional
 
 from . import backend_pb as pb
+from ..utils import faults
 
 log = logging.getLogger("localai_amd.servicer")
 
@@ -109,6 +110,9 @@ class EngineServicer:
 
     # ------------------------------------------------------------------ RPCs
     async def Health(self, request, context=None):
+        eng = getattr(self, "engine", None)
+        if eng is not None and not getattr(eng, "healthy", True):
+            return pb.Reply(message=f"unhealthy: {eng.fatal_error}".encode())
         return pb.Reply(message=b"OK")
 
     async def LoadModel(self, request, context=None):
@@ -214,6 +218,8 @@ class EngineServicer:
         return SamplingParams.from_predict_options(request)
 
     async def PredictStream(self, request, context=None):
+        if os.environ.get("LOCALAI_AMD_WORKER") and faults.hit("worker_exit"):
+            os._exit(17)  # injected fault: the worker process dies mid-service
         eng = self._require_engine()
         ch = _Channel(_pump_for(asyncio.get_running_loop()))
         rid = eng.add_request(self._prompt(request), self._params(request), ch.put, images=self._images(request))
@@ -238,6 +244,8 @@ class EngineServicer:
                     return
                 if buf:
                     yield pb.Reply(message=bytes(buf))
+                    if faults.hit("grpc_stream_drop"):
+                        raise faults.InjectedFault("gRPC stream dropped (injected fault)")
         finally:
             if not finished:
                 eng.abort(rid)  # client went away / generator closed: free the sequence (fixes Q4)

@@ -23,6 +23,7 @@ def main(argv=None) -> int:
     a = ap.parse_args(argv)
     logging.basicConfig(level=logging.DEBUG if os.environ.get("LOCALAI_DEBUG") == "true" else logging.INFO,
                         format="%(asctime)s %(levelname)s worker[%(process)d] %(message)s")
+    os.environ["LOCALAI_AMD_WORKER"] = "1"  # arms the worker-only fault sites (utils/faults.py)
     import torch  # noqa: F401  (loads the HIP runtime before our kernels)
     from .grpc.rpc import serve
     from .grpc.servicer import EngineServicer

@@ -1,0 +1,99 @@
+"""n-gram speculative decoding (exactly the greedy output, fewer forward passes) and the
+persistent prompt cache (prompt_cache_path: KV prefix blocks saved, restored into a fresh
+engine's prefix cache), on the CPU engine."""
+import os
+
+import pytest
+
+from localai_amd.engine.llm_engine import EngineConfig, LLMEngine
+from localai_amd.engine.sampling_params import SamplingParams
+from localai_amd.engine.speculative import ngram_draft
+
+
+def _engine(path, **kw):
+    return LLMEngine(EngineConfig(model_path=path, device="cpu", context_size=512, max_num_seqs=4,
+                                  use_graphs=False, block_size=16, **kw))
+
+
+def test_ngram_draft_lookup():
+    assert ngram_draft([1, 2, 3, 9, 1, 2, 3], 3) == [9, 1, 2]       # 3-gram match
+    assert ngram_draft([5, 6, 7, 5, 6], 2) == [7, 5]                # 2-gram match
+    assert ngram_draft([4, 8, 1, 4], 4) == [8, 1, 4]                # 1-gram, truncated at the end
+    assert ngram_draft([1, 2, 3], 4) == []                          # no earlier occurrence
+    assert ngram_draft([1, 2, 1, 2, 1], 2) == [2, 1]                # latest match wins
+    assert ngram_draft([3, 3], 0) == []
+
+
+def test_speculative_greedy_output_is_exact(tiny_model_path, monkeypatch):
+    """Whatever the drafts are (right, wrong, partly right), the output is the greedy output; right
+    drafts cut forward passes."""
+    import localai_amd.engine.llm_engine as le
+    eng = _engine(tiny_model_path)
+    prompt = "one two three four one two three four one two three four one two"
+    n_prompt = len(eng.tokenize(prompt))
+    truth, evs = [], []
+
+    def cb(ev):
+        if ev.token >= 0:
+            truth.append(ev.token)
+        if ev.finished:
+            evs.append(ev)
+
+    eng.add_request(prompt, SamplingParams(max_tokens=24, temperature=0.0, ignore_eos=True), cb)
+    while not evs:
+        eng.step()
+    base = eng.generate(prompt, SamplingParams(max_tokens=24, temperature=0.0, ignore_eos=True))
+    calls = [0]
+
+    def oracle(seq, k, **kw):  # alternately the true continuation and a wrong guess
+        calls[0] += 1
+        done = len(seq) - n_prompt
+        nxt = truth[done:done + k]
+        if calls[0] % 2 == 0 and nxt:
+            nxt = nxt[:1] + [(nxt[1] + 1) if len(nxt) > 1 else nxt[0]]
+        return list(nxt)
+
+    monkeypatch.setattr(le, "ngram_draft", oracle)
+    steps0 = eng.metrics["steps"]
+    spec = eng.generate(prompt, SamplingParams(max_tokens=24, temperature=0.0, ignore_eos=True, n_draft=4))
+    assert spec["completion_tokens"] == 24
+    assert spec["text"] == base["text"]
+    assert eng.metrics["spec_steps"] > 0 and eng.metrics["spec_accepted"] > 0
+    assert eng.metrics["steps"] - steps0 < 24  # accepted drafts saved forward passes
+    # the real n-gram drafter runs end to end too (exact output whatever it proposes)
+    monkeypatch.setattr(le, "ngram_draft", ngram_draft)
+    again = eng.generate(prompt, SamplingParams(max_tokens=24, temperature=0.0, ignore_eos=True, n_draft=4))
+    assert again["text"] == base["text"]
+
+
+def test_prompt_cache_persists_and_restores(tiny_model_path, tmp_path):
+    path = str(tmp_path / "cache" / "prompt.safetensors")
+    prompt = " ".join(f"w{i}" for i in range(60))
+    p = dict(max_tokens=4, temperature=0.0, ignore_eos=True, prompt_cache_path=path)
+    e1 = _engine(tiny_model_path)
+    r1 = e1.generate(prompt, SamplingParams(**p))
+    assert os.path.exists(path)
+    # a fresh engine (empty prefix cache) restores the blocks and reuses them
+    e2 = _engine(tiny_model_path)
+    bm = e2.sched.blocks()
+    assert bm.hit_tokens == 0
+    r2 = e2.generate(prompt, SamplingParams(**p, prompt_cache_ro=True))
+    assert bm.hit_tokens >= 16, bm.hit_tokens
+    assert r2["text"] == r1["text"]
+    # a foreign / corrupt file is ignored, not fatal
+    bad = tmp_path / "bad.safetensors"
+    bad.write_bytes(b"not a cache")
+    e3 = _engine(tiny_model_path)
+    r3 = e3.generate(prompt, SamplingParams(max_tokens=2, temperature=0.0, ignore_eos=True,
+                                            prompt_cache_path=str(bad), prompt_cache_ro=True))
+    assert r3["completion_tokens"] == 2
+
+
+@pytest.mark.parametrize("ro", [False, True])
+def test_prompt_cache_read_only_never_writes(tiny_model_path, tmp_path, ro):
+    path = str(tmp_path / f"pc_{ro}.safetensors")
+    e = _engine(tiny_model_path)
+    e.generate("a b c d e f g h i j k l m n o p q r s t u v w x y z",
+               SamplingParams(max_tokens=2, temperature=0.0, ignore_eos=True, prompt_cache_path=path,
+                              prompt_cache_ro=ro))
+    assert os.path.exists(path) is (not ro)
