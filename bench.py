@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--clients", type=int, default=int(os.environ.get("BENCH_CLIENTS", 4)),
                     help="load-generator processes (separate from the server process)")
     ap.add_argument("--cache-dir", default=os.environ.get("LOCALAI_AMD_CACHE", "/tmp/localai_amd_cache"))
+    ap.add_argument("--n-draft", type=int, default=0,
+                    help="engine mode: n-gram speculative draft length (model-config n_draft); 0 = off")
     return ap.parse_args()
 
 
@@ -192,7 +194,8 @@ def main():
                        else args.preset, "global_batch": args.concurrency * world, "seq_len": seq,
                        "prompt_tokens": args.prompt_len, "max_tokens": args.max_tokens,
                        "parallelism": f"dp{world}", "endpoint": "/v1/chat/completions (stream)",
-                       "mode": args.mode, "sampling": "greedy, mirostat 0, ignore_eos"},
+                       "mode": args.mode, "sampling": "greedy, mirostat 0, ignore_eos",
+                       **({"n_draft": args.n_draft} if args.n_draft else {})},
             "setup_s": {"model_gen": round(t_gen, 1), "load": round(t_load, 1), "graph_capture": round(t_capture, 1)},
         }
         print(json.dumps(out), flush=True)
@@ -230,7 +233,7 @@ class EngineRunner:
                         done[0] += 1
 
             eng.add_request(prompt, self.SP(max_tokens=self.args.max_tokens, temperature=0.0, ignore_eos=True,
-                                            mirostat=0, repeat_penalty=1.0), cb)
+                                            mirostat=0, repeat_penalty=1.0, n_draft=self.args.n_draft), cb)
         while done[0] < len(contents):
             eng.step()
         return ttft, ntok[0]

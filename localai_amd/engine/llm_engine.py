@@ -93,6 +93,9 @@ class Request:
     grammar: object = None       # native GrammarState (GBNF-constrained decoding)
     mm_pos: object = None        # {prompt position: row of mm_emb} for image-embedding positions
     mm_emb: object = None        # [rows, n_embd] f32 projected image embeddings (device)
+    spec_drafted: int = 0        # n-gram speculation bookkeeping (adaptive back-off)
+    spec_accepted: int = 0
+    spec_off: bool = False
 
 
 def _noop_callback(ev):  # follower ranks: the leader talks to the client
@@ -613,7 +616,7 @@ class LLMEngine:
         k = 0
         for r in self.requests.values():
             p = r.params
-            if (p.n_draft <= 0 or r.n_gen == 0 or r.grammar is not None or p.mirostat
+            if (p.n_draft <= 0 or r.n_gen == 0 or r.spec_off or r.grammar is not None or p.mirostat
                     or not (p.temperature <= 0.0 or p.top_k == 1) or p.logit_bias or p.repeat_penalty != 1.0
                     or p.frequency_penalty != 0.0 or p.presence_penalty != 0.0):
                 return 0
@@ -641,6 +644,9 @@ class LLMEngine:
             ctxl.append(L + len(d))
             drafts.append(d)
             tabs.append(bm.table(r.id))
+        if not any(drafts):  # nothing to verify: the ordinary (graph) decode step is cheaper
+            self._run_decode(plan, 1)
+            return
         bt = np.zeros((len(reqs), max(len(t) for t in tabs)), dtype=np.int32)
         for i, t in enumerate(tabs):
             bt[i, :len(t)] = t
@@ -665,6 +671,10 @@ class LLMEngine:
                 j += 1
             self.metrics["spec_drafted"] += len(d)
             self.metrics["spec_accepted"] += j
+            r.spec_drafted += len(d)
+            r.spec_accepted += j
+            if r.spec_drafted >= 32 and r.spec_accepted < 0.15 * r.spec_drafted:
+                r.spec_off = True  # low acceptance: a verify pass costs more than it saves
             out = d[:j] + [int(row[j])]
             for t in out:
                 self._on_token(r, t, now, append=False)
