@@ -46,6 +46,8 @@ def lib():
             "la_qgemm_skinny": [I, P, P, P, P, I, I, P, I, I, I, P, I, LNG, P],
             "la_qgemm_mid": [I, P, P, P, P, I, I, P, I, I, I, P, I, LNG, I, P],
             "la_qgemm_ws": [I, P, P, P, P, I, I, P, I, I, I, P, I, LNG, P],
+            "la_qgemv_dp4": [I, P, P, P, I, P, I, I, I, P, I, LNG, P],
+            "la_gemv_variant": [I],
             "la_add_norm": [P, P, LNG, I, P, I, P, P, P, I, I, F, I, P, P],
             "la_rope_kv": [P, LNG, I, P, P, P, P, I, I, I, I, I, I, P, P, P, I, P],
             "la_act": [P, LNG, I, P, P, I, I, I, P],
@@ -131,7 +133,8 @@ class QWeight:
             b = src.view(N, K // 256, 144)
             qs = b[:, :, 16:].contiguous().view(N, K // 2)
             hdr = b[:, :, :16].contiguous().view(N, K // 256 * 16)
-            return QWeight(FMT_Q4_K, N, K, (qs, hdr, None, None), ref=ref)
+            scm, dd = _q4k_gemv_planes(b[:, :, :16])
+            return QWeight(FMT_Q4_K, N, K, (qs, hdr, scm, dd), ref=ref)
         if t == GGMLType.Q6_K and K % 256 == 0:
             b = src.view(N, K // 256, 210)
             ql = b[:, :, :128].contiguous().view(N, K // 2)
@@ -159,6 +162,12 @@ class QWeight:
 
     def ptrs(self):
         return [_ptr(p) for p in self.planes]
+
+    @property
+    def gemv_ok(self) -> bool:
+        """Has the planes the int8-dot decode GEMV (gemv_dp4.hip) reads."""
+        return (self.fmt == FMT_Q6_K or (self.fmt == FMT_Q4_K and self.planes[2] is not None)) \
+            and self.K % 256 == 0
 
     def materialize_bf16(self) -> torch.Tensor:
         """HBM-resident bf16 copy for the large-M (prefill) GEMM path."""
@@ -203,6 +212,24 @@ class QWeight:
             c = per_row // world
             planes.append(p[:, rank * c:(rank + 1) * c].contiguous())
         return QWeight(self.fmt, self.N, k, tuple(planes), ref=ref)
+
+
+def _q4k_gemv_planes(h: torch.Tensor):
+    """From Q4_K block headers h [N, nsb, 16] (f16 d, f16 dmin, 12 packed 6-bit scales/mins)
+    build the two planes the decode GEMV reads: scm [N, nsb*16] = (sc0,m0,sc1,m1,...) and
+    dd [N, nsb*4] = (d, dmin).  Unpacking is ggml's get_scale_min_k4 [external, llama.cpp
+    ggml-quants.c], done once at load instead of per lane per step."""
+    N, nsb, _ = h.shape
+    q = h[:, :, 4:16].to(torch.int32)
+    sc = torch.empty(N, nsb, 8, dtype=torch.int32, device=h.device)
+    mn = torch.empty_like(sc)
+    sc[..., :4] = q[..., 0:4] & 63
+    mn[..., :4] = q[..., 4:8] & 63
+    sc[..., 4:] = (q[..., 8:12] & 0xF) | ((q[..., 0:4] >> 6) << 4)
+    mn[..., 4:] = (q[..., 8:12] >> 4) | ((q[..., 4:8] >> 6) << 4)
+    scm = torch.stack([sc, mn], -1).to(torch.uint8).reshape(N, nsb * 16).contiguous()
+    dd = h[:, :, :4].contiguous().view(N, nsb * 4)
+    return scm, dd
 
 
 def concat_rows(ws: Sequence[QWeight]) -> Optional[QWeight]:
@@ -291,7 +318,46 @@ def pick_splits(N: int, K: int, M: int) -> int:
     return best
 
 
+def _gemv_splits(ws, K: int, M: int) -> int:
+    """Split-K for the dp4 GEMV: ~2 workgroups per CU (pick_splits), then grown until the
+    workgroup's int8 activation image (kper bytes + 16-run sums + scales per row) fits 64 KiB."""
+    nsb = K // 256
+    S = min(pick_splits(w.N, w.K, M) for w in ws)
+    while nsb % S:
+        S -= 1
+    mt = 1 if M == 1 else (2 if M == 2 else 4)
+    while mt * (K // S) * (1 + 4 / 16 + 4 / 32) > 65536:
+        S = next(s for s in range(S + 1, nsb + 1) if nsb % s == 0)
+    return S
+
+
+def gemv_dp4(x: torch.Tensor, ws: Sequence[QWeight], S: int, out: torch.Tensor) -> None:
+    """out[S, M, sum(N)] = split-K partials of x @ [W0; W1; ...]^T from the int8-dot decode GEMV,
+    up to 3 weights (mixed Q4_K / Q6_K, same K) per launch."""
+    M, K = x.shape
+    Ntot = out.shape[-1]
+    # launch groups: <= 3 weights whose formats form at most two runs [FA ...][FB ...]
+    groups: List[List[QWeight]] = []
+    for w in ws:
+        g = groups[-1] if groups else None
+        if g is not None and len(g) < 3 and (len({v.fmt for v in g}) == 1 or w.fmt == g[-1].fmt):
+            g.append(w)
+        else:
+            groups.append([w])
+    col = 0
+    for seg in groups:
+        n = len(seg)
+        fmts = (ctypes.c_int * n)(*[w.fmt for w in seg])
+        planes = (ctypes.c_void_p * (4 * n))(*[p for w in seg for p in w.ptrs()])
+        Ns = (ctypes.c_int * n)(*[w.N for w in seg])
+        _check(lib().la_qgemv_dp4(n, fmts, planes, Ns, K, x.data_ptr(), K, M, S, out.data_ptr() + col * 4, Ntot,
+                                  M * Ntot, _stream()), "la_qgemv_dp4")
+        col += sum(w.N for w in seg)
+
+
 SKINNY_MAX_M = 64
+GEMV_MAX_M = 2           # M <= GEMV_MAX_M: int8-dot decode GEMV (gemv_dp4.hip, supports M <= 4) on Q4_K/Q6_K
+GEMV_DP4 = os.environ.get("LOCALAI_AMD_GEMV", "dp4") == "dp4"
 MID_MAX_M = 256          # 64 < M <= MID_MAX_M: quantised mid-M MFMA GEMM (gemm_mid.hip) or hipBLASLt
 MID_FMTS = (FMT_Q4_K, FMT_Q6_K, FMT_Q8_0)
 GEMM_AUTOTUNE = True
@@ -451,6 +517,17 @@ def linear_multi(x: torch.Tensor, ws: Sequence[QWeight], bias: Optional[torch.Te
             _run_ws(x, ws, S, out, Ntot)
         else:
             _run_mid(x, ws, S, out, Ntot, tile)
+        return Partial(out, bias)
+    use_gemv = (force == "dp4") or (force is None and use_skinny and GEMV_DP4 and M <= GEMV_MAX_M
+                                    and all(w.gemv_ok for w in ws))
+    if use_gemv:
+        if M > 4 or not all(w.gemv_ok for w in ws):
+            raise ValueError("linear: dp4 GEMV needs M <= 4 and Q4_K/Q6_K weights")
+        S = _gemv_splits(ws, K, M)
+        out = out_slabs
+        if out is None or out.shape != (S, M, Ntot):
+            out = torch.empty(S, M, Ntot, dtype=torch.float32, device=x.device)
+        gemv_dp4(x, ws, S, out)
         return Partial(out, bias)
     if use_skinny:
         S = min(pick_splits(w.N, w.K, M) for w in ws)

@@ -1,0 +1,428 @@
+// Batch-1..4 decode GEMV on packed int8 dot products (v_dot4_i32_i8), Q4_K and Q6_K weights.
+//
+// Why not MFMA here: at M <= 4 the bf16 MFMA path (gemm_skinny.hip) spends ~4.35 VALU lane-ops
+// per weight dequantising to bf16 (profiles/decode_gemv_study.md, skinny_pmc.md) and wastes
+// 15/16 of every 16x16 tile.  This kernel instead quantises the activation row once per
+// workgroup to int8 with one scale per 32 elements (ggml's q8_1 activation blocks, which is
+// what the reference's GPU build feeds its k-quant mmvq dot products) and multiplies the weights' raw
+// 4-/6-bit codes with 4-way int8 dots: ~1 VALU op per weight, so the kernel is left to stream.
+//
+// Work mapping (wave64): a row's super-block is 128 contiguous quant bytes, read by 8 adjacent
+// lanes x 16 B (fully used 128 B runs: 5.0 TB/s class access pattern, decode_gemv_study.md §1).
+// A wave covers 8 rows per load instruction, GV_RS row slots per wave, 4 waves per workgroup,
+// so a workgroup owns 64 rows and one K split; grid.y = split-K, partials go to fp32 slabs
+// [S][M][ldo] which the consumer (add_norm / rope_kv / act) sums -- the same contract as the
+// other GEMMs (ops.Partial).
+//
+// Activation image in LDS (per row m of x, for this split's K range):
+//   xq  int8 [kper]       q = round(x * 127 / absmax_32)   (ggml q8_1 blocks of 32)
+//   bs  int32 [kper/16]   sum of q over each 16-run (Q4_K min term, Q6_K -32 offset)
+//   dx  f32  [kper/32]    absmax_32 / 127
+// Weight side: Q4_K uses the qs plane plus two planes made at load time (ops.QWeight.from_raw):
+//   scm u8 [N][K/256][16]  (sc0,m0,sc1,m1, sc2,m2,...): the 6-bit scales/mins unpacked
+//   dd  u8 [N][K/256][4]   f16 d, f16 dmin
+// Q6_K uses its ql / qh / sc / d planes unchanged.
+// Reference semantics: ggml dequantize_row_q4_K / q6_K and ggml_vec_dot_q4_K_q8_K
+// [external, llama.cpp @ d5cb868 ggml/src/ggml-quants.c]; used for the decode MUL_MAT of
+// SURVEY.md §2.8 K5 (mmvq.cu in the reference build).
+// One launch may cover up to GV_SEGS weights of different formats sharing K (e.g. a Q4_K q|k
+// and a Q6_K v): grid.x walks the row blocks of all segments, each block branches (uniformly)
+// on its segment's format, and writes its columns side by side into the same slabs.
+//
+// The first super-block of weights is requested BEFORE the activation image is built, so the
+// weight stream's first HBM round trip overlaps the x load / quantisation prologue.
+#include "qweight.h"
+
+namespace la {
+
+constexpr int GV_THREADS = 256;
+constexpr int GV_RS = 2;                 // row slots (of 8 rows) per wave
+constexpr int GV_ROWS = 4 * 8 * GV_RS;   // rows per workgroup
+constexpr int GV_SEGS = 3;
+
+struct GVArgs {
+  QW w[GV_SEGS];
+  int fmt[GV_SEGS];
+  int blk_end[GV_SEGS];  // exclusive prefix sum of row blocks
+  int col0[GV_SEGS];     // first output column of each segment
+  int nseg;
+};
+
+LA_DEV int dot4(uint32_t a, uint32_t b, int c) { return __builtin_amdgcn_sdot4((int)a, (int)b, c, false); }
+
+template <int NT>
+LA_DEV u32x4 ldg16(const uint8_t* p) {
+  if constexpr (NT) return __builtin_nontemporal_load((const u32x4*)p);
+  else return *(const u32x4*)p;
+}
+
+// Quantise x[m, k0 : k0+kper] into the LDS image (ggml q8_1 granularity: one scale per 32).
+// Wave w handles super-blocks w, w+4, ...; lane l owns elements 4l..4l+3 of the super-block,
+// so 8 lanes share a 32-block and 4 lanes a 16-run.
+template <int MT>
+LA_DEV void quantize_x(const bf16* X, int ldx, int M, int k0, int kper, int8_t* xq, int* bs, float* dx) {
+  const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int nsb = kper >> 8;
+  for (int m = 0; m < MT; ++m) {
+    if (m >= M) break;
+    const bf16* xr = X + (size_t)m * ldx + k0;
+    int8_t* q = xq + m * kper;
+    int* b = bs + m * (kper >> 4);
+    float* d = dx + m * (kper >> 5);
+    for (int sb = wv; sb < nsb; sb += 4) {
+      const u32x2 raw = *(const u32x2*)(xr + sb * 256 + 4 * l);
+      const float v0 = bf16_bits_to_f(raw.x & 0xFFFFu), v1 = bf16_bits_to_f(raw.x >> 16);
+      const float v2 = bf16_bits_to_f(raw.y & 0xFFFFu), v3 = bf16_bits_to_f(raw.y >> 16);
+      const float amax = group_max<8>(fmaxf(fmaxf(fabsf(v0), fabsf(v1)), fmaxf(fabsf(v2), fabsf(v3))));
+      const float inv = amax > 0.f ? 127.f / amax : 0.f;
+      const int q0 = __float2int_rn(v0 * inv), q1 = __float2int_rn(v1 * inv);
+      const int q2 = __float2int_rn(v2 * inv), q3 = __float2int_rn(v3 * inv);
+      const uint32_t packed = (uint32_t)(q0 & 0xFF) | ((uint32_t)(q1 & 0xFF) << 8) |
+                              ((uint32_t)(q2 & 0xFF) << 16) | ((uint32_t)(q3 & 0xFF) << 24);
+      *(uint32_t*)(q + sb * 256 + 4 * l) = packed;
+      int s = q0 + q1 + q2 + q3;
+      s += __shfl_xor(s, 1, 64);
+      s += __shfl_xor(s, 2, 64);
+      if ((l & 3) == 0) b[sb * 16 + (l >> 2)] = s;
+      if ((l & 7) == 0) d[sb * 8 + (l >> 3)] = amax / 127.f;
+    }
+  }
+}
+
+template <int MT>
+LA_DEV void gv_store(const float (&acc)[MT][GV_RS], const int (&n)[GV_RS], int N, int M, int t, float* o,
+                     int ldo, int col0) {
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    if (m < M) {
+#pragma unroll
+      for (int s = 0; s < GV_RS; ++s) {
+        const float v = group_sum<8>(acc[m][s]);
+        if (t == 0 && n[s] < N) o[(size_t)m * ldo + col0 + n[s]] = v;
+      }
+    }
+  }
+}
+
+template <int MT, int NT, int EARLY>
+LA_DEV void gv_q4k(const QW& w, int row0, const bf16* X, int ldx, int M, int kper, float* o, int ldo, int col0,
+                   int8_t* xq, int* bs, float* dx) {
+  const int k0 = blockIdx.y * kper, nsb = kper >> 8, sb0 = k0 >> 8;
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = lane >> 3, t = lane & 7;
+  const int j = t >> 1, h = t & 1;
+  const int xlo = 64 * j + 16 * h;  // element offset of this lane's low-nibble run (high: +32)
+  const int blo = 4 * j + h;        // its 16-run index (high-nibble run: blo + 2)
+  const size_t qrow = (size_t)(w.K >> 1), srow = (size_t)(w.K >> 8) * 16, drow = (size_t)(w.K >> 8) * 4;
+  int n[GV_RS];
+  const uint8_t* qp[GV_RS];
+  const uint8_t* sp[GV_RS];
+  const uint8_t* dp[GV_RS];
+#pragma unroll
+  for (int s = 0; s < GV_RS; ++s) {
+    n[s] = row0 + wv * (8 * GV_RS) + s * 8 + r;
+    const size_t nc = n[s] < w.N ? n[s] : w.N - 1;  // clamped row for loads
+    qp[s] = w.p0 + nc * qrow + (size_t)sb0 * 128 + 16 * t;
+    sp[s] = w.p2 + nc * srow + (size_t)sb0 * 16 + 4 * j;
+    dp[s] = w.p3 + nc * drow + (size_t)sb0 * 4;
+  }
+  if constexpr (!EARLY) {
+    quantize_x<MT>(X, ldx, M, k0, kper, xq, bs, dx);
+    __syncthreads();
+  }
+  u32x4 qa[GV_RS];
+  uint32_t sa[GV_RS], da[GV_RS];
+#pragma unroll
+  for (int s = 0; s < GV_RS; ++s) {
+    qa[s] = ldg16<NT>(qp[s]);
+    sa[s] = *(const uint32_t*)sp[s];
+    da[s] = *(const uint32_t*)dp[s];
+  }
+  if constexpr (EARLY) {
+    quantize_x<MT>(X, ldx, M, k0, kper, xq, bs, dx);
+    __syncthreads();
+  }
+
+  float acc[MT][GV_RS];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int s = 0; s < GV_RS; ++s) acc[m][s] = 0.f;
+
+  for (int sb = 0; sb < nsb; ++sb) {
+    u32x4 qn[GV_RS];
+    uint32_t sn[GV_RS], dn[GV_RS];
+    if (sb + 1 < nsb) {
+#pragma unroll
+      for (int s = 0; s < GV_RS; ++s) {
+        qn[s] = ldg16<NT>(qp[s] + (sb + 1) * 128);
+        sn[s] = *(const uint32_t*)(sp[s] + (sb + 1) * 16);
+        dn[s] = *(const uint32_t*)(dp[s] + (sb + 1) * 4);
+      }
+    }
+    // unpack the nibbles once, reuse for every activation row
+    u32x4 lo[GV_RS], hi[GV_RS];
+#pragma unroll
+    for (int s = 0; s < GV_RS; ++s) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        lo[s][i] = qa[s][i] & 0x0F0F0F0Fu;
+        hi[s][i] = (qa[s][i] >> 4) & 0x0F0F0F0Fu;
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      if (m < M) {
+        const int8_t* xm = xq + m * kper + sb * 256;
+        const u32x4 xl = *(const u32x4*)(xm + xlo);
+        const u32x4 xh = *(const u32x4*)(xm + xlo + 32);
+        const int* bm = bs + m * (kper >> 4) + sb * 16;
+        const float* dm = dx + m * (kper >> 5) + sb * 8;
+        const float dxl = dm[2 * j], dxh = dm[2 * j + 1];
+        const float bl = (float)bm[blo] * dxl, bh = (float)bm[blo + 2] * dxh;
+#pragma unroll
+        for (int s = 0; s < GV_RS; ++s) {
+          int dl = dot4(lo[s][0], xl[0], 0), dh = dot4(hi[s][0], xh[0], 0);
+          dl = dot4(lo[s][1], xl[1], dl); dh = dot4(hi[s][1], xh[1], dh);
+          dl = dot4(lo[s][2], xl[2], dl); dh = dot4(hi[s][2], xh[2], dh);
+          dl = dot4(lo[s][3], xl[3], dl); dh = dot4(hi[s][3], xh[3], dh);
+          const uint32_t sc = sa[s];
+          const float fs = fmaf((float)(dl * (int)(sc & 0xFFu)), dxl, (float)(dh * (int)((sc >> 16) & 0xFFu)) * dxh);
+          const float fm = fmaf((float)((sc >> 8) & 0xFFu), bl, (float)(sc >> 24) * bh);
+          const float d = h2f((uint16_t)(da[s] & 0xFFFFu)), dmin = h2f((uint16_t)(da[s] >> 16));
+          acc[m][s] = fmaf(d, fs, fmaf(-dmin, fm, acc[m][s]));
+        }
+      }
+    }
+    if (sb + 1 < nsb) {
+#pragma unroll
+      for (int s = 0; s < GV_RS; ++s) {
+        qa[s] = qn[s];
+        sa[s] = sn[s];
+        da[s] = dn[s];
+      }
+    }
+  }
+  gv_store<MT>(acc, n, w.N, M, t, o, ldo, col0);
+}
+
+template <int MT, int NT, int EARLY>
+LA_DEV void gv_q6k(const QW& w, int row0, const bf16* X, int ldx, int M, int kper, float* o, int ldo, int col0,
+                   int8_t* xq, int* bs, float* dx) {
+  const int k0 = blockIdx.y * kper, nsb = kper >> 8, sb0 = k0 >> 8;
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = lane >> 3, t = lane & 7;
+  const int hh = t >> 2, u = t & 3, s2 = u >> 1;
+  const int xlo = 128 * hh + 32 * s2 + 16 * (u & 1);  // low-nibble run; high run at +64
+  const int blo = xlo >> 4;                             // 16-run index; high run at +4
+  const int shl = 4 - 2 * s2, shr = 2 * s2;
+  const int scb = 8 * (2 * s2 + (u & 1));               // bit offset of this lane's scale byte
+  const size_t lrow = (size_t)(w.K >> 1), hrow = (size_t)(w.K >> 2), crow = (size_t)(w.K >> 4),
+               drow = (size_t)(w.K >> 8) * 2;
+  int n[GV_RS];
+  const uint8_t* lp[GV_RS];
+  const uint8_t* hp[GV_RS];
+  const uint8_t* cp[GV_RS];
+  const uint8_t* dp[GV_RS];
+#pragma unroll
+  for (int s = 0; s < GV_RS; ++s) {
+    n[s] = row0 + wv * (8 * GV_RS) + s * 8 + r;
+    const size_t nc = n[s] < w.N ? n[s] : w.N - 1;
+    lp[s] = w.p0 + nc * lrow + (size_t)sb0 * 128 + 64 * hh + 16 * u;
+    hp[s] = w.p1 + nc * hrow + (size_t)sb0 * 64 + 32 * hh + 16 * (u & 1);
+    cp[s] = w.p2 + nc * crow + (size_t)sb0 * 16 + 8 * hh;
+    dp[s] = w.p3 + nc * drow + (size_t)sb0 * 2;
+  }
+  if constexpr (!EARLY) {
+    quantize_x<MT>(X, ldx, M, k0, kper, xq, bs, dx);
+    __syncthreads();
+  }
+  u32x4 la_[GV_RS], ha[GV_RS];
+  u32x2 ca[GV_RS];
+  uint32_t da[GV_RS];
+#pragma unroll
+  for (int s = 0; s < GV_RS; ++s) {
+    la_[s] = ldg16<NT>(lp[s]);
+    ha[s] = ldg16<NT>(hp[s]);
+    ca[s] = *(const u32x2*)cp[s];
+    da[s] = *(const uint16_t*)dp[s];
+  }
+  if constexpr (EARLY) {
+    quantize_x<MT>(X, ldx, M, k0, kper, xq, bs, dx);
+    __syncthreads();
+  }
+
+  float acc[MT][GV_RS];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int s = 0; s < GV_RS; ++s) acc[m][s] = 0.f;
+
+  for (int sb = 0; sb < nsb; ++sb) {
+    u32x4 ln[GV_RS], hn[GV_RS];
+    u32x2 cn[GV_RS];
+    uint32_t dn[GV_RS];
+    if (sb + 1 < nsb) {
+#pragma unroll
+      for (int s = 0; s < GV_RS; ++s) {
+        ln[s] = ldg16<NT>(lp[s] + (sb + 1) * 128);
+        hn[s] = ldg16<NT>(hp[s] + (sb + 1) * 64);
+        cn[s] = *(const u32x2*)(cp[s] + (sb + 1) * 16);
+        dn[s] = *(const uint16_t*)(dp[s] + (sb + 1) * 2);
+      }
+    }
+    u32x4 lo[GV_RS], hi[GV_RS];
+#pragma unroll
+    for (int s = 0; s < GV_RS; ++s) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        lo[s][i] = (la_[s][i] & 0x0F0F0F0Fu) | ((ha[s][i] << shl) & 0x30303030u);
+        hi[s][i] = ((la_[s][i] >> 4) & 0x0F0F0F0Fu) | ((ha[s][i] >> shr) & 0x30303030u);
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      if (m < M) {
+        const int8_t* xm = xq + m * kper + sb * 256;
+        const u32x4 xl = *(const u32x4*)(xm + xlo);
+        const u32x4 xh = *(const u32x4*)(xm + xlo + 64);
+        const int* bm = bs + m * (kper >> 4) + sb * 16;
+        const int bl = -32 * bm[blo], bh = -32 * bm[blo + 4];
+        const float* dm = dx + m * (kper >> 5) + sb * 8;
+        const float dxl = dm[xlo >> 5], dxh = dm[(xlo >> 5) + 2];
+#pragma unroll
+        for (int s = 0; s < GV_RS; ++s) {
+          int dl = dot4(lo[s][0], xl[0], bl), dh = dot4(hi[s][0], xh[0], bh);
+          dl = dot4(lo[s][1], xl[1], dl); dh = dot4(hi[s][1], xh[1], dh);
+          dl = dot4(lo[s][2], xl[2], dl); dh = dot4(hi[s][2], xh[2], dh);
+          dl = dot4(lo[s][3], xl[3], dl); dh = dot4(hi[s][3], xh[3], dh);
+          const int sl = __builtin_amdgcn_sbfe((int)ca[s].x, scb, 8);
+          const int sh = __builtin_amdgcn_sbfe((int)ca[s].y, scb, 8);
+          const float d = h2f((uint16_t)da[s]);
+          acc[m][s] = fmaf(d, fmaf((float)(dl * sl), dxl, (float)(dh * sh) * dxh), acc[m][s]);
+        }
+      }
+    }
+    if (sb + 1 < nsb) {
+#pragma unroll
+      for (int s = 0; s < GV_RS; ++s) {
+        la_[s] = ln[s];
+        ha[s] = hn[s];
+        ca[s] = cn[s];
+        da[s] = dn[s];
+      }
+    }
+  }
+  gv_store<MT>(acc, n, w.N, M, t, o, ldo, col0);
+}
+
+// Segments [0, nA) are format FA, [nA, nseg) format FB (a q|k + v fusion is (Q4_K, Q6_K)).
+// VAR bit 0: non-temporal weight loads; bit 1: weights requested before the x prologue.
+template <int MT, int FA, int FB, int VAR>
+__global__ __launch_bounds__(GV_THREADS) void qgemv_dp4_kernel(GVArgs a, const bf16* __restrict__ X, int ldx,
+                                                               int M, int kper, float* __restrict__ out,
+                                                               int ldo, long slab) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t gv_lds[];
+  int8_t* xq = (int8_t*)gv_lds;                                      // [MT][kper]
+  int* bs = (int*)(gv_lds + MT * kper);                              // [MT][kper/16]
+  float* dx = (float*)(gv_lds + MT * kper + MT * (kper >> 4) * 4);   // [MT][kper/32]
+  int seg = 0, blk = blockIdx.x;
+#pragma unroll
+  for (int i = 0; i < GV_SEGS - 1; ++i)
+    if (seg < a.nseg - 1 && blk >= a.blk_end[seg]) ++seg;
+  const int row0 = (blk - (seg ? a.blk_end[seg - 1] : 0)) * GV_ROWS;
+  float* o = out + (size_t)blockIdx.y * slab;
+  constexpr int NT = VAR & 1, EARLY = (VAR >> 1) & 1;
+  const bool fa = FA == FB || a.fmt[seg] == FA;
+  if (fa) {
+    if constexpr (FA == FMT_Q4_K) gv_q4k<MT, NT, EARLY>(a.w[seg], row0, X, ldx, M, kper, o, ldo, a.col0[seg], xq, bs, dx);
+    else gv_q6k<MT, NT, EARLY>(a.w[seg], row0, X, ldx, M, kper, o, ldo, a.col0[seg], xq, bs, dx);
+  } else if constexpr (FA != FB) {
+    if constexpr (FB == FMT_Q4_K) gv_q4k<MT, NT, EARLY>(a.w[seg], row0, X, ldx, M, kper, o, ldo, a.col0[seg], xq, bs, dx);
+    else gv_q6k<MT, NT, EARLY>(a.w[seg], row0, X, ldx, M, kper, o, ldo, a.col0[seg], xq, bs, dx);
+  }
+}
+
+static inline size_t gv_lds_bytes(int MT, int kper) {
+  return (size_t)MT * kper + (size_t)MT * (kper >> 4) * 4 + (size_t)MT * (kper >> 5) * 4;
+}
+
+static int g_gv_variant = 1;  // non-temporal weight loads, x prologue first (fastest on every decode shape)
+
+template <int MT, int FA, int FB>
+static int launch_gv(const GVArgs& a, int nblk, int K, const bf16* X, int ldx, int M, int splits, float* out,
+                     int ldo, long slab, hipStream_t st) {
+  const int kper = K / splits;
+  const size_t lds = gv_lds_bytes(MT, kper);
+  if (lds > 64 * 1024) return -3;
+  dim3 grid(nblk, splits);
+  switch (g_gv_variant) {
+#define GV_CASE(V) \
+    case V: hipLaunchKernelGGL((qgemv_dp4_kernel<MT, FA, FB, V>), grid, dim3(GV_THREADS), lds, st, a, X, ldx, M, kper, out, ldo, slab); break;
+    GV_CASE(0) GV_CASE(1) GV_CASE(2) GV_CASE(3)
+#undef GV_CASE
+    default: return -4;
+  }
+  return 0;
+}
+
+template <int FA, int FB>
+static int launch_gv_m(const GVArgs& a, int nblk, int K, const bf16* X, int ldx, int M, int splits, float* out,
+                       int ldo, long slab, hipStream_t st) {
+  if (M == 1) return launch_gv<1, FA, FB>(a, nblk, K, X, ldx, M, splits, out, ldo, slab, st);
+  if (M == 2) return launch_gv<2, FA, FB>(a, nblk, K, X, ldx, M, splits, out, ldo, slab, st);
+  return launch_gv<4, FA, FB>(a, nblk, K, X, ldx, M, splits, out, ldo, slab, st);
+}
+
+}  // namespace la
+
+// C ABI ---------------------------------------------------------------------------
+// nseg weights side by side: fmts[i], planes[4*i .. 4*i+3], Ns[i]; all share K.
+// Q4_K planes: p0 = qs, p2 = scm, p3 = dd (p1, the packed header, is unused here).
+// Q6_K planes: p0 = ql, p1 = qh, p2 = sc, p3 = d.
+extern "C" int la_qgemv_dp4(int nseg, const int* fmts, const void* const* planes, const int* Ns, int K,
+                            const void* X, int ldx, int M, int splits, void* out, int ldo, long slab,
+                            void* stream) {
+  using namespace la;
+  if (nseg < 1 || nseg > GV_SEGS || M < 1 || M > 4 || (K & 255) || splits < 1 || ((K >> 8) % splits) ||
+      ldx < K || slab < (long)M * ldo)
+    return -1;
+  GVArgs a{};
+  int nblk = 0, col = 0;
+  for (int i = 0; i < nseg; ++i) {
+    const int f = fmts[i], N = Ns[i];
+    const void* const* p = planes + 4 * i;
+    if (N < 1 || !p[0] || !p[2] || !p[3] || (f != FMT_Q4_K && f != FMT_Q6_K) || (f == FMT_Q6_K && !p[1])) return -2;
+    a.w[i] = QW{(const uint8_t*)p[0], (const uint8_t*)p[1], (const uint8_t*)p[2], (const uint8_t*)p[3], N, K};
+    a.fmt[i] = f;
+    a.col0[i] = col;
+    nblk += (N + GV_ROWS - 1) / GV_ROWS;
+    a.blk_end[i] = nblk;
+    col += N;
+  }
+  a.nseg = nseg;
+  if (ldo < col) return -1;
+  // formats must form at most two runs: [FA ...][FB ...]
+  int fa = a.fmt[0], fb = a.fmt[nseg - 1];
+  for (int i = 0; i < nseg; ++i)
+    if (a.fmt[i] != fa && a.fmt[i] != fb) return -2;
+  for (int i = 1; i < nseg; ++i)
+    if (a.fmt[i - 1] == fb && a.fmt[i] == fa && fa != fb) return -2;
+  hipStream_t st = (hipStream_t)stream;
+  const bf16* x = (const bf16*)X;
+  float* o = (float*)out;
+  int rc;
+  if (fa == FMT_Q4_K && fb == FMT_Q4_K) rc = launch_gv_m<FMT_Q4_K, FMT_Q4_K>(a, nblk, K, x, ldx, M, splits, o, ldo, slab, st);
+  else if (fa == FMT_Q6_K && fb == FMT_Q6_K) rc = launch_gv_m<FMT_Q6_K, FMT_Q6_K>(a, nblk, K, x, ldx, M, splits, o, ldo, slab, st);
+  else if (fa == FMT_Q4_K) rc = launch_gv_m<FMT_Q4_K, FMT_Q6_K>(a, nblk, K, x, ldx, M, splits, o, ldo, slab, st);
+  else rc = launch_gv_m<FMT_Q6_K, FMT_Q4_K>(a, nblk, K, x, ldx, M, splits, o, ldo, slab, st);
+  if (rc) return rc;
+  return (int)hipGetLastError();
+}
+
+// Tuning hook: select the kernel variant (bit 0 non-temporal loads, bit 1 early weight prefetch).
+extern "C" int la_gemv_variant(int v) {
+  if (v < 0 || v > 3) return -1;
+  la::g_gv_variant = v;
+  return 0;
+}

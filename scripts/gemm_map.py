@@ -54,7 +54,7 @@ for name, fmt, N, K in SHAPES:
     # enough distinct copies that the rotation overflows the 256 MiB Infinity Cache: weights
     # arrive cold from HBM like in the engine (one pass over the model per decode step)
     w0 = mk(fmt, N, K)
-    wbytes = w0.nbytes
+    wbytes = N * K // 256 * (144 if fmt == "q4k" else 210)   # GGUF bytes (extra load-time planes not counted)
     ncopy = max(2, -(-640 * 2**20 // wbytes))
     ws = [w0] + [mk(fmt, N, K) for _ in range(ncopy - 1)] if ncopy <= 64 else [w0]
     wbf = [w.materialize_bf16() for w in ws[:max(2, -(-640 * 2**20 // (N * K * 2)))]]
@@ -64,6 +64,8 @@ for name, fmt, N, K in SHAPES:
         paths = []
         if M <= ops.SKINNY_MAX_M:
             paths.append("skinny")
+        if M <= ops.GEMV_MAX_M:
+            paths.append("dp4")
         if M > 16:
             paths += ["blas"] + [f"mid:{t}:{S}" for t in ((42, 41, 22, 21) if M > 128 else (22, 21))
                                  for S in (1, 2, 4, 8) if ops._mid_split_ok(K, S)]

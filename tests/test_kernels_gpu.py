@@ -50,6 +50,55 @@ def test_skinny_gemm_splits_and_tail():
         assert (out.sum(0).cpu() - ref).abs().max().item() < 2e-2
 
 
+@pytest.mark.parametrize("t", [GGMLType.Q4_K, GGMLType.Q6_K])
+@pytest.mark.parametrize("M", [1, 2, 3, 4])
+def test_gemv_dp4(t, M):
+    """int8-dot decode GEMV (activations quantised per 256-block, ggml q8_K style) vs fp32:
+    N off the 64-row workgroup tile, every split of K, repeated launches bit-identical."""
+    N, K = 200, 3584
+    w = _qw(N, K, t, seed=11)
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    ref = x.float().cpu() @ w.ref.t()
+    tol = 2e-2 * max(1.0, ref.abs().max().item())
+    for S in (1, 2, 7, 14):
+        out = torch.full((S, M, N), float("nan"), dtype=torch.float32, device=DEV)
+        ops.gemv_dp4(x, [w], S, out)
+        err = (out.sum(0).cpu() - ref).abs().max().item()
+        assert err < tol, (S, err)
+        out2 = torch.empty_like(out)
+        ops.gemv_dp4(x, [w], S, out2)
+        assert torch.equal(out, out2)
+    y = ops.linear(x, w, force="dp4").dense().cpu()
+    assert (y - ref).abs().max().item() < tol
+
+
+@pytest.mark.parametrize("M", [1, 3])
+def test_gemv_dp4_segments(M):
+    """One launch over mixed-format weights side by side (Q4_K q|k + Q6_K v shape), plus a
+    4-weight call that spills into a second launch."""
+    K = 1024
+    ws = [_qw(136, K, GGMLType.Q4_K, seed=13), _qw(64, K, GGMLType.Q6_K, seed=14), _qw(72, K, GGMLType.Q4_K, seed=15),
+          _qw(40, K, GGMLType.Q6_K, seed=16)]
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    ref = torch.cat([x.float().cpu() @ w.ref.t() for w in ws], -1)
+    for n in (2, 3, 4):
+        y = ops.linear_multi(x, ws[:n], force="dp4").dense().cpu()
+        assert (y - ref[:, :y.shape[1]]).abs().max().item() < 5e-2, n
+
+
+def test_gemv_dp4_outlier_rows():
+    """Activation rows with large outliers (post-SwiGLU-like) stay within q8 accuracy."""
+    N, K = 128, 4096
+    w = _qw(N, K, GGMLType.Q4_K, seed=12)
+    x = torch.randn(1, K)
+    x[0, ::97] *= 40.0
+    x = x.to(DEV).to(torch.bfloat16)
+    ref = x.float().cpu() @ w.ref.t()
+    y = ops.linear(x, w, force="dp4").dense().cpu()
+    rel = ((y - ref).norm() / ref.norm()).item()
+    assert rel < 2e-2, rel
+
+
 @pytest.mark.parametrize("t", [GGMLType.Q4_K, GGMLType.Q6_K, GGMLType.Q8_0])
 @pytest.mark.parametrize("M", [65, 128, 200, 256, 300])
 def test_mid_gemm(t, M):
