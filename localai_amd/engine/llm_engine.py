@@ -62,6 +62,7 @@ class EngineConfig:
     decode_steps: int = 8             # device-resident decode steps per host round trip (graphs only)
     mmproj: str = ""                  # LLaVA vision tower + projector GGUF (images in prompts)
     bias_capacity: int = 16           # logit-bias / EOS-ban entries per sequence inside the graph
+    blas_tune: bool = True            # tune the hipBLASLt/rocBLAS solution per decode GEMM shape at warm-up
 
 
 @dataclass
@@ -854,9 +855,14 @@ class LLMEngine:
         """Capture decode graphs ahead of serving (the reference's LoadToMemory eager path)."""
         if not (self.cfg.use_graphs and self.device.type == "cuda"):
             return
-        for b in (batch_sizes or self.sched.buckets()):
-            if b not in self._graphs:
-                self._graphs[b] = self._capture(b)
+        tuning = self.cfg.blas_tune and ops.blas_tuning_start()
+        try:
+            for b in (batch_sizes or self.sched.buckets()):
+                if b not in self._graphs:
+                    self._graphs[b] = self._capture(b)
+        finally:
+            if tuning:
+                ops.blas_tuning_stop()
         torch.cuda.synchronize(self.device)
 
     # ------------------------------------------------------------------ sampling + output

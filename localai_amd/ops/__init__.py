@@ -407,6 +407,49 @@ def _run_ws(x, ws, S, out, Ntot):
         col += w.N
 
 
+def blas_tuning_start(path: Optional[str] = None) -> bool:
+    """Per-shape solution search for the library (hipBLASLt / rocBLAS) GEMMs, run while the engine
+    warms up its decode graphs: PyTorch-ROCm TunableOp times every candidate kernel of each new
+    (M, N, K) against a rotating 512 MiB buffer set (cold weights, as in decode) and keeps the
+    fastest.  Results persist in a CSV so a restart reuses them.  Tuning is switched off again
+    before serving (blas_tuning_stop): prefill chunk sizes vary and must never tune inline."""
+    if os.environ.get("LOCALAI_AMD_BLAS_TUNE", "1") == "0" or not torch.cuda.is_available():
+        return False
+    try:
+        import torch.cuda.tunable as tn
+    except ImportError:
+        return False
+    if path is None:
+        root = os.environ.get("LOCALAI_AMD_CACHE") or os.path.join(os.path.expanduser("~"), ".cache", "localai_amd")
+        os.makedirs(root, exist_ok=True)
+        name = torch.cuda.get_device_properties(torch.cuda.current_device()).gcnArchName.split(":")[0]
+        path = os.path.join(root, f"tunableop_{name}.csv")
+    tn.enable(True)
+    tn.set_filename(path)
+    if os.path.exists(path):
+        try:
+            tn.read_file(path)
+        except Exception:  # noqa: BLE001 - a stale/corrupt cache only costs a re-tune
+            pass
+    tn.set_max_tuning_duration(int(os.environ.get("LOCALAI_AMD_BLAS_TUNE_MS", "15")))
+    tn.set_max_tuning_iterations(20)
+    try:
+        tn.set_rotating_buffer_size(512)
+    except Exception:  # noqa: BLE001
+        pass
+    tn.tuning_enable(True)
+    return True
+
+
+def blas_tuning_stop() -> None:
+    import torch.cuda.tunable as tn
+    tn.tuning_enable(False)   # keep using the tuned solutions, never tune inline while serving
+    try:
+        tn.write_file()
+    except Exception:  # noqa: BLE001
+        pass
+
+
 def _run_blas(x, ws, Ntot):
     if len(ws) == 1:
         return torch.matmul(x, ws[0].materialize_bf16().t())

@@ -40,6 +40,34 @@ def main():
     for r in rows[:25]:
         print(f"| `{short(r['Name'])}` | {r['Calls']} | {float(r['TotalDurationNs']) / 1e6:.2f} | "
               f"{float(r['AverageNs']) / 1e3:.1f} | {float(r['Percentage']):.1f} |")
+    if trace and "--steady" in sys.argv:
+        steady(tr, int(sys.argv[sys.argv.index("--steady") + 1]))
+
+
+def steady(tr, n_layers):
+    """Decode-only steady state: every dispatch after the last prefill-attention kernel, per
+    decode step (= attn_decode dispatches / n_layers)."""
+    pre = [int(r["End_Timestamp"]) for r in tr if "attn_prefill" in r["Kernel_Name"]]
+    t_cut = max(pre) if pre else 0
+    sel = [r for r in tr if int(r["Start_Timestamp"]) > t_cut]
+    if not sel:
+        return
+    steps = sum(1 for r in sel if "attn_decode" in r["Kernel_Name"]) / n_layers
+    agg = {}
+    for r in sel:
+        k = short(r["Kernel_Name"])
+        d = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+        c, t = agg.get(k, (0, 0))
+        agg[k] = (c + 1, t + d)
+    busy = sum(t for _, t in agg.values())
+    span = max(int(r["End_Timestamp"]) for r in sel) - min(int(r["Start_Timestamp"]) for r in sel)
+    print(f"\n## Decode steady state (after the last prefill kernel)\n")
+    print(f"- {steps:.0f} decode steps, {busy / 1e3 / max(steps, 1):.1f} us kernel time per step, "
+          f"{span / 1e3 / max(steps, 1):.1f} us wall per step ({100 * busy / max(span, 1):.0f}% GPU-busy)")
+    print("\n| kernel | calls/step | us/step | avg us | % |\n|---|---:|---:|---:|---:|")
+    for k, (c, t) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:20]:
+        print(f"| `{k}` | {c / max(steps, 1):.1f} | {t / 1e3 / max(steps, 1):.1f} | {t / c / 1e3:.1f} | "
+              f"{100 * t / busy:.1f} |")
 
 
 if __name__ == "__main__":
