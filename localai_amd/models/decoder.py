@@ -272,8 +272,7 @@ class DecoderModel:
         if L.experts is not None:
             return self._moe(L, xn)
         gu = ops.linear_multi(xn, L.gate_up, bias=L.up_bias)
-        h = ops.act(gu, self.F, ops.ACT_SWIGLU if hp.act == "swiglu" else ops.ACT_GELU)
-        d = ops.linear(h, L.down)
+        d = ops.act_linear(gu, self.F, ops.ACT_SWIGLU if hp.act == "swiglu" else ops.ACT_GELU, L.down)
         return self._row_parallel_out(d, L.down_bias)
 
     def _moe(self, L: Layer, xn: torch.Tensor) -> ops.Partial:

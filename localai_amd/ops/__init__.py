@@ -46,7 +46,7 @@ def lib():
             "la_qgemm_skinny": [I, P, P, P, P, I, I, P, I, I, I, P, I, LNG, P],
             "la_qgemm_mid": [I, P, P, P, P, I, I, P, I, I, I, P, I, LNG, I, P],
             "la_qgemm_ws": [I, P, P, P, P, I, I, P, I, I, I, P, I, LNG, P],
-            "la_qgemv_dp4": [I, P, P, P, I, P, I, I, I, P, I, LNG, P],
+            "la_qgemv_dp4": [I, P, P, P, I, P, I, I, I, P, I, LNG, P, LNG, I, P, I, P],
             "la_gemv_variant": [I],
             "la_add_norm": [P, P, LNG, I, P, I, P, P, P, I, I, F, I, P, P],
             "la_rope_kv": [P, LNG, I, P, P, P, P, I, I, I, I, I, I, P, P, P, I, P],
@@ -331,10 +331,14 @@ def _gemv_splits(ws, K: int, M: int) -> int:
     return S
 
 
-def gemv_dp4(x: torch.Tensor, ws: Sequence[QWeight], S: int, out: torch.Tensor) -> None:
+def gemv_dp4(x: Optional[torch.Tensor], ws: Sequence[QWeight], S: int, out: torch.Tensor,
+             act_src: Optional[Partial] = None, act_mode: int = 0) -> None:
     """out[S, M, sum(N)] = split-K partials of x @ [W0; W1; ...]^T from the int8-dot decode GEMV,
-    up to 3 weights (mixed Q4_K / Q6_K, same K) per launch."""
-    M, K = x.shape
+    up to 3 weights (mixed Q4_K / Q6_K, same K) per launch.  With act_src (fp32 gate|up slabs)
+    x = act(act_src) is formed inside the GEMV prologue instead of being read."""
+    M = out.shape[1]
+    K = ws[0].K
+    a = (None, 0, 0, None) if act_src is None else act_src.src_args()
     Ntot = out.shape[-1]
     # launch groups: <= 3 weights whose formats form at most two runs [FA ...][FB ...]
     groups: List[List[QWeight]] = []
@@ -350,8 +354,9 @@ def gemv_dp4(x: torch.Tensor, ws: Sequence[QWeight], S: int, out: torch.Tensor) 
         fmts = (ctypes.c_int * n)(*[w.fmt for w in seg])
         planes = (ctypes.c_void_p * (4 * n))(*[p for w in seg for p in w.ptrs()])
         Ns = (ctypes.c_int * n)(*[w.N for w in seg])
-        _check(lib().la_qgemv_dp4(n, fmts, planes, Ns, K, x.data_ptr(), K, M, S, out.data_ptr() + col * 4, Ntot,
-                                  M * Ntot, _stream()), "la_qgemv_dp4")
+        _check(lib().la_qgemv_dp4(n, fmts, planes, Ns, K, None if x is None else x.data_ptr(), K, M, S,
+                                  out.data_ptr() + col * 4, Ntot, M * Ntot, a[0], a[1], a[2], a[3], act_mode,
+                                  _stream()), "la_qgemv_dp4")
         col += sum(w.N for w in seg)
 
 
@@ -724,6 +729,21 @@ def act(src: Partial, F: int, mode: int, out: Optional[torch.Tensor] = None) -> 
     a = src.src_args()
     _check(lib().la_act(a[0], a[1], a[2], a[3], out.data_ptr(), T, F, mode, _stream()), "la_act")
     return out
+
+
+def act_linear(src: Partial, F: int, mode: int, w: QWeight) -> Partial:
+    """down(act(gate|up)).  On the decode GEMV path (M <= GEMV_MAX_M, fp32 slab source) the
+    activation is computed inside the down GEMV's activation prologue -- no activation launch
+    and no bf16 round trip; otherwise act() then linear()."""
+    M = src.M
+    width = 2 * F if mode == ACT_SWIGLU else F
+    if (src.t.is_cuda and src.S >= 1 and src.S <= 16 and GEMV_DP4 and M <= GEMV_MAX_M and w.gemv_ok
+            and w.K == F and src.N == width):
+        S = _gemv_splits([w], w.K, M)
+        out = torch.empty(S, M, w.N, dtype=torch.float32, device=src.t.device)
+        gemv_dp4(None, [w], S, out, act_src=src, act_mode=mode)
+        return Partial(out)
+    return linear(act(src, F, mode), w)
 
 
 def reduce(src: Partial, dtype=torch.float32) -> torch.Tensor:

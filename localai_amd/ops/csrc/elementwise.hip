@@ -309,7 +309,10 @@ extern "C" int la_add_norm(void* residual, const void* add_p, long add_slab, int
                        (float*)residual, s, has_add, (const float*)w, (const float*)b, (bf16*)out, D, eps,  \
                        mode, (float*)out_f32);                                                            \
     break;
-  if (T <= 32 && D <= 1024 * 4 * 2) {
+  // one 1024-thread workgroup per row whenever the row fits two float4 per thread: a 256-row
+  // decode batch then puts 16 waves on every CU instead of 4 (the 256-thread variants below are
+  // left for very wide rows)
+  if (D <= 1024 * 4 * 2) {
     const int it4 = (D / 4 + 1023) / 1024;
     if (it4 == 1)
       hipLaunchKernelGGL((la::add_norm_kernel<1, 1024>), dim3(T), dim3(1024), 0, (hipStream_t)stream,

@@ -56,11 +56,56 @@ LA_DEV u32x4 ldg16(const uint8_t* p) {
   else return *(const u32x4*)p;
 }
 
+// Optional fused-activation source: instead of a bf16 x, the GEMV reads the fp32 split-K
+// slabs of the preceding gate|up GEMM and applies the activation while quantising, so the
+// decode MLP runs gate_up GEMV -> down GEMV with no activation launch in between
+// ("fused into the GEMM" -- here into the consumer's prologue).
+//   mode 0: x = silu(g) * u with g = row[k], u = row[F + k] (SwiGLU, row width 2F)
+//   mode 1: x = gelu_tanh(row[k]);  mode 2: x = quick_gelu(row[k])      (row width F)
+struct GVAct {
+  const float* p;      // [S][M][W] fp32 slabs, W = 2F (mode 0) or F; null = plain bf16 x
+  long slab;           // elements between slabs
+  int S;
+  const float* bias;   // optional per-column bias of the gate|up output (length W)
+  int mode, F;
+};
+
+LA_DEV float4 gv_sum_slabs(const GVAct& a, long idx, int col) {
+  float4 v = *(const float4*)(a.p + idx);
+  for (int s = 1; s < a.S; ++s) {
+    const float4 w = *(const float4*)(a.p + (long)s * a.slab + idx);
+    v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
+  }
+  if (a.bias) {
+    const float4 b = *(const float4*)(a.bias + col);
+    v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
+  }
+  return v;
+}
+
+LA_DEV float gv_act1(float x, int mode) {
+  if (mode == 1) return 0.5f * x * (1.f + tanhf(0.7978845608f * (x + 0.044715f * x * x * x)));
+  return x / (1.f + __expf(-1.702f * x));
+}
+
+// x[m, k .. k+3] from the activation source (in fp32, never rounded to bf16)
+LA_DEV void gv_act_x(const GVAct& a, int m, int k, float v[4]) {
+  const long W = a.mode == 0 ? 2L * a.F : (long)a.F;
+  const float4 g = gv_sum_slabs(a, m * W + k, k);
+  if (a.mode == 0) {
+    const float4 u = gv_sum_slabs(a, m * W + a.F + k, a.F + k);
+    v[0] = silu(g.x) * u.x; v[1] = silu(g.y) * u.y; v[2] = silu(g.z) * u.z; v[3] = silu(g.w) * u.w;
+  } else {
+    v[0] = gv_act1(g.x, a.mode); v[1] = gv_act1(g.y, a.mode); v[2] = gv_act1(g.z, a.mode); v[3] = gv_act1(g.w, a.mode);
+  }
+}
+
 // Quantise x[m, k0 : k0+kper] into the LDS image (ggml q8_1 granularity: one scale per 32).
 // Wave w handles super-blocks w, w+4, ...; lane l owns elements 4l..4l+3 of the super-block,
 // so 8 lanes share a 32-block and 4 lanes a 16-run.
 template <int MT>
-LA_DEV void quantize_x(const bf16* X, int ldx, int M, int k0, int kper, int8_t* xq, int* bs, float* dx) {
+LA_DEV void quantize_x(const bf16* X, int ldx, const GVAct& act, int M, int k0, int kper, int8_t* xq, int* bs,
+                       float* dx) {
   const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int nsb = kper >> 8;
   for (int m = 0; m < MT; ++m) {
@@ -70,9 +115,16 @@ LA_DEV void quantize_x(const bf16* X, int ldx, int M, int k0, int kper, int8_t* 
     int* b = bs + m * (kper >> 4);
     float* d = dx + m * (kper >> 5);
     for (int sb = wv; sb < nsb; sb += 4) {
-      const u32x2 raw = *(const u32x2*)(xr + sb * 256 + 4 * l);
-      const float v0 = bf16_bits_to_f(raw.x & 0xFFFFu), v1 = bf16_bits_to_f(raw.x >> 16);
-      const float v2 = bf16_bits_to_f(raw.y & 0xFFFFu), v3 = bf16_bits_to_f(raw.y >> 16);
+      float v0, v1, v2, v3;
+      if (act.p) {
+        float v[4];
+        gv_act_x(act, m, k0 + sb * 256 + 4 * l, v);
+        v0 = v[0]; v1 = v[1]; v2 = v[2]; v3 = v[3];
+      } else {
+        const u32x2 raw = *(const u32x2*)(xr + sb * 256 + 4 * l);
+        v0 = bf16_bits_to_f(raw.x & 0xFFFFu); v1 = bf16_bits_to_f(raw.x >> 16);
+        v2 = bf16_bits_to_f(raw.y & 0xFFFFu); v3 = bf16_bits_to_f(raw.y >> 16);
+      }
       const float amax = group_max<8>(fmaxf(fmaxf(fabsf(v0), fabsf(v1)), fmaxf(fabsf(v2), fabsf(v3))));
       const float inv = amax > 0.f ? 127.f / amax : 0.f;
       const int q0 = __float2int_rn(v0 * inv), q1 = __float2int_rn(v1 * inv);
@@ -105,7 +157,8 @@ LA_DEV void gv_store(const float (&acc)[MT][GV_RS], const int (&n)[GV_RS], int N
 }
 
 template <int MT, int NT, int EARLY>
-LA_DEV void gv_q4k(const QW& w, int row0, const bf16* X, int ldx, int M, int kper, float* o, int ldo, int col0,
+LA_DEV void gv_q4k(const QW& w, int row0, const bf16* X, int ldx, const GVAct& act, int M, int kper, float* o,
+                   int ldo, int col0,
                    int8_t* xq, int* bs, float* dx) {
   const int k0 = blockIdx.y * kper, nsb = kper >> 8, sb0 = k0 >> 8;
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -127,7 +180,7 @@ LA_DEV void gv_q4k(const QW& w, int row0, const bf16* X, int ldx, int M, int kpe
     dp[s] = w.p3 + nc * drow + (size_t)sb0 * 4;
   }
   if constexpr (!EARLY) {
-    quantize_x<MT>(X, ldx, M, k0, kper, xq, bs, dx);
+    quantize_x<MT>(X, ldx, act, M, k0, kper, xq, bs, dx);
     __syncthreads();
   }
   u32x4 qa[GV_RS];
@@ -139,7 +192,7 @@ LA_DEV void gv_q4k(const QW& w, int row0, const bf16* X, int ldx, int M, int kpe
     da[s] = *(const uint32_t*)dp[s];
   }
   if constexpr (EARLY) {
-    quantize_x<MT>(X, ldx, M, k0, kper, xq, bs, dx);
+    quantize_x<MT>(X, ldx, act, M, k0, kper, xq, bs, dx);
     __syncthreads();
   }
 
@@ -207,7 +260,8 @@ LA_DEV void gv_q4k(const QW& w, int row0, const bf16* X, int ldx, int M, int kpe
 }
 
 template <int MT, int NT, int EARLY>
-LA_DEV void gv_q6k(const QW& w, int row0, const bf16* X, int ldx, int M, int kper, float* o, int ldo, int col0,
+LA_DEV void gv_q6k(const QW& w, int row0, const bf16* X, int ldx, const GVAct& act, int M, int kper, float* o,
+                   int ldo, int col0,
                    int8_t* xq, int* bs, float* dx) {
   const int k0 = blockIdx.y * kper, nsb = kper >> 8, sb0 = k0 >> 8;
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -234,7 +288,7 @@ LA_DEV void gv_q6k(const QW& w, int row0, const bf16* X, int ldx, int M, int kpe
     dp[s] = w.p3 + nc * drow + (size_t)sb0 * 2;
   }
   if constexpr (!EARLY) {
-    quantize_x<MT>(X, ldx, M, k0, kper, xq, bs, dx);
+    quantize_x<MT>(X, ldx, act, M, k0, kper, xq, bs, dx);
     __syncthreads();
   }
   u32x4 la_[GV_RS], ha[GV_RS];
@@ -248,7 +302,7 @@ LA_DEV void gv_q6k(const QW& w, int row0, const bf16* X, int ldx, int M, int kpe
     da[s] = *(const uint16_t*)dp[s];
   }
   if constexpr (EARLY) {
-    quantize_x<MT>(X, ldx, M, k0, kper, xq, bs, dx);
+    quantize_x<MT>(X, ldx, act, M, k0, kper, xq, bs, dx);
     __syncthreads();
   }
 
@@ -320,7 +374,7 @@ LA_DEV void gv_q6k(const QW& w, int row0, const bf16* X, int ldx, int M, int kpe
 // VAR bit 0: non-temporal weight loads; bit 1: weights requested before the x prologue.
 template <int MT, int FA, int FB, int VAR>
 __global__ __launch_bounds__(GV_THREADS) void qgemv_dp4_kernel(GVArgs a, const bf16* __restrict__ X, int ldx,
-                                                               int M, int kper, float* __restrict__ out,
+                                                               GVAct act, int M, int kper, float* __restrict__ out,
                                                                int ldo, long slab) {
   extern __shared__ __attribute__((aligned(16))) uint8_t gv_lds[];
   int8_t* xq = (int8_t*)gv_lds;                                      // [MT][kper]
@@ -335,11 +389,11 @@ __global__ __launch_bounds__(GV_THREADS) void qgemv_dp4_kernel(GVArgs a, const b
   constexpr int NT = VAR & 1, EARLY = (VAR >> 1) & 1;
   const bool fa = FA == FB || a.fmt[seg] == FA;
   if (fa) {
-    if constexpr (FA == FMT_Q4_K) gv_q4k<MT, NT, EARLY>(a.w[seg], row0, X, ldx, M, kper, o, ldo, a.col0[seg], xq, bs, dx);
-    else gv_q6k<MT, NT, EARLY>(a.w[seg], row0, X, ldx, M, kper, o, ldo, a.col0[seg], xq, bs, dx);
+    if constexpr (FA == FMT_Q4_K) gv_q4k<MT, NT, EARLY>(a.w[seg], row0, X, ldx, act, M, kper, o, ldo, a.col0[seg], xq, bs, dx);
+    else gv_q6k<MT, NT, EARLY>(a.w[seg], row0, X, ldx, act, M, kper, o, ldo, a.col0[seg], xq, bs, dx);
   } else if constexpr (FA != FB) {
-    if constexpr (FB == FMT_Q4_K) gv_q4k<MT, NT, EARLY>(a.w[seg], row0, X, ldx, M, kper, o, ldo, a.col0[seg], xq, bs, dx);
-    else gv_q6k<MT, NT, EARLY>(a.w[seg], row0, X, ldx, M, kper, o, ldo, a.col0[seg], xq, bs, dx);
+    if constexpr (FB == FMT_Q4_K) gv_q4k<MT, NT, EARLY>(a.w[seg], row0, X, ldx, act, M, kper, o, ldo, a.col0[seg], xq, bs, dx);
+    else gv_q6k<MT, NT, EARLY>(a.w[seg], row0, X, ldx, act, M, kper, o, ldo, a.col0[seg], xq, bs, dx);
   }
 }
 
@@ -350,15 +404,15 @@ static inline size_t gv_lds_bytes(int MT, int kper) {
 static int g_gv_variant = 1;  // non-temporal weight loads, x prologue first (fastest on every decode shape)
 
 template <int MT, int FA, int FB>
-static int launch_gv(const GVArgs& a, int nblk, int K, const bf16* X, int ldx, int M, int splits, float* out,
-                     int ldo, long slab, hipStream_t st) {
+static int launch_gv(const GVArgs& a, int nblk, int K, const bf16* X, int ldx, const GVAct& act, int M, int splits,
+                     float* out, int ldo, long slab, hipStream_t st) {
   const int kper = K / splits;
   const size_t lds = gv_lds_bytes(MT, kper);
   if (lds > 64 * 1024) return -3;
   dim3 grid(nblk, splits);
   switch (g_gv_variant) {
 #define GV_CASE(V) \
-    case V: hipLaunchKernelGGL((qgemv_dp4_kernel<MT, FA, FB, V>), grid, dim3(GV_THREADS), lds, st, a, X, ldx, M, kper, out, ldo, slab); break;
+    case V: hipLaunchKernelGGL((qgemv_dp4_kernel<MT, FA, FB, V>), grid, dim3(GV_THREADS), lds, st, a, X, ldx, act, M, kper, out, ldo, slab); break;
     GV_CASE(0) GV_CASE(1) GV_CASE(2) GV_CASE(3)
 #undef GV_CASE
     default: return -4;
@@ -367,11 +421,11 @@ static int launch_gv(const GVArgs& a, int nblk, int K, const bf16* X, int ldx, i
 }
 
 template <int FA, int FB>
-static int launch_gv_m(const GVArgs& a, int nblk, int K, const bf16* X, int ldx, int M, int splits, float* out,
-                       int ldo, long slab, hipStream_t st) {
-  if (M == 1) return launch_gv<1, FA, FB>(a, nblk, K, X, ldx, M, splits, out, ldo, slab, st);
-  if (M == 2) return launch_gv<2, FA, FB>(a, nblk, K, X, ldx, M, splits, out, ldo, slab, st);
-  return launch_gv<4, FA, FB>(a, nblk, K, X, ldx, M, splits, out, ldo, slab, st);
+static int launch_gv_m(const GVArgs& a, int nblk, int K, const bf16* X, int ldx, const GVAct& act, int M, int splits,
+                       float* out, int ldo, long slab, hipStream_t st) {
+  if (M == 1) return launch_gv<1, FA, FB>(a, nblk, K, X, ldx, act, M, splits, out, ldo, slab, st);
+  if (M == 2) return launch_gv<2, FA, FB>(a, nblk, K, X, ldx, act, M, splits, out, ldo, slab, st);
+  return launch_gv<4, FA, FB>(a, nblk, K, X, ldx, act, M, splits, out, ldo, slab, st);
 }
 
 }  // namespace la
@@ -380,13 +434,24 @@ static int launch_gv_m(const GVArgs& a, int nblk, int K, const bf16* X, int ldx,
 // nseg weights side by side: fmts[i], planes[4*i .. 4*i+3], Ns[i]; all share K.
 // Q4_K planes: p0 = qs, p2 = scm, p3 = dd (p1, the packed header, is unused here).
 // Q6_K planes: p0 = ql, p1 = qh, p2 = sc, p3 = d.
+// act_p != null: x is act(gate|up) computed from fp32 slabs act_p [act_S][M][W] (X unused),
+// W = 2K for act_mode 0 (SwiGLU) else K; act_bias optional [W].
 extern "C" int la_qgemv_dp4(int nseg, const int* fmts, const void* const* planes, const int* Ns, int K,
                             const void* X, int ldx, int M, int splits, void* out, int ldo, long slab,
+                            const void* act_p, long act_slab, int act_S, const void* act_bias, int act_mode,
                             void* stream) {
   using namespace la;
   if (nseg < 1 || nseg > GV_SEGS || M < 1 || M > 4 || (K & 255) || splits < 1 || ((K >> 8) % splits) ||
-      ldx < K || slab < (long)M * ldo)
+      slab < (long)M * ldo)
     return -1;
+  GVAct act{(const float*)act_p, act_slab, act_S, (const float*)act_bias, act_mode, K};
+  if (act_p) {
+    if (act_S < 1 || act_S > 16 || act_mode < 0 || act_mode > 2 ||
+        act_slab < (long)M * (act_mode == 0 ? 2L * K : (long)K))
+      return -1;
+  } else if (!X || ldx < K) {
+    return -1;
+  }
   GVArgs a{};
   int nblk = 0, col = 0;
   for (int i = 0; i < nseg; ++i) {
@@ -412,10 +477,10 @@ extern "C" int la_qgemv_dp4(int nseg, const int* fmts, const void* const* planes
   const bf16* x = (const bf16*)X;
   float* o = (float*)out;
   int rc;
-  if (fa == FMT_Q4_K && fb == FMT_Q4_K) rc = launch_gv_m<FMT_Q4_K, FMT_Q4_K>(a, nblk, K, x, ldx, M, splits, o, ldo, slab, st);
-  else if (fa == FMT_Q6_K && fb == FMT_Q6_K) rc = launch_gv_m<FMT_Q6_K, FMT_Q6_K>(a, nblk, K, x, ldx, M, splits, o, ldo, slab, st);
-  else if (fa == FMT_Q4_K) rc = launch_gv_m<FMT_Q4_K, FMT_Q6_K>(a, nblk, K, x, ldx, M, splits, o, ldo, slab, st);
-  else rc = launch_gv_m<FMT_Q6_K, FMT_Q4_K>(a, nblk, K, x, ldx, M, splits, o, ldo, slab, st);
+  if (fa == FMT_Q4_K && fb == FMT_Q4_K) rc = launch_gv_m<FMT_Q4_K, FMT_Q4_K>(a, nblk, K, x, ldx, act, M, splits, o, ldo, slab, st);
+  else if (fa == FMT_Q6_K && fb == FMT_Q6_K) rc = launch_gv_m<FMT_Q6_K, FMT_Q6_K>(a, nblk, K, x, ldx, act, M, splits, o, ldo, slab, st);
+  else if (fa == FMT_Q4_K) rc = launch_gv_m<FMT_Q4_K, FMT_Q6_K>(a, nblk, K, x, ldx, act, M, splits, o, ldo, slab, st);
+  else rc = launch_gv_m<FMT_Q6_K, FMT_Q4_K>(a, nblk, K, x, ldx, act, M, splits, o, ldo, slab, st);
   if (rc) return rc;
   return (int)hipGetLastError();
 }
