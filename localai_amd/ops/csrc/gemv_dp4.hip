@@ -141,6 +141,53 @@ LA_DEV void quantize_x(const bf16* X, int ldx, const GVAct& act, int M, int k0, 
   }
 }
 
+// Register-staged variant of quantize_x for the common decode case (bf16 x, at most GV_XI
+// (row, super-block) items per thread): x_issue() only issues the loads, so the caller can put
+// the first weight loads behind them and the two HBM round trips overlap; x_commit() waits for
+// x alone (loads retire in issue order) and writes the LDS image.
+constexpr int GV_XI = 4;
+
+template <int MT>
+LA_DEV bool x_staged_ok(const GVAct& act, int kper) {
+  return !act.p && MT * (((kper >> 8) + 3) >> 2) <= GV_XI;
+}
+
+template <int MT>
+LA_DEV void x_issue(const bf16* X, int ldx, int M, int k0, int kper, u32x2 (&xr)[GV_XI]) {
+  const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int nsb = kper >> 8, per = (nsb + 3) >> 2;
+#pragma unroll
+  for (int it = 0; it < GV_XI; ++it) {
+    const int m = it / per, sb = wv + 4 * (it - m * per);
+    const bool ok = m < M && m < MT && sb < nsb;
+    xr[it] = *(const u32x2*)(X + (size_t)(ok ? m : 0) * ldx + k0 + (ok ? sb : 0) * 256 + 4 * l);
+  }
+}
+
+template <int MT>
+LA_DEV void x_commit(int M, int kper, const u32x2 (&xr)[GV_XI], int8_t* xq, int* bs, float* dx) {
+  const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int nsb = kper >> 8, per = (nsb + 3) >> 2;
+#pragma unroll
+  for (int it = 0; it < GV_XI; ++it) {
+    const int m = it / per, sb = wv + 4 * (it - m * per);
+    if (m >= M || m >= MT || sb >= nsb) continue;
+    const float v0 = bf16_bits_to_f(xr[it].x & 0xFFFFu), v1 = bf16_bits_to_f(xr[it].x >> 16);
+    const float v2 = bf16_bits_to_f(xr[it].y & 0xFFFFu), v3 = bf16_bits_to_f(xr[it].y >> 16);
+    const float amax = group_max<8>(fmaxf(fmaxf(fabsf(v0), fabsf(v1)), fmaxf(fabsf(v2), fabsf(v3))));
+    const float inv = amax > 0.f ? 127.f / amax : 0.f;
+    const int q0 = __float2int_rn(v0 * inv), q1 = __float2int_rn(v1 * inv);
+    const int q2 = __float2int_rn(v2 * inv), q3 = __float2int_rn(v3 * inv);
+    *(uint32_t*)(xq + m * kper + sb * 256 + 4 * l) = (uint32_t)(q0 & 0xFF) | ((uint32_t)(q1 & 0xFF) << 8) |
+                                                    ((uint32_t)(q2 & 0xFF) << 16) | ((uint32_t)(q3 & 0xFF) << 24);
+    int sm = q0 + q1 + q2 + q3;
+    sm += __shfl_xor(sm, 1, 64);
+    sm += __shfl_xor(sm, 2, 64);
+    if ((l & 3) == 0) bs[m * (kper >> 4) + sb * 16 + (l >> 2)] = sm;
+    if ((l & 7) == 0) dx[m * (kper >> 5) + sb * 8 + (l >> 3)] = amax / 127.f;
+  }
+}
+
 template <int MT>
 LA_DEV void gv_store(const float (&acc)[MT][GV_RS], const int (&n)[GV_RS], int N, int M, int t, float* o,
                      int ldo, int col0) {
@@ -179,9 +226,14 @@ LA_DEV void gv_q4k(const QW& w, int row0, const bf16* X, int ldx, const GVAct& a
     sp[s] = w.p2 + nc * srow + (size_t)sb0 * 16 + 4 * j;
     dp[s] = w.p3 + nc * drow + (size_t)sb0 * 4;
   }
+  const bool staged = !EARLY && x_staged_ok<MT>(act, kper);
+  u32x2 xr[GV_XI];
+  if (staged) x_issue<MT>(X, ldx, M, k0, kper, xr);
   if constexpr (!EARLY) {
-    quantize_x<MT>(X, ldx, act, M, k0, kper, xq, bs, dx);
-    __syncthreads();
+    if (!staged) {
+      quantize_x<MT>(X, ldx, act, M, k0, kper, xq, bs, dx);
+      __syncthreads();
+    }
   }
   u32x4 qa[GV_RS];
   uint32_t sa[GV_RS], da[GV_RS];
@@ -190,6 +242,10 @@ LA_DEV void gv_q4k(const QW& w, int row0, const bf16* X, int ldx, const GVAct& a
     qa[s] = ldg16<NT>(qp[s]);
     sa[s] = *(const uint32_t*)sp[s];
     da[s] = *(const uint32_t*)dp[s];
+  }
+  if (staged) {
+    x_commit<MT>(M, kper, xr, xq, bs, dx);
+    __syncthreads();
   }
   if constexpr (EARLY) {
     quantize_x<MT>(X, ldx, act, M, k0, kper, xq, bs, dx);
@@ -287,9 +343,14 @@ LA_DEV void gv_q6k(const QW& w, int row0, const bf16* X, int ldx, const GVAct& a
     cp[s] = w.p2 + nc * crow + (size_t)sb0 * 16 + 8 * hh;
     dp[s] = w.p3 + nc * drow + (size_t)sb0 * 2;
   }
+  const bool staged = !EARLY && x_staged_ok<MT>(act, kper);
+  u32x2 xr[GV_XI];
+  if (staged) x_issue<MT>(X, ldx, M, k0, kper, xr);
   if constexpr (!EARLY) {
-    quantize_x<MT>(X, ldx, act, M, k0, kper, xq, bs, dx);
-    __syncthreads();
+    if (!staged) {
+      quantize_x<MT>(X, ldx, act, M, k0, kper, xq, bs, dx);
+      __syncthreads();
+    }
   }
   u32x4 la_[GV_RS], ha[GV_RS];
   u32x2 ca[GV_RS];
@@ -300,6 +361,10 @@ LA_DEV void gv_q6k(const QW& w, int row0, const bf16* X, int ldx, const GVAct& a
     ha[s] = ldg16<NT>(hp[s]);
     ca[s] = *(const u32x2*)cp[s];
     da[s] = *(const uint16_t*)dp[s];
+  }
+  if (staged) {
+    x_commit<MT>(M, kper, xr, xq, bs, dx);
+    __syncthreads();
   }
   if constexpr (EARLY) {
     quantize_x<MT>(X, ldx, act, M, k0, kper, xq, bs, dx);
