@@ -19,11 +19,12 @@ namespace la {
 // MFMA flash-decoding.  Workgroup = (partition of <= PS keys, kv head, sequence), 4 waves; wave w
 // takes the partition's 32-key tiles w, w+4, ...
 //   S^T[16 keys x 16 heads] = K[16 keys x Dh] . Q^T[Dh x 16 heads]   (keys on MFMA rows)
-//   -> lane l holds the scores of head l&15 for keys 4(l>>4)+i, so the running max needs only
-//      two cross-lane shuffles (xor 16, 32) and P is already the lane's A-operand fragment;
+//   -> MFMA t (of 2 per 32-key tile) puts key 8(m>>2) + 4t + (m&3) on row m, so lane l ends up
+//      with the scores of head l&15 for the 8 CONSECUTIVE keys 8(l>>4) .. +7: the running max
+//      needs only two cross-lane shuffles (xor 16, 32) and P is already the lane's A fragment;
 //   O[16 heads x Dh] += P[16 heads x 32 keys] . V[32 keys x Dh]
-//   -> V is stored transposed per page ([Dh][BS]) so the B fragment (4 keys at one d) is a
-//      contiguous 8-byte load; no LDS staging, no transposes.
+//   -> V is stored transposed per page ([Dh][BS]) so the B fragment (8 consecutive keys at one
+//      d) is ONE 16-byte load; 16 lanes x 64 B full rows per instruction, no LDS, no transposes.
 // Latency structure (decode attention is latency-bound: a few KB per wave):
 //   * the partition's block-table slice is staged in LDS once (no bt -> K/V load chains);
 //   * every K and V load of tile i+1 is issued before tile i is computed (register double
@@ -47,7 +48,7 @@ struct DecShared {
 template <int DH>
 struct DecTile {
   bf16x8 k[2][(DH + 31) / 32];
-  bf16x4 v[2][DH / 16];
+  bf16x8 v[DH / 16];
 };
 
 template <int DH, int GT>
@@ -87,22 +88,23 @@ __global__ __launch_bounds__(DEC_T) void attn_decode_kernel(
   auto load_tile = [&](int kb, DecTile<DH>& T) {
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      // K rows: key kb + 16t + r;  V^T: keys kb + 16t + 4g .. +3 (all clamped to a real key)
-      const int kk = min(kb + 16 * t + r, kend - 1);
-      const int kv = min(kb + 16 * t + 4 * g, kend - 1) & ~3;
+      // K row r of MFMA t: key kb + 8(r>>2) + 4t + (r&3) (clamped to a real key)
+      const int kk = min(kb + 8 * (r >> 2) + 4 * t + (r & 3), kend - 1);
       const long pk = (long)sh.bt[(kk - t0) / BS] * Hkv * BS * DH + head_off;
-      const long pv = (long)sh.bt[(kv - t0) / BS] * Hkv * BS * DH + head_off;
       const bf16* krow = kc + pk + (long)(kk % BS) * DH;
 #pragma unroll
       for (int c = 0; c < KC; ++c) {
         const int d = min(32 * c + 8 * g, DH - 8);
         T.k[t][c] = *(const bf16x8*)(krow + d);
       }
+    }
+    // V^T: keys kb + 8g .. +7 at d (an 8-aligned run inside one page, clamped to a real key)
+    const int kv = min(kb + 8 * g, kend - 1) & ~7;
+    const long pv = (long)sh.bt[(kv - t0) / BS] * Hkv * BS * DH + head_off;
 #pragma unroll
-      for (int nd = 0; nd < ND; ++nd) {
-        const int d = 16 * nd + r;
-        T.v[t][nd] = *(const bf16x4*)(vc + pv + (long)d * BS + (kv % BS));
-      }
+    for (int nd = 0; nd < ND; ++nd) {
+      const int d = 16 * nd + r;
+      T.v[nd] = *(const bf16x8*)(vc + pv + (long)d * BS + (kv % BS));
     }
   };
 
@@ -128,7 +130,7 @@ __global__ __launch_bounds__(DEC_T) void attn_decode_kernel(
           acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, qf[c], acc, 0, 0, 0);
         }
 #pragma unroll
-        for (int i = 0; i < 4; ++i) s[t][i] = (kb + 16 * t + 4 * g + i < kend) ? acc[i] * scale_log2 : -INFINITY;
+        for (int i = 0; i < 4; ++i) s[t][i] = (kb + 8 * g + 4 * t + i < kend) ? acc[i] * scale_log2 : -INFINITY;
       }
       // online softmax for head r over this 32-key tile
       float mx = fmaxf(fmaxf(fmaxf(s[0][0], s[0][1]), fmaxf(s[0][2], s[0][3])),
@@ -158,15 +160,7 @@ __global__ __launch_bounds__(DEC_T) void attn_decode_kernel(
         for (int nd = 0; nd < ND; ++nd) o[nd][i] *= f;
       }
 #pragma unroll
-      for (int nd = 0; nd < ND; ++nd) {
-        bf16x8 vb;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          vb[i] = cur.v[0][nd][i];
-          vb[4 + i] = cur.v[1][nd][i];
-        }
-        o[nd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, vb, o[nd], 0, 0, 0);
-      }
+      for (int nd = 0; nd < ND; ++nd) o[nd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, cur.v[nd], o[nd], 0, 0, 0);
       cur = nxt;
     }
   }

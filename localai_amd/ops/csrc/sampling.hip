@@ -134,10 +134,25 @@ __global__ __launch_bounds__(SMP_T) void sample_kernel(const float* __restrict__
   const float* row = logits + (long)b * ld;
   const SampleRow P = params[b];
 
-  // max / argmax
+  // max / argmax: 16-byte loads when the row is aligned (4x fewer dependent iterations over a
+  // 128k vocabulary: the greedy path is one workgroup per row, so this loop IS its latency)
   float mv = -INFINITY;
   int mi = 0x7fffffff;
-  for (int i = threadIdx.x; i < V; i += SMP_T) {
+  int i0 = 0;
+  if ((((uintptr_t)row) & 15) == 0) {
+    const int V4 = V >> 2;
+    const float4* row4 = (const float4*)row;
+#pragma unroll 2
+    for (int j = threadIdx.x; j < V4; j += SMP_T) {
+      const float4 v = row4[j];
+      if (v.x > mv) { mv = v.x; mi = 4 * j; }
+      if (v.y > mv) { mv = v.y; mi = 4 * j + 1; }
+      if (v.z > mv) { mv = v.z; mi = 4 * j + 2; }
+      if (v.w > mv) { mv = v.w; mi = 4 * j + 3; }
+    }
+    i0 = V4 << 2;
+  }
+  for (int i = i0 + threadIdx.x; i < V; i += SMP_T) {
     const float v = row[i];
     if (v > mv) { mv = v; mi = i; }
   }
