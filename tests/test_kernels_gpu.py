@@ -72,6 +72,29 @@ def test_gemv_dp4(t, M):
     assert (y - ref).abs().max().item() < tol
 
 
+@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("M", [1, 2])
+def test_act_linear_fused(mode, M):
+    """down(act(gate|up)) with the activation inside the dp4 GEMV prologue vs fp32 (slab source
+    with S = 3 and a bias)."""
+    F, N = 1024, 200
+    w = _qw(N, F, GGMLType.Q6_K if mode else GGMLType.Q4_K, seed=17)
+    width = 2 * F if mode == 0 else F
+    slabs = torch.randn(3, M, width, device=DEV) * 0.7
+    bias = torch.randn(width, device=DEV) * 0.1
+    src = ops.Partial(slabs, bias)
+    y = ops.act_linear(src, F, mode, w).dense().cpu()
+    g = (slabs.sum(0) + bias).cpu()
+    if mode == 0:
+        h = torch.nn.functional.silu(g[:, :F]) * g[:, F:]
+    elif mode == 1:
+        h = torch.nn.functional.gelu(g, approximate="tanh")
+    else:
+        h = g * torch.sigmoid(1.702 * g)
+    ref = h @ w.ref.t()
+    assert (y - ref).abs().max().item() < 2e-2 * max(1.0, ref.abs().max().item())
+
+
 @pytest.mark.parametrize("M", [1, 3])
 def test_gemv_dp4_segments(M):
     """One launch over mixed-format weights side by side (Q4_K q|k + Q6_K v shape), plus a
