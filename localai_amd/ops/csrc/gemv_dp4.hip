@@ -9,7 +9,7 @@
 //
 // Work mapping (wave64): a row's super-block is 128 contiguous quant bytes, read by 8 adjacent
 // lanes x 16 B (fully used 128 B runs: 5.0 TB/s class access pattern, decode_gemv_study.md §1).
-// A wave covers 8 rows per load instruction, GV_RS row slots per wave, 4 waves per workgroup,
+// A wave covers 8 rows per load instruction, RS row slots per wave, 4 waves per workgroup,
 // so a workgroup owns 64 rows and one K split; grid.y = split-K, partials go to fp32 slabs
 // [S][M][ldo] which the consumer (add_norm / rope_kv / act) sums -- the same contract as the
 // other GEMMs (ops.Partial).
@@ -36,8 +36,9 @@
 namespace la {
 
 constexpr int GV_THREADS = 256;
-constexpr int GV_RS = 2;                 // row slots (of 8 rows) per wave
-constexpr int GV_ROWS = 4 * 8 * GV_RS;   // rows per workgroup
+// row slots (of 8 rows) per wave: 2 by default, 1 or 4 in the tuning variants (VAR bits 2/3)
+template <int VAR>
+constexpr int gv_rs() { return (VAR & 4) ? 1 : ((VAR & 8) ? 4 : 2); }
 constexpr int GV_SEGS = 3;
 
 struct GVArgs {
@@ -188,14 +189,14 @@ LA_DEV void x_commit(int M, int kper, const u32x2 (&xr)[GV_XI], int8_t* xq, int*
   }
 }
 
-template <int MT>
-LA_DEV void gv_store(const float (&acc)[MT][GV_RS], const int (&n)[GV_RS], int N, int M, int t, float* o,
+template <int MT, int RS>
+LA_DEV void gv_store(const float (&acc)[MT][RS], const int (&n)[RS], int N, int M, int t, float* o,
                      int ldo, int col0) {
 #pragma unroll
   for (int m = 0; m < MT; ++m) {
     if (m < M) {
 #pragma unroll
-      for (int s = 0; s < GV_RS; ++s) {
+      for (int s = 0; s < RS; ++s) {
         const float v = group_sum<8>(acc[m][s]);
         if (t == 0 && n[s] < N) o[(size_t)m * ldo + col0 + n[s]] = v;
       }
@@ -203,7 +204,7 @@ LA_DEV void gv_store(const float (&acc)[MT][GV_RS], const int (&n)[GV_RS], int N
   }
 }
 
-template <int MT, int NT, int EARLY>
+template <int MT, int NT, int EARLY, int RS>
 LA_DEV void gv_q4k(const QW& w, int row0, const bf16* X, int ldx, const GVAct& act, int M, int kper, float* o,
                    int ldo, int col0,
                    int8_t* xq, int* bs, float* dx) {
@@ -214,13 +215,13 @@ LA_DEV void gv_q4k(const QW& w, int row0, const bf16* X, int ldx, const GVAct& a
   const int xlo = 64 * j + 16 * h;  // element offset of this lane's low-nibble run (high: +32)
   const int blo = 4 * j + h;        // its 16-run index (high-nibble run: blo + 2)
   const size_t qrow = (size_t)(w.K >> 1), srow = (size_t)(w.K >> 8) * 16, drow = (size_t)(w.K >> 8) * 4;
-  int n[GV_RS];
-  const uint8_t* qp[GV_RS];
-  const uint8_t* sp[GV_RS];
-  const uint8_t* dp[GV_RS];
+  int n[RS];
+  const uint8_t* qp[RS];
+  const uint8_t* sp[RS];
+  const uint8_t* dp[RS];
 #pragma unroll
-  for (int s = 0; s < GV_RS; ++s) {
-    n[s] = row0 + wv * (8 * GV_RS) + s * 8 + r;
+  for (int s = 0; s < RS; ++s) {
+    n[s] = row0 + wv * (8 * RS) + s * 8 + r;
     const size_t nc = n[s] < w.N ? n[s] : w.N - 1;  // clamped row for loads
     qp[s] = w.p0 + nc * qrow + (size_t)sb0 * 128 + 16 * t;
     sp[s] = w.p2 + nc * srow + (size_t)sb0 * 16 + 4 * j;
@@ -235,10 +236,10 @@ LA_DEV void gv_q4k(const QW& w, int row0, const bf16* X, int ldx, const GVAct& a
       __syncthreads();
     }
   }
-  u32x4 qa[GV_RS];
-  uint32_t sa[GV_RS], da[GV_RS];
+  u32x4 qa[RS];
+  uint32_t sa[RS], da[RS];
 #pragma unroll
-  for (int s = 0; s < GV_RS; ++s) {
+  for (int s = 0; s < RS; ++s) {
     qa[s] = ldg16<NT>(qp[s]);
     sa[s] = *(const uint32_t*)sp[s];
     da[s] = *(const uint32_t*)dp[s];
@@ -252,27 +253,27 @@ LA_DEV void gv_q4k(const QW& w, int row0, const bf16* X, int ldx, const GVAct& a
     __syncthreads();
   }
 
-  float acc[MT][GV_RS];
+  float acc[MT][RS];
 #pragma unroll
   for (int m = 0; m < MT; ++m)
 #pragma unroll
-    for (int s = 0; s < GV_RS; ++s) acc[m][s] = 0.f;
+    for (int s = 0; s < RS; ++s) acc[m][s] = 0.f;
 
   for (int sb = 0; sb < nsb; ++sb) {
-    u32x4 qn[GV_RS];
-    uint32_t sn[GV_RS], dn[GV_RS];
+    u32x4 qn[RS];
+    uint32_t sn[RS], dn[RS];
     if (sb + 1 < nsb) {
 #pragma unroll
-      for (int s = 0; s < GV_RS; ++s) {
+      for (int s = 0; s < RS; ++s) {
         qn[s] = ldg16<NT>(qp[s] + (sb + 1) * 128);
         sn[s] = *(const uint32_t*)(sp[s] + (sb + 1) * 16);
         dn[s] = *(const uint32_t*)(dp[s] + (sb + 1) * 4);
       }
     }
     // unpack the nibbles once, reuse for every activation row
-    u32x4 lo[GV_RS], hi[GV_RS];
+    u32x4 lo[RS], hi[RS];
 #pragma unroll
-    for (int s = 0; s < GV_RS; ++s) {
+    for (int s = 0; s < RS; ++s) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         lo[s][i] = qa[s][i] & 0x0F0F0F0Fu;
@@ -290,7 +291,7 @@ LA_DEV void gv_q4k(const QW& w, int row0, const bf16* X, int ldx, const GVAct& a
         const float dxl = dm[2 * j], dxh = dm[2 * j + 1];
         const float bl = (float)bm[blo] * dxl, bh = (float)bm[blo + 2] * dxh;
 #pragma unroll
-        for (int s = 0; s < GV_RS; ++s) {
+        for (int s = 0; s < RS; ++s) {
           int dl = dot4(lo[s][0], xl[0], 0), dh = dot4(hi[s][0], xh[0], 0);
           dl = dot4(lo[s][1], xl[1], dl); dh = dot4(hi[s][1], xh[1], dh);
           dl = dot4(lo[s][2], xl[2], dl); dh = dot4(hi[s][2], xh[2], dh);
@@ -305,17 +306,17 @@ LA_DEV void gv_q4k(const QW& w, int row0, const bf16* X, int ldx, const GVAct& a
     }
     if (sb + 1 < nsb) {
 #pragma unroll
-      for (int s = 0; s < GV_RS; ++s) {
+      for (int s = 0; s < RS; ++s) {
         qa[s] = qn[s];
         sa[s] = sn[s];
         da[s] = dn[s];
       }
     }
   }
-  gv_store<MT>(acc, n, w.N, M, t, o, ldo, col0);
+  gv_store<MT, RS>(acc, n, w.N, M, t, o, ldo, col0);
 }
 
-template <int MT, int NT, int EARLY>
+template <int MT, int NT, int EARLY, int RS>
 LA_DEV void gv_q6k(const QW& w, int row0, const bf16* X, int ldx, const GVAct& act, int M, int kper, float* o,
                    int ldo, int col0,
                    int8_t* xq, int* bs, float* dx) {
@@ -329,14 +330,14 @@ LA_DEV void gv_q6k(const QW& w, int row0, const bf16* X, int ldx, const GVAct& a
   const int scb = 8 * (2 * s2 + (u & 1));               // bit offset of this lane's scale byte
   const size_t lrow = (size_t)(w.K >> 1), hrow = (size_t)(w.K >> 2), crow = (size_t)(w.K >> 4),
                drow = (size_t)(w.K >> 8) * 2;
-  int n[GV_RS];
-  const uint8_t* lp[GV_RS];
-  const uint8_t* hp[GV_RS];
-  const uint8_t* cp[GV_RS];
-  const uint8_t* dp[GV_RS];
+  int n[RS];
+  const uint8_t* lp[RS];
+  const uint8_t* hp[RS];
+  const uint8_t* cp[RS];
+  const uint8_t* dp[RS];
 #pragma unroll
-  for (int s = 0; s < GV_RS; ++s) {
-    n[s] = row0 + wv * (8 * GV_RS) + s * 8 + r;
+  for (int s = 0; s < RS; ++s) {
+    n[s] = row0 + wv * (8 * RS) + s * 8 + r;
     const size_t nc = n[s] < w.N ? n[s] : w.N - 1;
     lp[s] = w.p0 + nc * lrow + (size_t)sb0 * 128 + 64 * hh + 16 * u;
     hp[s] = w.p1 + nc * hrow + (size_t)sb0 * 64 + 32 * hh + 16 * (u & 1);
@@ -352,11 +353,11 @@ LA_DEV void gv_q6k(const QW& w, int row0, const bf16* X, int ldx, const GVAct& a
       __syncthreads();
     }
   }
-  u32x4 la_[GV_RS], ha[GV_RS];
-  u32x2 ca[GV_RS];
-  uint32_t da[GV_RS];
+  u32x4 la_[RS], ha[RS];
+  u32x2 ca[RS];
+  uint32_t da[RS];
 #pragma unroll
-  for (int s = 0; s < GV_RS; ++s) {
+  for (int s = 0; s < RS; ++s) {
     la_[s] = ldg16<NT>(lp[s]);
     ha[s] = ldg16<NT>(hp[s]);
     ca[s] = *(const u32x2*)cp[s];
@@ -371,28 +372,28 @@ LA_DEV void gv_q6k(const QW& w, int row0, const bf16* X, int ldx, const GVAct& a
     __syncthreads();
   }
 
-  float acc[MT][GV_RS];
+  float acc[MT][RS];
 #pragma unroll
   for (int m = 0; m < MT; ++m)
 #pragma unroll
-    for (int s = 0; s < GV_RS; ++s) acc[m][s] = 0.f;
+    for (int s = 0; s < RS; ++s) acc[m][s] = 0.f;
 
   for (int sb = 0; sb < nsb; ++sb) {
-    u32x4 ln[GV_RS], hn[GV_RS];
-    u32x2 cn[GV_RS];
-    uint32_t dn[GV_RS];
+    u32x4 ln[RS], hn[RS];
+    u32x2 cn[RS];
+    uint32_t dn[RS];
     if (sb + 1 < nsb) {
 #pragma unroll
-      for (int s = 0; s < GV_RS; ++s) {
+      for (int s = 0; s < RS; ++s) {
         ln[s] = ldg16<NT>(lp[s] + (sb + 1) * 128);
         hn[s] = ldg16<NT>(hp[s] + (sb + 1) * 64);
         cn[s] = *(const u32x2*)(cp[s] + (sb + 1) * 16);
         dn[s] = *(const uint16_t*)(dp[s] + (sb + 1) * 2);
       }
     }
-    u32x4 lo[GV_RS], hi[GV_RS];
+    u32x4 lo[RS], hi[RS];
 #pragma unroll
-    for (int s = 0; s < GV_RS; ++s) {
+    for (int s = 0; s < RS; ++s) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         lo[s][i] = (la_[s][i] & 0x0F0F0F0Fu) | ((ha[s][i] << shl) & 0x30303030u);
@@ -410,7 +411,7 @@ LA_DEV void gv_q6k(const QW& w, int row0, const bf16* X, int ldx, const GVAct& a
         const float* dm = dx + m * (kper >> 5) + sb * 8;
         const float dxl = dm[xlo >> 5], dxh = dm[(xlo >> 5) + 2];
 #pragma unroll
-        for (int s = 0; s < GV_RS; ++s) {
+        for (int s = 0; s < RS; ++s) {
           int dl = dot4(lo[s][0], xl[0], bl), dh = dot4(hi[s][0], xh[0], bh);
           dl = dot4(lo[s][1], xl[1], dl); dh = dot4(hi[s][1], xh[1], dh);
           dl = dot4(lo[s][2], xl[2], dl); dh = dot4(hi[s][2], xh[2], dh);
@@ -424,7 +425,7 @@ LA_DEV void gv_q6k(const QW& w, int row0, const bf16* X, int ldx, const GVAct& a
     }
     if (sb + 1 < nsb) {
 #pragma unroll
-      for (int s = 0; s < GV_RS; ++s) {
+      for (int s = 0; s < RS; ++s) {
         la_[s] = ln[s];
         ha[s] = hn[s];
         ca[s] = cn[s];
@@ -432,7 +433,7 @@ LA_DEV void gv_q6k(const QW& w, int row0, const bf16* X, int ldx, const GVAct& a
       }
     }
   }
-  gv_store<MT>(acc, n, w.N, M, t, o, ldo, col0);
+  gv_store<MT, RS>(acc, n, w.N, M, t, o, ldo, col0);
 }
 
 // Segments [0, nA) are format FA, [nA, nseg) format FB (a q|k + v fusion is (Q4_K, Q6_K)).
@@ -449,16 +450,17 @@ __global__ __launch_bounds__(GV_THREADS) void qgemv_dp4_kernel(GVArgs a, const b
 #pragma unroll
   for (int i = 0; i < GV_SEGS - 1; ++i)
     if (seg < a.nseg - 1 && blk >= a.blk_end[seg]) ++seg;
-  const int row0 = (blk - (seg ? a.blk_end[seg - 1] : 0)) * GV_ROWS;
+  constexpr int RS = gv_rs<VAR>();
+  const int row0 = (blk - (seg ? a.blk_end[seg - 1] : 0)) * (32 * RS);
   float* o = out + (size_t)blockIdx.y * slab;
   constexpr int NT = VAR & 1, EARLY = (VAR >> 1) & 1;
   const bool fa = FA == FB || a.fmt[seg] == FA;
   if (fa) {
-    if constexpr (FA == FMT_Q4_K) gv_q4k<MT, NT, EARLY>(a.w[seg], row0, X, ldx, act, M, kper, o, ldo, a.col0[seg], xq, bs, dx);
-    else gv_q6k<MT, NT, EARLY>(a.w[seg], row0, X, ldx, act, M, kper, o, ldo, a.col0[seg], xq, bs, dx);
+    if constexpr (FA == FMT_Q4_K) gv_q4k<MT, NT, EARLY, RS>(a.w[seg], row0, X, ldx, act, M, kper, o, ldo, a.col0[seg], xq, bs, dx);
+    else gv_q6k<MT, NT, EARLY, RS>(a.w[seg], row0, X, ldx, act, M, kper, o, ldo, a.col0[seg], xq, bs, dx);
   } else if constexpr (FA != FB) {
-    if constexpr (FB == FMT_Q4_K) gv_q4k<MT, NT, EARLY>(a.w[seg], row0, X, ldx, act, M, kper, o, ldo, a.col0[seg], xq, bs, dx);
-    else gv_q6k<MT, NT, EARLY>(a.w[seg], row0, X, ldx, act, M, kper, o, ldo, a.col0[seg], xq, bs, dx);
+    if constexpr (FB == FMT_Q4_K) gv_q4k<MT, NT, EARLY, RS>(a.w[seg], row0, X, ldx, act, M, kper, o, ldo, a.col0[seg], xq, bs, dx);
+    else gv_q6k<MT, NT, EARLY, RS>(a.w[seg], row0, X, ldx, act, M, kper, o, ldo, a.col0[seg], xq, bs, dx);
   }
 }
 
@@ -466,7 +468,7 @@ static inline size_t gv_lds_bytes(int MT, int kper) {
   return (size_t)MT * kper + (size_t)MT * (kper >> 4) * 4 + (size_t)MT * (kper >> 5) * 4;
 }
 
-static int g_gv_variant = 1;  // non-temporal weight loads, x prologue first (fastest on every decode shape)
+static int g_gv_variant = 5;  // non-temporal weight loads, x staged first, one 8-row slot per wave (fastest overall)
 
 template <int MT, int FA, int FB>
 static int launch_gv(const GVArgs& a, int nblk, int K, const bf16* X, int ldx, const GVAct& act, int M, int splits,
@@ -478,7 +480,7 @@ static int launch_gv(const GVArgs& a, int nblk, int K, const bf16* X, int ldx, c
   switch (g_gv_variant) {
 #define GV_CASE(V) \
     case V: hipLaunchKernelGGL((qgemv_dp4_kernel<MT, FA, FB, V>), grid, dim3(GV_THREADS), lds, st, a, X, ldx, act, M, kper, out, ldo, slab); break;
-    GV_CASE(0) GV_CASE(1) GV_CASE(2) GV_CASE(3)
+    GV_CASE(0) GV_CASE(1) GV_CASE(2) GV_CASE(3) GV_CASE(5) GV_CASE(9)
 #undef GV_CASE
     default: return -4;
   }
@@ -519,6 +521,7 @@ extern "C" int la_qgemv_dp4(int nseg, const int* fmts, const void* const* planes
   }
   GVArgs a{};
   int nblk = 0, col = 0;
+  const int rows = 32 * ((g_gv_variant & 4) ? 1 : ((g_gv_variant & 8) ? 4 : 2));  // rows per workgroup
   for (int i = 0; i < nseg; ++i) {
     const int f = fmts[i], N = Ns[i];
     const void* const* p = planes + 4 * i;
@@ -526,7 +529,7 @@ extern "C" int la_qgemv_dp4(int nseg, const int* fmts, const void* const* planes
     a.w[i] = QW{(const uint8_t*)p[0], (const uint8_t*)p[1], (const uint8_t*)p[2], (const uint8_t*)p[3], N, K};
     a.fmt[i] = f;
     a.col0[i] = col;
-    nblk += (N + GV_ROWS - 1) / GV_ROWS;
+    nblk += (N + rows - 1) / rows;
     a.blk_end[i] = nblk;
     col += N;
   }
@@ -552,7 +555,7 @@ extern "C" int la_qgemv_dp4(int nseg, const int* fmts, const void* const* planes
 
 // Tuning hook: select the kernel variant (bit 0 non-temporal loads, bit 1 early weight prefetch).
 extern "C" int la_gemv_variant(int v) {
-  if (v < 0 || v > 3) return -1;
+  if (!(v >= 0 && v <= 3) && v != 5 && v != 9) return -1;
   la::g_gv_variant = v;
   return 0;
 }

@@ -52,15 +52,18 @@ SHAPES = [("qk", [("q4k", 5120, 4096)]), ("v", [("q6k", 1024, 4096)]), ("qkv", [
           ("o", [("q4k", 4096, 4096)]), ("gate_up", [("q4k", 28672, 4096)]), ("down", [("q4k", 4096, 14336)]),
           ("down6", [("q6k", 4096, 14336)]), ("lm_head", [("q6k", 128256, 4096)])]
 variants = [int(v) for v in os.environ.get("GEMV_VARIANTS", "0,1,2,3").split(",")]
+sweep_s = os.environ.get("GEMV_SWEEP_S") == "1"   # time every split-K factor (variant 1) instead
 M = int(os.environ.get("GEMV_M", "1"))
 for name, specs in SHAPES:
     groups, wbytes = copies(specs)
     K = specs[0][2]
     Ntot = sum(N for _, N, _ in specs)
     x = (torch.randn(M, K, device=dev) * 0.5).to(torch.bfloat16)
-    S = ops._gemv_splits(groups[0], K, M)
-    out = torch.empty(S, M, Ntot, dtype=torch.float32, device=dev)
-    for v in variants:
+    S0 = ops._gemv_splits(groups[0], K, M)
+    nsb = K // 256
+    runs = [(int(os.environ.get("GEMV_SWEEP_VAR", "5")), S) for S in range(1, min(nsb, 32) + 1) if nsb % S == 0] if sweep_s else [(v, S0) for v in variants]
+    for v, S in runs:
+        out = torch.empty(S, M, Ntot, dtype=torch.float32, device=dev)
         assert ops.lib().la_gemv_variant(v) == 0
         cnt = [0]
 
@@ -69,5 +72,6 @@ for name, specs in SHAPES:
             cnt[0] += 1
             ops.gemv_dp4(x, groups[i % len(groups)], S, out)
         us = timeit(fn, max(20, 2 * len(groups)))
-        print(f"{name:8s} M={M} S={S:2d} var={v} {us:8.2f} us  {wbytes / us / 1e6:5.2f} TB/s", flush=True)
-ops.lib().la_gemv_variant(1)
+        print(f"{name:8s} M={M} S={S:2d}{'*' if S == S0 else ' '} var={v} {us:8.2f} us  {wbytes / us / 1e6:5.2f} TB/s",
+              flush=True)
+ops.lib().la_gemv_variant(5)
