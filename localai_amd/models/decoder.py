@@ -324,12 +324,14 @@ class DecoderModel:
         n = len(self.layers)
         for i, L in enumerate(self.layers):
             qkv = ops.linear_multi(xn, L.qkv, bias=L.qkv_bias)
-            q = ops.rope_kv(qkv, fb.pos, fb.slots, self.cos_sin, self.Hq, self.Hkv, self.Dh, self.rot, hp.rope_mode,
-                            kv.k[i], kv.v[i], kv.block_size)
             if fb.decode:
-                a = ops.attn_decode(q, kv.k[i], kv.v[i], fb.block_tables, fb.seq_lens, self.scale, fb.max_len,
-                                    workspace=attn_workspace)
+                # RoPE + KV append fused into the decode attention launch (rope_kv when not fusable)
+                a = ops.attn_decode_rope(qkv, fb.pos, fb.slots, self.cos_sin, self.Hq, self.Hkv, self.Dh, self.rot,
+                                         hp.rope_mode, kv.k[i], kv.v[i], fb.block_tables, fb.seq_lens, self.scale,
+                                         fb.max_len, workspace=attn_workspace)
             else:
+                q = ops.rope_kv(qkv, fb.pos, fb.slots, self.cos_sin, self.Hq, self.Hkv, self.Dh, self.rot,
+                                hp.rope_mode, kv.k[i], kv.v[i], kv.block_size)
                 a = ops.attn_prefill(q, kv.k[i], kv.v[i], fb.cu_q, fb.ctx_lens, fb.block_tables, self.scale,
                                      tiles=fb.tiles)
             o = self._row_parallel_out(ops.linear(a.view(T, self.Hq * self.Dh), L.wo), L.wo_bias)

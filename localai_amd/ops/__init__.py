@@ -54,7 +54,7 @@ def lib():
             "la_reduce_slabs": [P, LNG, I, P, I, I, P, P, P],
             "la_embed": [I, P, P, P, P, I, I, P, I, P, F, P],
             "la_dequant": [I, P, P, P, P, I, I, P, P],
-            "la_attn_decode": [P, P, P, P, I, P, I, I, I, I, I, F, I, I, P, P, P, P, P],
+            "la_attn_decode": [P, P, P, P, I, P, I, I, I, I, I, F, I, I, P, P, P, P, P, LNG, I, P, P, P, P, P],
             "la_attn_prefill": [P, P, P, P, I, P, P, P, I, I, I, I, I, F, P, P],
             "la_sample": [P, LNG, I, I, P, P, P, P, P],
             "la_penalties": [P, LNG, I, P, I, P, P, I, P, P],
@@ -817,8 +817,52 @@ def attn_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, b
     po, pml, tk = workspace[:3]
     _check(lib().la_attn_decode(q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr(),
                                 block_tables.shape[1], seq_lens.data_ptr(), B, Hq, Hkv, Dh, BS, float(scale), P, PS,
-                                out.data_ptr(), po.data_ptr(), pml.data_ptr(), tk.data_ptr(), _stream()),
+                                out.data_ptr(), po.data_ptr(), pml.data_ptr(), tk.data_ptr(), None, 0, 0, None, None,
+                                None, None, _stream()),
            "la_attn_decode")
+    return out
+
+
+# Off by default: measured on MI355X (Llama-3-8B Q4_K_M, engine bench) the fused launch is not
+# faster -- C=1 435.5 vs 440.4 tok/s, C=256 26.43k vs 26.55k -- because the q|k|v slab loads move
+# onto the attention kernel's critical path instead of disappearing with the rope_kv launch.
+FUSED_DECODE_ROPE = os.environ.get("LOCALAI_AMD_FUSED_ROPE", "0") == "1"
+
+
+def attn_decode_rope(qkv: Partial, pos: torch.Tensor, slots: torch.Tensor, cos_sin: torch.Tensor, Hq: int,
+                     Hkv: int, Dh: int, rot: int, mode: int, k_cache: torch.Tensor, v_cache: torch.Tensor,
+                     block_tables: torch.Tensor, seq_lens: torch.Tensor, scale: float, max_seq_len: int,
+                     out: Optional[torch.Tensor] = None,
+                     workspace: Optional[Tuple[torch.Tensor, ...]] = None) -> torch.Tensor:
+    """Decode step attention with the step's RoPE + paged KV append fused into the attention
+    kernel (one launch instead of rope_kv + attn_decode).  Same numerics as the two-kernel path
+    (q/k rotated in fp32, rounded to bf16).  Falls back to rope_kv + attn_decode for NEOX /
+    partial rotary, Dh not a multiple of 32, or CPU tensors."""
+    T = qkv.M
+    nblk, _, BS, _ = k_cache.shape
+    fusable = (FUSED_DECODE_ROPE and qkv.t.is_cuda and mode == 0 and rot == Dh and Dh % 32 == 0
+               and k_cache.dtype == torch.bfloat16 and v_cache.dtype == torch.bfloat16
+               and qkv.N == (Hq + 2 * Hkv) * Dh and (qkv.S >= 1 or qkv.t.dtype == torch.bfloat16)
+               and tuple(cos_sin.shape[1:]) == (Dh // 2, 2))
+    if not fusable:
+        q = rope_kv(qkv, pos, slots, cos_sin, Hq, Hkv, Dh, rot, mode, k_cache, v_cache, BS)
+        return attn_decode(q, k_cache, v_cache, block_tables, seq_lens, scale, max_seq_len, out=out,
+                           workspace=workspace)
+    if Hq % Hkv or tuple(v_cache.shape) != (nblk, Hkv, Dh, BS) or k_cache.shape[3] != Dh:
+        raise ValueError("attn_decode_rope: head/cache shape mismatch")
+    P, PS = decode_partitions(T, Hkv, max_seq_len, BS)
+    if out is None:
+        out = torch.empty(T, Hq, Dh, dtype=torch.bfloat16, device=qkv.t.device)
+    if (workspace is None or len(workspace) < 3 or workspace[0].numel() < T * Hq * P * Dh
+            or workspace[1].numel() < T * Hq * P * 2 or workspace[2].numel() < T * Hkv):
+        workspace = decode_workspace(T, Hq, Hkv, Dh, max_seq_len, qkv.t.device, BS)
+    po, pml, tk = workspace[:3]
+    a = qkv.src_args()
+    _check(lib().la_attn_decode(None, k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr(),
+                                block_tables.shape[1], seq_lens.data_ptr(), T, Hq, Hkv, Dh, BS, float(scale), P, PS,
+                                out.data_ptr(), po.data_ptr(), pml.data_ptr(), tk.data_ptr(), a[0], a[1], a[2], a[3],
+                                pos.data_ptr(), slots.data_ptr(), cos_sin.data_ptr(), _stream()),
+           "la_attn_decode(rope)")
     return out
 
 

@@ -51,12 +51,63 @@ struct DecTile {
   bf16x8 v[DH / 16];
 };
 
+// Fused RoPE + KV append for decode (replaces the rope_kv launch of a decode step): the kernel
+// reads the q|k|v GEMM output itself (fp32 split-K slabs or one bf16 matrix, optional bias),
+// rotates q for its heads, and the workgroup whose partition holds the newest key rotates k
+// and writes k / v of that token into the paged cache before its own tile loads read them.
+// NORM (adjacent-pair) rotary over the full head only; anything else uses rope_kv.
+struct DecRope {
+  const void* p;         // null: q comes pre-rotated in `q` (unfused path)
+  long slab;             // elements between fp32 slabs
+  int S;                 // fp32 slabs (0: p is one bf16 [B][W] matrix)
+  const float* bias;     // [W] or null
+  const int* pos;        // [B] rotary position of the new token
+  const int* slots;      // [B] cache slot of the new token (< 0: no append)
+  const float* cos_sin;  // [max_pos][DH/2][2]
+  int W;                 // row width (Hq + 2 Hkv) * DH
+};
+
+// x[b, col .. col+N) of the q|k|v source, summed over slabs (+bias), in fp32.  N in {1, 2, 8};
+// col is a multiple of N.  Every slab load of a group of 8 is issued before the first add
+// (clamped slab index, masked -- never a branch), so the slabs cost one memory round trip.
+template <int N>
+LA_DEV void rope_src_load(const DecRope& R, int b, int col, float (&v)[N]) {
+  typedef float fvec __attribute__((ext_vector_type(N)));
+  typedef __bf16 bvec __attribute__((ext_vector_type(N)));
+  const long idx = (long)b * R.W + col;
+  if (R.S == 0) {
+    const bvec s = *(const bvec*)((const bf16*)R.p + idx);
+#pragma unroll
+    for (int j = 0; j < N; ++j) v[j] = (float)s[j];
+  } else {
+    const float* f = (const float*)R.p + idx;
+#pragma unroll
+    for (int j = 0; j < N; ++j) v[j] = 0.f;
+    for (int s0 = 0; s0 < R.S; s0 += 8) {
+      fvec t[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) t[i] = *(const fvec*)(f + (long)min(s0 + i, R.S - 1) * R.slab);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float m = (s0 + i < R.S) ? 1.f : 0.f;
+#pragma unroll
+        for (int j = 0; j < N; ++j) v[j] = fmaf(m, t[i][j], v[j]);
+      }
+    }
+  }
+  if (R.bias) {
+    const fvec bb = *(const fvec*)(R.bias + col);
+#pragma unroll
+    for (int j = 0; j < N; ++j) v[j] += bb[j];
+  }
+}
+
 template <int DH, int GT>
 __global__ __launch_bounds__(DEC_T) void attn_decode_kernel(
     const bf16* __restrict__ q, const bf16* __restrict__ kc, const bf16* __restrict__ vc,
     const int* __restrict__ block_tables, int max_blocks, const int* __restrict__ seq_lens, int Hkv, int G,
     int BS, float scale_log2, int PS, bf16* __restrict__ out, float* __restrict__ part_o,
-    float* __restrict__ part_ml, int P, int* __restrict__ tickets) {
+    float* __restrict__ part_ml, int P, int* __restrict__ tickets, DecRope R) {
   constexpr int KC = (DH + 31) / 32;  // 32-wide k chunks of the QK^T product
   constexpr int ND = DH / 16;         // 16-wide d tiles of the PV product
   __shared__ DecShared<DH, GT> sh;
@@ -75,12 +126,54 @@ __global__ __launch_bounds__(DEC_T) void attn_decode_kernel(
 
   // Q^T fragments: lane holds Q[head r][d = 32c + 8g .. +8]
   bf16x8 qf[KC];
+  if (R.p) {
+    const float* cs = R.cos_sin + (long)R.pos[b] * DH;  // DH/2 (cos, sin) pairs
 #pragma unroll
-  for (int c = 0; c < KC; ++c) {
-    const int d = 32 * c + 8 * g;
-    bf16x8 v = {};
-    if (r < G && d < DH) v = *(const bf16x8*)(q + ((long)b * Hq + kvh * G + r) * DH + d);
-    qf[c] = v;
+    for (int c = 0; c < KC; ++c) {
+      const int d = 32 * c + 8 * g;
+      bf16x8 v = {};
+      if (r < G) {
+        float x[8];
+        rope_src_load<8>(R, b, (kvh * G + r) * DH + d, x);
+#pragma unroll
+        for (int j = 0; j < 8; j += 2) {
+          const float cc = cs[d + j], sn = cs[d + j + 1];  // pair (d+j)/2: (cos, sin) at d+j, d+j+1
+          v[j] = (bf16)(x[j] * cc - x[j + 1] * sn);
+          v[j + 1] = (bf16)(x[j] * sn + x[j + 1] * cc);
+        }
+      }
+      qf[c] = v;
+    }
+    // the partition holding the newest key appends its k (rotated) and v to the cache
+    const int slot = R.slots[b];
+    if (slot >= 0 && L - 1 >= t0 && L - 1 < kend) {
+      const int blk = slot / BS, off = slot - blk * BS;
+      if (tid < DH / 2) {
+        float x[2];
+        rope_src_load<2>(R, b, (Hq + kvh) * DH + 2 * tid, x);
+        const float cc = cs[2 * tid], sn = cs[2 * tid + 1];
+        bf16* kd = (bf16*)kc + (((long)blk * Hkv + kvh) * BS + off) * DH + 2 * tid;
+        kd[0] = (bf16)(x[0] * cc - x[1] * sn);
+        kd[1] = (bf16)(x[0] * sn + x[1] * cc);
+      } else if (tid < DH / 2 + DH) {
+        const int d = tid - DH / 2;
+        float x[1];
+        rope_src_load<1>(R, b, (Hq + Hkv + kvh) * DH + d, x);
+        ((bf16*)vc)[(((long)blk * Hkv + kvh) * DH + d) * BS + off] = (bf16)x[0];  // V^T page [Dh][BS]
+      }
+      // Only this workgroup reads the appended key back (pages never straddle partitions, and
+      // L1 starts each launch clean), so same-CU ordering suffices: the stores reach the XCD's
+      // L2 before the barrier below; no agent-scope fence (MI355X_MICROARCH: ~3.5 us each).
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < KC; ++c) {
+      const int d = 32 * c + 8 * g;
+      bf16x8 v = {};
+      if (r < G && d < DH) v = *(const bf16x8*)(q + ((long)b * Hq + kvh * G + r) * DH + d);
+      qf[c] = v;
+    }
   }
   __syncthreads();
 
@@ -406,10 +499,16 @@ __global__ __launch_bounds__(PF_T) void attn_prefill_kernel(
 // C ABI ------------------------------------------------------------------------------------
 extern "C" int la_attn_decode(const void* q, const void* kc, const void* vc, const int* block_tables, int max_blocks,
                               const int* seq_lens, int B, int Hq, int Hkv, int Dh, int BS, float scale, int P, int PS,
-                              void* out, void* part_o, void* part_ml, void* tickets, void* stream) {
+                              void* out, void* part_o, void* part_ml, void* tickets, const void* rope_p,
+                              long rope_slab, int rope_S, const void* rope_bias, const int* pos, const int* slots,
+                              const float* cos_sin, void* stream) {
   if (Hq % Hkv || Hq / Hkv > 16 || (BS % 16) || (128 % BS && BS % 128) || (PS % 128) || P < 1 ||
       PS / BS > la::DEC_MAXBT || P > 64 || (P > 1 && !tickets))
     return -1;
+  // rope_p != null: fused RoPE + KV append from the q|k|v GEMM output (q unused)
+  if (rope_p && ((Dh & 31) || !pos || !slots || !cos_sin || rope_S < 0)) return -1;
+  if (!rope_p && !q) return -1;
+  const la::DecRope R{rope_p, rope_slab, rope_S, (const float*)rope_bias, pos, slots, cos_sin, (Hq + 2 * Hkv) * Dh};
   const int G = Hq / Hkv;
   hipStream_t st = (hipStream_t)stream;
   dim3 grid(P, Hkv, B);
@@ -420,7 +519,7 @@ extern "C" int la_attn_decode(const void* q, const void* kc, const void* vc, con
 #define DEC(D, GT)                                                                                                 \
   hipLaunchKernelGGL((la::attn_decode_kernel<D, GT>), grid, dim3(la::DEC_T), 0, st, (const bf16*)q,              \
                      (const bf16*)kc, (const bf16*)vc, block_tables, max_blocks, seq_lens, Hkv, G, BS, sl2, PS,  \
-                     (bf16*)out, po, pml, P, tk)
+                     (bf16*)out, po, pml, P, tk, R)
 #define DEC_G(D)                          \
   if (G == 1) DEC(D, 1);                  \
   else if (G == 2) DEC(D, 2);             \

@@ -273,6 +273,40 @@ def test_attn_decode(Hq, Hkv, Dh, BS):
         assert (out.float().cpu() - ref.float()).abs().max().item() < 2e-2
 
 
+@pytest.mark.parametrize("src", ["slabs", "bf16"])
+def test_attn_decode_fused_rope(src):
+    """Decode attention with RoPE + KV append fused in == rope_kv + attn_decode (outputs and the
+    appended cache entries), over split-KV partitions (graph bound 4096) and a padded row."""
+    Hq, Hkv, Dh, BS = 32, 8, 128, 32
+    lens = [1, 37, 300, 1025, 1]
+    kc, vc, bt = _paged_setup(lens, Hkv, Dh, BS, seed=5)
+    B, W = len(lens), (Hq + 2 * Hkv) * Dh
+    g = torch.Generator().manual_seed(6)
+    if src == "slabs":
+        part = ops.Partial(torch.randn(3, B, W, generator=g).to(DEV), torch.randn(W, generator=g).to(DEV) * 0.1)
+    else:
+        part = ops.Partial(torch.randn(B, W, generator=g).to(torch.bfloat16).to(DEV))
+    pos = torch.tensor([l - 1 for l in lens], dtype=torch.int32, device=DEV)
+    slots = torch.tensor([int(bt[i, (l - 1) // BS]) * BS + (l - 1) % BS for i, l in enumerate(lens)],
+                         dtype=torch.int32, device=DEV)
+    slots[-1] = -1                                   # padded graph row: no append
+    sl = torch.tensor(lens, dtype=torch.int32, device=DEV)
+    cs = ops.rope_cos_sin(4096, Dh, 500000.0, DEV)
+    outs = []
+    saved = ops.FUSED_DECODE_ROPE
+    for fused in (False, True):
+        k, v = kc.clone().to(DEV), vc.clone().to(DEV)
+        ops.FUSED_DECODE_ROPE = fused
+        try:
+            o = ops.attn_decode_rope(part, pos, slots, cs, Hq, Hkv, Dh, Dh, 0, k, v, bt.to(DEV), sl, 0.088, 4096)
+        finally:
+            ops.FUSED_DECODE_ROPE = saved
+        outs.append((o.float().cpu(), k.cpu(), v.cpu()))
+    (o0, k0, v0), (o1, k1, v1) = outs
+    assert torch.equal(k0, k1) and torch.equal(v0, v1)
+    assert (o0 - o1).abs().max().item() < 1e-2
+
+
 def test_attn_decode_batch1_long():
     Hq, Hkv, Dh, BS = 32, 8, 128, 32
     lens = [3000]
