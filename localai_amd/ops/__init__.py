@@ -427,8 +427,10 @@ def blas_tuning_start(path: Optional[str] = None) -> bool:
     if path is None:
         root = os.environ.get("LOCALAI_AMD_CACHE") or os.path.join(os.path.expanduser("~"), ".cache", "localai_amd")
         os.makedirs(root, exist_ok=True)
-        name = torch.cuda.get_device_properties(torch.cuda.current_device()).gcnArchName.split(":")[0]
-        path = os.path.join(root, f"tunableop_{name}.csv")
+        dev = torch.cuda.current_device()
+        name = torch.cuda.get_device_properties(dev).gcnArchName.split(":")[0]
+        # one file per device: data-parallel ranks on one node tune (and write) concurrently
+        path = os.path.join(root, f"tunableop_{name}_dev{dev}.csv")
     tn.enable(True)
     tn.set_filename(path)
     if os.path.exists(path):

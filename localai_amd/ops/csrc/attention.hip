@@ -36,6 +36,7 @@ namespace la {
 // Scores live in the log2 domain (scale * log2 e folded in): every exponential is one v_exp_f32.
 constexpr int DEC_T = 256;
 constexpr int DEC_MAXBT = 2048;  // block-table entries of one partition staged in LDS
+constexpr int DEC_ONE_PART = 256;  // sequences up to this many keys run as a single partition
 
 template <int DH, int GT>
 struct DecShared {
@@ -106,7 +107,7 @@ template <int DH, int GT>
 __global__ __launch_bounds__(DEC_T) void attn_decode_kernel(
     const bf16* __restrict__ q, const bf16* __restrict__ kc, const bf16* __restrict__ vc,
     const int* __restrict__ block_tables, int max_blocks, const int* __restrict__ seq_lens, int Hkv, int G,
-    int BS, float scale_log2, int PS, bf16* __restrict__ out, float* __restrict__ part_o,
+    int BS, float scale_log2, int PS_grid, bf16* __restrict__ out, float* __restrict__ part_o,
     float* __restrict__ part_ml, int P, int* __restrict__ tickets, DecRope R) {
   constexpr int KC = (DH + 31) / 32;  // 32-wide k chunks of the QK^T product
   constexpr int ND = DH / 16;         // 16-wide d tiles of the PV product
@@ -115,6 +116,11 @@ __global__ __launch_bounds__(DEC_T) void attn_decode_kernel(
   const int p = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
   const int Hq = Hkv * G;
   const int L = seq_lens[b];
+  // The grid's partitioning is fixed when a decode graph is captured (for the context bound);
+  // a short sequence takes ONE partition of DEC_ONE_PART keys instead, so it skips the split-KV
+  // merge round trip (partials + ticket + last-arriver reduction) -- worth more than the
+  // parallelism at a few hundred keys.  Decided per sequence, uniformly for its workgroups.
+  const int PS = (L <= DEC_ONE_PART && PS_grid < DEC_ONE_PART) ? DEC_ONE_PART : PS_grid;
   const int t0 = p * PS;
   if (t0 >= L) return;  // empty partition: the combiner only waits for ceil(L / PS) of them
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
