@@ -355,19 +355,24 @@ class EngineServicer:
         return r
 
     async def Rerank(self, request, context=None):
-        """Cross-scoring with the loaded LM: relevance = mean log-likelihood proxy via embeddings
-        cosine (no dedicated reranker model family yet)."""
+        """Jina rerank (reference `backend/python/rerankers/backend.py:60-95`).  A cross-encoder
+        GGUF (BERT with a RANK head) scores each (query, doc) pair; any other model falls back to
+        the cosine of its pooled embeddings (bi-encoder ranking)."""
         eng = self._require_engine()
         loop = asyncio.get_running_loop()
         docs = list(request.documents)
-        vecs = await loop.run_in_executor(None, lambda: eng.embed([request.query] + docs))
-        import math
-        q = vecs[0]
-        qn = math.sqrt(sum(x * x for x in q)) or 1.0
         scored = []
-        for i, v in enumerate(vecs[1:]):
-            vn = math.sqrt(sum(x * x for x in v)) or 1.0
-            scored.append((sum(a * b for a, b in zip(q, v)) / (qn * vn), i))
+        if getattr(eng, "is_ranker", False):
+            rel = await loop.run_in_executor(None, lambda: eng.rerank(request.query, docs))
+            scored = [(s, i) for i, s in enumerate(rel)]
+        else:
+            vecs = await loop.run_in_executor(None, lambda: eng.embed([request.query] + docs))
+            import math
+            q = vecs[0]
+            qn = math.sqrt(sum(x * x for x in q)) or 1.0
+            for i, v in enumerate(vecs[1:]):
+                vn = math.sqrt(sum(x * x for x in v)) or 1.0
+                scored.append((sum(a * b for a, b in zip(q, v)) / (qn * vn), i))
         scored.sort(reverse=True)
         top = request.top_n if request.top_n > 0 else len(scored)
         res = pb.RerankResult()

@@ -6,6 +6,11 @@ WordPiece tokenisation follows llama.cpp's WPM conventions for converted vocabul
 pieces that start a word carry a leading U+2581, continuation pieces are stored bare);
 encoder = post-LayerNorm transformer with bidirectional attention; pooling mean (default) or
 CLS, L2-normalised.
+
+Cross-encoder rerankers (llama.cpp pooling_type 4 = RANK; `cls.weight`/`cls.bias` dense + tanh,
+then `cls.output.weight`/`cls.output.bias` to one logit) score "[CLS] query [SEP] doc [SEP]"
+pairs with segment ids 0/1: the reference's `rerankers` Python backend
+(`backend/python/rerankers/backend.py:60-95`, Jina `/v1/rerank`) on this engine.
 """
 from __future__ import annotations
 
@@ -107,7 +112,7 @@ class BertEmbedder:
         self.heads = int(kv[f"{a}.attention.head_count"])
         self.eps = float(kv.get(f"{a}.attention.layer_norm_epsilon", 1e-12))
         self.max_pos = int(kv.get(f"{a}.context_length", 512))
-        self.pooling = int(kv.get(f"{a}.pooling_type", 1))  # 1 mean, 2 cls
+        self.pooling = int(kv.get(f"{a}.pooling_type", 1))  # 1 mean, 2 cls, 4 rank
         toks = [t if isinstance(t, str) else t.decode("utf-8", "replace") for t in kv["tokenizer.ggml.tokens"]]
 
         def tid(name, default):
@@ -144,21 +149,32 @@ class BertEmbedder:
                 up=t(b + "ffn_up.weight", mm=True), up_b=t(b + "ffn_up.bias"),
                 down=t(b + "ffn_down.weight", mm=True), down_b=t(b + "ffn_down.bias"),
                 ln2=(t(b + "layer_output_norm.weight"), t(b + "layer_output_norm.bias"))))
+        # classification head of a cross-encoder (absent in sentence-embedding models)
+        self.cls_w, self.cls_b = t("cls.weight", False), t("cls.bias", False)
+        self.cls_out_w, self.cls_out_b = t("cls.output.weight", False), t("cls.output.bias", False)
         self.busy = False
         self.last_request_stats = {}
 
     def tokenize(self, text: str, add_bos=None) -> List[int]:
         return self.tok.encode(text)
 
+    @property
+    def is_ranker(self) -> bool:
+        return self.cls_out_w is not None
+
     @torch.inference_mode()
-    def _encode(self, ids: List[int]) -> torch.Tensor:
+    def _hidden(self, ids: List[int], types: Optional[List[int]] = None) -> torch.Tensor:
         ids = ids[: self.max_pos]
         n = len(ids)
         D, H = self.dim, self.heads
         it = torch.tensor(ids, dtype=torch.long, device=self.device)
         x = self.tok_emb[it] + self.pos_emb[:n]
         if self.type_emb is not None:
-            x = x + self.type_emb[0]
+            if types is not None and self.type_emb.shape[0] > 1:
+                tt = torch.tensor(types[:n], dtype=torch.long, device=self.device)
+                x = x + self.type_emb[tt]
+            else:
+                x = x + self.type_emb[0]
         x = F.layer_norm(x, (D,), self.emb_ln[0], self.emb_ln[1], self.eps)
         for ly in self.layers:
             qkv = (x.to(self.mmdt) @ ly["qkv"].t()).float() + ly["qkv_b"]
@@ -169,8 +185,35 @@ class BertEmbedder:
             h = F.gelu((x.to(self.mmdt) @ ly["up"].t()).float() + ly["up_b"])
             h = (h.to(self.mmdt) @ ly["down"].t()).float() + ly["down_b"]
             x = F.layer_norm(x + h, (D,), ly["ln2"][0], ly["ln2"][1], self.eps)
-        v = x[0] if self.pooling == 2 else x.mean(0)
+        return x
+
+    def _encode(self, ids: List[int]) -> torch.Tensor:
+        x = self._hidden(ids)
+        v = x[0] if self.pooling in (2, 4) else x.mean(0)
         return F.normalize(v, dim=0)
+
+    @torch.inference_mode()
+    def score(self, query: str, doc: str) -> float:
+        """Cross-encoder relevance logit of (query, doc): CLS -> tanh(dense) -> 1 logit."""
+        if not self.is_ranker:
+            raise RuntimeError("this BERT model has no classification head (cls.output.weight)")
+        q = self.tok.encode(query)                     # [CLS] q [SEP]
+        d = self.tok.encode(doc, add_special=False) + [self.tok.sep]
+        ids = q + d
+        types = [0] * len(q) + [1] * len(d)
+        c = self._hidden(ids, types)[0]
+        if self.cls_w is not None:
+            c = torch.tanh(c @ self.cls_w.t() + (self.cls_b if self.cls_b is not None else 0))
+        y = c @ self.cls_out_w.t()
+        if self.cls_out_b is not None:
+            y = y + self.cls_out_b
+        return float(y.reshape(-1)[0])
+
+    def rerank(self, query: str, docs: Sequence[str]) -> List[float]:
+        """Relevance in (0, 1) per document: sigmoid of the cross-encoder logit (the
+        single-label CrossEncoder convention of sentence-transformers/rerankers)."""
+        import math
+        return [1.0 / (1.0 + math.exp(-self.score(query, d))) for d in docs]
 
     def embed(self, texts: Sequence, pool: str = "mean", timeout: float = 600.0) -> List[List[float]]:
         out = []

@@ -341,9 +341,10 @@ def write_mmproj(path: str, out_dim: int, dim: int = 1024, n_layer: int = 23, he
 
 
 def write_bert(path: str, dim: int = 384, n_layer: int = 6, heads: int = 12, ffn: int = 1536, ctx: int = 512,
-               seed: int = 0, std: float = 0.05, words: Optional[List[str]] = None) -> str:
+               seed: int = 0, std: float = 0.05, words: Optional[List[str]] = None, ranker: bool = False) -> str:
     """Random-init llama.cpp-style `bert` GGUF (all-MiniLM-L6-v2 geometry by default) with a small
-    WordPiece vocabulary (specials, U+2581-prefixed word pieces, bare continuation pieces)."""
+    WordPiece vocabulary (specials, U+2581-prefixed word pieces, bare continuation pieces).
+    ranker=True writes a cross-encoder (pooling_type 4 = RANK, cls / cls.output head)."""
     words = words or ("the a an of to and in is it that for on with as was at by be this are from or have "
                       "model server token request graph kernel memory stream batch hello world image text "
                       "quick brown fox dog cat red green blue gpu fast slow").split()
@@ -361,7 +362,7 @@ def write_bert(path: str, dim: int = 384, n_layer: int = 6, heads: int = 12, ffn
     w.add_uint32("bert.attention.head_count", heads)
     w.add_float32("bert.attention.layer_norm_epsilon", 1e-12)
     w.add_bool("bert.attention.causal", False)
-    w.add_uint32("bert.pooling_type", 1)
+    w.add_uint32("bert.pooling_type", 4 if ranker else 1)
     w.add_string("tokenizer.ggml.model", "bert")
     w.add_array("tokenizer.ggml.tokens", toks, GGUFValueType.STRING)
     w.add_array("tokenizer.ggml.token_type", [3] * 5 + [1] * (len(toks) - 5), GGUFValueType.INT32)
@@ -381,6 +382,9 @@ def write_bert(path: str, dim: int = 384, n_layer: int = 6, heads: int = 12, ffn
                     (b + "ffn_up.weight", (ffn, dim)), (b + "ffn_up.bias", (ffn,)),
                     (b + "ffn_down.weight", (dim, ffn)), (b + "ffn_down.bias", (dim,)),
                     (b + "layer_output_norm.weight", (dim,)), (b + "layer_output_norm.bias", (dim,))]
+    if ranker:
+        tensors += [("cls.weight", (dim, dim)), ("cls.bias", (dim,)), ("cls.output.weight", (1, dim)),
+                    ("cls.output.bias", (1,))]
     for name, shape in tensors:
         n = int(np.prod(shape))
         if name.endswith("norm.weight"):
