@@ -175,6 +175,8 @@ class LLMEngine:
         for L in m.layers:
             for w in L.qkv + L.gate_up + [L.wo] + ([L.down] if L.down is not None else []):
                 w.materialize_bf16()
+            ops.fuse_bf16(L.qkv)       # one library GEMM for a mixed-format q|k + v
+            ops.fuse_bf16(L.gate_up)
             if L.experts:
                 for gu, d in L.experts:
                     for w in gu + [d]:

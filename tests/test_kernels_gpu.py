@@ -184,6 +184,22 @@ def test_linear_multi_mixed_formats(M):
     assert (y - ref).abs().max().item() < 5e-2
 
 
+def test_fused_bf16_library_path():
+    """q|k (Q4_K) + v (Q6_K) behind one bf16 matrix: one library GEMM, same result, and the
+    per-weight bf16 copies become row slices of the fused buffer."""
+    K = 512
+    ws = [_qw(256, K, GGMLType.Q4_K, seed=7), _qw(128, K, GGMLType.Q6_K, seed=8)]
+    x = torch.randn(300, K, device=DEV).to(torch.bfloat16)
+    sep = ops.linear_multi(x, ws, force="blas").dense().cpu()
+    fused = ops.fuse_bf16(ws)
+    assert fused.shape == (384, K)
+    assert ws[1].materialize_bf16().data_ptr() == fused.data_ptr() + 256 * K * 2
+    one = ops.linear_multi(x, ws, force="blas").dense().cpu()
+    assert (one - sep).abs().max().item() < 1e-2
+    ref = torch.cat([x.float().cpu() @ w.ref.t() for w in ws], -1)
+    assert (one - ref).abs().max().item() < 5e-2
+
+
 def test_dequant_and_large_m_linear():
     w = _qw(256, 512, GGMLType.Q4_K, seed=1)
     wb = w.materialize_bf16().float().cpu()
