@@ -20,6 +20,7 @@ struct SampleRow {
 };
 
 constexpr int SMP_T = 1024;
+constexpr int SMP_BATCH = 8;  // float4 loads in flight per thread in the argmax scan
 constexpr int CAP = 1024;
 
 LA_DEV uint32_t fkey(float f) {  // order-preserving float -> uint
@@ -134,21 +135,29 @@ __global__ __launch_bounds__(SMP_T) void sample_kernel(const float* __restrict__
   const float* row = logits + (long)b * ld;
   const SampleRow P = params[b];
 
-  // max / argmax: 16-byte loads when the row is aligned (4x fewer dependent iterations over a
-  // 128k vocabulary: the greedy path is one workgroup per row, so this loop IS its latency)
+  // max / argmax: 16-byte loads when the row is aligned, SMP_BATCH of them issued before the
+  // first compare (clamped indices, never branched on, so they all stay in flight): a 128k
+  // vocabulary is 4 HBM round trips per thread instead of 16 -- the greedy path is one
+  // workgroup per row, so this loop IS its latency.  Clamped duplicates re-read element
+  // V4-1 with its own index, which cannot change the (value, lowest index) result.
   float mv = -INFINITY;
   int mi = 0x7fffffff;
   int i0 = 0;
   if ((((uintptr_t)row) & 15) == 0) {
     const int V4 = V >> 2;
     const float4* row4 = (const float4*)row;
-#pragma unroll 2
-    for (int j = threadIdx.x; j < V4; j += SMP_T) {
-      const float4 v = row4[j];
-      if (v.x > mv) { mv = v.x; mi = 4 * j; }
-      if (v.y > mv) { mv = v.y; mi = 4 * j + 1; }
-      if (v.z > mv) { mv = v.z; mi = 4 * j + 2; }
-      if (v.w > mv) { mv = v.w; mi = 4 * j + 3; }
+    for (int j0 = threadIdx.x; j0 < V4; j0 += SMP_BATCH * SMP_T) {
+      float4 v[SMP_BATCH];
+#pragma unroll
+      for (int k = 0; k < SMP_BATCH; ++k) v[k] = row4[min(j0 + k * SMP_T, V4 - 1)];
+#pragma unroll
+      for (int k = 0; k < SMP_BATCH; ++k) {
+        const int j = min(j0 + k * SMP_T, V4 - 1);
+        if (v[k].x > mv) { mv = v[k].x; mi = 4 * j; }
+        if (v[k].y > mv) { mv = v[k].y; mi = 4 * j + 1; }
+        if (v[k].z > mv) { mv = v[k].z; mi = 4 * j + 2; }
+        if (v[k].w > mv) { mv = v[k].w; mi = 4 * j + 3; }
+      }
     }
     i0 = V4 << 2;
   }

@@ -374,6 +374,24 @@ def test_sample_greedy():
     assert torch.equal(t.cpu().long(), l.argmax(-1).cpu())
 
 
+@pytest.mark.parametrize("V", [128256, 32003, 4099])
+def test_sample_greedy_ties_and_tails(V):
+    """Batched argmax loads (clamped tail indices): ties resolve to the lowest index, and the
+    maximum may sit in the last float4 or in the unaligned scalar tail."""
+    B = 4
+    l = torch.randn(B, V, device=DEV)
+    l[0, 17] = l[0, V - 1] = 50.0          # tie: lowest index wins
+    l[1, V - 1] = 60.0                     # max in the clamped last element
+    l[2, (V // 4) * 4 - 1] = 70.0          # max in the last aligned float4
+    t = ops.sample(l, _params(B)).cpu().long()
+    assert t.tolist()[:3] == [17, V - 1, (V // 4) * 4 - 1]
+    assert int(t[3]) == int(l[3].argmax())
+    # unaligned row base (ld odd): scalar path only
+    l2 = torch.randn(2, V + 1, device=DEV)[:, 1:]
+    t2 = ops.sample(l2, _params(2)).cpu().long()
+    assert torch.equal(t2, l2.argmax(-1).cpu())
+
+
 def test_sample_topk1_equals_greedy():
     B, V = 4, 32000
     l = torch.randn(B, V, device=DEV)
