@@ -72,6 +72,69 @@ LA_DEV void block_argmax(float& v, int& i, SmpShared& sh) {
     if (sh.fred[k] > v || (sh.fred[k] == v && sh.ired[k] < i)) { v = sh.fred[k]; i = sh.ired[k]; }
 }
 
+// f(value, index) over one logits row, every element once, increasing index per thread.
+// Aligned rows stream float4s with SMP_BATCH loads in flight per thread (clamped indices,
+// masked calls): each full pass over a 128k vocabulary is then 4 memory round trips per
+// thread, not 125 dependent scalar loads -- the sampler makes up to ~10 such passes.
+template <typename F>
+LA_DEV void row_foreach(const float* row, int V, F&& f) {
+  int i0 = 0;
+  if ((((uintptr_t)row) & 15) == 0) {
+    const int V4 = V >> 2;
+    const float4* row4 = (const float4*)row;
+    for (int j0 = threadIdx.x; j0 < V4; j0 += SMP_BATCH * SMP_T) {
+      float4 v[SMP_BATCH];
+#pragma unroll
+      for (int k = 0; k < SMP_BATCH; ++k) v[k] = row4[min(j0 + k * SMP_T, V4 - 1)];
+#pragma unroll
+      for (int k = 0; k < SMP_BATCH; ++k) {
+        const int j = j0 + k * SMP_T;
+        if (j < V4) { f(v[k].x, 4 * j); f(v[k].y, 4 * j + 1); f(v[k].z, 4 * j + 2); f(v[k].w, 4 * j + 3); }
+      }
+    }
+    i0 = V4 << 2;
+  }
+  for (int i = i0 + threadIdx.x; i < V; i += SMP_T) f(row[i], i);
+}
+
+// f(value, index) over row[lo, hi) in order (one thread's contiguous chunk), 8 loads in flight;
+// f returns false to stop early.
+template <typename F>
+LA_DEV void chunk_foreach(const float* row, int lo, int hi, F&& f) {
+  for (int i0 = lo; i0 < hi; i0 += 8) {
+    float r[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) r[k] = row[min(i0 + k, hi - 1)];
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (i0 + k < hi && !f(r[k], i0 + k)) return;
+  }
+}
+
+// exclusive prefix sum over the block (thread order); total -> *tot
+LA_DEV float block_excl_scan(float v, SmpShared& sh, float* tot) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  __syncthreads();
+  if (lane == 63) sh.fred[w] = x;
+  __syncthreads();
+  float base = 0.f, t = 0.f;
+#pragma unroll
+  for (int k = 0; k < SMP_T / 64; ++k) {
+    const float c = sh.fred[k];
+    if (k < w) base += c;
+    t += c;
+  }
+  __syncthreads();
+  *tot = t;
+  return base + x - v;
+}
+
 // k-th largest key (1-based) among row keys via 4-pass 8-bit radix select
 LA_DEV uint32_t radix_kth(const float* row, int V, int k, SmpShared& sh) {
   uint32_t prefix = 0, mask = 0;
@@ -79,19 +142,38 @@ LA_DEV uint32_t radix_kth(const float* row, int V, int k, SmpShared& sh) {
   for (int shift = 24; shift >= 0; shift -= 8) {
     for (int i = threadIdx.x; i < 256; i += SMP_T) sh.hist[i] = 0;
     __syncthreads();
-    for (int i = threadIdx.x; i < V; i += SMP_T) {
-      const uint32_t key = fkey(row[i]);
+    row_foreach(row, V, [&](float v, int) {
+      const uint32_t key = fkey(v);
       if ((key & mask) == prefix) atomicAdd(&sh.hist[(key >> shift) & 255u], 1u);
-    }
+    });
     __syncthreads();
-    if (threadIdx.x == 0) {
-      int acc = 0, d = 255;
-      for (; d > 0; --d) {
-        if (acc + (int)sh.hist[d] >= kleft) break;
-        acc += sh.hist[d];
+    if (threadIdx.x < 64) {
+      // digit search from 255 down, one wave: lane l owns digits 255-4l .. 252-4l, a lane
+      // prefix scan gives each lane the count above its digits, and the first lane whose
+      // running count reaches kleft walks its 4 digits (same answer as a serial scan that
+      // stops at digit 0)
+      const int l = threadIdx.x;
+      int c4[4], own = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) { c4[q] = (int)sh.hist[255 - 4 * l - q]; own += c4[q]; }
+      int inc = own;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(inc, o, 64);
+        if (l >= o) inc += y;
       }
-      sh.kleft = kleft - acc;
-      sh.prefix = prefix | ((uint32_t)d << shift);
+      const unsigned long long hit = __ballot(inc >= kleft);
+      const int L = hit ? (__ffsll((long long)hit) - 1) : 63;
+      if (l == L) {
+        int acc = inc - own, d = 255 - 4 * l;
+#pragma unroll
+        for (int q = 0; q < 4; ++q, --d) {
+          if (d == 0 || acc + c4[q] >= kleft) break;
+          acc += c4[q];
+        }
+        sh.kleft = kleft - acc;
+        sh.prefix = prefix | ((uint32_t)d << shift);
+      }
     }
     __syncthreads();
     prefix = sh.prefix;
@@ -178,37 +260,31 @@ __global__ __launch_bounds__(SMP_T) void sample_kernel(const float* __restrict__
     // temperature, then keep p >= 2^-mu (prefix of the sorted list), renormalise, sample
     const float invT = 1.f / P.temp;
     float z = 0.f;
-    for (int i = threadIdx.x; i < V; i += SMP_T) z += __expf((row[i] - mv) * invT);
+    row_foreach(row, V, [&](float v, int) { z += __expf((v - mv) * invT); });
     z = block_sum<SMP_T>(z, sh.fred);
     const float m = mu[b];
     const float thr = exp2f(-m) * z;  // unnormalised mass threshold
-    // contiguous chunk per thread for an ordered prefix scan
+    // contiguous chunk per thread (row is L2-resident by now) for an ordered prefix scan
     const int C = (V + SMP_T - 1) / SMP_T;
     const int lo = threadIdx.x * C, hi = min(V, lo + C);
     float part = 0.f;
-    for (int i = lo; i < hi; ++i) {
-      const float e = __expf((row[i] - mv) * invT);
+    chunk_foreach(row, lo, hi, [&](float v, int i) {
+      const float e = __expf((v - mv) * invT);
       if (e >= thr || i == mi) part += e;
-    }
-    sh.scan[threadIdx.x] = part;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      float acc = 0.f;
-      for (int i = 0; i < SMP_T; ++i) { const float t = sh.scan[i]; sh.scan[i] = acc; acc += t; }
-      sh.fred[0] = acc;
-      sh.sel = mi;
-    }
-    __syncthreads();
-    const float zk = sh.fred[0];
+      return true;
+    });
+    if (threadIdx.x == 0) sh.sel = mi;
+    float zk;
+    float acc = block_excl_scan(part, sh, &zk);
     const float target = u01 * zk;
-    float acc = sh.scan[threadIdx.x];
     if (target >= acc && target < acc + part) {
-      for (int i = lo; i < hi; ++i) {
-        const float e = __expf((row[i] - mv) * invT);
-        if (!(e >= thr || i == mi)) continue;
+      chunk_foreach(row, lo, hi, [&](float v, int i) {
+        const float e = __expf((v - mv) * invT);
+        if (!(e >= thr || i == mi)) return true;
         acc += e;
-        if (target < acc) { sh.sel = i; break; }
-      }
+        if (target < acc) { sh.sel = i; return false; }
+        return true;
+      });
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -230,32 +306,30 @@ __global__ __launch_bounds__(SMP_T) void sample_kernel(const float* __restrict__
   // Z over the top-k set (top_p normalisation in llama.cpp is over the post-top-k list)
   float zk = 0.f;
   int cnt = 0;
-  for (int i = threadIdx.x; i < V; i += SMP_T) {
-    const float v = row[i];
-    if (k == V || fkey(v) >= key_k) zk += __expf(v - mv);
-  }
-  zk = block_sum<SMP_T>(zk, sh.fred);
   float thr = -INFINITY;
   if (P.min_p > 0.f && P.min_p <= 1.f) thr = mv + logf(P.min_p);
-  // count candidates; if > CAP raise the threshold to the CAP-th largest
-  for (int i = threadIdx.x; i < V; i += SMP_T) {
-    const float v = row[i];
-    if ((k == V || fkey(v) >= key_k) && v >= thr) ++cnt;
-  }
+  // Z over the top-k set, and the candidate count (if > CAP the threshold rises to the
+  // CAP-th largest) in one pass
+  row_foreach(row, V, [&](float v, int) {
+    if (k == V || fkey(v) >= key_k) {
+      zk += __expf(v - mv);
+      if (v >= thr) ++cnt;
+    }
+  });
+  zk = block_sum<SMP_T>(zk, sh.fred);
   cnt = (int)block_sum<SMP_T>((float)cnt, sh.fred);
   uint32_t key_c = 0;
   bool capped = false;
   if (cnt > CAP) { key_c = radix_kth(row, V, CAP, sh); capped = true; }
   if (threadIdx.x == 0) sh.count = 0;
   __syncthreads();
-  for (int i = threadIdx.x; i < V; i += SMP_T) {
-    const float v = row[i];
+  row_foreach(row, V, [&](float v, int i) {
     const uint32_t kk = fkey(v);
     if ((k == V || kk >= key_k) && v >= thr && (!capped || kk >= key_c)) {
       const int slot = atomicAdd(&sh.count, 1);
       if (slot < CAP) { sh.cval[slot] = v; sh.cidx[slot] = i; }
     }
-  }
+  });
   __syncthreads();
   int n = min(sh.count, CAP);
   block_sort_desc(sh, n);
