@@ -62,8 +62,27 @@ static void json_escape_append(std::string& out, const char* s, size_t n) {
           out += "\\u00";
           out += hex[c >> 4];
           out += hex[c & 15];
-        } else {
+        } else if (c < 0x80) {
           out += static_cast<char>(c);
+        } else {
+          // a random-init (or byte-fallback) model can emit byte tokens that never complete a
+          // UTF-8 sequence; JSON must stay valid UTF-8, so such bytes become U+FFFD
+          const size_t len = c >= 0xF0 && c < 0xF5 ? 4 : c >= 0xE0 ? (c < 0xF0 ? 3 : 0) : c >= 0xC2 ? 2 : 0;
+          bool ok = len != 0 && i + len <= n;
+          for (size_t k = 1; ok && k < len; ++k) ok = (static_cast<unsigned char>(s[i + k]) & 0xC0) == 0x80;
+          if (ok && len >= 3) {
+            const unsigned char c1 = static_cast<unsigned char>(s[i + 1]);
+            if (c == 0xE0 && c1 < 0xA0) ok = false;       // overlong
+            if (c == 0xED && c1 >= 0xA0) ok = false;      // surrogate
+            if (c == 0xF0 && c1 < 0x90) ok = false;       // overlong
+            if (c == 0xF4 && c1 >= 0x90) ok = false;      // > U+10FFFF
+          }
+          if (ok) {
+            out.append(s + i, len);
+            i += len - 1;
+          } else {
+            out += "\xEF\xBF\xBD";
+          }
         }
     }
   }

@@ -153,3 +153,21 @@ def test_emit_run_matches_python_semantics():
     assert texts[2] is None or texts[2] == b"Hel"
     assert texts[3] == b"Hello wor"
     assert texts[4] == b"Hello world"
+
+
+def test_json_escape_keeps_output_valid_utf8():
+    """SSE chunks are built in C++ from raw token bytes; dangling or malformed UTF-8 (byte-fallback
+    tokens that never complete a code point) must become U+FFFD so every chunk parses as JSON."""
+    import json
+
+    def esc(raw):
+        out = core.json_escape(raw)
+        return out if isinstance(out, bytes) else out.encode("utf-8", "surrogateescape")
+
+    for raw in [b"plain \"q\" \\ \n\t\x01", "h\u00e9llo \u20ac \U0001d11e".encode()]:
+        assert json.loads(b'"' + esc(raw) + b'"') == raw.decode()
+    for raw in [b"\xdf(", b"ab\xe2\x82", b"\xc0\xaf", b"\xed\xa0\x80", b"\xf4\x90\x80\x80", b"\xff", b"\x80x"]:
+        out = esc(raw)
+        out.decode("utf-8")  # strict: valid UTF-8
+        s = json.loads(b'"' + out + b'"')
+        assert "\ufffd" in s and s.replace("\ufffd", "") == raw.decode("utf-8", "ignore")
