@@ -42,9 +42,9 @@ def _page(title: str, body: str, script: str = "") -> HTMLResponse:
                         f"<script>{script}</script></body></html>")
 
 
-def _model_select(models, selected: str) -> str:
+def _model_select(models, selected: str, id_: str = "model") -> str:
     opts = "".join(f"<option{' selected' if m == selected else ''}>{html.escape(m)}</option>" for m in models)
-    return f"<select id='model'>{opts}</select>"
+    return f"<select id='{id_}'>{opts}</select>"
 
 
 _AUTH_JS = """
@@ -121,6 +121,42 @@ async function gen(){
   if(!r.ok){st.textContent = 'error: ' + r.status + ' ' + await r.text(); return;}
   const j = await r.json(); st.textContent = '';
   document.getElementById('img').src = 'data:image/png;base64,' + j.data[0].b64_json;
+}
+"""
+
+_TALK_JS = _AUTH_JS + """
+// push-to-talk loop of the reference's /talk page (core/http/routes/ui.go talk route):
+// microphone -> /v1/audio/transcriptions -> /v1/chat/completions -> /tts -> playback
+let rec = null, chunks = [], history = [];
+function val(id){ return document.getElementById(id).value; }
+async function toggle(){
+  const st = document.getElementById('st'), b = document.getElementById('rec');
+  if(rec){ rec.stop(); b.textContent = 'Record'; return; }
+  const stream = await navigator.mediaDevices.getUserMedia({audio:true});
+  rec = new MediaRecorder(stream); chunks = [];
+  rec.ondataavailable = e => chunks.push(e.data);
+  rec.onstop = async () => {
+    rec = null; stream.getTracks().forEach(t => t.stop());
+    st.textContent = 'transcribing...';
+    const fd = new FormData(); fd.append('file', new Blob(chunks, {type:'audio/webm'}), 'talk.webm');
+    fd.append('model', val('whisper'));
+    const h = hdrs(); delete h['Content-Type'];
+    const tr = await fetch('/v1/audio/transcriptions', {method:'POST', headers:h, body:fd});
+    if(!tr.ok){ st.textContent = 'transcription error: ' + tr.status; return; }
+    const text = (await tr.json()).text || '';
+    history.push({role:'user', content:text}); st.textContent = 'you: ' + text + ' / thinking...';
+    const cr = await fetch('/v1/chat/completions', {method:'POST', headers:hdrs(), body: JSON.stringify({
+      model: val('model'), messages: history})});
+    if(!cr.ok){ st.textContent = 'chat error: ' + cr.status; return; }
+    const reply = (await cr.json()).choices[0].message.content || '';
+    history.push({role:'assistant', content:reply});
+    document.getElementById('log').textContent += '> ' + text + '\\n' + reply + '\\n';
+    const sp = await fetch('/tts', {method:'POST', headers:hdrs(), body: JSON.stringify({model: val('tts'), input: reply})});
+    if(!sp.ok){ st.textContent = 'tts error: ' + sp.status; return; }
+    const a = document.getElementById('audio'); a.src = URL.createObjectURL(await sp.blob()); a.play();
+    st.textContent = '';
+  };
+  rec.start(); b.textContent = 'Stop';
 }
 """
 
@@ -205,6 +241,15 @@ def build_router(state) -> APIRouter:
     async def text2image_model(model: str):
         return await text2image(model)
 
+    async def talk():
+        ms = models()
+        first = ms[0] if ms else ""
+        sel = [_model_select(ms, first, k) for k in ("model", "whisper", "tts")]
+        body = ("<h2>Talk</h2><div class=row><label>LLM</label>" + sel[0] + "<label>whisper</label>" + sel[1]
+                + "<label>tts</label>" + sel[2] + "</div><div class=row><button id=rec onclick='toggle()'>Record"
+                "</button></div><pre id=log></pre><audio id=audio controls></audio><div id=st class=muted></div>")
+        return _page("Talk", body, _TALK_JS)
+
     r.add_api_route("/", home, methods=["GET"])
     if not state.cfg.disable_webui:
         r.add_api_route("/browse", browse, methods=["GET"])
@@ -214,5 +259,6 @@ def build_router(state) -> APIRouter:
         r.add_api_route("/tts/{model}", tts_model, methods=["GET"])
         r.add_api_route("/text2image/", text2image, methods=["GET"])
         r.add_api_route("/text2image/{model}", text2image_model, methods=["GET"])
+        r.add_api_route("/talk/", talk, methods=["GET"])
     return r
 

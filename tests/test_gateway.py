@@ -84,7 +84,7 @@ def test_web_ui_pages(client):
     assert client.model_name in w["models"]
     page = client.get("/", headers={"accept": "text/html"})
     assert page.status_code == 200 and "Installed models" in page.text and client.model_name in page.text
-    for path in ("/chat/", f"/chat/{client.model_name}", "/tts/", "/text2image/", "/browse"):
+    for path in ("/chat/", f"/chat/{client.model_name}", "/tts/", "/text2image/", "/browse", "/talk/"):
         r = client.get(path, headers={"accept": "text/html"})
         assert r.status_code == 200, path
         assert "<main>" in r.text
