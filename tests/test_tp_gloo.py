@@ -46,7 +46,23 @@ def _worker(rank, world, port, path, q):
         dist.destroy_process_group()
 
 
-def test_tp2_leader_follower(tiny_model_path):
+import pytest
+
+
+@pytest.fixture(params=["tiny-llama", "tiny-mixtral", "tiny-phi2"])
+def tp_model_path(request, tiny_model_path, tmp_path_factory):
+    """Llama (dense GQA), Mixtral (TP-within-expert: every expert's F sharded, router replicated)
+    and Phi-2 (LayerNorm + biases, NEOX partial rotary, biases added once after the all-reduce)."""
+    if request.param == "tiny-llama":
+        return tiny_model_path
+    from localai_amd.models import synth
+    p = tmp_path_factory.mktemp("tp") / f"{request.param}.gguf"
+    synth.write_model(str(p), request.param, exact=True)
+    return str(p)
+
+
+def test_tp2_leader_follower(tp_model_path):
+    tiny_model_path = tp_model_path
     from localai_amd.engine.llm_engine import EngineConfig, LLMEngine
     from localai_amd.engine.sampling_params import SamplingParams
     single = LLMEngine(EngineConfig(model_path=tiny_model_path, device="cpu", context_size=256, max_num_seqs=4,
