@@ -82,9 +82,14 @@ __global__ __launch_bounds__(NT) void add_norm_kernel(float* __restrict__ residu
   const int nv = D >> 2;
   float* rrow = residual + (long)t * D;
   float v[IT][4];
+  // the norm weight/bias loads do not depend on the reduction: issue them with the row loads so
+  // their HBM round trip overlaps the residual/slab fetch instead of following the block barrier
+  float4 ww[IT], bb[IT];
 #pragma unroll
   for (int i = 0; i < IT; ++i) {
     const int c = min(threadIdx.x + i * NT, nv - 1);  // clamped: loads never branch
+    ww[i] = out ? *(const float4*)(w + 4 * c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    bb[i] = b ? *(const float4*)(b + 4 * c) : make_float4(0.f, 0.f, 0.f, 0.f);
     const float4 r = *(const float4*)(rrow + 4 * c);
     v[i][0] = r.x; v[i][1] = r.y; v[i][2] = r.z; v[i][3] = r.w;
     if (has_add) {
@@ -125,11 +130,8 @@ __global__ __launch_bounds__(NT) void add_norm_kernel(float* __restrict__ residu
   for (int i = 0; i < IT; ++i) {
     const int c = threadIdx.x + i * NT;
     if (c < nv) {
-      const float4 ww = *(const float4*)(w + 4 * c);
-      float4 bb = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (b) bb = *(const float4*)(b + 4 * c);
-      float o[4] = {(v[i][0] - mean) * rstd * ww.x + bb.x, (v[i][1] - mean) * rstd * ww.y + bb.y,
-                    (v[i][2] - mean) * rstd * ww.z + bb.z, (v[i][3] - mean) * rstd * ww.w + bb.w};
+      float o[4] = {(v[i][0] - mean) * rstd * ww[i].x + bb[i].x, (v[i][1] - mean) * rstd * ww[i].y + bb[i].y,
+                    (v[i][2] - mean) * rstd * ww[i].z + bb[i].z, (v[i][3] - mean) * rstd * ww[i].w + bb[i].w};
       bf16x4 ob = {(bf16)o[0], (bf16)o[1], (bf16)o[2], (bf16)o[3]};
       *(bf16x4*)(out + (long)t * D + 4 * c) = ob;
       if (out_f32) *(float4*)(out_f32 + (long)t * D + 4 * c) = make_float4(o[0], o[1], o[2], o[3]);
