@@ -197,8 +197,48 @@ def cmd_transcript(a) -> int:
     return 0
 
 
+def _hf_scan(a, fetch=None) -> int:
+    """core/cli/util.go:75-110 (best effort, HuggingFace only): scan the given URIs, or with none
+    given every installed gallery model; exit 1 when a known-unsafe file is found."""
+    from .utils.downloader import UnsafeFilesFound, hf_scan
+    print("LocalAI Security Scanner - This is BEST EFFORT functionality! Currently limited to huggingface models!")
+    bad = []
+    if not a.file:
+        from .gallery import safety_scan_gallery_models
+        try:
+            galleries = json.loads(a.galleries or "[]")
+        except ValueError:
+            print("unable to load galleries")
+            galleries = []
+        try:
+            bad = safety_scan_gallery_models(galleries, a.models_path, fetch=fetch)
+        except Exception as e:
+            print(f"unable to list gallery models: {e}")
+            return 1
+    for uri in a.file:
+        print(f"scanning specific uri {uri}")
+        try:
+            hf_scan(uri, fetch=fetch)
+        except UnsafeFilesFound as e:
+            bad.append({"uri": uri, "clamAV": e.result["clamAVInfectedFiles"], "pickles": e.result["dangerousPickles"]})
+        except Exception as e:  # not an HF repo / scan unreachable: not a verdict (reference ignores it)
+            print(f"scan skipped for {uri}: {e}")
+    for b in bad:
+        print(f"! WARNING ! A known-vulnerable model is included: {json.dumps(b)}")
+    if not bad:
+        print("No security warnings were detected for your installed models. Please note that this is a "
+              "BEST EFFORT tool, and all issues may not be detected.")
+    return 1 if bad else 0
+
+
 def cmd_util(a) -> int:
     from .gguf import gguf_info
+    if a.action == "hf-scan":
+        return _hf_scan(a)
+    if a.file and len(a.file) != 1:
+        print(f"util {a.action}: exactly one file")
+        return 2
+    a.file = a.file[0] if a.file else ""
     if a.action == "gguf-info":
         info = gguf_info(a.file)
         print(json.dumps(info, indent=2, default=str))
@@ -263,8 +303,10 @@ def build_parser() -> argparse.ArgumentParser:
     t.add_argument("--threads", default=None)
     t.add_argument("--models-path", default=None)
     u = sub.add_parser("util")
-    u.add_argument("action", choices=["gguf-info", "usecase-heuristic"])
-    u.add_argument("file")
+    u.add_argument("action", choices=["gguf-info", "usecase-heuristic", "hf-scan"])
+    u.add_argument("file", nargs="*", help="GGUF/config file, or the URIs to scan (hf-scan)")
+    u.add_argument("--models-path", default=os.environ.get("LOCALAI_MODELS_PATH", os.environ.get("MODELS_PATH", "models")))
+    u.add_argument("--galleries", default=os.environ.get("LOCALAI_GALLERIES", os.environ.get("GALLERIES", "[]")))
     f = sub.add_parser("federated", help="request-level load balancer over LocalAI instances")
     f.add_argument("--address", default=os.environ.get("LOCALAI_ADDRESS", ":8080"))
     f.add_argument("--workers", default="", help="comma-separated worker base URLs")

@@ -271,3 +271,25 @@ class GalleryService:
 
 def new_op_id() -> str:
     return str(uuid.uuid4())
+
+
+def safety_scan_gallery_models(galleries: List[dict], base_path: str, fetch=None) -> List[dict]:
+    """core/gallery/gallery.go:242-264: scan the files of every INSTALLED gallery model with the
+    Hub's safety scan; returns one {model, uri, clamAV, pickles} record per flagged file.  Only an
+    unsafe verdict counts -- unreachable scans and non-HF URIs are skipped, as in the reference."""
+    from .utils.downloader import UnsafeFilesFound, hf_scan
+    flagged = []
+    for m in available_models(galleries, base_path):
+        if not m.installed:
+            continue
+        for f in m.files:
+            try:
+                hf_scan(f.get("uri", ""), fetch=fetch)
+            except UnsafeFilesFound as e:
+                flagged.append({"model": m.name, "uri": f.get("uri"), "clamAV": e.result["clamAVInfectedFiles"],
+                                "pickles": e.result["dangerousPickles"]})
+                break  # the reference stops at the first unsafe file of a model
+            except Exception:
+                continue
+    return flagged
+

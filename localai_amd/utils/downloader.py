@@ -133,3 +133,39 @@ def download_file(uri: str, dst: str, sha: str = "",
             raise ValueError(f"SHA mismatch for file {dst!r} ( calculated: {got} != metadata: {sha} )")
     os.replace(tmp, dst)
     return dst
+
+
+# ------------------------------------------------------------------ HuggingFace safety scan
+# pkg/downloader/huggingface.go:12-49: ask the Hub's scan API about a repository's files
+# (ClamAV + dangerous pickle imports).  Best effort, as in the reference: only huggingface URIs.
+
+class NonHuggingFaceFile(ValueError):
+    pass
+
+
+class UnsafeFilesFound(RuntimeError):
+    def __init__(self, result: dict):
+        super().__init__("unsafe files found")
+        self.result = result
+
+
+def hf_scan(uri: str, fetch: Optional[Callable[[str], bytes]] = None) -> dict:
+    """Returns the scan result ({repositoryId, revision, hasUnsafeFile, clamAVInfectedFiles,
+    dangerousPickles, scansDone}); raises UnsafeFilesFound when the Hub flags a file."""
+    import json
+    parts = resolve_url(uri).split("/")
+    if len(parts) <= 4 or parts[2] != "huggingface.co":
+        raise NonHuggingFaceFile("not a huggingface repo")
+    url = f"https://huggingface.co/api/models/{parts[3]}/{parts[4]}/scan"
+    if fetch is None:
+        def fetch(u: str) -> bytes:
+            with urllib.request.urlopen(u, timeout=30) as r:
+                if r.status != 200:
+                    raise RuntimeError(f"unexpected status code during HuggingFaceScan: {r.status}")
+                return r.read()
+    res = json.loads(fetch(url))
+    res.setdefault("clamAVInfectedFiles", [])
+    res.setdefault("dangerousPickles", [])
+    if res.get("hasUnsafeFile"):
+        raise UnsafeFilesFound(res)
+    return res
