@@ -33,7 +33,9 @@ def build_router(state) -> APIRouter:
 
     async def system():
         backends = sorted(b for b in ENGINE_BACKENDS if b) + [STORE_BACKEND] + list(state.cfg.external_grpc_backends)
-        return {"backends": backends, "loaded_models": [{"id": m.id} for m in state.manager.list_loaded()]}
+        from ..utils.sysinfo import system_info
+        return {"backends": backends, "loaded_models": [{"id": m.id} for m in state.manager.list_loaded()],
+                "system": system_info()}
 
     r.add_api_route("/system", system, methods=["GET"])
 

@@ -214,3 +214,8 @@ def test_files_and_assistants(client, tmp_path):
     assert client.delete(f"/v1/assistants/{a['id']}/files/{fid}").json()["deleted"]
     assert client.delete(f"/v1/assistants/{a['id']}").json()["deleted"]
     assert client.delete(f"/v1/files/{fid}").json()["deleted"]
+
+
+def test_system_route_reports_inventory(client):
+    j = client.get("/system").json()
+    assert "backends" in j and "cpu" in j["system"] and isinstance(j["system"]["gpus"], list)
