@@ -248,6 +248,37 @@ __global__ __launch_bounds__(256) void act_kernel(Src src, bf16* __restrict__ ou
   *(bf16x4*)(out + (long)t * F + c) = ob;
 }
 
+// bf16 source without bias (the hipBLASLt gate|up output at batch decode / prefill): 8 elements
+// per thread so every load and store is a 16-byte vector (halves the memory instructions of
+// act_kernel, which moves 4-wide 8-byte vectors)
+__global__ __launch_bounds__(256) void act8_kernel(const bf16* __restrict__ src, bf16* __restrict__ out, int F,
+                                                   int mode) {
+  const int t = blockIdx.y;
+  const int c = (blockIdx.x * blockDim.x + threadIdx.x) * 8;
+  if (c >= F) return;
+  const int W = (mode == 0) ? 2 * F : F;
+  const bf16x8 a = *(const bf16x8*)(src + (long)t * W + c);
+  bf16x8 ob;
+  if (mode == 0) {
+    const bf16x8 b = *(const bf16x8*)(src + (long)t * W + F + c);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ob[j] = (bf16)(silu((float)a[j]) * (float)b[j]);
+  } else if (mode == 1) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float x = (float)a[j];
+      ob[j] = (bf16)(0.5f * x * (1.f + tanhf(0.7978845608f * (x + 0.044715f * x * x * x))));
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float x = (float)a[j];
+      ob[j] = (bf16)(x / (1.f + __expf(-1.702f * x)));
+    }
+  }
+  *(bf16x8*)(out + (long)t * F + c) = ob;
+}
+
 // sum split-K slabs (+bias) -> f32 or bf16 matrix [T][N]
 __global__ __launch_bounds__(256) void reduce_slabs_kernel(Src src, int N, float* __restrict__ out_f32,
                                                            bf16* __restrict__ out_bf16) {
@@ -350,6 +381,12 @@ extern "C" int la_rope_kv(const void* qkv_p, long slab, int S, const void* bias,
 extern "C" int la_act(const void* p, long slab, int S, const void* bias, void* out, int T, int F, int mode,
                       void* stream) {
   if (F & 3) return -1;
+  if (S == 0 && bias == nullptr && (F & 7) == 0 && ((uintptr_t)p & 15) == 0 && ((uintptr_t)out & 15) == 0) {
+    dim3 grid((F / 8 + 255) / 256, T);
+    hipLaunchKernelGGL(la::act8_kernel, grid, dim3(256), 0, (hipStream_t)stream, (const bf16*)p, (bf16*)out, F,
+                       mode);
+    return (int)hipGetLastError();
+  }
   Src s{p, slab, S, (const float*)bias};
   dim3 grid((F / 4 + 255) / 256, T);
   hipLaunchKernelGGL(la::act_kernel, grid, dim3(256), 0, (hipStream_t)stream, s, (bf16*)out, F, mode);

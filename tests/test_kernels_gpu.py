@@ -251,6 +251,24 @@ def test_act(mode):
     assert (y.float().cpu() - yr.float()).abs().max().item() < 5e-2
 
 
+@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("F", [14336, 1032, 1028])
+def test_act_bf16_source(mode, F):
+    """bf16 GEMM output (hipBLASLt path): F % 8 == 0 takes the 16-byte act8 kernel, else 4-wide."""
+    T = 5
+    W = 2 * F if mode == 0 else F
+    x = (torch.randn(T, W, device=DEV) * 3).to(torch.bfloat16)
+    y = ops.act(ops.Partial(x), F, mode)
+    xf = x.float().cpu()
+    if mode == 0:
+        yr = torch.nn.functional.silu(xf[:, :F]) * xf[:, F:]
+    elif mode == 1:
+        yr = torch.nn.functional.gelu(xf, approximate="tanh")
+    else:
+        yr = xf * torch.sigmoid(1.702 * xf)
+    assert (y.float().cpu() - yr).abs().max().item() < 5e-2 * max(1.0, yr.abs().max().item() / 8)
+
+
 @pytest.mark.parametrize("t", [GGMLType.Q4_K, GGMLType.Q6_K, GGMLType.Q8_0])
 def test_embed(t):
     w = _qw(100, 512, t)
