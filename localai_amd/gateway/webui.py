@@ -12,6 +12,7 @@ from __future__ import annotations
 
 import html
 import time
+import urllib.parse
 
 from fastapi import APIRouter, Request
 from fastapi.responses import HTMLResponse, JSONResponse
@@ -85,9 +86,12 @@ inp.addEventListener('keydown', e => { if(e.key === 'Enter' && !e.shiftKey){ e.p
 """
 
 _BROWSE_JS = _AUTH_JS + """
-async function install(id){
+async function install(btn){
+  // gallery ids and names come from third-party indexes: they travel as data-* attribute values
+  // (HTML-escaped by the server, read back as plain strings), never as JS source
+  const id = btn.dataset.id;
   const r = await fetch('/models/apply', {method:'POST', headers:hdrs(), body: JSON.stringify({id})});
-  const j = await r.json(); const cell = document.getElementById('st-' + CSS.escape(id));
+  const j = await r.json(); const cell = btn.closest('tr').querySelector('td.st');
   if(!j.uuid){cell.textContent = 'error'; return;}
   for(;;){
     const s = await (await fetch('/models/jobs/' + j.uuid, {headers:hdrs()})).json();
@@ -95,7 +99,8 @@ async function install(id){
     if(s.processed) break; await new Promise(r => setTimeout(r, 1000));
   }
 }
-async function remove(name){
+async function remove(btn){
+  const name = btn.dataset.name;
   await fetch('/models/delete/' + encodeURIComponent(name), {method:'POST', headers:hdrs()});
   location.reload();
 }
@@ -175,7 +180,7 @@ def build_router(state) -> APIRouter:
         loaded = {m.id for m in state.manager.list_loaded()}
         rows = "".join(
             f"<tr><td>{html.escape(m)}</td><td>{'loaded' if m in loaded else ''}</td>"
-            f"<td><a href='/chat/{html.escape(m)}'>chat</a></td></tr>" for m in models())
+            f"<td><a href='/chat/{html.escape(urllib.parse.quote(m, safe=''))}'>chat</a></td></tr>" for m in models())
         body = (f"<h2>Installed models</h2><table><thead><tr><th>model</th><th>state</th><th></th></tr></thead>"
                 f"<tbody>{rows or '<tr><td colspan=3 class=muted>no models yet: install one from the gallery</td></tr>'}"
                 f"</tbody></table><p class=muted>version {html.escape(__version__)} · "
@@ -198,11 +203,12 @@ def build_router(state) -> APIRouter:
             gid = m.get("id") or f"{m.get('gallery', {}).get('name', '')}@{m.get('name', '')}"
             name = m.get("name", gid)
             key = (name + " " + " ".join(m.get("tags") or []) + " " + (m.get("description") or "")).lower()
-            act = (f"<button onclick=\"remove('{html.escape(name)}')\">delete</button>" if name in installed else
-                   f"<button onclick=\"install('{html.escape(gid)}')\">install</button>")
-            rows.append(f"<tr data-k='{html.escape(key)}'><td>{html.escape(name)}</td>"
+            act = (f"<button data-name=\"{html.escape(name)}\" onclick='remove(this)'>delete</button>"
+                   if name in installed else
+                   f"<button data-id=\"{html.escape(gid)}\" onclick='install(this)'>install</button>")
+            rows.append(f"<tr data-k=\"{html.escape(key)}\"><td>{html.escape(name)}</td>"
                         f"<td class=muted>{html.escape((m.get('description') or '')[:140])}</td>"
-                        f"<td>{act}</td><td id='st-{html.escape(gid)}'></td></tr>")
+                        f"<td>{act}</td><td class=st></td></tr>")
         body = ("<h2>Model gallery</h2><div class=row><input id=q placeholder='search' oninput='filter()'></div>"
                 + (f"<p class=muted>gallery unavailable: {html.escape(err)}</p>" if err else "")
                 + "<table><thead><tr><th>model</th><th>description</th><th></th><th>status</th></tr></thead>"

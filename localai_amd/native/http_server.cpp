@@ -108,7 +108,13 @@ struct Conn {
   bool closed = false;       // peer gone / fatal error
   bool drain_close = false;  // close once the output buffer is flushed
   bool want_out = false;     // EPOLLOUT armed
+  bool rd_closed = false;    // peer half-closed (shutdown(SHUT_WR)); answer what is buffered, then close
   std::string peer;
+  // request being received (I/O thread only): the head is parsed once and its bytes dropped from
+  // `in`; a chunked body is decoded incrementally into head.body, consumed chunks leave `in` too
+  bool have_head = false, chunked = false, expect = false, conn_close = false, sent_continue = false;
+  size_t clen = 0;
+  Request head;
 };
 
 class Server {
@@ -151,6 +157,8 @@ class Server {
 
   int port() const { return port_; }
   int notify_fd() const { return notify_; }
+  size_t max_body() const { return max_body_; }
+  void set_max_body(size_t n) { max_body_ = n; }  // before start()
 
   void start() {
     if (th_.joinable()) return;
@@ -357,13 +365,18 @@ class Server {
       c->out.append(p, n);
       if (!c->want_out) {
         c->want_out = true;
-        epoll_event ev{};
-        ev.events = EPOLLIN | EPOLLOUT | EPOLLRDHUP;
-        ev.data.u64 = c->id;
-        epoll_ctl(ep_, EPOLL_CTL_MOD, c->fd, &ev);
+        rearm(c);
       }
     }
     return true;
+  }
+
+  // caller holds c->mu: read interest until the peer half-closes, write interest while output is queued
+  void rearm(Conn* c) {
+    epoll_event ev{};
+    ev.events = (c->rd_closed ? 0u : static_cast<uint32_t>(EPOLLIN | EPOLLRDHUP)) | (c->want_out ? EPOLLOUT : 0u);
+    ev.data.u64 = c->id;
+    epoll_ctl(ep_, EPOLL_CTL_MOD, c->fd, &ev);
   }
 
   void drop(const std::shared_ptr<Conn>& c) {
@@ -404,112 +417,160 @@ class Server {
     }
   }
 
-  // Parse as many complete requests as allowed (one in flight per connection).
+  // Parse as many complete requests as allowed (one in flight per connection). The head is parsed
+  // once; a body is taken when complete. Chunked bodies are decoded incrementally (each recv only
+  // looks at new chunks) and both body kinds are held to max_body_ before they are buffered.
   void parse(const std::shared_ptr<Conn>& c) {
     for (;;) {
       {
         std::lock_guard<std::mutex> g(c->mu);
         if (c->busy || c->closed) return;
       }
-      const size_t he = c->in.find("\r\n\r\n");
-      if (he == std::string::npos) {
-        if (c->in.size() > (1u << 20)) bad(c, 431);
-        return;
-      }
-      Request r;
-      r.conn = c->id;
-      r.peer = c->peer;
-      size_t p = 0;
-      const size_t le = c->in.find("\r\n");
-      {
-        const std::string line = c->in.substr(0, le);
-        const size_t s1 = line.find(' ');
-        const size_t s2 = line.rfind(' ');
-        if (s1 == std::string::npos || s2 == s1) {
-          bad(c, 400);
-          return;
-        }
-        r.method = line.substr(0, s1);
-        r.target = line.substr(s1 + 1, s2 - s1 - 1);
-        r.version = line.substr(s2 + 1);
-      }
-      p = le + 2;
-      size_t clen = 0;
-      bool chunked = false, conn_close = (r.version == "HTTP/1.0"), expect = false;
-      while (p < he) {
-        const size_t e = c->in.find("\r\n", p);
-        const size_t colon = c->in.find(':', p);
-        if (colon != std::string::npos && colon < e) {
-          std::string k = c->in.substr(p, colon - p);
-          for (auto& ch : k) ch = static_cast<char>(tolower(ch));
-          size_t vs = colon + 1;
-          while (vs < e && (c->in[vs] == ' ' || c->in[vs] == '\t')) ++vs;
-          size_t ve = e;
-          while (ve > vs && (c->in[ve - 1] == ' ' || c->in[ve - 1] == '\t')) --ve;
-          std::string v = c->in.substr(vs, ve - vs);
-          if (k == "content-length") clen = strtoull(v.c_str(), nullptr, 10);
-          else if (k == "transfer-encoding" && v.find("chunked") != std::string::npos) chunked = true;
-          else if (k == "connection") {
-            std::string lv = v;
-            for (auto& ch : lv) ch = static_cast<char>(tolower(ch));
-            if (lv.find("close") != std::string::npos) conn_close = true;
-            if (lv.find("keep-alive") != std::string::npos) conn_close = false;
-          } else if (k == "expect") expect = true;
-          r.headers.emplace_back(std::move(k), std::move(v));
-        }
-        p = e + 2;
-      }
-      size_t body_start = he + 4, consumed = 0;
-      if (chunked) {
-        size_t q = body_start;
-        std::string body;
+      if (!c->have_head && !parse_head(c)) return;
+      if (c->chunked) {
+        size_t q = 0;
         bool complete = false;
         for (;;) {
           const size_t e = c->in.find("\r\n", q);
-          if (e == std::string::npos) break;
-          const size_t n = strtoull(c->in.substr(q, e - q).c_str(), nullptr, 16);
+          if (e == std::string::npos) {
+            if (c->in.size() - q > 4096) return bad(c, 400);  // chunk-size line without an end
+            break;
+          }
+          char* endp = nullptr;
+          const std::string line = c->in.substr(q, e - q);
+          errno = 0;
+          const unsigned long long n = strtoull(line.c_str(), &endp, 16);
+          if (endp == line.c_str() || errno == ERANGE || (*endp && *endp != ';' && *endp != ' ' && *endp != '\t'))
+            return bad(c, 400);
           if (n == 0) {
-            const size_t t = c->in.find("\r\n", e + 2);  // (no trailers supported) final CRLF
-            if (t == std::string::npos) break;
-            consumed = t + 2;
+            // last-chunk, optional trailer fields, empty line
+            size_t t;
+            if (c->in.compare(e + 2, 2, "\r\n") == 0) t = e + 4;
+            else {
+              const size_t te = c->in.find("\r\n\r\n", e + 2);
+              if (te == std::string::npos) break;
+              t = te + 4;
+            }
+            q = t;
             complete = true;
             break;
           }
-          if (c->in.size() < e + 2 + n + 2) break;
-          body.append(c->in, e + 2, n);
+          if (n > max_body_ || c->head.body.size() + n > max_body_) return bad(c, 413);
+          if (c->in.size() - (e + 2) < n + 2) break;
+          c->head.body.append(c->in, e + 2, n);
           q = e + 2 + n + 2;
         }
+        c->in.erase(0, q);
         if (!complete) {
-          if (expect) send_continue(c);
+          if (c->expect && !c->sent_continue) {
+            c->sent_continue = true;
+            send_continue(c);
+          }
           return;
         }
-        r.body = std::move(body);
       } else {
-        if (clen > max_body_) {
-          bad(c, 413);
+        if (c->in.size() < c->clen) {
+          if (c->expect && !c->sent_continue) {
+            c->sent_continue = true;
+            send_continue(c);
+          }
           return;
         }
-        if (c->in.size() < body_start + clen) {
-          if (expect) send_continue(c);
-          return;
-        }
-        r.body = c->in.substr(body_start, clen);
-        consumed = body_start + clen;
+        c->head.body = c->in.substr(0, c->clen);
+        c->in.erase(0, c->clen);
       }
-      c->in.erase(0, consumed);
+      c->have_head = false;
       {
         std::lock_guard<std::mutex> g(c->mu);
         c->busy = true;
-        c->close_after = conn_close;
+        c->close_after = c->conn_close || c->rd_closed;
       }
       {
         std::lock_guard<std::mutex> g(q_mu_);
-        q_.push_back(std::move(r));
+        q_.push_back(std::move(c->head));
       }
+      c->head = Request();
       uint64_t one = 1;
       (void)!::write(notify_, &one, 8);
     }
   }
+
+  // Request line + headers of the next request into c->head; false if incomplete or rejected.
+  bool parse_head(const std::shared_ptr<Conn>& c) {
+    const size_t he = c->in.find("\r\n\r\n");
+    if (he == std::string::npos) {
+      if (c->in.size() > (1u << 20)) bad(c, 431);
+      return false;
+    }
+    Request& r = c->head;
+    r = Request();
+    r.conn = c->id;
+    r.peer = c->peer;
+    const size_t le = c->in.find("\r\n");
+    {
+      const std::string line = c->in.substr(0, le);
+      const size_t s1 = line.find(' ');
+      const size_t s2 = line.rfind(' ');
+      if (s1 == std::string::npos || s2 == s1) {
+        bad(c, 400);
+        return false;
+      }
+      r.method = line.substr(0, s1);
+      r.target = line.substr(s1 + 1, s2 - s1 - 1);
+      r.version = line.substr(s2 + 1);
+    }
+    size_t p = le + 2;
+    c->clen = 0;
+    c->chunked = false;
+    c->expect = false;
+    c->sent_continue = false;
+    c->conn_close = (r.version == "HTTP/1.0");
+    bool bad_len = false;
+    while (p < he) {
+      const size_t e = c->in.find("\r\n", p);
+      const size_t colon = c->in.find(':', p);
+      if (colon != std::string::npos && colon < e) {
+        std::string k = c->in.substr(p, colon - p);
+        for (auto& ch : k) ch = static_cast<char>(tolower(ch));
+        size_t vs = colon + 1;
+        while (vs < e && (c->in[vs] == ' ' || c->in[vs] == '\t')) ++vs;
+        size_t ve = e;
+        while (ve > vs && (c->in[ve - 1] == ' ' || c->in[ve - 1] == '\t')) --ve;
+        std::string v = c->in.substr(vs, ve - vs);
+        if (k == "content-length") {
+          char* endp = nullptr;
+          errno = 0;
+          c->clen = strtoull(v.c_str(), &endp, 10);
+          if (v.empty() || *endp || errno == ERANGE) bad_len = true;
+        } else if (k == "transfer-encoding" && v.find("chunked") != std::string::npos) {
+          c->chunked = true;
+        } else if (k == "connection") {
+          std::string lv = v;
+          for (auto& ch : lv) ch = static_cast<char>(tolower(ch));
+          if (lv.find("close") != std::string::npos) c->conn_close = true;
+          if (lv.find("keep-alive") != std::string::npos) c->conn_close = false;
+        } else if (k == "expect") {
+          c->expect = true;
+        }
+        r.headers.emplace_back(std::move(k), std::move(v));
+      }
+      p = e + 2;
+    }
+    c->in.erase(0, he + 4);
+    if (bad_len && !c->chunked) {
+      bad(c, 400);
+      return false;
+    }
+    if (!c->chunked && c->clen > max_body_) {
+      bad(c, 413);
+      return false;
+    }
+    c->have_head = true;
+    return true;
+  }
+
+  // bytes of unparsed input a connection may hold: one maximal body plus a head
+  size_t in_cap() const { return max_body_ + (2u << 20); }
 
   void send_continue(const std::shared_ptr<Conn>& c) {
     static const char k100[] = "HTTP/1.1 100 Continue\r\n\r\n";
@@ -579,21 +640,19 @@ class Server {
           if (c->out.empty() && c->drain_close) c->closed = true;
           if (c->out.empty() && c->want_out && !c->closed) {
             c->want_out = false;
-            epoll_event ev{};
-            ev.events = EPOLLIN | EPOLLRDHUP;
-            ev.data.u64 = c->id;
-            epoll_ctl(ep_, EPOLL_CTL_MOD, c->fd, &ev);
+            rearm(c.get());
           }
         }
-        bool gone = false;
+        bool gone = false, eof = false;
         if (e & (EPOLLIN | EPOLLRDHUP | EPOLLHUP | EPOLLERR)) {
           for (;;) {
             const ssize_t r = ::recv(c->fd, buf, sizeof(buf), MSG_DONTWAIT);
             if (r > 0) {
               c->in.append(buf, static_cast<size_t>(r));
+              if (c->in.size() > in_cap()) break;  // checked below
               continue;
             }
-            if (r == 0) gone = true;
+            if (r == 0) eof = true;
             else if (errno == EINTR) continue;
             else if (errno != EAGAIN && errno != EWOULDBLOCK) gone = true;
             break;
@@ -604,7 +663,30 @@ class Server {
           drop(c);
           continue;
         }
+        bool busy;
+        {
+          std::lock_guard<std::mutex> g(c->mu);
+          busy = c->busy;
+        }
+        // a client that keeps pipelining while its request is served cannot grow `in` without bound
+        if (busy && c->in.size() > in_cap()) {
+          drop(c);
+          continue;
+        }
         parse(c);
+        if (eof) {
+          // half-close after a complete request is legal: answer it, then close; nothing
+          // complete buffered (or a partial request) -> the connection is finished
+          std::lock_guard<std::mutex> g(c->mu);
+          if (!c->busy && c->out.empty()) {
+            c->closed = true;
+          } else {
+            c->rd_closed = true;
+            c->close_after = true;
+            if (!c->busy) c->drain_close = true;
+            rearm(c.get());
+          }
+        }
         bool dead;
         {
           std::lock_guard<std::mutex> g(c->mu);
@@ -761,6 +843,7 @@ void register_http(py::module& m) {
       .def(py::init<const std::string&, int, int>(), py::arg("host"), py::arg("port"), py::arg("backlog") = 4096)
       .def_property_readonly("port", &Server::port)
       .def_property_readonly("notify_fd", &Server::notify_fd)
+      .def_property("max_body", &Server::max_body, &Server::set_max_body)
       .def("start", &Server::start)
       .def("stop", &Server::stop, py::call_guard<py::gil_scoped_release>())
       .def("take_requests", &Server::take_requests)

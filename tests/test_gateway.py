@@ -219,3 +219,20 @@ def test_files_and_assistants(client, tmp_path):
 def test_system_route_reports_inventory(client):
     j = client.get("/system").json()
     assert "backends" in j and "cpu" in j["system"] and isinstance(j["system"]["gpus"], list)
+
+
+def test_browse_page_escapes_gallery_names(engine, tmp_path_factory):
+    """A gallery entry named with a quote must not break out of the button's handler (the
+    reference renders with html/template, which escapes by context: core/http/elements/gallery.go)."""
+    from fastapi.testclient import TestClient
+    from localai_amd.gateway.app import create_app_for_engine
+    d = tmp_path_factory.mktemp("gal")
+    evil = "x');fetch('/evil')//"
+    (d / "index.yaml").write_text(f'- name: "{evil}"\n  description: "d"\n  urls: []\n')
+    ac = _app_config(tmp_path_factory, galleries=[{"name": "g", "url": f"file://{d / 'index.yaml'}"}])
+    app, _ = create_app_for_engine(engine, name="tiny", app_config=ac, models_path=str(d))
+    with TestClient(app) as c:
+        page = c.get("/browse", headers={"accept": "text/html"}).text
+    assert "fetch(&#x27;/evil&#x27;)" in page, page[page.find("<main>"):][:600]  # escaped attribute text only
+    assert "install(this)" in page and "install('" not in page
+    assert "onclick=\"install" not in page

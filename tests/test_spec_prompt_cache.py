@@ -72,7 +72,13 @@ def test_prompt_cache_persists_and_restores(tiny_model_path, tmp_path):
     p = dict(max_tokens=4, temperature=0.0, ignore_eos=True, prompt_cache_path=path)
     e1 = _engine(tiny_model_path)
     r1 = e1.generate(prompt, SamplingParams(**p))
+    e1._pcache.flush()  # the file is written by a background thread, off the engine loop
     assert os.path.exists(path)
+    # the same prompt again: the file already holds that prefix, so nothing is rewritten
+    mt = os.path.getmtime(path)
+    e1.generate(prompt, SamplingParams(**p))
+    e1._pcache.flush()
+    assert os.path.getmtime(path) == mt
     # a fresh engine (empty prefix cache) restores the blocks and reuses them
     e2 = _engine(tiny_model_path)
     bm = e2.sched.blocks()
@@ -96,4 +102,5 @@ def test_prompt_cache_read_only_never_writes(tiny_model_path, tmp_path, ro):
     e.generate("a b c d e f g h i j k l m n o p q r s t u v w x y z",
                SamplingParams(max_tokens=2, temperature=0.0, ignore_eos=True, prompt_cache_path=path,
                               prompt_cache_ro=ro))
+    e._pcache.flush()
     assert os.path.exists(path) is (not ro)
