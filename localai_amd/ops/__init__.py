@@ -46,6 +46,8 @@ def lib():
             "la_qgemm_skinny": [I, P, P, P, P, I, I, P, I, I, I, P, I, LNG, P],
             "la_qgemm_mid": [I, P, P, P, P, I, I, P, I, I, I, P, I, LNG, I, P],
             "la_qgemm_ws": [I, P, P, P, P, I, I, P, I, I, I, P, I, LNG, P],
+            "la_dq_swizzle": [I, P, P, P, I, I, P, P, P],
+            "la_qgemm_dq": [I, P, P, I, I, P, I, I, I, P, I, LNG, I, I, P],
             "la_qgemv_dp4": [I, P, P, P, I, P, I, I, I, P, I, LNG, P, LNG, I, P, I, P],
             "la_gemv_variant": [I],
             "la_add_norm": [P, P, LNG, I, P, I, P, P, P, I, I, F, I, P, P],
@@ -107,6 +109,7 @@ class QWeight:
     planes: Tuple[Optional[torch.Tensor], ...]   # p0..p3 device planes (GPU path)
     ref: Optional[torch.Tensor] = None            # fp32 [N, K] (CPU path / oracle)
     bf16: Optional[torch.Tensor] = None           # optional HBM-resident bf16 copy (prefill GEMMs)
+    dq: Optional[Tuple[torch.Tensor, torch.Tensor]] = None  # fragment-ordered Q4_K copy (gemm_dq.hip)
 
     @property
     def device(self) -> torch.device:
@@ -182,6 +185,25 @@ class QWeight:
                        "la_dequant")
                 self.bf16 = out
         return self.bf16
+
+    @property
+    def dq_ok(self) -> bool:
+        """Can feed the in-register-dequant batch GEMM (gemm_dq.hip): Q4_K with its unpacked
+        scale planes."""
+        return self.fmt == FMT_Q4_K and self.planes[2] is not None and self.K % 256 == 0
+
+    def dq_planes(self) -> Tuple[torch.Tensor, torch.Tensor]:
+        """Fragment-ordered copy for gemm_dq.hip, built once on the device: codes [NB][K/64][64][16 B]
+        and per-(column, K-step) scale records [NB/4][K/64][4][32][8 B] (0.625 B per weight), NB =
+        32-column blocks with N padded to the kernel's 256-column tile."""
+        if self.dq is None:
+            nb, ks = (self.N + 255) // 256 * 8, self.K // 64
+            qsw = torch.empty(nb * ks * 1024, dtype=torch.uint8, device=self.device)
+            ssw = torch.empty(nb // 4 * ks * 1024, dtype=torch.uint8, device=self.device)
+            _check(lib().la_dq_swizzle(self.fmt, _ptr(self.planes[0]), _ptr(self.planes[2]), _ptr(self.planes[3]),
+                                       self.N, self.K, qsw.data_ptr(), ssw.data_ptr(), _stream()), "la_dq_swizzle")
+            self.dq = (qsw, ssw)
+        return self.dq
 
     def dequant_f32(self) -> torch.Tensor:
         if self.ref is not None:
@@ -366,6 +388,10 @@ GEMV_DP4 = os.environ.get("LOCALAI_AMD_GEMV", "dp4") == "dp4"
 MID_MAX_M = 256          # 64 < M <= MID_MAX_M: quantised mid-M MFMA GEMM (gemm_mid.hip) or hipBLASLt
 MID_FMTS = (FMT_Q4_K, FMT_Q6_K, FMT_Q8_0)
 GEMM_AUTOTUNE = True
+# gemm_dq.hip joins the autotune candidates only on request: it needs a second (fragment-ordered)
+# copy of every Q4_K weight it times, and measured on par with qgemm_mid / hipBLASLt at decode
+# batch 256 (profiles/decode_gemv_study.md §5)
+GEMM_DQ = os.environ.get("LOCALAI_AMD_DQ", "0") == "1"
 # (M, K, ((fmt, N), ...)) -> ("mid", S) | ("blas", 0); filled by _autotune_mid at warm-up (eager
 # runs before each decode-graph capture), consulted during capture / replay.
 _GEMM_CHOICE: dict = {}
@@ -409,6 +435,25 @@ def _run_ws(x, ws, S, out, Ntot):
     for w in ws:
         _check(lib().la_qgemm_ws(w.fmt, *w.ptrs(), w.N, w.K, x.data_ptr(), K, M, S, out.data_ptr() + col * 4,
                                  Ntot, M * Ntot, _stream()), "la_qgemm_ws")
+        col += w.N
+
+
+def _dq_ok(ws, K: int, S: int) -> bool:
+    """In-register-dequant GEMM (gemm_dq.hip): Q4_K weights, equal K splits."""
+    return all(w.dq_ok for w in ws) and (K // 64) % S == 0
+
+
+def _run_dq(x, ws, S, out, Ntot, wnt=2):
+    """out: fp32 slabs [S, M, Ntot], or a bf16 [M, Ntot] matrix (S == 1)."""
+    M, K = x.shape
+    bf = out.dtype == torch.bfloat16
+    col = 0
+    for w in ws:
+        qsw, ssw = w.dq_planes()
+        esz = 2 if bf else 4
+        _check(lib().la_qgemm_dq(w.fmt, qsw.data_ptr(), ssw.data_ptr(), w.N, w.K, x.data_ptr(), K, M, S,
+                                 out.data_ptr() + col * esz, Ntot, 0 if bf else M * Ntot, int(bf), wnt, _stream()),
+               "la_qgemm_dq")
         col += w.N
 
 
@@ -517,6 +562,8 @@ def _autotune_mid(x, ws, key, Ntot):
     cands = [("blas", 0, 0)] + [("mid", S, t) for t in tiles for S in (1, 2, 4, 8) if _mid_split_ok(K, S)]
     if M > 128:
         cands += [("ws", S, 0) for S in (1, 2, 4, 8) if _ws_ok(ws, K, S)]
+    if GEMM_DQ:
+        cands += [("dq", S, 0) for S in (1, 2, 4, 8) if _dq_ok(ws, K, S)]
     outs = {S: torch.empty(S, M, Ntot, dtype=torch.float32, device=x.device) for _, S, _ in cands if S}
     best, best_t = ("blas", 0, 0), float("inf")
     for kind, S, t in cands:
@@ -524,6 +571,8 @@ def _autotune_mid(x, ws, key, Ntot):
             fn = lambda: _run_blas(x, ws, Ntot)  # noqa: E731
         elif kind == "ws":
             fn = lambda S=S: _run_ws(x, ws, S, outs[S], Ntot)  # noqa: E731
+        elif kind == "dq":
+            fn = lambda S=S: _run_dq(x, ws, S, outs[S], Ntot)  # noqa: E731
         else:
             fn = lambda S=S, t=t: _run_mid(x, ws, S, outs[S], Ntot, t)  # noqa: E731
         fn()
@@ -569,7 +618,7 @@ def linear_multi(x: torch.Tensor, ws: Sequence[QWeight], bias: Optional[torch.Te
     skinny_ok = all(w.K % 256 == 0 for w in ws)
     use_skinny = (M <= SKINNY_MAX_M and skinny_ok) if force is None else force == "skinny"
     mid_ok = skinny_ok and all(w.fmt in MID_FMTS for w in ws)
-    S, tile, use_ws = 0, 0, False
+    S, tile, use_ws, use_dq = 0, 0, False, False
     if force == "ws":
         S, use_ws = 1, True
     if force == "mid":
@@ -581,15 +630,18 @@ def linear_multi(x: torch.Tensor, ws: Sequence[QWeight], bias: Optional[torch.Te
         choice = _GEMM_CHOICE.get(key)
         if choice is None and GEMM_AUTOTUNE and not torch.cuda.is_current_stream_capturing():
             choice = _autotune_mid(x, ws, key, Ntot)
-        if choice is not None and choice[0] in ("mid", "ws"):
+        if choice is not None and choice[0] in ("mid", "ws", "dq"):
             S, tile = choice[1], choice[2]
             use_ws = choice[0] == "ws"
+            use_dq = choice[0] == "dq"
     if S:
         out = out_slabs
         if out is None or out.shape != (S, M, Ntot):
             out = torch.empty(S, M, Ntot, dtype=torch.float32, device=x.device)
         if use_ws:
             _run_ws(x, ws, S, out, Ntot)
+        elif use_dq:
+            _run_dq(x, ws, S, out, Ntot)
         else:
             _run_mid(x, ws, S, out, Ntot, tile)
         return Partial(out, bias)

@@ -528,3 +528,41 @@ def test_moe_grouped_gemm(T):
         e = int(idc.view(-1)[p])
         ref[t] += float(wts.view(-1)[p]) * (h[p].float().cpu() @ dn[e].ref.t())
     assert (z.cpu() - ref).abs().max() < 2e-2 * max(1.0, ref.abs().max())
+
+
+@pytest.mark.parametrize("M", [1, 100, 256, 300])
+@pytest.mark.parametrize("K", [1024, 3584])
+def test_dq_gemm(M, K):
+    """In-register-dequant Q4_K batch GEMM (gemm_dq.hip) vs the fp32 reference: N off the 32 and
+    256 tiles, several M tiles, every equal split of the K-steps (fp32
+    slabs) and the bf16 single-matrix output; repeated launches bit-identical."""
+    N = 200
+    w = _qw(N, K, GGMLType.Q4_K, seed=19)
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    ref = x.float().cpu() @ w.ref.t()
+    tol = 3e-2 * max(1.0, ref.abs().max().item())
+    for wnt in (1,):
+        for S in (1, 2, 4, 7):
+            if (K // 64) % S:
+                continue
+            out = torch.full((S, M, N), float("nan"), dtype=torch.float32, device=DEV)
+            ops._run_dq(x, [w], S, out, N, wnt)
+            y = out.sum(0).cpu()
+            assert (y - ref).abs().max().item() < tol, (wnt, S)
+            out2 = torch.empty_like(out)
+            ops._run_dq(x, [w], S, out2, N, wnt)
+            assert torch.equal(out, out2)
+        ob = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+        ops._run_dq(x, [w], 1, ob, N, wnt)
+        assert (ob.float().cpu() - ref).abs().max().item() < tol, wnt
+
+
+def test_dq_gemm_two_weights_side_by_side():
+    """q|k-style call: two Q4_K weights written into column ranges of one output."""
+    K, M = 2048, 256
+    ws = [_qw(320, K, GGMLType.Q4_K, seed=21), _qw(96, K, GGMLType.Q4_K, seed=22)]
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    ref = torch.cat([x.float().cpu() @ w.ref.t() for w in ws], -1)
+    out = torch.empty(2, M, 416, dtype=torch.float32, device=DEV)
+    ops._run_dq(x, ws, 2, out, 416)
+    assert (out.sum(0).cpu() - ref).abs().max().item() < 3e-2 * max(1.0, ref.abs().max().item())
