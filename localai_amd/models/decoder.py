@@ -68,16 +68,19 @@ class ForwardBatch:
 
 
 class KVCache:
-    """Per-layer paged K/V pools: K [num_blocks, Hkv_local, block_size, head_dim], V transposed
-    [num_blocks, Hkv_local, head_dim, block_size] (bf16)."""
+    """Per-layer paged K/V pools: K [num_blocks, Hkv_local, block_size, head_dim], V transposed in
+    groups of 8 keys [num_blocks, Hkv_local, block_size/8, head_dim, 8] (bf16)."""
 
     def __init__(self, n_layer: int, num_blocks: int, n_kv: int, block_size: int, head_dim: int, device,
                  dtype=torch.bfloat16):
         self.num_blocks, self.block_size = num_blocks, block_size
         self.k = [torch.zeros(num_blocks, n_kv, block_size, head_dim, dtype=dtype, device=device)
                   for _ in range(n_layer)]
-        # V pages are stored transposed ([head_dim][block_size]) -- see ops/csrc/attention.hip
-        self.v = [torch.zeros(num_blocks, n_kv, head_dim, block_size, dtype=dtype, device=device)
+        # V pages are stored transposed per 8-key group ([block_size/8][head_dim][8]) -- see
+        # ops/csrc/attention.hip
+        if block_size % 8:
+            raise ValueError(f"block_size {block_size} must be a multiple of 8")
+        self.v = [torch.zeros(num_blocks, n_kv, block_size // 8, head_dim, 8, dtype=dtype, device=device)
                   for _ in range(n_layer)]
 
     @staticmethod

@@ -775,7 +775,7 @@ def rope_kv(qkv: Partial, pos: torch.Tensor, slots: Optional[torch.Tensor], cos_
             ok = sl >= 0
             blk, off = sl[ok] // block_size, sl[ok] % block_size
             k_cache[blk, :, off] = k[ok]
-            v_cache[blk, :, :, off] = v[ok]
+            v_cache[blk, :, off // 8, :, off % 8] = v[ok]
         if q_out is not None:
             q_out.copy_(q)
             return q_out
@@ -883,7 +883,7 @@ def attn_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, b
     block_tables [B,maxb] i32; seq_lens [B] i32."""
     B, Hq, Dh = q.shape
     nblk, Hkv, BS, Dh2 = k_cache.shape
-    if Dh2 != Dh or Hq % Hkv or tuple(v_cache.shape) != (nblk, Hkv, Dh, BS):
+    if Dh2 != Dh or Hq % Hkv or tuple(v_cache.shape) != (nblk, Hkv, BS // 8, Dh, 8):
         raise ValueError("attn_decode: head/cache shape mismatch")
     if not q.is_cuda:
         return _attn_ref_decode(q, k_cache, v_cache, block_tables, seq_lens, scale)
@@ -927,7 +927,7 @@ def attn_decode_rope(qkv: Partial, pos: torch.Tensor, slots: torch.Tensor, cos_s
         q = rope_kv(qkv, pos, slots, cos_sin, Hq, Hkv, Dh, rot, mode, k_cache, v_cache, BS)
         return attn_decode(q, k_cache, v_cache, block_tables, seq_lens, scale, max_seq_len, out=out,
                            workspace=workspace)
-    if Hq % Hkv or tuple(v_cache.shape) != (nblk, Hkv, Dh, BS) or k_cache.shape[3] != Dh:
+    if Hq % Hkv or tuple(v_cache.shape) != (nblk, Hkv, BS // 8, Dh, 8) or k_cache.shape[3] != Dh:
         raise ValueError("attn_decode_rope: head/cache shape mismatch")
     P, PS = decode_partitions(T, Hkv, max_seq_len, BS)
     if out is None:
@@ -945,10 +945,22 @@ def attn_decode_rope(qkv: Partial, pos: torch.Tensor, slots: torch.Tensor, cos_s
     return out
 
 
+def v_pages(nblk: int, Hkv: int, BS: int, Dh: int, dtype=torch.bfloat16, device=None) -> torch.Tensor:
+    """An empty V cache in the kernels' layout: [nblk, Hkv, BS/8, Dh, 8]."""
+    return torch.zeros(nblk, Hkv, BS // 8, Dh, 8, dtype=dtype, device=device)
+
+
+def v_from_rows(v: torch.Tensor) -> torch.Tensor:
+    """[nblk, Hkv, BS, Dh] (key-major pages) -> the V cache layout [nblk, Hkv, BS/8, Dh, 8]."""
+    n, h, bs, d = v.shape
+    return v.view(n, h, bs // 8, 8, d).transpose(3, 4).contiguous()
+
+
 def _gather_kv(cache, bt_row, L, transposed=False):
-    """-> [Hkv, L, Dh] from K pages [nblk,Hkv,BS,Dh] or transposed V pages [nblk,Hkv,Dh,BS]."""
+    """-> [Hkv, L, Dh] from K pages [nblk,Hkv,BS,Dh] or V pages [nblk,Hkv,BS/8,Dh,8]."""
     if transposed:
-        cache = cache.transpose(2, 3)
+        n, h, g, d, e = cache.shape
+        cache = cache.transpose(3, 4).reshape(n, h, g * e, d)
     BS = cache.shape[2]
     nb = (L + BS - 1) // BS
     blocks = cache[bt_row[:nb].long()]                  # [nb, Hkv, BS, Dh]

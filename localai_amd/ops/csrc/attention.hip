@@ -1,9 +1,12 @@
 // Paged attention for the engine (replaces ggml-cuda fattn*.cu / softmax.cu / the KQ,KQV
 // batched GEMMs of the non-FA path; SURVEY §2.8 K7, K11, K12, K15 [external]).
 //
-// KV cache layout (per layer): K [num_blocks][Hkv][BS][Dh] and V^T [num_blocks][Hkv][Dh][BS] bf16:
-// one page of one kv-head is BS*Dh*2 contiguous bytes (8 KiB at BS=32, Dh=128); V is stored
-// transposed inside the page so the PV MFMA's B operand (8 keys at one d) is a vector load.
+// KV cache layout (per layer): K [num_blocks][Hkv][BS][Dh] and V [num_blocks][Hkv][BS/8][Dh][8]
+// bf16: one page of one kv-head is BS*Dh*2 contiguous bytes (8 KiB at BS=32, Dh=128).  V is
+// stored transposed in groups of 8 keys ([key group][d][8 keys]), so the PV MFMA's B operand (8
+// consecutive keys at one d) is one 16-byte load, and appending one token touches 16-byte
+// segments of ONE 2 KiB group run instead of every 64-byte row of the page (a fully transposed
+// [Dh][BS] page made each decode append a 2-byte write into 128 separate cache lines).
 //
 // * attn_decode: one query row per sequence.  Workgroup = (partition of <=PS keys, kv head,
 //   sequence); the G = Hq/Hkv query heads sharing a kv head are packed so K/V are read from
@@ -165,7 +168,7 @@ __global__ __launch_bounds__(DEC_T) void attn_decode_kernel(
         const int d = tid - DH / 2;
         float x[1];
         rope_src_load<1>(R, b, (Hq + Hkv + kvh) * DH + d, x);
-        ((bf16*)vc)[(((long)blk * Hkv + kvh) * DH + d) * BS + off] = (bf16)x[0];  // V^T page [Dh][BS]
+        ((bf16*)vc)[((long)blk * Hkv + kvh) * DH * BS + ((off >> 3) * DH + d) * 8 + (off & 7)] = (bf16)x[0];
       }
       // Only this workgroup reads the appended key back (pages never straddle partitions, and
       // L1 starts each launch clean), so same-CU ordering suffices: the stores reach the XCD's
@@ -203,7 +206,7 @@ __global__ __launch_bounds__(DEC_T) void attn_decode_kernel(
 #pragma unroll
     for (int nd = 0; nd < ND; ++nd) {
       const int d = 16 * nd + r;
-      T.v[nd] = *(const bf16x8*)(vc + pv + (long)d * BS + (kv % BS));
+      T.v[nd] = *(const bf16x8*)(vc + pv + ((long)((kv % BS) >> 3) * DH + d) * 8);
     }
   };
 
@@ -424,12 +427,12 @@ __global__ __launch_bounds__(PF_T) void attn_prefill_kernel(
       *(bf16x8*)(ks + kr * KS + d) = kv;
     }
     for (int cidx = tid; cidx < DP * (PF_KT / 8); cidx += PF_T) {
-      const int d = cidx / (PF_KT / 8), q8 = (cidx % (PF_KT / 8)) * 8;
+      const int d = cidx % DP, q8 = (cidx / DP) * 8;  // consecutive threads: consecutive d of one key group
       const int key = k0 + q8;
       bf16x8 vv = {};
       if (key < kend && d < DH) {
         const int blk = bt[key / BS], off = key % BS;
-        vv = *(const bf16x8*)(vc + (((long)blk * Hkv + kvh) * DH + d) * BS + off);
+        vv = *(const bf16x8*)(vc + ((long)blk * Hkv + kvh) * DH * BS + ((off >> 3) * DH + d) * 8);
         if (key + 8 > kend) {
 #pragma unroll
           for (int j = 0; j < 8; ++j)

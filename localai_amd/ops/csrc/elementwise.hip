@@ -142,7 +142,7 @@ __global__ __launch_bounds__(NT) void add_norm_kernel(float* __restrict__ residu
 // ------------------------------------------------------------------------------------
 // RoPE on q,k + append k,v into the paged cache.
 // qkv row layout: [Hq*Dh | Hkv*Dh | Hkv*Dh].  K cache [num_blocks][Hkv][BS][Dh], V cache transposed
-// per page: [num_blocks][Hkv][Dh][BS] (bf16).
+// in groups of 8 keys: [num_blocks][Hkv][BS/8][Dh][8] (bf16, see attention.hip).
 // cos_sin: [max_pos][rot/2][2] f32 (host-precomputed table: guide App. B "trig tables").
 // mode 0 = NORM (adjacent pairs, llama/mistral GGUF), 1 = NEOX (half-split, phi-2).
 __global__ __launch_bounds__(256) void rope_kv_kernel(Src qkv, const int* __restrict__ pos,
@@ -175,9 +175,9 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(Src qkv, const int* __rest
     } else {
       if (slot < 0) continue;
       const int vh = head - Hq - Hkv, blk = slot / BS, off = slot - blk * BS;
-      dst = vc + (((long)blk * Hkv + vh) * Dh + d0) * BS + off;  // V^T page layout [Dh][BS]
+      dst = vc + ((long)blk * Hkv + vh) * Dh * BS + ((off >> 3) * Dh + d0) * 8 + (off & 7);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) dst[(long)j * BS] = (bf16)v[j];
+      for (int j = 0; j < 4; ++j) dst[8 * j] = (bf16)v[j];
       continue;
     }
     if (mode == 0) {
@@ -214,6 +214,70 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(Src qkv, const int* __rest
     }
     bf16x4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
     *(bf16x4*)dst = o;
+  }
+}
+
+// Fast path of rope_kv: NORM (adjacent-pair) rotary over the whole head, DH in {64, 128}.  One
+// thread per 8 consecutive elements of a row (16-byte source loads, two float4 cos/sin loads,
+// 16-byte q / k stores; the 8 V values of a unit land in one 128-byte line of the grouped-
+// transposed V page).  The block's token position and slot are read once.
+LA_DEV void load8(const Src& s, long idx, int col, float v[8]) {
+  if (s.S == 0) {
+    const bf16x8 b = *(const bf16x8*)((const bf16*)s.p + idx);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (float)b[j];
+    if (s.bias) {
+      const float4 b0 = *(const float4*)(s.bias + col), b1 = *(const float4*)(s.bias + col + 4);
+      v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w;
+      v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
+    }
+  } else {
+    load4(s, idx, col, v);
+    load4(s, idx + 4, col + 4, v + 4);
+  }
+}
+
+template <int DH>
+__global__ __launch_bounds__(256) void rope_kv8_kernel(Src qkv, const int* __restrict__ pos,
+                                                       const int* __restrict__ slots,
+                                                       const float* __restrict__ cos_sin, int Hq, int Hkv,
+                                                       bf16* __restrict__ q_out, bf16* __restrict__ kc,
+                                                       bf16* __restrict__ vc, int BS) {
+  const int t = blockIdx.x;
+  const int W = (Hq + 2 * Hkv) * DH;
+  const int p = pos[t];
+  const int slot = slots ? slots[t] : -1;
+  const long row = (long)t * W;
+  const float* cs = cos_sin + (long)p * DH;  // DH/2 pairs x (cos, sin)
+  const int units = W >> 3;
+  const int u = blockIdx.y * blockDim.x + threadIdx.x;
+  if (u >= units) return;
+  const int col = u * 8;
+  const int head = col / DH, d0 = col - head * DH;
+  float v[8];
+  load8(qkv, row + col, col, v);
+  if (head >= Hq + Hkv) {  // v: no rotation
+    if (slot < 0) return;
+    const int vh = head - Hq - Hkv, blk = slot / BS, off = slot - blk * BS;
+    bf16* dst = vc + ((long)blk * Hkv + vh) * DH * BS + ((off >> 3) * DH + d0) * 8 + (off & 7);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dst[8 * j] = (bf16)v[j];
+    return;
+  }
+  const float4 c0 = *(const float4*)(cs + d0), c1 = *(const float4*)(cs + d0 + 4);  // pairs d0/2 .. d0/2+3
+  const float cc[4] = {c0.x, c0.z, c1.x, c1.z}, sn[4] = {c0.y, c0.w, c1.y, c1.w};
+  bf16x8 o;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float x0 = v[2 * j], x1 = v[2 * j + 1];
+    o[2 * j] = (bf16)(x0 * cc[j] - x1 * sn[j]);
+    o[2 * j + 1] = (bf16)(x0 * sn[j] + x1 * cc[j]);
+  }
+  if (head < Hq) {
+    *(bf16x8*)(q_out + ((long)t * Hq + head) * DH + d0) = o;
+  } else if (slot >= 0) {
+    const int kh = head - Hq, blk = slot / BS, off = slot - blk * BS;
+    *(bf16x8*)(kc + (((long)blk * Hkv + kh) * BS + off) * DH + d0) = o;
   }
 }
 
@@ -371,6 +435,17 @@ extern "C" int la_rope_kv(const void* qkv_p, long slab, int S, const void* bias,
                           void* kc, void* vc, int BS, void* stream) {
   if ((Dh & 3) || (rot & 3) || rot > Dh) return -1;
   Src s{qkv_p, slab, S, (const float*)bias};
+  if (mode == 0 && rot == Dh && (Dh == 128 || Dh == 64) && (BS & 7) == 0) {
+    const int units8 = (Hq + 2 * Hkv) * Dh / 8;
+    dim3 grid(T, (units8 + 255) / 256);
+    if (Dh == 128)
+      hipLaunchKernelGGL(la::rope_kv8_kernel<128>, grid, dim3(256), 0, (hipStream_t)stream, s, pos, slots, cos_sin,
+                         Hq, Hkv, (bf16*)q_out, (bf16*)kc, (bf16*)vc, BS);
+    else
+      hipLaunchKernelGGL(la::rope_kv8_kernel<64>, grid, dim3(256), 0, (hipStream_t)stream, s, pos, slots, cos_sin,
+                         Hq, Hkv, (bf16*)q_out, (bf16*)kc, (bf16*)vc, BS);
+    return (int)hipGetLastError();
+  }
   const int units = (Hq + 2 * Hkv) * Dh / 4;
   hipLaunchKernelGGL(la::rope_kv_kernel, dim3(T, (units + 255) / 256), dim3(256), 0, (hipStream_t)stream, s, pos,
                      slots, cos_sin, Hq,

@@ -15,7 +15,7 @@ for B, L in [(1, 256), (1, 2000), (64, 512), (256, 256), (256, 384)]:
     nb = (L + BS - 1) // BS
     nblk = B * nb + 8
     kc = (torch.randn(nblk, Hkv, BS, Dh, device=dev) * 0.5).to(torch.bfloat16)
-    vc = (torch.randn(nblk, Hkv, Dh, BS, device=dev) * 0.5).to(torch.bfloat16)
+    vc = ops.v_from_rows((torch.randn(nblk, Hkv, BS, Dh, device=dev) * 0.5).to(torch.bfloat16))
     bt = torch.randperm(B * nb, device=dev).to(torch.int32).view(B, nb)
     sl = torch.full((B,), L, dtype=torch.int32, device=dev)
     q = torch.randn(B, Hq, Dh, device=dev).to(torch.bfloat16)

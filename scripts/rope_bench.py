@@ -36,7 +36,7 @@ def timeit(fn, iters=20):
 for T, S in [(1, 8), (256, 0)]:
     nblk = T * 8 + 8
     kc = torch.zeros(nblk, Hkv, BS, Dh, dtype=torch.bfloat16, device=dev)
-    vc = torch.zeros(nblk, Hkv, Dh, BS, dtype=torch.bfloat16, device=dev)
+    vc = ops.v_pages(nblk, Hkv, BS, Dh, device=dev)
     src = (torch.randn(T, W, device=dev).to(torch.bfloat16) if S == 0
            else torch.randn(S, T, W, device=dev))
     p = ops.Partial(src)

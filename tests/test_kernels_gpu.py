@@ -232,7 +232,7 @@ def test_rope_kv(mode, Dh, rot):
     slots = torch.tensor([0, 17, 33, 50, -1], dtype=torch.int32, device=DEV)
     cs = ops.rope_cos_sin(256, rot, 10000.0, DEV)
     kc = torch.zeros(nblk, Hkv, BS, Dh, dtype=torch.bfloat16, device=DEV)
-    vc = torch.zeros(nblk, Hkv, Dh, BS, dtype=torch.bfloat16, device=DEV)
+    vc = ops.v_pages(nblk, Hkv, BS, Dh, device=DEV)
     kr, vr = kc.cpu().clone(), vc.cpu().clone()
     q = ops.rope_kv(ops.Partial(qkv), pos, slots, cs, Hq, Hkv, Dh, rot, mode, kc, vc, BS)
     qr = ops.rope_kv(ops.Partial(qkv.cpu()), pos.cpu(), slots.cpu(), cs.cpu(), Hq, Hkv, Dh, rot, mode, kr, vr, BS)
@@ -282,7 +282,7 @@ def _paged_setup(lens, Hkv, Dh, BS, seed=0):
     maxb = max((l + BS - 1) // BS for l in lens)
     nblk = sum((l + BS - 1) // BS for l in lens) + 3
     kc = torch.randn(nblk, Hkv, BS, Dh, generator=g).to(torch.bfloat16)
-    vc = torch.randn(nblk, Hkv, Dh, BS, generator=g).to(torch.bfloat16)  # transposed V pages
+    vc = ops.v_from_rows(torch.randn(nblk, Hkv, BS, Dh, generator=g).to(torch.bfloat16))  # V cache layout
     perm = torch.randperm(nblk, generator=g)
     bt = torch.zeros(len(lens), maxb, dtype=torch.int32)
     c = 0
