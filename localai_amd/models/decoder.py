@@ -18,6 +18,7 @@ vocab-parallel lm_head + all-gather.  Experts (Mixtral) are split the same way
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence
 
@@ -27,6 +28,9 @@ import torch
 from .. import ops
 from ..gguf import GGML_BLOCK, GGMLType, GGUFReader, dequantize, quantize
 from .hparams import HParams
+
+# batch-1/2 decode: q|k|v GEMV with RoPE + KV append in its epilogue (ops.qkv_rope_dp4)
+FUSED_QKV_ROPE = os.environ.get("LOCALAI_AMD_QKV_ROPE", "1") == "1"
 
 
 @dataclass
@@ -313,6 +317,21 @@ class DecoderModel:
         self.tp.all_reduce(out)
         return ops.Partial(out.unsqueeze(0))
 
+    def _post_attn(self, i: int, L: Layer, xn: torch.Tensor, res: torch.Tensor, o: ops.Partial) -> torch.Tensor:
+        """Residual + norm around the MLP of layer i; returns the next layer's normed input."""
+        hp = self.hp
+        eps, nm = hp.norm_eps, self.norm_mode
+        nxt = self.layers[i + 1] if i + 1 < len(self.layers) else None
+        nw = nxt.attn_norm if nxt is not None else self.out_norm
+        nb = nxt.attn_norm_b if nxt is not None else self.out_norm_b
+        if hp.parallel_residual:
+            f = self._mlp(L, xn)
+            ops.add_norm(res, o, nw, nb, eps, nm, want_out=False)
+            return ops.add_norm(res, f, nw, nb, eps, nm)
+        xn = ops.add_norm(res, o, L.ffn_norm, L.ffn_norm_b, eps, nm)
+        f = self._mlp(L, xn)
+        return ops.add_norm(res, f, nw, nb, eps, nm)
+
     def forward(self, fb: ForwardBatch, kv: KVCache, attn_workspace=None, return_hidden: bool = False) -> torch.Tensor:
         """Returns fp32 logits [R, V] for the rows selected by fb.logits_idx (or, with
         return_hidden, the final-norm hidden states [T, D])."""
@@ -324,8 +343,18 @@ class DecoderModel:
             res.index_copy_(0, fb.inject_idx, fb.inject_rows.to(res.dtype))
         L0 = self.layers[0]
         xn = ops.add_norm(res, None, L0.attn_norm, L0.attn_norm_b, eps, nm)
-        n = len(self.layers)
+        fuse_qkv = fb.decode and FUSED_QKV_ROPE and ops.qkv_rope_ok(xn, self.layers[0].qkv, self.layers[0].qkv_bias,
+                                                                    hp.rope_mode, self.rot, self.Dh, kv.block_size)
         for i, L in enumerate(self.layers):
+            if fuse_qkv:
+                # batch-1/2 decode: q|k|v GEMV with RoPE + the paged K/V append in its epilogue
+                q = ops.qkv_rope_dp4(xn, L.qkv, fb.pos, fb.slots, self.cos_sin, self.Hq, self.Hkv, self.Dh,
+                                     kv.k[i], kv.v[i], kv.block_size)
+                a = ops.attn_decode(q, kv.k[i], kv.v[i], fb.block_tables, fb.seq_lens, self.scale, fb.max_len,
+                                    workspace=attn_workspace)
+                o = self._row_parallel_out(ops.linear(a.view(T, self.Hq * self.Dh), L.wo), L.wo_bias)
+                xn = self._post_attn(i, L, xn, res, o)
+                continue
             qkv = ops.linear_multi(xn, L.qkv, bias=L.qkv_bias)
             if fb.decode:
                 # RoPE + KV append fused into the decode attention launch (rope_kv when not fusable)
@@ -338,17 +367,7 @@ class DecoderModel:
                 a = ops.attn_prefill(q, kv.k[i], kv.v[i], fb.cu_q, fb.ctx_lens, fb.block_tables, self.scale,
                                      tiles=fb.tiles)
             o = self._row_parallel_out(ops.linear(a.view(T, self.Hq * self.Dh), L.wo), L.wo_bias)
-            nxt = self.layers[i + 1] if i + 1 < n else None
-            nw = nxt.attn_norm if nxt is not None else self.out_norm
-            nb = nxt.attn_norm_b if nxt is not None else self.out_norm_b
-            if hp.parallel_residual:
-                f = self._mlp(L, xn)
-                ops.add_norm(res, o, nw, nb, eps, nm, want_out=False)
-                xn = ops.add_norm(res, f, nw, nb, eps, nm)
-            else:
-                xn = ops.add_norm(res, o, L.ffn_norm, L.ffn_norm_b, eps, nm)
-                f = self._mlp(L, xn)
-                xn = ops.add_norm(res, f, nw, nb, eps, nm)
+            xn = self._post_attn(i, L, xn, res, o)
         if return_hidden:
             return xn
         rows = xn if fb.logits_idx is None else xn.index_select(0, fb.logits_idx)

@@ -50,6 +50,7 @@ def lib():
             "la_qgemm_dq": [I, P, P, I, I, P, I, I, I, P, I, LNG, I, I, P],
             "la_qgemv_dp4": [I, P, P, P, I, P, I, I, I, P, I, LNG, P, LNG, I, P, I, P],
             "la_gemv_variant": [I],
+            "la_qgemv_dp4_rope": [I, P, P, P, I, P, I, P, P, P, I, I, I, P, P, P, I, P],
             "la_add_norm": [P, P, LNG, I, P, I, P, P, P, I, I, F, I, P, P],
             "la_rope_kv": [P, LNG, I, P, P, P, P, I, I, I, I, I, I, P, P, P, I, P],
             "la_act": [P, LNG, I, P, P, I, I, I, P],
@@ -71,6 +72,9 @@ def lib():
             fn = getattr(L, name)
             fn.argtypes = args
             fn.restype = I
+        gv = os.environ.get("LOCALAI_AMD_GEMV_VARIANT")
+        if gv is not None:
+            _check(L.la_gemv_variant(int(gv)), "la_gemv_variant")
         _LIB = L
         return L
 
@@ -380,6 +384,39 @@ def gemv_dp4(x: Optional[torch.Tensor], ws: Sequence[QWeight], S: int, out: torc
                                   out.data_ptr() + col * 4, Ntot, M * Ntot, a[0], a[1], a[2], a[3], act_mode,
                                   _stream()), "la_qgemv_dp4")
         col += sum(w.N for w in seg)
+
+
+def qkv_rope_ok(x: torch.Tensor, ws: Sequence[QWeight], bias, mode: int, rot: int, Dh: int, block_size: int) -> bool:
+    """The fused decode q|k|v GEMV + RoPE + KV append (gemv_dp4.hip GVRope) applies: GPU, batch
+    <= GEMV_MAX_M, Q4_K/Q6_K weights, no bias, NORM rotary over the whole head."""
+    return (x.is_cuda and GEMV_DP4 and x.shape[0] <= GEMV_MAX_M and bias is None and mode == 0 and rot == Dh
+            and Dh % 2 == 0 and block_size % 8 == 0 and len(ws) <= 3 and all(w.gemv_ok for w in ws)
+            and len({w.K for w in ws}) == 1 and ws[0].K % 1024 == 0)
+
+
+def qkv_rope_dp4(x: torch.Tensor, ws: Sequence[QWeight], pos: torch.Tensor, slots: torch.Tensor,
+                 cos_sin: torch.Tensor, Hq: int, Hkv: int, Dh: int, k_cache: torch.Tensor, v_cache: torch.Tensor,
+                 block_size: int, q_out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """q = rope(x @ Wq^T) [M, Hq, Dh] bf16; k = rope(x @ Wk^T) and v = x @ Wv^T appended to the paged
+    cache at `slots` -- one GEMV launch (split-K 1) with the rotation and the append in its
+    epilogue, instead of a GEMV + rope_kv."""
+    M, K = x.shape
+    if x.dtype != torch.bfloat16 or not x.is_contiguous():
+        raise ValueError("qkv_rope_dp4: x must be contiguous bf16")
+    if sum(w.N for w in ws) != (Hq + 2 * Hkv) * Dh:
+        raise ValueError("qkv_rope_dp4: weights do not form q|k|v")
+    if pos.dtype != torch.int32 or slots.dtype != torch.int32 or pos.numel() < M or slots.numel() < M:
+        raise ValueError("qkv_rope_dp4: pos / slots must be int32 [M]")
+    if q_out is None:
+        q_out = torch.empty(M, Hq, Dh, dtype=torch.bfloat16, device=x.device)
+    n = len(ws)
+    fmts = (ctypes.c_int * n)(*[w.fmt for w in ws])
+    planes = (ctypes.c_void_p * (4 * n))(*[p for w in ws for p in w.ptrs()])
+    Ns = (ctypes.c_int * n)(*[w.N for w in ws])
+    _check(lib().la_qgemv_dp4_rope(n, fmts, planes, Ns, K, x.data_ptr(), M, pos.data_ptr(), slots.data_ptr(),
+                                   cos_sin.data_ptr(), Hq, Hkv, Dh, q_out.data_ptr(), k_cache.data_ptr(),
+                                   v_cache.data_ptr(), block_size, _stream()), "la_qgemv_dp4_rope")
+    return q_out
 
 
 SKINNY_MAX_M = 64

@@ -189,9 +189,60 @@ LA_DEV void x_commit(int M, int kper, const u32x2 (&xr)[GV_XI], int8_t* xq, int*
   }
 }
 
+// Fused RoPE + paged-KV append epilogue for the decode q|k|v GEMV (split-K 1): the GEMV's
+// output row n of the fused [q | k | v] projection is complete in the 8 lanes of its row group,
+// and NORM rotary pairs adjacent rows (2i, 2i+1) = adjacent row groups of one wave (lane ^ 8),
+// so the rotation is one shuffle.  q goes to q_out (bf16, [M][Hq][Dh]), k / v of token m to its
+// cache slot (V in the grouped-transposed page layout of attention.hip).  Replaces the rope_kv
+// launch of a batch-1/2 decode step (SURVEY §2.8 K9 + K10 fused into K5).
+struct GVRope {
+  const int* pos;        // [M] rotary position of each token
+  const int* slots;      // [M] cache slot (< 0: no append)
+  const float* cos_sin;  // [max_pos][Dh/2][2]
+  bf16* q_out;           // null: plain fp32 slab epilogue
+  bf16* kc;
+  bf16* vc;
+  int Hq, Hkv, Dh, BS;
+};
+
 template <int MT, int RS>
 LA_DEV void gv_store(const float (&acc)[MT][RS], const int (&n)[RS], int N, int M, int t, float* o,
-                     int ldo, int col0) {
+                     int ldo, int col0, const GVRope& rp) {
+  if (rp.q_out) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      if (m < M) {
+        const int p = rp.pos[m], slot = rp.slots[m];
+        const float* cs = rp.cos_sin + (long)p * rp.Dh;
+#pragma unroll
+        for (int s = 0; s < RS; ++s) {
+          const float v = group_sum<8>(acc[m][s]);
+          const float partner = __shfl_xor(v, 8, 64);  // row n ^ 1
+          const int col = col0 + n[s];
+          const int head = col / rp.Dh, d = col - head * rp.Dh;
+          float y = v;
+          if (head < rp.Hq + rp.Hkv) {
+            const float c = cs[d & ~1], sn = cs[(d & ~1) + 1];
+            y = (d & 1) ? fmaf(partner, sn, v * c) : fmaf(-partner, sn, v * c);
+          }
+          if (t != 0 || n[s] >= N || (lane & 7)) continue;
+          if (head < rp.Hq) {
+            rp.q_out[((long)m * rp.Hq + head) * rp.Dh + d] = (bf16)y;
+          } else if (slot >= 0) {
+            const int blk = slot / rp.BS, off = slot - blk * rp.BS;
+            if (head < rp.Hq + rp.Hkv) {
+              rp.kc[(((long)blk * rp.Hkv + head - rp.Hq) * rp.BS + off) * rp.Dh + d] = (bf16)y;
+            } else {
+              const int vh = head - rp.Hq - rp.Hkv;
+              rp.vc[((long)blk * rp.Hkv + vh) * rp.Dh * rp.BS + ((off >> 3) * rp.Dh + d) * 8 + (off & 7)] = (bf16)y;
+            }
+          }
+        }
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int m = 0; m < MT; ++m) {
     if (m < M) {
@@ -204,10 +255,10 @@ LA_DEV void gv_store(const float (&acc)[MT][RS], const int (&n)[RS], int N, int 
   }
 }
 
-template <int MT, int NT, int EARLY, int RS>
+template <int MT, int NT, int EARLY, int RS, int PD = 0>
 LA_DEV void gv_q4k(const QW& w, int row0, const bf16* X, int ldx, const GVAct& act, int M, int kper, float* o,
                    int ldo, int col0,
-                   int8_t* xq, int* bs, float* dx) {
+                   int8_t* xq, int* bs, float* dx, const GVRope& rp) {
   const int k0 = blockIdx.y * kper, nsb = kper >> 8, sb0 = k0 >> 8;
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = lane >> 3, t = lane & 7;
@@ -258,7 +309,81 @@ LA_DEV void gv_q4k(const QW& w, int row0, const bf16* X, int ldx, const GVAct& a
   for (int m = 0; m < MT; ++m)
 #pragma unroll
     for (int s = 0; s < RS; ++s) acc[m][s] = 0.f;
+  if constexpr (PD > 0) {
+    // PD-deep register ring (nsb % PD == 0, host-checked): super-block sb lives in slot sb % PD and
+    // the slot is refilled with sb + PD right after use, so PD super-blocks stay in flight (a
+    // split-K-1 workgroup walks all 16 super-blocks of a 4096-wide row serially)
+    u32x4 qr[PD][RS];
+    uint32_t sr[PD][RS], dr[PD][RS];
+#pragma unroll
+    for (int s = 0; s < RS; ++s) {
+      qr[0][s] = qa[s];
+      sr[0][s] = sa[s];
+      dr[0][s] = da[s];
+    }
+#pragma unroll
+    for (int i = 1; i < PD; ++i)
+#pragma unroll
+      for (int s = 0; s < RS; ++s) {
+        qr[i][s] = ldg16<NT>(qp[s] + i * 128);
+        sr[i][s] = *(const uint32_t*)(sp[s] + i * 16);
+        dr[i][s] = *(const uint32_t*)(dp[s] + i * 4);
+      }
+    for (int sb0 = 0; sb0 < nsb; sb0 += PD) {
+#pragma unroll
+      for (int i = 0; i < PD; ++i) {
+        const int sb = sb0 + i;
+#pragma unroll
+        for (int s = 0; s < RS; ++s) {
+          qa[s] = qr[i][s];
+          sa[s] = sr[i][s];
+          da[s] = dr[i][s];
+        }
+        const int nx = min(sb + PD, nsb - 1);  // clamped tail reload: harmless, keeps the ring uniform
+#pragma unroll
+        for (int s = 0; s < RS; ++s) {
+          qr[i][s] = ldg16<NT>(qp[s] + nx * 128);
+          sr[i][s] = *(const uint32_t*)(sp[s] + nx * 16);
+          dr[i][s] = *(const uint32_t*)(dp[s] + nx * 4);
+        }
+        // unpack the nibbles once, reuse for every activation row
+        u32x4 lo[RS], hi[RS];
+    #pragma unroll
+        for (int s = 0; s < RS; ++s) {
+    #pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            lo[s][i] = qa[s][i] & 0x0F0F0F0Fu;
+            hi[s][i] = (qa[s][i] >> 4) & 0x0F0F0F0Fu;
+          }
+        }
+    #pragma unroll
+        for (int m = 0; m < MT; ++m) {
+          if (m < M) {
+            const int8_t* xm = xq + m * kper + sb * 256;
+            const u32x4 xl = *(const u32x4*)(xm + xlo);
+            const u32x4 xh = *(const u32x4*)(xm + xlo + 32);
+            const int* bm = bs + m * (kper >> 4) + sb * 16;
+            const float* dm = dx + m * (kper >> 5) + sb * 8;
+            const float dxl = dm[2 * j], dxh = dm[2 * j + 1];
+            const float bl = (float)bm[blo] * dxl, bh = (float)bm[blo + 2] * dxh;
+    #pragma unroll
+            for (int s = 0; s < RS; ++s) {
+              int dl = dot4(lo[s][0], xl[0], 0), dh = dot4(hi[s][0], xh[0], 0);
+              dl = dot4(lo[s][1], xl[1], dl); dh = dot4(hi[s][1], xh[1], dh);
+              dl = dot4(lo[s][2], xl[2], dl); dh = dot4(hi[s][2], xh[2], dh);
+              dl = dot4(lo[s][3], xl[3], dl); dh = dot4(hi[s][3], xh[3], dh);
+              const uint32_t sc = sa[s];
+              const float fs = fmaf((float)(dl * (int)(sc & 0xFFu)), dxl, (float)(dh * (int)((sc >> 16) & 0xFFu)) * dxh);
+              const float fm = fmaf((float)((sc >> 8) & 0xFFu), bl, (float)(sc >> 24) * bh);
+              const float d = h2f((uint16_t)(da[s] & 0xFFFFu)), dmin = h2f((uint16_t)(da[s] >> 16));
+              acc[m][s] = fmaf(d, fs, fmaf(-dmin, fm, acc[m][s]));
+            }
+          }
+        }
 
+      }
+    }
+  } else {
   for (int sb = 0; sb < nsb; ++sb) {
     u32x4 qn[RS];
     uint32_t sn[RS], dn[RS];
@@ -313,13 +438,14 @@ LA_DEV void gv_q4k(const QW& w, int row0, const bf16* X, int ldx, const GVAct& a
       }
     }
   }
-  gv_store<MT, RS>(acc, n, w.N, M, t, o, ldo, col0);
+  }
+  gv_store<MT, RS>(acc, n, w.N, M, t, o, ldo, col0, rp);
 }
 
-template <int MT, int NT, int EARLY, int RS>
+template <int MT, int NT, int EARLY, int RS, int PD = 0>
 LA_DEV void gv_q6k(const QW& w, int row0, const bf16* X, int ldx, const GVAct& act, int M, int kper, float* o,
                    int ldo, int col0,
-                   int8_t* xq, int* bs, float* dx) {
+                   int8_t* xq, int* bs, float* dx, const GVRope& rp) {
   const int k0 = blockIdx.y * kper, nsb = kper >> 8, sb0 = k0 >> 8;
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = lane >> 3, t = lane & 7;
@@ -377,7 +503,81 @@ LA_DEV void gv_q6k(const QW& w, int row0, const bf16* X, int ldx, const GVAct& a
   for (int m = 0; m < MT; ++m)
 #pragma unroll
     for (int s = 0; s < RS; ++s) acc[m][s] = 0.f;
-
+  if constexpr (PD > 0) {
+    // PD-deep register ring, as in gv_q4k
+    u32x4 lr[PD][RS], hr[PD][RS];
+    u32x2 cr[PD][RS];
+    uint32_t dr[PD][RS];
+#pragma unroll
+    for (int s = 0; s < RS; ++s) {
+      lr[0][s] = la_[s];
+      hr[0][s] = ha[s];
+      cr[0][s] = ca[s];
+      dr[0][s] = da[s];
+    }
+#pragma unroll
+    for (int i = 1; i < PD; ++i)
+#pragma unroll
+      for (int s = 0; s < RS; ++s) {
+        lr[i][s] = ldg16<NT>(lp[s] + i * 128);
+        hr[i][s] = ldg16<NT>(hp[s] + i * 64);
+        cr[i][s] = *(const u32x2*)(cp[s] + i * 16);
+        dr[i][s] = *(const uint16_t*)(dp[s] + i * 2);
+      }
+    for (int sb0 = 0; sb0 < nsb; sb0 += PD) {
+#pragma unroll
+      for (int i = 0; i < PD; ++i) {
+        const int sb = sb0 + i;
+#pragma unroll
+        for (int s = 0; s < RS; ++s) {
+          la_[s] = lr[i][s];
+          ha[s] = hr[i][s];
+          ca[s] = cr[i][s];
+          da[s] = dr[i][s];
+        }
+        const int nx = min(sb + PD, nsb - 1);
+#pragma unroll
+        for (int s = 0; s < RS; ++s) {
+          lr[i][s] = ldg16<NT>(lp[s] + nx * 128);
+          hr[i][s] = ldg16<NT>(hp[s] + nx * 64);
+          cr[i][s] = *(const u32x2*)(cp[s] + nx * 16);
+          dr[i][s] = *(const uint16_t*)(dp[s] + nx * 2);
+        }
+    u32x4 lo[RS], hi[RS];
+#pragma unroll
+    for (int s = 0; s < RS; ++s) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        lo[s][i] = (la_[s][i] & 0x0F0F0F0Fu) | ((ha[s][i] << shl) & 0x30303030u);
+        hi[s][i] = ((la_[s][i] >> 4) & 0x0F0F0F0Fu) | ((ha[s][i] >> shr) & 0x30303030u);
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      if (m < M) {
+        const int8_t* xm = xq + m * kper + sb * 256;
+        const u32x4 xl = *(const u32x4*)(xm + xlo);
+        const u32x4 xh = *(const u32x4*)(xm + xlo + 64);
+        const int* bm = bs + m * (kper >> 4) + sb * 16;
+        const int bl = -32 * bm[blo], bh = -32 * bm[blo + 4];
+        const float* dm = dx + m * (kper >> 5) + sb * 8;
+        const float dxl = dm[xlo >> 5], dxh = dm[(xlo >> 5) + 2];
+#pragma unroll
+        for (int s = 0; s < RS; ++s) {
+          int dl = dot4(lo[s][0], xl[0], bl), dh = dot4(hi[s][0], xh[0], bh);
+          dl = dot4(lo[s][1], xl[1], dl); dh = dot4(hi[s][1], xh[1], dh);
+          dl = dot4(lo[s][2], xl[2], dl); dh = dot4(hi[s][2], xh[2], dh);
+          dl = dot4(lo[s][3], xl[3], dl); dh = dot4(hi[s][3], xh[3], dh);
+          const int sl = __builtin_amdgcn_sbfe((int)ca[s].x, scb, 8);
+          const int sh = __builtin_amdgcn_sbfe((int)ca[s].y, scb, 8);
+          const float d = h2f((uint16_t)da[s]);
+          acc[m][s] = fmaf(d, fmaf((float)(dl * sl), dxl, (float)(dh * sh) * dxh), acc[m][s]);
+        }
+      }
+    }
+      }
+    }
+  } else {
   for (int sb = 0; sb < nsb; ++sb) {
     u32x4 ln[RS], hn[RS];
     u32x2 cn[RS];
@@ -433,7 +633,8 @@ LA_DEV void gv_q6k(const QW& w, int row0, const bf16* X, int ldx, const GVAct& a
       }
     }
   }
-  gv_store<MT, RS>(acc, n, w.N, M, t, o, ldo, col0);
+  }
+  gv_store<MT, RS>(acc, n, w.N, M, t, o, ldo, col0, rp);
 }
 
 // Segments [0, nA) are format FA, [nA, nseg) format FB (a q|k + v fusion is (Q4_K, Q6_K)).
@@ -441,7 +642,7 @@ LA_DEV void gv_q6k(const QW& w, int row0, const bf16* X, int ldx, const GVAct& a
 template <int MT, int FA, int FB, int VAR>
 __global__ __launch_bounds__(GV_THREADS) void qgemv_dp4_kernel(GVArgs a, const bf16* __restrict__ X, int ldx,
                                                                GVAct act, int M, int kper, float* __restrict__ out,
-                                                               int ldo, long slab) {
+                                                               int ldo, long slab, GVRope rp) {
   extern __shared__ __attribute__((aligned(16))) uint8_t gv_lds[];
   int8_t* xq = (int8_t*)gv_lds;                                      // [MT][kper]
   int* bs = (int*)(gv_lds + MT * kper);                              // [MT][kper/16]
@@ -453,14 +654,14 @@ __global__ __launch_bounds__(GV_THREADS) void qgemv_dp4_kernel(GVArgs a, const b
   constexpr int RS = gv_rs<VAR>();
   const int row0 = (blk - (seg ? a.blk_end[seg - 1] : 0)) * (32 * RS);
   float* o = out + (size_t)blockIdx.y * slab;
-  constexpr int NT = VAR & 1, EARLY = (VAR >> 1) & 1;
+  constexpr int NT = VAR & 1, EARLY = (VAR >> 1) & 1, PD = (VAR & 16) ? 4 : 0;
   const bool fa = FA == FB || a.fmt[seg] == FA;
   if (fa) {
-    if constexpr (FA == FMT_Q4_K) gv_q4k<MT, NT, EARLY, RS>(a.w[seg], row0, X, ldx, act, M, kper, o, ldo, a.col0[seg], xq, bs, dx);
-    else gv_q6k<MT, NT, EARLY, RS>(a.w[seg], row0, X, ldx, act, M, kper, o, ldo, a.col0[seg], xq, bs, dx);
+    if constexpr (FA == FMT_Q4_K) gv_q4k<MT, NT, EARLY, RS, PD>(a.w[seg], row0, X, ldx, act, M, kper, o, ldo, a.col0[seg], xq, bs, dx, rp);
+    else gv_q6k<MT, NT, EARLY, RS, PD>(a.w[seg], row0, X, ldx, act, M, kper, o, ldo, a.col0[seg], xq, bs, dx, rp);
   } else if constexpr (FA != FB) {
-    if constexpr (FB == FMT_Q4_K) gv_q4k<MT, NT, EARLY, RS>(a.w[seg], row0, X, ldx, act, M, kper, o, ldo, a.col0[seg], xq, bs, dx);
-    else gv_q6k<MT, NT, EARLY, RS>(a.w[seg], row0, X, ldx, act, M, kper, o, ldo, a.col0[seg], xq, bs, dx);
+    if constexpr (FB == FMT_Q4_K) gv_q4k<MT, NT, EARLY, RS, PD>(a.w[seg], row0, X, ldx, act, M, kper, o, ldo, a.col0[seg], xq, bs, dx, rp);
+    else gv_q6k<MT, NT, EARLY, RS, PD>(a.w[seg], row0, X, ldx, act, M, kper, o, ldo, a.col0[seg], xq, bs, dx, rp);
   }
 }
 
@@ -472,15 +673,19 @@ static int g_gv_variant = 5;  // non-temporal weight loads, x staged first, one 
 
 template <int MT, int FA, int FB>
 static int launch_gv(const GVArgs& a, int nblk, int K, const bf16* X, int ldx, const GVAct& act, int M, int splits,
-                     float* out, int ldo, long slab, hipStream_t st) {
+                     float* out, int ldo, long slab, hipStream_t st, const GVRope& rp) {
   const int kper = K / splits;
   const size_t lds = gv_lds_bytes(MT, kper);
   if (lds > 64 * 1024) return -3;
   dim3 grid(nblk, splits);
-  switch (g_gv_variant) {
+  // the fused-RoPE launch runs split-K 1: each workgroup walks the whole row, so it takes the
+  // 4-deep weight ring (VAR bit 4) of the default variant
+  int var = (rp.q_out && g_gv_variant == 5) ? 21 : g_gv_variant;
+  if ((var & 16) && ((kper >> 8) % 4)) var &= ~16;  // the ring walks whole groups of 4 super-blocks
+  switch (var) {
 #define GV_CASE(V) \
-    case V: hipLaunchKernelGGL((qgemv_dp4_kernel<MT, FA, FB, V>), grid, dim3(GV_THREADS), lds, st, a, X, ldx, act, M, kper, out, ldo, slab); break;
-    GV_CASE(0) GV_CASE(1) GV_CASE(2) GV_CASE(3) GV_CASE(5) GV_CASE(9)
+    case V: hipLaunchKernelGGL((qgemv_dp4_kernel<MT, FA, FB, V>), grid, dim3(GV_THREADS), lds, st, a, X, ldx, act, M, kper, out, ldo, slab, rp); break;
+    GV_CASE(0) GV_CASE(1) GV_CASE(2) GV_CASE(3) GV_CASE(5) GV_CASE(9) GV_CASE(21)
 #undef GV_CASE
     default: return -4;
   }
@@ -489,10 +694,10 @@ static int launch_gv(const GVArgs& a, int nblk, int K, const bf16* X, int ldx, c
 
 template <int FA, int FB>
 static int launch_gv_m(const GVArgs& a, int nblk, int K, const bf16* X, int ldx, const GVAct& act, int M, int splits,
-                       float* out, int ldo, long slab, hipStream_t st) {
-  if (M == 1) return launch_gv<1, FA, FB>(a, nblk, K, X, ldx, act, M, splits, out, ldo, slab, st);
-  if (M == 2) return launch_gv<2, FA, FB>(a, nblk, K, X, ldx, act, M, splits, out, ldo, slab, st);
-  return launch_gv<4, FA, FB>(a, nblk, K, X, ldx, act, M, splits, out, ldo, slab, st);
+                       float* out, int ldo, long slab, hipStream_t st, const GVRope& rp) {
+  if (M == 1) return launch_gv<1, FA, FB>(a, nblk, K, X, ldx, act, M, splits, out, ldo, slab, st, rp);
+  if (M == 2) return launch_gv<2, FA, FB>(a, nblk, K, X, ldx, act, M, splits, out, ldo, slab, st, rp);
+  return launch_gv<4, FA, FB>(a, nblk, K, X, ldx, act, M, splits, out, ldo, slab, st, rp);
 }
 
 }  // namespace la
@@ -503,10 +708,10 @@ static int launch_gv_m(const GVArgs& a, int nblk, int K, const bf16* X, int ldx,
 // Q6_K planes: p0 = ql, p1 = qh, p2 = sc, p3 = d.
 // act_p != null: x is act(gate|up) computed from fp32 slabs act_p [act_S][M][W] (X unused),
 // W = 2K for act_mode 0 (SwiGLU) else K; act_bias optional [W].
-extern "C" int la_qgemv_dp4(int nseg, const int* fmts, const void* const* planes, const int* Ns, int K,
-                            const void* X, int ldx, int M, int splits, void* out, int ldo, long slab,
-                            const void* act_p, long act_slab, int act_S, const void* act_bias, int act_mode,
-                            void* stream) {
+static int qgemv_dp4_impl(int nseg, const int* fmts, const void* const* planes, const int* Ns, int K,
+                          const void* X, int ldx, int M, int splits, void* out, int ldo, long slab,
+                          const void* act_p, long act_slab, int act_S, const void* act_bias, int act_mode,
+                          void* stream, const la::GVRope& rp) {
   using namespace la;
   if (nseg < 1 || nseg > GV_SEGS || M < 1 || M > 4 || (K & 255) || splits < 1 || ((K >> 8) % splits) ||
       slab < (long)M * ldo)
@@ -545,17 +750,43 @@ extern "C" int la_qgemv_dp4(int nseg, const int* fmts, const void* const* planes
   const bf16* x = (const bf16*)X;
   float* o = (float*)out;
   int rc;
-  if (fa == FMT_Q4_K && fb == FMT_Q4_K) rc = launch_gv_m<FMT_Q4_K, FMT_Q4_K>(a, nblk, K, x, ldx, act, M, splits, o, ldo, slab, st);
-  else if (fa == FMT_Q6_K && fb == FMT_Q6_K) rc = launch_gv_m<FMT_Q6_K, FMT_Q6_K>(a, nblk, K, x, ldx, act, M, splits, o, ldo, slab, st);
-  else if (fa == FMT_Q4_K) rc = launch_gv_m<FMT_Q4_K, FMT_Q6_K>(a, nblk, K, x, ldx, act, M, splits, o, ldo, slab, st);
-  else rc = launch_gv_m<FMT_Q6_K, FMT_Q4_K>(a, nblk, K, x, ldx, act, M, splits, o, ldo, slab, st);
+  if (fa == FMT_Q4_K && fb == FMT_Q4_K) rc = launch_gv_m<FMT_Q4_K, FMT_Q4_K>(a, nblk, K, x, ldx, act, M, splits, o, ldo, slab, st, rp);
+  else if (fa == FMT_Q6_K && fb == FMT_Q6_K) rc = launch_gv_m<FMT_Q6_K, FMT_Q6_K>(a, nblk, K, x, ldx, act, M, splits, o, ldo, slab, st, rp);
+  else if (fa == FMT_Q4_K) rc = launch_gv_m<FMT_Q4_K, FMT_Q6_K>(a, nblk, K, x, ldx, act, M, splits, o, ldo, slab, st, rp);
+  else rc = launch_gv_m<FMT_Q6_K, FMT_Q4_K>(a, nblk, K, x, ldx, act, M, splits, o, ldo, slab, st, rp);
   if (rc) return rc;
   return (int)hipGetLastError();
 }
 
+extern "C" int la_qgemv_dp4(int nseg, const int* fmts, const void* const* planes, const int* Ns, int K,
+                            const void* X, int ldx, int M, int splits, void* out, int ldo, long slab,
+                            const void* act_p, long act_slab, int act_S, const void* act_bias, int act_mode,
+                            void* stream) {
+  la::GVRope rp{};
+  return qgemv_dp4_impl(nseg, fmts, planes, Ns, K, X, ldx, M, splits, out, ldo, slab, act_p, act_slab, act_S,
+                        act_bias, act_mode, stream, rp);
+}
+
+// Decode q|k|v projection with RoPE (NORM pairs over the whole head) and the paged K/V append
+// fused into the GEMV epilogue: no split-K (each output row is complete in one workgroup), q to
+// q_out [M][Hq][Dh] bf16, k / v of token m to cache slot slots[m] (skipped when < 0).
+extern "C" int la_qgemv_dp4_rope(int nseg, const int* fmts, const void* const* planes, const int* Ns, int K,
+                                 const void* X, int M, const int* pos, const int* slots, const float* cos_sin,
+                                 int Hq, int Hkv, int Dh, void* q_out, void* kc, void* vc, int BS, void* stream) {
+  if (!q_out || !kc || !vc || !pos || !slots || !cos_sin || (Dh & 1) || Dh < 2 || BS < 8 || (BS & 7)) return -1;
+  if ((K >> 8) % 4) return -1;  // the 4-deep weight ring walks whole groups of 4 super-blocks
+  int W = 0;
+  for (int i = 0; i < nseg; ++i) W += Ns[i];
+  if (W != (Hq + 2 * Hkv) * Dh) return -1;
+  la::GVRope rp{pos, slots, cos_sin, (__bf16*)q_out, (__bf16*)kc, (__bf16*)vc, Hq, Hkv, Dh, BS};
+  // out / slab are unused by the rope epilogue; pass a non-null dummy that passes the checks
+  return qgemv_dp4_impl(nseg, fmts, planes, Ns, K, X, K, M, 1, q_out, W, (long)M * W, nullptr, 0, 0, nullptr, 0,
+                        stream, rp);
+}
+
 // Tuning hook: select the kernel variant (bit 0 non-temporal loads, bit 1 early weight prefetch).
 extern "C" int la_gemv_variant(int v) {
-  if (!(v >= 0 && v <= 3) && v != 5 && v != 9) return -1;
+  if (!(v >= 0 && v <= 3) && v != 5 && v != 9 && v != 21) return -1;
   la::g_gv_variant = v;
   return 0;
 }

@@ -72,3 +72,28 @@ def steady(tr, n_layers):
 
 if __name__ == "__main__":
     main()
+
+
+def by_grid(tr, n_layers, top=16):
+    """Steady-state decode time per (kernel, grid size): separates the shapes one kernel serves
+    (e.g. the GEMV's qkv / o / gate_up / down launches)."""
+    pre = [int(r["End_Timestamp"]) for r in tr if "attn_prefill" in r["Kernel_Name"]]
+    t_cut = max(pre) if pre else 0
+    sel = [r for r in tr if int(r["Start_Timestamp"]) > t_cut]
+    steps = sum(1 for r in sel if "attn_decode" in r["Kernel_Name"]) / n_layers
+    gcol = next((c for c in ("Grid_Size", "Grid_Size_X", "grid_size") if c in sel[0]), None)
+    agg = {}
+    for r in sel:
+        k = (short(r["Kernel_Name"]), r.get(gcol, "?") if gcol else "?")
+        d = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+        c, t = agg.get(k, (0, 0))
+        agg[k] = (c + 1, t + d)
+    print("\n## Steady state by (kernel, grid)\n\n| kernel | grid | calls/step | avg us | us/step |\n|---|---:|---:|---:|---:|")
+    for (k, g), (c, t) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:top]:
+        print(f"| `{k}` | {g} | {c / max(steps, 1):.1f} | {t / c / 1e3:.1f} | {t / 1e3 / max(steps, 1):.1f} |")
+
+
+if __name__ == "__main__" and "--by-grid" in sys.argv:
+    d = sys.argv[1]
+    trace = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)
+    by_grid(list(csv.DictReader(open(trace[0]))), int(sys.argv[sys.argv.index("--by-grid") + 1]))

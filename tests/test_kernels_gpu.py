@@ -566,3 +566,26 @@ def test_dq_gemm_two_weights_side_by_side():
     out = torch.empty(2, M, 416, dtype=torch.float32, device=DEV)
     ops._run_dq(x, ws, 2, out, 416)
     assert (out.sum(0).cpu() - ref).abs().max().item() < 3e-2 * max(1.0, ref.abs().max().item())
+
+
+@pytest.mark.parametrize("M", [1, 2])
+def test_qkv_rope_dp4_fused(M):
+    """q|k|v decode GEMV with RoPE + paged K/V append in its epilogue vs the unfused GEMV + rope_kv
+    (Llama-3 head shape, Q4_K q|k + Q6_K v segments; token 1 of M=2 has no cache slot)."""
+    Hq, Hkv, Dh, BS, K, nblk = 8, 2, 128, 32, 2048, 4
+    qk = _qw((Hq + Hkv) * Dh, K, GGMLType.Q4_K, seed=31)
+    v = _qw(Hkv * Dh, K, GGMLType.Q6_K, seed=32)
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    cs = ops.rope_cos_sin(512, Dh, 500000.0, DEV)
+    pos = torch.tensor([37, 200][:M], dtype=torch.int32, device=DEV)
+    slots = torch.tensor([45, -1][:M], dtype=torch.int32, device=DEV)
+    kc, vc = torch.zeros(nblk, Hkv, BS, Dh, dtype=torch.bfloat16, device=DEV), ops.v_pages(nblk, Hkv, BS, Dh, device=DEV)
+    q = ops.qkv_rope_dp4(x, [qk, v], pos, slots, cs, Hq, Hkv, Dh, kc, vc, BS)
+    kr, vr = torch.zeros_like(kc), torch.zeros_like(vc)
+    qkv = ops.linear_multi(x, [qk, v], force="dp4")
+    qr = ops.rope_kv(qkv, pos, slots, cs, Hq, Hkv, Dh, Dh, 0, kr, vr, BS)
+    tol = 2e-2 * max(1.0, qr.float().abs().max().item())
+    assert (q.float() - qr.float()).abs().max().item() < tol
+    assert (kc.float() - kr.float()).abs().max().item() < tol
+    assert (vc.float() - vr.float()).abs().max().item() < tol
+    assert kc.abs().sum().item() > 0 and vc.abs().sum().item() > 0
