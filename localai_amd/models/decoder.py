@@ -38,11 +38,14 @@ class TPInfo:
     rank: int = 0
     world: int = 1
     group: object = None
+    car: object = None  # parallel.custom_ar.CustomAllReduce (one-shot over xGMI peer buffers) or None
 
     def all_reduce(self, t: torch.Tensor):
         if self.world > 1:
+            if self.car is not None and self.car.supports(t):
+                return self.car.all_reduce(t)   # latency-bound decode rows
             import torch.distributed as dist
-            dist.all_reduce(t, group=self.group)
+            dist.all_reduce(t, group=self.group)  # RCCL: prefill chunks, CPU (gloo)
         return t
 
     def all_gather_cols(self, t: torch.Tensor) -> torch.Tensor:

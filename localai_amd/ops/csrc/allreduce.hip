@@ -1,0 +1,162 @@
+// One-shot all-reduce over peer-mapped IPC buffers, for the latency-bound tensor-parallel decode
+// messages (SURVEY §2.9 "Planned TP collective shapes", §2.11: "custom one-shot / two-shot
+// all-reduce kernels over peer-mapped IPC buffers for latency-critical decode messages").
+//
+// On an 8-GPU MI355X node every GPU has a direct xGMI link to each of its 7 peers, so a
+// one-shot read-reduce (every rank reads every peer's chunk directly) uses all links at once,
+// where a ring would move each byte over one link per step; a 16 KiB decode row is two orders of
+// magnitude below the size where bandwidth matters, so the cost is one flag round trip.
+//
+// Buffers: every rank owns one hipMalloc'd region, exported with hipIpcGetMemHandle and opened by
+// the other ranks (parallel/custom_ar.py):
+//   [flags  : AR_MAXB blocks x AR_MAXR ranks int32]   epochs written by the PEERS
+//   [counter: AR_MAXB int32]                          this rank's per-block call count
+//   [err    : int32]                                  set when a wait timed out
+//   [data   : 2 slots x AR_MAXB x 4 KiB]              this rank's input, by epoch parity
+// Block b always owns elements [1024 b, 1024 b + 1024) and the 4 KiB at 4096 b of a slot, whatever
+// the message size or element type, so every block is an independent channel (its own flag row,
+// counter and data bytes) and calls of different sizes can follow each other freely.
+// Protocol, per block b (one chunk of the message), call epoch e (= ++counter[b]), slot e & 1:
+//   1. copy the chunk of the local input into the own data slot;
+//   2. release (system scope), then store e into flag[b][rank] of every PEER buffer;
+//   3. wait until flag[b][q] >= e for every peer q in the own buffer (bounded spin: a dead peer
+//      sets err and the block proceeds instead of hanging the GPU), then acquire (system scope);
+//   4. out[chunk] = sum over ranks 0..R-1 in rank order (fp32), so every rank gets the same bits.
+// Two data slots suffice without a closing barrier: a peer signals call n+1 only after its call n
+// kernel (all of its reads of slot n & 1) has completed, and this rank rewrites that slot at call
+// n+2, after it has seen those signals.  Each block touches only its own chunk, flag row and
+// counter, so there is no grid-wide synchronisation and the kernel replays inside a hipGraph.
+#include "common.h"
+
+namespace la {
+
+constexpr int AR_MAXB = 256;  // blocks (chunks) per call
+constexpr int AR_MAXR = 8;    // ranks
+constexpr int AR_T = 256;
+constexpr long AR_FLAGS = 0, AR_COUNTER = AR_MAXB * AR_MAXR * 4, AR_ERR = AR_COUNTER + AR_MAXB * 4;
+constexpr long AR_DATA = 16384;  // data area offset (header rounded up)
+constexpr long AR_CHUNK = 1024;  // elements per block
+constexpr long AR_SLOT = AR_MAXB * AR_CHUNK * 4;  // bytes per parity slot (1 MiB)
+
+struct ARArgs {
+  const void* in;
+  void* out;
+  long n;          // elements
+  int bf16;        // element type: 1 bf16, 0 fp32
+  int rank, world;
+  uint8_t* bufs[AR_MAXR];
+  long spin_limit;
+};
+
+LA_DEV int ar_load_flag(const int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); }
+
+__global__ __launch_bounds__(AR_T) void allreduce_oneshot_kernel(ARArgs a) {
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const long e0 = (long)b * AR_CHUNK;
+  const long e1 = min(a.n, e0 + AR_CHUNK);
+  uint8_t* own = a.bufs[a.rank];
+  int* counter = (int*)(own + AR_COUNTER) + b;
+  const int ep = *counter + 1;
+  const long slot = AR_DATA + (long)(ep & 1) * AR_SLOT + (long)b * AR_CHUNK * 4;  // this block's 4 KiB
+  const int esz = a.bf16 ? 2 : 4;
+
+  // 1. local chunk -> own data slot (16-byte vectors; e0 and e1 - e0 are multiples of 8 elements
+  //    except possibly the message tail, handled element-wise)
+  {
+    const uint8_t* src = (const uint8_t*)a.in + e0 * esz;
+    uint8_t* dst = own + slot;
+    const long bytes = (e1 - e0) * esz, v16 = bytes >> 4;
+    for (long i = tid; i < v16; i += AR_T) ((u32x4*)dst)[i] = ((const u32x4*)src)[i];
+    for (long i = (v16 << 4) + tid; i < bytes; i += AR_T) dst[i] = src[i];
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave's stores have left it
+  __syncthreads();
+  // 2. publish: the chunk reaches memory before the flag (system-scope release by the signalling lanes)
+  if (tid < a.world && tid != a.rank) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int* peer_flag = (int*)(a.bufs[tid] + AR_FLAGS) + b * AR_MAXR + a.rank;
+    __hip_atomic_store(peer_flag, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  // 3. wait for every peer's chunk b of this epoch (bounded)
+  if (tid < a.world && tid != a.rank) {
+    const int* f = (const int*)(own + AR_FLAGS) + b * AR_MAXR + tid;
+    long spins = 0;
+    while (ar_load_flag(f) < ep) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > a.spin_limit) {
+        __hip_atomic_store((int*)(own + AR_ERR), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: peers' data, not stale lines
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  // 4. reduce in rank order (identical bits on every rank)
+  for (long i = e0 + tid * 8; i < e1; i += AR_T * 8) {
+    const int cnt = (int)min(8L, e1 - i);
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int r = 0; r < a.world; ++r) {
+      const uint8_t* src = a.bufs[r] + slot + (i - e0) * esz;
+      if (a.bf16) {
+        if (cnt == 8) {
+          const bf16x8 v = *(const bf16x8*)src;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[j] += (float)v[j];
+        } else {
+          for (int j = 0; j < cnt; ++j) acc[j] += (float)((const bf16*)src)[j];
+        }
+      } else {
+        if (cnt == 8) {
+          const f32x4 v0 = *(const f32x4*)src, v1 = *(const f32x4*)(src + 16);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            acc[j] += v0[j];
+            acc[j + 4] += v1[j];
+          }
+        } else {
+          for (int j = 0; j < cnt; ++j) acc[j] += ((const float*)src)[j];
+        }
+      }
+    }
+    if (a.bf16) {
+      bf16* o = (bf16*)a.out + i;
+      for (int j = 0; j < cnt; ++j) o[j] = (bf16)acc[j];
+    } else {
+      float* o = (float*)a.out + i;
+      for (int j = 0; j < cnt; ++j) o[j] = acc[j];
+    }
+  }
+  if (tid == 0) *counter = ep;
+}
+
+}  // namespace la
+
+// C ABI ---------------------------------------------------------------------------
+extern "C" long la_ar_buffer_bytes() { return la::AR_DATA + 2 * la::AR_SLOT; }
+extern "C" long la_ar_max_elems() { return la::AR_MAXB * la::AR_CHUNK; }
+extern "C" long la_ar_err_offset() { return la::AR_ERR; }
+
+// bufs: world device pointers (own + opened peers) of regions of la_ar_buffer_bytes() bytes.
+extern "C" int la_allreduce_oneshot(const void* in, void* out, long n, int bf16, int rank, int world,
+                                    const void* const* bufs, long spin_limit, void* stream) {
+  using namespace la;
+  if (world < 1 || world > AR_MAXR || rank < 0 || rank >= world || n < 1) return -1;
+  if (n > AR_MAXB * AR_CHUNK) return -2;
+  ARArgs a{};
+  a.in = in;
+  a.out = out;
+  a.n = n;
+  a.bf16 = bf16;
+  a.rank = rank;
+  a.world = world;
+  a.spin_limit = spin_limit;
+  for (int r = 0; r < world; ++r) {
+    if (!bufs[r]) return -1;
+    a.bufs[r] = (uint8_t*)bufs[r];
+  }
+  const int nb = (int)((n + AR_CHUNK - 1) / AR_CHUNK);
+  hipLaunchKernelGGL(allreduce_oneshot_kernel, dim3(nb), dim3(AR_T), 0, (hipStream_t)stream, a);
+  return (int)hipGetLastError();
+}

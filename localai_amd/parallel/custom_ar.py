@@ -1,0 +1,173 @@
+"""One-shot all-reduce over IPC-mapped peer buffers (ops/csrc/allreduce.hip) for the tensor-parallel
+decode messages; RCCL stays the path for anything larger (prefill chunks) or when peer mapping is
+unavailable.  SURVEY §2.9 (planned TP collective shapes) and §2.11 (custom one-shot all-reduce
+over peer-mapped IPC buffers, hipIpcGetMemHandle).  The reference has no collective of its own:
+its only tensor parallelism is vLLM's NCCL (backend/python/vllm/backend.py:102-103).
+
+Setup (once per TP group): every rank hipMallocs one region (flags, per-block call counters, two
+1 MiB data slots), exports it with hipIpcGetMemHandle, all-gathers the 64-byte handles over the
+group, and opens the peers' handles with hipIpcOpenMemHandle.  Each call is then one kernel on
+the caller's stream -- capturable in the decode hipGraph, since the per-block epochs live in
+device memory.
+"""
+from __future__ import annotations
+
+import ctypes
+import logging
+import os
+from typing import List, Optional
+
+import torch
+
+log = logging.getLogger("localai_amd.custom_ar")
+
+HIP_IPC_HANDLE_SIZE = 64
+_hipIpcMemLazyEnablePeerAccess = 0x1
+
+
+class _HipIpcHandle(ctypes.Structure):
+    _fields_ = [("reserved", ctypes.c_char * HIP_IPC_HANDLE_SIZE)]
+
+
+def _hip():
+    """The HIP runtime torch itself loaded (one runtime per process)."""
+    import torch.cuda  # noqa: F401
+    lib = os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so")
+    h = ctypes.CDLL(lib if os.path.exists(lib) else "libamdhip64.so")
+    h.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
+    h.hipFree.argtypes = [ctypes.c_void_p]
+    h.hipMemset.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t]
+    h.hipIpcGetMemHandle.argtypes = [ctypes.POINTER(_HipIpcHandle), ctypes.c_void_p]
+    h.hipIpcOpenMemHandle.argtypes = [ctypes.POINTER(ctypes.c_void_p), _HipIpcHandle, ctypes.c_uint]
+    h.hipIpcCloseMemHandle.argtypes = [ctypes.c_void_p]
+    h.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    for f in ("hipMalloc", "hipFree", "hipMemset", "hipIpcGetMemHandle", "hipIpcOpenMemHandle",
+              "hipIpcCloseMemHandle", "hipMemcpy"):
+        getattr(h, f).restype = ctypes.c_int
+    return h
+
+
+class CustomAllReduce:
+    """In-place sum over the ranks of `group` for fp32 / bf16 tensors of at most `max_elems`."""
+
+    # ~1 s of polling (s_sleep 2 + one system-scope load per poll): a peer that never arrives costs one bounded wait
+    # (err flag set, result wrong) instead of a hung GPU
+    SPIN_LIMIT = 1 << 20
+
+    def __init__(self, group, rank: int, world: int, device: torch.device):
+        from .. import ops
+        import torch.distributed as dist
+        if world < 2 or world > 8:
+            raise ValueError("custom all-reduce needs 2..8 ranks")
+        self.rank, self.world, self.device = rank, world, torch.device(device)
+        self.L = ops.lib()
+        self.L.la_ar_buffer_bytes.restype = ctypes.c_long
+        self.L.la_ar_max_elems.restype = ctypes.c_long
+        self.L.la_ar_err_offset.restype = ctypes.c_long
+        self.L.la_allreduce_oneshot.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_long, ctypes.c_int,
+                                                ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_long,
+                                                ctypes.c_void_p]
+        self.L.la_allreduce_oneshot.restype = ctypes.c_int
+        self.max_elems = int(self.L.la_ar_max_elems())
+        self.nbytes = int(self.L.la_ar_buffer_bytes())
+        self.hip = _hip()
+        self.own = None
+        self._opened: List[int] = []
+        err = ""
+        with torch.cuda.device(self.device):
+            # every rank reaches every collective below whatever fails locally, and all of them
+            # agree at the end: a group where one rank cannot map a peer must stay on RCCL
+            hb = b""
+            try:
+                ptr = ctypes.c_void_p()
+                self._check(self.hip.hipMalloc(ctypes.byref(ptr), self.nbytes), "hipMalloc")
+                self.own = ptr.value
+                self._check(self.hip.hipMemset(ctypes.c_void_p(self.own), 0, self.nbytes), "hipMemset")
+                torch.cuda.synchronize(self.device)
+                hnd = _HipIpcHandle()
+                self._check(self.hip.hipIpcGetMemHandle(ctypes.byref(hnd), ctypes.c_void_p(self.own)),
+                            "hipIpcGetMemHandle")
+                hb = ctypes.string_at(ctypes.addressof(hnd), HIP_IPC_HANDLE_SIZE)  # .reserved stops at a NUL
+            except Exception as e:  # noqa: BLE001
+                err = str(e)
+            handles: List[Optional[bytes]] = [None] * world
+            dist.all_gather_object(handles, hb, group=group)
+            self.ptrs: List[int] = []
+            for r, h_bytes in enumerate(handles):
+                if r == rank:
+                    self.ptrs.append(self.own or 0)
+                    continue
+                if err or not h_bytes or len(h_bytes) != HIP_IPC_HANDLE_SIZE:
+                    err = err or f"rank {r} exported no handle"
+                    self.ptrs.append(0)
+                    continue
+                try:
+                    h = _HipIpcHandle()
+                    ctypes.memmove(ctypes.addressof(h), h_bytes, HIP_IPC_HANDLE_SIZE)
+                    p = ctypes.c_void_p()
+                    self._check(self.hip.hipIpcOpenMemHandle(ctypes.byref(p), h, _hipIpcMemLazyEnablePeerAccess),
+                                f"hipIpcOpenMemHandle(rank {r})")
+                    self.ptrs.append(p.value)
+                    self._opened.append(p.value)
+                except Exception as e:  # noqa: BLE001
+                    err = str(e)
+                    self.ptrs.append(0)
+            oks: List[Optional[str]] = [None] * world
+            dist.all_gather_object(oks, err, group=group)
+            bad = [f"rank {r}: {m}" for r, m in enumerate(oks) if m]
+            if bad:
+                self.close()
+                raise RuntimeError("; ".join(bad))
+        self._bufs = (ctypes.c_void_p * world)(*self.ptrs)
+
+    @staticmethod
+    def _check(rc: int, what: str):
+        if rc != 0:
+            raise RuntimeError(f"{what} failed with hipError {rc}")
+
+    def supports(self, t: torch.Tensor) -> bool:
+        return (t.is_cuda and t.dtype in (torch.float32, torch.bfloat16) and t.is_contiguous()
+                and 0 < t.numel() <= self.max_elems)
+
+    def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
+        """In place; the caller checks supports(t).  Runs on the current stream."""
+        rc = self.L.la_allreduce_oneshot(t.data_ptr(), t.data_ptr(), t.numel(), int(t.dtype == torch.bfloat16),
+                                         self.rank, self.world, self._bufs, self.SPIN_LIMIT,
+                                         torch.cuda.current_stream(self.device).cuda_stream)
+        if rc != 0:
+            raise RuntimeError(f"la_allreduce_oneshot failed with code {rc}")
+        return t
+
+    def timed_out(self) -> bool:
+        """True if a wait ever hit the spin limit (a peer never arrived): results since are suspect."""
+        v = ctypes.c_int(0)
+        torch.cuda.synchronize(self.device)
+        self._check(self.hip.hipMemcpy(ctypes.byref(v), ctypes.c_void_p(self.own + int(self.L.la_ar_err_offset())),
+                                       4, 2), "hipMemcpy")  # hipMemcpyDeviceToHost
+        return v.value != 0
+
+    def close(self):
+        if getattr(self, "own", None) is None:
+            return
+        try:
+            torch.cuda.synchronize(self.device)
+            for p in self._opened:
+                self.hip.hipIpcCloseMemHandle(ctypes.c_void_p(p))
+            self._opened = []
+            self.hip.hipFree(ctypes.c_void_p(self.own))
+        finally:
+            self.own = None
+
+
+def maybe_create(group, rank: int, world: int, device) -> Optional[CustomAllReduce]:
+    """A CustomAllReduce for a GPU TP group, or None (CPU, a single rank, LOCALAI_AMD_CUSTOM_AR=0,
+    or peer mapping refused) -- callers then keep RCCL."""
+    if world < 2 or not torch.cuda.is_available() or str(device) == "cpu":
+        return None
+    if os.environ.get("LOCALAI_AMD_CUSTOM_AR", "1") == "0":
+        return None
+    try:
+        return CustomAllReduce(group, rank, world, torch.device(device))
+    except Exception as e:  # noqa: BLE001 - no IPC / peer access: RCCL only
+        log.warning("custom all-reduce unavailable (%s); using RCCL", e)
+        return None

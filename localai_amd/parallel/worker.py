@@ -45,6 +45,9 @@ def build_engine(args, rank, world, dev, ctrl):
     from ..engine.llm_engine import EngineConfig, LLMEngine
     from ..models.decoder import TPInfo
     tp = TPInfo(rank=rank, world=world, group=dist.group.WORLD if world > 1 else None)
+    if world > 1:
+        from .custom_ar import maybe_create
+        tp.car = maybe_create(dist.group.WORLD, rank, world, dev)
     cfg = EngineConfig(model_path=args.model, device=dev, context_size=args.context, max_num_seqs=args.max_num_seqs,
                        max_batched_tokens=args.max_batched_tokens, use_graphs=not args.eager,
                        decode_steps=args.decode_steps)

@@ -1,0 +1,85 @@
+"""Two-or-more-rank check of the one-shot IPC all-reduce (parallel/custom_ar.py): exact rank-ordered
+sums for fp32 / bf16 messages of 1, 3 and 64 decode rows, a ragged tail and the largest size,
+back-to-back calls of different sizes, and replay inside a captured hipGraph.  Launch with
+    python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 scripts/ar_check.py
+Every rank may share one GPU (LOCALAI_AMD_AR_SAME_GPU=1): the buffers are then IPC-mapped inside
+one device, which exercises the whole protocol except the xGMI transport itself."""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+import torch.distributed as dist
+
+from localai_amd.parallel.custom_ar import CustomAllReduce
+
+
+def inputs(rank, n, dtype, dev, call):
+    g = torch.Generator(device="cpu").manual_seed(1000 * call + rank)
+    return torch.randn(n, generator=g).to(dtype).to(dev)
+
+
+def expected(world, n, dtype, dev, call):
+    acc = torch.zeros(n, dtype=torch.float32, device=dev)
+    for r in range(world):
+        acc += inputs(r, n, dtype, dev, call).float()
+    return acc.to(dtype)
+
+
+def main():
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    local = 0 if os.environ.get("LOCALAI_AMD_AR_SAME_GPU") == "1" else int(os.environ.get("LOCAL_RANK", rank))
+    dev = torch.device(f"cuda:{local}")
+    torch.cuda.set_device(dev)
+    dist.init_process_group("gloo")
+    car = CustomAllReduce(dist.group.WORLD, rank, world, dev)
+    cases = [(4096, torch.float32), (3 * 4096, torch.float32), (4096, torch.bfloat16), (1000, torch.float32),
+             (64 * 4096, torch.float32), (car.max_elems, torch.bfloat16), (4096 + 8, torch.bfloat16)]
+    for call, (n, dt) in enumerate(cases):
+        t = inputs(rank, n, dt, dev, call)
+        car.all_reduce(t)
+        torch.cuda.synchronize()
+        ref = expected(world, n, dt, dev, call)
+        err = (t.float() - ref.float()).abs().max().item()
+        assert err == 0.0, (rank, n, dt, err)
+    # graph capture: three calls of mixed sizes, replayed twice with fresh inputs
+    bufs = [torch.empty(n, dtype=dt, device=dev) for n, dt in cases[:3]]
+    srcs = [torch.empty_like(b) for b in bufs]
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            for b, src in zip(bufs, srcs):
+                b.copy_(src)
+                car.all_reduce(b)
+    torch.cuda.current_stream().wait_stream(s)
+    for rep in range(2):
+        for i, (n, dt) in enumerate(cases[:3]):
+            srcs[i].copy_(inputs(rank, n, dt, dev, 100 + 10 * rep + i))
+        dist.barrier()
+        g.replay()
+        torch.cuda.synchronize()
+        for i, (n, dt) in enumerate(cases[:3]):
+            ref = expected(world, n, dt, dev, 100 + 10 * rep + i)
+            assert (bufs[i].float() - ref.float()).abs().max().item() == 0.0, (rank, "graph", rep, i)
+    assert not car.timed_out()
+    # latency of one decode row (same-GPU numbers say nothing about xGMI; recorded for reference)
+    t = inputs(rank, 4096, torch.float32, dev, 7)
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(200):
+        car.all_reduce(t)
+    torch.cuda.synchronize()
+    us = (time.perf_counter() - t0) / 200 * 1e6
+    dist.barrier()
+    car.close()
+    if rank == 0:
+        print(f"AR_OK world={world} one-row all-reduce {us:.1f} us/call")
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

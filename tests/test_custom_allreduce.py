@@ -1,0 +1,27 @@
+"""One-shot IPC all-reduce (ops/csrc/allreduce.hip, parallel/custom_ar.py) with two ranks sharing
+the one GPU of the test box: exact sums, mixed sizes, graph replay (scripts/ar_check.py).  The
+ranks run as child processes of torch.distributed.run, started from here."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.gpu
+def test_custom_allreduce_two_ranks_one_gpu():
+    env = dict(os.environ, LOCALAI_AMD_AR_SAME_GPU="1")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", "29533", os.path.join(ROOT, "scripts", "ar_check.py")],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "AR_OK" in r.stdout, r.stdout[-2000:]
+
+
+def test_tpinfo_falls_back_without_custom_ar():
+    """CPU / gloo TP groups never get a CustomAllReduce (maybe_create returns None)."""
+    from localai_amd.parallel.custom_ar import maybe_create
+    assert maybe_create(None, 0, 2, "cpu") is None
+    assert maybe_create(None, 0, 1, "cuda:0") is None
