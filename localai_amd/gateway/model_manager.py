@@ -227,6 +227,8 @@ class ModelManager:
                "--max-num-seqs", os.environ.get("LOCALAI_MAX_NUM_SEQS", "256")]
         if opts.EnforceEager:
             cmd.append("--eager")
+        if cfg.raw.get("expert_parallel"):  # model-config extension (not in the reference schema)
+            cmd.append("--expert-parallel")
         proc = subprocess.Popen(cmd, env=dict(os.environ))
         h = GRPCBackend(addr)
         g = dict(cfg.raw.get("grpc") or {})

@@ -39,6 +39,7 @@ class TPInfo:
     world: int = 1
     group: object = None
     car: object = None  # parallel.custom_ar.CustomAllReduce (one-shot over xGMI peer buffers) or None
+    ep: bool = False    # MoE layers: expert parallelism (each rank holds E/world whole experts)
 
     def all_reduce(self, t: torch.Tensor):
         if self.world > 1:
@@ -150,6 +151,17 @@ class DecoderModel:
             raise ValueError(f"TP={W} must divide heads ({hp.n_head}/{hp.n_head_kv})")
         self.Hq, self.Hkv, self.Dh = hp.n_head // W, hp.n_head_kv // W, hp.head_dim
         self.F = hp.n_ff // W
+        # expert parallelism: rank R holds experts [R*El, (R+1)*El) whole (no F split).  The MoE input
+        # is replicated across the group (it follows the attention all-reduce), so each rank runs its
+        # local experts for the tokens routed to them and the same all-reduce that closes a TP MLP
+        # sums the experts' weighted outputs: no all-to-all is needed with replicated activations.
+        self.ep = bool(tp.ep and hp.n_expert and W > 1)
+        if self.ep and hp.n_expert % W:
+            raise ValueError(f"expert parallelism {W} must divide the expert count {hp.n_expert}")
+        self.E_local = hp.n_expert // W if self.ep else hp.n_expert
+        self.ep_base = R * self.E_local if self.ep else 0
+        if self.ep:
+            self.F = hp.n_ff
         self.rot = hp.rope_dim or hp.head_dim
         self.scale = 1.0 / math.sqrt(hp.head_dim)
         self.norm_mode = 0 if hp.norm_type == "rms" else 1
@@ -205,10 +217,11 @@ class DecoderModel:
             if hp.n_expert:
                 router = f32(b + "ffn_gate_inp.weight").view(hp.n_expert, hp.n_embd)
                 experts = []
-                for e in range(hp.n_expert):
-                    ge = self._expert_slice(T[b + "ffn_gate_exps.weight"], e, rows=fs)
-                    ue = self._expert_slice(T[b + "ffn_up_exps.weight"], e, rows=fs)
-                    de = self._expert_slice(T[b + "ffn_down_exps.weight"], e, cols=sl(hp.n_ff))
+                for e in range(self.ep_base, self.ep_base + self.E_local):
+                    efs = None if self.ep else fs  # EP: whole experts, TP-within-expert: F slices
+                    ge = self._expert_slice(T[b + "ffn_gate_exps.weight"], e, rows=efs)
+                    ue = self._expert_slice(T[b + "ffn_up_exps.weight"], e, rows=efs)
+                    de = self._expert_slice(T[b + "ffn_down_exps.weight"], e, cols=None if self.ep else sl(hp.n_ff))
                     gu = ops.concat_rows([ge, ue])
                     experts.append(([gu] if gu is not None else [ge, ue], de))
             elif hp.arch == "phi2":
@@ -293,18 +306,25 @@ class DecoderModel:
         logits = xn.float() @ L.router.t()                       # [T, E]
         w, idx = torch.topk(torch.softmax(logits, -1), hp.n_expert_used, -1)
         w = w / w.sum(-1, keepdim=True)
+        El, base = self.E_local, self.ep_base
+        if self.ep:
+            # expert ids of this rank -> 0..El-1; tokens' other picks -> El (a group nobody runs)
+            loc = idx - base
+            idx_l = torch.where((loc >= 0) & (loc < El), loc, torch.full_like(loc, El))
+        else:
+            idx_l = idx
         if L.moe_gu is not None and T <= 64 and xn.is_cuda:
             # graph-capturable grouped path: device routing, one weight stream per active expert,
             # routing-weighted outputs land as extra slabs summed by the next kernel
             k = hp.n_expert_used
-            order, off = ops.moe_route(idx.to(torch.int32), hp.n_expert)
+            order, off = ops.moe_route(idx_l.to(torch.int32), El + 1 if self.ep else El)
             gu = ops.moe_linear(xn, L.moe_gu, order, off, k, T)
             h = ops.act(gu, self.F, ops.ACT_SWIGLU)
             d = ops.moe_linear(h, L.moe_down, order, off, k, T, down=True,
-                               wts=w.reshape(-1).float().contiguous())
+                               wts=w.reshape(-1).float().contiguous(), zero=self.ep)
             return self._row_parallel_out(d, None)
         out = torch.zeros(T, hp.n_embd, dtype=torch.float32, device=xn.device)
-        flat_e = idx.reshape(-1)
+        flat_e = idx_l.reshape(-1)
         flat_t = torch.arange(T, device=xn.device).repeat_interleave(hp.n_expert_used)
         flat_w = w.reshape(-1)
         for e, (gate_up, down) in enumerate(L.experts):

@@ -1229,13 +1229,15 @@ def moe_route(ids: torch.Tensor, E: int, order: Optional[torch.Tensor] = None, o
 
 
 def moe_linear(x: torch.Tensor, mw: MoEWeights, order: torch.Tensor, off: torch.Tensor, topk: int, T: int,
-               down: bool = False, wts: Optional[torch.Tensor] = None) -> Partial:
+               down: bool = False, wts: Optional[torch.Tensor] = None, zero: bool = False) -> Partial:
     """Grouped expert GEMM.  gate/up (down=False): x [T, K] -> Partial [S, T*topk, N] (row = pair).
     down (down=True): x [T*topk, K] (row = pair) -> Partial [S*topk, T, N], each slab scaled by
-    the routing weight, so summing the slabs performs the weighted top-k combine."""
+    the routing weight, so summing the slabs performs the weighted top-k combine.  Pairs routed to
+    an expert id >= mw.E (expert parallelism: another rank's expert) are not computed; with
+    zero=True their down-projection rows read as 0."""
     if not x.is_cuda:
         P = T * topk
-        flat_e = torch.empty(P, dtype=torch.long)
+        flat_e = torch.full((P,), -1, dtype=torch.long)
         offs = off.tolist()
         for e in range(mw.E):
             flat_e[order[offs[e]:offs[e + 1]].long()] = e
@@ -1243,11 +1245,14 @@ def moe_linear(x: torch.Tensor, mw: MoEWeights, order: torch.Tensor, off: torch.
             out = torch.zeros(topk, T, mw.N)
             for p in range(P):
                 t, slot = divmod(p, topk)
+                if flat_e[p] < 0:
+                    continue
                 out[slot, t] = (x[p].float() @ mw.experts[int(flat_e[p])].dequant_f32().t()) * float(wts[p])
         else:
             out = torch.zeros(1, P, mw.N)
             for p in range(P):
-                out[0, p] = x[p // topk].float() @ mw.experts[int(flat_e[p])].dequant_f32().t()
+                if flat_e[p] >= 0:
+                    out[0, p] = x[p // topk].float() @ mw.experts[int(flat_e[p])].dequant_f32().t()
         return Partial(out)
     if x.dtype != torch.bfloat16 or not x.is_contiguous():
         raise ValueError("moe_linear: x must be contiguous bf16")
@@ -1260,7 +1265,8 @@ def moe_linear(x: torch.Tensor, mw: MoEWeights, order: torch.Tensor, off: torch.
         S -= 1
     P = T * topk
     if down:
-        out = torch.empty(S * topk, T, mw.N, dtype=torch.float32, device=x.device)
+        alloc = torch.zeros if zero else torch.empty
+        out = alloc(S * topk, T, mw.N, dtype=torch.float32, device=x.device)
         slab = T * mw.N
     else:
         out = torch.empty(S, P, mw.N, dtype=torch.float32, device=x.device)

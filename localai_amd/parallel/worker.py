@@ -44,7 +44,8 @@ def build_engine(args, rank, world, dev, ctrl):
     import torch.distributed as dist
     from ..engine.llm_engine import EngineConfig, LLMEngine
     from ..models.decoder import TPInfo
-    tp = TPInfo(rank=rank, world=world, group=dist.group.WORLD if world > 1 else None)
+    tp = TPInfo(rank=rank, world=world, group=dist.group.WORLD if world > 1 else None,
+                ep=bool(getattr(args, "expert_parallel", False)))
     if world > 1:
         from .custom_ar import maybe_create
         tp.car = maybe_create(dist.group.WORLD, rank, world, dev)
@@ -65,6 +66,9 @@ def main(argv=None) -> int:
     ap.add_argument("--max-batched-tokens", type=int, default=8192)
     ap.add_argument("--decode-steps", type=int, default=8)
     ap.add_argument("--eager", action="store_true")
+    ap.add_argument("--expert-parallel", action="store_true",
+                    default=os.environ.get("LOCALAI_AMD_EP", "0") == "1",
+                    help="MoE models: each rank holds whole experts (E / world) instead of an F slice of every expert")
     a = ap.parse_args(argv)
     logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s tp-worker %(message)s")
     rank, world, dev, ctrl = init_distributed()

@@ -589,3 +589,30 @@ def test_qkv_rope_dp4_fused(M):
     assert (kc.float() - kr.float()).abs().max().item() < tol
     assert (vc.float() - vr.float()).abs().max().item() < tol
     assert kc.abs().sum().item() > 0 and vc.abs().sum().item() > 0
+
+
+@pytest.mark.parametrize("T", [1, 5])
+def test_moe_grouped_gemm_expert_parallel(T):
+    """Expert-parallel grouping: this rank holds experts 0..El-1; picks of other ranks' experts are
+    routed to the extra group El, never computed, and read as 0 in the zero-initialised combine."""
+    El, topk, D, F = 4, 2, 512, 768
+    gu = [_qw(2 * F, D, GGMLType.Q4_K, seed=50 + e) for e in range(El)]
+    dn = [_qw(D, F, GGMLType.Q6_K, seed=60 + e) for e in range(El)]
+    mg, md = ops.MoEWeights(gu), ops.MoEWeights(dn)
+    x = torch.randn(T, D, device=DEV).to(torch.bfloat16)
+    ids = torch.stack([torch.randperm(2 * El)[:topk] for _ in range(T)]).to(torch.int32)  # global ids 0..2El-1
+    ids_l = torch.where(ids < El, ids, torch.full_like(ids, El)).to(DEV)
+    wts = torch.rand(T, topk, device=DEV)
+    order, off = ops.moe_route(ids_l, El + 1)
+    gup = ops.moe_linear(x, mg, order, off, topk, T)
+    h = torch.randn(T * topk, F, device=DEV).to(torch.bfloat16)
+    z = ops.moe_linear(h, md, order, off, topk, T, down=True, wts=wts.reshape(-1).contiguous(), zero=True).dense()
+    ref = torch.zeros(T, D)
+    for p in range(T * topk):
+        t, _ = divmod(p, topk)
+        e = int(ids.view(-1)[p])
+        if e < El:
+            ref[t] += float(wts.view(-1)[p]) * (h[p].float().cpu() @ dn[e].ref.t())
+            r_gu = x[t].float().cpu() @ gu[e].ref.t()
+            assert (gup.dense()[p].cpu() - r_gu).abs().max() < 2e-2 * max(1.0, r_gu.abs().max())
+    assert (z.cpu() - ref).abs().max() < 2e-2 * max(1.0, ref.abs().max())

@@ -18,7 +18,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, path, q):
+def _worker(rank, world, port, path, q, ep=False):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -28,7 +28,7 @@ def _worker(rank, world, port, path, q):
         from localai_amd.engine.sampling_params import SamplingParams
         from localai_amd.models.decoder import TPInfo
         ctrl = dist.new_group(backend="gloo")
-        tp = TPInfo(rank=rank, world=world, group=dist.group.WORLD)
+        tp = TPInfo(rank=rank, world=world, group=dist.group.WORLD, ep=ep)
         eng = LLMEngine(EngineConfig(model_path=path, device="cpu", context_size=256, max_num_seqs=4,
                                      use_graphs=False), tp=tp, ctrl_group=ctrl)
         if rank == 0:
@@ -37,8 +37,9 @@ def _worker(rank, world, port, path, q):
                 res = eng.generate(prompt, SamplingParams(max_tokens=5, temperature=0.0, ignore_eos=True))
                 outs.append((res["text"], res["completion_tokens"]))
             emb = eng.embed(["embed me"])[0]
+            n_exp = len(eng.model.layers[0].experts or [])
             eng.shutdown()
-            q.put((rank, outs, len(emb)))
+            q.put((rank, outs, len(emb), n_exp))
         else:
             eng.run_follower()
             q.put((rank, eng.metrics["requests"], eng.metrics["gen_tokens"]))
@@ -62,6 +63,22 @@ def tp_model_path(request, tiny_model_path, tmp_path_factory):
 
 
 def test_tp2_leader_follower(tp_model_path):
+    _run_tp2(tp_model_path)
+
+
+def test_ep2_mixtral(tiny_model_path, tmp_path_factory):
+    """Expert parallelism (TPInfo.ep): each rank holds half of the experts whole, the MoE output
+    is summed by the all-reduce that closes the MLP; greedy output agrees with one rank."""
+    from localai_amd.models import synth
+    p = tmp_path_factory.mktemp("ep") / "tiny-mixtral.gguf"
+    synth.write_model(str(p), "tiny-mixtral", exact=True)
+    n_exp = _run_tp2(str(p), ep=True)
+    from localai_amd.gguf import GGUFReader
+    from localai_amd.models.hparams import HParams
+    assert n_exp == HParams.from_gguf(GGUFReader(str(p))).n_expert // 2
+
+
+def _run_tp2(tp_model_path, ep=False):
     tiny_model_path = tp_model_path
     from localai_amd.engine.llm_engine import EngineConfig, LLMEngine
     from localai_amd.engine.sampling_params import SamplingParams
@@ -71,7 +88,7 @@ def test_tp2_leader_follower(tp_model_path):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, tiny_model_path, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, tiny_model_path, q, ep)) for r in range(2)]
     for p in procs:
         p.start()
     out, t0 = {}, time.time()
@@ -85,10 +102,11 @@ def test_tp2_leader_follower(tp_model_path):
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
-    _, outs, emb_len = out[0]
+    _, outs, emb_len, n_exp = out[0]
     _, f_requests, f_tokens = out[1]
     assert [n for _, n in outs] == [5, 5]
     assert f_requests == 2 and f_tokens == 10      # the follower ran the same two requests
     assert emb_len == single.model.hp.n_embd
     # sharded reductions change bf16 summation order; the first token must agree
     assert outs[0][0][:1] == ref["text"][:1]
+    return n_exp
