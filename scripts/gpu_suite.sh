@@ -1,0 +1,6 @@
+# full GPU suite in one process (verbose, per-test timeout) + smoke
+set -o pipefail
+R=$GRAFT_REPO_ROOT; cd $R && mkdir -p gpurun_out
+export LOCALAI_AMD_CACHE=/tmp/la_cache
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?; grep -E "passed|failed|error" gpurun_out/pytest_gpu.log | tail -3; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('SMOKE_OK')" > gpurun_out/smoke.log 2>&1 && tail -2 gpurun_out/smoke.log
