@@ -57,7 +57,7 @@ def lib():
             "la_reduce_slabs": [P, LNG, I, P, I, I, P, P, P],
             "la_embed": [I, P, P, P, P, I, I, P, I, P, F, P],
             "la_dequant": [I, P, P, P, P, I, I, P, P],
-            "la_attn_decode": [P, P, P, P, I, P, I, I, I, I, I, F, I, I, P, P, P, P, P, LNG, I, P, P, P, P, P],
+            "la_attn_decode": [P, P, P, P, I, P, I, I, I, I, I, F, I, I, P, P, P, P, P, LNG, I, P, P, P, P, I, P],
             "la_attn_prefill": [P, P, P, P, I, P, P, P, I, I, I, I, I, F, P, P],
             "la_sample": [P, LNG, I, I, P, P, P, P, P],
             "la_penalties": [P, LNG, I, P, I, P, P, I, P, P],
@@ -891,14 +891,29 @@ def embed(tokens: torch.Tensor, w: QWeight, scale: float = 1.0, out: Optional[to
 # ---------------------------------------------------------------------------------------
 
 DEC_TARGET_WAVES = 2048  # ~16 waves per CU over 256 CUs
+# (sequence, kv head) pairs for which attn_decode runs single-wave workgroups: 2048 of them
+# (decode batch 256 x 8 kv heads) are resident at once at 2 waves per SIMD, so every workgroup's
+# latency chain (seq_len -> block table -> first K/V tile) starts in ONE residency round, where
+# 4-wave workgroups go through 4 rounds.  Measured on MI355X (scripts/attn_bench.py, KV cycled
+# through 8 layers' worth of HBM): B=256 x L=384 72.6 vs 74.9 us, B=256 x L=256 equal, but
+# B=128 (two partitions per sequence) 50.6 vs 40.2 us and B=512 (two rounds) 119.7 vs 114.0 us,
+# hence the window
+DEC_NW1_MIN = int(os.environ.get("LOCALAI_AMD_DEC_NW1_MIN", "2048"))
+DEC_NW1_MAX = 2048
+
+
+def decode_waves(B: int, Hkv: int) -> int:
+    """Waves per attn_decode workgroup (1 or 4) for a batch of B sequences."""
+    return 1 if DEC_NW1_MIN <= B * Hkv <= max(DEC_NW1_MAX, DEC_NW1_MIN) else 4
 
 
 def decode_partitions(B: int, Hkv: int, max_len: int, block_size: int = 32) -> Tuple[int, int]:
     """Split-KV partitioning for attn_decode: (P, PS).  Enough partitions to put ~16 waves on
-    every CU; each workgroup (4 waves) covers PS keys (multiple of 128, at most 2048 pages so
-    the partition's block-table slice fits the kernel's LDS stage)."""
+    every CU; each workgroup (decode_waves waves) covers PS keys (multiple of 128, at most 2048
+    pages so the partition's block-table slice fits the kernel's LDS stage)."""
     max_len = max(1, max_len)
-    P = max(1, min(-(-DEC_TARGET_WAVES // (B * Hkv * 4)), -(-max_len // 128), 64))
+    nw = decode_waves(B, Hkv)
+    P = max(1, min(-(-DEC_TARGET_WAVES // (B * Hkv * nw)), -(-max_len // 128), 64))
     P = max(P, -(-max_len // (2048 * block_size)))
     PS = -(-(-(-max_len // P)) // 128) * 128
     P = -(-max_len // PS)
@@ -934,7 +949,7 @@ def attn_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, b
     _check(lib().la_attn_decode(q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr(),
                                 block_tables.shape[1], seq_lens.data_ptr(), B, Hq, Hkv, Dh, BS, float(scale), P, PS,
                                 out.data_ptr(), po.data_ptr(), pml.data_ptr(), tk.data_ptr(), None, 0, 0, None, None,
-                                None, None, _stream()),
+                                None, None, decode_waves(B, Hkv), _stream()),
            "la_attn_decode")
     return out
 
@@ -977,7 +992,7 @@ def attn_decode_rope(qkv: Partial, pos: torch.Tensor, slots: torch.Tensor, cos_s
     _check(lib().la_attn_decode(None, k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr(),
                                 block_tables.shape[1], seq_lens.data_ptr(), T, Hq, Hkv, Dh, BS, float(scale), P, PS,
                                 out.data_ptr(), po.data_ptr(), pml.data_ptr(), tk.data_ptr(), a[0], a[1], a[2], a[3],
-                                pos.data_ptr(), slots.data_ptr(), cos_sin.data_ptr(), _stream()),
+                                pos.data_ptr(), slots.data_ptr(), cos_sin.data_ptr(), decode_waves(T, Hkv), _stream()),
            "la_attn_decode(rope)")
     return out
 

@@ -37,14 +37,18 @@ namespace la {
 //     release/acquire ticket per (sequence, kv head); the ticket resets itself for the next
 //     launch / graph replay), so there is no separate combine launch.
 // Scores live in the log2 domain (scale * log2 e folded in): every exponential is one v_exp_f32.
-constexpr int DEC_T = 256;
+// Workgroup = NW waves of one (partition, kv head, sequence).  NW = 4 splits a partition's tiles
+// over 4 waves (few sequences: more waves in flight per key); NW = 1 gives every wave a whole
+// partition (batch decode: B x Hkv >= 1024 single-wave workgroups fill the chip in ONE residency
+// round, so the seq_len -> block table -> first tile latency chain is paid once per CU instead
+// of once per 4-wave round, and no cross-wave LDS merge is needed).
 constexpr int DEC_MAXBT = 2048;  // block-table entries of one partition staged in LDS
 constexpr int DEC_ONE_PART = 256;  // sequences up to this many keys run as a single partition
 
-template <int DH, int GT>
+template <int DH, int GT, int NW>
 struct DecShared {
-  float ow[4][GT][DH];
-  float mw[4][16], lw[4][16];
+  float ow[NW < 2 ? 2 : NW][GT][DH];  // wave partials (NW > 1); the split-KV merge weights reuse it
+  float mw[NW][16], lw[NW][16];
   int bt[DEC_MAXBT];
   int last;
 };
@@ -106,15 +110,16 @@ LA_DEV void rope_src_load(const DecRope& R, int b, int col, float (&v)[N]) {
   }
 }
 
-template <int DH, int GT>
-__global__ __launch_bounds__(DEC_T) void attn_decode_kernel(
+template <int DH, int GT, int NW>
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) void attn_decode_kernel(
     const bf16* __restrict__ q, const bf16* __restrict__ kc, const bf16* __restrict__ vc,
     const int* __restrict__ block_tables, int max_blocks, const int* __restrict__ seq_lens, int Hkv, int G,
     int BS, float scale_log2, int PS_grid, bf16* __restrict__ out, float* __restrict__ part_o,
     float* __restrict__ part_ml, int P, int* __restrict__ tickets, DecRope R) {
   constexpr int KC = (DH + 31) / 32;  // 32-wide k chunks of the QK^T product
   constexpr int ND = DH / 16;         // 16-wide d tiles of the PV product
-  __shared__ DecShared<DH, GT> sh;
+  constexpr int NT = NW * 64;
+  __shared__ DecShared<DH, GT, NW> sh;
 
   const int p = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
   const int Hq = Hkv * G;
@@ -131,7 +136,7 @@ __global__ __launch_bounds__(DEC_T) void attn_decode_kernel(
   const int kend = min(L, t0 + PS);
   const int nbt = (kend - t0 + BS - 1) / BS;
   const int* bt = block_tables + (long)b * max_blocks + t0 / BS;
-  for (int i = tid; i < nbt; i += DEC_T) sh.bt[i] = bt[i];
+  for (int i = tid; i < nbt; i += NT) sh.bt[i] = bt[i];
 
   // Q^T fragments: lane holds Q[head r][d = 32c + 8g .. +8]
   bf16x8 qf[KC];
@@ -157,18 +162,20 @@ __global__ __launch_bounds__(DEC_T) void attn_decode_kernel(
     const int slot = R.slots[b];
     if (slot >= 0 && L - 1 >= t0 && L - 1 < kend) {
       const int blk = slot / BS, off = slot - blk * BS;
-      if (tid < DH / 2) {
-        float x[2];
-        rope_src_load<2>(R, b, (Hq + kvh) * DH + 2 * tid, x);
-        const float cc = cs[2 * tid], sn = cs[2 * tid + 1];
-        bf16* kd = (bf16*)kc + (((long)blk * Hkv + kvh) * BS + off) * DH + 2 * tid;
-        kd[0] = (bf16)(x[0] * cc - x[1] * sn);
-        kd[1] = (bf16)(x[0] * sn + x[1] * cc);
-      } else if (tid < DH / 2 + DH) {
-        const int d = tid - DH / 2;
-        float x[1];
-        rope_src_load<1>(R, b, (Hq + Hkv + kvh) * DH + d, x);
-        ((bf16*)vc)[((long)blk * Hkv + kvh) * DH * BS + ((off >> 3) * DH + d) * 8 + (off & 7)] = (bf16)x[0];
+      for (int j = tid; j < DH / 2 + DH; j += NT) {
+        if (j < DH / 2) {
+          float x[2];
+          rope_src_load<2>(R, b, (Hq + kvh) * DH + 2 * j, x);
+          const float cc = cs[2 * j], sn = cs[2 * j + 1];
+          bf16* kd = (bf16*)kc + (((long)blk * Hkv + kvh) * BS + off) * DH + 2 * j;
+          kd[0] = (bf16)(x[0] * cc - x[1] * sn);
+          kd[1] = (bf16)(x[0] * sn + x[1] * cc);
+        } else {
+          const int d = j - DH / 2;
+          float x[1];
+          rope_src_load<1>(R, b, (Hq + Hkv + kvh) * DH + d, x);
+          ((bf16*)vc)[((long)blk * Hkv + kvh) * DH * BS + ((off >> 3) * DH + d) * 8 + (off & 7)] = (bf16)x[0];
+        }
       }
       // Only this workgroup reads the appended key back (pages never straddle partitions, and
       // L1 starts each launch clean), so same-CU ordering suffices: the stores reach the XCD's
@@ -219,8 +226,8 @@ __global__ __launch_bounds__(DEC_T) void attn_decode_kernel(
   if (kb < kend) {
     DecTile<DH> cur, nxt;
     load_tile(kb, cur);
-    for (; kb < kend; kb += 128) {
-      if (kb + 128 < kend) load_tile(kb + 128, nxt);
+    for (; kb < kend; kb += 32 * NW) {
+      if (kb + 32 * NW < kend) load_tile(kb + 32 * NW, nxt);
       float s[2][4];
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
@@ -269,6 +276,33 @@ __global__ __launch_bounds__(DEC_T) void attn_decode_kernel(
   // wave totals: lsum over the 4 lane groups (same head r)
   lsum += __shfl_xor(lsum, 16, 64);
   lsum += __shfl_xor(lsum, 32, 64);
+  const int np = (L + PS - 1) / PS;  // partitions holding keys of this sequence
+  if constexpr (NW == 1) {
+    // one wave per workgroup: its accumulators ARE the partition's result (no LDS merge).
+    // o[nd][i] is head 4g+i at d = 16nd + r; that head's (m, l) live in lane 4g+i.
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int h = 4 * g + i;
+      const float lh = __shfl(lsum, h, 64), mh = __shfl(m, h, 64);
+      if (h < G) {
+        const int hq = kvh * G + h;
+        if (np == 1) {
+          const float inv = lh > 0.f ? 1.f / lh : 0.f;
+#pragma unroll
+          for (int nd = 0; nd < ND; ++nd) out[((long)b * Hq + hq) * DH + 16 * nd + r] = (bf16)(o[nd][i] * inv);
+        } else {
+#pragma unroll
+          for (int nd = 0; nd < ND; ++nd) part_o[(((long)b * Hq + hq) * P + p) * DH + 16 * nd + r] = o[nd][i];
+          if (r == 0) {
+            float* ml = part_ml + (((long)b * Hq + hq) * P + p) * 2;
+            ml[0] = mh;
+            ml[1] = lh;
+          }
+        }
+      }
+    }
+    if (np == 1) return;
+  } else {
   if (g == 0) {
     sh.mw[wave][r] = m;
     sh.lw[wave][r] = lsum;
@@ -279,16 +313,15 @@ __global__ __launch_bounds__(DEC_T) void attn_decode_kernel(
     for (int i = 0; i < 4; ++i)
       if (4 * g + i < GT) sh.ow[wave][min(4 * g + i, GT - 1)][16 * nd + r] = o[nd][i];
   __syncthreads();
-  const int np = (L + PS - 1) / PS;  // partitions holding keys of this sequence
-  for (int i = tid; i < G * DH; i += DEC_T) {
+  for (int i = tid; i < G * DH; i += NT) {
     const int h = i / DH, d = i % DH;
     float M = -INFINITY;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) M = fmaxf(M, sh.mw[w][h]);
+    for (int w = 0; w < NW; ++w) M = fmaxf(M, sh.mw[w][h]);
     const float Ms = (M == -INFINITY) ? 0.f : M;
     float num = 0.f, den = 0.f;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) {
+    for (int w = 0; w < NW; ++w) {
       const float f = exp2f(sh.mw[w][h] - Ms);
       num += f * sh.ow[w][h][d];
       den += f * sh.lw[w][h];
@@ -306,6 +339,7 @@ __global__ __launch_bounds__(DEC_T) void attn_decode_kernel(
     }
   }
   if (np == 1) return;
+  }
   // ---- split-KV merge by the last-arriving partition of (b, kvh)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -342,7 +376,7 @@ __global__ __launch_bounds__(DEC_T) void attn_decode_kernel(
     wts[np * G + tid] = den > 0.f ? 1.f / den : 0.f;
   }
   __syncthreads();
-  for (int i = tid; i < G * DH; i += DEC_T) {
+  for (int i = tid; i < G * DH; i += NT) {
     const int h = i / DH, d = i % DH;
     const float* po = part_o + (hb + (long)h * P) * DH + d;
     float num = 0.f;
@@ -510,8 +544,9 @@ extern "C" int la_attn_decode(const void* q, const void* kc, const void* vc, con
                               const int* seq_lens, int B, int Hq, int Hkv, int Dh, int BS, float scale, int P, int PS,
                               void* out, void* part_o, void* part_ml, void* tickets, const void* rope_p,
                               long rope_slab, int rope_S, const void* rope_bias, const int* pos, const int* slots,
-                              const float* cos_sin, void* stream) {
+                              const float* cos_sin, int nw, void* stream) {
   if (Hq % Hkv || Hq / Hkv > 16 || (BS % 16) || (128 % BS && BS % 128) || (PS % 128) || P < 1 ||
+      (nw != 1 && nw != 4) ||
       PS / BS > la::DEC_MAXBT || P > 64 || (P > 1 && !tickets))
     return -1;
   // rope_p != null: fused RoPE + KV append from the q|k|v GEMM output (q unused)
@@ -525,10 +560,17 @@ extern "C" int la_attn_decode(const void* q, const void* kc, const void* vc, con
   float* pml = (float*)part_ml;
   int* tk = (int*)tickets;
   const float sl2 = scale * 1.4426950408889634f;
-#define DEC(D, GT)                                                                                                 \
-  hipLaunchKernelGGL((la::attn_decode_kernel<D, GT>), grid, dim3(la::DEC_T), 0, st, (const bf16*)q,              \
+#define DEC_NW(D, GT, NW)                                                                                         \
+  hipLaunchKernelGGL((la::attn_decode_kernel<D, GT, NW>), grid, dim3(NW * 64), 0, st, (const bf16*)q,           \
                      (const bf16*)kc, (const bf16*)vc, block_tables, max_blocks, seq_lens, Hkv, G, BS, sl2, PS,  \
                      (bf16*)out, po, pml, P, tk, R)
+#define DEC(D, GT)          \
+  do {                      \
+    if (nw == 1)            \
+      DEC_NW(D, GT, 1);     \
+    else                    \
+      DEC_NW(D, GT, 4);     \
+  } while (0)
 #define DEC_G(D)                          \
   if (G == 1) DEC(D, 1);                  \
   else if (G == 2) DEC(D, 2);             \
@@ -544,6 +586,7 @@ extern "C" int la_attn_decode(const void* q, const void* kc, const void* vc, con
   }
 #undef DEC_G
 #undef DEC
+#undef DEC_NW
   return (int)hipGetLastError();
 }
 

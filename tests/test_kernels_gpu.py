@@ -295,7 +295,10 @@ def _paged_setup(lens, Hkv, Dh, BS, seed=0):
 
 @pytest.mark.parametrize("Hq,Hkv,Dh,BS", [(32, 8, 128, 32), (32, 32, 80, 32), (8, 1, 64, 16), (64, 8, 128, 32),
                                          (16, 1, 96, 64)])
-def test_attn_decode(Hq, Hkv, Dh, BS):
+@pytest.mark.parametrize("nw1", [False, True])
+def test_attn_decode(Hq, Hkv, Dh, BS, nw1, monkeypatch):
+    if nw1:  # single-wave workgroups (the batch-decode variant) on a small batch
+        monkeypatch.setattr(ops, "DEC_NW1_MIN", 1)
     lens = [1, 37, 300, 1025]
     kc, vc, bt = _paged_setup(lens, Hkv, Dh, BS)
     q = torch.randn(len(lens), Hq, Dh).to(torch.bfloat16)
@@ -308,10 +311,13 @@ def test_attn_decode(Hq, Hkv, Dh, BS):
 
 
 @pytest.mark.parametrize("src", ["slabs", "bf16"])
-def test_attn_decode_fused_rope(src):
+@pytest.mark.parametrize("nw1", [False, True])
+def test_attn_decode_fused_rope(src, nw1, monkeypatch):
     """Decode attention with RoPE + KV append fused in == rope_kv + attn_decode (outputs and the
     appended cache entries), over split-KV partitions (graph bound 4096) and a padded row."""
     Hq, Hkv, Dh, BS = 32, 8, 128, 32
+    if nw1:
+        monkeypatch.setattr(ops, "DEC_NW1_MIN", 1)
     lens = [1, 37, 300, 1025, 1]
     kc, vc, bt = _paged_setup(lens, Hkv, Dh, BS, seed=5)
     B, W = len(lens), (Hq + 2 * Hkv) * Dh
@@ -339,6 +345,25 @@ def test_attn_decode_fused_rope(src):
     (o0, k0, v0), (o1, k1, v1) = outs
     assert torch.equal(k0, k1) and torch.equal(v0, v1)
     assert (o0 - o1).abs().max().item() < 1e-2
+
+
+def test_attn_decode_large_batch(monkeypatch):
+    """Batch decode shapes that select single-wave workgroups by themselves: 256 sequences x 8 kv
+    heads (one partition each at the graph bound) and, with the window widened, 128 x 8 (two
+    partitions, merged)."""
+    Hq, Hkv, Dh, BS = 32, 8, 128, 32
+    for B in (256, 128):
+        if B == 128:
+            monkeypatch.setattr(ops, "DEC_NW1_MIN", 1024)
+        assert ops.decode_waves(B, Hkv) == 1
+        g = torch.Generator().manual_seed(B)
+        lens = torch.randint(1, 700, (B,), generator=g).tolist()
+        kc, vc, bt = _paged_setup(lens, Hkv, Dh, BS, seed=B)
+        q = torch.randn(B, Hq, Dh, generator=g).to(torch.bfloat16)
+        sl = torch.tensor(lens, dtype=torch.int32)
+        ref = ops.attn_decode(q, kc, vc, bt, sl, 0.088, max(lens))
+        out = ops.attn_decode(q.to(DEV), kc.to(DEV), vc.to(DEV), bt.to(DEV), sl.to(DEV), 0.088, 1024)
+        assert (out.float().cpu() - ref.float()).abs().max().item() < 2e-2
 
 
 def test_attn_decode_batch1_long():
