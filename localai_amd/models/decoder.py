@@ -32,6 +32,8 @@ from .hparams import HParams
 # batch-1/2 decode: q|k|v GEMV with RoPE + KV append in its epilogue (ops.qkv_rope_dp4)
 FUSED_QKV_ROPE = os.environ.get("LOCALAI_AMD_QKV_ROPE", "1") == "1"
 
+_ACT = {"swiglu": ops.ACT_SWIGLU, "gelu": ops.ACT_GELU, "geglu": ops.ACT_GEGLU}
+
 
 @dataclass
 class TPInfo:
@@ -191,7 +193,7 @@ class DecoderModel:
         for i in range(hp.n_layer):
             b = f"blk.{i}."
             qs, ks = sl(qd), sl(kvd)
-            if hp.arch == "phi2":
+            if b + "attn_qkv.weight" in T:  # phi-2 / phi-3: one fused [q; k; v] projection
                 qkv_name = b + "attn_qkv.weight"
                 qkv = [qw(qkv_name, rows=slice(qs.start, qs.stop)),
                        qw(qkv_name, rows=slice(qd + ks.start, qd + ks.stop)),
@@ -232,7 +234,11 @@ class DecoderModel:
                 if down_b is not None and R != 0:
                     down_b = torch.zeros_like(down_b)
             else:
-                g, u = qw(b + "ffn_gate.weight", rows=fs), qw(b + "ffn_up.weight", rows=fs)
+                if b + "ffn_gate.weight" in T:
+                    g, u = qw(b + "ffn_gate.weight", rows=fs), qw(b + "ffn_up.weight", rows=fs)
+                else:  # phi-3: ffn_up holds [gate; up] (2 n_ff rows)
+                    g = qw(b + "ffn_up.weight", rows=fs)
+                    u = qw(b + "ffn_up.weight", rows=slice(hp.n_ff + fs.start, hp.n_ff + fs.stop))
                 gu = ops.concat_rows([g, u])
                 gate_up = [gu] if gu is not None else [g, u]
                 down = qw(b + "ffn_down.weight", cols=fs)
@@ -295,7 +301,7 @@ class DecoderModel:
         if L.experts is not None:
             return self._moe(L, xn)
         gu = ops.linear_multi(xn, L.gate_up, bias=L.up_bias)
-        d = ops.act_linear(gu, self.F, ops.ACT_SWIGLU if hp.act == "swiglu" else ops.ACT_GELU, L.down)
+        d = ops.act_linear(gu, self.F, _ACT[hp.act], L.down)
         return self._row_parallel_out(d, L.down_bias)
 
     def _moe(self, L: Layer, xn: torch.Tensor) -> ops.Partial:
@@ -361,7 +367,7 @@ class DecoderModel:
         hp = self.hp
         eps, nm = hp.norm_eps, self.norm_mode
         T = fb.tokens.shape[0]
-        res = ops.embed(fb.tokens, self.tok_embd)
+        res = ops.embed(fb.tokens, self.tok_embd, hp.embed_scale)
         if fb.inject_idx is not None:
             res.index_copy_(0, fb.inject_idx, fb.inject_rows.to(res.dtype))
         L0 = self.layers[0]
@@ -410,6 +416,7 @@ class DecoderModel:
         Tn = len(tokens)
         x = self.tok_embd.dequant_f32().to(dev)[t] if self.tok_embd.ref is not None else \
             self.tok_embd.materialize_bf16().float().cpu()[t]
+        x = x * hp.embed_scale
 
         def deq(w):
             return (w.ref if w.ref is not None else w.materialize_bf16().float()).cpu()
@@ -476,6 +483,8 @@ class DecoderModel:
                     gu = gu + L.up_bias.cpu()
                 if hp.act == "swiglu":
                     hh = torch.nn.functional.silu(gu[:, :self.F]) * gu[:, self.F:]
+                elif hp.act == "geglu":
+                    hh = torch.nn.functional.gelu(gu[:, :self.F], approximate="tanh") * gu[:, self.F:]
                 else:
                     hh = torch.nn.functional.gelu(gu, approximate="tanh")
                 d = hh @ deq(L.down).t()

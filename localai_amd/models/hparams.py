@@ -27,7 +27,8 @@ class HParams:
     n_expert: int = 0
     n_expert_used: int = 0
     parallel_residual: bool = False   # phi-2: h = x + attn(ln x) + mlp(ln x)
-    act: str = "swiglu"               # "swiglu" | "gelu"
+    act: str = "swiglu"               # "swiglu" | "gelu" | "geglu" (Gemma: gelu(gate) * up)
+    embed_scale: float = 1.0          # Gemma scales the token embeddings by sqrt(n_embd)
     tied_embeddings: bool = False
     name: str = ""
 
@@ -82,7 +83,8 @@ class HParams:
             n_expert=int(g("expert_count", 0) or 0),
             n_expert_used=int(g("expert_used_count", 0) or 0),
             parallel_residual=a == "phi2",
-            act="gelu" if a in ("phi2", "gptneox", "falcon") else "swiglu",
+            act="gelu" if a in ("phi2", "gptneox", "falcon") else ("geglu" if a in ("gemma", "gemma2") else "swiglu"),
+            embed_scale=float(n_embd) ** 0.5 if a in ("gemma", "gemma2") else 1.0,
             tied_embeddings="output.weight" not in r.tensors,
             name=str(r.kv.get("general.name", "")),
         )

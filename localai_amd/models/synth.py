@@ -48,9 +48,15 @@ class Preset:
     n_expert: int = 0
     n_expert_used: int = 0
     rope_dim: Optional[int] = None
+    head_dim: Optional[int] = None   # default n_embd // n_head (Gemma: 256 with q_dim != n_embd)
     qtype: str = "Q4_K_M"            # Q4_K_M | Q4_K | Q8_0 | F16 | F32
-    tokenizer: str = "llama3"        # llama3 | mistral | phi2
+    tokenizer: str = "llama3"        # llama3 | mistral | phi2 | chatml
+    tied: bool = False               # no output.weight: the lm_head is token_embd (Gemma, small Qwen2)
     name: str = "synthetic"
+
+    @property
+    def hd(self) -> int:
+        return self.head_dim or self.n_embd // self.n_head
 
 
 PRESETS: Dict[str, Preset] = {
@@ -73,7 +79,27 @@ PRESETS: Dict[str, Preset] = {
                            n_expert=4, n_expert_used=2, qtype="Q4_K", name="tiny-mixtral"),
     "tiny-phi2": Preset(arch="phi2", n_layer=2, n_embd=256, n_head=4, n_head_kv=4, n_ff=512, n_vocab=32256,
                         ctx=512, rope_theta=10000.0, rope_dim=32, qtype="Q8_0", tokenizer="phi2", name="tiny-phi2"),
+    # Qwen2: q/k/v biases, NEOX rotary, ChatML; Phi-3: fused attn_qkv and gate|up ffn_up, head dim 96;
+    # Gemma: head dim 256 (q_dim != n_embd), GeGLU, sqrt(n_embd)-scaled embeddings, tied lm_head
+    "tiny-qwen2": Preset(arch="qwen2", n_layer=2, n_embd=256, n_head=4, n_head_kv=2, n_ff=512, n_vocab=32256,
+                         ctx=512, rope_theta=1e6, eps=1e-6, qtype="Q4_K", tokenizer="chatml", name="tiny-qwen2"),
+    "tiny-phi3": Preset(arch="phi3", n_layer=2, n_embd=768, n_head=8, n_head_kv=8, n_ff=512, n_vocab=32064,
+                        ctx=512, rope_theta=10000.0, qtype="Q4_K", tokenizer="mistral", name="tiny-phi3"),
+    "tiny-gemma": Preset(arch="gemma", n_layer=2, n_embd=256, n_head=2, n_head_kv=1, head_dim=256, n_ff=512,
+                         n_vocab=32256, ctx=512, rope_theta=10000.0, eps=1e-6, qtype="Q4_K", tokenizer="mistral",
+                         tied=True, name="tiny-gemma"),
+    "qwen2-7b": Preset(arch="qwen2", n_layer=28, n_embd=3584, n_head=28, n_head_kv=4, n_ff=18944, n_vocab=152064,
+                       ctx=32768, rope_theta=1e6, eps=1e-6, tokenizer="chatml", name="Qwen2-7B-Instruct (random-init)"),
+    "phi3-mini": Preset(arch="phi3", n_layer=32, n_embd=3072, n_head=32, n_head_kv=32, n_ff=8192, n_vocab=32064,
+                        ctx=4096, rope_theta=10000.0, tokenizer="mistral", name="Phi-3-mini-4k-instruct (random-init)"),
+    "gemma-7b": Preset(arch="gemma", n_layer=28, n_embd=3072, n_head=16, n_head_kv=16, head_dim=256, n_ff=24576,
+                       n_vocab=256000, ctx=8192, rope_theta=10000.0, eps=1e-6, tokenizer="mistral", tied=True,
+                       name="gemma-7b-it (random-init)"),
 }
+
+CHATML_TEMPLATE = ("{% for message in messages %}{{'<|im_start|>' + message['role'] + '\n' + message['content'] + "
+                   "'<|im_end|>' + '\n'}}{% endfor %}{% if add_generation_prompt %}{{ '<|im_start|>assistant\n' }}"
+                   "{% endif %}")
 
 
 def _bpe_asset():
@@ -116,7 +142,7 @@ def build_vocab(p: Preset):
             i += 1
         scores = [0.0] * 259 + [-float(i) for i in range(len(toks) - 259)]
         return "llama", toks, types, None, scores, 1, 2, {"tokenizer.ggml.add_bos_token": True}
-    n_special = 256 if p.tokenizer == "llama3" else 1
+    n_special = {"llama3": 256, "chatml": 3}.get(p.tokenizer, 1)
     n_normal = p.n_vocab - n_special
     toks = list(base[:n_normal])
     i = 0
@@ -131,6 +157,12 @@ def build_vocab(p: Preset):
         bos, eos = n_normal + 0, n_normal + 9
         extra = {"tokenizer.ggml.pre": "llama-bpe", "tokenizer.chat_template": LLAMA3_TEMPLATE,
                  "tokenizer.ggml.add_bos_token": True, "tokenizer.ggml.eot_token_id": n_normal + 9}
+    elif p.tokenizer == "chatml":  # Qwen2: <|endoftext|>, <|im_start|>, <|im_end|> (eos of the instruct models)
+        toks += ["<|endoftext|>", "<|im_start|>", "<|im_end|>"]
+        types += [3, 3, 3]
+        bos, eos = n_normal, n_normal + 2
+        extra = {"tokenizer.ggml.pre": "qwen2", "tokenizer.chat_template": CHATML_TEMPLATE,
+                 "tokenizer.ggml.add_bos_token": False, "tokenizer.ggml.eot_token_id": n_normal + 2}
     else:  # phi2: <|endoftext|> is bos = eos
         toks.append("<|endoftext|>")
         types.append(3)
@@ -168,7 +200,7 @@ def _tensor_types(p: Preset, name: str, layer: int) -> int:
 
 def tensor_list(p: Preset):
     """(name, shape, layer) for every tensor of the preset, torch/numpy order."""
-    d, hd = p.n_embd, p.n_embd // p.n_head
+    d, hd = p.n_embd, p.hd
     qd, kvd = p.n_head * hd, p.n_head_kv * hd
     out = [("token_embd.weight", (p.n_vocab, d), -1)]
     for i in range(p.n_layer):
@@ -180,9 +212,16 @@ def tensor_list(p: Preset):
                     (b + "ffn_up.weight", (p.n_ff, d), i), (b + "ffn_up.bias", (p.n_ff,), i),
                     (b + "ffn_down.weight", (d, p.n_ff), i), (b + "ffn_down.bias", (d,), i)]
             continue
+        if p.arch == "phi3":
+            out += [(b + "attn_norm.weight", (d,), i), (b + "attn_qkv.weight", (qd + 2 * kvd, d), i),
+                    (b + "attn_output.weight", (d, qd), i), (b + "ffn_norm.weight", (d,), i),
+                    (b + "ffn_up.weight", (2 * p.n_ff, d), i), (b + "ffn_down.weight", (d, p.n_ff), i)]
+            continue
         out += [(b + "attn_norm.weight", (d,), i), (b + "attn_q.weight", (qd, d), i),
                 (b + "attn_k.weight", (kvd, d), i), (b + "attn_v.weight", (kvd, d), i),
                 (b + "attn_output.weight", (d, qd), i), (b + "ffn_norm.weight", (d,), i)]
+        if p.arch == "qwen2":
+            out += [(b + "attn_q.bias", (qd,), i), (b + "attn_k.bias", (kvd,), i), (b + "attn_v.bias", (kvd,), i)]
         if p.n_expert:
             E = p.n_expert
             out += [(b + "ffn_gate_inp.weight", (E, d), i), (b + "ffn_gate_exps.weight", (E, p.n_ff, d), i),
@@ -194,7 +233,8 @@ def tensor_list(p: Preset):
     if p.arch == "phi2":
         out.append(("output_norm.bias", (d,), -1))
         out.append(("output.bias", (p.n_vocab,), -1))
-    out.append(("output.weight", (p.n_vocab, d), -1))
+    if not p.tied:
+        out.append(("output.weight", (p.n_vocab, d), -1))
     return out
 
 
@@ -207,7 +247,7 @@ def write_model(path: str, preset: str | Preset, seed: int = 0, exact: bool = Fa
     model, toks, types, merges, scores, bos, eos, extra = build_vocab(p)
     w = GGUFWriter(path, p.arch)
     a = p.arch
-    hd = p.n_embd // p.n_head
+    hd = p.hd
     w.add_string("general.name", p.name)
     w.add_uint32("general.file_type", 15 if p.qtype == "Q4_K_M" else 7)
     w.add_uint32(f"{a}.context_length", p.ctx)
@@ -218,6 +258,9 @@ def write_model(path: str, preset: str | Preset, seed: int = 0, exact: bool = Fa
     w.add_uint32(f"{a}.attention.head_count_kv", p.n_head_kv)
     w.add_float32(f"{a}.rope.freq_base", p.rope_theta)
     w.add_uint32(f"{a}.rope.dimension_count", p.rope_dim or hd)
+    if p.head_dim:
+        w.add_uint32(f"{a}.attention.key_length", hd)
+        w.add_uint32(f"{a}.attention.value_length", hd)
     if a == "phi2":
         w.add_float32(f"{a}.attention.layer_norm_epsilon", p.eps)
     else:

@@ -826,7 +826,8 @@ def rope_kv(qkv: Partial, pos: torch.Tensor, slots: Optional[torch.Tensor], cos_
     return q_out
 
 
-ACT_SWIGLU, ACT_GELU, ACT_GELU_QUICK = 0, 1, 2
+ACT_SWIGLU, ACT_GELU, ACT_GELU_QUICK, ACT_GEGLU = 0, 1, 2, 3
+GLU_ACTS = (ACT_SWIGLU, ACT_GEGLU)  # gate|up sources of width 2F
 
 
 def act(src: Partial, F: int, mode: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -835,6 +836,8 @@ def act(src: Partial, F: int, mode: int, out: Optional[torch.Tensor] = None) -> 
         x = src.dense()
         if mode == ACT_SWIGLU:
             y = torch.nn.functional.silu(x[:, :F]) * x[:, F:2 * F]
+        elif mode == ACT_GEGLU:
+            y = torch.nn.functional.gelu(x[:, :F], approximate="tanh") * x[:, F:2 * F]
         elif mode == ACT_GELU:
             y = torch.nn.functional.gelu(x, approximate="tanh")
         else:
@@ -852,7 +855,7 @@ def act_linear(src: Partial, F: int, mode: int, w: QWeight) -> Partial:
     activation is computed inside the down GEMV's activation prologue -- no activation launch
     and no bf16 round trip; otherwise act() then linear()."""
     M = src.M
-    width = 2 * F if mode == ACT_SWIGLU else F
+    width = 2 * F if mode in GLU_ACTS else F
     if (src.t.is_cuda and src.S >= 1 and src.S <= 16 and GEMV_DP4 and M <= GEMV_MAX_M and w.gemv_ok
             and w.K == F and src.N == width):
         S = _gemv_splits([w], w.K, M)

@@ -222,12 +222,19 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
   for (int i = 0; i < ND; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m = -INFINITY, lsum = 0.f;
 
+  // register double buffer up to Dh 128; a Dh-256 tile (Gemma) is 128 VGPRs on its own, so it
+  // is loaded at the top of each iteration instead (no prefetch, no spills)
+  constexpr bool DB = DH <= 128;
   int kb = t0 + 32 * wave;
   if (kb < kend) {
     DecTile<DH> cur, nxt;
-    load_tile(kb, cur);
+    if constexpr (DB) load_tile(kb, cur);
     for (; kb < kend; kb += 32 * NW) {
-      if (kb + 32 * NW < kend) load_tile(kb + 32 * NW, nxt);
+      if constexpr (DB) {
+        if (kb + 32 * NW < kend) load_tile(kb + 32 * NW, nxt);
+      } else {
+        load_tile(kb, cur);
+      }
       float s[2][4];
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
@@ -270,7 +277,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
       }
 #pragma unroll
       for (int nd = 0; nd < ND; ++nd) o[nd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, cur.v[nd], o[nd], 0, 0, 0);
-      cur = nxt;
+      if constexpr (DB) cur = nxt;
     }
   }
   // wave totals: lsum over the 4 lane groups (same head r)
@@ -582,6 +589,7 @@ extern "C" int la_attn_decode(const void* q, const void* kc, const void* vc, con
     case 80: DEC_G(80); break;
     case 96: DEC_G(96); break;
     case 128: DEC_G(128); break;
+    case 256: DEC_G(256); break;
     default: return -2;
   }
 #undef DEC_G
@@ -605,6 +613,7 @@ extern "C" int la_attn_prefill(const void* q, const void* kc, const void* vc, co
     case 80: PF(80); break;
     case 96: PF(96); break;
     case 128: PF(128); break;
+    case 256: PF(256); break;
     default: return -2;
   }
 #undef PF

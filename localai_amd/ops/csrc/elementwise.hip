@@ -285,19 +285,22 @@ __global__ __launch_bounds__(256) void rope_kv8_kernel(Src qkv, const int* __res
 // Activations.  mode 0: SwiGLU  out[t][i] = silu(x[t][i]) * x[t][F+i]   (src width 2F)
 //               mode 1: GELU(tanh) out[t][i] = gelu(x[t][i])             (src width F)
 //               mode 2: GELU-quick (CLIP)  x * sigmoid(1.702 x)
+//               mode 3: GeGLU (Gemma)  out[t][i] = gelu(x[t][i]) * x[t][F+i]   (src width 2F)
+LA_DEV float gelu_tanh(float x) { return 0.5f * x * (1.f + tanhf(0.7978845608f * (x + 0.044715f * x * x * x))); }
+
 __global__ __launch_bounds__(256) void act_kernel(Src src, bf16* __restrict__ out, int F, int mode) {
   const int t = blockIdx.y;
   const int c = (blockIdx.x * blockDim.x + threadIdx.x) * 4;
   if (c >= F) return;
-  const int W = (mode == 0) ? 2 * F : F;
+  const int W = (mode == 0 || mode == 3) ? 2 * F : F;
   float a[4];
   load4(src, (long)t * W + c, c, a);
   float o[4];
-  if (mode == 0) {
+  if (mode == 0 || mode == 3) {
     float b[4];
     load4(src, (long)t * W + F + c, F + c, b);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) o[j] = silu(a[j]) * b[j];
+    for (int j = 0; j < 4; ++j) o[j] = (mode == 0 ? silu(a[j]) : gelu_tanh(a[j])) * b[j];
   } else if (mode == 1) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -320,13 +323,17 @@ __global__ __launch_bounds__(256) void act8_kernel(const bf16* __restrict__ src,
   const int t = blockIdx.y;
   const int c = (blockIdx.x * blockDim.x + threadIdx.x) * 8;
   if (c >= F) return;
-  const int W = (mode == 0) ? 2 * F : F;
+  const int W = (mode == 0 || mode == 3) ? 2 * F : F;
   const bf16x8 a = *(const bf16x8*)(src + (long)t * W + c);
   bf16x8 ob;
   if (mode == 0) {
     const bf16x8 b = *(const bf16x8*)(src + (long)t * W + F + c);
 #pragma unroll
     for (int j = 0; j < 8; ++j) ob[j] = (bf16)(silu((float)a[j]) * (float)b[j]);
+  } else if (mode == 3) {
+    const bf16x8 b = *(const bf16x8*)(src + (long)t * W + F + c);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ob[j] = (bf16)(gelu_tanh((float)a[j]) * (float)b[j]);
   } else if (mode == 1) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -455,7 +462,7 @@ extern "C" int la_rope_kv(const void* qkv_p, long slab, int S, const void* bias,
 
 extern "C" int la_act(const void* p, long slab, int S, const void* bias, void* out, int T, int F, int mode,
                       void* stream) {
-  if (F & 3) return -1;
+  if ((F & 3) || mode < 0 || mode > 3) return -1;
   if (S == 0 && bias == nullptr && (F & 7) == 0 && ((uintptr_t)p & 15) == 0 && ((uintptr_t)out & 15) == 0) {
     dim3 grid((F / 8 + 255) / 256, T);
     hipLaunchKernelGGL(la::act8_kernel, grid, dim3(256), 0, (hipStream_t)stream, (const bf16*)p, (bf16*)out, F,

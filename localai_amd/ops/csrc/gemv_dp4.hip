@@ -63,6 +63,7 @@ LA_DEV u32x4 ldg16(const uint8_t* p) {
 // ("fused into the GEMM" -- here into the consumer's prologue).
 //   mode 0: x = silu(g) * u with g = row[k], u = row[F + k] (SwiGLU, row width 2F)
 //   mode 1: x = gelu_tanh(row[k]);  mode 2: x = quick_gelu(row[k])      (row width F)
+//   mode 3: x = gelu_tanh(g) * u (GeGLU, row width 2F)
 struct GVAct {
   const float* p;      // [S][M][W] fp32 slabs, W = 2F (mode 0) or F; null = plain bf16 x
   long slab;           // elements between slabs
@@ -91,11 +92,16 @@ LA_DEV float gv_act1(float x, int mode) {
 
 // x[m, k .. k+3] from the activation source (in fp32, never rounded to bf16)
 LA_DEV void gv_act_x(const GVAct& a, int m, int k, float v[4]) {
-  const long W = a.mode == 0 ? 2L * a.F : (long)a.F;
+  const bool glu = a.mode == 0 || a.mode == 3;
+  const long W = glu ? 2L * a.F : (long)a.F;
   const float4 g = gv_sum_slabs(a, m * W + k, k);
   if (a.mode == 0) {
     const float4 u = gv_sum_slabs(a, m * W + a.F + k, a.F + k);
     v[0] = silu(g.x) * u.x; v[1] = silu(g.y) * u.y; v[2] = silu(g.z) * u.z; v[3] = silu(g.w) * u.w;
+  } else if (a.mode == 3) {
+    const float4 u = gv_sum_slabs(a, m * W + a.F + k, a.F + k);
+    v[0] = gv_act1(g.x, 1) * u.x; v[1] = gv_act1(g.y, 1) * u.y; v[2] = gv_act1(g.z, 1) * u.z;
+    v[3] = gv_act1(g.w, 1) * u.w;
   } else {
     v[0] = gv_act1(g.x, a.mode); v[1] = gv_act1(g.y, a.mode); v[2] = gv_act1(g.z, a.mode); v[3] = gv_act1(g.w, a.mode);
   }
@@ -707,7 +713,7 @@ static int launch_gv_m(const GVArgs& a, int nblk, int K, const bf16* X, int ldx,
 // Q4_K planes: p0 = qs, p2 = scm, p3 = dd (p1, the packed header, is unused here).
 // Q6_K planes: p0 = ql, p1 = qh, p2 = sc, p3 = d.
 // act_p != null: x is act(gate|up) computed from fp32 slabs act_p [act_S][M][W] (X unused),
-// W = 2K for act_mode 0 (SwiGLU) else K; act_bias optional [W].
+// W = 2K for act_mode 0 (SwiGLU) / 3 (GeGLU) else K; act_bias optional [W].
 static int qgemv_dp4_impl(int nseg, const int* fmts, const void* const* planes, const int* Ns, int K,
                           const void* X, int ldx, int M, int splits, void* out, int ldo, long slab,
                           const void* act_p, long act_slab, int act_S, const void* act_bias, int act_mode,
@@ -718,8 +724,8 @@ static int qgemv_dp4_impl(int nseg, const int* fmts, const void* const* planes, 
     return -1;
   GVAct act{(const float*)act_p, act_slab, act_S, (const float*)act_bias, act_mode, K};
   if (act_p) {
-    if (act_S < 1 || act_S > 16 || act_mode < 0 || act_mode > 2 ||
-        act_slab < (long)M * (act_mode == 0 ? 2L * K : (long)K))
+    if (act_S < 1 || act_S > 16 || act_mode < 0 || act_mode > 3 ||
+        act_slab < (long)M * ((act_mode == 0 || act_mode == 3) ? 2L * K : (long)K))
       return -1;
   } else if (!X || ldx < K) {
     return -1;

@@ -104,7 +104,8 @@ def test_embeddings_shape_and_determinism(eng):
     assert max(abs(x - y) for x, y in zip(a, b)) < 1e-5
 
 
-@pytest.mark.parametrize("preset", ["tiny-mixtral", "tiny-phi2", "tiny-llama-q8"])
+@pytest.mark.parametrize("preset", ["tiny-mixtral", "tiny-phi2", "tiny-llama-q8", "tiny-qwen2", "tiny-phi3",
+                                    "tiny-gemma"])
 def test_model_families_generate(preset, tmp_path):
     p = str(tmp_path / f"{preset}.gguf")
     synth.write_model(p, preset, exact=True)
@@ -114,6 +115,27 @@ def test_model_families_generate(preset, tmp_path):
     ids = e.tokenize("hello")
     ref = e.model.reference_logits(ids)[-1]
     assert torch.isfinite(ref).all()
+    # the engine's first greedy token is the oracle's argmax (or within a rounding tie of it)
+    first = e.tokenize("hello" + r["text"])[len(ids)] if r["text"] else None
+    if first is not None:
+        top = torch.topk(ref, 2)
+        assert first == int(top.indices[0]) or float(top.values[0] - ref[first]) < 0.05
+
+
+def test_new_family_hparams(tmp_path):
+    """GGUF metadata -> HParams for the Qwen2 / Phi-3 / Gemma layouts."""
+    from localai_amd.gguf import GGUFReader
+    from localai_amd.models.hparams import HParams
+    got = {}
+    for preset in ("tiny-qwen2", "tiny-phi3", "tiny-gemma"):
+        p = str(tmp_path / f"{preset}.gguf")
+        synth.write_model(p, preset)
+        got[preset] = HParams.from_gguf(GGUFReader(p))
+    q, ph, g = got["tiny-qwen2"], got["tiny-phi3"], got["tiny-gemma"]
+    assert q.rope_mode == 1 and q.act == "swiglu" and q.norm_eps == pytest.approx(1e-6)
+    assert ph.head_dim == 96 and ph.rope_mode == 1 and ph.act == "swiglu"
+    assert g.head_dim == 256 and g.q_dim == 512 and g.act == "geglu" and g.tied_embeddings
+    assert g.embed_scale == pytest.approx(16.0)
 
 
 def _png(color, size=40):

@@ -72,6 +72,25 @@ def test_mixtral_moe_graph_decode(tmp_path):
     assert first == int(top.indices[0]) or float(top.values[0] - ref[first]) < 0.05
 
 
+@pytest.mark.parametrize("preset", ["tiny-qwen2", "tiny-phi3", "tiny-gemma"])
+def test_model_families_graph_decode(preset, tmp_path):
+    """Qwen2 (q/k/v biases), Phi-3 (fused qkv + gate|up, head dim 96), Gemma (head dim 256, GeGLU,
+    scaled embeddings): multi-step graph decode == single-step, first token == the fp32 oracle."""
+    from localai_amd.models import synth
+    p = str(tmp_path / f"{preset}.gguf")
+    synth.write_model(p, preset, exact=True)
+    a = _run(_eng(p, 1), ["family check", "two"], max_tokens=8, temperature=0.0, ignore_eos=True)
+    b = _run(_eng(p, 8), ["family check", "two"], max_tokens=8, temperature=0.0, ignore_eos=True)
+    assert [x[1] for x in a] == [8, 8] and a == b
+    eng = _eng(p, 8)
+    ids = eng.tokenize("family check")
+    ref = eng.model.reference_logits(ids)[-1]
+    res = eng.generate("family check", SamplingParams(max_tokens=2, temperature=0.0, ignore_eos=True))
+    first = eng.tokenize("family check" + res["text"])[len(ids)]
+    top = torch.topk(ref, 2)
+    assert first == int(top.indices[0]) or float(top.values[0] - ref[first]) < 0.05
+
+
 def test_llava_on_gpu(tiny_model_path, tmp_path):
     import io
     from PIL import Image
