@@ -116,6 +116,9 @@ class Layer:
     experts: Optional[List[tuple]] = None            # [(gate_up list, down)] per expert
     moe_gu: Optional[object] = None                  # ops.MoEWeights (fused gate|up of every expert)
     moe_down: Optional[object] = None                # ops.MoEWeights
+    post_attn_norm: Optional[torch.Tensor] = None    # Gemma-2: RMSNorm of the attention output
+    post_ffw_norm: Optional[torch.Tensor] = None     # Gemma-2: RMSNorm of the MLP output
+    window: int = 0                                  # sliding-window attention span (0: full)
 
 
 def _raw2d(t, rows: Optional[slice] = None, cols: Optional[slice] = None):
@@ -165,7 +168,7 @@ class DecoderModel:
         if self.ep:
             self.F = hp.n_ff
         self.rot = hp.rope_dim or hp.head_dim
-        self.scale = 1.0 / math.sqrt(hp.head_dim)
+        self.scale = hp.attn_scale or 1.0 / math.sqrt(hp.head_dim)
         self.norm_mode = 0 if hp.norm_type == "rms" else 1
         T = reader.tensors
         dev = device
@@ -254,7 +257,10 @@ class DecoderModel:
                 qkv=qkv, qkv_bias=qkv_bias, wo=wo, wo_bias=wo_b,
                 ffn_norm=f32(b + "ffn_norm.weight"), ffn_norm_b=f32(b + "ffn_norm.bias"),
                 gate_up=gate_up, up_bias=up_b, down=down, down_bias=down_b,
-                router=router, experts=experts, moe_gu=moe_gu, moe_down=moe_down))
+                router=router, experts=experts, moe_gu=moe_gu, moe_down=moe_down,
+                post_attn_norm=f32(b + "post_attention_norm.weight"), post_ffw_norm=f32(b + "post_ffw_norm.weight"),
+                # Gemma-2 alternates sliding-window (even) and global (odd) layers
+                window=hp.sliding_window if hp.sliding_window and i % 2 == 0 else 0))
         self.out_norm = f32("output_norm.weight")
         self.out_norm_b = f32("output_norm.bias")
         vs = sl(hp.n_vocab)
@@ -357,9 +363,21 @@ class DecoderModel:
             f = self._mlp(L, xn)
             ops.add_norm(res, o, nw, nb, eps, nm, want_out=False)
             return ops.add_norm(res, f, nw, nb, eps, nm)
+        if L.post_attn_norm is not None:
+            o = self._post_norm(o, L.post_attn_norm)
         xn = ops.add_norm(res, o, L.ffn_norm, L.ffn_norm_b, eps, nm)
         f = self._mlp(L, xn)
+        if L.post_ffw_norm is not None:
+            f = self._post_norm(f, L.post_ffw_norm)
         return ops.add_norm(res, f, nw, nb, eps, nm)
+
+    def _post_norm(self, p: ops.Partial, w: torch.Tensor) -> ops.Partial:
+        """RMSNorm(p) * w as an fp32 partial (Gemma-2's post-attention / post-FFW norms)."""
+        T = p.M
+        zero = torch.zeros(T, self.hp.n_embd, dtype=torch.float32, device=p.t.device)
+        y = torch.empty_like(zero)
+        ops.add_norm(zero, p, w, None, self.hp.norm_eps, self.norm_mode, out_f32=y)
+        return ops.Partial(y.unsqueeze(0))
 
     def forward(self, fb: ForwardBatch, kv: KVCache, attn_workspace=None, return_hidden: bool = False) -> torch.Tensor:
         """Returns fp32 logits [R, V] for the rows selected by fb.logits_idx (or, with
@@ -380,7 +398,7 @@ class DecoderModel:
                 q = ops.qkv_rope_dp4(xn, L.qkv, fb.pos, fb.slots, self.cos_sin, self.Hq, self.Hkv, self.Dh,
                                      kv.k[i], kv.v[i], kv.block_size)
                 a = ops.attn_decode(q, kv.k[i], kv.v[i], fb.block_tables, fb.seq_lens, self.scale, fb.max_len,
-                                    workspace=attn_workspace)
+                                    workspace=attn_workspace, softcap=hp.attn_softcap, window=L.window)
                 o = self._row_parallel_out(ops.linear(a.view(T, self.Hq * self.Dh), L.wo), L.wo_bias)
                 xn = self._post_attn(i, L, xn, res, o)
                 continue
@@ -389,12 +407,13 @@ class DecoderModel:
                 # RoPE + KV append fused into the decode attention launch (rope_kv when not fusable)
                 a = ops.attn_decode_rope(qkv, fb.pos, fb.slots, self.cos_sin, self.Hq, self.Hkv, self.Dh, self.rot,
                                          hp.rope_mode, kv.k[i], kv.v[i], fb.block_tables, fb.seq_lens, self.scale,
-                                         fb.max_len, workspace=attn_workspace)
+                                         fb.max_len, workspace=attn_workspace, softcap=hp.attn_softcap,
+                                         window=L.window)
             else:
                 q = ops.rope_kv(qkv, fb.pos, fb.slots, self.cos_sin, self.Hq, self.Hkv, self.Dh, self.rot,
                                 hp.rope_mode, kv.k[i], kv.v[i], kv.block_size)
                 a = ops.attn_prefill(q, kv.k[i], kv.v[i], fb.cu_q, fb.ctx_lens, fb.block_tables, self.scale,
-                                     tiles=fb.tiles)
+                                     tiles=fb.tiles, softcap=hp.attn_softcap, window=L.window)
             o = self._row_parallel_out(ops.linear(a.view(T, self.Hq * self.Dh), L.wo), L.wo_bias)
             xn = self._post_attn(i, L, xn, res, o)
         if return_hidden:
@@ -405,7 +424,11 @@ class DecoderModel:
             logits = lp.t[0]
         else:
             logits = ops.reduce(lp)
-        return self.tp.all_gather_cols(logits)
+        logits = self.tp.all_gather_cols(logits)
+        if self.hp.final_softcap:
+            c = self.hp.final_softcap
+            logits = torch.tanh(logits / c) * c
+        return logits
 
     def reference_logits(self, tokens: Sequence[int]) -> torch.Tensor:
         """Plain fp32 PyTorch forward of one sequence (no paging): the numerics oracle for the
@@ -458,11 +481,19 @@ class DecoderModel:
             G = Hq // Hkv
             k = k.repeat_interleave(G, 1)
             v = v.repeat_interleave(G, 1)
-            att = torch.einsum("qhd,khd->hqk", q, k) * self.scale + mask
+            att = torch.einsum("qhd,khd->hqk", q, k) * self.scale
+            if hp.attn_softcap:
+                att = torch.tanh(att / hp.attn_softcap) * hp.attn_softcap
+            att = att + mask
+            if L.window:
+                pos = torch.arange(Tn)
+                att = att.masked_fill((pos.view(-1, 1) - pos.view(1, -1)) >= L.window, float("-inf"))
             a = torch.einsum("hqk,khd->qhd", torch.softmax(att, -1), v).reshape(Tn, Hq * Dh)
             o = a @ deq(L.wo).t()
             if L.wo_bias is not None:
                 o = o + L.wo_bias.cpu()
+            if L.post_attn_norm is not None:
+                o = norm(o, L.post_attn_norm, None)
 
             def mlp(hin):
                 if L.experts is not None:
@@ -490,6 +521,8 @@ class DecoderModel:
                 d = hh @ deq(L.down).t()
                 if L.down_bias is not None:
                     d = d + L.down_bias.cpu()
+                if L.post_ffw_norm is not None:
+                    d = norm(d, L.post_ffw_norm, None)
                 return d
 
             if hp.parallel_residual:
@@ -501,4 +534,6 @@ class DecoderModel:
         lg = x @ deq(self.output).t()
         if self.out_bias is not None:
             lg = lg + self.out_bias.cpu()
+        if hp.final_softcap:
+            lg = torch.tanh(lg / hp.final_softcap) * hp.final_softcap
         return lg

@@ -29,6 +29,10 @@ class HParams:
     parallel_residual: bool = False   # phi-2: h = x + attn(ln x) + mlp(ln x)
     act: str = "swiglu"               # "swiglu" | "gelu" | "geglu" (Gemma: gelu(gate) * up)
     embed_scale: float = 1.0          # Gemma scales the token embeddings by sqrt(n_embd)
+    attn_softcap: float = 0.0         # Gemma-2: scores -> cap * tanh(scores / cap)
+    final_softcap: float = 0.0        # Gemma-2: logits -> cap * tanh(logits / cap)
+    sliding_window: int = 0           # Gemma-2: even layers attend to the last `sliding_window` keys
+    attn_scale: float = 0.0           # query scale override (0: 1/sqrt(head_dim))
     tied_embeddings: bool = False
     name: str = ""
 
@@ -85,6 +89,13 @@ class HParams:
             parallel_residual=a == "phi2",
             act="gelu" if a in ("phi2", "gptneox", "falcon") else ("geglu" if a in ("gemma", "gemma2") else "swiglu"),
             embed_scale=float(n_embd) ** 0.5 if a in ("gemma", "gemma2") else 1.0,
+            attn_softcap=float(g("attn_logit_softcapping", 0.0) or 0.0) if a == "gemma2" else 0.0,
+            final_softcap=float(g("final_logit_softcapping", 0.0) or 0.0) if a == "gemma2" else 0.0,
+            sliding_window=int(g("attention.sliding_window", 0) or 0) if a == "gemma2" else 0,
+            # Gemma-2 27B scales queries by 1/sqrt(n_embd / n_head) (query_pre_attn_scalar 144), not
+            # 1/sqrt(head_dim) (llama.cpp build_gemma2)
+            attn_scale=(float(n_embd // n_head) ** -0.5
+                        if a == "gemma2" and int(g("block_count")) == 46 else 0.0),
             tied_embeddings="output.weight" not in r.tensors,
             name=str(r.kv.get("general.name", "")),
         )

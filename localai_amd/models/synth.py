@@ -52,6 +52,9 @@ class Preset:
     qtype: str = "Q4_K_M"            # Q4_K_M | Q4_K | Q8_0 | F16 | F32
     tokenizer: str = "llama3"        # llama3 | mistral | phi2 | chatml
     tied: bool = False               # no output.weight: the lm_head is token_embd (Gemma, small Qwen2)
+    attn_softcap: float = 0.0        # Gemma-2 keys
+    final_softcap: float = 0.0
+    sliding_window: int = 0
     name: str = "synthetic"
 
     @property
@@ -88,6 +91,13 @@ PRESETS: Dict[str, Preset] = {
     "tiny-gemma": Preset(arch="gemma", n_layer=2, n_embd=256, n_head=2, n_head_kv=1, head_dim=256, n_ff=512,
                          n_vocab=32256, ctx=512, rope_theta=10000.0, eps=1e-6, qtype="Q4_K", tokenizer="mistral",
                          tied=True, name="tiny-gemma"),
+    "tiny-gemma2": Preset(arch="gemma2", n_layer=2, n_embd=256, n_head=2, n_head_kv=1, head_dim=256, n_ff=512,
+                          n_vocab=32256, ctx=512, rope_theta=10000.0, eps=1e-6, qtype="Q4_K", tokenizer="mistral",
+                          tied=True, attn_softcap=50.0, final_softcap=30.0, sliding_window=24, name="tiny-gemma2"),
+    "gemma2-9b": Preset(arch="gemma2", n_layer=42, n_embd=3584, n_head=16, n_head_kv=8, head_dim=256, n_ff=14336,
+                        n_vocab=256000, ctx=8192, rope_theta=10000.0, eps=1e-6, tokenizer="mistral", tied=True,
+                        attn_softcap=50.0, final_softcap=30.0, sliding_window=4096,
+                        name="gemma-2-9b-it (random-init)"),
     "qwen2-7b": Preset(arch="qwen2", n_layer=28, n_embd=3584, n_head=28, n_head_kv=4, n_ff=18944, n_vocab=152064,
                        ctx=32768, rope_theta=1e6, eps=1e-6, tokenizer="chatml", name="Qwen2-7B-Instruct (random-init)"),
     "phi3-mini": Preset(arch="phi3", n_layer=32, n_embd=3072, n_head=32, n_head_kv=32, n_ff=8192, n_vocab=32064,
@@ -222,6 +232,8 @@ def tensor_list(p: Preset):
                 (b + "attn_output.weight", (d, qd), i), (b + "ffn_norm.weight", (d,), i)]
         if p.arch == "qwen2":
             out += [(b + "attn_q.bias", (qd,), i), (b + "attn_k.bias", (kvd,), i), (b + "attn_v.bias", (kvd,), i)]
+        if p.arch == "gemma2":
+            out += [(b + "post_attention_norm.weight", (d,), i), (b + "post_ffw_norm.weight", (d,), i)]
         if p.n_expert:
             E = p.n_expert
             out += [(b + "ffn_gate_inp.weight", (E, d), i), (b + "ffn_gate_exps.weight", (E, p.n_ff, d), i),
@@ -261,6 +273,12 @@ def write_model(path: str, preset: str | Preset, seed: int = 0, exact: bool = Fa
     if p.head_dim:
         w.add_uint32(f"{a}.attention.key_length", hd)
         w.add_uint32(f"{a}.attention.value_length", hd)
+    if p.attn_softcap:
+        w.add_float32(f"{a}.attn_logit_softcapping", p.attn_softcap)
+    if p.final_softcap:
+        w.add_float32(f"{a}.final_logit_softcapping", p.final_softcap)
+    if p.sliding_window:
+        w.add_uint32(f"{a}.attention.sliding_window", p.sliding_window)
     if a == "phi2":
         w.add_float32(f"{a}.attention.layer_norm_epsilon", p.eps)
     else:

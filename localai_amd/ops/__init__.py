@@ -57,8 +57,8 @@ def lib():
             "la_reduce_slabs": [P, LNG, I, P, I, I, P, P, P],
             "la_embed": [I, P, P, P, P, I, I, P, I, P, F, P],
             "la_dequant": [I, P, P, P, P, I, I, P, P],
-            "la_attn_decode": [P, P, P, P, I, P, I, I, I, I, I, F, I, I, P, P, P, P, P, LNG, I, P, P, P, P, I, P],
-            "la_attn_prefill": [P, P, P, P, I, P, P, P, I, I, I, I, I, F, P, P],
+            "la_attn_decode": [P, P, P, P, I, P, I, I, I, I, I, F, I, I, P, P, P, P, P, LNG, I, P, P, P, P, F, I, I, P],
+            "la_attn_prefill": [P, P, P, P, I, P, P, P, I, I, I, I, I, F, P, F, I, P],
             "la_sample": [P, LNG, I, I, P, P, P, P, P],
             "la_penalties": [P, LNG, I, P, I, P, P, I, P, P],
             "la_sample_row_bytes": [],
@@ -717,8 +717,10 @@ def linear_multi(x: torch.Tensor, ws: Sequence[QWeight], bias: Optional[torch.Te
 
 def add_norm(residual: torch.Tensor, add: Optional[Partial], weight: torch.Tensor,
              bias: Optional[torch.Tensor], eps: float, mode: int = 0,
-             out: Optional[torch.Tensor] = None, want_out: bool = True) -> Optional[torch.Tensor]:
-    """residual[T,D] (fp32, updated in place) += add;  return norm(residual)*w(+b) as bf16."""
+             out: Optional[torch.Tensor] = None, want_out: bool = True,
+             out_f32: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+    """residual[T,D] (fp32, updated in place) += add;  return norm(residual)*w(+b) as bf16
+    (out_f32: also written unrounded, in fp32)."""
     T, D = residual.shape
     if add is not None and (add.M != T or add.N != D):
         raise ValueError(f"add_norm: add {tuple(add.t.shape)} vs residual {T}x{D}")
@@ -736,6 +738,8 @@ def add_norm(residual: torch.Tensor, add: Optional[Partial], weight: torch.Tenso
             y = (x - mu) * torch.rsqrt(var + eps) * weight
             if bias is not None:
                 y = y + bias
+        if out_f32 is not None:
+            out_f32.copy_(y)
         return y.to(torch.bfloat16)
     assert residual.dtype == torch.float32 and residual.is_contiguous()
     if want_out and out is None:
@@ -743,7 +747,7 @@ def add_norm(residual: torch.Tensor, add: Optional[Partial], weight: torch.Tenso
     a = add.src_args() if add is not None else (None, 0, 0, None)
     _check(lib().la_add_norm(residual.data_ptr(), a[0], a[1], a[2], a[3], int(add is not None),
                              weight.data_ptr(), _ptr(bias), _ptr(out) if want_out else None, T, D,
-                             float(eps), mode, None, _stream()), "la_add_norm")
+                             float(eps), mode, _ptr(out_f32), _stream()), "la_add_norm")
     return out if want_out else None
 
 
@@ -933,15 +937,17 @@ def decode_workspace(B: int, Hq: int, Hkv: int, Dh: int, max_len: int, device, b
 
 def attn_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, block_tables: torch.Tensor,
                 seq_lens: torch.Tensor, scale: float, max_seq_len: int, out: Optional[torch.Tensor] = None,
-                workspace: Optional[Tuple[torch.Tensor, ...]] = None) -> torch.Tensor:
-    """q [B,Hq,Dh] bf16; K cache [nblk,Hkv,BS,Dh]; V cache (transposed pages) [nblk,Hkv,Dh,BS];
-    block_tables [B,maxb] i32; seq_lens [B] i32."""
+                workspace: Optional[Tuple[torch.Tensor, ...]] = None, softcap: float = 0.0,
+                window: int = 0) -> torch.Tensor:
+    """q [B,Hq,Dh] bf16; K cache [nblk,Hkv,BS,Dh]; V cache (grouped-transposed pages)
+    [nblk,Hkv,BS/8,Dh,8]; block_tables [B,maxb] i32; seq_lens [B] i32.  softcap > 0: scores
+    softcap * tanh(s / softcap); window > 0: only the last `window` keys are attended (Gemma-2)."""
     B, Hq, Dh = q.shape
     nblk, Hkv, BS, Dh2 = k_cache.shape
     if Dh2 != Dh or Hq % Hkv or tuple(v_cache.shape) != (nblk, Hkv, BS // 8, Dh, 8):
         raise ValueError("attn_decode: head/cache shape mismatch")
     if not q.is_cuda:
-        return _attn_ref_decode(q, k_cache, v_cache, block_tables, seq_lens, scale)
+        return _attn_ref_decode(q, k_cache, v_cache, block_tables, seq_lens, scale, softcap, window)
     P, PS = decode_partitions(B, Hkv, max_seq_len, BS)
     if out is None:
         out = torch.empty(B, Hq, Dh, dtype=torch.bfloat16, device=q.device)
@@ -952,7 +958,7 @@ def attn_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, b
     _check(lib().la_attn_decode(q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr(),
                                 block_tables.shape[1], seq_lens.data_ptr(), B, Hq, Hkv, Dh, BS, float(scale), P, PS,
                                 out.data_ptr(), po.data_ptr(), pml.data_ptr(), tk.data_ptr(), None, 0, 0, None, None,
-                                None, None, decode_waves(B, Hkv), _stream()),
+                                None, None, float(softcap), int(window), decode_waves(B, Hkv), _stream()),
            "la_attn_decode")
     return out
 
@@ -967,7 +973,8 @@ def attn_decode_rope(qkv: Partial, pos: torch.Tensor, slots: torch.Tensor, cos_s
                      Hkv: int, Dh: int, rot: int, mode: int, k_cache: torch.Tensor, v_cache: torch.Tensor,
                      block_tables: torch.Tensor, seq_lens: torch.Tensor, scale: float, max_seq_len: int,
                      out: Optional[torch.Tensor] = None,
-                     workspace: Optional[Tuple[torch.Tensor, ...]] = None) -> torch.Tensor:
+                     workspace: Optional[Tuple[torch.Tensor, ...]] = None, softcap: float = 0.0,
+                     window: int = 0) -> torch.Tensor:
     """Decode step attention with the step's RoPE + paged KV append fused into the attention
     kernel (one launch instead of rope_kv + attn_decode).  Same numerics as the two-kernel path
     (q/k rotated in fp32, rounded to bf16).  Falls back to rope_kv + attn_decode for NEOX /
@@ -981,7 +988,7 @@ def attn_decode_rope(qkv: Partial, pos: torch.Tensor, slots: torch.Tensor, cos_s
     if not fusable:
         q = rope_kv(qkv, pos, slots, cos_sin, Hq, Hkv, Dh, rot, mode, k_cache, v_cache, BS)
         return attn_decode(q, k_cache, v_cache, block_tables, seq_lens, scale, max_seq_len, out=out,
-                           workspace=workspace)
+                           workspace=workspace, softcap=softcap, window=window)
     if Hq % Hkv or tuple(v_cache.shape) != (nblk, Hkv, BS // 8, Dh, 8) or k_cache.shape[3] != Dh:
         raise ValueError("attn_decode_rope: head/cache shape mismatch")
     P, PS = decode_partitions(T, Hkv, max_seq_len, BS)
@@ -995,7 +1002,8 @@ def attn_decode_rope(qkv: Partial, pos: torch.Tensor, slots: torch.Tensor, cos_s
     _check(lib().la_attn_decode(None, k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr(),
                                 block_tables.shape[1], seq_lens.data_ptr(), T, Hq, Hkv, Dh, BS, float(scale), P, PS,
                                 out.data_ptr(), po.data_ptr(), pml.data_ptr(), tk.data_ptr(), a[0], a[1], a[2], a[3],
-                                pos.data_ptr(), slots.data_ptr(), cos_sin.data_ptr(), decode_waves(T, Hkv), _stream()),
+                                pos.data_ptr(), slots.data_ptr(), cos_sin.data_ptr(), float(softcap), int(window),
+                                decode_waves(T, Hkv), _stream()),
            "la_attn_decode(rope)")
     return out
 
@@ -1022,7 +1030,16 @@ def _gather_kv(cache, bt_row, L, transposed=False):
     return blocks.permute(1, 0, 2, 3).reshape(cache.shape[1], nb * BS, cache.shape[3])[:, :L]
 
 
-def _attn_ref_decode(q, kc, vc, bt, sl, scale):
+def _softcap_window(s, softcap, window, qpos, kpos):
+    """Gemma-2 score transforms of the CPU references: soft-capping, then the sliding window."""
+    if softcap > 0:
+        s = softcap * torch.tanh(s / softcap)
+    if window > 0:
+        s = s.masked_fill(qpos - kpos >= window, float("-inf"))
+    return s
+
+
+def _attn_ref_decode(q, kc, vc, bt, sl, scale, softcap=0.0, window=0):
     B, Hq, Dh = q.shape
     Hkv = kc.shape[1]
     G = Hq // Hkv
@@ -1033,6 +1050,7 @@ def _attn_ref_decode(q, kc, vc, bt, sl, scale):
         v = _gather_kv(vc, bt[b], L, transposed=True).float()
         qq = q[b].float().view(Hkv, G, Dh)
         s = torch.einsum("hgd,hld->hgl", qq, k) * scale
+        s = _softcap_window(s, softcap, window, torch.tensor(L - 1), torch.arange(L))
         p = torch.softmax(s, -1)
         out[b] = torch.einsum("hgl,hld->hgd", p, v).reshape(Hq, Dh).to(q.dtype)
     return out
@@ -1052,12 +1070,12 @@ def prefill_tiles(q_lens: Sequence[int], device) -> torch.Tensor:
 def attn_prefill(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, cu_q: torch.Tensor,
                  ctx_lens: torch.Tensor, block_tables: torch.Tensor, scale: float,
                  tiles: Optional[torch.Tensor] = None, q_lens: Optional[Sequence[int]] = None,
-                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                 out: Optional[torch.Tensor] = None, softcap: float = 0.0, window: int = 0) -> torch.Tensor:
     """Causal attention for new tokens. q [T,Hq,Dh]; cu_q [nseq+1]; ctx_lens [nseq] (cached+new)."""
     T, Hq, Dh = q.shape
     Hkv = k_cache.shape[1]
     if not q.is_cuda:
-        return _attn_ref_prefill(q, k_cache, v_cache, cu_q, ctx_lens, block_tables, scale)
+        return _attn_ref_prefill(q, k_cache, v_cache, cu_q, ctx_lens, block_tables, scale, softcap, window)
     if tiles is None:
         cq = cu_q.cpu().tolist()
         tiles = prefill_tiles([cq[i + 1] - cq[i] for i in range(len(cq) - 1)], q.device)
@@ -1066,11 +1084,11 @@ def attn_prefill(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, 
     _check(lib().la_attn_prefill(q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), tiles.data_ptr(),
                                  tiles.shape[0], cu_q.data_ptr(), ctx_lens.data_ptr(), block_tables.data_ptr(),
                                  block_tables.shape[1], Hq, Hkv, Dh, k_cache.shape[2], float(scale),
-                                 out.data_ptr(), _stream()), "la_attn_prefill")
+                                 out.data_ptr(), float(softcap), int(window), _stream()), "la_attn_prefill")
     return out
 
 
-def _attn_ref_prefill(q, kc, vc, cu_q, ctx_lens, bt, scale):
+def _attn_ref_prefill(q, kc, vc, cu_q, ctx_lens, bt, scale, softcap=0.0, window=0):
     T, Hq, Dh = q.shape
     Hkv = kc.shape[1]
     G = Hq // Hkv
@@ -1088,6 +1106,7 @@ def _attn_ref_prefill(q, kc, vc, cu_q, ctx_lens, bt, scale):
         sc = torch.einsum("hqd,hld->hql", qq, k) * scale
         qpos = torch.arange(L - ql, L).view(-1, 1)
         kpos = torch.arange(L).view(1, -1)
+        sc = _softcap_window(sc, softcap, window, qpos, kpos)
         sc = sc.masked_fill(kpos > qpos, float("-inf"))
         p = torch.softmax(sc, -1)
         out[a:b] = torch.einsum("hql,hld->hqd", p, v).transpose(0, 1).to(q.dtype)

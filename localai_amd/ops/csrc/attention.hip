@@ -115,7 +115,8 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
     const bf16* __restrict__ q, const bf16* __restrict__ kc, const bf16* __restrict__ vc,
     const int* __restrict__ block_tables, int max_blocks, const int* __restrict__ seq_lens, int Hkv, int G,
     int BS, float scale_log2, int PS_grid, bf16* __restrict__ out, float* __restrict__ part_o,
-    float* __restrict__ part_ml, int P, int* __restrict__ tickets, DecRope R) {
+    float* __restrict__ part_ml, int P, int* __restrict__ tickets, DecRope R, float cap_l2, float cap_mul,
+    int window) {
   constexpr int KC = (DH + 31) / 32;  // 32-wide k chunks of the QK^T product
   constexpr int ND = DH / 16;         // 16-wide d tiles of the PV product
   constexpr int NT = NW * 64;
@@ -131,6 +132,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
   const int PS = (L <= DEC_ONE_PART && PS_grid < DEC_ONE_PART) ? DEC_ONE_PART : PS_grid;
   const int t0 = p * PS;
   if (t0 >= L) return;  // empty partition: the combiner only waits for ceil(L / PS) of them
+  const int wlo = window > 0 ? L - window : 0;  // first key inside the sliding window
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 15, g = lane >> 4;
   const int kend = min(L, t0 + PS);
@@ -246,7 +248,13 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
           acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, qf[c], acc, 0, 0, 0);
         }
 #pragma unroll
-        for (int i = 0; i < 4; ++i) s[t][i] = (kb + 8 * g + 4 * t + i < kend) ? acc[i] * scale_log2 : -INFINITY;
+        for (int i = 0; i < 4; ++i) {
+          const int key = kb + 8 * g + 4 * t + i;
+          // Gemma-2 logit soft-capping cap * tanh(s / cap) (cap_l2 = cap * log2 e, 0: off) and
+          // sliding-window attention (keys at least `window` positions behind the query masked)
+          const float sv = cap_l2 > 0.f ? cap_l2 * tanhf(acc[i] * cap_mul) : acc[i] * scale_log2;
+          s[t][i] = (key < kend && key >= wlo) ? sv : -INFINITY;
+        }
       }
       // online softmax for head r over this 32-key tile
       float mx = fmaxf(fmaxf(fmaxf(s[0][0], s[0][1]), fmaxf(s[0][2], s[0][3])),
@@ -411,7 +419,7 @@ __global__ __launch_bounds__(PF_T) void attn_prefill_kernel(
     const int* __restrict__ cu_q,           // [nseq+1] token offsets of each seq's queries
     const int* __restrict__ ctx_lens,       // [nseq] total keys (cached + new)
     const int* __restrict__ block_tables, int max_blocks, int Hq, int Hkv, int BS, float scale,
-    bf16* __restrict__ out) {
+    bf16* __restrict__ out, float cap, int window) {
   constexpr int DP = (DH + 31) / 32 * 32;  // padded head dim for the MFMA k loop
   constexpr int KC = DP / 32;               // k-chunks of 32
   constexpr int ND = DP / 16;               // 16-wide output column tiles
@@ -503,9 +511,14 @@ __global__ __launch_bounds__(PF_T) void attn_prefill_kernel(
       const int qr = r0 + wave * 16 + 4 * fq + i;
       const int qpos = pos0 + qr;
       float v0 = sacc[0][i] * sl2, v1 = sacc[1][i] * sl2;
+      if (cap > 0.f) {  // soft-capping (Gemma-2): cap * tanh(s / cap), in the log2 domain
+        v0 = cap * 1.4426950408889634f * tanhf(sacc[0][i] * scale / cap);
+        v1 = cap * 1.4426950408889634f * tanhf(sacc[1][i] * scale / cap);
+      }
       const int key0 = k0 + fr, key1 = k0 + 16 + fr;
-      if (key0 > qpos || key0 >= kend || qr >= qlen) v0 = -INFINITY;
-      if (key1 > qpos || key1 >= kend || qr >= qlen) v1 = -INFINITY;
+      const int wlo = window > 0 ? qpos - window + 1 : 0;
+      if (key0 > qpos || key0 >= kend || qr >= qlen || key0 < wlo) v0 = -INFINITY;
+      if (key1 > qpos || key1 >= kend || qr >= qlen || key1 < wlo) v1 = -INFINITY;
       float mx = group_max<16>(fmaxf(v0, v1));
       const float mnew = fmaxf(mrow[i], mx);
       const float msafe = (mnew == -INFINITY) ? 0.f : mnew;
@@ -551,7 +564,7 @@ extern "C" int la_attn_decode(const void* q, const void* kc, const void* vc, con
                               const int* seq_lens, int B, int Hq, int Hkv, int Dh, int BS, float scale, int P, int PS,
                               void* out, void* part_o, void* part_ml, void* tickets, const void* rope_p,
                               long rope_slab, int rope_S, const void* rope_bias, const int* pos, const int* slots,
-                              const float* cos_sin, int nw, void* stream) {
+                              const float* cos_sin, float softcap, int window, int nw, void* stream) {
   if (Hq % Hkv || Hq / Hkv > 16 || (BS % 16) || (128 % BS && BS % 128) || (PS % 128) || P < 1 ||
       (nw != 1 && nw != 4) ||
       PS / BS > la::DEC_MAXBT || P > 64 || (P > 1 && !tickets))
@@ -567,10 +580,12 @@ extern "C" int la_attn_decode(const void* q, const void* kc, const void* vc, con
   float* pml = (float*)part_ml;
   int* tk = (int*)tickets;
   const float sl2 = scale * 1.4426950408889634f;
+  const float cap_l2 = softcap > 0.f ? softcap * 1.4426950408889634f : 0.f;
+  const float cap_mul = softcap > 0.f ? scale / softcap : 0.f;
 #define DEC_NW(D, GT, NW)                                                                                         \
   hipLaunchKernelGGL((la::attn_decode_kernel<D, GT, NW>), grid, dim3(NW * 64), 0, st, (const bf16*)q,           \
                      (const bf16*)kc, (const bf16*)vc, block_tables, max_blocks, seq_lens, Hkv, G, BS, sl2, PS,  \
-                     (bf16*)out, po, pml, P, tk, R)
+                     (bf16*)out, po, pml, P, tk, R, cap_l2, cap_mul, window)
 #define DEC(D, GT)          \
   do {                      \
     if (nw == 1)            \
@@ -600,14 +615,15 @@ extern "C" int la_attn_decode(const void* q, const void* kc, const void* vc, con
 
 extern "C" int la_attn_prefill(const void* q, const void* kc, const void* vc, const int* tiles, int ntiles,
                                const int* cu_q, const int* ctx_lens, const int* block_tables, int max_blocks, int Hq,
-                               int Hkv, int Dh, int BS, float scale, void* out, void* stream) {
+                               int Hkv, int Dh, int BS, float scale, void* out, float softcap, int window,
+                               void* stream) {
   if (Hq % Hkv) return -1;
   hipStream_t st = (hipStream_t)stream;
   dim3 grid(ntiles, Hq);
 #define PF(D)                                                                                                     \
   hipLaunchKernelGGL(la::attn_prefill_kernel<D>, grid, dim3(la::PF_T), 0, st, (const bf16*)q, (const bf16*)kc,    \
                      (const bf16*)vc, tiles, cu_q, ctx_lens, block_tables, max_blocks, Hq, Hkv, BS, scale,       \
-                     (bf16*)out)
+                     (bf16*)out, softcap, window)
   switch (Dh) {
     case 64: PF(64); break;
     case 80: PF(80); break;

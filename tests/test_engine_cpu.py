@@ -105,7 +105,7 @@ def test_embeddings_shape_and_determinism(eng):
 
 
 @pytest.mark.parametrize("preset", ["tiny-mixtral", "tiny-phi2", "tiny-llama-q8", "tiny-qwen2", "tiny-phi3",
-                                    "tiny-gemma"])
+                                    "tiny-gemma", "tiny-gemma2"])
 def test_model_families_generate(preset, tmp_path):
     p = str(tmp_path / f"{preset}.gguf")
     synth.write_model(p, preset, exact=True)
@@ -136,6 +136,29 @@ def test_new_family_hparams(tmp_path):
     assert ph.head_dim == 96 and ph.rope_mode == 1 and ph.act == "swiglu"
     assert g.head_dim == 256 and g.q_dim == 512 and g.act == "geglu" and g.tied_embeddings
     assert g.embed_scale == pytest.approx(16.0)
+    p2 = str(tmp_path / "g2.gguf")
+    synth.write_model(p2, "tiny-gemma2")
+    g2 = HParams.from_gguf(GGUFReader(p2))
+    assert (g2.attn_softcap, g2.final_softcap, g2.sliding_window) == (50.0, 30.0, 24) and g2.act == "geglu"
+
+
+def test_gemma2_window_and_softcap_engine_matches_oracle(tmp_path):
+    """A prompt longer than the sliding window: the engine's chunked paged attention (softcap,
+    window on layer 0, post norms, final-logit softcap) reproduces the oracle's last-token logits."""
+    p = str(tmp_path / "g2.gguf")
+    synth.write_model(p, "tiny-gemma2", exact=True)
+    e = _engine(p)
+    prompt = "the quick brown fox jumps over the lazy dog " * 4
+    ids = e.tokenize(prompt)
+    assert len(ids) > 24
+    ref = e.model.reference_logits(ids)[-1]
+    r = e.generate(prompt, SamplingParams(max_tokens=1, temperature=0.0, ignore_eos=True))
+    full = e.tokenize(prompt + r["text"])
+    first = full[len(ids)] if r["text"] and full[:len(ids)] == ids else None
+    assert torch.isfinite(ref).all() and float(ref.abs().max()) <= 30.0 + 1e-4
+    if first is not None:
+        top = torch.topk(ref, 2)
+        assert first == int(top.indices[0]) or float(top.values[0] - ref[first]) < 0.05
 
 
 def _png(color, size=40):

@@ -72,7 +72,7 @@ def test_mixtral_moe_graph_decode(tmp_path):
     assert first == int(top.indices[0]) or float(top.values[0] - ref[first]) < 0.05
 
 
-@pytest.mark.parametrize("preset", ["tiny-qwen2", "tiny-phi3", "tiny-gemma"])
+@pytest.mark.parametrize("preset", ["tiny-qwen2", "tiny-phi3", "tiny-gemma", "tiny-gemma2"])
 def test_model_families_graph_decode(preset, tmp_path):
     """Qwen2 (q/k/v biases), Phi-3 (fused qkv + gate|up, head dim 96), Gemma (head dim 256, GeGLU,
     scaled embeddings): multi-step graph decode == single-step, first token == the fp32 oracle."""

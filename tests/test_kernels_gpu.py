@@ -641,3 +641,30 @@ def test_moe_grouped_gemm_expert_parallel(T):
             r_gu = x[t].float().cpu() @ gu[e].ref.t()
             assert (gup.dense()[p].cpu() - r_gu).abs().max() < 2e-2 * max(1.0, r_gu.abs().max())
     assert (z.cpu() - ref).abs().max() < 2e-2 * max(1.0, ref.abs().max())
+
+
+@pytest.mark.parametrize("Dh", [128, 256])
+def test_attn_softcap_window(Dh):
+    """Gemma-2 attention transforms on the GPU kernels (decode incl. split-KV partitions, and
+    prefill over a prefix-cached context) vs the CPU references: cap * tanh(s / cap) and a
+    sliding window shorter than the context."""
+    Hq, Hkv, BS, cap, win = 8, 2, 32, 50.0 / 8, 100
+    lens = [37, 300, 1025]
+    kc, vc, bt = _paged_setup(lens, Hkv, Dh, BS, seed=9)
+    g = torch.Generator().manual_seed(10)
+    q = (torch.randn(len(lens), Hq, Dh, generator=g) * 3).to(torch.bfloat16)
+    sl = torch.tensor(lens, dtype=torch.int32)
+    ref = ops.attn_decode(q, kc, vc, bt, sl, 0.088, max(lens), softcap=cap, window=win)
+    for ml in (max(lens), 4096):
+        out = ops.attn_decode(q.to(DEV), kc.to(DEV), vc.to(DEV), bt.to(DEV), sl.to(DEV), 0.088, ml, softcap=cap,
+                              window=win)
+        assert (out.float().cpu() - ref.float()).abs().max().item() < 2e-2
+    qlens, ctx = [70, 5, 150], [70, 41, 300]
+    kc, vc, bt = _paged_setup(ctx, Hkv, Dh, BS, seed=11)
+    qp = (torch.randn(sum(qlens), Hq, Dh, generator=g) * 3).to(torch.bfloat16)
+    cu = torch.tensor([0] + list(np.cumsum(qlens)), dtype=torch.int32)
+    cl = torch.tensor(ctx, dtype=torch.int32)
+    ref = ops.attn_prefill(qp, kc, vc, cu, cl, bt, 0.088, softcap=cap, window=win)
+    out = ops.attn_prefill(qp.to(DEV), kc.to(DEV), vc.to(DEV), cu.to(DEV), cl.to(DEV), bt.to(DEV), 0.088,
+                           softcap=cap, window=win)
+    assert (out.float().cpu() - ref.float()).abs().max().item() < 3e-2
