@@ -63,6 +63,7 @@ class EngineConfig:
     mmproj: str = ""                  # LLaVA vision tower + projector GGUF (images in prompts)
     bias_capacity: int = 16           # logit-bias / EOS-ban entries per sequence inside the graph
     blas_tune: bool = True            # tune the hipBLASLt/rocBLAS solution per decode GEMM shape at warm-up
+    lora_adapters: tuple = ()         # ((adapter GGUF path, scale), ...) merged into the weights at load
 
 
 @dataclass
@@ -127,7 +128,12 @@ class LLMEngine:
             ro["freq_scale"] = cfg.rope_freq_scale
         if cfg.rope_scaling:
             ro["type"] = cfg.rope_scaling
-        self.model = DecoderModel(self.reader, self.device, tp=tp, max_pos=cfg.context_size, rope_overrides=ro)
+        lora = None
+        if cfg.lora_adapters:
+            from ..models.lora import LoraSet
+            lora = LoraSet(cfg.lora_adapters)
+        self.model = DecoderModel(self.reader, self.device, tp=tp, max_pos=cfg.context_size, rope_overrides=ro,
+                                  lora=lora)
         self.hp = self.model.hp
         self.vocab = core.Vocab(self.tokenizer.pieces)
         self.gvocab = core.GrammarVocab(self.tokenizer.pieces, sorted(self.tokenizer.eog))

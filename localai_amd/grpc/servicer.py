@@ -153,7 +153,8 @@ class EngineServicer:
                 embeddings=request.Embeddings, rope_freq_base=request.RopeFreqBase,
                 rope_freq_scale=request.RopeFreqScale, rope_scaling=request.RopeScaling,
                 use_graphs=not request.EnforceEager,
-                mmproj=self._mmproj_path(request, path))
+                mmproj=self._mmproj_path(request, path),
+                lora_adapters=self._lora(request, path))
             loop = asyncio.get_running_loop()
             eng = await loop.run_in_executor(None, lambda: LLMEngine(cfg, tp=self.tp))
             await loop.run_in_executor(None, eng.warmup)
@@ -170,6 +171,15 @@ class EngineServicer:
             log.exception("LoadModel failed")
             self.state = pb.StatusResponse.ERROR
             return pb.Result(success=False, message=f"could not load model: {e}")
+
+    @staticmethod
+    def _lora(request, model_path: str):
+        """grpc-server.cpp:2263-2271: an adapter only when both LoraAdapter and LoraBase are set,
+        relative to the model's directory, scale LoraScale (1.0 when 0)."""
+        if not request.LoraAdapter or not request.LoraBase:
+            return ()
+        from ..models.lora import adapter_path
+        return ((adapter_path(model_path, request.LoraAdapter), float(request.LoraScale or 1.0)),)
 
     @staticmethod
     def _mmproj_path(request, model_path: str) -> str:

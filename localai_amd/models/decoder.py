@@ -1,5 +1,5 @@
-"""Decoder-only transformer families served by the engine: llama (Llama-2/3, Mistral),
-llama+MoE (Mixtral), phi2.
+"""Decoder-only transformer families served by the engine: llama (Llama-2/3, Mistral, Yi,
+DeepSeek-coder), llama+MoE (Mixtral), phi2, phi3, qwen2, gemma, gemma2, command-r, starcoder2.
 
 Replaces the llama.cpp graph the reference's backend drives through llama_decode
 (`backend/cpp/llama/grpc-server.cpp:1910`, [external]).  The forward pass is a fixed
@@ -147,7 +147,7 @@ def _raw2d(t, rows: Optional[slice] = None, cols: Optional[slice] = None):
 
 class DecoderModel:
     def __init__(self, reader: GGUFReader, device: torch.device, tp: Optional[TPInfo] = None,
-                 max_pos: Optional[int] = None, rope_overrides: Optional[dict] = None):
+                 max_pos: Optional[int] = None, rope_overrides: Optional[dict] = None, lora=None):
         self.hp = hp = HParams.from_gguf(reader)
         self.device = device
         self.tp = tp = tp or TPInfo()
@@ -180,6 +180,16 @@ class DecoderModel:
             return torch.from_numpy(arr).to(dev)
 
         def qw(name, rows=None, cols=None):
+            if lora is not None and name in lora:
+                # LoRA-adapted weight: base + deltas merged in fp32, kept as BF16 (models/lora.py)
+                t = T[name]
+                w = lora.merged(name, dequantize(t.data, t.ggml_type, t.shape).reshape(t.shape[-2], t.shape[-1]))
+                if rows is not None:
+                    w = w[rows]
+                if cols is not None:
+                    w = w[:, cols]
+                w = np.ascontiguousarray(w)
+                return ops.QWeight.from_raw(quantize(w, GGMLType.BF16), GGMLType.BF16, w.shape, dev)
             raw, shape, gt = _raw2d(T[name], rows, cols)
             return ops.QWeight.from_raw(raw, gt, shape, dev)
 
@@ -229,7 +239,7 @@ class DecoderModel:
                     de = self._expert_slice(T[b + "ffn_down_exps.weight"], e, cols=None if self.ep else sl(hp.n_ff))
                     gu = ops.concat_rows([ge, ue])
                     experts.append(([gu] if gu is not None else [ge, ue], de))
-            elif hp.arch == "phi2":
+            elif b + "ffn_gate.weight" not in T and hp.act == "gelu":  # phi-2 / starcoder2: up -> gelu -> down
                 gate_up = [qw(b + "ffn_up.weight", rows=fs)]
                 up_b = vec_slice(f32(b + "ffn_up.bias"), fs)
                 down = qw(b + "ffn_down.weight", cols=fs)
@@ -425,6 +435,8 @@ class DecoderModel:
         else:
             logits = ops.reduce(lp)
         logits = self.tp.all_gather_cols(logits)
+        if self.hp.logit_scale != 1.0:
+            logits = logits * self.hp.logit_scale
         if self.hp.final_softcap:
             c = self.hp.final_softcap
             logits = torch.tanh(logits / c) * c
@@ -534,6 +546,7 @@ class DecoderModel:
         lg = x @ deq(self.output).t()
         if self.out_bias is not None:
             lg = lg + self.out_bias.cpu()
+        lg = lg * hp.logit_scale
         if hp.final_softcap:
             lg = torch.tanh(lg / hp.final_softcap) * hp.final_softcap
         return lg

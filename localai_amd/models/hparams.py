@@ -33,6 +33,7 @@ class HParams:
     final_softcap: float = 0.0        # Gemma-2: logits -> cap * tanh(logits / cap)
     sliding_window: int = 0           # Gemma-2: even layers attend to the last `sliding_window` keys
     attn_scale: float = 0.0           # query scale override (0: 1/sqrt(head_dim))
+    logit_scale: float = 1.0          # Command-R multiplies the logits (0.0625)
     tied_embeddings: bool = False
     name: str = ""
 
@@ -57,7 +58,8 @@ class HParams:
         if "token_embd.weight" in r.tensors:
             n_vocab = r.tensors["token_embd.weight"].shape[0]
         rope_dim = int(g("rope.dimension_count", head_dim))
-        neox_archs = {"phi2", "phi3", "qwen2", "qwen2moe", "gptneox", "stablelm", "gemma", "gemma2", "falcon"}
+        neox_archs = {"phi2", "phi3", "qwen2", "qwen2moe", "gptneox", "stablelm", "gemma", "gemma2", "falcon",
+                      "starcoder2"}
         eps = g("attention.layer_norm_rms_epsilon")
         norm_type = "rms"
         if eps is None:
@@ -86,8 +88,11 @@ class HParams:
             norm_type=norm_type,
             n_expert=int(g("expert_count", 0) or 0),
             n_expert_used=int(g("expert_used_count", 0) or 0),
-            parallel_residual=a == "phi2",
-            act="gelu" if a in ("phi2", "gptneox", "falcon") else ("geglu" if a in ("gemma", "gemma2") else "swiglu"),
+            # phi-2 / Command-R: h = x + attn(ln x) + mlp(ln x)
+            parallel_residual=a in ("phi2", "command-r"),
+            act="gelu" if a in ("phi2", "gptneox", "falcon", "starcoder2")
+            else ("geglu" if a in ("gemma", "gemma2") else "swiglu"),
+            logit_scale=float(g("logit_scale", 1.0) or 1.0),
             embed_scale=float(n_embd) ** 0.5 if a in ("gemma", "gemma2") else 1.0,
             attn_softcap=float(g("attn_logit_softcapping", 0.0) or 0.0) if a == "gemma2" else 0.0,
             final_softcap=float(g("final_logit_softcapping", 0.0) or 0.0) if a == "gemma2" else 0.0,

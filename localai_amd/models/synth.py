@@ -17,7 +17,7 @@ import json
 import os
 from dataclasses import dataclass, field, replace
 from pathlib import Path
-from typing import Dict, List, Optional
+from typing import Dict, List, Optional, Sequence
 
 import numpy as np
 
@@ -55,6 +55,7 @@ class Preset:
     attn_softcap: float = 0.0        # Gemma-2 keys
     final_softcap: float = 0.0
     sliding_window: int = 0
+    logit_scale: float = 0.0         # Command-R
     name: str = "synthetic"
 
     @property
@@ -98,6 +99,14 @@ PRESETS: Dict[str, Preset] = {
                         n_vocab=256000, ctx=8192, rope_theta=10000.0, eps=1e-6, tokenizer="mistral", tied=True,
                         attn_softcap=50.0, final_softcap=30.0, sliding_window=4096,
                         name="gemma-2-9b-it (random-init)"),
+    # Command-R: bias-free LayerNorm, parallel residual, logit scale, tied lm_head; StarCoder2: LayerNorm
+    # with bias, biased projections, gelu MLP without a gate, NEOX rotary
+    "tiny-command-r": Preset(arch="command-r", n_layer=2, n_embd=256, n_head=4, n_head_kv=2, n_ff=512,
+                             n_vocab=32256, ctx=512, rope_theta=8e6, qtype="Q4_K", tokenizer="llama3", tied=True,
+                             logit_scale=0.0625, name="tiny-command-r"),
+    "tiny-starcoder2": Preset(arch="starcoder2", n_layer=2, n_embd=256, n_head=4, n_head_kv=2, n_ff=512,
+                              n_vocab=32256, ctx=512, rope_theta=1e5, qtype="Q8_0", tokenizer="phi2",
+                              name="tiny-starcoder2"),
     "qwen2-7b": Preset(arch="qwen2", n_layer=28, n_embd=3584, n_head=28, n_head_kv=4, n_ff=18944, n_vocab=152064,
                        ctx=32768, rope_theta=1e6, eps=1e-6, tokenizer="chatml", name="Qwen2-7B-Instruct (random-init)"),
     "phi3-mini": Preset(arch="phi3", n_layer=32, n_embd=3072, n_head=32, n_head_kv=32, n_ff=8192, n_vocab=32064,
@@ -222,6 +231,20 @@ def tensor_list(p: Preset):
                     (b + "ffn_up.weight", (p.n_ff, d), i), (b + "ffn_up.bias", (p.n_ff,), i),
                     (b + "ffn_down.weight", (d, p.n_ff), i), (b + "ffn_down.bias", (d,), i)]
             continue
+        if p.arch in ("command-r", "starcoder2"):
+            out += [(b + "attn_norm.weight", (d,), i), (b + "attn_q.weight", (qd, d), i),
+                    (b + "attn_k.weight", (kvd, d), i), (b + "attn_v.weight", (kvd, d), i),
+                    (b + "attn_output.weight", (d, qd), i)]
+            if p.arch == "command-r":  # parallel block: one norm, gated MLP
+                out += [(b + "ffn_gate.weight", (p.n_ff, d), i), (b + "ffn_up.weight", (p.n_ff, d), i),
+                        (b + "ffn_down.weight", (d, p.n_ff), i)]
+            else:
+                out += [(b + "attn_norm.bias", (d,), i), (b + "attn_q.bias", (qd,), i), (b + "attn_k.bias", (kvd,), i),
+                        (b + "attn_v.bias", (kvd,), i), (b + "attn_output.bias", (d,), i),
+                        (b + "ffn_norm.weight", (d,), i), (b + "ffn_norm.bias", (d,), i),
+                        (b + "ffn_up.weight", (p.n_ff, d), i), (b + "ffn_up.bias", (p.n_ff,), i),
+                        (b + "ffn_down.weight", (d, p.n_ff), i), (b + "ffn_down.bias", (d,), i)]
+            continue
         if p.arch == "phi3":
             out += [(b + "attn_norm.weight", (d,), i), (b + "attn_qkv.weight", (qd + 2 * kvd, d), i),
                     (b + "attn_output.weight", (d, qd), i), (b + "ffn_norm.weight", (d,), i),
@@ -245,6 +268,8 @@ def tensor_list(p: Preset):
     if p.arch == "phi2":
         out.append(("output_norm.bias", (d,), -1))
         out.append(("output.bias", (p.n_vocab,), -1))
+    if p.arch == "starcoder2":
+        out.append(("output_norm.bias", (d,), -1))
     if not p.tied:
         out.append(("output.weight", (p.n_vocab, d), -1))
     return out
@@ -279,7 +304,9 @@ def write_model(path: str, preset: str | Preset, seed: int = 0, exact: bool = Fa
         w.add_float32(f"{a}.final_logit_softcapping", p.final_softcap)
     if p.sliding_window:
         w.add_uint32(f"{a}.attention.sliding_window", p.sliding_window)
-    if a == "phi2":
+    if p.logit_scale:
+        w.add_float32(f"{a}.logit_scale", p.logit_scale)
+    if a in ("phi2", "command-r", "starcoder2"):
         w.add_float32(f"{a}.attention.layer_norm_epsilon", p.eps)
     else:
         w.add_float32(f"{a}.attention.layer_norm_rms_epsilon", p.eps)
@@ -333,6 +360,29 @@ def write_model(path: str, preset: str | Preset, seed: int = 0, exact: bool = Fa
             raise NotImplementedError(t)
 
         w.add_tensor(name, shape, t, payload)
+    w.write()
+    return path
+
+
+def write_lora(path: str, base_path: str, targets: Sequence[str] = ("attn_q", "ffn_down"), rank: int = 4,
+               alpha: float = 8.0, seed: int = 0, std: float = 0.05) -> str:
+    """A LoRA adapter GGUF for the model at base_path in llama.cpp's adapter layout: every weight
+    `blk.N.<target>.weight` gets `.lora_a` [rank, K] and `.lora_b` [N, rank] (F32)."""
+    from ..gguf import GGUFReader
+    base = GGUFReader(base_path, load_tensors=False)
+    w = GGUFWriter(path, base.architecture)
+    w.add_string("general.type", "adapter")
+    w.add_string("adapter.type", "lora")
+    w.add_float32("adapter.lora.alpha", alpha)
+    rng = np.random.default_rng(seed)
+    for name, t in base.tensors.items():
+        if not any(name.endswith(f".{tg}.weight") for tg in targets):
+            continue
+        N, K = t.shape[-2], t.shape[-1]
+        a = (std * rng.standard_normal((rank, K))).astype(np.float32)
+        b = (std * rng.standard_normal((N, rank))).astype(np.float32)
+        w.add_tensor(name + ".lora_a", (rank, K), GGMLType.F32, a.reshape(-1))
+        w.add_tensor(name + ".lora_b", (N, rank), GGMLType.F32, b.reshape(-1))
     w.write()
     return path
 

@@ -72,7 +72,8 @@ def test_mixtral_moe_graph_decode(tmp_path):
     assert first == int(top.indices[0]) or float(top.values[0] - ref[first]) < 0.05
 
 
-@pytest.mark.parametrize("preset", ["tiny-qwen2", "tiny-phi3", "tiny-gemma", "tiny-gemma2"])
+@pytest.mark.parametrize("preset", ["tiny-qwen2", "tiny-phi3", "tiny-gemma", "tiny-gemma2", "tiny-command-r",
+                                    "tiny-starcoder2"])
 def test_model_families_graph_decode(preset, tmp_path):
     """Qwen2 (q/k/v biases), Phi-3 (fused qkv + gate|up, head dim 96), Gemma (head dim 256, GeGLU,
     scaled embeddings): multi-step graph decode == single-step, first token == the fp32 oracle."""
@@ -87,6 +88,29 @@ def test_model_families_graph_decode(preset, tmp_path):
     ref = eng.model.reference_logits(ids)[-1]
     res = eng.generate("family check", SamplingParams(max_tokens=2, temperature=0.0, ignore_eos=True))
     first = eng.tokenize("family check" + res["text"])[len(ids)]
+    top = torch.topk(ref, 2)
+    assert first == int(top.indices[0]) or float(top.values[0] - ref[first]) < 0.05
+
+
+def test_lora_adapter_on_gpu(tmp_path):
+    """A LoRA-merged model (BF16 adapted weights next to Q4_K ones) through the GPU kernels and
+    graph decode: multi-step == single-step, first token == the merged model's fp32 oracle."""
+    from localai_amd.models import synth
+    base = synth.write_model(str(tmp_path / "base.gguf"), "tiny-llama", exact=True)
+    ad = synth.write_lora(str(tmp_path / "ad.gguf"), base, targets=("attn_q", "attn_v", "ffn_up", "ffn_down"),
+                          std=0.2)
+
+    def eng(K):
+        return LLMEngine(EngineConfig(model_path=base, device="cuda:0", context_size=256, max_num_seqs=8,
+                                      max_batched_tokens=512, decode_steps=K, lora_adapters=((ad, 1.0),)))
+    a = _run(eng(1), ["lora one", "two"], max_tokens=8, temperature=0.0, ignore_eos=True)
+    b = _run(eng(8), ["lora one", "two"], max_tokens=8, temperature=0.0, ignore_eos=True)
+    assert [x[1] for x in a] == [8, 8] and a == b
+    e = eng(8)
+    ids = e.tokenize("lora one")
+    ref = e.model.reference_logits(ids)[-1]
+    res = e.generate("lora one", SamplingParams(max_tokens=2, temperature=0.0, ignore_eos=True))
+    first = e.tokenize("lora one" + res["text"])[len(ids)]
     top = torch.topk(ref, 2)
     assert first == int(top.indices[0]) or float(top.values[0] - ref[first]) < 0.05
 
