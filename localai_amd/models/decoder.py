@@ -119,6 +119,9 @@ class Layer:
     post_attn_norm: Optional[torch.Tensor] = None    # Gemma-2: RMSNorm of the attention output
     post_ffw_norm: Optional[torch.Tensor] = None     # Gemma-2: RMSNorm of the MLP output
     window: int = 0                                  # sliding-window attention span (0: full)
+    shexp_gate_up: Optional[List[ops.QWeight]] = None  # Qwen2-MoE shared expert (TP-sliced like a dense MLP)
+    shexp_down: Optional[ops.QWeight] = None
+    shexp_gate: Optional[torch.Tensor] = None        # [D] f32: sigmoid(x . g) scales the shared expert
 
 
 def _raw2d(t, rows: Optional[slice] = None, cols: Optional[slice] = None):
@@ -255,6 +258,14 @@ class DecoderModel:
                 gu = ops.concat_rows([g, u])
                 gate_up = [gu] if gu is not None else [g, u]
                 down = qw(b + "ffn_down.weight", cols=fs)
+            shexp_gu = shexp_down = shexp_gate = None
+            if b + "ffn_up_shexp.weight" in T:
+                fsh = sl(hp.n_ff_shexp)  # sliced by rank even under EP: the all-reduce sums it once
+                g, u = qw(b + "ffn_gate_shexp.weight", rows=fsh), qw(b + "ffn_up_shexp.weight", rows=fsh)
+                gu = ops.concat_rows([g, u])
+                shexp_gu = [gu] if gu is not None else [g, u]
+                shexp_down = qw(b + "ffn_down_shexp.weight", cols=fsh)
+                shexp_gate = f32(b + "ffn_gate_inp_shexp.weight")
             moe_gu = moe_down = None
             if experts and all(len(gu) == 1 for gu, _ in experts):
                 try:
@@ -268,6 +279,7 @@ class DecoderModel:
                 ffn_norm=f32(b + "ffn_norm.weight"), ffn_norm_b=f32(b + "ffn_norm.bias"),
                 gate_up=gate_up, up_bias=up_b, down=down, down_bias=down_b,
                 router=router, experts=experts, moe_gu=moe_gu, moe_down=moe_down,
+                shexp_gate_up=shexp_gu, shexp_down=shexp_down, shexp_gate=shexp_gate,
                 post_attn_norm=f32(b + "post_attention_norm.weight"), post_ffw_norm=f32(b + "post_ffw_norm.weight"),
                 # Gemma-2 alternates sliding-window (even) and global (odd) layers
                 window=hp.sliding_window if hp.sliding_window and i % 2 == 0 else 0))
@@ -327,7 +339,8 @@ class DecoderModel:
         T = xn.shape[0]
         logits = xn.float() @ L.router.t()                       # [T, E]
         w, idx = torch.topk(torch.softmax(logits, -1), hp.n_expert_used, -1)
-        w = w / w.sum(-1, keepdim=True)
+        if hp.moe_renorm:
+            w = w / w.sum(-1, keepdim=True)
         El, base = self.E_local, self.ep_base
         if self.ep:
             # expert ids of this rank -> 0..El-1; tokens' other picks -> El (a group nobody runs)
@@ -344,6 +357,8 @@ class DecoderModel:
             h = ops.act(gu, self.F, ops.ACT_SWIGLU)
             d = ops.moe_linear(h, L.moe_down, order, off, k, T, down=True,
                                wts=w.reshape(-1).float().contiguous(), zero=self.ep)
+            if L.shexp_down is not None:
+                d = ops.Partial((ops.reduce(d) + self._shared_expert(L, xn)).unsqueeze(0))
             return self._row_parallel_out(d, None)
         out = torch.zeros(T, hp.n_embd, dtype=torch.float32, device=xn.device)
         flat_e = idx_l.reshape(-1)
@@ -359,8 +374,16 @@ class DecoderModel:
             h = ops.act(gu, self.F, ops.ACT_SWIGLU)
             d = ops.reduce(ops.linear(h, down))
             out.index_add_(0, rows, d * flat_w[sel].unsqueeze(1))
+        if L.shexp_down is not None:
+            out += self._shared_expert(L, xn)
         self.tp.all_reduce(out)
         return ops.Partial(out.unsqueeze(0))
+
+    def _shared_expert(self, L: Layer, xn: torch.Tensor) -> torch.Tensor:
+        """Qwen2-MoE: sigmoid(x . g_shexp) * down(silu(gate x) * up x), this rank's F slice, fp32 [T, D]."""
+        gu = ops.linear_multi(xn, L.shexp_gate_up)
+        sh = ops.reduce(ops.act_linear(gu, self.hp.n_ff_shexp // self.tp.world, ops.ACT_SWIGLU, L.shexp_down))
+        return sh * torch.sigmoid(xn.float() @ L.shexp_gate).unsqueeze(1)
 
     def _post_attn(self, i: int, L: Layer, xn: torch.Tensor, res: torch.Tensor, o: ops.Partial) -> torch.Tensor:
         """Residual + norm around the MLP of layer i; returns the next layer's normed input."""
@@ -511,7 +534,8 @@ class DecoderModel:
                 if L.experts is not None:
                     lg = hin @ L.router.cpu().t()
                     w, idx = torch.topk(torch.softmax(lg, -1), hp.n_expert_used, -1)
-                    w = w / w.sum(-1, keepdim=True)
+                    if hp.moe_renorm:
+                        w = w / w.sum(-1, keepdim=True)
                     out = torch.zeros_like(hin)
                     for tt in range(Tn):
                         for j in range(hp.n_expert_used):
@@ -520,6 +544,11 @@ class DecoderModel:
                             ff = gu.shape[-1] // 2
                             hh = torch.nn.functional.silu(gu[:, :ff]) * gu[:, ff:]
                             out[tt] += w[tt, j] * (hh @ deq(dw).t())[0]
+                    if L.shexp_down is not None:
+                        gu = torch.cat([hin @ deq(ww).t() for ww in L.shexp_gate_up], -1)
+                        ff = gu.shape[-1] // 2
+                        sh = (torch.nn.functional.silu(gu[:, :ff]) * gu[:, ff:]) @ deq(L.shexp_down).t()
+                        out = out + torch.sigmoid(hin @ L.shexp_gate.cpu()).unsqueeze(1) * sh
                     return out
                 gu = torch.cat([hin @ deq(w).t() for w in L.gate_up], -1)
                 if L.up_bias is not None:

@@ -26,6 +26,8 @@ class HParams:
     norm_type: str = "rms"            # "rms" | "layer"
     n_expert: int = 0
     n_expert_used: int = 0
+    moe_renorm: bool = True           # renormalise the top-k routing weights (Mixtral); Qwen2-MoE does not
+    n_ff_shexp: int = 0               # Qwen2-MoE shared expert width (0: none)
     parallel_residual: bool = False   # phi-2: h = x + attn(ln x) + mlp(ln x)
     act: str = "swiglu"               # "swiglu" | "gelu" | "geglu" (Gemma: gelu(gate) * up)
     embed_scale: float = 1.0          # Gemma scales the token embeddings by sqrt(n_embd)
@@ -68,6 +70,8 @@ class HParams:
         n_ff = g("feed_forward_length")
         if isinstance(n_ff, list):
             n_ff = n_ff[0]
+        if a == "qwen2moe":  # the routed experts' width; no dense FFN
+            n_ff = g("expert_feed_forward_length", n_ff)
         hp = HParams(
             arch=a,
             n_layer=int(g("block_count")),
@@ -88,6 +92,8 @@ class HParams:
             norm_type=norm_type,
             n_expert=int(g("expert_count", 0) or 0),
             n_expert_used=int(g("expert_used_count", 0) or 0),
+            moe_renorm=a != "qwen2moe",
+            n_ff_shexp=int(g("expert_shared_feed_forward_length", 0) or 0) if a == "qwen2moe" else 0,
             # phi-2 / Command-R: h = x + attn(ln x) + mlp(ln x)
             parallel_residual=a in ("phi2", "command-r"),
             act="gelu" if a in ("phi2", "gptneox", "falcon", "starcoder2")

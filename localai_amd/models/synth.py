@@ -56,6 +56,7 @@ class Preset:
     final_softcap: float = 0.0
     sliding_window: int = 0
     logit_scale: float = 0.0         # Command-R
+    n_ff_shexp: int = 0              # Qwen2-MoE shared expert width
     name: str = "synthetic"
 
     @property
@@ -107,6 +108,10 @@ PRESETS: Dict[str, Preset] = {
     "tiny-starcoder2": Preset(arch="starcoder2", n_layer=2, n_embd=256, n_head=4, n_head_kv=2, n_ff=512,
                               n_vocab=32256, ctx=512, rope_theta=1e5, qtype="Q8_0", tokenizer="phi2",
                               name="tiny-starcoder2"),
+    # Qwen2-MoE: routed experts without top-k renormalisation + a sigmoid-gated shared expert
+    "tiny-qwen2moe": Preset(arch="qwen2moe", n_layer=2, n_embd=256, n_head=4, n_head_kv=2, n_ff=256, n_vocab=32256,
+                            ctx=512, rope_theta=1e6, eps=1e-6, n_expert=4, n_expert_used=2, n_ff_shexp=512,
+                            qtype="Q4_K", tokenizer="chatml", name="tiny-qwen2moe"),
     "qwen2-7b": Preset(arch="qwen2", n_layer=28, n_embd=3584, n_head=28, n_head_kv=4, n_ff=18944, n_vocab=152064,
                        ctx=32768, rope_theta=1e6, eps=1e-6, tokenizer="chatml", name="Qwen2-7B-Instruct (random-init)"),
     "phi3-mini": Preset(arch="phi3", n_layer=32, n_embd=3072, n_head=32, n_head_kv=32, n_ff=8192, n_vocab=32064,
@@ -196,7 +201,7 @@ def _more_bits(i: int, n: int) -> bool:
 
 def _tensor_types(p: Preset, name: str, layer: int) -> int:
     if name.endswith("norm.weight") or name.endswith(".bias") or name == "rope_freqs.weight" or \
-            name.endswith("ffn_gate_inp.weight"):
+            name.endswith("ffn_gate_inp.weight") or name.endswith("ffn_gate_inp_shexp.weight"):
         return GGMLType.F32
     q = p.qtype
     if q == "F32":
@@ -253,8 +258,11 @@ def tensor_list(p: Preset):
         out += [(b + "attn_norm.weight", (d,), i), (b + "attn_q.weight", (qd, d), i),
                 (b + "attn_k.weight", (kvd, d), i), (b + "attn_v.weight", (kvd, d), i),
                 (b + "attn_output.weight", (d, qd), i), (b + "ffn_norm.weight", (d,), i)]
-        if p.arch == "qwen2":
+        if p.arch in ("qwen2", "qwen2moe"):
             out += [(b + "attn_q.bias", (qd,), i), (b + "attn_k.bias", (kvd,), i), (b + "attn_v.bias", (kvd,), i)]
+        if p.n_ff_shexp:
+            out += [(b + "ffn_gate_inp_shexp.weight", (d,), i), (b + "ffn_gate_shexp.weight", (p.n_ff_shexp, d), i),
+                    (b + "ffn_up_shexp.weight", (p.n_ff_shexp, d), i), (b + "ffn_down_shexp.weight", (d, p.n_ff_shexp), i)]
         if p.arch == "gemma2":
             out += [(b + "post_attention_norm.weight", (d,), i), (b + "post_ffw_norm.weight", (d,), i)]
         if p.n_expert:
@@ -314,6 +322,9 @@ def write_model(path: str, preset: str | Preset, seed: int = 0, exact: bool = Fa
     if p.n_expert:
         w.add_uint32(f"{a}.expert_count", p.n_expert)
         w.add_uint32(f"{a}.expert_used_count", p.n_expert_used)
+    if p.n_ff_shexp:
+        w.add_uint32(f"{a}.expert_feed_forward_length", p.n_ff)
+        w.add_uint32(f"{a}.expert_shared_feed_forward_length", p.n_ff_shexp)
     w.add_string("tokenizer.ggml.model", model)
     w.add_array("tokenizer.ggml.tokens", toks, GGUFValueType.STRING)
     w.add_array("tokenizer.ggml.token_type", types, GGUFValueType.INT32)
@@ -343,7 +354,7 @@ def write_model(path: str, preset: str | Preset, seed: int = 0, exact: bool = Fa
                 return (1.0 + 0.1 * rng.standard_normal(n)).astype(np.float32)
             if name.endswith(".bias"):
                 return (0.02 * rng.standard_normal(n)).astype(np.float32)
-            if name.endswith("ffn_gate_inp.weight"):
+            if name.endswith("ffn_gate_inp.weight") or name.endswith("ffn_gate_inp_shexp.weight"):
                 return (std * rng.standard_normal(n)).astype(np.float32)
             sd = std
             if name == "token_embd.weight":

@@ -50,10 +50,11 @@ def _worker(rank, world, port, path, q, ep=False):
 import pytest
 
 
-@pytest.fixture(params=["tiny-llama", "tiny-mixtral", "tiny-phi2"])
+@pytest.fixture(params=["tiny-llama", "tiny-mixtral", "tiny-phi2", "tiny-qwen2moe"])
 def tp_model_path(request, tiny_model_path, tmp_path_factory):
-    """Llama (dense GQA), Mixtral (TP-within-expert: every expert's F sharded, router replicated)
-    and Phi-2 (LayerNorm + biases, NEOX partial rotary, biases added once after the all-reduce)."""
+    """Llama (dense GQA), Mixtral (TP-within-expert: every expert's F sharded, router replicated),
+    Phi-2 (LayerNorm + biases, NEOX partial rotary, biases added once after the all-reduce) and
+    Qwen2-MoE (unaligned expert F shards, sigmoid-gated shared expert sliced like a dense MLP)."""
     if request.param == "tiny-llama":
         return tiny_model_path
     from localai_amd.models import synth
