@@ -29,10 +29,18 @@ def build(force: bool = False, verbose: bool = False, sanitize: bool = False) ->
     return LIB
 
 
+# AddressSanitizer + UndefinedBehaviorSanitizer build of the native core (host code only), kept apart
+# from the production module: tests/test_native_sanitizers.py reruns the native test files against it
+# in a child interpreter with the ASan runtime preloaded
+ASAN_DIR = HERE / "_asan"
+
+
 def build_module(name: str, force: bool = False, verbose: bool = False, sanitize: bool = False) -> Path:
     SRCS = [HERE / s for s in MODULES[name]]
-    LIB = HERE / f"{name}{EXT}"
-    stamp = HERE / f"{name}.stamp"
+    out_dir = ASAN_DIR if sanitize else HERE
+    out_dir.mkdir(exist_ok=True)
+    LIB = out_dir / f"{name}{EXT}"
+    stamp = out_dir / f"{name}.stamp"
     dig = _digest(SRCS + [HERE / h for h in HEADERS]) + ("-asan" if sanitize else "")
     if not force and LIB.exists() and stamp.exists() and stamp.read_text().strip() == dig:
         return LIB
@@ -41,7 +49,8 @@ def build_module(name: str, force: bool = False, verbose: bool = False, sanitize
     flags = ["-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Wno-sign-compare",
              f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}"]
     if sanitize:
-        flags += ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-g"]
+        flags = [f for f in flags if f != "-O2"] + ["-O1", "-fsanitize=address,undefined",
+                                                    "-fno-sanitize-recover=undefined", "-fno-omit-frame-pointer", "-g"]
     tmp = str(LIB) + ".tmp"
     cmd = [cxx, *flags, *map(str, SRCS), "-o", tmp, "-lpthread"]
     if verbose:
