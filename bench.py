@@ -39,6 +39,10 @@ def parse():
     ap.add_argument("--preset", default=os.environ.get("BENCH_PRESET", "llama3-8b"))
     ap.add_argument("--mode", default=os.environ.get("BENCH_MODE", "http"), choices=["http", "engine"])
     ap.add_argument("--context", type=int, default=2048)
+    ap.add_argument("--batch-tokens", type=int, default=int(os.environ.get("BENCH_BATCH_TOKENS", 0)),
+                    help="prefill tokens per engine step (0: max(8192, 8 prompts))")
+    ap.add_argument("--decode-steps", type=int, default=int(os.environ.get("BENCH_DECODE_STEPS", 0)),
+                    help="device decode steps per host round trip (0: engine default)")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--server", default=os.environ.get("BENCH_SERVER", "native"), choices=["native", "uvicorn"])
     ap.add_argument("--clients", type=int, default=int(os.environ.get("BENCH_CLIENTS", 4)),
@@ -120,10 +124,12 @@ def main():
     from localai_amd.engine.llm_engine import EngineConfig, LLMEngine
 
     t0 = time.time()
+    extra = {"decode_steps": args.decode_steps} if args.decode_steps else {}
     cfg = EngineConfig(model_path=path, device=dev, context_size=args.context,
-                       max_num_seqs=max(args.concurrency, 1), max_batched_tokens=max(8192, args.prompt_len * 8),
+                       max_num_seqs=max(args.concurrency, 1),
+                       max_batched_tokens=args.batch_tokens or max(8192, args.prompt_len * 8),
                        use_graphs=not args.no_graphs,
-                       max_kv_tokens=args.concurrency * (args.prompt_len + args.max_tokens + 64) + 4096)
+                       max_kv_tokens=args.concurrency * (args.prompt_len + args.max_tokens + 64) + 4096, **extra)
     eng = LLMEngine(cfg)
     t_load = time.time() - t0
     t0 = time.time()
