@@ -155,9 +155,13 @@ class DecoderModel:
         self.device = device
         self.tp = tp = tp or TPInfo()
         W, R = tp.world, tp.rank
-        if hp.n_head % W or hp.n_head_kv % W:
-            raise ValueError(f"TP={W} must divide heads ({hp.n_head}/{hp.n_head_kv})")
-        self.Hq, self.Hkv, self.Dh = hp.n_head // W, hp.n_head_kv // W, hp.head_dim
+        # more ranks than kv heads (Qwen2-7B's 4 kv heads at TP=8, Gemma-2B's 1): each kv head is
+        # replicated on the W / n_head_kv ranks whose query heads read it (their GQA groups line up)
+        self.kv_rep = W // hp.n_head_kv if W > hp.n_head_kv and W % hp.n_head_kv == 0 else 1
+        if hp.n_head % W or (hp.n_head_kv % W and self.kv_rep == 1):
+            raise ValueError(f"TP={W} must divide the query heads ({hp.n_head}) and divide or be a multiple of "
+                             f"the kv heads ({hp.n_head_kv})")
+        self.Hq, self.Hkv, self.Dh = hp.n_head // W, max(1, hp.n_head_kv // W), hp.head_dim
         self.F = hp.n_ff // W
         # expert parallelism: rank R holds experts [R*El, (R+1)*El) whole (no F split).  The MoE input
         # is replicated across the group (it follows the attention all-reduce), so each rank runs its
@@ -209,6 +213,9 @@ class DecoderModel:
         for i in range(hp.n_layer):
             b = f"blk.{i}."
             qs, ks = sl(qd), sl(kvd)
+            if self.kv_rep > 1:  # this rank's (replicated) kv head
+                kvh = R // self.kv_rep
+                ks = slice(kvh * hp.head_dim, (kvh + 1) * hp.head_dim)
             if b + "attn_qkv.weight" in T:  # phi-2 / phi-3: one fused [q; k; v] projection
                 qkv_name = b + "attn_qkv.weight"
                 qkv = [qw(qkv_name, rows=slice(qs.start, qs.stop)),

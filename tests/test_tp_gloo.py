@@ -79,7 +79,7 @@ def test_ep2_mixtral(tiny_model_path, tmp_path_factory):
     assert n_exp == HParams.from_gguf(GGUFReader(str(p))).n_expert // 2
 
 
-def _run_tp2(tp_model_path, ep=False):
+def _run_tp2(tp_model_path, ep=False, world=2):
     tiny_model_path = tp_model_path
     from localai_amd.engine.llm_engine import EngineConfig, LLMEngine
     from localai_amd.engine.sampling_params import SamplingParams
@@ -89,7 +89,7 @@ def _run_tp2(tp_model_path, ep=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, tiny_model_path, q, ep)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, tiny_model_path, q, ep)) for r in range(world)]
     for p in procs:
         p.start()
     out, t0 = {}, time.time()
@@ -104,10 +104,17 @@ def _run_tp2(tp_model_path, ep=False):
         p.join(60)
         assert p.exitcode == 0
     _, outs, emb_len, n_exp = out[0]
-    _, f_requests, f_tokens = out[1]
     assert [n for _, n in outs] == [5, 5]
-    assert f_requests == 2 and f_tokens == 10      # the follower ran the same two requests
+    for r in range(1, world):
+        _, f_requests, f_tokens = out[r]
+        assert f_requests == 2 and f_tokens == 10  # every follower ran the same two requests
     assert emb_len == single.model.hp.n_embd
     # sharded reductions change bf16 summation order; the first token must agree
     assert outs[0][0][:1] == ref["text"][:1]
     return n_exp
+
+
+def test_tp4_replicated_kv_heads(tiny_model_path):
+    """TP=4 over a model with 2 kv heads: each kv head lives on the 2 ranks whose query heads read
+    it (DecoderModel.kv_rep), so TP degrees above the kv-head count (Qwen2-7B at TP=8) work."""
+    _run_tp2(tiny_model_path, world=4)
