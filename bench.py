@@ -124,7 +124,7 @@ def main():
     from localai_amd.engine.llm_engine import EngineConfig, LLMEngine
 
     t0 = time.time()
-    extra = {"decode_steps": args.decode_steps} if args.decode_steps else {}
+    extra = {"decode_steps": args.decode_steps, "decode_steps_wide": args.decode_steps} if args.decode_steps else {}
     cfg = EngineConfig(model_path=path, device=dev, context_size=args.context,
                        max_num_seqs=max(args.concurrency, 1),
                        max_batched_tokens=args.batch_tokens or max(8192, args.prompt_len * 8),

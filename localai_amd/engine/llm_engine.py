@@ -60,6 +60,11 @@ class EngineConfig:
     rope_freq_scale: float = 0.0
     rope_scaling: str = ""
     decode_steps: int = 8             # device-resident decode steps per host round trip (graphs only)
+    # ... and at batch >= wide_batch with nothing waiting: the host round trip (sync, emit, schedule,
+    # upload) is then paid half as often (batch 256: +1.4 % tok/s measured, arrivals still cut a
+    # run short through the num_waiting check)
+    decode_steps_wide: int = 16
+    wide_batch: int = 128
     mmproj: str = ""                  # LLaVA vision tower + projector GGUF (images in prompts)
     bias_capacity: int = 16           # logit-bias / EOS-ban entries per sequence inside the graph
     blas_tune: bool = True            # tune the hipBLASLt/rocBLAS solution per decode GEMM shape at warm-up
@@ -603,6 +608,8 @@ class LLMEngine:
         s = self.sched
         if s.num_waiting > 0 and s.num_running < self.cfg.max_num_seqs:
             return 1  # admit new prompts promptly
+        if len(self.requests) >= self.cfg.wide_batch and s.num_waiting == 0:
+            K = max(K, self.cfg.decode_steps_wide)
         rem_tok, rem_ctx = 1, K
         for r in self.requests.values():
             if r.n_gen == 0 or self._needs_host_sampling(r):
@@ -800,7 +807,7 @@ class LLMEngine:
         dev = self.device
         MB = self.max_blocks
         cap = max(1, Bp * self.cfg.bias_capacity)
-        K = max(1, self.cfg.decode_steps)
+        K = max(1, self.cfg.decode_steps, self.cfg.decode_steps_wide)
         # all per-run inputs live in one int32 block (uploaded with a single copy)
         prm_words = Bp * ops.SAMPLE_ROW_DTYPE.itemsize // 4
         layout = [("tokens", Bp), ("pos", Bp), ("slots", Bp), ("lens", Bp), ("bt", Bp * MB), ("step", 1),

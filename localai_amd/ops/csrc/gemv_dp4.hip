@@ -643,6 +643,109 @@ LA_DEV void gv_q6k(const QW& w, int row0, const bf16* X, int ldx, const GVAct& a
   gv_store<MT, RS>(acc, n, w.N, M, t, o, ldo, col0, rp);
 }
 
+// Q8_0 (ggml block_q8_0: f16 d + 32 int8 per 32 weights; planes p0 = qs [N][K] int8, p1 = d
+// [N][K/32] f16): lane t of a row group takes the 32-weight block t of each 256-weight chunk
+// (two 16-B loads), 8 v_dot4 against the int8 activation block, one scale product per block --
+// symmetric codes, so no 16-run sums.  Reference: ggml_vec_dot_q8_0_q8_0 [external, llama.cpp @
+// d5cb868 ggml/src/ggml-quants.c].
+template <int MT, int NT, int EARLY, int RS, int PD = 0>
+LA_DEV void gv_q8(const QW& w, int row0, const bf16* X, int ldx, const GVAct& act, int M, int kper, float* o,
+                  int ldo, int col0, int8_t* xq, int* bs, float* dx, const GVRope& rp) {
+  const int k0 = blockIdx.y * kper, nsb = kper >> 8, sb0 = k0 >> 8;
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = lane >> 3, t = lane & 7;
+  const size_t qrow = (size_t)w.K, drow = (size_t)(w.K >> 5) * 2;
+  int n[RS];
+  const uint8_t* qp[RS];
+  const uint8_t* dp[RS];
+#pragma unroll
+  for (int s = 0; s < RS; ++s) {
+    n[s] = row0 + wv * (8 * RS) + s * 8 + r;
+    const size_t nc = n[s] < w.N ? n[s] : w.N - 1;  // clamped row for loads
+    qp[s] = w.p0 + nc * qrow + (size_t)sb0 * 256 + 32 * t;
+    dp[s] = w.p1 + nc * drow + ((size_t)sb0 * 8 + t) * 2;
+  }
+  const bool staged = !EARLY && x_staged_ok<MT>(act, kper);
+  u32x2 xr[GV_XI];
+  if (staged) x_issue<MT>(X, ldx, M, k0, kper, xr);
+  if constexpr (!EARLY) {
+    if (!staged) {
+      quantize_x<MT>(X, ldx, act, M, k0, kper, xq, bs, dx);
+      __syncthreads();
+    }
+  }
+  // PD-deep register ring over 256-weight chunks (PD 0: a 2-deep double buffer)
+  constexpr int D = PD > 0 ? PD : 2;
+  u32x4 qa[D][RS][2];
+  uint32_t da[D][RS];
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+#pragma unroll
+    for (int s = 0; s < RS; ++s) {
+      const int sb = min(i, nsb - 1);
+      qa[i][s][0] = ldg16<NT>(qp[s] + sb * 256);
+      qa[i][s][1] = ldg16<NT>(qp[s] + sb * 256 + 16);
+      da[i][s] = *(const uint16_t*)(dp[s] + sb * 16);
+    }
+  if (staged) {
+    x_commit<MT>(M, kper, xr, xq, bs, dx);
+    __syncthreads();
+  }
+  if constexpr (EARLY) {
+    quantize_x<MT>(X, ldx, act, M, k0, kper, xq, bs, dx);
+    __syncthreads();
+  }
+  float acc[MT][RS];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int s = 0; s < RS; ++s) acc[m][s] = 0.f;
+  for (int sb0i = 0; sb0i < nsb; sb0i += D) {
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      const int sb = sb0i + i;
+      if (sb >= nsb) break;
+      u32x4 q0[RS], q1[RS];
+      uint32_t dd[RS];
+#pragma unroll
+      for (int s = 0; s < RS; ++s) {
+        q0[s] = qa[i][s][0];
+        q1[s] = qa[i][s][1];
+        dd[s] = da[i][s];
+      }
+      const int nx = min(sb + D, nsb - 1);  // clamped tail reload: harmless, keeps the ring uniform
+#pragma unroll
+      for (int s = 0; s < RS; ++s) {
+        qa[i][s][0] = ldg16<NT>(qp[s] + nx * 256);
+        qa[i][s][1] = ldg16<NT>(qp[s] + nx * 256 + 16);
+        da[i][s] = *(const uint16_t*)(dp[s] + nx * 16);
+      }
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        if (m < M) {
+          const int8_t* xm = xq + m * kper + sb * 256 + 32 * t;
+          const u32x4 x0 = *(const u32x4*)xm;
+          const u32x4 x1 = *(const u32x4*)(xm + 16);
+          const float dxm = dx[m * (kper >> 5) + sb * 8 + t];
+#pragma unroll
+          for (int s = 0; s < RS; ++s) {
+            int di = dot4(q0[s][0], x0[0], 0);
+            di = dot4(q0[s][1], x0[1], di);
+            di = dot4(q0[s][2], x0[2], di);
+            di = dot4(q0[s][3], x0[3], di);
+            di = dot4(q1[s][0], x1[0], di);
+            di = dot4(q1[s][1], x1[1], di);
+            di = dot4(q1[s][2], x1[2], di);
+            di = dot4(q1[s][3], x1[3], di);
+            acc[m][s] = fmaf(h2f((uint16_t)dd[s]) * dxm, (float)di, acc[m][s]);
+          }
+        }
+      }
+    }
+  }
+  gv_store<MT, RS>(acc, n, w.N, M, t, o, ldo, col0, rp);
+}
+
 // Segments [0, nA) are format FA, [nA, nseg) format FB (a q|k + v fusion is (Q4_K, Q6_K)).
 // VAR bit 0: non-temporal weight loads; bit 1: weights requested before the x prologue.
 template <int MT, int FA, int FB, int VAR>
@@ -662,7 +765,9 @@ __global__ __launch_bounds__(GV_THREADS) void qgemv_dp4_kernel(GVArgs a, const b
   float* o = out + (size_t)blockIdx.y * slab;
   constexpr int NT = VAR & 1, EARLY = (VAR >> 1) & 1, PD = (VAR & 16) ? 4 : 0;
   const bool fa = FA == FB || a.fmt[seg] == FA;
-  if (fa) {
+  if constexpr (FA == FMT_Q8_0) {  // Q8_0 launches are homogeneous (host-checked)
+    gv_q8<MT, NT, EARLY, RS, PD>(a.w[seg], row0, X, ldx, act, M, kper, o, ldo, a.col0[seg], xq, bs, dx, rp);
+  } else if (fa) {
     if constexpr (FA == FMT_Q4_K) gv_q4k<MT, NT, EARLY, RS, PD>(a.w[seg], row0, X, ldx, act, M, kper, o, ldo, a.col0[seg], xq, bs, dx, rp);
     else gv_q6k<MT, NT, EARLY, RS, PD>(a.w[seg], row0, X, ldx, act, M, kper, o, ldo, a.col0[seg], xq, bs, dx, rp);
   } else if constexpr (FA != FB) {
@@ -736,7 +841,11 @@ static int qgemv_dp4_impl(int nseg, const int* fmts, const void* const* planes, 
   for (int i = 0; i < nseg; ++i) {
     const int f = fmts[i], N = Ns[i];
     const void* const* p = planes + 4 * i;
-    if (N < 1 || !p[0] || !p[2] || !p[3] || (f != FMT_Q4_K && f != FMT_Q6_K) || (f == FMT_Q6_K && !p[1])) return -2;
+    if (f == FMT_Q8_0) {
+      if (N < 1 || !p[0] || !p[1]) return -2;
+    } else if (N < 1 || !p[0] || !p[2] || !p[3] || (f != FMT_Q4_K && f != FMT_Q6_K) || (f == FMT_Q6_K && !p[1])) {
+      return -2;
+    }
     a.w[i] = QW{(const uint8_t*)p[0], (const uint8_t*)p[1], (const uint8_t*)p[2], (const uint8_t*)p[3], N, K};
     a.fmt[i] = f;
     a.col0[i] = col;
@@ -756,7 +865,9 @@ static int qgemv_dp4_impl(int nseg, const int* fmts, const void* const* planes, 
   const bf16* x = (const bf16*)X;
   float* o = (float*)out;
   int rc;
-  if (fa == FMT_Q4_K && fb == FMT_Q4_K) rc = launch_gv_m<FMT_Q4_K, FMT_Q4_K>(a, nblk, K, x, ldx, act, M, splits, o, ldo, slab, st, rp);
+  if ((fa == FMT_Q8_0) != (fb == FMT_Q8_0)) return -2;  // Q8_0 weights launch on their own
+  if (fa == FMT_Q8_0) rc = launch_gv_m<FMT_Q8_0, FMT_Q8_0>(a, nblk, K, x, ldx, act, M, splits, o, ldo, slab, st, rp);
+  else if (fa == FMT_Q4_K && fb == FMT_Q4_K) rc = launch_gv_m<FMT_Q4_K, FMT_Q4_K>(a, nblk, K, x, ldx, act, M, splits, o, ldo, slab, st, rp);
   else if (fa == FMT_Q6_K && fb == FMT_Q6_K) rc = launch_gv_m<FMT_Q6_K, FMT_Q6_K>(a, nblk, K, x, ldx, act, M, splits, o, ldo, slab, st, rp);
   else if (fa == FMT_Q4_K) rc = launch_gv_m<FMT_Q4_K, FMT_Q6_K>(a, nblk, K, x, ldx, act, M, splits, o, ldo, slab, st, rp);
   else rc = launch_gv_m<FMT_Q6_K, FMT_Q4_K>(a, nblk, K, x, ldx, act, M, splits, o, ldo, slab, st, rp);

@@ -11,7 +11,7 @@ import numpy as np
 import torch
 
 from localai_amd import ops
-from localai_amd.gguf import GGMLType, random_q4_k_blocks, random_q6_k_blocks
+from localai_amd.gguf import GGMLType, random_q4_k_blocks, random_q6_k_blocks, random_q8_0_blocks
 
 dev = torch.device("cuda:0")
 rng = np.random.default_rng(0)
@@ -35,7 +35,12 @@ def timeit(fn, iters):
     return best
 
 
+BYTES_256 = {"q4k": 144, "q6k": 210, "q8": 272}
+
+
 def mk(fmt, N, K):
+    if fmt == "q8":
+        return ops.QWeight.from_raw(random_q8_0_blocks(rng, N * K // 32, 0.02), GGMLType.Q8_0, (N, K), dev)
     if fmt == "q4k":
         return ops.QWeight.from_raw(random_q4_k_blocks(rng, N * K // 256, 0.02), GGMLType.Q4_K, (N, K), dev)
     return ops.QWeight.from_raw(random_q6_k_blocks(rng, N * K // 256, 0.02), GGMLType.Q6_K, (N, K), dev)
@@ -43,7 +48,7 @@ def mk(fmt, N, K):
 
 def copies(specs):
     """enough copies of the weight group that one rotation overflows L2 + the 256 MiB MALL"""
-    one = sum(N * K // 256 * (144 if f == "q4k" else 210) for f, N, K in specs)
+    one = sum(N * K // 256 * BYTES_256[f] for f, N, K in specs)
     n = max(2, min(48, -(-640 * 2**20 // one)))
     return [[mk(f, N, K) for f, N, K in specs] for _ in range(n)], one
 
@@ -51,6 +56,9 @@ def copies(specs):
 SHAPES = [("qk", [("q4k", 5120, 4096)]), ("v", [("q6k", 1024, 4096)]), ("qkv", [("q4k", 5120, 4096), ("q6k", 1024, 4096)]),
           ("o", [("q4k", 4096, 4096)]), ("gate_up", [("q4k", 28672, 4096)]), ("down", [("q4k", 4096, 14336)]),
           ("down6", [("q6k", 4096, 14336)]), ("lm_head", [("q6k", 128256, 4096)])]
+if os.environ.get("GEMV_SHAPES") == "q8":  # Llama-3-8B Q8_0
+    SHAPES = [("qkv8", [("q8", 6144, 4096)]), ("o8", [("q8", 4096, 4096)]), ("gate_up8", [("q8", 28672, 4096)]),
+              ("down8", [("q8", 4096, 14336)])]
 variants = [int(v) for v in os.environ.get("GEMV_VARIANTS", "0,1,2,3").split(",")]
 sweep_s = os.environ.get("GEMV_SWEEP_S") == "1"   # time every split-K factor (variant 1) instead
 M = int(os.environ.get("GEMV_M", "1"))

@@ -45,6 +45,18 @@ def test_multistep_decode_matches_single_step(tiny_model_path, sp):
         assert x[0] == y[0]
 
 
+def test_wide_batch_decode_steps_match_single_step(tiny_model_path):
+    """The longer device-resident run used at wide batches (decode_steps_wide) produces the
+    single-step token stream, including runs cut short by max_tokens."""
+    prompts = ["one", "two three", "four five six", "seven", "eight nine"]
+    sp = dict(max_tokens=21, temperature=0.0, ignore_eos=True)
+    a = _run(_eng(tiny_model_path, 1), prompts, **sp)
+    wide = LLMEngine(EngineConfig(model_path=tiny_model_path, device="cuda:0", context_size=256, max_num_seqs=8,
+                                  max_batched_tokens=512, decode_steps=4, decode_steps_wide=16, wide_batch=2))
+    b = _run(wide, prompts, **sp)
+    assert a == b and all(x[1] == 21 for x in b)
+
+
 def test_engine_greedy_matches_reference_first_token(tiny_model_path):
     eng = _eng(tiny_model_path, 8)
     prompt = "reference check"

@@ -50,7 +50,7 @@ def test_skinny_gemm_splits_and_tail():
         assert (out.sum(0).cpu() - ref).abs().max().item() < 2e-2
 
 
-@pytest.mark.parametrize("t", [GGMLType.Q4_K, GGMLType.Q6_K])
+@pytest.mark.parametrize("t", [GGMLType.Q4_K, GGMLType.Q6_K, GGMLType.Q8_0])
 @pytest.mark.parametrize("M", [1, 2, 3, 4])
 def test_gemv_dp4(t, M):
     """int8-dot decode GEMV (activations quantised per 256-block, ggml q8_K style) vs fp32:
@@ -668,3 +668,30 @@ def test_attn_softcap_window(Dh):
     out = ops.attn_prefill(qp.to(DEV), kc.to(DEV), vc.to(DEV), cu.to(DEV), cl.to(DEV), bt.to(DEV), 0.088,
                            softcap=cap, window=win)
     assert (out.float().cpu() - ref.float()).abs().max().item() < 3e-2
+
+
+
+@pytest.mark.parametrize("M", [1, 2])
+def test_gemv_dp4_q8_0_mixed_groups_and_rope(M):
+    """Q8_0 weights never share a launch with K-quants (a Q8_0 q|k|v next to a Q6_K weight splits
+    into homogeneous launches), and the q|k|v + RoPE + KV-append launch runs on Q8_0."""
+    K = 1024
+    ws = [_qw(96, K, GGMLType.Q8_0, seed=21), _qw(64, K, GGMLType.Q6_K, seed=22), _qw(40, K, GGMLType.Q8_0, seed=23)]
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    y = ops.linear_multi(x, ws, force="dp4").dense().cpu()
+    ref = torch.cat([x.float().cpu() @ w.ref.t() for w in ws], -1)
+    assert (y - ref).abs().max().item() < 2e-2 * max(1.0, ref.abs().max().item())
+    Hq, Hkv, Dh, BS, K2, nblk = 8, 2, 128, 32, 2048, 4
+    qkv = _qw((Hq + 2 * Hkv) * Dh, K2, GGMLType.Q8_0, seed=24)
+    x2 = torch.randn(M, K2, device=DEV).to(torch.bfloat16)
+    cs = ops.rope_cos_sin(512, Dh, 500000.0, DEV)
+    pos = torch.tensor([37, 200][:M], dtype=torch.int32, device=DEV)
+    slots = torch.tensor([45, 3][:M], dtype=torch.int32, device=DEV)
+    kc, vc = torch.zeros(nblk, Hkv, BS, Dh, dtype=torch.bfloat16, device=DEV), ops.v_pages(nblk, Hkv, BS, Dh, device=DEV)
+    assert ops.qkv_rope_ok(x2, [qkv], None, 0, Dh, Dh, BS)
+    q = ops.qkv_rope_dp4(x2, [qkv], pos, slots, cs, Hq, Hkv, Dh, kc, vc, BS)
+    kr, vr = torch.zeros_like(kc), torch.zeros_like(vc)
+    qr = ops.rope_kv(ops.linear(x2, qkv, force="skinny"), pos, slots, cs, Hq, Hkv, Dh, Dh, 0, kr, vr, BS)
+    tol = 3e-2 * max(1.0, qr.float().abs().max().item())
+    assert (q.float() - qr.float()).abs().max().item() < tol
+    assert (kc.float() - kr.float()).abs().max().item() < tol and (vc.float() - vr.float()).abs().max().item() < tol
