@@ -122,6 +122,8 @@ class Layer:
     shexp_gate_up: Optional[List[ops.QWeight]] = None  # Qwen2-MoE shared expert (TP-sliced like a dense MLP)
     shexp_down: Optional[ops.QWeight] = None
     shexp_gate: Optional[torch.Tensor] = None        # [D] f32: sigmoid(x . g) scales the shared expert
+    mla: Optional[dict] = None                       # DeepSeek-V2 latent attention weights (see _mla_qkv)
+    F: int = 0                                       # this layer's FFN width when it differs from self.F
 
 
 def _raw2d(t, rows: Optional[slice] = None, cols: Optional[slice] = None):
@@ -162,6 +164,12 @@ class DecoderModel:
             raise ValueError(f"TP={W} must divide the query heads ({hp.n_head}) and divide or be a multiple of "
                              f"the kv heads ({hp.n_head_kv})")
         self.Hq, self.Hkv, self.Dh = hp.n_head // W, max(1, hp.n_head_kv // W), hp.head_dim
+        if hp.kv_lora_rank:
+            if W > 1:
+                raise ValueError("DeepSeek-V2 latent attention runs on a single GPU (no tensor parallelism)")
+            # MLA decompresses K and V per query head: the cache holds n_head heads of the key
+            # width (V padded to it, see _mla_qkv)
+            self.Hkv = hp.n_head
         self.F = hp.n_ff // W
         # expert parallelism: rank R holds experts [R*El, (R+1)*El) whole (no F split).  The MoE input
         # is replicated across the group (it follows the attention all-reduce), so each rank runs its
@@ -213,10 +221,15 @@ class DecoderModel:
         for i in range(hp.n_layer):
             b = f"blk.{i}."
             qs, ks = sl(qd), sl(kvd)
+            mla = None
+            if hp.kv_lora_rank:
+                mla = self._load_mla(b, T, qw, f32)
             if self.kv_rep > 1:  # this rank's (replicated) kv head
                 kvh = R // self.kv_rep
                 ks = slice(kvh * hp.head_dim, (kvh + 1) * hp.head_dim)
-            if b + "attn_qkv.weight" in T:  # phi-2 / phi-3: one fused [q; k; v] projection
+            if mla is not None:
+                qkv, qkv_bias = [], None
+            elif b + "attn_qkv.weight" in T:  # phi-2 / phi-3: one fused [q; k; v] projection
                 qkv_name = b + "attn_qkv.weight"
                 qkv = [qw(qkv_name, rows=slice(qs.start, qs.stop)),
                        qw(qkv_name, rows=slice(qd + ks.start, qd + ks.stop)),
@@ -231,22 +244,24 @@ class DecoderModel:
                 if b + "attn_q.bias" in T:
                     qkv_bias = torch.cat([f32(b + "attn_q.bias")[qs], f32(b + "attn_k.bias")[ks],
                                           f32(b + "attn_v.bias")[ks]])
-            qkv = ops.fuse_runs(qkv)  # q|k|v, or q|k + v when v has its own format (Q4_K_M)
-            wo = qw(b + "attn_output.weight", cols=sl(qd))
+            qkv = ops.fuse_runs(qkv) if qkv else qkv  # q|k|v, or q|k + v when v has its own format (Q4_K_M)
+            wo = qw(b + "attn_output.weight", cols=sl(hp.n_head * hp.head_dim_v if mla is not None else qd))
             wo_b = f32(b + "attn_output.bias")
             if wo_b is not None and R != 0:
                 wo_b = torch.zeros_like(wo_b)  # bias added once across TP ranks
             fs = sl(hp.n_ff)
+            ff_exp = hp.n_ff_exp or hp.n_ff  # expert width (DeepSeek-V2: != the dense layers' n_ff)
             router = experts = None
             gate_up, down, up_b, down_b = [], None, None, None
-            if hp.n_expert:
+            moe_layer = hp.n_expert and i >= hp.n_layer_dense_lead and b + "ffn_gate_inp.weight" in T
+            if moe_layer:
                 router = f32(b + "ffn_gate_inp.weight").view(hp.n_expert, hp.n_embd)
                 experts = []
                 for e in range(self.ep_base, self.ep_base + self.E_local):
-                    efs = None if self.ep else fs  # EP: whole experts, TP-within-expert: F slices
+                    efs = None if self.ep else sl(ff_exp)  # EP: whole experts, TP-within-expert: F slices
                     ge = self._expert_slice(T[b + "ffn_gate_exps.weight"], e, rows=efs)
                     ue = self._expert_slice(T[b + "ffn_up_exps.weight"], e, rows=efs)
-                    de = self._expert_slice(T[b + "ffn_down_exps.weight"], e, cols=None if self.ep else sl(hp.n_ff))
+                    de = self._expert_slice(T[b + "ffn_down_exps.weight"], e, cols=None if self.ep else sl(ff_exp))
                     gu = ops.concat_rows([ge, ue])
                     experts.append(([gu] if gu is not None else [ge, ue], de))
             elif b + "ffn_gate.weight" not in T and hp.act == "gelu":  # phi-2 / starcoder2: up -> gelu -> down
@@ -286,7 +301,8 @@ class DecoderModel:
                 ffn_norm=f32(b + "ffn_norm.weight"), ffn_norm_b=f32(b + "ffn_norm.bias"),
                 gate_up=gate_up, up_bias=up_b, down=down, down_bias=down_b,
                 router=router, experts=experts, moe_gu=moe_gu, moe_down=moe_down,
-                shexp_gate_up=shexp_gu, shexp_down=shexp_down, shexp_gate=shexp_gate,
+                shexp_gate_up=shexp_gu, shexp_down=shexp_down, shexp_gate=shexp_gate, mla=mla,
+                F=(ff_exp if moe_layer else hp.n_ff) // W if hp.n_ff_exp else 0,
                 post_attn_norm=f32(b + "post_attention_norm.weight"), post_ffw_norm=f32(b + "post_ffw_norm.weight"),
                 # Gemma-2 alternates sliding-window (even) and global (odd) layers
                 window=hp.sliding_window if hp.sliding_window and i % 2 == 0 else 0))
@@ -305,9 +321,70 @@ class DecoderModel:
         ro = rope_overrides or {}
         theta = ro.get("freq_base") or hp.rope_theta
         fscale = ro.get("freq_scale") or hp.rope_freq_scale
+        yarn = ro.get("yarn")
+        if yarn is None and ro.get("type", hp.rope_scaling) == "yarn":
+            # YaRN declared in the GGUF (rope.scaling.*): DeepSeek-V2 passes the rotation an
+            # attn_factor of 1 / (1 + 0.1 ln(1 / freq_scale)) so cos/sin stay unscaled and the
+            # magnitude correction lives in the query scale (HParams.attn_scale)
+            yarn = {"orig_ctx": hp.rope_orig_ctx or hp.n_ctx_train,
+                    "attn_factor": 1.0 / (1.0 + 0.1 * math.log(1.0 / fscale))
+                    if hp.kv_lora_rank and fscale < 1.0 else 1.0}
         self.cos_sin = ops.rope_cos_sin(self.max_pos, self.rot, theta, dev, freq_scale=fscale,
                                         freq_factors=rope_freqs, rope_type=ro.get("type", hp.rope_scaling),
-                                        yarn=ro.get("yarn"))
+                                        yarn=yarn)
+
+    def _load_mla(self, b: str, T, qw, f32) -> dict:
+        """DeepSeek-V2 latent-attention weights (llama.cpp build_deepseek2 [external]).  The q
+        projection's rows are reordered per head from [nope | rope] to [rope | nope] so the rotary
+        part is the head's FIRST n_rot dims (the layout rope_kv rotates); K is assembled the same
+        way, and q.k over the head is unchanged by the common permutation."""
+        hp = self.hp
+        H, dk, rot = hp.n_head, hp.head_dim, self.rot
+        perm = np.concatenate([np.r_[h * dk + dk - rot:(h + 1) * dk, h * dk:h * dk + dk - rot] for h in range(H)])
+
+        def qw_rows(name):
+            t = T[name]
+            raw, (N, K), gt = _raw2d(t)
+            rows = raw.reshape(N, -1)[perm].reshape(-1)
+            return ops.QWeight.from_raw(np.ascontiguousarray(rows), gt, (N, K), self.device)
+
+        m = {"kv_a": qw(b + "attn_kv_a_mqa.weight"), "kv_a_norm": f32(b + "attn_kv_a_norm.weight"),
+             "kv_b": qw(b + "attn_kv_b.weight")}
+        if hp.q_lora_rank:
+            m["q_a"] = qw(b + "attn_q_a.weight")
+            m["q_a_norm"] = f32(b + "attn_q_a_norm.weight")
+            m["q_b"] = qw_rows(b + "attn_q_b.weight")
+        else:
+            m["q"] = qw_rows(b + "attn_q.weight")
+        return m
+
+    def _mla_qkv(self, L: Layer, xn: torch.Tensor) -> ops.Partial:
+        """q | k | v rows for rope_kv / attention from the latent projections: q per head
+        [rope | nope]; c = RMSNorm(x Wkv_a[:rank]), k_pe = x Wkv_a[rank:] (one head, shared);
+        [k_nope | v] = c Wkv_b per head; K = [k_pe | k_nope], V = [v | 0] (padded to the key width)."""
+        hp = self.hp
+        m = L.mla
+        T = xn.shape[0]
+        H, dk, dv, rot, r = hp.n_head, hp.head_dim, hp.head_dim_v, self.rot, hp.kv_lora_rank
+        eps = hp.norm_eps
+        if "q" in m:
+            q = ops.reduce(ops.linear(xn, m["q"]))
+        else:
+            qa = ops.reduce(ops.linear(xn, m["q_a"]))
+            q = ops.reduce(ops.linear(ops.add_norm(qa, None, m["q_a_norm"], None, eps), m["q_b"]))
+        kva = ops.reduce(ops.linear(xn, m["kv_a"]))                       # [T, rank + rot]
+        c = ops.add_norm(kva[:, :r].contiguous(), None, m["kv_a_norm"], None, eps)
+        kv = ops.reduce(ops.linear(c, m["kv_b"])).view(T, H, (dk - rot) + dv)
+        k = torch.cat([kva[:, r:].unsqueeze(1).expand(T, H, rot), kv[:, :, :dk - rot]], -1)
+        v = torch.cat([kv[:, :, dk - rot:], kv.new_zeros(T, H, dk - dv)], -1)
+        return ops.Partial(torch.cat([q, k.reshape(T, H * dk), v.reshape(T, H * dk)], -1).unsqueeze(0))
+
+    def _attn_out(self, L: Layer, a: torch.Tensor, T: int) -> ops.Partial:
+        if L.mla is not None:  # drop the value padding: [T, H, dk] -> [T, H * dv]
+            a = a.view(T, self.Hq, self.Dh)[:, :, :self.hp.head_dim_v].reshape(T, -1).contiguous()
+        else:
+            a = a.view(T, self.Hq * self.Dh)
+        return self._row_parallel_out(ops.linear(a, L.wo), L.wo_bias)
 
     def _expert_slice(self, t, e, rows=None, cols=None):
         E = t.shape[0]
@@ -336,7 +413,7 @@ class DecoderModel:
         if L.experts is not None:
             return self._moe(L, xn)
         gu = ops.linear_multi(xn, L.gate_up, bias=L.up_bias)
-        d = ops.act_linear(gu, self.F, _ACT[hp.act], L.down)
+        d = ops.act_linear(gu, L.F or self.F, _ACT[hp.act], L.down)
         return self._row_parallel_out(d, L.down_bias)
 
     def _moe(self, L: Layer, xn: torch.Tensor) -> ops.Partial:
@@ -348,6 +425,8 @@ class DecoderModel:
         w, idx = torch.topk(torch.softmax(logits, -1), hp.n_expert_used, -1)
         if hp.moe_renorm:
             w = w / w.sum(-1, keepdim=True)
+        if hp.expert_weights_scale != 1.0:
+            w = w * hp.expert_weights_scale
         El, base = self.E_local, self.ep_base
         if self.ep:
             # expert ids of this rank -> 0..El-1; tokens' other picks -> El (a group nobody runs)
@@ -361,7 +440,7 @@ class DecoderModel:
             k = hp.n_expert_used
             order, off = ops.moe_route(idx_l.to(torch.int32), El + 1 if self.ep else El)
             gu = ops.moe_linear(xn, L.moe_gu, order, off, k, T)
-            h = ops.act(gu, self.F, ops.ACT_SWIGLU)
+            h = ops.act(gu, L.F or self.F, ops.ACT_SWIGLU)
             d = ops.moe_linear(h, L.moe_down, order, off, k, T, down=True,
                                wts=w.reshape(-1).float().contiguous(), zero=self.ep)
             if L.shexp_down is not None:
@@ -378,7 +457,7 @@ class DecoderModel:
             rows = flat_t[sel]
             xe = xn.index_select(0, rows).contiguous()
             gu = ops.linear_multi(xe, gate_up)
-            h = ops.act(gu, self.F, ops.ACT_SWIGLU)
+            h = ops.act(gu, L.F or self.F, ops.ACT_SWIGLU)
             d = ops.reduce(ops.linear(h, down))
             out.index_add_(0, rows, d * flat_w[sel].unsqueeze(1))
         if L.shexp_down is not None:
@@ -387,9 +466,12 @@ class DecoderModel:
         return ops.Partial(out.unsqueeze(0))
 
     def _shared_expert(self, L: Layer, xn: torch.Tensor) -> torch.Tensor:
-        """Qwen2-MoE: sigmoid(x . g_shexp) * down(silu(gate x) * up x), this rank's F slice, fp32 [T, D]."""
+        """Shared expert(s): down(silu(gate x) * up x) on this rank's F slice, fp32 [T, D]; scaled by
+        sigmoid(x . g_shexp) for Qwen2-MoE, unscaled for DeepSeek-V2."""
         gu = ops.linear_multi(xn, L.shexp_gate_up)
         sh = ops.reduce(ops.act_linear(gu, self.hp.n_ff_shexp // self.tp.world, ops.ACT_SWIGLU, L.shexp_down))
+        if L.shexp_gate is None:
+            return sh
         return sh * torch.sigmoid(xn.float() @ L.shexp_gate).unsqueeze(1)
 
     def _post_attn(self, i: int, L: Layer, xn: torch.Tensor, res: torch.Tensor, o: ops.Partial) -> torch.Tensor:
@@ -442,7 +524,7 @@ class DecoderModel:
                 o = self._row_parallel_out(ops.linear(a.view(T, self.Hq * self.Dh), L.wo), L.wo_bias)
                 xn = self._post_attn(i, L, xn, res, o)
                 continue
-            qkv = ops.linear_multi(xn, L.qkv, bias=L.qkv_bias)
+            qkv = self._mla_qkv(L, xn) if L.mla is not None else ops.linear_multi(xn, L.qkv, bias=L.qkv_bias)
             if fb.decode:
                 # RoPE + KV append fused into the decode attention launch (rope_kv when not fusable)
                 a = ops.attn_decode_rope(qkv, fb.pos, fb.slots, self.cos_sin, self.Hq, self.Hkv, self.Dh, self.rot,
@@ -454,7 +536,7 @@ class DecoderModel:
                                 hp.rope_mode, kv.k[i], kv.v[i], kv.block_size)
                 a = ops.attn_prefill(q, kv.k[i], kv.v[i], fb.cu_q, fb.ctx_lens, fb.block_tables, self.scale,
                                      tiles=fb.tiles, softcap=hp.attn_softcap, window=L.window)
-            o = self._row_parallel_out(ops.linear(a.view(T, self.Hq * self.Dh), L.wo), L.wo_bias)
+            o = self._attn_out(L, a, T)
             xn = self._post_attn(i, L, xn, res, o)
         if return_hidden:
             return xn
@@ -512,9 +594,21 @@ class DecoderModel:
 
         Hq, Hkv, Dh = self.Hq, self.Hkv, self.Dh
         mask = torch.triu(torch.full((Tn, Tn), float("-inf")), 1)
+        def rms(x, w):
+            return x * torch.rsqrt(x.pow(2).mean(-1, keepdim=True) + hp.norm_eps) * w.cpu()
+
         for L in self.layers:
             h = norm(x, L.attn_norm, L.attn_norm_b)
-            qkv = torch.cat([h @ deq(w).t() for w in L.qkv], -1)
+            if L.mla is not None:  # latent attention, same [rope | nope] head layout as _mla_qkv
+                m, H, dk, dv, rt, r = L.mla, hp.n_head, hp.head_dim, hp.head_dim_v, self.rot, hp.kv_lora_rank
+                q = h @ deq(m["q"]).t() if "q" in m else rms(h @ deq(m["q_a"]).t(), m["q_a_norm"]) @ deq(m["q_b"]).t()
+                kva = h @ deq(m["kv_a"]).t()
+                kvb = (rms(kva[:, :r], m["kv_a_norm"]) @ deq(m["kv_b"]).t()).view(Tn, H, dk - rt + dv)
+                kk = torch.cat([kva[:, r:].unsqueeze(1).expand(Tn, H, rt), kvb[:, :, :dk - rt]], -1)
+                vv = torch.cat([kvb[:, :, dk - rt:], kvb.new_zeros(Tn, H, dk - dv)], -1)
+                qkv = torch.cat([q, kk.reshape(Tn, -1), vv.reshape(Tn, -1)], -1)
+            else:
+                qkv = torch.cat([h @ deq(w).t() for w in L.qkv], -1)
             if L.qkv_bias is not None:
                 qkv = qkv + L.qkv_bias.cpu()
             q = rope(qkv[:, :Hq * Dh].view(Tn, Hq, Dh))
@@ -530,7 +624,8 @@ class DecoderModel:
             if L.window:
                 pos = torch.arange(Tn)
                 att = att.masked_fill((pos.view(-1, 1) - pos.view(1, -1)) >= L.window, float("-inf"))
-            a = torch.einsum("hqk,khd->qhd", torch.softmax(att, -1), v).reshape(Tn, Hq * Dh)
+            a = torch.einsum("hqk,khd->qhd", torch.softmax(att, -1), v)
+            a = a[:, :, :hp.head_dim_v].reshape(Tn, -1) if L.mla is not None else a.reshape(Tn, Hq * Dh)
             o = a @ deq(L.wo).t()
             if L.wo_bias is not None:
                 o = o + L.wo_bias.cpu()
@@ -543,6 +638,7 @@ class DecoderModel:
                     w, idx = torch.topk(torch.softmax(lg, -1), hp.n_expert_used, -1)
                     if hp.moe_renorm:
                         w = w / w.sum(-1, keepdim=True)
+                    w = w * hp.expert_weights_scale
                     out = torch.zeros_like(hin)
                     for tt in range(Tn):
                         for j in range(hp.n_expert_used):
@@ -555,15 +651,18 @@ class DecoderModel:
                         gu = torch.cat([hin @ deq(ww).t() for ww in L.shexp_gate_up], -1)
                         ff = gu.shape[-1] // 2
                         sh = (torch.nn.functional.silu(gu[:, :ff]) * gu[:, ff:]) @ deq(L.shexp_down).t()
-                        out = out + torch.sigmoid(hin @ L.shexp_gate.cpu()).unsqueeze(1) * sh
+                        if L.shexp_gate is not None:
+                            sh = torch.sigmoid(hin @ L.shexp_gate.cpu()).unsqueeze(1) * sh
+                        out = out + sh
                     return out
                 gu = torch.cat([hin @ deq(w).t() for w in L.gate_up], -1)
                 if L.up_bias is not None:
                     gu = gu + L.up_bias.cpu()
+                F = L.F or self.F
                 if hp.act == "swiglu":
-                    hh = torch.nn.functional.silu(gu[:, :self.F]) * gu[:, self.F:]
+                    hh = torch.nn.functional.silu(gu[:, :F]) * gu[:, F:]
                 elif hp.act == "geglu":
-                    hh = torch.nn.functional.gelu(gu[:, :self.F], approximate="tanh") * gu[:, self.F:]
+                    hh = torch.nn.functional.gelu(gu[:, :F], approximate="tanh") * gu[:, F:]
                 else:
                     hh = torch.nn.functional.gelu(gu, approximate="tanh")
                 d = hh @ deq(L.down).t()

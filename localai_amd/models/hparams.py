@@ -28,6 +28,14 @@ class HParams:
     n_expert_used: int = 0
     moe_renorm: bool = True           # renormalise the top-k routing weights (Mixtral); Qwen2-MoE does not
     n_ff_shexp: int = 0               # Qwen2-MoE shared expert width (0: none)
+    # DeepSeek-V2 multi-head latent attention + fine-grained MoE
+    kv_lora_rank: int = 0             # MLA: compressed kv width (0: regular attention)
+    q_lora_rank: int = 0              # MLA: compressed q width (0: one q projection, V2-Lite)
+    head_dim_v: int = 0               # MLA: value head width (keys: head_dim = nope + rope dims)
+    n_ff_exp: int = 0                 # routed / shared expert width when it differs from n_ff
+    n_layer_dense_lead: int = 0       # leading layers with a dense FFN instead of experts
+    expert_weights_scale: float = 1.0
+    yarn_log_mul: float = 0.0         # DeepSeek-V2: query scale mscale = 1 + yarn_log_mul * ln(factor)
     parallel_residual: bool = False   # phi-2: h = x + attn(ln x) + mlp(ln x)
     act: str = "swiglu"               # "swiglu" | "gelu" | "geglu" (Gemma: gelu(gate) * up)
     embed_scale: float = 1.0          # Gemma scales the token embeddings by sqrt(n_embd)
@@ -72,6 +80,7 @@ class HParams:
             n_ff = n_ff[0]
         if a == "qwen2moe":  # the routed experts' width; no dense FFN
             n_ff = g("expert_feed_forward_length", n_ff)
+        ds2 = a == "deepseek2"
         hp = HParams(
             arch=a,
             n_layer=int(g("block_count")),
@@ -92,8 +101,15 @@ class HParams:
             norm_type=norm_type,
             n_expert=int(g("expert_count", 0) or 0),
             n_expert_used=int(g("expert_used_count", 0) or 0),
-            moe_renorm=a != "qwen2moe",
+            moe_renorm=a not in ("qwen2moe", "deepseek2"),
             n_ff_shexp=int(g("expert_shared_feed_forward_length", 0) or 0) if a == "qwen2moe" else 0,
+            kv_lora_rank=int(g("attention.kv_lora_rank", 0) or 0) if ds2 else 0,
+            q_lora_rank=int(g("attention.q_lora_rank", 0) or 0) if ds2 else 0,
+            head_dim_v=int(g("attention.value_length", head_dim) or head_dim) if ds2 else 0,
+            n_ff_exp=int(g("expert_feed_forward_length", 0) or 0) if ds2 else 0,
+            n_layer_dense_lead=int(g("leading_dense_block_count", 0) or 0) if ds2 else 0,
+            expert_weights_scale=float(g("expert_weights_scale", 1.0) or 1.0) if ds2 else 1.0,
+            yarn_log_mul=float(g("rope.scaling.yarn_log_multiplier", 0.0) or 0.0) if ds2 else 0.0,
             # phi-2 / Command-R: h = x + attn(ln x) + mlp(ln x)
             parallel_residual=a in ("phi2", "command-r"),
             act="gelu" if a in ("phi2", "gptneox", "falcon", "starcoder2")
@@ -110,4 +126,11 @@ class HParams:
             tied_embeddings="output.weight" not in r.tensors,
             name=str(r.kv.get("general.name", "")),
         )
+        if ds2:
+            hp.n_ff_shexp = hp.n_ff_exp * int(g("expert_shared_count", 0) or 0)
+            if hp.rope_scaling == "yarn" and hp.rope_freq_scale < 1.0:
+                # llama.cpp build_deepseek2: kq_scale = mscale^2 / sqrt(head_dim_k)
+                import math
+                ms = 1.0 + hp.yarn_log_mul * math.log(1.0 / hp.rope_freq_scale)
+                hp.attn_scale = ms * ms / math.sqrt(hp.head_dim)
         return hp

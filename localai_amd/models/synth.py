@@ -57,6 +57,12 @@ class Preset:
     sliding_window: int = 0
     logit_scale: float = 0.0         # Command-R
     n_ff_shexp: int = 0              # Qwen2-MoE shared expert width
+    kv_lora_rank: int = 0            # DeepSeek-V2 latent attention (head_dim = key width, rope_dim = rotary part)
+    head_dim_v: int = 0
+    n_ff_exp: int = 0
+    n_expert_shared: int = 0
+    n_layer_dense_lead: int = 0
+    yarn_factor: float = 0.0
     name: str = "synthetic"
 
     @property
@@ -113,6 +119,13 @@ PRESETS: Dict[str, Preset] = {
     "tiny-qwen2moe": Preset(arch="qwen2moe", n_layer=2, n_embd=256, n_head=4, n_head_kv=2, n_ff=256, n_vocab=32256,
                             ctx=512, rope_theta=1e6, eps=1e-6, n_expert=4, n_expert_used=2, n_ff_shexp=512,
                             qtype="Q4_K", tokenizer="chatml", name="tiny-qwen2moe"),
+    # DeepSeek-V2: latent attention (kv_lora_rank, 192-wide keys with a 64-dim shared rotary part,
+    # 128-wide values), a leading dense layer, fine-grained experts plus shared experts, YaRN
+    "tiny-deepseek2": Preset(arch="deepseek2", n_layer=2, n_embd=256, n_head=4, n_head_kv=4, head_dim=192,
+                             head_dim_v=128, rope_dim=64, kv_lora_rank=256, n_ff=512, n_ff_exp=256, n_expert=4,
+                             n_expert_used=2, n_expert_shared=1, n_layer_dense_lead=1, n_vocab=32256, ctx=512,
+                             rope_theta=10000.0, eps=1e-6, yarn_factor=4.0, qtype="Q8_0", tokenizer="llama3",
+                             name="tiny-deepseek2"),
     "qwen2-7b": Preset(arch="qwen2", n_layer=28, n_embd=3584, n_head=28, n_head_kv=4, n_ff=18944, n_vocab=152064,
                        ctx=32768, rope_theta=1e6, eps=1e-6, tokenizer="chatml", name="Qwen2-7B-Instruct (random-init)"),
     "phi3-mini": Preset(arch="phi3", n_layer=32, n_embd=3072, n_head=32, n_head_kv=32, n_ff=8192, n_vocab=32064,
@@ -251,6 +264,22 @@ def tensor_list(p: Preset):
                         (b + "ffn_up.weight", (p.n_ff, d), i), (b + "ffn_up.bias", (p.n_ff,), i),
                         (b + "ffn_down.weight", (d, p.n_ff), i), (b + "ffn_down.bias", (d,), i)]
             continue
+        if p.arch == "deepseek2":
+            vd, rk = p.head_dim_v, p.kv_lora_rank
+            out += [(b + "attn_norm.weight", (d,), i), (b + "attn_q.weight", (qd, d), i),
+                    (b + "attn_kv_a_mqa.weight", (rk + p.rope_dim, d), i), (b + "attn_kv_a_norm.weight", (rk,), i),
+                    (b + "attn_kv_b.weight", (p.n_head * (hd - p.rope_dim + vd), rk), i),
+                    (b + "attn_output.weight", (d, p.n_head * vd), i), (b + "ffn_norm.weight", (d,), i)]
+            if i < p.n_layer_dense_lead:
+                out += [(b + "ffn_gate.weight", (p.n_ff, d), i), (b + "ffn_up.weight", (p.n_ff, d), i),
+                        (b + "ffn_down.weight", (d, p.n_ff), i)]
+            else:
+                E, fe, fs_ = p.n_expert, p.n_ff_exp, p.n_ff_exp * p.n_expert_shared
+                out += [(b + "ffn_gate_inp.weight", (E, d), i), (b + "ffn_gate_exps.weight", (E, fe, d), i),
+                        (b + "ffn_up_exps.weight", (E, fe, d), i), (b + "ffn_down_exps.weight", (E, d, fe), i),
+                        (b + "ffn_gate_shexp.weight", (fs_, d), i), (b + "ffn_up_shexp.weight", (fs_, d), i),
+                        (b + "ffn_down_shexp.weight", (d, fs_), i)]
+            continue
         if p.arch == "phi3":
             out += [(b + "attn_norm.weight", (d,), i), (b + "attn_qkv.weight", (qd + 2 * kvd, d), i),
                     (b + "attn_output.weight", (d, qd), i), (b + "ffn_norm.weight", (d,), i),
@@ -306,7 +335,7 @@ def write_model(path: str, preset: str | Preset, seed: int = 0, exact: bool = Fa
     w.add_uint32(f"{a}.rope.dimension_count", p.rope_dim or hd)
     if p.head_dim:
         w.add_uint32(f"{a}.attention.key_length", hd)
-        w.add_uint32(f"{a}.attention.value_length", hd)
+        w.add_uint32(f"{a}.attention.value_length", p.head_dim_v or hd)
     if p.attn_softcap:
         w.add_float32(f"{a}.attn_logit_softcapping", p.attn_softcap)
     if p.final_softcap:
@@ -315,6 +344,17 @@ def write_model(path: str, preset: str | Preset, seed: int = 0, exact: bool = Fa
         w.add_uint32(f"{a}.attention.sliding_window", p.sliding_window)
     if p.logit_scale:
         w.add_float32(f"{a}.logit_scale", p.logit_scale)
+    if p.kv_lora_rank:
+        w.add_uint32(f"{a}.attention.kv_lora_rank", p.kv_lora_rank)
+        w.add_uint32(f"{a}.expert_feed_forward_length", p.n_ff_exp)
+        w.add_uint32(f"{a}.expert_shared_count", p.n_expert_shared)
+        w.add_uint32(f"{a}.leading_dense_block_count", p.n_layer_dense_lead)
+        w.add_float32(f"{a}.expert_weights_scale", 1.0)
+    if p.yarn_factor:
+        w.add_string(f"{a}.rope.scaling.type", "yarn")
+        w.add_float32(f"{a}.rope.scaling.factor", p.yarn_factor)
+        w.add_uint32(f"{a}.rope.scaling.original_context_length", p.ctx // int(p.yarn_factor))
+        w.add_float32(f"{a}.rope.scaling.yarn_log_multiplier", 0.0707)
     if a in ("phi2", "command-r", "starcoder2"):
         w.add_float32(f"{a}.attention.layer_norm_epsilon", p.eps)
     else:

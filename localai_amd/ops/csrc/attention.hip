@@ -604,6 +604,7 @@ extern "C" int la_attn_decode(const void* q, const void* kc, const void* vc, con
     case 80: DEC_G(80); break;
     case 96: DEC_G(96); break;
     case 128: DEC_G(128); break;
+    case 192: DEC_G(192); break;  // DeepSeek-V2 latent attention keys (128 nope + 64 rope)
     case 256: DEC_G(256); break;
     default: return -2;
   }
@@ -629,6 +630,7 @@ extern "C" int la_attn_prefill(const void* q, const void* kc, const void* vc, co
     case 80: PF(80); break;
     case 96: PF(96); break;
     case 128: PF(128); break;
+    case 192: PF(192); break;
     case 256: PF(256); break;
     default: return -2;
   }

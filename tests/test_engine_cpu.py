@@ -106,7 +106,7 @@ def test_embeddings_shape_and_determinism(eng):
 
 @pytest.mark.parametrize("preset", ["tiny-mixtral", "tiny-phi2", "tiny-llama-q8", "tiny-qwen2", "tiny-phi3",
                                     "tiny-gemma", "tiny-gemma2", "tiny-command-r", "tiny-starcoder2",
-                                    "tiny-qwen2moe"])
+                                    "tiny-qwen2moe", "tiny-deepseek2"])
 def test_model_families_generate(preset, tmp_path):
     p = str(tmp_path / f"{preset}.gguf")
     synth.write_model(p, preset, exact=True)

@@ -85,7 +85,7 @@ def test_mixtral_moe_graph_decode(tmp_path):
 
 
 @pytest.mark.parametrize("preset", ["tiny-qwen2", "tiny-phi3", "tiny-gemma", "tiny-gemma2", "tiny-command-r",
-                                    "tiny-starcoder2", "tiny-qwen2moe"])
+                                    "tiny-starcoder2", "tiny-qwen2moe", "tiny-deepseek2"])
 def test_model_families_graph_decode(preset, tmp_path):
     """Qwen2 (q/k/v biases), Phi-3 (fused qkv + gate|up, head dim 96), Gemma (head dim 256, GeGLU,
     scaled embeddings): multi-step graph decode == single-step, first token == the fp32 oracle."""

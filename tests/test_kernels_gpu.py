@@ -294,7 +294,7 @@ def _paged_setup(lens, Hkv, Dh, BS, seed=0):
 
 
 @pytest.mark.parametrize("Hq,Hkv,Dh,BS", [(32, 8, 128, 32), (32, 32, 80, 32), (8, 1, 64, 16), (64, 8, 128, 32),
-                                         (16, 1, 96, 64), (8, 1, 256, 32), (16, 16, 256, 32)])
+                                         (16, 1, 96, 64), (8, 1, 256, 32), (16, 16, 256, 32), (16, 16, 192, 32)])
 @pytest.mark.parametrize("nw1", [False, True])
 def test_attn_decode(Hq, Hkv, Dh, BS, nw1, monkeypatch):
     if nw1:  # single-wave workgroups (the batch-decode variant) on a small batch
@@ -377,7 +377,7 @@ def test_attn_decode_batch1_long():
     assert (out.float().cpu() - ref.float()).abs().max().item() < 2e-2
 
 
-@pytest.mark.parametrize("Hq,Hkv,Dh", [(32, 8, 128), (32, 32, 80), (8, 1, 256)])
+@pytest.mark.parametrize("Hq,Hkv,Dh", [(32, 8, 128), (32, 32, 80), (8, 1, 256), (16, 16, 192)])
 def test_attn_prefill(Hq, Hkv, Dh):
     # (new tokens, total context) per sequence: plain prefill, prefix-cached, chunked
     qlens = [70, 5, 33]
