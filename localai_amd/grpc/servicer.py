@@ -134,6 +134,16 @@ class EngineServicer:
             ctx = request.ContextSize or 2048
             if request.MaxModelLen:
                 ctx = request.MaxModelLen
+            from ..models.whisper import WhisperModel, is_whisper_ggml
+            if is_whisper_ggml(path):
+                # whisper.cpp GGML speech model (the reference's whisper backend)
+                loop = asyncio.get_running_loop()
+                wm = await loop.run_in_executor(None, lambda: WhisperModel(path, dev))
+                with self._lock:
+                    self.engine, self.loaded_path = wm, os.path.abspath(path)
+                    self.model_name = os.path.basename(path)
+                    self.state = pb.StatusResponse.READY
+                return pb.Result(success=True, message="Loaded")
             from ..gguf import GGUFReader
             if GGUFReader(path).architecture in ("bert", "nomic-bert"):
                 # sentence-embedding encoder (bert-embeddings / sentencetransformers backends)
@@ -403,7 +413,19 @@ class EngineServicer:
         raise Unimplemented("SoundGeneration")
 
     async def AudioTranscription(self, request, context=None):
-        raise Unimplemented("AudioTranscription")
+        """backend/go/transcribe/whisper/whisper.go:27-104: audio -> 16 kHz mono -> segments + text."""
+        from ..models.whisper import WhisperModel, load_audio
+        if not isinstance(self.engine, WhisperModel):
+            raise Unimplemented("AudioTranscription (the loaded model is not a whisper model)")
+        wm = self.engine
+
+        def run():
+            audio = load_audio(request.dst)
+            return wm.transcribe(audio, language=request.language, translate=bool(request.translate))
+        segs, text = await asyncio.get_running_loop().run_in_executor(None, run)
+        return pb.TranscriptResult(
+            segments=[pb.TranscriptSegment(id=s.id, start=s.start_ns, end=s.end_ns, text=s.text, tokens=s.tokens)
+                      for s in segs], text=text)
 
     def shutdown(self):
         if self.engine is not None:

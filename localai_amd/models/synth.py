@@ -13,6 +13,7 @@ tokens (Llama-3's <|begin_of_text|> ... <|eot_id|> at 128000+).
 from __future__ import annotations
 
 import gzip
+import math
 import json
 import os
 from dataclasses import dataclass, field, replace
@@ -436,6 +437,61 @@ def write_lora(path: str, base_path: str, targets: Sequence[str] = ("attn_q", "f
         w.add_tensor(name + ".lora_a", (rank, K), GGMLType.F32, a.reshape(-1))
         w.add_tensor(name + ".lora_b", (N, rank), GGMLType.F32, b.reshape(-1))
     w.write()
+    return path
+
+
+def write_whisper(path: str, n_audio_state: int = 64, n_audio_head: int = 2, n_audio_layer: int = 2,
+                  n_text_state: int = 64, n_text_head: int = 2, n_text_layer: int = 2, n_mels: int = 80,
+                  multilingual: bool = True, seed: int = 0, std: float = 0.05) -> str:
+    """Random-init whisper.cpp GGML model (the `ggml-*.bin` layout of the reference's whisper
+    backend) with the real vocabulary size, a Slaney mel filterbank and the OpenAI tensor names."""
+    from ..tokenizer import unicode_to_bytes
+    from .whisper import WhisperHParams, mel_filters, write_ggml
+    n_vocab = 51865 if multilingual else 51864
+    hp = WhisperHParams(n_vocab, 1500, n_audio_state, n_audio_head, n_audio_layer, 448, n_text_state, n_text_head,
+                        n_text_layer, n_mels, 1)
+    u2b = unicode_to_bytes()
+    words = []
+    for t in _bpe_asset()["tokens"]:
+        try:
+            words.append(bytes(u2b[c] for c in t))
+        except KeyError:
+            continue
+        if len(words) == 50256:
+            break
+    while len(words) < 50256:
+        words.append(b"<fill%d>" % len(words))
+    rng = np.random.default_rng(seed)
+    t = {}
+
+    def r(*shape, sd=std):
+        return (sd * rng.standard_normal(shape)).astype(np.float32)
+
+    da, dt = n_audio_state, n_text_state
+    t["encoder.positional_embedding"] = r(1500, da, sd=0.5)
+    t["encoder.conv1.weight"], t["encoder.conv1.bias"] = r(da, n_mels, 3, sd=0.2), r(da)
+    t["encoder.conv2.weight"], t["encoder.conv2.bias"] = r(da, da, 3, sd=0.2), r(da)
+
+    def block(p, d, cross):
+        for ln in ("attn_ln", "mlp_ln") + (("cross_attn_ln",) if cross else ()):
+            t[p + ln + ".weight"], t[p + ln + ".bias"] = 1 + r(d, sd=0.1), r(d)
+        for a in ("attn",) + (("cross_attn",) if cross else ()):
+            for nm in ("query", "key", "value", "out"):
+                t[f"{p}{a}.{nm}.weight"] = r(d, d, sd=1.0 / math.sqrt(d))
+                if nm != "key":
+                    t[f"{p}{a}.{nm}.bias"] = r(d)
+        t[p + "mlp.0.weight"], t[p + "mlp.0.bias"] = r(4 * d, d, sd=1.0 / math.sqrt(d)), r(4 * d)
+        t[p + "mlp.2.weight"], t[p + "mlp.2.bias"] = r(d, 4 * d, sd=0.5 / math.sqrt(d)), r(d)
+
+    for i in range(n_audio_layer):
+        block(f"encoder.blocks.{i}.", da, False)
+    t["encoder.ln_post.weight"], t["encoder.ln_post.bias"] = 1 + r(da, sd=0.1), r(da)
+    t["decoder.positional_embedding"] = r(448, dt, sd=0.1)
+    t["decoder.token_embedding.weight"] = r(n_vocab, dt, sd=0.5)
+    for i in range(n_text_layer):
+        block(f"decoder.blocks.{i}.", dt, True)
+    t["decoder.ln.weight"], t["decoder.ln.bias"] = 1 + r(dt, sd=0.1), r(dt)
+    write_ggml(path, hp, mel_filters(n_mels), words, t)
     return path
 
 
