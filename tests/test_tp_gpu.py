@@ -1,0 +1,22 @@
+"""TP=2 engine on the MI355X with both ranks on the one GPU of the test box (scripts/tp_rehearsal.py):
+column/row-parallel layers on the HIP kernels, decode all-reduces through the IPC one-shot kernel,
+greedy output agreeing with TP=1.  The ranks are child processes of torch.distributed.run."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.gpu
+def test_tp2_engine_two_ranks_one_gpu(tmp_path):
+    from localai_amd.models import synth
+    p = synth.write_model(str(tmp_path / "tp.gguf"), "tiny-llama", exact=True)
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", "29541",
+                        os.path.join(ROOT, "scripts", "tp_rehearsal.py"), p],
+                       cwd=ROOT, env=dict(os.environ), capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "TP_OK" in r.stdout, r.stdout[-2000:]
