@@ -50,11 +50,13 @@ def _worker(rank, world, port, path, q, ep=False):
 import pytest
 
 
-@pytest.fixture(params=["tiny-llama", "tiny-mixtral", "tiny-phi2", "tiny-qwen2moe"])
+@pytest.fixture(params=["tiny-llama", "tiny-mixtral", "tiny-phi2", "tiny-qwen2moe", "tiny-gemma2", "tiny-phi3"])
 def tp_model_path(request, tiny_model_path, tmp_path_factory):
     """Llama (dense GQA), Mixtral (TP-within-expert: every expert's F sharded, router replicated),
     Phi-2 (LayerNorm + biases, NEOX partial rotary, biases added once after the all-reduce) and
-    Qwen2-MoE (unaligned expert F shards, sigmoid-gated shared expert sliced like a dense MLP)."""
+    Qwen2-MoE (unaligned expert F shards, sigmoid-gated shared expert sliced like a dense MLP),
+    Gemma-2 (one kv head replicated on both ranks, post-norms on the reduced outputs, soft-capping)
+    and Phi-3 (fused q|k|v and gate|up tensors sliced per rank)."""
     if request.param == "tiny-llama":
         return tiny_model_path
     from localai_amd.models import synth
