@@ -51,9 +51,22 @@ def _looks_like_url(s: str) -> bool:
                                          "ollama://", "file://"))
 
 
+def _copy_tree(o: Any) -> Any:
+    """Deep copy of YAML/JSON-shaped data (dicts, lists, scalars): every request gets a private
+    config (request fields override it), so this runs per request -- copy.deepcopy's memo
+    bookkeeping cost ~5x more on a gallery-sized config."""
+    if isinstance(o, dict):
+        return {k: _copy_tree(v) for k, v in o.items()}
+    if isinstance(o, list):
+        return [_copy_tree(v) for v in o]
+    if isinstance(o, (str, int, float, bool)) or o is None:
+        return o
+    return copy.deepcopy(o)
+
+
 class BackendConfig:
     def __init__(self, raw: Optional[Dict[str, Any]] = None):
-        self.raw: Dict[str, Any] = copy.deepcopy(raw) if raw else {}
+        self.raw: Dict[str, Any] = _copy_tree(raw) if raw else {}
         self.raw.setdefault("parameters", {})
         if self.raw["parameters"] is None:
             self.raw["parameters"] = {}
