@@ -147,7 +147,10 @@ def main():
         runner = EngineRunner(eng, args)
 
     def wave(w):
-        return runner.wave([m + f" (wave {w})" for m in msgs])
+        # the wave tag leads the message: no prompt shares more than the chat-template header with a
+        # prompt of an earlier wave, so every wave prefills its 256 prompts in full (a trailing tag
+        # would let the engine's prefix cache skip ~90 % of the prefill of every repeated wave)
+        return runner.wave([f"(wave {w}) " + m for m in msgs])
 
     for w in range(args.warmup):
         wave(-1 - w)
