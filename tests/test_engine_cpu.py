@@ -241,3 +241,25 @@ def test_engine_trace_timeline(tiny_model_path, tmp_path, monkeypatch):
     assert len(req) == 1 and req[0]["args"]["correlation_id"] == "cid-42"
     assert req[0]["args"]["completion_tokens"] == 3 and req[0]["dur"] > 0
     assert any(ev["name"] == "first_token" and ev["args"]["correlation_id"] == "cid-42" for ev in doc["traceEvents"])
+
+
+def test_prefill_tuning_step_packs_one_full_chunk(tiny_model_path):
+    """warmup()'s TunableOp pass must hit the exact full-chunk GEMM shape M = max_batched_tokens
+    (hipBLASLt solutions are tuned per exact M): one prefill forward of that many tokens, then
+    an idle engine with its serving counters untouched."""
+    e = _engine(tiny_model_path, seqs=16, max_batched_tokens=1024, ctx=256)
+    seen = []
+    fwd = e.model.forward
+
+    def spy(fb, kv):
+        if not fb.decode:
+            seen.append(int(fb.tokens.numel()))
+        return fwd(fb, kv)
+
+    e.model.forward = spy
+    before = dict(e.metrics)
+    e._tune_prefill()
+    assert seen == [1024]
+    assert not e.requests and e.metrics == before
+    out = e.generate("hello", SamplingParams(max_tokens=3, temperature=0.0))
+    assert out["completion_tokens"] == 3
