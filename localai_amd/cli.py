@@ -266,6 +266,25 @@ def cmd_federated(a) -> int:
     return 0
 
 
+def cmd_explorer(a) -> int:
+    """`core/cli/explorer.go:22-49`: network directory + discovery (gateway/explorer.py)."""
+    import threading
+
+    from .gateway.explorer import Database, DiscoveryServer, create_explorer_app, parse_duration
+    db = Database(a.pool_database)
+    dur = parse_duration(a.connection_timeout)
+    if a.only_sync:
+        DiscoveryServer(db, dur, a.connection_error_threshold).start(keep_running=False)
+        return 0
+    if a.with_sync:
+        ds = DiscoveryServer(db, dur, a.connection_error_threshold)
+        threading.Thread(target=ds.start, name="explorer-sync", daemon=True).start()
+    from .gateway.native_server import NativeHTTPServer
+    host, port = parse_address(a.address)
+    NativeHTTPServer(create_explorer_app(db), host, port).run()
+    return 0
+
+
 def cmd_worker(a) -> int:
     from .parallel.worker import main as worker_main
     rest = list(a.rest)
@@ -312,6 +331,17 @@ def build_parser() -> argparse.ArgumentParser:
     f.add_argument("--workers", default="", help="comma-separated worker base URLs")
     f.add_argument("--random-worker", action="store_true")
     f.add_argument("--target-worker", default="")
+    e = sub.add_parser("explorer", help="directory of LocalAI networks with worker discovery")
+    env = os.environ.get
+    e.add_argument("--address", default=env("LOCALAI_ADDRESS", env("ADDRESS", ":8080")))
+    e.add_argument("--pool-database", default=env("LOCALAI_POOL_DATABASE", env("POOL_DATABASE", "explorer.json")))
+    e.add_argument("--connection-timeout", default=env("LOCALAI_CONNECTION_TIMEOUT", env("CONNECTION_TIMEOUT", "2m")))
+    e.add_argument("--connection-error-threshold", type=int,
+                   default=int(env("LOCALAI_CONNECTION_ERROR_THRESHOLD", env("CONNECTION_ERROR_THRESHOLD", "3"))))
+    e.add_argument("--with-sync", action="store_true",
+                   default=env("LOCALAI_WITH_SYNC", env("WITH_SYNC", "")).lower() in ("1", "true"))
+    e.add_argument("--only-sync", action="store_true",
+                   default=env("LOCALAI_ONLY_SYNC", env("ONLY_SYNC", "")).lower() in ("1", "true"))
     w = sub.add_parser("worker", help="tensor-parallel engine worker group (replaces llama-cpp-rpc workers)")
     w.add_argument("rest", nargs=argparse.REMAINDER)
     return ap
@@ -327,7 +357,7 @@ def main(argv: Optional[List[str]] = None) -> int:
         ap.print_help()
         return 2
     fn = {"run": cmd_run, "models": cmd_models, "transcript": cmd_transcript, "util": cmd_util,
-          "worker": cmd_worker, "federated": cmd_federated}.get(a.cmd) or getattr(a, "fn", None)
+          "worker": cmd_worker, "federated": cmd_federated, "explorer": cmd_explorer}.get(a.cmd) or getattr(a, "fn", None)
     return fn(a)
 
 
