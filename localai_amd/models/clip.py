@@ -5,7 +5,9 @@ Preprocessing (PIL decode -> resize -> center crop / pad -> normalise) runs on t
 runs on the device in bf16: patch embedding as one GEMM over unfolded patches (im2col), fused
 QKV, SDPA attention, LayerNorm / quick-GELU, the two-layer GELU projector into the LLM's
 embedding space.  LLaVA-1.5 (one 336^2 tile -> 576 embeddings) and LLaVA-1.6 "anyres"
-(grid tiles + a base tile, spatial unpadding, image_newline rows) layouts are supported.
+(grid tiles + a base tile, spatial unpadding, image_newline rows) layouts are supported, and so are
+SigLIP-style towers without a class token (moondream2's mmproj: 378^2 / patch 14 -> 729
+embeddings, GELU, post-LayerNorm only; clip.cpp treats `v.class_embd` as optional the same way).
 """
 from __future__ import annotations
 
@@ -65,7 +67,7 @@ class ClipVision:
         pe = t("v.patch_embd.weight")                       # [D, 3, p, p]
         self.patch_w = pe.reshape(D, -1).to(dtype)          # im2col GEMM weight [D, 3*p*p]
         self.patch_b = t("v.patch_embd.bias", False)
-        self.cls = t("v.class_embd")
+        self.cls = t("v.class_embd", False)  # SigLIP towers (moondream2) have no class token
         self.pos = t("v.position_embd.weight")
         self.pre_ln = (t("v.pre_ln.weight", False), t("v.pre_ln.bias", False))
         self.post_ln = (t("v.post_ln.weight", False), t("v.post_ln.bias", False))
@@ -148,7 +150,9 @@ class ClipVision:
         h = (cols.to(self.dtype) @ self.patch_w.t()).float()                  # im2col patch GEMM
         if self.patch_b is not None:
             h = h + self.patch_b
-        h = torch.cat([self.cls.view(1, 1, D).expand(n, 1, D), h], 1) + self.pos[: h.shape[1] + 1]
+        if self.cls is not None:
+            h = torch.cat([self.cls.view(1, 1, D).expand(n, 1, D), h], 1)
+        h = h + self.pos[: h.shape[1]]
         if self.pre_ln[0] is not None:
             h = F.layer_norm(h, (D,), self.pre_ln[0], self.pre_ln[1], self.eps)
         L = h.shape[1]
@@ -167,7 +171,8 @@ class ClipVision:
             h = res + (f.to(self.dtype) @ ly["f2_w"].t()).float() + ly["f2_b"]
         if self.post_ln[0] is not None:
             h = F.layer_norm(h, (D,), self.post_ln[0], self.post_ln[1], self.eps)
-        h = h[:, 1:]                                                           # drop CLS
+        if self.cls is not None:
+            h = h[:, 1:]                                                       # drop CLS
         y = (h.to(self.dtype) @ self.mm0[0].t()).float() + self.mm0[1]
         y = F.gelu(y)
         y = (y.to(self.dtype) @ self.mm2[0].t()).float() + self.mm2[1]

@@ -510,9 +510,10 @@ def ensure_model(preset: str, cache_dir: Optional[str] = None, **kw) -> str:
 
 def write_mmproj(path: str, out_dim: int, dim: int = 1024, n_layer: int = 23, heads: int = 16, ffn: int = 4096,
                  image_size: int = 336, patch: int = 14, seed: int = 0, std: float = 0.02,
-                 pinpoints: Optional[List[int]] = None) -> str:
+                 pinpoints: Optional[List[int]] = None, siglip: bool = False) -> str:
     """Random-init llama.cpp-style LLaVA mmproj GGUF (CLIP ViT-L/14 layout + mlp2x_gelu projector).
-    Defaults are the LLaVA-1.5/1.6 vision tower; tests pass tiny dims."""
+    Defaults are the LLaVA-1.5/1.6 vision tower; tests pass tiny dims.  `siglip`: the moondream2
+    layout instead -- no class token, post-LayerNorm instead of pre-LayerNorm, GELU, mean/std 0.5."""
     w = GGUFWriter(path, "clip")
     w.add_bool("clip.has_vision_encoder", True)
     w.add_bool("clip.has_llava_projector", True)
@@ -525,16 +526,23 @@ def write_mmproj(path: str, out_dim: int, dim: int = 1024, n_layer: int = 23, he
     w.add_uint32("clip.vision.attention.head_count", heads)
     w.add_float32("clip.vision.attention.layer_norm_epsilon", 1e-5)
     w.add_uint32("clip.vision.block_count", n_layer)
-    w.add_array("clip.vision.image_mean", [0.48145466, 0.4578275, 0.40821073], GGUFValueType.FLOAT32)
-    w.add_array("clip.vision.image_std", [0.26862954, 0.26130258, 0.27577711], GGUFValueType.FLOAT32)
-    w.add_bool("clip.use_gelu", False)
+    mean = [0.5, 0.5, 0.5] if siglip else [0.48145466, 0.4578275, 0.40821073]
+    sd = [0.5, 0.5, 0.5] if siglip else [0.26862954, 0.26130258, 0.27577711]
+    w.add_array("clip.vision.image_mean", mean, GGUFValueType.FLOAT32)
+    w.add_array("clip.vision.image_std", sd, GGUFValueType.FLOAT32)
+    w.add_bool("clip.use_gelu", siglip)
     if pinpoints:
         w.add_array("clip.vision.image_grid_pinpoints", pinpoints, GGUFValueType.INT32)
         w.add_string("clip.vision.mm_patch_merge_type", "spatial_unpad")
     rng = np.random.default_rng(seed)
     npatch = (image_size // patch) ** 2
-    tensors = [("v.patch_embd.weight", (dim, 3, patch, patch)), ("v.class_embd", (dim,)),
-               ("v.position_embd.weight", (npatch + 1, dim)), ("v.pre_ln.weight", (dim,)), ("v.pre_ln.bias", (dim,))]
+    if siglip:
+        tensors = [("v.patch_embd.weight", (dim, 3, patch, patch)), ("v.patch_embd.bias", (dim,)),
+                   ("v.position_embd.weight", (npatch, dim)), ("v.post_ln.weight", (dim,)), ("v.post_ln.bias", (dim,))]
+    else:
+        tensors = [("v.patch_embd.weight", (dim, 3, patch, patch)), ("v.class_embd", (dim,)),
+                   ("v.position_embd.weight", (npatch + 1, dim)), ("v.pre_ln.weight", (dim,)),
+                   ("v.pre_ln.bias", (dim,))]
     for i in range(n_layer):
         b = f"v.blk.{i}."
         for nm in ("attn_q", "attn_k", "attn_v", "attn_out"):
@@ -548,7 +556,7 @@ def write_mmproj(path: str, out_dim: int, dim: int = 1024, n_layer: int = 23, he
         tensors.append(("model.image_newline", (out_dim,)))
     for name, shape in tensors:
         n = int(np.prod(shape))
-        if name.endswith(("ln1.weight", "ln2.weight", "pre_ln.weight")):
+        if name.endswith(("ln1.weight", "ln2.weight", "pre_ln.weight", "post_ln.weight")):
             a = (1.0 + 0.05 * rng.standard_normal(n)).astype(np.float32)
         else:
             a = (std * rng.standard_normal(n)).astype(np.float32)

@@ -1,8 +1,10 @@
 """LLM engine on CPU (torch reference ops): greedy decoding vs. the fp32 oracle, sampling
 params, stop words, max tokens, abort, continuous batching consistency, model families
 (llama / mixtral MoE / phi2), embeddings.  The same engine drives the HIP kernels on GPU."""
+import math
 import threading
 
+import numpy as np
 import pytest
 import torch
 
@@ -215,6 +217,76 @@ def test_llava16_anyres_layout(tiny_model_path, tmp_path):
     assert layout is not None and tiles.shape[0] == 1 + layout[0] * layout[1]
     emb = cv.embed_image(_png((90, 90, 90), size=50))
     assert emb.shape[1] == n_embd and emb.shape[0] > 4 and torch.isfinite(emb).all()
+
+
+def _siglip_reference(mm_path, pix):
+    """Plain fp32 SigLIP tower + mlp projector straight from the GGUF tensors (no class token,
+    post-LayerNorm, exact GELU) -- the oracle for ClipVision's moondream2 path."""
+    import torch.nn.functional as F
+
+    from localai_amd.gguf import GGUFReader, dequantize
+    r = GGUFReader(mm_path)
+    kv = r.kv
+
+    def t(n):
+        x = r.tensors[n]
+        return torch.from_numpy(np.ascontiguousarray(dequantize(x.data, x.ggml_type, x.shape).reshape(x.shape),
+                                                     dtype=np.float32))
+    D, P, H = int(kv["clip.vision.embedding_length"]), int(kv["clip.vision.patch_size"]), \
+        int(kv["clip.vision.attention.head_count"])
+    x = F.conv2d(pix.float(), t("v.patch_embd.weight"), t("v.patch_embd.bias"), stride=P)
+    h = x.flatten(2).transpose(1, 2) + t("v.position_embd.weight")
+    n, L, _ = h.shape
+    for i in range(int(kv["clip.vision.block_count"])):
+        b = f"v.blk.{i}."
+        a = F.layer_norm(h, (D,), t(b + "ln1.weight"), t(b + "ln1.bias"), 1e-5)
+        q, k, v = (F.linear(a, t(b + f"attn_{c}.weight"), t(b + f"attn_{c}.bias")).view(n, L, H, D // H)
+                   .transpose(1, 2) for c in "qkv")
+        att = torch.softmax(q @ k.transpose(-1, -2) / math.sqrt(D // H), -1) @ v
+        h = h + F.linear(att.transpose(1, 2).reshape(n, L, D), t(b + "attn_out.weight"), t(b + "attn_out.bias"))
+        a = F.layer_norm(h, (D,), t(b + "ln2.weight"), t(b + "ln2.bias"), 1e-5)
+        f1w, f2w = t(b + "ffn_down.weight"), t(b + "ffn_up.weight")
+        f1b, f2b = t(b + "ffn_down.bias"), t(b + "ffn_up.bias")
+        if f1w.shape[1] != D:
+            f1w, f2w, f1b, f2b = f2w, f1w, f2b, f1b
+        h = h + F.linear(F.gelu(F.linear(a, f1w, f1b)), f2w, f2b)
+    h = F.layer_norm(h, (D,), t("v.post_ln.weight"), t("v.post_ln.bias"), 1e-5)
+    y = F.gelu(F.linear(h, t("mm.0.weight"), t("mm.0.bias")))
+    return F.linear(y, t("mm.2.weight"), t("mm.2.bias"))
+
+
+def test_moondream_siglip_tower(tmp_path):
+    """moondream2 layout (gallery/moondream.yaml): a phi2 text model with a SigLIP mmproj that has
+    no class token -- every patch becomes a prompt embedding; the tower matches an fp32 oracle."""
+    from localai_amd.gguf import GGUFReader
+    from localai_amd.models.clip import ClipVision
+    txt = str(tmp_path / "moondream-text.gguf")
+    synth.write_model(txt, "tiny-phi2", exact=True)
+    n_embd = int(GGUFReader(txt).kv["phi2.embedding_length"])
+    mm = synth.write_mmproj(str(tmp_path / "moondream-mmproj.gguf"), out_dim=n_embd, dim=64, n_layer=2, heads=4,
+                            ffn=128, image_size=42, patch=14, siglip=True)
+    cv = ClipVision(mm, torch.device("cpu"))
+    assert cv.cls is None and cv.n_patches == 9
+    tiles, layout = cv.preprocess(_png((30, 160, 60), size=60))
+    assert layout is None and tiles.shape == (1, 3, 42, 42)
+    got = cv.encode_tiles(tiles)
+    ref = _siglip_reference(mm, tiles)
+    assert got.shape == ref.shape == (1, 9, n_embd)
+    err = float((got - ref).abs().max() / ref.abs().max())
+    assert err < 3e-2, err  # bf16 GEMM operands vs fp32
+    e = _engine(txt, mmproj=mm)
+    got_ev = {}
+
+    def cb(ev):
+        if ev.finished:
+            got_ev.update(n_prompt=ev.prompt_tokens, n=ev.completion_tokens, err=ev.error)
+    prompt = "[img-0]\nQuestion: What is this?\n\nAnswer:"
+    e.add_request(prompt, SamplingParams(max_tokens=3, temperature=0.0, ignore_eos=True), cb,
+                  images=[_png((30, 160, 60), size=60)])
+    while not got_ev:
+        e.step()
+    assert got_ev["err"] == "" and got_ev["n"] == 3
+    assert got_ev["n_prompt"] == len(e.tokenize(prompt.replace("[img-0]", ""))) + 9
 
 
 def test_engine_trace_timeline(tiny_model_path, tmp_path, monkeypatch):
