@@ -93,14 +93,24 @@ class MetricsMiddleware:
 def create_app(state: AppState) -> FastAPI:
     from contextlib import asynccontextmanager
 
+    cfg = state.cfg
+    p2p_node = None
+    if cfg.p2p:
+        from .p2p import P2PNode, advertise_url
+        p2p_node = P2PNode(cfg.p2p_token, cfg.p2p_network_id, advertise_url(cfg.address))
+        cfg.p2p_token = p2p_node.token  # a generated token is what /api/p2p/token serves
+
     @asynccontextmanager
     async def lifespan(app):
         state.manager.start_watchdog()
+        if p2p_node is not None:
+            p2p_node.start()
         yield
+        if p2p_node is not None:
+            p2p_node.stop()
         await state.manager.stop_all()
 
     app = FastAPI(title="LocalAI (MI355X)", lifespan=lifespan, docs_url="/swagger", openapi_url="/swagger/doc.json")
-    cfg = state.cfg
 
     @app.exception_handler(APIError)
     async def _api_err(request: Request, e: APIError):
@@ -123,14 +133,16 @@ def create_app(state: AppState) -> FastAPI:
         origins = [o for o in cfg.cors_allow_origins.split(",") if o] or ["*"]
         app.add_middleware(CORSMiddleware, allow_origins=origins, allow_methods=["*"], allow_headers=["*"])
 
-    from . import openai_routes, localai_routes, files_routes, gallery_routes, webui
+    from . import openai_routes, localai_routes, files_routes, gallery_routes, p2p, webui
     app.include_router(openai_routes.build_router(state))
     app.include_router(files_routes.build_router(state))
     app.include_router(localai_routes.build_router(state))
     app.include_router(webui.build_router(state))
+    app.include_router(p2p.build_router(p2p_node))
     if not cfg.disable_gallery_endpoint:
         app.include_router(gallery_routes.build_router(state))
     app.state.localai = state
+    app.state.p2p = p2p_node
     return app
 
 
