@@ -37,6 +37,7 @@ ENGINE_BACKENDS = {"", "llama-cpp", "llama", "llama-cpp-hipblas", "llama-cpp-cud
                    "vllm", "transformers",
                    "whisper"}  # whisper.cpp GGML models run on the native worker (models/whisper.py)
 STORE_BACKEND = "local-store"
+HF_BACKENDS = {"huggingface", "langchain-huggingface"}  # remote Inference API (grpc/huggingface.py)
 
 
 def free_port() -> int:
@@ -181,6 +182,13 @@ class ModelManager:
         ext = self.app.external_grpc_backends
         if backend in ext:
             return await self._start_external(mid, backend, ext[backend], cfg)
+        if backend in HF_BACKENDS:
+            from ..grpc.huggingface import HuggingFaceServicer
+            sv = HuggingFaceServicer()
+            res = await sv.LoadModel(grpc_model_options(cfg, self.app, self.models_path), None)
+            if not res.success:
+                raise RuntimeError(f"could not load model: {res.message}")
+            return LoadedModel(mid, "huggingface", EmbeddedBackend(sv), servicer=sv)
         if backend == STORE_BACKEND:
             from ..grpc.servicer import EngineServicer
             sv = EngineServicer(device=self._pick_device(cfg))
