@@ -30,7 +30,8 @@ import numpy as np
 import torch
 
 from .. import ops
-from ..gguf import GGUFReader
+from ..gguf import GGUFReader  # noqa: F401 (re-exported for callers)
+from ..models.hf_checkpoint import open_model
 from ..models.decoder import DecoderModel, ForwardBatch, TPInfo
 from ..native import core
 from ..tokenizer import Tokenizer
@@ -124,7 +125,7 @@ class LLMEngine:
         if self.device.type == "cuda":
             torch.cuda.set_device(self.device)
             ops.lib()  # fail loudly if the kernel library is missing on a GPU box
-        self.reader = GGUFReader(cfg.model_path)
+        self.reader = open_model(cfg.model_path)  # GGUF file or HF checkpoint directory
         self.tokenizer = Tokenizer.from_gguf(self.reader)
         ro = {}
         if cfg.rope_freq_base:

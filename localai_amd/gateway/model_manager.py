@@ -196,7 +196,8 @@ class ModelManager:
         if backend not in ENGINE_BACKENDS:
             raise RuntimeError(f"backend {backend!r} is not available (register it with --external-grpc-backends)")
         opts = grpc_model_options(cfg, self.app, self.models_path)
-        if not os.path.isfile(opts.ModelFile):
+        from ..models.hf_checkpoint import is_hf_checkpoint
+        if not (os.path.isfile(opts.ModelFile) or is_hf_checkpoint(opts.ModelFile)):
             raise RuntimeError(f"could not load model: model file {opts.ModelFile} not found")
         tp = int(cfg.raw.get("tensor_parallel_size") or 0)
         if tp > 1:

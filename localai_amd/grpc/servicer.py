@@ -118,7 +118,8 @@ class EngineServicer:
     async def LoadModel(self, request, context=None):
         from ..engine.llm_engine import EngineConfig, LLMEngine
         path = request.ModelFile or request.Model
-        if not os.path.isfile(path):
+        from ..models.hf_checkpoint import is_hf_checkpoint
+        if not (os.path.isfile(path) or is_hf_checkpoint(path)):
             return pb.Result(success=False, message=f"model file not found: {path}")
         if self.engine is not None and getattr(self, "loaded_path", "") == os.path.abspath(path):
             return pb.Result(success=True, message="Loaded")  # pre-loaded (tensor-parallel worker group)
@@ -145,7 +146,7 @@ class EngineServicer:
                     self.state = pb.StatusResponse.READY
                 return pb.Result(success=True, message="Loaded")
             from ..gguf import GGUFReader
-            if GGUFReader(path).architecture in ("bert", "nomic-bert"):
+            if os.path.isfile(path) and GGUFReader(path).architecture in ("bert", "nomic-bert"):
                 # sentence-embedding encoder (bert-embeddings / sentencetransformers backends)
                 from ..models.bert import BertConfig, BertEmbedder
                 loop = asyncio.get_running_loop()

@@ -622,3 +622,61 @@ def write_bert(path: str, dim: int = 384, n_layer: int = 6, heads: int = 12, ffn
         w.add_tensor(name, shape, t, quantize(a, t))
     w.write()
     return path
+
+
+def write_hf_checkpoint(out_dir: str, kind: str = "llama", n_layer: int = 2, hidden: int = 64, heads: int = 4,
+                        kv_heads: int = 2, ffn: int = 128, n_experts: int = 0, seed: int = 0,
+                        rope_scaling: Optional[dict] = None, dtype: str = "float32") -> str:
+    """Random-init Hugging Face checkpoint directory (config.json, model.safetensors, tokenizer.json,
+    tokenizer_config.json) built with `transformers` itself, so a test can compare the engine with
+    the library's own forward.  kind: llama | mistral | qwen2 | mixtral.  The tokenizer is a byte-level
+    BPE (this package's 32k asset + the Llama-3 special tokens) with the Llama-3 chat template."""
+    import torch
+    import transformers as tf
+    from tokenizers import Regex, Tokenizer as HFTok, decoders, models, pre_tokenizers
+
+    from ..tokenizer import LLAMA3_PAT
+    a = _bpe_asset()
+    n_normal = len(a["tokens"])
+    vocab = {t: i for i, t in enumerate(a["tokens"])}
+    specials = [LLAMA3_SPECIAL.get(k, f"<|reserved_special_token_{k}|>") for k in range(16)]
+    n_vocab = n_normal + len(specials)
+    bos, eos = n_normal + 0, n_normal + 9
+    torch.manual_seed(seed)
+    common = dict(vocab_size=n_vocab, hidden_size=hidden, intermediate_size=ffn, num_hidden_layers=n_layer,
+                  num_attention_heads=heads, num_key_value_heads=kv_heads, max_position_embeddings=512,
+                  rms_norm_eps=1e-5, bos_token_id=bos, eos_token_id=eos, tie_word_embeddings=False)
+    if rope_scaling:
+        common["rope_scaling"] = rope_scaling
+    if kind in ("llama", "mistral"):
+        cfg = (tf.LlamaConfig if kind == "llama" else tf.MistralConfig)(rope_theta=500000.0, **common)
+        model = (tf.LlamaForCausalLM if kind == "llama" else tf.MistralForCausalLM)(cfg)
+    elif kind == "qwen2":
+        model = tf.Qwen2ForCausalLM(tf.Qwen2Config(rope_theta=1000000.0, **common))
+    elif kind == "mixtral":
+        model = tf.MixtralForCausalLM(tf.MixtralConfig(num_local_experts=n_experts or 4, num_experts_per_tok=2,
+                                                       rope_theta=1000000.0, **common))
+    else:
+        raise ValueError(kind)
+    with torch.no_grad():  # larger-than-default weights so the logits are not all near zero
+        for n, p in model.named_parameters():
+            if p.dim() >= 2:
+                p.normal_(0.0, 0.08)
+            elif "norm" in n:
+                p.copy_(1.0 + 0.1 * torch.randn_like(p))
+            else:
+                p.normal_(0.0, 0.05)
+    model = model.to(getattr(torch, dtype))
+    os.makedirs(out_dir, exist_ok=True)
+    model.save_pretrained(out_dir, safe_serialization=True)
+    tok = HFTok(models.BPE(vocab=vocab, merges=[tuple(m.split(" ", 1)) for m in a["merges"]], ignore_merges=True))
+    tok.pre_tokenizer = pre_tokenizers.Sequence([pre_tokenizers.Split(Regex(LLAMA3_PAT), behavior="isolated"),
+                                                 pre_tokenizers.ByteLevel(add_prefix_space=False, use_regex=False)])
+    tok.decoder = decoders.ByteLevel()
+    from tokenizers import AddedToken
+    tok.add_special_tokens([AddedToken(s, special=True, normalized=False) for s in specials])
+    tok.save(os.path.join(out_dir, "tokenizer.json"))
+    with open(os.path.join(out_dir, "tokenizer_config.json"), "w") as f:
+        json.dump({"bos_token": specials[0], "eos_token": specials[9], "add_bos_token": True,
+                   "chat_template": LLAMA3_TEMPLATE, "tokenizer_class": "PreTrainedTokenizerFast"}, f)
+    return out_dir

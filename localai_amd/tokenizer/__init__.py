@@ -48,7 +48,8 @@ def unicode_to_bytes() -> Dict[str, int]:
 class Tokenizer:
     def __init__(self, model: str, tokens: List[str], types: List[int], scores: Optional[List[float]],
                  merges: Optional[List[str]], bos: int, eos: int, add_bos: bool, pre: str = "default",
-                 eot: Optional[int] = None, add_space_prefix: bool = True, chat_template: str = ""):
+                 eot: Optional[int] = None, add_space_prefix: bool = True, chat_template: str = "",
+                 hf_json: str = ""):
         self.model = model
         self.tokens = tokens
         self.types = types or [TOKEN_NORMAL] * len(tokens)
@@ -68,7 +69,12 @@ class Tokenizer:
                                               "<end_of_turn>", "</s>", "<|end|>"):
                 self.eog.add(i)
         self._hf = None
-        if model == "gpt2":
+        if model == "gpt2" and hf_json:
+            # an HF checkpoint's tokenizer.json (models/hf_checkpoint.py): its own pre-tokenizer and
+            # BPE model; specials are split off above, so no post-processor / added-token handling
+            from tokenizers import Tokenizer as HFTok
+            self._hf = HFTok.from_file(hf_json)
+        elif model == "gpt2":
             self._init_bpe(merges or [])
         self.pieces = [self._piece_bytes(i) for i in range(len(tokens))]
         nl = self.encode("\n", add_bos=False)
@@ -92,7 +98,7 @@ class Tokenizer:
         pre = g("tokenizer.ggml.pre", "default")
         asp = bool(g("tokenizer.ggml.add_space_prefix", model == "llama"))
         return cls(model, tokens, types, scores, merges, bos, eos, add_bos, pre, None if eot is None else int(eot),
-                   asp, g("tokenizer.chat_template", "") or "")
+                   asp, g("tokenizer.chat_template", "") or "", g("tokenizer.hf.json", "") or "")
 
     def _init_bpe(self, merges: List[str]):
         from tokenizers import Regex, Tokenizer as HFTok, decoders, models, pre_tokenizers
