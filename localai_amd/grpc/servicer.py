@@ -146,7 +146,9 @@ class EngineServicer:
                     self.state = pb.StatusResponse.READY
                 return pb.Result(success=True, message="Loaded")
             from ..gguf import GGUFReader
-            if os.path.isfile(path) and GGUFReader(path).architecture in ("bert", "nomic-bert"):
+            from ..models.hf_checkpoint import hf_architecture
+            arch = GGUFReader(path).architecture if os.path.isfile(path) else hf_architecture(path)
+            if arch in ("bert", "nomic-bert"):
                 # sentence-embedding encoder (bert-embeddings / sentencetransformers backends)
                 from ..models.bert import BertConfig, BertEmbedder
                 loop = asyncio.get_running_loop()

@@ -22,7 +22,7 @@ import numpy as np
 import torch
 import torch.nn.functional as F
 
-from ..gguf import GGUFReader, dequantize
+from ..gguf import dequantize
 
 SPACE = "▁"
 
@@ -103,7 +103,8 @@ class BertEmbedder:
     def __init__(self, cfg: BertConfig):
         self.cfg = cfg
         self.device = torch.device(cfg.device)
-        r = GGUFReader(cfg.model_path)
+        from .hf_checkpoint import open_model
+        r = open_model(cfg.model_path)  # bert GGUF or an HF BertModel / cross-encoder checkpoint
         kv = r.kv
         a = r.architecture
         self.arch = a

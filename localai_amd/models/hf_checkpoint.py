@@ -30,7 +30,9 @@ import numpy as np
 from ..gguf import GGMLType, GGUFTensor
 
 ARCH_OF = {"LlamaForCausalLM": "llama", "MistralForCausalLM": "llama", "MixtralForCausalLM": "llama",
-           "Qwen2ForCausalLM": "qwen2"}
+           "Qwen2ForCausalLM": "qwen2",
+           # sentence-transformers encoders and cross-encoder rerankers (models/bert.py)
+           "BertModel": "bert", "BertForMaskedLM": "bert", "BertForSequenceClassification": "bert"}
 
 # token types (llama.cpp / GGUF)
 T_NORMAL, T_UNKNOWN, T_CONTROL, T_USER, T_UNUSED, T_BYTE = 1, 2, 3, 4, 5, 6
@@ -39,6 +41,16 @@ T_NORMAL, T_UNKNOWN, T_CONTROL, T_USER, T_UNUSED, T_BYTE = 1, 2, 3, 4, 5, 6
 def is_hf_checkpoint(path: str) -> bool:
     return os.path.isdir(path) and os.path.isfile(os.path.join(path, "config.json")) and bool(
         glob.glob(os.path.join(path, "*.safetensors")))
+
+
+def hf_architecture(path: str) -> str:
+    """Engine architecture name of an HF checkpoint directory ("" when unknown)."""
+    try:
+        with open(os.path.join(path, "config.json")) as f:
+            archs = json.load(f).get("architectures") or []
+    except (OSError, ValueError):
+        return ""
+    return ARCH_OF.get(archs[0], "") if archs else ""
 
 
 def open_model(path: str):
@@ -90,6 +102,9 @@ class HFCheckpointReader:
         self.arch = ARCH_OF[cls]
         self.kv: Dict[str, Any] = {}
         self.tensors: Dict[str, GGUFTensor] = {}
+        if self.arch == "bert":
+            self._bert()
+            return
         self._hparams()
         self._load_tensors()
         self._tokenizer()
@@ -329,3 +344,91 @@ class HFCheckpointReader:
         for i, t in (tcfg.get("added_tokens_decoder") or {}).items():
             out.append({"id": int(i), "content": t.get("content", ""), "special": t.get("special", False)})
         return sorted(out, key=lambda t: t["id"])
+
+    # ---- BERT encoders (sentence-transformers / cross-encoders) ---------------------------
+    def _bert(self):
+        """BertModel / BertForSequenceClassification -> the `bert` layout models/bert.py reads
+        (llama.cpp's bert GGUF names): post-LN encoder, WordPiece vocab with word-initial pieces
+        marked by U+2581 and "##" continuations bare, pooling from sentence-transformers'
+        1_Pooling/config.json (CLS or mean), RANK pooling plus the `cls.*` head for a
+        single-logit sequence classifier (a cross-encoder reranker)."""
+        from safetensors import safe_open
+        c, kv = self.config, self.kv
+        hf: Dict[str, Any] = {}
+        for fn in sorted(glob.glob(os.path.join(self.path, "*.safetensors"))):
+            with safe_open(fn, framework="pt") as f:
+                for k in f.keys():
+                    hf[k[5:] if k.startswith("bert.") else k] = f.get_tensor(k)
+        kv["general.architecture"] = "bert"
+        kv["general.name"] = os.path.basename(os.path.normpath(self.path))
+        kv["bert.context_length"] = int(c.get("max_position_embeddings", 512))
+        kv["bert.embedding_length"] = int(c["hidden_size"])
+        kv["bert.feed_forward_length"] = int(c["intermediate_size"])
+        kv["bert.block_count"] = int(c["num_hidden_layers"])
+        kv["bert.attention.head_count"] = int(c["num_attention_heads"])
+        kv["bert.attention.layer_norm_epsilon"] = float(c.get("layer_norm_eps", 1e-12))
+        kv["bert.attention.causal"] = False
+        ranker = self.hf_class == "BertForSequenceClassification"
+        pool = 1
+        pc = self._json(os.path.join("1_Pooling", "config.json"))
+        if pc.get("pooling_mode_cls_token"):
+            pool = 2
+        kv["bert.pooling_type"] = 4 if ranker else pool
+
+        def put(gname, hname, required=True):
+            t = hf.pop(hname, None)
+            if t is None:
+                if required:
+                    raise KeyError(f"{self.path}: missing tensor {hname}")
+                return
+            arr, ty = self._np(t)
+            self._put(gname, arr, ty)
+        put("token_embd.weight", "embeddings.word_embeddings.weight")
+        put("token_types.weight", "embeddings.token_type_embeddings.weight", required=False)
+        put("position_embd.weight", "embeddings.position_embeddings.weight")
+        put("token_embd_norm.weight", "embeddings.LayerNorm.weight")
+        put("token_embd_norm.bias", "embeddings.LayerNorm.bias")
+        for i in range(int(c["num_hidden_layers"])):
+            p, b = f"encoder.layer.{i}.", f"blk.{i}."
+            for g, h in (("attn_q", "attention.self.query"), ("attn_k", "attention.self.key"),
+                         ("attn_v", "attention.self.value"), ("attn_output", "attention.output.dense"),
+                         ("attn_output_norm", "attention.output.LayerNorm"), ("ffn_up", "intermediate.dense"),
+                         ("ffn_down", "output.dense"), ("layer_output_norm", "output.LayerNorm")):
+                put(b + g + ".weight", p + h + ".weight")
+                put(b + g + ".bias", p + h + ".bias")
+        if ranker:
+            put("cls.weight", "pooler.dense.weight")
+            put("cls.bias", "pooler.dense.bias")
+            put("cls.output.weight", "classifier.weight")
+            put("cls.output.bias", "classifier.bias")
+        # vocabulary: vocab.txt (one piece per line) or tokenizer.json's WordPiece vocab
+        vt = os.path.join(self.path, "vocab.txt")
+        if os.path.isfile(vt):
+            with open(vt, encoding="utf-8") as f:
+                pieces = [ln.rstrip("\n") for ln in f]
+        else:
+            model = (self._json("tokenizer.json").get("model") or {})
+            if model.get("type") != "WordPiece":
+                raise ValueError(f"{self.path}: no vocab.txt and no WordPiece tokenizer.json")
+            voc = model["vocab"]
+            pieces = [""] * (max(voc.values()) + 1)
+            for t, i in voc.items():
+                pieces[i] = t
+        toks, types = [], []
+        for t in pieces:
+            if t.startswith("[") and t.endswith("]"):
+                toks.append(t)
+                types.append(T_CONTROL)
+            elif t.startswith("##"):
+                toks.append(t[2:])
+                types.append(T_NORMAL)
+            else:
+                toks.append("\u2581" + t)
+                types.append(T_NORMAL)
+        kv["tokenizer.ggml.model"] = "bert"
+        kv["tokenizer.ggml.tokens"] = toks
+        kv["tokenizer.ggml.token_type"] = types
+        for key, name in (("unknown_token_id", "[UNK]"), ("cls_token_id", "[CLS]"), ("seperator_token_id", "[SEP]"),
+                          ("padding_token_id", "[PAD]")):
+            if name in toks:
+                kv[f"tokenizer.ggml.{key}"] = toks.index(name)
