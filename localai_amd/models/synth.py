@@ -680,3 +680,33 @@ def write_hf_checkpoint(out_dir: str, kind: str = "llama", n_layer: int = 2, hid
         json.dump({"bos_token": specials[0], "eos_token": specials[9], "add_bos_token": True,
                    "chat_template": LLAMA3_TEMPLATE, "tokenizer_class": "PreTrainedTokenizerFast"}, f)
     return out_dir
+
+
+def write_hf_mamba(out_dir: str, hidden: int = 64, n_layer: int = 2, state: int = 16, seed: int = 0,
+                   dtype: str = "float32") -> str:
+    """Random-init transformers `MambaForCausalLM` directory with this package's byte-level BPE
+    tokenizer (`<|endoftext|>` = eos, the MAMBA_CHAT convention)."""
+    import torch
+    import transformers as tf
+    from tokenizers import AddedToken, Regex, Tokenizer as HFTok, decoders, models, pre_tokenizers
+
+    from ..tokenizer import GPT2_PAT
+    a = _bpe_asset()
+    vocab = {t: i for i, t in enumerate(a["tokens"])}
+    n_vocab = len(vocab) + 1
+    torch.manual_seed(seed)
+    cfg = tf.MambaConfig(vocab_size=n_vocab, hidden_size=hidden, state_size=state, num_hidden_layers=n_layer,
+                         eos_token_id=n_vocab - 1, bos_token_id=n_vocab - 1, pad_token_id=n_vocab - 1)
+    m = tf.MambaForCausalLM(cfg)
+    with torch.no_grad():
+        for n, p in m.named_parameters():
+            if p.dim() >= 2 and "conv1d" not in n:
+                p.normal_(0.0, 0.08)
+    m.to(getattr(torch, dtype)).save_pretrained(out_dir, safe_serialization=True)
+    tok = HFTok(models.BPE(vocab=vocab, merges=[tuple(x.split(" ", 1)) for x in a["merges"]]))
+    tok.pre_tokenizer = pre_tokenizers.Sequence([pre_tokenizers.Split(Regex(GPT2_PAT), behavior="isolated"),
+                                                 pre_tokenizers.ByteLevel(add_prefix_space=False, use_regex=False)])
+    tok.decoder = decoders.ByteLevel()
+    tok.add_special_tokens([AddedToken("<|endoftext|>", special=True)])
+    tok.save(os.path.join(out_dir, "tokenizer.json"))
+    return out_dir

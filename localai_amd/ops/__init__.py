@@ -53,6 +53,8 @@ def lib():
             "la_qgemv_dp4_rope": [I, P, P, P, I, P, I, P, P, P, I, I, I, P, P, P, I, P],
             "la_add_norm": [P, P, LNG, I, P, I, P, P, P, I, I, F, I, P, P],
             "la_rope_kv": [P, LNG, I, P, P, P, P, I, I, I, I, I, I, P, P, P, I, P],
+            "la_mamba_conv_step": [P, P, LNG, P, P, P, I, I, I, P],
+            "la_mamba_ssm_step": [P, P, P, P, LNG, I, I, P, P, P, LNG, P, I, I, I, P],
             "la_act": [P, LNG, I, P, P, I, I, I, P],
             "la_reduce_slabs": [P, LNG, I, P, I, I, P, P, P],
             "la_embed": [I, P, P, P, P, I, I, P, I, P, F, P],
@@ -1345,3 +1347,37 @@ def penalties(logits: torch.Tensor, hist: torch.Tensor, hist_len: torch.Tensor, 
                               hist_len.data_ptr(), pen.data_ptr(), nl_token, _ptr(penalize_nl), _stream()),
            "la_penalties")
     return logits
+
+
+# ---------------------------------------------------------------------------------------
+# Mamba decode step (mamba.hip)
+# ---------------------------------------------------------------------------------------
+
+def mamba_conv_step(conv_state: torch.Tensor, xz: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor],
+                    out: torch.Tensor) -> torch.Tensor:
+    """conv_state [B, I, K] fp32 (rolled in place); xz [B, >=2I] fp32; w [I, K] fp32 -> out [B, I]."""
+    B, I, K = conv_state.shape
+    for t in (conv_state, xz, w, out):
+        assert t.dtype == torch.float32 and t.is_cuda and t.stride(-1) == 1
+    assert conv_state.is_contiguous() and w.shape == (I, K) and out.shape == (B, I) and out.is_contiguous()
+    assert xz.shape[0] == B and xz.shape[1] >= 2 * I and (bias is None or bias.shape == (I,))
+    _check(lib().la_mamba_conv_step(conv_state.data_ptr(), xz.data_ptr(), xz.stride(0), w.data_ptr(),
+                                    None if bias is None else bias.data_ptr(), out.data_ptr(), B, I, K, _stream()),
+           "la_mamba_conv_step")
+    return out
+
+
+def mamba_ssm_step(ssm_state: torch.Tensor, x: torch.Tensor, dt: torch.Tensor, bc: torch.Tensor, off_b: int,
+                   off_c: int, A: torch.Tensor, D: torch.Tensor, xz: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+    """Selective-state update of one token: ssm_state [B, I, N] fp32 (in place), x / dt [B, I],
+    bc [B, *] holding B at off_b and C at off_c, A [I, N] (negative), D [I], z = xz[:, I:2I]."""
+    B, I, N = ssm_state.shape
+    for t in (ssm_state, x, dt, bc, A, D, xz, out):
+        assert t.dtype == torch.float32 and t.is_cuda and t.stride(-1) == 1
+    assert ssm_state.is_contiguous() and x.is_contiguous() and dt.is_contiguous() and out.is_contiguous()
+    assert A.shape == (I, N) and D.shape == (I,) and bc.shape[0] == B and bc.shape[1] >= max(off_b, off_c) + N
+    assert xz.shape[0] == B and xz.shape[1] >= 2 * I
+    _check(lib().la_mamba_ssm_step(ssm_state.data_ptr(), x.data_ptr(), dt.data_ptr(), bc.data_ptr(), bc.stride(0),
+                                   off_b, off_c, A.data_ptr(), D.data_ptr(), xz.data_ptr(), xz.stride(0),
+                                   out.data_ptr(), B, I, N, _stream()), "la_mamba_ssm_step")
+    return out
