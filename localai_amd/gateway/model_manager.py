@@ -34,7 +34,7 @@ log = logging.getLogger("localai_amd.models")
 
 ENGINE_BACKENDS = {"", "llama-cpp", "llama", "llama-cpp-hipblas", "llama-cpp-cuda", "llama-cpp-avx2",
                    "llama-cpp-avx", "llama-cpp-fallback", "llama-cpp-grpc", "llama-ggml", "localai-amd",
-                   "vllm", "transformers",
+                   "vllm", "transformers", "autogptq",  # HF / GPTQ checkpoint directories (hf_checkpoint.py)
                    "whisper"}  # whisper.cpp GGML models run on the native worker (models/whisper.py)
 STORE_BACKEND = "local-store"
 HF_BACKENDS = {"huggingface", "langchain-huggingface"}  # remote Inference API (grpc/huggingface.py)

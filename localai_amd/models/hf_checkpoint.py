@@ -184,6 +184,33 @@ class HFCheckpointReader:
             return t.contiguous().numpy(), GGMLType.F16
         return t.float().contiguous().numpy(), GGMLType.F32
 
+    def _gptq_config(self) -> Optional[dict]:
+        q = self.config.get("quantization_config") or self._json("quantize_config.json")
+        if not q:
+            return None
+        if str(q.get("quant_method", "gptq")).lower() != "gptq":
+            raise ValueError(f"{self.path}: quantization {q.get('quant_method')} is not supported (GPTQ is)")
+        return q
+
+    @staticmethod
+    def _gptq_dequant(qweight, qzeros, scales, g_idx, bits: int, v1_zero_offset: bool):
+        """GPTQ linear -> float weight [N, K] (torch, fp32).  qweight int32 [K*bits/32, N] packs
+        32/bits input rows per word (low bits first); qzeros int32 [G, N*bits/32] packs output
+        columns the same way (AutoGPTQ's v1 format stores zero - 1); scales [G, N]; g_idx [K] maps
+        each input row to its group (act-order checkpoints permute it)."""
+        import torch
+        pack, mask = 32 // bits, (1 << bits) - 1
+        sh = torch.arange(pack, dtype=torch.int32) * bits
+        Kp, N = qweight.shape
+        q = ((qweight.unsqueeze(1) >> sh.view(1, pack, 1)) & mask).reshape(Kp * pack, N)        # [K, N]
+        G = qzeros.shape[0]
+        z = ((qzeros.unsqueeze(2) >> sh.view(1, 1, pack)) & mask).reshape(G, -1)[:, :N]         # [G, N]
+        if v1_zero_offset:
+            z = z + 1
+        gi = g_idx.long()
+        w = (q.float() - z[gi].float()) * scales.float()[gi]                                    # [K, N]
+        return w.t().contiguous()
+
     def _load_tensors(self):
         from safetensors import safe_open
         files = sorted(glob.glob(os.path.join(self.path, "*.safetensors")))
@@ -192,6 +219,23 @@ class HFCheckpointReader:
             with safe_open(fn, framework="pt") as f:
                 for k in f.keys():
                     hf[k] = f.get_tensor(k)
+        gq = self._gptq_config()
+        if gq is not None:
+            import torch
+            bits = int(gq.get("bits", 4))
+            if bits not in (2, 4, 8):
+                raise ValueError(f"{self.path}: GPTQ bits={bits} not supported")
+            gs = int(gq.get("group_size", 128))
+            v1 = str(gq.get("checkpoint_format", "gptq")).lower() != "gptq_v2"
+            for k in [k for k in hf if k.endswith(".qweight")]:
+                base = k[:-len(".qweight")]
+                qw = hf.pop(k)
+                K = qw.shape[0] * (32 // bits)
+                gi = hf.pop(base + ".g_idx", None)
+                if gi is None:  # no act-order: consecutive groups of group_size input rows
+                    gi = torch.arange(K, dtype=torch.int32) // (gs if gs > 0 else K)
+                w = self._gptq_dequant(qw, hf.pop(base + ".qzeros"), hf.pop(base + ".scales"), gi, bits, v1)
+                hf[base + ".weight"] = w.to(torch.float16)  # served on the bf16 paths like any f16 weight
         c = self.config
         n_layer = int(c["num_hidden_layers"])
         llama = self.arch == "llama"

@@ -710,3 +710,65 @@ def write_hf_mamba(out_dir: str, hidden: int = 64, n_layer: int = 2, state: int 
     tok.add_special_tokens([AddedToken("<|endoftext|>", special=True)])
     tok.save(os.path.join(out_dir, "tokenizer.json"))
     return out_dir
+
+
+def gptq_quantize_checkpoint(src_dir: str, out_dir: str, oracle_dir: str, group_size: int = 32, bits: int = 4,
+                             act_order: bool = False, seed: int = 0) -> str:
+    """GPTQ-format copy of an HF checkpoint (every decoder linear as qweight / qzeros / scales /
+    g_idx, AutoGPTQ v1 packing with zero - 1 stored) plus, in `oracle_dir`, the same model with the
+    quantised-then-dequantised float weights -- what a GPTQ loader must reproduce.  Plain
+    round-to-nearest asymmetric quantisation per (group, output column); act_order shuffles which
+    input rows share a group (g_idx), as desc_act checkpoints do."""
+    import shutil
+
+    import torch
+    from safetensors.torch import load_file, save_file
+    rng = np.random.default_rng(seed)
+    sd = load_file(os.path.join(src_dir, "model.safetensors"))
+    pack, qmax = 32 // bits, (1 << bits) - 1
+    out, orc = {}, {}
+    for k, t in sd.items():
+        lin = k.endswith(".weight") and t.dim() == 2 and ".layers." in k and "norm" not in k
+        if not lin:
+            out[k] = t
+            orc[k] = t
+            continue
+        W = t.float().numpy().T.copy()                       # [K, N]
+        K, N = W.shape
+        G = K // group_size
+        order = rng.permutation(K) if act_order else np.arange(K)
+        g_idx = np.empty(K, dtype=np.int32)
+        g_idx[order] = np.arange(K) // group_size           # rows order[j] share group j // group_size
+        scales = np.zeros((G, N), np.float32)
+        zeros = np.zeros((G, N), np.int64)
+        for g in range(G):
+            rows = W[g_idx == g]
+            lo, hi = np.minimum(rows.min(0), 0), np.maximum(rows.max(0), 0)
+            sc = np.maximum((hi - lo) / qmax, 1e-8).astype(np.float16).astype(np.float32)
+            scales[g], zeros[g] = sc, np.clip(np.round(-lo / sc), 0, qmax)
+        q = np.clip(np.round(W / scales[g_idx]) + zeros[g_idx], 0, qmax).astype(np.int64)   # [K, N]
+        deq = (q - zeros[g_idx]) * scales[g_idx]
+        qw = np.zeros((K // pack, N), np.int64)
+        for j in range(pack):
+            qw |= q[j::pack] << (bits * j)
+        zs = zeros - 1                                       # AutoGPTQ v1 stores zero - 1 (as unsigned bits)
+        qz = np.zeros((G, N // pack), np.int64)
+        for j in range(pack):
+            qz |= (zs[:, j::pack] & qmax) << (bits * j)
+        base = k[:-len(".weight")]
+        out[base + ".qweight"] = torch.from_numpy(qw.astype(np.uint32).view(np.int32))
+        out[base + ".qzeros"] = torch.from_numpy(qz.astype(np.uint32).view(np.int32))
+        out[base + ".scales"] = torch.from_numpy(scales.astype(np.float16))
+        out[base + ".g_idx"] = torch.from_numpy(g_idx)
+        orc[k] = torch.from_numpy(deq.T.astype(np.float32)).to(t.dtype)
+    for d, tensors in ((out_dir, out), (oracle_dir, orc)):
+        os.makedirs(d, exist_ok=True)
+        for fn in os.listdir(src_dir):
+            if fn != "model.safetensors":
+                shutil.copy(os.path.join(src_dir, fn), os.path.join(d, fn))
+        save_file({k: v.contiguous() for k, v in tensors.items()}, os.path.join(d, "model.safetensors"),
+                  metadata={"format": "pt"})
+    with open(os.path.join(out_dir, "quantize_config.json"), "w") as f:
+        json.dump({"bits": bits, "group_size": group_size, "desc_act": act_order, "sym": False,
+                   "quant_method": "gptq", "checkpoint_format": "gptq"}, f)
+    return out_dir

@@ -124,3 +124,17 @@ def test_hf_checkpoint_on_gpu(tmp_path, kind):
     top = torch.topk(ref, 2)
     if float(top.values[0] - top.values[1]) > 0.05 * float(ref.abs().max()):
         assert res["text"].startswith(e.tokenizer.decode([int(top.indices[0])]))
+
+
+@pytest.mark.parametrize("act_order", [False, True])
+def test_gptq_checkpoint(tmp_path, act_order):
+    """autogptq backend: a GPTQ checkpoint (4-bit, groups of 32, optionally act-order) loads with
+    the same logits as the float model holding its dequantised weights (transformers oracle)."""
+    src = synth.write_hf_checkpoint(str(tmp_path / "src"), kind="llama", n_layer=2)
+    q = synth.gptq_quantize_checkpoint(src, str(tmp_path / "gptq"), str(tmp_path / "oracle"), act_order=act_order)
+    e = LLMEngine(EngineConfig(model_path=q, device="cpu", context_size=256, max_num_seqs=2, use_graphs=False))
+    ids = e.tokenize(TEXT)
+    ours = e.model.reference_logits(ids).float()
+    ref = _hf_logits(str(tmp_path / "oracle"), ids)
+    err = float((ours - ref).abs().max() / ref.abs().max())
+    assert err < 3e-3, err  # the loader rounds dequantised weights to f16
