@@ -537,6 +537,73 @@ def dequantize(raw: np.ndarray, t: int, shape: Tuple[int, ...]) -> np.ndarray:
                 sv = np.concatenate([np.repeat(s_lo, 16, axis=1), np.repeat(s_hi, 16, axis=1)], axis=1)
                 out[:, 128 * h + base: 128 * h + base + 32] = d[:, None] * sv * qv
         return out.reshape(shape)
+    if t in (GGMLType.Q4_1, GGMLType.Q5_0, GGMLType.Q5_1):
+        # legacy 32-element blocks (ggml-quants.c dequantize_row_q4_1 / q5_0 / q5_1):
+        # fp16 d [, fp16 m] [, u32 high bits], 16 bytes of nibbles (element j low, j + 16 high)
+        nb = GGML_BLOCK[t][1]
+        b = raw.reshape(-1, nb)
+        d = b[:, 0:2].copy().view(np.float16).astype(np.float32)
+        o = 2
+        m = None
+        if t != GGMLType.Q5_0:
+            m = b[:, 2:4].copy().view(np.float16).astype(np.float32)
+            o = 4
+        qs = b[:, -16:].astype(np.int32)
+        lo, hi = qs & 0xF, qs >> 4
+        if t != GGMLType.Q4_1:
+            qh = b[:, o:o + 4].copy().view(np.uint32).astype(np.int64)        # [nb, 1]
+            j = np.arange(16)
+            lo = lo | (((qh >> j) & 1) << 4)
+            hi = hi | (((qh >> (j + 16)) & 1) << 4)
+        q = np.concatenate([lo, hi], axis=1).astype(np.float32)
+        if t == GGMLType.Q5_0:
+            return ((q - 16) * d).reshape(shape)
+        return (q * d + m).reshape(shape)
+    if t == GGMLType.Q2_K:
+        # struct { u8 scales[16]; u8 qs[64]; f16 d; f16 dmin; }: per 128-element half, four 2-bit
+        # planes of 32 bytes; each 16-element run has its own 4-bit scale and 4-bit min
+        b = raw.reshape(-1, 84)
+        sc = b[:, 0:16].astype(np.float32)
+        qs = b[:, 16:80].astype(np.int32)
+        d = b[:, 80:82].copy().view(np.float16).astype(np.float32)
+        dmin = b[:, 82:84].copy().view(np.float16).astype(np.float32)
+        out = np.empty((b.shape[0], 256), dtype=np.float32)
+        for h in range(2):
+            q = qs[:, 32 * h: 32 * h + 32]
+            for j in range(4):
+                for half in range(2):
+                    i = 8 * h + 2 * j + half
+                    s = sc[:, i:i + 1]
+                    v = (q[:, 16 * half: 16 * half + 16] >> (2 * j)) & 3
+                    base = 128 * h + 32 * j + 16 * half
+                    out[:, base: base + 16] = d * (s % 16) * v - dmin * np.floor(s / 16)
+        return out.reshape(shape)
+    if t == GGMLType.Q3_K:
+        # struct { u8 hmask[32]; u8 qs[64]; u8 scales[12]; f16 d; }: 2 low bits in qs, the third
+        # (inverted: set = no -4) in hmask, sixteen 6-bit signed scales packed in 12 bytes
+        b = raw.reshape(-1, 110)
+        hm = b[:, 0:32].astype(np.int32)
+        qs = b[:, 32:96].astype(np.int32)
+        a = b[:, 96:108].copy().view(np.uint32).astype(np.int64)                # [nb, 3]
+        d = b[:, 108:110].copy().view(np.float16).astype(np.float32)
+        k1, k2 = 0x03030303, 0x0F0F0F0F
+        a0, a1, tmp = a[:, 0], a[:, 1], a[:, 2]
+        aux = np.stack([(a0 & k2) | (((tmp >> 0) & k1) << 4), (a1 & k2) | (((tmp >> 2) & k1) << 4),
+                        ((a0 >> 4) & k2) | (((tmp >> 4) & k1) << 4), ((a1 >> 4) & k2) | (((tmp >> 6) & k1) << 4)],
+                       axis=1).astype(np.uint32)
+        scales = aux.view(np.int8).reshape(-1, 16).astype(np.float32) - 32
+        out = np.empty((b.shape[0], 256), dtype=np.float32)
+        for h in range(2):
+            q = qs[:, 32 * h: 32 * h + 32]
+            for j in range(4):
+                bit = 1 << (4 * h + j)
+                for half in range(2):
+                    i = 8 * h + 2 * j + half
+                    sl = slice(16 * half, 16 * half + 16)
+                    v = ((q[:, sl] >> (2 * j)) & 3) - np.where(hm[:, sl] & bit, 0, 4)
+                    base = 128 * h + 32 * j + 16 * half
+                    out[:, base: base + 16] = (d * scales[:, i:i + 1]) * v
+        return out.reshape(shape)
     raise NotImplementedError(f"dequantize {GGMLType(t).name}")
 
 
