@@ -54,9 +54,13 @@ def hf_architecture(path: str) -> str:
 
 
 def open_model(path: str):
-    """GGUF file or HF checkpoint directory -> reader with the GGUFReader interface."""
+    """GGUF file, HF checkpoint directory or pre-GGUF ggjt v3 file -> reader with the GGUFReader
+    interface."""
     if is_hf_checkpoint(path):
         return HFCheckpointReader(path)
+    from .ggml_legacy import GGJTReader, is_ggjt
+    if is_ggjt(path):
+        return GGJTReader(path)
     from ..gguf import GGUFReader
     return GGUFReader(path)
 
