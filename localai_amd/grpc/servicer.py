@@ -147,7 +147,9 @@ class EngineServicer:
                 return pb.Result(success=True, message="Loaded")
             from ..gguf import GGUFReader
             from ..models.hf_checkpoint import hf_architecture
-            arch = GGUFReader(path).architecture if os.path.isfile(path) else hf_architecture(path)
+            from ..models.ggml_legacy import is_ggjt
+            arch = (hf_architecture(path) if not os.path.isfile(path) else "llama" if is_ggjt(path)
+                    else GGUFReader(path).architecture)
             if arch in ("bert", "nomic-bert"):
                 # sentence-embedding encoder (bert-embeddings / sentencetransformers backends)
                 from ..models.bert import BertConfig, BertEmbedder

@@ -37,3 +37,29 @@ def test_ggjt_old_versions_refused(tmp_path):
     p.write_bytes(struct.pack("<II", 0x67676A74, 1) + b"\0" * 64)
     with pytest.raises(ValueError, match="pre-v3"):
         GGJTReader(str(p))
+
+
+def test_llama_ggml_backend_through_gateway(tmp_path):
+    from fastapi.testclient import TestClient
+
+    from localai_amd.config.app_config import ApplicationConfig
+    from localai_amd.config.backend_config import BackendConfig
+    from localai_amd.gateway.app import create_app
+    from localai_amd.gateway.state import AppState
+    mdir = tmp_path / "models"
+    mdir.mkdir()
+    gg = str(tmp_path / "m.gguf")
+    synth.write_model(gg, "tiny-llama", exact=True, tokenizer="mistral", n_vocab=2048)
+    write_ggjt(str(mdir / "old-model.ggmlv3.q8_0.bin"), gg)
+    ac = ApplicationConfig(models_path=str(mdir), upload_dir=str(tmp_path / "up"), config_dir=str(tmp_path / "cfg"),
+                           image_dir=str(tmp_path / "img"), audio_dir=str(tmp_path / "aud"))
+    ac.engine_mode = "inprocess"
+    st = AppState(ac)
+    bc = BackendConfig({"name": "old", "backend": "llama-ggml", "context_size": 256,
+                        "parameters": {"model": "old-model.ggmlv3.q8_0.bin", "temperature": 0}})
+    bc.set_defaults()
+    st.configs.add(bc)
+    with TestClient(create_app(st)) as c:
+        r = c.post("/v1/completions", json={"model": "old", "prompt": "hello", "max_tokens": 3, "ignore_eos": True})
+        assert r.status_code == 200, r.text
+        assert r.json()["usage"]["completion_tokens"] == 3
