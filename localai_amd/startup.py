@@ -44,7 +44,15 @@ def install_models(galleries: List[dict], models_path: str, models: List[str], l
                 name = hashlib.md5(url.encode()).hexdigest()
                 with open(os.path.join(models_path, name + ".yaml"), "wb") as f:
                     f.write(library.resolve_content(url))
-            elif looks_like_url(url) and not url.startswith(("oci://", "ollama://")):
+            elif url.startswith(("oci://", "ollama://")):
+                # model_preload.go:57-78: the image name becomes the file name ("/" and ":" -> "__")
+                name = url.split("://", 1)[1].replace("/", "__").replace(":", "__")
+                verify_path(name, models_path)
+                dst = os.path.join(models_path, name)
+                if not os.path.exists(dst):
+                    download_file(url, dst)
+                log.info("[startup] installed model from OCI repository: %s", name)
+            elif looks_like_url(url):
                 fn = filename_from_url(url)
                 verify_path(fn, models_path)
                 dst = os.path.join(models_path, fn)

@@ -2,13 +2,17 @@
 
 URI schemes: http(s)://, file://, huggingface://owner/repo/file[@branch], github:org/repo/path[@br],
 github://org/repo/path[@br].  Downloads stream to `<dst>.partial`, are SHA-256 checked when a hash
-is given, then renamed atomically.  (OCI/ollama pulls are not supported: no registry client.)
+is given, then renamed atomically.  `oci://` images are unpacked into the model directory and
+`ollama://` models fetched as their model blob (utils/oci.py).  An interrupted http(s) download
+resumes from its `.partial` with a Range request when the server supports it (the reference
+deletes the partial and starts over, `pkg/downloader/uri.go:193-205`).
 """
 from __future__ import annotations
 
 import hashlib
 import os
 import shutil
+import urllib.error
 import urllib.parse
 import urllib.request
 from typing import Callable, Optional
@@ -99,8 +103,10 @@ def read_uri(uri: str, base_path: str = "") -> bytes:
 def download_file(uri: str, dst: str, sha: str = "",
                   progress: Optional[Callable[[str, int, int], None]] = None, auth: str = ""):
     """DownloadFile: skip if present with matching hash; stream to .partial; verify; rename."""
-    if uri.startswith((OCI, OLLAMA)):
-        raise NotImplementedError("OCI/ollama registries are not supported in this build")
+    if uri.startswith(OCI):  # uri.go:226-232: the image's layers go into the model directory
+        from .oci import pull_image
+        pull_image(uri[len(OCI):], os.path.dirname(os.path.abspath(dst)) or ".", progress)
+        return dst
     if os.path.exists(dst):
         if not sha or sha256_file(dst).lower() == sha.lower():
             return dst
@@ -109,23 +115,37 @@ def download_file(uri: str, dst: str, sha: str = "",
     tmp = dst + ".partial"
     if uri.startswith(LOCAL):
         shutil.copyfile(uri[len(LOCAL):], tmp)
+    elif uri.startswith(OLLAMA):
+        from .oci import ollama_fetch_model
+        ollama_fetch_model(uri[len(OLLAMA):], tmp, progress)
     else:
         req = urllib.request.Request(resolve_url(uri))
         if auth:
             req.add_header("Authorization", auth)
         elif os.environ.get("HUGGINGFACE_HUB_TOKEN") and "huggingface.co" in req.full_url:
             req.add_header("Authorization", "Bearer " + os.environ["HUGGINGFACE_HUB_TOKEN"])
-        with urllib.request.urlopen(req, timeout=60) as r, open(tmp, "wb") as f:  # noqa: S310
-            total = int(r.headers.get("Content-Length") or 0)
-            done = 0
-            while True:
-                b = r.read(1 << 22)
-                if not b:
-                    break
-                f.write(b)
-                done += len(b)
-                if progress:
-                    progress(os.path.basename(dst), done, total)
+        have = os.path.getsize(tmp) if os.path.exists(tmp) else 0
+        if have:  # an earlier attempt left a partial: ask for the rest only
+            req.add_header("Range", f"bytes={have}-")
+        try:
+            r = urllib.request.urlopen(req, timeout=60)  # noqa: S310
+        except urllib.error.HTTPError as e:
+            if not (e.code == 416 and have):  # 416: the partial already holds the whole file
+                raise
+            r = None
+        if r is not None:
+            resumed = bool(have) and r.status == 206
+            with r, open(tmp, "ab" if resumed else "wb") as f:
+                done = have if resumed else 0
+                total = int(r.headers.get("Content-Length") or 0) + done
+                while True:
+                    b = r.read(1 << 22)
+                    if not b:
+                        break
+                    f.write(b)
+                    done += len(b)
+                    if progress:
+                        progress(os.path.basename(dst), done, total)
     if sha:
         got = sha256_file(tmp)
         if got.lower() != sha.lower():
