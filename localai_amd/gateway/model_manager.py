@@ -39,6 +39,7 @@ ENGINE_BACKENDS = {"", "llama-cpp", "llama", "llama-cpp-hipblas", "llama-cpp-cud
 STORE_BACKEND = "local-store"
 HF_BACKENDS = {"huggingface", "langchain-huggingface"}  # remote Inference API (grpc/huggingface.py)
 MAMBA_BACKEND = "mamba"  # selective state-space LMs (models/mamba.py, ops/csrc/mamba.hip)
+RWKV_BACKEND = "rwkv"    # RWKV-4 recurrent LMs (models/rwkv.py)
 
 
 def free_port() -> int:
@@ -190,13 +191,13 @@ class ModelManager:
             if not res.success:
                 raise RuntimeError(f"could not load model: {res.message}")
             return LoadedModel(mid, "huggingface", EmbeddedBackend(sv), servicer=sv)
-        if backend == MAMBA_BACKEND:
-            from ..grpc.mamba_servicer import MambaServicer
-            sv = MambaServicer(device=self._pick_device(cfg))
+        if backend in (MAMBA_BACKEND, RWKV_BACKEND):
+            from ..grpc.mamba_servicer import MambaServicer, RwkvServicer
+            sv = (MambaServicer if backend == MAMBA_BACKEND else RwkvServicer)(device=self._pick_device(cfg))
             res = await sv.LoadModel(grpc_model_options(cfg, self.app, self.models_path), None)
             if not res.success:
                 raise RuntimeError(f"could not load model: {res.message}")
-            return LoadedModel(mid, "mamba", EmbeddedBackend(sv), servicer=sv)
+            return LoadedModel(mid, backend, EmbeddedBackend(sv), servicer=sv)
         if backend == STORE_BACKEND:
             from ..grpc.servicer import EngineServicer
             sv = EngineServicer(device=self._pick_device(cfg))

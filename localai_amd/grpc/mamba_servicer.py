@@ -1,9 +1,12 @@
-"""`mamba` backend servicer (backend.proto) over models/mamba.py.
+"""`mamba` and `rwkv` backend servicers (backend.proto) over the recurrent models
+(models/mamba.py, models/rwkv.py).
 
-Mirrors `backend/python/mamba/backend.py`: one request at a time (the reference runs one gRPC
-worker), `Tokens == 0` -> 2000 new tokens, `TopP == 0` -> 0.9, generation stops at the eos token;
-stop strings from the request are honoured here too, and the final streamed Reply carries the
-token counts like the engine's streams.
+Mamba mirrors `backend/python/mamba/backend.py`: one request at a time (the reference runs one
+gRPC worker), `Tokens == 0` -> 2000 new tokens, `TopP == 0` -> 0.9, generation stops at the eos
+token.  RWKV mirrors `backend/go/llm/rwkv/rwkv.go`: stop word "\n" unless the request names stop
+words, tokenizer file from `tokenizer` or `<model>.tokenizer.json`, TokenizeString.  Stop strings
+are honoured with UTF-8 / partial-stop hold-back, and the final streamed Reply carries the token
+counts like the engine's streams.
 """
 from __future__ import annotations
 
@@ -16,6 +19,8 @@ from . import backend_pb as pb
 
 
 class MambaServicer:
+    DEFAULT_STOPS: List[str] = []
+
     def __init__(self, device: str = ""):
         self.device = device
         self.model = None
@@ -28,17 +33,24 @@ class MambaServicer:
     async def Status(self, request, context):
         return pb.StatusResponse(state=self.state)
 
+    def _check(self, path: str) -> bool:
+        from ..models.mamba import is_mamba_checkpoint
+        return is_mamba_checkpoint(path)
+
+    def _build(self, path: str, dev: str, request):
+        from ..models.mamba import MambaLM
+        return MambaLM(path, dev)
+
     async def LoadModel(self, request, context):
-        from ..models.mamba import MambaLM, is_mamba_checkpoint
         path = request.ModelFile or request.Model
-        if not is_mamba_checkpoint(path):
-            return pb.Result(success=False, message=f"not a Mamba checkpoint directory: {path}")
+        if not self._check(path):
+            return pb.Result(success=False, message=f"not a {type(self).__name__[:-9]} checkpoint: {path}")
         dev = self.device
         if not dev:
             import torch
             dev = "cuda:0" if torch.cuda.is_available() else "cpu"
         try:
-            m = await asyncio.get_running_loop().run_in_executor(None, lambda: MambaLM(path, dev))
+            m = await asyncio.get_running_loop().run_in_executor(None, lambda: self._build(path, dev, request))
         except Exception as e:  # noqa: BLE001 - reported to the caller like the reference
             return pb.Result(success=False, message=f"Unexpected {e!r}")
         self.model, self.state = m, pb.StatusResponse.READY
@@ -65,7 +77,7 @@ class MambaServicer:
         max_new = request.Tokens if request.Tokens > 0 else 2000
         top_p = request.TopP if request.TopP > 0 else 0.9
         gen = torch.Generator().manual_seed(request.Seed if request.Seed > 0 else int.from_bytes(os.urandom(4), "little"))
-        stops: List[str] = [s for s in request.StopPrompts if s]
+        stops: List[str] = [s for s in request.StopPrompts if s] or list(self.DEFAULT_STOPS)
         ids = m.tokenize(request.Prompt)
         st = m.new_state(1)
         logits = m.prefill(ids, st)[-1]
@@ -134,3 +146,15 @@ class MambaServicer:
             if text:
                 yield pb.Reply(message=text.encode("utf-8"))
         yield pb.Reply(message=b"", tokens=last[1], prompt_tokens=last[0])
+
+
+class RwkvServicer(MambaServicer):
+    DEFAULT_STOPS = ["\n"]  # rwkv.go:41-44
+
+    def _check(self, path: str) -> bool:
+        from ..models.rwkv import is_rwkv_checkpoint
+        return is_rwkv_checkpoint(path)
+
+    def _build(self, path: str, dev: str, request):
+        from ..models.rwkv import RwkvLM
+        return RwkvLM(path, dev, request.Tokenizer)

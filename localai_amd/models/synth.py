@@ -772,3 +772,37 @@ def gptq_quantize_checkpoint(src_dir: str, out_dir: str, oracle_dir: str, group_
         json.dump({"bits": bits, "group_size": group_size, "desc_act": act_order, "sym": False,
                    "quant_method": "gptq", "checkpoint_format": "gptq"}, f)
     return out_dir
+
+
+def write_hf_rwkv(out_dir: str, hidden: int = 64, n_layer: int = 2, seed: int = 0) -> str:
+    """Random-init transformers `RwkvForCausalLM` (RWKV-4) directory with this package's byte-level
+    BPE tokenizer; rescale_every=0 so eval-mode forwards are not rescaled."""
+    import torch
+    import transformers as tf
+    from tokenizers import Regex, Tokenizer as HFTok, decoders, models, pre_tokenizers
+
+    from ..tokenizer import GPT2_PAT
+    a = _bpe_asset()
+    vocab = {t: i for i, t in enumerate(a["tokens"])}
+    torch.manual_seed(seed)
+    cfg = tf.RwkvConfig(vocab_size=len(vocab), hidden_size=hidden, num_hidden_layers=n_layer,
+                        attention_hidden_size=hidden, intermediate_size=4 * hidden, context_length=256,
+                        rescale_every=0, bos_token_id=0, eos_token_id=0)
+    m = tf.RwkvForCausalLM(cfg)
+    with torch.no_grad():
+        for n, p in m.named_parameters():
+            if p.dim() >= 2:
+                p.normal_(0.0, 0.1)
+            elif "time_decay" in n:
+                p.copy_(torch.randn_like(p) * 0.5 - 1.0)
+            elif "time_first" in n:
+                p.copy_(torch.randn_like(p) * 0.3)
+            elif "time_mix" in n:
+                p.copy_(torch.rand_like(p))
+    m.save_pretrained(out_dir, safe_serialization=True)
+    tok = HFTok(models.BPE(vocab=vocab, merges=[tuple(x.split(" ", 1)) for x in a["merges"]]))
+    tok.pre_tokenizer = pre_tokenizers.Sequence([pre_tokenizers.Split(Regex(GPT2_PAT), behavior="isolated"),
+                                                 pre_tokenizers.ByteLevel(add_prefix_space=False, use_regex=False)])
+    tok.decoder = decoders.ByteLevel()
+    tok.save(os.path.join(out_dir, "tokenizer.json"))
+    return out_dir
