@@ -450,16 +450,17 @@ class DecoderModel:
         flat_e = idx_l.reshape(-1)
         flat_t = torch.arange(T, device=xn.device).repeat_interleave(hp.n_expert_used)
         flat_w = w.reshape(-1)
-        for e, (gate_up, down) in enumerate(L.experts):
-            sel = (flat_e == e).nonzero(as_tuple=True)[0]
-            if sel.numel() == 0:
-                continue
-            rows = flat_t[sel]
-            xe = xn.index_select(0, rows).contiguous()
-            gu = ops.linear_multi(xe, gate_up)
-            h = ops.act(gu, L.F or self.F, ops.ACT_SWIGLU)
-            d = ops.reduce(ops.linear(h, down))
-            out.index_add_(0, rows, d * flat_w[sel].unsqueeze(1))
+        with ops.blas_tuning_paused():  # per-expert M varies every step: never tune those shapes
+            for e, (gate_up, down) in enumerate(L.experts):
+                sel = (flat_e == e).nonzero(as_tuple=True)[0]
+                if sel.numel() == 0:
+                    continue
+                rows = flat_t[sel]
+                xe = xn.index_select(0, rows).contiguous()
+                gu = ops.linear_multi(xe, gate_up)
+                h = ops.act(gu, L.F or self.F, ops.ACT_SWIGLU)
+                d = ops.reduce(ops.linear(h, down))
+                out.index_add_(0, rows, d * flat_w[sel].unsqueeze(1))
         if L.shexp_down is not None:
             out += self._shared_expert(L, xn)
         self.tp.all_reduce(out)

@@ -538,6 +538,31 @@ def blas_tuning_start(path: Optional[str] = None) -> bool:
     return True
 
 
+class blas_tuning_paused:
+    """Context: library GEMMs inside run on already-tuned or default solutions without tuning new
+    shapes.  For GEMMs whose M changes every step (a MoE expert's routed rows during prefill): each
+    new (M, N, K) would otherwise be tuned during warm-up -- hundreds of shapes, minutes of start-up."""
+
+    def __enter__(self):
+        self.prev = False
+        if not torch.cuda.is_available():
+            return self
+        try:
+            import torch.cuda.tunable as tn
+            self.prev = tn.is_enabled() and tn.tuning_is_enabled()
+            if self.prev:
+                tn.tuning_enable(False)
+        except (ImportError, RuntimeError):
+            pass
+        return self
+
+    def __exit__(self, *exc):
+        if self.prev:
+            import torch.cuda.tunable as tn
+            tn.tuning_enable(True)
+        return False
+
+
 def blas_tuning_stop() -> None:
     import torch.cuda.tunable as tn
     tn.tuning_enable(False)   # keep using the tuned solutions, never tune inline while serving
