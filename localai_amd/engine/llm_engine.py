@@ -987,31 +987,34 @@ class LLMEngine:
         (whole-vocabulary scan if none is), and re-run the sampler chain on those -- i.e. the
         sampler's distribution restricted to grammar-valid tokens (llama.cpp resample path)."""
         toks = np.array(toks, copy=True)
-        for j, r in enumerate(reqs):
-            gs = r.grammar
-            if gs is None or r.done:
-                continue
-            t = int(toks[j])
-            if gs.check(t):
-                continue
-            row = logits[j].float()
-            n = min(self.GRAMMAR_TOPN, row.shape[0])
-            vals, idx = torch.topk(row, n)
-            idx_np = idx.cpu().numpy().astype(np.int32)
-            ok = gs.filter(idx_np).astype(bool)
+        need = [j for j, r in enumerate(reqs)
+                if r.grammar is not None and not r.done and not r.grammar.check(int(toks[j]))]
+        if not need:
+            return toks
+        # one batched top-N and one device->host copy for every row the grammar rejected
+        sub = logits[torch.tensor(need, device=logits.device)].float()
+        n = min(self.GRAMMAR_TOPN, sub.shape[1])
+        vals, idx = torch.topk(sub, n, dim=-1)
+        vals_h, idx_h = vals.cpu(), idx.cpu().numpy().astype(np.int32)
+        rows_h = None
+        for k, j in enumerate(need):
+            gs = reqs[j].grammar
+            ok = gs.filter(idx_h[k]).astype(bool)
             if ok.any():
-                cand_ids = idx_np[ok]
-                cand_vals = vals.cpu()[torch.from_numpy(ok)]
+                cand_ids = idx_h[k][ok]
+                cand_vals = vals_h[k][torch.from_numpy(ok)]
             else:
-                mask = gs.mask().astype(bool)
+                mask = gs.mask().astype(bool)  # whole vocabulary (byte-trie walk in the native core)
                 if not mask.any():
                     toks[j] = -1  # nothing can follow: the grammar is complete
                     continue
+                if rows_h is None:
+                    rows_h = sub.cpu()
                 cand_ids = np.nonzero(mask)[0].astype(np.int32)
-                cand_vals = row.cpu()[torch.from_numpy(cand_ids).long()]
-            sub = prm[j:j + 1].copy()
-            k = int(ops.sample_ref(cand_vals.view(1, -1), sub)[0])
-            toks[j] = int(cand_ids[k])
+                cand_vals = rows_h[k][torch.from_numpy(cand_ids).long()]
+            one = prm[j:j + 1].copy()
+            c = int(ops.sample_ref(cand_vals.view(1, -1), one)[0])
+            toks[j] = int(cand_ids[c])
         return toks
 
     def _sample_host_mirostat1(self, logits, reqs):

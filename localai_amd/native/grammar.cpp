@@ -427,12 +427,40 @@ static bool partial_ok(const std::vector<Stack>& stacks, const Utf8& u) {
   return false;
 }
 
+// Byte trie over the vocabulary's token pieces: node 0 is the root; `toks` are the tokens whose
+// piece ends at the node.  The whole-vocabulary mask walks it depth-first, feeding one byte per
+// edge, so a prefix the grammar rejects prunes every token below it at once.
+struct TrieNode {
+  std::vector<std::pair<uint8_t, int>> kids;
+  std::vector<int32_t> toks;
+};
+
 class GrammarVocab {
  public:
   explicit GrammarVocab(std::vector<py::bytes> pieces, std::vector<int32_t> eog) : eog_(eog.begin(), eog.end()) {
     pieces_.reserve(pieces.size());
     for (auto& p : pieces) pieces_.push_back(std::string(p));
+    trie_.emplace_back();
+    for (size_t t = 0; t < pieces_.size(); ++t) {
+      const std::string& b = pieces_[t];
+      if (b.empty() || is_eog((int)t)) continue;
+      int node = 0;
+      for (unsigned char c : b) {
+        int next = -1;
+        for (auto& kv : trie_[node].kids)
+          if (kv.first == c) { next = kv.second; break; }
+        if (next < 0) {
+          next = (int)trie_.size();
+          trie_[node].kids.emplace_back(c, next);
+          trie_.emplace_back();
+        }
+        node = next;
+      }
+      trie_[node].toks.push_back((int32_t)t);
+    }
   }
+  const std::vector<TrieNode>& trie() const { return trie_; }
+  const std::vector<int32_t>& eog_list() const { return eog_; }
   const std::string& piece(int t) const {
     static const std::string empty;
     return (t >= 0 && t < (int)pieces_.size()) ? pieces_[t] : empty;
@@ -443,6 +471,7 @@ class GrammarVocab {
  private:
   std::vector<std::string> pieces_;
   std::vector<int32_t> eog_;
+  std::vector<TrieNode> trie_;
 };
 
 class GrammarState {
@@ -490,14 +519,43 @@ class GrammarState {
     return out;
   }
 
-  // whole-vocabulary mask (slow path)
+  // whole-vocabulary mask: depth-first over the byte trie (same decisions as check() per token)
   py::array_t<uint8_t> mask() const {
+    const size_t V = v_->size();
+    py::array_t<uint8_t> out(V);
+    auto* o = out.mutable_data();
+    py::gil_scoped_release rel;
+    std::fill(o, o + V, 0);
+    const bool end_ok = can_end();
+    for (int32_t t : v_->eog_list())
+      if (t >= 0 && (size_t)t < V) o[t] = end_ok ? 1 : 0;
+    trie_walk(0, stacks_, u_, o);
+    return out;
+  }
+
+  // reference implementation: one check() per token (tests compare the two)
+  py::array_t<uint8_t> mask_linear() const {
     const size_t V = v_->size();
     py::array_t<uint8_t> out(V);
     auto* o = out.mutable_data();
     py::gil_scoped_release rel;
     for (size_t t = 0; t < V; ++t) o[t] = check((int)t) ? 1 : 0;
     return out;
+  }
+
+  void trie_walk(int node, const std::vector<Stack>& stacks, const Utf8& u, uint8_t* o) const {
+    const auto& trie = v_->trie();
+    std::vector<Stack> st, tmp;
+    for (const auto& kv : trie[node].kids) {
+      st = stacks;
+      Utf8 uu = u;
+      const std::string one(1, (char)kv.first);
+      if (!feed_bytes(g_->rules, st, uu, one, tmp)) continue;  // rejected prefix: prune the subtree
+      const TrieNode& child = trie[kv.second];
+      if (!child.toks.empty() && partial_ok(st, uu))
+        for (int32_t t : child.toks) o[t] = 1;
+      if (!child.kids.empty()) trie_walk(kv.second, st, uu, o);
+    }
   }
 
   bool accept(int tok) {
@@ -552,6 +610,7 @@ void register_grammar(py::module& m) {
       .def("check_bytes", &GrammarState::check_piece)
       .def("filter", &GrammarState::filter)
       .def("mask", &GrammarState::mask)
+      .def("mask_linear", &GrammarState::mask_linear)
       .def("accept", &GrammarState::accept)
       .def("accept_bytes", &GrammarState::accept_bytes)
       .def("can_end", &GrammarState::can_end)

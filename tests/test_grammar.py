@@ -76,3 +76,40 @@ def test_engine_constrained_generation(tiny_model_path):
     assert st.accept_bytes(r["text"].encode())
     if r["finish_reason"] == "stop":
         json.loads(r["text"])
+
+
+def test_trie_mask_equals_linear_scan():
+    """The whole-vocabulary mask (depth-first over the vocabulary's byte trie, pruning rejected
+    prefixes) decides every token exactly like one check() per token, at every state of a
+    function-call grammar walk and with a pending partial UTF-8 code point."""
+    import random
+
+    import numpy as np
+
+    import localai_amd.functions as fx
+    from localai_amd.models import synth
+    from localai_amd.tokenizer import unicode_to_bytes
+    a = synth._bpe_asset()
+    u2b = unicode_to_bytes()
+    pieces = []
+    for t in a["tokens"][:6000]:
+        try:
+            pieces.append(bytes(u2b[c] for c in t))
+        except KeyError:
+            pieces.append(t.encode())
+    pieces += ["é".encode()[:1], "é".encode()[1:], "😀".encode()[:2], b"", b"\"", b"{\"", b"\":\""]
+    eog = [len(pieces)]
+    pieces.append(b"")
+    funcs = [{"name": "get_weather", "parameters": {"type": "object", "properties": {
+        "location": {"type": "string"}, "unit": {"type": "string", "enum": ["celsius", "fahrenheit"]},
+        "days": {"type": "integer"}}, "required": ["location", "unit", "days"]}}]
+    g = fx.structure_grammar(fx.to_json_structure(funcs), fx.grammar_options({}))
+    st = core.GrammarState(core.Grammar(g), core.GrammarVocab(pieces, eog))
+    rng = random.Random(0)
+    for step in range(40):
+        m_trie, m_lin = np.asarray(st.mask()), np.asarray(st.mask_linear())
+        assert (m_trie == m_lin).all(), step
+        ok = np.nonzero(m_lin)[0]
+        if len(ok) == 0:
+            break
+        assert st.accept(int(rng.choice(list(ok))))
