@@ -53,9 +53,11 @@ def main():
     eng = LLMEngine(EngineConfig(model_path=txt, device=dev, context_size=4096, max_num_seqs=max(a.concurrency, 1),
                                  max_batched_tokens=8192, mmproj=mm))
     eng.warmup()
-    imgs = [_png(i) for i in range(a.concurrency)]
     best = None
     for w in range(a.waves + 1):
+        # new images every wave: the prefix cache keys image positions by the image's hash, so a
+        # repeated image would skip the vision tower and its prefill
+        imgs = [_png(w * 1000 + i) for i in range(a.concurrency)]
         done, ttft, ntok = [0], [], [0]
         lock = threading.Lock()
         t0 = time.perf_counter()
