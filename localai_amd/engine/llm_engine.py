@@ -145,6 +145,7 @@ class LLMEngine:
         self.gvocab = core.GrammarVocab(self.tokenizer.pieces, sorted(self.tokenizer.eog))
         self._eog_list = sorted(self.tokenizer.eog)
         self._grammars: Dict[str, object] = {}
+        self._mm_embs: Dict[int, list] = {}  # inbox "mm" item -> its images' embeddings (batched encode)
         self.clip = None
         if cfg.mmproj:
             from ..models.clip import ClipVision
@@ -428,8 +429,22 @@ class LLMEngine:
             dist.broadcast_object_list(box, src=0, group=self.ctrl)
             if not self.leader:
                 items = [self._from_wire(w) for w in box[0]]
+        mm = [it for it in items if isinstance(it, tuple) and it[0] == "mm"]
+        if len(mm) > 1 and self.clip is not None:
+            # every image that arrived this step goes through the vision tower in shared batches
+            try:
+                flat = [im for it in mm for im in it[3]]
+                embs = self.clip.embed_images(flat)
+                o = 0
+                for k, it in enumerate(mm):
+                    n = len(it[3])
+                    self._mm_embs[id(it)] = embs[o:o + n]
+                    o += n
+            except Exception:  # a bad image: fall back to per-request encoding (errors per request)
+                self._mm_embs.clear()
         for item in items:
             self._apply(item)
+        self._mm_embs.clear()
 
     @staticmethod
     def _to_wire(item):
@@ -466,7 +481,7 @@ class LLMEngine:
             return
         if isinstance(item, tuple) and item[0] == "mm":
             try:
-                item = self._build_mm_request(*item[1:])
+                item = self._build_mm_request(*item[1:], embs=self._mm_embs.get(id(item)))
             except Exception as e:  # bad image / too long: report to the caller
                 log.exception("multimodal request failed")
                 item[5](Event(finished=True, finish_reason="error", error=f"image processing failed: {e}"))
@@ -498,13 +513,14 @@ class LLMEngine:
 
     IMG_MARK = re.compile(r"\[img-(\d+)\]")
 
-    def _build_mm_request(self, rid, prompt, images, params, callback, sink) -> Request:
+    def _build_mm_request(self, rid, prompt, images, params, callback, sink, embs=None) -> Request:
         """Tokenise around `[img-N]` markers (LocalAI's multimodal template) and splice the
         projected CLIP embeddings of image N in.  Image positions carry placeholder token ids
         above the vocabulary, derived from the image hash so prefix caching never matches two
         different images."""
         V = self.hp.n_vocab
-        embs = [self.clip.embed_image(im) for im in images]
+        if embs is None:
+            embs = self.clip.embed_images(list(images))
         parts = self.IMG_MARK.split(prompt)
         used = {int(parts[i]) for i in range(1, len(parts), 2)}
         seq: List = [("img", i) for i in range(len(embs)) if i not in used]  # unreferenced: up front

@@ -180,8 +180,26 @@ class ClipVision:
 
     def embed_image(self, data) -> torch.Tensor:
         """One image -> [n_tokens, out_dim] f32 rows to splice into the prompt."""
-        tiles, layout = self.preprocess(data)
-        e = self.encode_tiles(tiles)
+        return self.embed_images([data])[0]
+
+    TILE_BATCH = 64  # tiles per vision-tower launch sequence (bounds the attention workspace)
+
+    def embed_images(self, datas) -> List[torch.Tensor]:
+        """Several images (e.g. every request that arrived in one engine step) through the vision
+        tower together: their tiles are concatenated into batches of up to TILE_BATCH, so the ViT's
+        GEMMs run at batch 64 instead of one image's 1-5 tiles at a time."""
+        pre = [self.preprocess(d) for d in datas]
+        tiles = torch.cat([t for t, _ in pre], 0)
+        enc = torch.cat([self.encode_tiles(tiles[i:i + self.TILE_BATCH])
+                         for i in range(0, tiles.shape[0], self.TILE_BATCH)], 0)
+        out, o = [], 0
+        for t, layout in pre:
+            out.append(self._assemble(enc[o:o + t.shape[0]], layout))
+            o += t.shape[0]
+        return out
+
+    def _assemble(self, e: torch.Tensor, layout) -> torch.Tensor:
+        """Encoded tiles of one image -> its prompt rows (anyres: base tile, unpadded grid, newlines)."""
         if layout is None:
             return e[0]
         gw, gh, ow, oh = layout

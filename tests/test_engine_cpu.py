@@ -335,3 +335,37 @@ def test_prefill_tuning_step_packs_one_full_chunk(tiny_model_path):
     assert not e.requests and e.metrics == before
     out = e.generate("hello", SamplingParams(max_tokens=3, temperature=0.0))
     assert out["completion_tokens"] == 3
+
+
+def test_batched_vision_tower_matches_single(tiny_model_path, tmp_path):
+    """Images of requests arriving in one step share vision-tower batches; embeddings equal the
+    one-image-at-a-time path, also across anyres layouts with different tile counts."""
+    from localai_amd.gguf import GGUFReader
+    from localai_amd.models.clip import ClipVision
+    n_embd = int(GGUFReader(tiny_model_path).kv["llama.embedding_length"])
+    mm = synth.write_mmproj(str(tmp_path / "mm16.gguf"), out_dim=n_embd, dim=64, n_layer=1, heads=4, ffn=128,
+                            image_size=28, patch=14, pinpoints=[28, 56, 56, 28, 56, 56])
+    cv = ClipVision(mm, torch.device("cpu"))
+    cv.TILE_BATCH = 3  # force several tower launches across image boundaries
+    imgs = [_png((10, 20, 30), size=50), _png((200, 10, 10), size=20), _png((5, 99, 7), size=70)]
+    batched = cv.embed_images(imgs)
+    for im, b in zip(imgs, batched):
+        single = cv.embed_image(im)
+        assert b.shape == single.shape and torch.allclose(b, single, atol=1e-5)
+    e = _engine(tiny_model_path, mmproj=mm)
+    got = {}
+
+    def cb_for(i):
+        def cb(ev):
+            if ev.finished:
+                got[i] = (ev.prompt_tokens, ev.completion_tokens, ev.error)
+        return cb
+    for i, im in enumerate(imgs):  # all queued before the next step: one batched encode
+        e.add_request(f"[img-0]request {i}", SamplingParams(max_tokens=2, temperature=0.0, ignore_eos=True),
+                      cb_for(i), images=[im])
+    while len(got) < 3:
+        e.step()
+    for i, im in enumerate(imgs):
+        n_img = cv.embed_image(im).shape[0]
+        assert got[i][2] == "" and got[i][1] == 2
+        assert got[i][0] == n_img + len(e.tokenize(f"request {i}"))
