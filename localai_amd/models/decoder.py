@@ -31,6 +31,8 @@ from .hparams import HParams
 
 # batch-1/2 decode: q|k|v GEMV with RoPE + KV append in its epilogue (ops.qkv_rope_dp4)
 FUSED_QKV_ROPE = os.environ.get("LOCALAI_AMD_QKV_ROPE", "1") == "1"
+# MoE decode batches route with the fused router kernel (moe.hip); =1 falls back to the torch ops
+FUSED_ROUTER_OFF = os.environ.get("LOCALAI_AMD_FUSED_ROUTER_OFF", "0") == "1"
 
 _ACT = {"swiglu": ops.ACT_SWIGLU, "gelu": ops.ACT_GELU, "geglu": ops.ACT_GEGLU}
 
@@ -421,13 +423,26 @@ class DecoderModel:
         quantised GEMMs on the routed rows (K17), weighted scatter-add."""
         hp = self.hp
         T = xn.shape[0]
+        El, base = self.E_local, self.ep_base
+        if L.moe_gu is not None and T <= 64 and xn.is_cuda and not FUSED_ROUTER_OFF:
+            # decode batches: one fused router launch (softmax, top-k, renorm, EP remap) feeds the
+            # grouped expert GEMMs; no host round trip anywhere (graph-capturable)
+            k = hp.n_expert_used
+            ids, wts = ops.moe_router(xn, L.router, k, hp.moe_renorm, hp.expert_weights_scale,
+                                      base if self.ep else 0, El if self.ep else 0)
+            order, off = ops.moe_route(ids, El + 1 if self.ep else El)
+            gu = ops.moe_linear(xn, L.moe_gu, order, off, k, T)
+            h = ops.act(gu, L.F or self.F, ops.ACT_SWIGLU)
+            d = ops.moe_linear(h, L.moe_down, order, off, k, T, down=True, wts=wts, zero=self.ep)
+            if L.shexp_down is not None:
+                d = ops.Partial((ops.reduce(d) + self._shared_expert(L, xn)).unsqueeze(0))
+            return self._row_parallel_out(d, None)
         logits = xn.float() @ L.router.t()                       # [T, E]
         w, idx = torch.topk(torch.softmax(logits, -1), hp.n_expert_used, -1)
         if hp.moe_renorm:
             w = w / w.sum(-1, keepdim=True)
         if hp.expert_weights_scale != 1.0:
             w = w * hp.expert_weights_scale
-        El, base = self.E_local, self.ep_base
         if self.ep:
             # expert ids of this rank -> 0..El-1; tokens' other picks -> El (a group nobody runs)
             loc = idx - base

@@ -66,6 +66,7 @@ def lib():
             "la_sample_row_bytes": [],
             "la_logit_bias": [P, LNG, P, P, P, P, I, P],
             "la_moe_route": [P, I, I, I, P, P, P],
+            "la_moe_router": [P, I, P, I, I, I, I, I, F, I, I, P, P, P],
             "la_moe_gemm": [I, I, P, I, I, I, P, P, I, P, I, I, I, P, P, I, LNG, I, P],
             "la_qw_size": [],
             "la_decode_advance": [P, P, P, P, P, P, I, I, I, P, I, P, P, P],
@@ -1277,6 +1278,33 @@ class MoEWeights:
                 qw[e]["p"] = [_ptr(p) or 0 for p in w.planes]
                 qw[e]["N"], qw[e]["K"] = w.N, w.K
             self.desc = torch.from_numpy(qw.view(np.uint8).copy()).to(dev)
+
+
+def moe_router(xn: torch.Tensor, router: torch.Tensor, topk: int, renorm: bool, scale: float = 1.0,
+               ep_base: int = 0, ep_local: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Fused router for decode batches: xn [T, D] bf16, router [E, D] fp32 -> (ids [T, topk] int32,
+    weights [T*topk] fp32): softmax over E, top-k by probability, optional renormalisation and
+    scale; under expert parallelism ids are local (ep_base..ep_base+ep_local-1 -> 0..) and other
+    ranks' experts map to ep_local."""
+    T, D = xn.shape
+    E = router.shape[0]
+    local = ep_local or E
+    if not xn.is_cuda:
+        p = torch.softmax(xn.float() @ router.t(), -1)
+        w, idx = torch.topk(p, topk, -1)
+        if renorm:
+            w = w / w.sum(-1, keepdim=True)
+        loc = idx - ep_base
+        ids = torch.where((loc >= 0) & (loc < local), loc, torch.full_like(loc, local)).to(torch.int32)
+        return ids, (w * scale).reshape(-1).float()
+    assert xn.dtype == torch.bfloat16 and xn.stride(-1) == 1 and router.dtype == torch.float32
+    assert router.is_contiguous() and router.shape[1] == D and D % 8 == 0 and E <= 256 and topk <= min(16, E)
+    ids = torch.empty(T, topk, dtype=torch.int32, device=xn.device)
+    wts = torch.empty(T * topk, dtype=torch.float32, device=xn.device)
+    _check(lib().la_moe_router(xn.data_ptr(), xn.stride(0), router.data_ptr(), E, D, T, topk, int(renorm),
+                               float(scale), ep_base, local, ids.data_ptr(), wts.data_ptr(), _stream()),
+           "la_moe_router")
+    return ids, wts
 
 
 def moe_route(ids: torch.Tensor, E: int, order: Optional[torch.Tensor] = None, off: Optional[torch.Tensor] = None):

@@ -42,6 +42,68 @@ __global__ __launch_bounds__(256) void moe_route_kernel(const int* __restrict__ 
   }
 }
 
+// Fused router for decode-sized batches: one workgroup per token.  Each wave takes experts
+// e = wave, wave + 4, ...: a 64-lane dot of the token's bf16 hidden row with the fp32 router row
+// (shuffle reduction), logits into LDS; then one lane does softmax over E, top-k by probability
+// (lowest id first on ties), optional renormalisation and scale, and writes the expert ids --
+// remapped to this rank's local ids under expert parallelism (others -> E_local) -- and weights.
+// Replaces the router GEMM, softmax, top-k sort, renorm and dtype-copy launches (about ten small
+// kernels per MoE layer at batch 1).
+__global__ __launch_bounds__(256) void moe_router_kernel(const bf16* __restrict__ x, int ldx,
+                                                         const float* __restrict__ wr, int E, int D, int topk,
+                                                         int renorm, float scale, int ep_base, int ep_local,
+                                                         int* __restrict__ ids, float* __restrict__ wts) {
+  __shared__ float lg[256];
+  const int t = blockIdx.x;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const bf16* xr = x + (size_t)t * ldx;
+  for (int e = wave; e < E; e += 4) {
+    const float* w = wr + (size_t)e * D;
+    float acc = 0.0f;
+    for (int i = lane * 8; i < D; i += 64 * 8) {
+      const bf16x8 xv = *(const bf16x8*)(xr + i);
+      const float4 w0 = *(const float4*)(w + i), w1 = *(const float4*)(w + i + 4);
+      acc += bf2f(xv[0]) * w0.x + bf2f(xv[1]) * w0.y + bf2f(xv[2]) * w0.z + bf2f(xv[3]) * w0.w +
+             bf2f(xv[4]) * w1.x + bf2f(xv[5]) * w1.y + bf2f(xv[6]) * w1.z + bf2f(xv[7]) * w1.w;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    if (lane == 0) lg[e] = acc;
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  float mx = -INFINITY;
+  for (int e = 0; e < E; ++e) mx = fmaxf(mx, lg[e]);
+  float z = 0.0f;
+  for (int e = 0; e < E; ++e) {
+    lg[e] = __expf(lg[e] - mx);
+    z += lg[e];
+  }
+  const float inv = 1.0f / z;
+  unsigned long long taken[4] = {0ull, 0ull, 0ull, 0ull};  // E <= 256
+  float sel[16];
+  int sid[16];
+  float sum = 0.0f;
+  for (int k = 0; k < topk; ++k) {
+    int best = -1;
+    float bv = -1.0f;
+    for (int e = 0; e < E; ++e) {
+      if ((taken[e >> 6] >> (e & 63)) & 1ull) continue;
+      if (lg[e] > bv) { bv = lg[e]; best = e; }
+    }
+    taken[best >> 6] |= 1ull << (best & 63);
+    sid[k] = best;
+    sel[k] = bv * inv;
+    sum += sel[k];
+  }
+  for (int k = 0; k < topk; ++k) {
+    const float wv = (renorm ? sel[k] / sum : sel[k]) * scale;
+    const int loc = sid[k] - ep_base;
+    ids[t * topk + k] = (loc >= 0 && loc < ep_local) ? loc : ep_local;
+    wts[t * topk + k] = wv;
+  }
+}
+
 template <int FMT, int MT, bool DOWN>
 __global__ __launch_bounds__(MOE_THREADS, 2) void moe_gemm_kernel(
     const QW* __restrict__ qws, const int* __restrict__ order, const int* __restrict__ off, int topk,
@@ -164,6 +226,14 @@ static void launch_moe(const QW* qws, int N, int K, int E, const int* order, con
 }
 
 }  // namespace la
+
+extern "C" int la_moe_router(const void* x, int ldx, const float* wr, int E, int D, int T, int topk, int renorm,
+                             float scale, int ep_base, int ep_local, int* ids, float* wts, void* stream) {
+  if (E < 1 || E > 256 || topk < 1 || topk > 16 || topk > E || (D & 7) || T < 1) return -1;
+  hipLaunchKernelGGL(la::moe_router_kernel, dim3(T), dim3(256), 0, (hipStream_t)stream, (const bf16*)x, ldx,
+                     wr, E, D, topk, renorm, scale, ep_base, ep_local, ids, wts);
+  return (int)hipGetLastError();
+}
 
 extern "C" int la_moe_route(const int* ids, int T, int topk, int E, int* order, int* off, void* stream) {
   if (E > 256 || E < 1) return -1;

@@ -695,3 +695,33 @@ def test_gemv_dp4_q8_0_mixed_groups_and_rope(M):
     tol = 3e-2 * max(1.0, qr.float().abs().max().item())
     assert (q.float() - qr.float()).abs().max().item() < tol
     assert (kc.float() - kr.float()).abs().max().item() < tol and (vc.float() - vr.float()).abs().max().item() < tol
+
+
+@pytest.mark.parametrize("E,k,renorm,scale,ep", [(8, 2, True, 1.0, None), (60, 4, False, 1.0, None),
+                                                 (64, 6, False, 16.0, None), (8, 2, True, 1.0, (4, 4))])
+def test_moe_router_fused(E, k, renorm, scale, ep):
+    """Fused decode router (moe.hip) vs softmax / top-k / renorm / scale / EP remap in fp32 torch."""
+    torch.manual_seed(E + k)
+    T, D = 5, 4096
+    xn = (torch.randn(T, D, device="cuda") * 0.5).to(torch.bfloat16)
+    router = torch.randn(E, D, device="cuda") * 0.05
+    base, local = ep if ep else (0, 0)
+    ids, wts = ops.moe_router(xn, router, k, renorm, scale, base, local)
+    torch.cuda.synchronize()
+    p = torch.softmax(xn.float() @ router.t(), -1)
+    w_ref, i_ref = torch.topk(p, k, -1)
+    if renorm:
+        w_ref = w_ref / w_ref.sum(-1, keepdim=True)
+    w_ref = w_ref * scale
+    L = local or E
+    loc = i_ref - base
+    i_ref = torch.where((loc >= 0) & (loc < L), loc, torch.full_like(loc, L))
+    gap = (torch.sort(p, -1, descending=True).values[:, k - 1] - torch.sort(p, -1, descending=True).values[:, k])
+    for t in range(T):
+        if float(gap[t]) < 1e-4:
+            continue  # a near-tie at the k-th expert may resolve either way
+        assert sorted(ids[t].tolist()) == sorted(i_ref[t].tolist())
+        got = dict(zip(ids[t].tolist(), wts.view(T, k)[t].tolist()))
+        for e, wv in zip(i_ref[t].tolist(), w_ref[t].tolist()):
+            if e != L:  # remote experts' weights are not compared (their rows are skipped)
+                assert abs(got[e] - wv) < 1e-4 * max(1.0, scale)
