@@ -13,7 +13,7 @@ from .. import __version__
 from ..config.backend_config import BackendConfig
 from ..grpc import backend_pb as pb
 from .metrics import CONTENT_TYPE
-from .model_manager import ENGINE_BACKENDS, HF_BACKENDS, MAMBA_BACKEND, RWKV_BACKEND, STORE_BACKEND
+from .model_manager import ENGINE_BACKENDS, HF_BACKENDS, MAMBA_BACKEND, RWKV_BACKEND, SD_BACKENDS, STORE_BACKEND
 from .openai_routes import APIError, merge_request_with_config, model_from_context, read_request
 
 
@@ -32,7 +32,8 @@ def build_router(state) -> APIRouter:
     r.add_api_route("/version", version, methods=["GET"])
 
     async def system():
-        backends = sorted(set(b for b in ENGINE_BACKENDS if b) | HF_BACKENDS | {MAMBA_BACKEND, RWKV_BACKEND}) + \
+        backends = sorted(set(b for b in ENGINE_BACKENDS if b) | HF_BACKENDS | SD_BACKENDS |
+                          {MAMBA_BACKEND, RWKV_BACKEND}) + \
             [STORE_BACKEND] + list(state.cfg.external_grpc_backends)
         from ..utils.sysinfo import system_info
         return {"backends": backends, "loaded_models": [{"id": m.id} for m in state.manager.list_loaded()],

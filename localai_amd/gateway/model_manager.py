@@ -40,6 +40,7 @@ STORE_BACKEND = "local-store"
 HF_BACKENDS = {"huggingface", "langchain-huggingface"}  # remote Inference API (grpc/huggingface.py)
 MAMBA_BACKEND = "mamba"  # selective state-space LMs (models/mamba.py, ops/csrc/mamba.hip)
 RWKV_BACKEND = "rwkv"    # RWKV-4 recurrent LMs (models/rwkv.py)
+SD_BACKENDS = {"diffusers", "stablediffusion"}  # Stable Diffusion 1.x / 2.x pipelines (models/sd.py)
 
 
 def free_port() -> int:
@@ -194,6 +195,13 @@ class ModelManager:
         if backend in (MAMBA_BACKEND, RWKV_BACKEND):
             from ..grpc.mamba_servicer import MambaServicer, RwkvServicer
             sv = (MambaServicer if backend == MAMBA_BACKEND else RwkvServicer)(device=self._pick_device(cfg))
+            res = await sv.LoadModel(grpc_model_options(cfg, self.app, self.models_path), None)
+            if not res.success:
+                raise RuntimeError(f"could not load model: {res.message}")
+            return LoadedModel(mid, backend, EmbeddedBackend(sv), servicer=sv)
+        if backend in SD_BACKENDS:
+            from ..grpc.diffusers_servicer import DiffusersServicer
+            sv = DiffusersServicer(device=self._pick_device(cfg))
             res = await sv.LoadModel(grpc_model_options(cfg, self.app, self.models_path), None)
             if not res.success:
                 raise RuntimeError(f"could not load model: {res.message}")

@@ -1,0 +1,75 @@
+"""`diffusers` / `stablediffusion` backend servicer (backend.proto LoadModel + GenerateImage) over
+the native Stable Diffusion pipeline (models/sd.py).
+
+Mirrors `backend/python/diffusers/backend.py`: LoadModel keeps `CFGScale` (7 when unset),
+`CLIPSkip` and `SchedulerType`; GenerateImage uses `step` (1 when unset), width / height,
+`negative_prompt`, seeds its generator when `seed > 0`, and honours `EnableParameters` (a comma
+list naming which of negative_prompt / width / height / num_inference_steps reach the pipeline,
+"none" for none of them -- the rest take the pipeline defaults: sample_size * 8 pixels, 50 steps).
+One image at a time (the reference runs one gRPC worker per backend).
+"""
+from __future__ import annotations
+
+import asyncio
+import threading
+
+from . import backend_pb as pb
+
+
+class DiffusersServicer:
+    def __init__(self, device: str = ""):
+        self.device = device
+        self.pipe = None
+        self.cfg_scale = 7.0
+        self.state = pb.StatusResponse.UNINITIALIZED
+        self._lock = threading.Lock()
+
+    async def Health(self, request, context=None):
+        return pb.Reply(message=b"OK")
+
+    async def Status(self, request, context=None):
+        return pb.StatusResponse(state=self.state)
+
+    async def LoadModel(self, request, context=None):
+        from ..models.sd import StableDiffusion, is_sd_pipeline
+        path = request.ModelFile or request.Model
+        if not is_sd_pipeline(path):
+            return pb.Result(success=False, message=f"not a diffusers pipeline directory: {path}")
+        dev = self.device
+        if not dev:
+            import torch
+            dev = "cuda:0" if torch.cuda.is_available() else "cpu"
+        try:
+            p = await asyncio.get_running_loop().run_in_executor(
+                None, lambda: StableDiffusion(path, dev, request.SchedulerType, int(request.CLIPSkip or 0)))
+        except Exception as e:  # noqa: BLE001 - reported to the caller like the reference
+            return pb.Result(success=False, message=f"Unexpected {e!r}")
+        self.pipe, self.state = p, pb.StatusResponse.READY
+        self.cfg_scale = float(request.CFGScale) if request.CFGScale else 7.0
+        return pb.Result(success=True, message="Model loaded successfully")
+
+    def shutdown(self):
+        self.pipe, self.state = None, pb.StatusResponse.UNINITIALIZED
+
+    def _generate(self, request):
+        p = self.pipe
+        if p is None:
+            raise RuntimeError("no model loaded")
+        default_px = p.unet_sample_size * p.vae_scale
+        options = {"negative_prompt": request.negative_prompt, "width": request.width, "height": request.height,
+                   "num_inference_steps": request.step if request.step else 1}
+        keys = list(options)
+        if request.EnableParameters:
+            keys = [] if request.EnableParameters == "none" else [k.strip() for k in request.EnableParameters.split(",")]
+        kw = {k: options[k] for k in keys if k in options}
+        w = int(kw.get("width") or default_px)
+        h = int(kw.get("height") or default_px)
+        with self._lock:
+            img = p(request.positive_prompt, kw.get("negative_prompt", ""), w, h,
+                    steps=int(kw.get("num_inference_steps", 50)), guidance_scale=self.cfg_scale,
+                    seed=request.seed if request.seed > 0 else None)
+            p.save(img, request.dst)
+
+    async def GenerateImage(self, request, context=None):
+        await asyncio.get_running_loop().run_in_executor(None, self._generate, request)
+        return pb.Result(message="Media generated", success=True)

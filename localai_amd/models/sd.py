@@ -1,0 +1,494 @@
+"""Stable Diffusion 1.x / 2.x text-to-image, served by the `diffusers` / `stablediffusion`
+backends (reference: `backend/python/diffusers/backend.py:147-471` -- LoadModel keeps
+`CFGScale` (default 7), `CLIPSkip`, `SchedulerType`; GenerateImage takes `step` (default 1),
+width / height, `negative_prompt`, `seed` and `EnableParameters`, runs the pipeline and saves a
+PNG to `dst`).
+
+Reads the diffusers directory layout (`model_index.json`, `unet/`, `vae/`, `text_encoder/`,
+`tokenizer/`, `scheduler/`, each with `config.json` + safetensors).  The modules below are named
+like the checkpoint's tensors so `load_state_dict(strict=True)` checks every weight:
+
+* CLIP text encoder (pre-LN transformer, causal mask, quick-GELU / GELU, optional clip-skip);
+* UNet2DConditionModel: sinusoidal timestep embedding, ResNet blocks with time conditioning,
+  Transformer2D blocks (self-attention, cross-attention to the prompt, GEGLU feed-forward),
+  stride-2 downsamplers, nearest-2x upsamplers, skip concatenation;
+* AutoencoderKL decoder (post-quant conv, ResNet / single-head attention mid block, upsampling
+  ResNet stacks).
+
+Classifier-free guidance runs conditional and unconditional branches as one batch of 2.  On
+the GPU everything is bf16 (convolutions through MIOpen, attention through PyTorch's fused SDPA,
+the GEMMs through hipBLASLt); the schedulers keep latents in fp32.  Schedulers: DDIM
+(eta 0, "leading" spacing with `steps_offset`) and Euler (discrete, "leading"), the two
+`SchedulerType` values `ddim` / `euler` of backend.py:74-143; anything else falls back to DDIM.
+"""
+from __future__ import annotations
+
+import json
+import math
+import os
+from typing import Dict, List, Optional, Sequence
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+def _cfg(path: str) -> dict:
+    with open(path) as f:
+        return json.load(f)
+
+
+def _load_weights(d: str) -> Dict[str, torch.Tensor]:
+    from safetensors.torch import load_file
+    for n in ("diffusion_pytorch_model.safetensors", "model.safetensors"):
+        p = os.path.join(d, n)
+        if os.path.isfile(p):
+            return load_file(p)
+    for n in ("diffusion_pytorch_model.bin", "pytorch_model.bin"):
+        p = os.path.join(d, n)
+        if os.path.isfile(p):
+            return torch.load(p, map_location="cpu", weights_only=True)
+    raise FileNotFoundError(f"no weights in {d}")
+
+
+def is_sd_pipeline(path: str) -> bool:
+    return os.path.isdir(path) and os.path.isfile(os.path.join(path, "unet", "config.json")) and \
+        os.path.isfile(os.path.join(path, "vae", "config.json"))
+
+
+# ------------------------------------------------------------------ CLIP text encoder
+class _ClipLayer(nn.Module):
+    def __init__(self, d: int, heads: int, inter: int, act: str):
+        super().__init__()
+        self.heads, self.act = heads, act
+        self.layer_norm1, self.layer_norm2 = nn.LayerNorm(d), nn.LayerNorm(d)
+        self.self_attn = nn.Module()
+        for n in ("q_proj", "k_proj", "v_proj", "out_proj"):
+            setattr(self.self_attn, n, nn.Linear(d, d))
+        self.mlp = nn.Module()
+        self.mlp.fc1, self.mlp.fc2 = nn.Linear(d, inter), nn.Linear(inter, d)
+
+    def forward(self, x):
+        B, L, D = x.shape
+        h = self.layer_norm1(x)
+        a = self.self_attn
+        q, k, v = (p(h).view(B, L, self.heads, -1).transpose(1, 2) for p in (a.q_proj, a.k_proj, a.v_proj))
+        o = F.scaled_dot_product_attention(q, k, v, is_causal=True).transpose(1, 2).reshape(B, L, D)
+        x = x + a.out_proj(o)
+        h = self.mlp.fc1(self.layer_norm2(x))
+        h = h * torch.sigmoid(1.702 * h) if self.act == "quick_gelu" else F.gelu(h)
+        return x + self.mlp.fc2(h)
+
+
+class ClipTextEncoder(nn.Module):
+    def __init__(self, c: dict):
+        super().__init__()
+        d = c["hidden_size"]
+        self.eps = float(c.get("layer_norm_eps", 1e-5))
+        self.text_model = nn.Module()
+        tm = self.text_model
+        tm.embeddings = nn.Module()
+        tm.embeddings.token_embedding = nn.Embedding(c["vocab_size"], d)
+        tm.embeddings.position_embedding = nn.Embedding(c["max_position_embeddings"], d)
+        tm.encoder = nn.Module()
+        tm.encoder.layers = nn.ModuleList(_ClipLayer(d, c["num_attention_heads"], c["intermediate_size"],
+                                                     c.get("hidden_act", "quick_gelu"))
+                                          for _ in range(c["num_hidden_layers"]))
+        tm.final_layer_norm = nn.LayerNorm(d)
+        for m in self.modules():
+            if isinstance(m, nn.LayerNorm):
+                m.eps = self.eps
+
+    def forward(self, ids: torch.Tensor, clip_skip: int = 0) -> torch.Tensor:
+        tm = self.text_model
+        x = tm.embeddings.token_embedding(ids) + tm.embeddings.position_embedding.weight[: ids.shape[1]]
+        layers = tm.encoder.layers
+        # diffusers' clip_skip: the hidden state `clip_skip` layers before the last, then final LN
+        for ly in layers[: len(layers) - clip_skip]:
+            x = ly(x)
+        return tm.final_layer_norm(x)
+
+
+# ------------------------------------------------------------------ UNet / VAE building blocks
+class _Resnet(nn.Module):
+    def __init__(self, cin: int, cout: int, groups: int, eps: float, temb: Optional[int]):
+        super().__init__()
+        self.norm1 = nn.GroupNorm(groups, cin, eps=eps)
+        self.conv1 = nn.Conv2d(cin, cout, 3, padding=1)
+        if temb:
+            self.time_emb_proj = nn.Linear(temb, cout)
+        self.norm2 = nn.GroupNorm(groups, cout, eps=eps)
+        self.conv2 = nn.Conv2d(cout, cout, 3, padding=1)
+        if cin != cout:
+            self.conv_shortcut = nn.Conv2d(cin, cout, 1)
+
+    def forward(self, x, temb=None):
+        h = self.conv1(F.silu(self.norm1(x)))
+        if temb is not None:
+            h = h + self.time_emb_proj(F.silu(temb))[:, :, None, None]
+        h = self.conv2(F.silu(self.norm2(h)))
+        return (self.conv_shortcut(x) if hasattr(self, "conv_shortcut") else x) + h
+
+
+class _Attn(nn.Module):
+    def __init__(self, d: int, heads: int, ctx: Optional[int] = None, bias: bool = False):
+        super().__init__()
+        self.heads = heads
+        self.to_q = nn.Linear(d, d, bias=bias)
+        self.to_k = nn.Linear(ctx or d, d, bias=bias)
+        self.to_v = nn.Linear(ctx or d, d, bias=bias)
+        self.to_out = nn.ModuleList([nn.Linear(d, d)])
+
+    def forward(self, x, ctx=None):
+        B, L, D = x.shape
+        c = x if ctx is None else ctx
+        q = self.to_q(x).view(B, L, self.heads, -1).transpose(1, 2)
+        k = self.to_k(c).view(B, c.shape[1], self.heads, -1).transpose(1, 2)
+        v = self.to_v(c).view(B, c.shape[1], self.heads, -1).transpose(1, 2)
+        o = F.scaled_dot_product_attention(q, k, v).transpose(1, 2).reshape(B, L, D)
+        return self.to_out[0](o)
+
+
+class _GEGLU(nn.Module):
+    def __init__(self, d: int, inner: int):
+        super().__init__()
+        self.proj = nn.Linear(d, 2 * inner)
+
+    def forward(self, x):
+        h, g = self.proj(x).chunk(2, dim=-1)
+        return h * F.gelu(g)
+
+
+class _TBlock(nn.Module):
+    def __init__(self, d: int, heads: int, ctx: int):
+        super().__init__()
+        self.norm1, self.norm2, self.norm3 = nn.LayerNorm(d), nn.LayerNorm(d), nn.LayerNorm(d)
+        self.attn1, self.attn2 = _Attn(d, heads), _Attn(d, heads, ctx)
+        self.ff = nn.Module()
+        self.ff.net = nn.ModuleList([_GEGLU(d, 4 * d), nn.Identity(), nn.Linear(4 * d, d)])
+
+    def forward(self, x, ctx):
+        x = x + self.attn1(self.norm1(x))
+        x = x + self.attn2(self.norm2(x), ctx)
+        h = self.ff.net[0](self.norm3(x))
+        return x + self.ff.net[2](h)
+
+
+class _Transformer2D(nn.Module):
+    def __init__(self, c: int, heads: int, ctx: int, groups: int, linear_proj: bool):
+        super().__init__()
+        self.linear = linear_proj
+        self.norm = nn.GroupNorm(groups, c, eps=1e-6)
+        self.proj_in = nn.Linear(c, c) if linear_proj else nn.Conv2d(c, c, 1)
+        self.transformer_blocks = nn.ModuleList([_TBlock(c, heads, ctx)])
+        self.proj_out = nn.Linear(c, c) if linear_proj else nn.Conv2d(c, c, 1)
+
+    def forward(self, x, ctx):
+        B, C, H, W = x.shape
+        h = self.norm(x)
+        if not self.linear:
+            h = self.proj_in(h)
+        h = h.permute(0, 2, 3, 1).reshape(B, H * W, C)
+        if self.linear:
+            h = self.proj_in(h)
+        for b in self.transformer_blocks:
+            h = b(h, ctx)
+        if self.linear:
+            h = self.proj_out(h)
+        h = h.reshape(B, H, W, C).permute(0, 3, 1, 2)
+        if not self.linear:
+            h = self.proj_out(h)
+        return x + h
+
+
+class _Down(nn.Module):
+    def __init__(self, c: int, pad: int = 1):
+        super().__init__()
+        self.pad = pad
+        self.conv = nn.Conv2d(c, c, 3, stride=2, padding=pad)
+
+    def forward(self, x):
+        if self.pad == 0:  # the VAE encoder pads right / bottom only
+            x = F.pad(x, (0, 1, 0, 1))
+        return self.conv(x)
+
+
+class _Up(nn.Module):
+    def __init__(self, c: int):
+        super().__init__()
+        self.conv = nn.Conv2d(c, c, 3, padding=1)
+
+    def forward(self, x):
+        return self.conv(F.interpolate(x, scale_factor=2.0, mode="nearest"))
+
+
+def _per_block(v, n: int) -> List[int]:
+    return list(v) if isinstance(v, (list, tuple)) else [v] * n
+
+
+class UNet(nn.Module):
+    def __init__(self, c: dict):
+        super().__init__()
+        ch = list(c["block_out_channels"])
+        n = len(ch)
+        lpb = int(c.get("layers_per_block", 2))
+        g, eps = int(c.get("norm_num_groups", 32)), float(c.get("norm_eps", 1e-5))
+        ctx = int(c["cross_attention_dim"])
+        # diffusers: `attention_head_dim` holds the number of heads when num_attention_heads is unset
+        heads = _per_block(c.get("num_attention_heads") or c.get("attention_head_dim", 8), n)
+        lin = bool(c.get("use_linear_projection", False))
+        self.flip = bool(c.get("flip_sin_to_cos", True))
+        self.shift = float(c.get("freq_shift", 0))
+        temb = ch[0] * 4
+        self.conv_in = nn.Conv2d(c.get("in_channels", 4), ch[0], 3, padding=1)
+        self.time_embedding = nn.Module()
+        self.time_embedding.linear_1 = nn.Linear(ch[0], temb)
+        self.time_embedding.linear_2 = nn.Linear(temb, temb)
+        downs, prev = [], ch[0]
+        for i, t in enumerate(c["down_block_types"]):
+            b = nn.Module()
+            b.resnets = nn.ModuleList(_Resnet(prev if j == 0 else ch[i], ch[i], g, eps, temb) for j in range(lpb))
+            if "CrossAttn" in t:
+                b.attentions = nn.ModuleList(_Transformer2D(ch[i], heads[i], ctx, g, lin) for _ in range(lpb))
+            if i < n - 1:
+                b.downsamplers = nn.ModuleList([_Down(ch[i])])
+            downs.append(b)
+            prev = ch[i]
+        self.down_blocks = nn.ModuleList(downs)
+        self.mid_block = nn.Module()
+        self.mid_block.resnets = nn.ModuleList([_Resnet(ch[-1], ch[-1], g, eps, temb) for _ in range(2)])
+        self.mid_block.attentions = nn.ModuleList([_Transformer2D(ch[-1], heads[-1], ctx, g, lin)])
+        rch, rheads = ch[::-1], heads[::-1]
+        ups, prev = [], ch[-1]
+        for i, t in enumerate(c["up_block_types"]):
+            out, skip_in = rch[i], rch[min(i + 1, n - 1)]
+            b = nn.Module()
+            b.resnets = nn.ModuleList(
+                _Resnet((prev if j == 0 else out) + (skip_in if j == lpb else out), out, g, eps, temb)
+                for j in range(lpb + 1))
+            if "CrossAttn" in t:
+                b.attentions = nn.ModuleList(_Transformer2D(out, rheads[i], ctx, g, lin) for _ in range(lpb + 1))
+            if i < n - 1:
+                b.upsamplers = nn.ModuleList([_Up(out)])
+            ups.append(b)
+            prev = out
+        self.up_blocks = nn.ModuleList(ups)
+        self.conv_norm_out = nn.GroupNorm(g, ch[0], eps=eps)
+        self.conv_out = nn.Conv2d(ch[0], c.get("out_channels", 4), 3, padding=1)
+        self.ch0 = ch[0]
+
+    def _tproj(self, t: torch.Tensor) -> torch.Tensor:
+        half = self.ch0 // 2
+        f = torch.exp(-math.log(10000) * torch.arange(half, dtype=torch.float32, device=t.device) / (half - self.shift))
+        e = t.float()[:, None] * f[None]
+        e = torch.cat([torch.cos(e), torch.sin(e)] if self.flip else [torch.sin(e), torch.cos(e)], dim=-1)
+        return e
+
+    def forward(self, x, t, ctx):
+        temb = self._tproj(t).to(x.dtype)
+        temb = self.time_embedding.linear_2(F.silu(self.time_embedding.linear_1(temb)))
+        h = self.conv_in(x)
+        skips = [h]
+        for b in self.down_blocks:
+            for j, r in enumerate(b.resnets):
+                h = r(h, temb)
+                if hasattr(b, "attentions"):
+                    h = b.attentions[j](h, ctx)
+                skips.append(h)
+            if hasattr(b, "downsamplers"):
+                h = b.downsamplers[0](h)
+                skips.append(h)
+        m = self.mid_block
+        h = m.attentions[0](m.resnets[0](h, temb), ctx)
+        h = m.resnets[1](h, temb)
+        for b in self.up_blocks:
+            for j, r in enumerate(b.resnets):
+                h = r(torch.cat([h, skips.pop()], dim=1), temb)
+                if hasattr(b, "attentions"):
+                    h = b.attentions[j](h, ctx)
+            if hasattr(b, "upsamplers"):
+                h = b.upsamplers[0](h)
+        return self.conv_out(F.silu(self.conv_norm_out(h)))
+
+
+class _VaeAttn(nn.Module):
+    def __init__(self, c: int, groups: int, eps: float):
+        super().__init__()
+        self.group_norm = nn.GroupNorm(groups, c, eps=eps)
+        self.to_q, self.to_k, self.to_v = nn.Linear(c, c), nn.Linear(c, c), nn.Linear(c, c)
+        self.to_out = nn.ModuleList([nn.Linear(c, c)])
+
+    def forward(self, x):
+        B, C, H, W = x.shape
+        h = self.group_norm(x).reshape(B, C, H * W).transpose(1, 2)
+        q, k, v = (p(h)[:, None] for p in (self.to_q, self.to_k, self.to_v))
+        o = F.scaled_dot_product_attention(q, k, v)[:, 0]
+        return x + self.to_out[0](o).transpose(1, 2).reshape(B, C, H, W)
+
+
+class VaeDecoder(nn.Module):
+    def __init__(self, c: dict):
+        super().__init__()
+        ch = list(c["block_out_channels"])
+        lpb = int(c.get("layers_per_block", 2))
+        g = int(c.get("norm_num_groups", 32))
+        lat = int(c.get("latent_channels", 4))
+        self.scaling = float(c.get("scaling_factor", 0.18215))
+        self.post_quant_conv = nn.Conv2d(lat, lat, 1)
+        d = nn.Module()
+        d.conv_in = nn.Conv2d(lat, ch[-1], 3, padding=1)
+        d.mid_block = nn.Module()
+        d.mid_block.resnets = nn.ModuleList([_Resnet(ch[-1], ch[-1], g, 1e-6, None) for _ in range(2)])
+        d.mid_block.attentions = nn.ModuleList([_VaeAttn(ch[-1], g, 1e-6)])
+        rch, ups, prev = ch[::-1], [], ch[-1]
+        for i in range(len(ch)):
+            b = nn.Module()
+            b.resnets = nn.ModuleList(_Resnet(prev if j == 0 else rch[i], rch[i], g, 1e-6, None) for j in range(lpb + 1))
+            if i < len(ch) - 1:
+                b.upsamplers = nn.ModuleList([_Up(rch[i])])
+            ups.append(b)
+            prev = rch[i]
+        d.up_blocks = nn.ModuleList(ups)
+        d.conv_norm_out = nn.GroupNorm(g, ch[0], eps=1e-6)
+        d.conv_out = nn.Conv2d(ch[0], c.get("out_channels", 3), 3, padding=1)
+        self.decoder = d
+
+    def forward(self, z):
+        d = self.decoder
+        h = d.conv_in(self.post_quant_conv(z / self.scaling))
+        h = d.mid_block.resnets[1](d.mid_block.attentions[0](d.mid_block.resnets[0](h)))
+        for b in d.up_blocks:
+            for r in b.resnets:
+                h = r(h)
+            if hasattr(b, "upsamplers"):
+                h = b.upsamplers[0](h)
+        return d.conv_out(F.silu(d.conv_norm_out(h)))
+
+
+def _vae_names(sd: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
+    """Decoder tensors only; older VAE checkpoints name the attention `query/key/value/proj_attn`
+    and store them as 1x1 convolutions."""
+    ren = {".query.": ".to_q.", ".key.": ".to_k.", ".value.": ".to_v.", ".proj_attn.": ".to_out.0."}
+    out = {}
+    for k, v in sd.items():
+        if not (k.startswith("decoder.") or k.startswith("post_quant_conv.")):
+            continue
+        for a, b in ren.items():
+            k = k.replace(a, b)
+        if ".attentions." in k and k.endswith(".weight") and v.dim() == 4:
+            v = v[:, :, 0, 0]
+        out[k] = v
+    return out
+
+
+# ------------------------------------------------------------------ schedulers
+class Scheduler:
+    """DDIM (eta 0) or Euler-discrete over the scaled-linear beta schedule, "leading" spacing."""
+
+    def __init__(self, c: dict, kind: str = "ddim"):
+        n = int(c.get("num_train_timesteps", 1000))
+        b0, b1 = float(c.get("beta_start", 0.00085)), float(c.get("beta_end", 0.012))
+        if c.get("beta_schedule", "scaled_linear") == "linear":
+            betas = torch.linspace(b0, b1, n, dtype=torch.float64)
+        else:
+            betas = torch.linspace(b0 ** 0.5, b1 ** 0.5, n, dtype=torch.float64) ** 2
+        self.ac = torch.cumprod(1.0 - betas, 0)
+        self.n_train = n
+        self.offset = int(c.get("steps_offset", 1))
+        self.final_ac = 1.0 if c.get("set_alpha_to_one", False) else float(self.ac[0])
+        self.pred = c.get("prediction_type", "epsilon")
+        self.kind = kind if kind in ("ddim", "euler") else "ddim"
+
+    def timesteps(self, steps: int) -> List[int]:
+        r = self.n_train // steps
+        return [i * r + self.offset for i in range(steps)][::-1]
+
+    def init_sigma(self, ts: Sequence[int]) -> float:
+        if self.kind == "euler":
+            a = float(self.ac[ts[0]])
+            return math.sqrt((1 - a) / a + 1)  # x_T = x0 + sigma * eps has variance sigma^2 + 1
+        return 1.0
+
+    def scale_input(self, x: torch.Tensor, t: int) -> torch.Tensor:
+        if self.kind == "euler":
+            a = float(self.ac[t])
+            return x / math.sqrt((1 - a) / a + 1)
+        return x
+
+    def _x0_eps(self, out, x, a):
+        if self.pred == "v_prediction":
+            x0 = math.sqrt(a) * x - math.sqrt(1 - a) * out
+            return x0, math.sqrt(a) * out + math.sqrt(1 - a) * x
+        return (x - math.sqrt(1 - a) * out) / math.sqrt(a), out
+
+    def step(self, out: torch.Tensor, t: int, t_prev: Optional[int], x: torch.Tensor) -> torch.Tensor:
+        a = float(self.ac[t])
+        a_prev = float(self.ac[t_prev]) if t_prev is not None else self.final_ac
+        if self.kind == "euler":
+            # latents carry sigma scaling: x = x0 + sigma * eps, with x0 / eps from the model
+            s, s_prev = math.sqrt((1 - a) / a), (math.sqrt((1 - a_prev) / a_prev) if t_prev is not None else 0.0)
+            x0, eps = self._x0_eps(out, x / math.sqrt(s * s + 1), a)
+            return x0 + s_prev * eps if t_prev is not None else x0
+        x0, eps = self._x0_eps(out, x, a)
+        return math.sqrt(a_prev) * x0 + math.sqrt(1 - a_prev) * eps
+
+
+# ------------------------------------------------------------------ pipeline
+class StableDiffusion:
+    def __init__(self, path: str, device: str = "cpu", scheduler: str = "", clip_skip: int = 0):
+        self.device = torch.device(device)
+        self.dtype = torch.bfloat16 if self.device.type == "cuda" else torch.float32
+        self.clip_skip = clip_skip
+        self.text = ClipTextEncoder(_cfg(os.path.join(path, "text_encoder", "config.json")))
+        # transformers 4 keeps the `text_model.` prefix, transformers 5 drops it
+        self.text.load_state_dict({(k if k.startswith("text_model.") else "text_model." + k): v
+                                   for k, v in _load_weights(os.path.join(path, "text_encoder")).items()
+                                   if "position_ids" not in k}, strict=True)
+        ucfg = _cfg(os.path.join(path, "unet", "config.json"))
+        self.unet_sample_size = int(ucfg.get("sample_size", 64))
+        self.unet = UNet(ucfg)
+        self.unet.load_state_dict(_load_weights(os.path.join(path, "unet")), strict=True)
+        self.vae = VaeDecoder(_cfg(os.path.join(path, "vae", "config.json")))
+        self.vae.load_state_dict(_vae_names(_load_weights(os.path.join(path, "vae"))), strict=True)
+        for m in (self.text, self.unet, self.vae):
+            m.to(self.device, self.dtype).eval().requires_grad_(False)
+        sc = os.path.join(path, "scheduler", "scheduler_config.json")
+        self.sched_cfg = _cfg(sc) if os.path.isfile(sc) else {}
+        self.sched = Scheduler(self.sched_cfg, (scheduler or "ddim").lower())
+        from transformers import CLIPTokenizer
+        self.tok = CLIPTokenizer.from_pretrained(os.path.join(path, "tokenizer"))
+        self.max_len = self.text.text_model.embeddings.position_embedding.weight.shape[0]
+        self.latent_ch = self.unet.conv_in.in_channels
+        self.vae_scale = 2 ** (len(self.vae.decoder.up_blocks) - 1)
+
+    def _encode(self, prompts: List[str]) -> torch.Tensor:
+        ids = self.tok(prompts, padding="max_length", max_length=self.max_len, truncation=True,
+                       return_tensors="pt").input_ids.to(self.device)
+        return self.text(ids, self.clip_skip)
+
+    @torch.inference_mode()
+    def __call__(self, prompt: str, negative_prompt: str = "", width: int = 512, height: int = 512,
+                 steps: int = 1, guidance_scale: float = 7.0, seed: Optional[int] = None) -> torch.Tensor:
+        """-> uint8 image [H, W, 3] on the CPU."""
+        g = torch.Generator().manual_seed(seed if seed is not None else int.from_bytes(os.urandom(4), "little"))
+        h, w = max(1, height // self.vae_scale), max(1, width // self.vae_scale)
+        cfg = guidance_scale > 1.0
+        ctx = self._encode([negative_prompt, prompt] if cfg else [prompt])
+        ts = self.sched.timesteps(max(1, steps))
+        x = torch.randn(1, self.latent_ch, h, w, generator=g).to(self.device) * self.sched.init_sigma(ts)
+        for i, t in enumerate(ts):
+            xin = self.sched.scale_input(x, t)
+            xin = torch.cat([xin, xin]) if cfg else xin
+            tt = torch.full((xin.shape[0],), t, device=self.device)
+            out = self.unet(xin.to(self.dtype), tt, ctx).float()
+            if cfg:
+                u, c = out.chunk(2)
+                out = u + guidance_scale * (c - u)
+            x = self.sched.step(out, t, ts[i + 1] if i + 1 < len(ts) else None, x)
+        img = self.vae(x.to(self.dtype)).float()
+        img = ((img[0] / 2 + 0.5).clamp(0, 1) * 255).round().to(torch.uint8)
+        return img.permute(1, 2, 0).cpu()
+
+    def save(self, img: torch.Tensor, dst: str):
+        from PIL import Image
+        Image.fromarray(img.numpy()).save(dst)

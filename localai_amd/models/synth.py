@@ -806,3 +806,78 @@ def write_hf_rwkv(out_dir: str, hidden: int = 64, n_layer: int = 2, seed: int = 
     tok.decoder = decoders.ByteLevel()
     tok.save(os.path.join(out_dir, "tokenizer.json"))
     return out_dir
+
+
+SD15_UNET = dict(block_out_channels=[320, 640, 1280, 1280], layers_per_block=2, cross_attention_dim=768,
+                 attention_head_dim=8, norm_num_groups=32, in_channels=4, out_channels=4, sample_size=64,
+                 down_block_types=["CrossAttnDownBlock2D"] * 3 + ["DownBlock2D"],
+                 up_block_types=["UpBlock2D"] + ["CrossAttnUpBlock2D"] * 3, flip_sin_to_cos=True, freq_shift=0)
+SD15_VAE = dict(block_out_channels=[128, 256, 512, 512], layers_per_block=2, latent_channels=4, norm_num_groups=32,
+                in_channels=3, out_channels=3, scaling_factor=0.18215)
+SD15_TEXT = dict(hidden_size=768, num_hidden_layers=12, num_attention_heads=12, intermediate_size=3072,
+                 vocab_size=49408, max_position_embeddings=77, hidden_act="quick_gelu")
+
+
+def _clip_byte_vocab():
+    """A byte-level CLIP BPE vocabulary with no merges: every byte, every byte + `</w>`, and the
+    two specials -- enough for transformers' CLIPTokenizer to tokenise any text."""
+    bs = list(range(ord("!"), ord("~") + 1)) + list(range(0xA1, 0xAD)) + list(range(0xAE, 0x100))
+    cs, n = bs[:], 0
+    for b in range(256):
+        if b not in bs:
+            bs.append(b)
+            cs.append(256 + n)
+            n += 1
+    chars = [chr(c) for c in cs]
+    toks = chars + [c + "</w>" for c in chars] + ["<|startoftext|>", "<|endoftext|>"]
+    return {t: i for i, t in enumerate(toks)}
+
+
+def write_sd_pipeline(out_dir: str, size: str = "tiny", seed: int = 0, v_prediction: bool = False) -> str:
+    """Random-init Stable Diffusion pipeline directory in the diffusers layout (model_index.json,
+    unet/, vae/, text_encoder/ (transformers CLIPTextModel), tokenizer/, scheduler/).
+    size="sd15": the SD-1.5 architecture (860M-parameter UNet); "tiny": a two-level toy."""
+    import torch
+    import transformers as tf
+    from safetensors.torch import save_file
+
+    from .sd import UNet, VaeDecoder
+    if size == "sd15":
+        uc, vc, tc = dict(SD15_UNET), dict(SD15_VAE), dict(SD15_TEXT)
+    else:
+        uc = dict(SD15_UNET, block_out_channels=[32, 64], layers_per_block=1, cross_attention_dim=32,
+                  attention_head_dim=[2, 4], norm_num_groups=8, sample_size=8,
+                  down_block_types=["CrossAttnDownBlock2D", "DownBlock2D"],
+                  up_block_types=["UpBlock2D", "CrossAttnUpBlock2D"])
+        vc = dict(SD15_VAE, block_out_channels=[16, 32], layers_per_block=1, norm_num_groups=8)
+        vocab = _clip_byte_vocab()
+        tc = dict(SD15_TEXT, hidden_size=32, num_hidden_layers=2, num_attention_heads=2, intermediate_size=64,
+                  vocab_size=len(vocab), bos_token_id=vocab["<|startoftext|>"], eos_token_id=vocab["<|endoftext|>"],
+                  pad_token_id=vocab["<|endoftext|>"])
+    if v_prediction:
+        uc["use_linear_projection"] = True
+    torch.manual_seed(seed)
+    for sub in ("unet", "vae", "text_encoder", "tokenizer", "scheduler"):
+        os.makedirs(os.path.join(out_dir, sub), exist_ok=True)
+    for sub, cls, c in (("unet", UNet, uc), ("vae", VaeDecoder, vc)):
+        m = cls(c)
+        with open(os.path.join(out_dir, sub, "config.json"), "w") as f:
+            json.dump(dict(c, _class_name="UNet2DConditionModel" if sub == "unet" else "AutoencoderKL"), f)
+        dt = torch.bfloat16 if size == "sd15" else torch.float32  # halves the 3.4 GB SD-1.5 UNet file
+        save_file({k: v.to(dt).contiguous() for k, v in m.state_dict().items()},
+                  os.path.join(out_dir, sub, "diffusion_pytorch_model.safetensors"))
+    te = tf.CLIPTextModel(tf.CLIPTextConfig(**tc))
+    te.save_pretrained(os.path.join(out_dir, "text_encoder"), safe_serialization=True)
+    vocab = _clip_byte_vocab()
+    with open(os.path.join(out_dir, "tokenizer", "vocab.json"), "w") as f:
+        json.dump(vocab, f)
+    with open(os.path.join(out_dir, "tokenizer", "merges.txt"), "w") as f:
+        f.write("#version: 0.2\n")
+    with open(os.path.join(out_dir, "scheduler", "scheduler_config.json"), "w") as f:
+        json.dump({"_class_name": "DDIMScheduler", "beta_start": 0.00085, "beta_end": 0.012,
+                   "beta_schedule": "scaled_linear", "num_train_timesteps": 1000, "steps_offset": 1,
+                   "set_alpha_to_one": False, "clip_sample": False,
+                   "prediction_type": "v_prediction" if v_prediction else "epsilon"}, f)
+    with open(os.path.join(out_dir, "model_index.json"), "w") as f:
+        json.dump({"_class_name": "StableDiffusionPipeline"}, f)
+    return out_dir

@@ -1,0 +1,143 @@
+"""Stable Diffusion pipeline (models/sd.py) and the diffusers backend.
+
+Oracles: the CLIP text encoder against transformers' CLIPTextModel on the same weights (exact,
+with and without clip-skip); the DDIM / Euler schedulers against closed form (a denoiser that
+returns the true noise must land on the clean latent).  The UNet / VAE have no oracle in this
+image (diffusers is not installed): parity unpinned -- they are checked for strict weight-name
+coverage on load, shapes, determinism under a seed, and CFG / scheduler plumbing.
+"""
+import asyncio
+import base64
+import io
+import math
+import os
+
+import pytest
+import torch
+
+from localai_amd.grpc import backend_pb as pb
+from localai_amd.models import synth
+from localai_amd.models.sd import Scheduler, StableDiffusion
+
+
+@pytest.fixture(scope="module")
+def pipe_dir(tmp_path_factory):
+    d = tmp_path_factory.mktemp("sd") / "sd-tiny"
+    synth.write_sd_pipeline(str(d))
+    return str(d)
+
+
+@pytest.mark.parametrize("skip", [0, 1])
+def test_text_encoder_matches_transformers(pipe_dir, skip):
+    import transformers as tf
+    p = StableDiffusion(pipe_dir, "cpu", clip_skip=skip)
+    te = tf.CLIPTextModel.from_pretrained(os.path.join(pipe_dir, "text_encoder")).eval()
+    ids = p.tok(["a red fox in the snow", "x"], padding="max_length", max_length=77, truncation=True,
+                return_tensors="pt").input_ids
+    with torch.no_grad():
+        tm = getattr(te, "text_model", te)
+        hs = te(ids, output_hidden_states=True).hidden_states
+        ref = tm.final_layer_norm(hs[-(skip + 1)])
+        got = p.text(ids, skip)
+    torch.testing.assert_close(got, ref, atol=1e-5, rtol=1e-5)
+
+
+@pytest.mark.parametrize("kind", ["ddim", "euler"])
+@pytest.mark.parametrize("pred", ["epsilon", "v_prediction"])
+def test_scheduler_recovers_clean_latent_with_oracle_denoiser(kind, pred):
+    s = Scheduler({"set_alpha_to_one": True, "prediction_type": pred}, kind)
+    g = torch.Generator().manual_seed(0)
+    x0, eps = torch.randn(1, 4, 8, 8, generator=g), torch.randn(1, 4, 8, 8, generator=g)
+    ts = s.timesteps(10)
+    assert ts[0] == 901 and ts[-1] == 1 and len(ts) == 10
+    a = float(s.ac[ts[0]])
+    # the noisy latent in each scheduler's own parameterisation
+    x = math.sqrt(a) * x0 + math.sqrt(1 - a) * eps if kind == "ddim" else x0 + math.sqrt((1 - a) / a) * eps
+    for i, t in enumerate(ts):
+        at = float(s.ac[t])
+        out = eps if pred == "epsilon" else math.sqrt(at) * eps - math.sqrt(1 - at) * x0
+        x = s.step(out, t, ts[i + 1] if i + 1 < len(ts) else None, x)
+    torch.testing.assert_close(x, x0, atol=1e-5, rtol=1e-5)
+
+
+def test_pipeline_shapes_determinism_and_guidance(pipe_dir):
+    p = StableDiffusion(pipe_dir, "cpu")
+    a = p("a cat", "blurry", 64, 48, steps=3, guidance_scale=7.0, seed=5)
+    assert a.shape == (48, 64, 3) and a.dtype == torch.uint8
+    assert torch.equal(a, p("a cat", "blurry", 64, 48, steps=3, guidance_scale=7.0, seed=5))
+    assert not torch.equal(a, p("a cat", "blurry", 64, 48, steps=3, guidance_scale=7.0, seed=6))
+    assert not torch.equal(a, p("a cat", "blurry", 64, 48, steps=3, guidance_scale=1.0, seed=5))
+    p.sched = Scheduler(p.sched_cfg, "euler")
+    assert p("a cat", "", 32, 32, steps=2, seed=1).shape == (32, 32, 3)
+
+
+def test_unet_rejects_missing_weights(pipe_dir, tmp_path):
+    import shutil
+
+    from safetensors.torch import load_file, save_file
+    d = tmp_path / "broken"
+    shutil.copytree(pipe_dir, d)
+    f = d / "unet" / "diffusion_pytorch_model.safetensors"
+    sd = load_file(str(f))
+    sd.pop(next(k for k in sd if "attn2.to_k" in k))
+    save_file(sd, str(f))
+    with pytest.raises(RuntimeError, match="Missing key"):
+        StableDiffusion(str(d), "cpu")
+
+
+def test_servicer_generate_image(pipe_dir, tmp_path):
+    from PIL import Image
+
+    from localai_amd.grpc.diffusers_servicer import DiffusersServicer
+    sv = DiffusersServicer(device="cpu")
+    dst = str(tmp_path / "out.png")
+
+    async def go():
+        assert (await sv.LoadModel(pb.ModelOptions(ModelFile=pipe_dir, CFGScale=5.0, SchedulerType="euler"))).success
+        r = await sv.GenerateImage(pb.GenerateImageRequest(positive_prompt="a boat", negative_prompt="", width=40,
+                                                           height=32, step=2, seed=3, dst=dst))
+        assert r.success
+        # EnableParameters=none: pipeline defaults (sample_size * 2 px for the two-level toy VAE)
+        await sv.GenerateImage(pb.GenerateImageRequest(positive_prompt="a boat", width=40, height=32, step=1,
+                                                       EnableParameters="none", seed=3, dst=dst + ".2.png"))
+    asyncio.run(go())
+    assert sv.cfg_scale == 5.0 and sv.pipe.sched.kind == "euler"
+    assert Image.open(dst).size == (40, 32)
+    px = sv.pipe.unet_sample_size * sv.pipe.vae_scale
+    assert Image.open(dst + ".2.png").size == (px, px)
+
+
+def test_gateway_images_endpoint(pipe_dir, tmp_path):
+    import shutil
+
+    from fastapi.testclient import TestClient
+    from PIL import Image
+
+    from localai_amd.config.app_config import ApplicationConfig
+    from localai_amd.config.backend_config import BackendConfig
+    from localai_amd.gateway.app import create_app
+    from localai_amd.gateway.state import AppState
+    mdir = tmp_path / "models"
+    shutil.copytree(pipe_dir, mdir / "sd-tiny")
+    ac = ApplicationConfig(models_path=str(mdir), upload_dir=str(tmp_path / "up"), config_dir=str(tmp_path / "cfg"),
+                           image_dir=str(tmp_path / "img"), audio_dir=str(tmp_path / "aud"))
+    st = AppState(ac)
+    bc = BackendConfig({"name": "sd", "backend": "diffusers", "parameters": {"model": "sd-tiny"},
+                        "diffusers": {"cfg_scale": 6, "scheduler_type": "ddim"}})
+    bc.set_defaults()
+    st.configs.add(bc)
+    with TestClient(create_app(st)) as c:
+        r = c.post("/v1/images/generations", json={"model": "sd", "prompt": "a lighthouse|fog", "size": "32x32",
+                                                   "step": 2, "response_format": "b64_json"})
+        assert r.status_code == 200, r.text
+        img = Image.open(io.BytesIO(base64.b64decode(r.json()["data"][0]["b64_json"])))
+        assert img.size == (32, 32)
+        assert "diffusers" in c.get("/system").json()["backends"]
+
+
+@pytest.mark.gpu
+def test_pipeline_on_gpu_matches_cpu_layout(pipe_dir):
+    """bf16 on the GPU vs fp32 on the CPU: same seed, same scheduler -> close images."""
+    a = StableDiffusion(pipe_dir, "cpu")("a cat", "", 32, 32, steps=2, seed=7).float()
+    b = StableDiffusion(pipe_dir, "cuda:0")("a cat", "", 32, 32, steps=2, seed=7).float()
+    assert (a - b).abs().mean() < 4.0
