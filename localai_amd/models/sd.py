@@ -435,8 +435,13 @@ class Scheduler:
 
 # ------------------------------------------------------------------ pipeline
 class StableDiffusion:
-    def __init__(self, path: str, device: str = "cpu", scheduler: str = "", clip_skip: int = 0):
+    def __init__(self, path: str, device: str = "cpu", scheduler: str = "", clip_skip: int = 0,
+                 channels_last: Optional[bool] = None):
         self.device = torch.device(device)
+        # NHWC activations for the MIOpen convolutions (LOCALAI_AMD_SD_NHWC=0 keeps NCHW)
+        if channels_last is None:
+            channels_last = os.environ.get("LOCALAI_AMD_SD_NHWC", "1") != "0"
+        self.channels_last = channels_last and self.device.type == "cuda"
         self.dtype = torch.bfloat16 if self.device.type == "cuda" else torch.float32
         self.clip_skip = clip_skip
         self.text = ClipTextEncoder(_cfg(os.path.join(path, "text_encoder", "config.json")))
@@ -452,6 +457,9 @@ class StableDiffusion:
         self.vae.load_state_dict(_vae_names(_load_weights(os.path.join(path, "vae"))), strict=True)
         for m in (self.text, self.unet, self.vae):
             m.to(self.device, self.dtype).eval().requires_grad_(False)
+        if self.channels_last:
+            self.unet.to(memory_format=torch.channels_last)
+            self.vae.to(memory_format=torch.channels_last)
         sc = os.path.join(path, "scheduler", "scheduler_config.json")
         self.sched_cfg = _cfg(sc) if os.path.isfile(sc) else {}
         self.sched = Scheduler(self.sched_cfg, (scheduler or "ddim").lower())
@@ -480,7 +488,10 @@ class StableDiffusion:
             xin = self.sched.scale_input(x, t)
             xin = torch.cat([xin, xin]) if cfg else xin
             tt = torch.full((xin.shape[0],), t, device=self.device)
-            out = self.unet(xin.to(self.dtype), tt, ctx).float()
+            xin = xin.to(self.dtype)
+            if self.channels_last:
+                xin = xin.contiguous(memory_format=torch.channels_last)
+            out = self.unet(xin, tt, ctx).float()
             if cfg:
                 u, c = out.chunk(2)
                 out = u + guidance_scale * (c - u)

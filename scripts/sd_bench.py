@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--size", type=int, default=512)
     ap.add_argument("--runs", type=int, default=2)
+    ap.add_argument("--nchw", action="store_true", help="keep NCHW activations (default NHWC)")
     a = ap.parse_args()
     import torch
     from localai_amd.models import synth
@@ -30,7 +31,7 @@ def main():
         synth.write_sd_pipeline(d, size="sd15")
     print("pipeline written", flush=True)
     dev = "cuda:0" if torch.cuda.is_available() else "cpu"
-    p = StableDiffusion(d, dev)
+    p = StableDiffusion(d, dev, channels_last=not a.nchw)
     p("warm up", "", a.size, a.size, steps=2, seed=1)
     best = None
     for r in range(a.runs):
@@ -41,7 +42,7 @@ def main():
         best = el if best is None else min(best, el)
         print(f"run {r}: {el:.3f} s", flush=True)
     print(json.dumps({"metric": "SD-1.5 txt2img, diffusers backend", "size": a.size, "steps": a.steps,
-                      "s_per_image": round(best, 3), "unet_it_s": round(a.steps / best, 2), "cfg": True,
+                      "s_per_image": round(best, 3), "unet_it_s": round(a.steps / best, 2), "cfg": True, "layout": "nchw" if a.nchw else "nhwc",
                       "dtype": str(p.dtype).replace("torch.", "")}), flush=True)
 
 
