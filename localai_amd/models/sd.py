@@ -15,6 +15,10 @@ like the checkpoint's tensors so `load_state_dict(strict=True)` checks every wei
 * AutoencoderKL decoder (post-quant conv, ResNet / single-head attention mid block, upsampling
   ResNet stacks).
 
+GroupNorm (+ the SiLU that follows it in every ResNet block) runs as one hand-written HIP kernel
+pair on NHWC bf16 activations (ops/csrc/groupnorm.hip); it was the largest kernel-time item of the
+PyTorch path (profiles/r2c_sd15.md).
+
 Classifier-free guidance runs conditional and unconditional branches as one batch of 2.  On
 the GPU everything is bf16 (convolutions through MIOpen, attention through PyTorch's fused SDPA,
 the GEMMs through hipBLASLt); the schedulers keep latents in fp32.  Schedulers: DDIM
@@ -110,6 +114,17 @@ class ClipTextEncoder(nn.Module):
 
 
 # ------------------------------------------------------------------ UNet / VAE building blocks
+def _gn(norm: nn.GroupNorm, x: torch.Tensor, silu: bool = False) -> torch.Tensor:
+    """GroupNorm (+ SiLU): the fused HIP kernel (ops/csrc/groupnorm.hip) on bf16 NHWC activations,
+    PyTorch elsewhere (CPU, NCHW)."""
+    if x.is_cuda:
+        from .. import ops
+        if ops.groupnorm_supported(x, norm.num_groups):
+            return ops.groupnorm_nhwc(x, norm.num_groups, norm.weight, norm.bias, norm.eps, silu)
+    y = F.group_norm(x, norm.num_groups, norm.weight, norm.bias, norm.eps)
+    return F.silu(y) if silu else y
+
+
 class _Resnet(nn.Module):
     def __init__(self, cin: int, cout: int, groups: int, eps: float, temb: Optional[int]):
         super().__init__()
@@ -123,10 +138,10 @@ class _Resnet(nn.Module):
             self.conv_shortcut = nn.Conv2d(cin, cout, 1)
 
     def forward(self, x, temb=None):
-        h = self.conv1(F.silu(self.norm1(x)))
+        h = self.conv1(_gn(self.norm1, x, True))
         if temb is not None:
             h = h + self.time_emb_proj(F.silu(temb))[:, :, None, None]
-        h = self.conv2(F.silu(self.norm2(h)))
+        h = self.conv2(_gn(self.norm2, h, True))
         return (self.conv_shortcut(x) if hasattr(self, "conv_shortcut") else x) + h
 
 
@@ -185,7 +200,7 @@ class _Transformer2D(nn.Module):
 
     def forward(self, x, ctx):
         B, C, H, W = x.shape
-        h = self.norm(x)
+        h = _gn(self.norm, x)
         if not self.linear:
             h = self.proj_in(h)
         h = h.permute(0, 2, 3, 1).reshape(B, H * W, C)
@@ -308,7 +323,7 @@ class UNet(nn.Module):
                     h = b.attentions[j](h, ctx)
             if hasattr(b, "upsamplers"):
                 h = b.upsamplers[0](h)
-        return self.conv_out(F.silu(self.conv_norm_out(h)))
+        return self.conv_out(_gn(self.conv_norm_out, h, True))
 
 
 class _VaeAttn(nn.Module):
@@ -320,7 +335,7 @@ class _VaeAttn(nn.Module):
 
     def forward(self, x):
         B, C, H, W = x.shape
-        h = self.group_norm(x).reshape(B, C, H * W).transpose(1, 2)
+        h = _gn(self.group_norm, x).reshape(B, C, H * W).transpose(1, 2)
         q, k, v = (p(h)[:, None] for p in (self.to_q, self.to_k, self.to_v))
         o = F.scaled_dot_product_attention(q, k, v)[:, 0]
         return x + self.to_out[0](o).transpose(1, 2).reshape(B, C, H, W)
@@ -362,7 +377,7 @@ class VaeDecoder(nn.Module):
                 h = r(h)
             if hasattr(b, "upsamplers"):
                 h = b.upsamplers[0](h)
-        return d.conv_out(F.silu(d.conv_norm_out(h)))
+        return d.conv_out(_gn(d.conv_norm_out, h, True))
 
 
 def _vae_names(sd: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:

@@ -54,6 +54,7 @@ def lib():
             "la_add_norm": [P, P, LNG, I, P, I, P, P, P, I, I, F, I, P, P],
             "la_rope_kv": [P, LNG, I, P, P, P, P, I, I, I, I, I, I, P, P, P, I, P],
             "la_mamba_conv_step": [P, P, LNG, P, P, P, I, I, I, P],
+            "la_groupnorm_nhwc": [P, P, P, P, P, I, I, I, I, I, F, I, P],
             "la_mamba_ssm_step": [P, P, P, P, LNG, I, I, P, P, P, LNG, P, I, I, I, P],
             "la_act": [P, LNG, I, P, P, I, I, I, P],
             "la_reduce_slabs": [P, LNG, I, P, I, I, P, P, P],
@@ -1434,3 +1435,32 @@ def mamba_ssm_step(ssm_state: torch.Tensor, x: torch.Tensor, dt: torch.Tensor, b
                                    off_b, off_c, A.data_ptr(), D.data_ptr(), xz.data_ptr(), xz.stride(0),
                                    out.data_ptr(), B, I, N, _stream()), "la_mamba_ssm_step")
     return out
+
+
+# ---------------------------------------------------------------------------------------
+# GroupNorm (+ SiLU) over NHWC bf16 activations (groupnorm.hip) -- the SD UNet / VAE norms
+# ---------------------------------------------------------------------------------------
+
+def groupnorm_supported(x: torch.Tensor, groups: int) -> bool:
+    if not (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4):
+        return False
+    C = x.shape[1]
+    return (x.is_contiguous(memory_format=torch.channels_last) and groups <= 64 and C % groups == 0
+            and (C // groups) % 2 == 0 and C <= 2048)
+
+
+def groupnorm_nhwc(x: torch.Tensor, groups: int, weight: Optional[torch.Tensor], bias: Optional[torch.Tensor],
+                   eps: float, silu: bool = False) -> torch.Tensor:
+    """x [B, C, H, W] bf16 in channels_last memory -> GroupNorm(x) (SiLU'd when `silu`), same layout."""
+    assert groupnorm_supported(x, groups), "groupnorm_nhwc: bf16 channels_last, even channels per group, C <= 2048"
+    B, C, H, W = x.shape
+    for t in (weight, bias):
+        assert t is None or (t.dtype == torch.bfloat16 and t.is_contiguous() and t.numel() == C)
+    HW = H * W
+    rows = max(1, -(-HW * B // 1024))  # ~1024 workgroups over the chip
+    S = -(-HW // rows)
+    part = torch.empty(B * S * groups * 2, dtype=torch.float32, device=x.device)
+    y = torch.empty_like(x, memory_format=torch.channels_last)
+    _check(lib().la_groupnorm_nhwc(x.data_ptr(), y.data_ptr(), _ptr(weight), _ptr(bias), part.data_ptr(), B, HW, C,
+                                   groups, rows, float(eps), int(silu), _stream()), "la_groupnorm_nhwc")
+    return y

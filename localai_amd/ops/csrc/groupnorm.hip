@@ -1,0 +1,151 @@
+// GroupNorm (+ optional SiLU) over NHWC bf16 activations, gfx950 -- the Stable Diffusion UNet /
+// VAE normalisation (models/sd.py: ResNet norm1/norm2 + SiLU, Transformer2D norm, conv_norm_out).
+//
+// PyTorch's GroupNorm on these shapes runs three kernels (row moments over one workgroup per
+// (batch, group) -- only 64 workgroups for SD's 2 x 32 groups -- fused params, then a separate
+// elementwise pass and another one for SiLU).  Here:
+//   la_gn_stats : grid (S chunks of pixels, B).  Each workgroup streams its chunk row by row
+//                 (a row = C contiguous bf16, read as bf16x2 lanes: coalesced), every thread owning
+//                 fixed channel pairs, so per-group fp32 sum / sum-of-squares stay in registers; one
+//                 LDS reduction per workgroup writes [B, S, G, 2] partials.  S is chosen by the host
+//                 so B*S >= ~1024 workgroups fill the 256 CUs.
+//   la_gn_apply : same grid; each workgroup folds the S partials of its groups into mean / rstd,
+//                 precomputes per-channel scale / shift (gamma, beta) and writes
+//                 y = x * scale + shift, SiLU'd when asked, in one pass.
+// Channels per group must be even (a bf16x2 lane never straddles two groups) and C <= 2048.
+#include <hip/hip_bfloat16.h>
+#include <hip/hip_runtime.h>
+
+namespace la {
+
+constexpr int GN_THREADS = 256;
+constexpr int GN_MAXP = 4;  // channel pairs per thread: C <= 2 * 256 * 4
+constexpr int GN_MAXG = 64;
+
+__device__ __forceinline__ float bf2f(unsigned short v) { return __uint_as_float((unsigned)v << 16); }
+__device__ __forceinline__ unsigned short f2bf(float f) {
+  unsigned u = __float_as_uint(f);
+  u += 0x7FFFu + ((u >> 16) & 1u);  // round to nearest even
+  return (unsigned short)(u >> 16);
+}
+
+__global__ void __launch_bounds__(GN_THREADS) gn_stats_kernel(const unsigned* __restrict__ x, float* __restrict__ part,
+                                                              int HW, int C, int G, int rows_per_chunk, int S) {
+  const int s = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
+  const int P = C >> 1, cg = C / G;
+  const int r0 = s * rows_per_chunk, r1 = min(HW, r0 + rows_per_chunk);
+  // C/2 <= 256: several rows per step, one pair per lane; otherwise one row per step
+  const int RS = P <= GN_THREADS ? GN_THREADS / P : 1;
+  const int tr = P <= GN_THREADS ? t / P : 0, pb = P <= GN_THREADS ? t % P : t;
+  float sum[GN_MAXP], sq[GN_MAXP];
+#pragma unroll
+  for (int i = 0; i < GN_MAXP; ++i) sum[i] = sq[i] = 0.0f;
+  const unsigned* xb = x + (long)b * HW * P;
+  for (int r = r0 + tr; tr < RS && r < r1; r += RS) {
+    const unsigned* row = xb + (long)r * P;
+#pragma unroll
+    for (int i = 0; i < GN_MAXP; ++i) {
+      const int p = pb + i * GN_THREADS;
+      if (p < P) {
+        const unsigned v = row[p];
+        const float a = bf2f((unsigned short)(v & 0xFFFF)), c = bf2f((unsigned short)(v >> 16));
+        sum[i] += a + c;
+        sq[i] += a * a + c * c;
+      }
+    }
+  }
+  __shared__ float acc[GN_MAXG * 2];
+  for (int i = t; i < 2 * G; i += GN_THREADS) acc[i] = 0.0f;
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < GN_MAXP; ++i) {
+    const int p = pb + i * GN_THREADS;
+    if (tr < RS && p < P) {
+      const int g = (2 * p) / cg;
+      atomicAdd(&acc[2 * g], sum[i]);
+      atomicAdd(&acc[2 * g + 1], sq[i]);
+    }
+  }
+  __syncthreads();
+  float* out = part + ((long)b * S + s) * G * 2;
+  for (int i = t; i < 2 * G; i += GN_THREADS) out[i] = acc[i];
+}
+
+__global__ void __launch_bounds__(GN_THREADS) gn_apply_kernel(const unsigned* __restrict__ x, unsigned* __restrict__ y,
+                                                              const unsigned short* __restrict__ gamma,
+                                                              const unsigned short* __restrict__ beta,
+                                                              const float* __restrict__ part, int HW, int C, int G,
+                                                              int rows_per_chunk, int S, float eps, int silu) {
+  const int s = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
+  const int P = C >> 1, cg = C / G;
+  __shared__ float stat[GN_MAXG * 2];
+  if (t < G) {
+    float su = 0.0f, sqs = 0.0f;
+    const float* pb = part + (long)b * S * G * 2;
+    for (int k = 0; k < S; ++k) {
+      su += pb[(long)k * G * 2 + 2 * t];
+      sqs += pb[(long)k * G * 2 + 2 * t + 1];
+    }
+    const float n = (float)HW * cg;
+    const float mean = su / n;
+    const float var = fmaxf(sqs / n - mean * mean, 0.0f);
+    stat[2 * t] = mean;
+    stat[2 * t + 1] = rsqrtf(var + eps);
+  }
+  __syncthreads();
+  const int RS = P <= GN_THREADS ? GN_THREADS / P : 1;
+  const int tr = P <= GN_THREADS ? t / P : 0, pb = P <= GN_THREADS ? t % P : t;
+  float sc[GN_MAXP][2], sh[GN_MAXP][2];
+#pragma unroll
+  for (int i = 0; i < GN_MAXP; ++i) {
+    const int p = pb + i * GN_THREADS;
+    if (p < P) {
+      const int g = (2 * p) / cg;
+      const float mean = stat[2 * g], rstd = stat[2 * g + 1];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const float ga = gamma ? bf2f(gamma[2 * p + j]) : 1.0f, be = beta ? bf2f(beta[2 * p + j]) : 0.0f;
+        sc[i][j] = rstd * ga;
+        sh[i][j] = be - mean * rstd * ga;
+      }
+    }
+  }
+  const int r0 = s * rows_per_chunk, r1 = min(HW, r0 + rows_per_chunk);
+  const long base = (long)b * HW * P;
+  for (int r = r0 + tr; tr < RS && r < r1; r += RS) {
+    const unsigned* row = x + base + (long)r * P;
+    unsigned* orow = y + base + (long)r * P;
+#pragma unroll
+    for (int i = 0; i < GN_MAXP; ++i) {
+      const int p = pb + i * GN_THREADS;
+      if (p < P) {
+        const unsigned v = row[p];
+        float a = bf2f((unsigned short)(v & 0xFFFF)) * sc[i][0] + sh[i][0];
+        float c = bf2f((unsigned short)(v >> 16)) * sc[i][1] + sh[i][1];
+        if (silu) {
+          a = a / (1.0f + __expf(-a));
+          c = c / (1.0f + __expf(-c));
+        }
+        orow[p] = (unsigned)f2bf(a) | ((unsigned)f2bf(c) << 16);
+      }
+    }
+  }
+}
+
+}  // namespace la
+
+// x, y: [B, HW, C] bf16 (NHWC); gamma / beta: [C] bf16 or null; part: fp32 workspace of B*S*G*2.
+extern "C" int la_groupnorm_nhwc(const void* x, void* y, const void* gamma, const void* beta, float* part, int B,
+                                 int HW, int C, int G, int rows_per_chunk, float eps, int silu, void* stream) {
+  if (B <= 0 || HW <= 0 || C <= 0 || G <= 0 || G > la::GN_MAXG || C % G || (C / G) % 2 ||
+      C > 2 * la::GN_THREADS * la::GN_MAXP || rows_per_chunk <= 0)
+    return (int)hipErrorInvalidValue;
+  const int S = (HW + rows_per_chunk - 1) / rows_per_chunk;
+  const dim3 grid((unsigned)S, (unsigned)B);
+  hipLaunchKernelGGL(la::gn_stats_kernel, grid, dim3(la::GN_THREADS), 0, (hipStream_t)stream, (const unsigned*)x,
+                     part, HW, C, G, rows_per_chunk, S);
+  hipLaunchKernelGGL(la::gn_apply_kernel, grid, dim3(la::GN_THREADS), 0, (hipStream_t)stream, (const unsigned*)x,
+                     (unsigned*)y, (const unsigned short*)gamma, (const unsigned short*)beta, part, HW, C, G,
+                     rows_per_chunk, S, eps, silu);
+  return (int)hipGetLastError();
+}

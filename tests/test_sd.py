@@ -14,6 +14,7 @@ import os
 
 import pytest
 import torch
+import torch.nn.functional as F
 
 from localai_amd.grpc import backend_pb as pb
 from localai_amd.models import synth
@@ -141,3 +142,24 @@ def test_pipeline_on_gpu_matches_cpu_layout(pipe_dir):
     a = StableDiffusion(pipe_dir, "cpu")("a cat", "", 32, 32, steps=2, seed=7).float()
     b = StableDiffusion(pipe_dir, "cuda:0")("a cat", "", 32, 32, steps=2, seed=7).float()
     assert (a - b).abs().mean() < 4.0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape,groups", [((2, 320, 64, 64), 32), ((2, 1280, 8, 8), 32), ((1, 128, 96, 80), 32),
+                                          ((2, 640, 16, 16), 32), ((1, 96, 5, 7), 8), ((3, 2048, 4, 4), 64)])
+@pytest.mark.parametrize("silu", [False, True])
+def test_groupnorm_nhwc_kernel_matches_fp32(shape, groups, silu):
+    from localai_amd import ops
+    torch.manual_seed(0)
+    C = shape[1]
+    x = (torch.randn(shape, device="cuda") * 3 + 0.5).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (torch.rand(C, device="cuda") + 0.5).to(torch.bfloat16)
+    b = torch.randn(C, device="cuda").to(torch.bfloat16)
+    ref = F.group_norm(x.float(), groups, w.float(), b.float(), 1e-5)
+    ref = F.silu(ref) if silu else ref
+    got = ops.groupnorm_nhwc(x, groups, w, b, 1e-5, silu)
+    assert got.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(got.float(), ref, atol=3e-2, rtol=2e-2)
+    got = ops.groupnorm_nhwc(x, groups, None, None, 1e-5, silu)  # affine-free
+    ref = F.group_norm(x.float(), groups, None, None, 1e-5)
+    torch.testing.assert_close(got.float(), F.silu(ref) if silu else ref, atol=3e-2, rtol=2e-2)
