@@ -54,7 +54,7 @@ def lib():
             "la_add_norm": [P, P, LNG, I, P, I, P, P, P, I, I, F, I, P, P],
             "la_rope_kv": [P, LNG, I, P, P, P, P, I, I, I, I, I, I, P, P, P, I, P],
             "la_mamba_conv_step": [P, P, LNG, P, P, P, I, I, I, P],
-            "la_groupnorm_nhwc": [P, P, P, P, P, I, I, I, I, I, F, I, P],
+            "la_groupnorm_nhwc": [P, P, P, P, P, I, I, I, I, I, I, F, I, P],
             "la_mamba_ssm_step": [P, P, P, P, LNG, I, I, P, P, P, LNG, P, I, I, I, P],
             "la_act": [P, LNG, I, P, P, I, I, I, P],
             "la_reduce_slabs": [P, LNG, I, P, I, I, P, P, P],
@@ -1445,7 +1445,8 @@ def groupnorm_supported(x: torch.Tensor, groups: int) -> bool:
     if not (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4):
         return False
     C = x.shape[1]
-    return (x.is_contiguous(memory_format=torch.channels_last) and groups <= 64 and C % groups == 0
+    return (x.is_contiguous(memory_format=torch.channels_last) and groups <= 64 and 256 % (2 * groups) == 0
+            and C % groups == 0
             and (C // groups) % 2 == 0 and C <= 2048)
 
 
@@ -1457,10 +1458,11 @@ def groupnorm_nhwc(x: torch.Tensor, groups: int, weight: Optional[torch.Tensor],
     for t in (weight, bias):
         assert t is None or (t.dtype == torch.bfloat16 and t.is_contiguous() and t.numel() == C)
     HW = H * W
-    rows = max(1, -(-HW * B // 1024))  # ~1024 workgroups over the chip
-    S = -(-HW // rows)
+    rows_s = max(1, -(-HW * B // 256))    # statistics: ~256 workgroups, few partials
+    rows_a = max(1, -(-HW * B // 1024))   # apply: ~1024 workgroups over the chip
+    S = -(-HW // rows_s)
     part = torch.empty(B * S * groups * 2, dtype=torch.float32, device=x.device)
     y = torch.empty_like(x, memory_format=torch.channels_last)
     _check(lib().la_groupnorm_nhwc(x.data_ptr(), y.data_ptr(), _ptr(weight), _ptr(bias), part.data_ptr(), B, HW, C,
-                                   groups, rows, float(eps), int(silu), _stream()), "la_groupnorm_nhwc")
+                                   groups, rows_s, rows_a, float(eps), int(silu), _stream()), "la_groupnorm_nhwc")
     return y

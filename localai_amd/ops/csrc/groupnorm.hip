@@ -7,9 +7,10 @@
 //   la_gn_stats : grid (S chunks of pixels, B).  Each workgroup streams its chunk row by row
 //                 (a row = C contiguous bf16, read as bf16x2 lanes: coalesced), every thread owning
 //                 fixed channel pairs, so per-group fp32 sum / sum-of-squares stay in registers; one
-//                 LDS reduction per workgroup writes [B, S, G, 2] partials.  S is chosen by the host
-//                 so B*S >= ~1024 workgroups fill the 256 CUs.
-//   la_gn_apply : same grid; each workgroup folds the S partials of its groups into mean / rstd,
+//                 LDS reduction per workgroup writes [B, S, G, 2] partials.  B*S ~ 256 workgroups
+//                 (one pass over the tensor; few partials to fold).
+//   la_gn_apply : grid (pixel chunks, B); each workgroup folds the S partials (read coalesced by
+//                 all lanes, LDS-summed) into mean / rstd,
 //                 precomputes per-channel scale / shift (gamma, beta) and writes
 //                 y = x * scale + shift, SiLU'd when asked, in one pass.
 // Channels per group must be even (a bf16x2 lane never straddles two groups) and C <= 2048.
@@ -76,21 +77,34 @@ __global__ void __launch_bounds__(GN_THREADS) gn_apply_kernel(const unsigned* __
                                                               const unsigned short* __restrict__ beta,
                                                               const float* __restrict__ part, int HW, int C, int G,
                                                               int rows_per_chunk, int S, float eps, int silu) {
+  // rows_per_chunk: this kernel's pixels per workgroup; S: number of stats partials per batch
   const int s = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
   const int P = C >> 1, cg = C / G;
+  // fold the S stats partials [S, G, 2] of this batch: all lanes read them coalesced, lane t
+  // owning slot t % 2G (2G divides the workgroup), then an LDS sum over the 256 / 2G lanes per slot
+  __shared__ float red[GN_THREADS];
   __shared__ float stat[GN_MAXG * 2];
-  if (t < G) {
-    float su = 0.0f, sqs = 0.0f;
-    const float* pb = part + (long)b * S * G * 2;
-    for (int k = 0; k < S; ++k) {
-      su += pb[(long)k * G * 2 + 2 * t];
-      sqs += pb[(long)k * G * 2 + 2 * t + 1];
+  {
+    const int G2 = 2 * G, slot = t % G2, KS = GN_THREADS / G2;
+    const float* pp = part + (long)b * S * G2;
+    float a = 0.0f;
+#pragma unroll 8
+    for (int k = t / G2; k < S; k += KS) a += pp[(long)k * G2 + slot];
+    red[t] = a;
+    __syncthreads();
+    if (t < G2) {
+      float v = 0.0f;
+      for (int j = 0; j < KS; ++j) v += red[j * G2 + t];
+      stat[t] = v;
     }
-    const float n = (float)HW * cg;
-    const float mean = su / n;
-    const float var = fmaxf(sqs / n - mean * mean, 0.0f);
-    stat[2 * t] = mean;
-    stat[2 * t + 1] = rsqrtf(var + eps);
+    __syncthreads();
+    if (t < G) {
+      const float n = (float)HW * cg;
+      const float mean = stat[2 * t] / n;
+      const float var = fmaxf(stat[2 * t + 1] / n - mean * mean, 0.0f);
+      red[2 * t] = mean;
+      red[2 * t + 1] = rsqrtf(var + eps);
+    }
   }
   __syncthreads();
   const int RS = P <= GN_THREADS ? GN_THREADS / P : 1;
@@ -101,7 +115,7 @@ __global__ void __launch_bounds__(GN_THREADS) gn_apply_kernel(const unsigned* __
     const int p = pb + i * GN_THREADS;
     if (p < P) {
       const int g = (2 * p) / cg;
-      const float mean = stat[2 * g], rstd = stat[2 * g + 1];
+      const float mean = red[2 * g], rstd = red[2 * g + 1];
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const float ga = gamma ? bf2f(gamma[2 * p + j]) : 1.0f, be = beta ? bf2f(beta[2 * p + j]) : 0.0f;
@@ -135,17 +149,20 @@ __global__ void __launch_bounds__(GN_THREADS) gn_apply_kernel(const unsigned* __
 }  // namespace la
 
 // x, y: [B, HW, C] bf16 (NHWC); gamma / beta: [C] bf16 or null; part: fp32 workspace of B*S*G*2.
+// rows_stats / rows_apply: pixels per workgroup of the two kernels (the statistics pass uses
+// coarser chunks so the apply pass has few partials to fold).
 extern "C" int la_groupnorm_nhwc(const void* x, void* y, const void* gamma, const void* beta, float* part, int B,
-                                 int HW, int C, int G, int rows_per_chunk, float eps, int silu, void* stream) {
+                                 int HW, int C, int G, int rows_stats, int rows_apply, float eps, int silu,
+                                 void* stream) {
   if (B <= 0 || HW <= 0 || C <= 0 || G <= 0 || G > la::GN_MAXG || C % G || (C / G) % 2 ||
-      C > 2 * la::GN_THREADS * la::GN_MAXP || rows_per_chunk <= 0)
+      la::GN_THREADS % (2 * G) || C > 2 * la::GN_THREADS * la::GN_MAXP || rows_stats <= 0 || rows_apply <= 0)
     return (int)hipErrorInvalidValue;
-  const int S = (HW + rows_per_chunk - 1) / rows_per_chunk;
-  const dim3 grid((unsigned)S, (unsigned)B);
-  hipLaunchKernelGGL(la::gn_stats_kernel, grid, dim3(la::GN_THREADS), 0, (hipStream_t)stream, (const unsigned*)x,
-                     part, HW, C, G, rows_per_chunk, S);
-  hipLaunchKernelGGL(la::gn_apply_kernel, grid, dim3(la::GN_THREADS), 0, (hipStream_t)stream, (const unsigned*)x,
-                     (unsigned*)y, (const unsigned short*)gamma, (const unsigned short*)beta, part, HW, C, G,
-                     rows_per_chunk, S, eps, silu);
+  const int S = (HW + rows_stats - 1) / rows_stats;
+  const int SA = (HW + rows_apply - 1) / rows_apply;
+  hipLaunchKernelGGL(la::gn_stats_kernel, dim3((unsigned)S, (unsigned)B), dim3(la::GN_THREADS), 0,
+                     (hipStream_t)stream, (const unsigned*)x, part, HW, C, G, rows_stats, S);
+  hipLaunchKernelGGL(la::gn_apply_kernel, dim3((unsigned)SA, (unsigned)B), dim3(la::GN_THREADS), 0,
+                     (hipStream_t)stream, (const unsigned*)x, (unsigned*)y, (const unsigned short*)gamma,
+                     (const unsigned short*)beta, part, HW, C, G, rows_apply, S, eps, silu);
   return (int)hipGetLastError();
 }
