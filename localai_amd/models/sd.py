@@ -482,7 +482,35 @@ class StableDiffusion:
         self.tok = CLIPTokenizer.from_pretrained(os.path.join(path, "tokenizer"))
         self.max_len = self.text.text_model.embeddings.position_embedding.weight.shape[0]
         self.latent_ch = self.unet.conv_in.in_channels
+        # one hipGraph per (batch, latent size) replays the whole UNet step (~1300 launches)
+        self.use_graphs = self.device.type == "cuda" and os.environ.get("LOCALAI_AMD_SD_GRAPH", "1") != "0"
+        self._graphs: Dict[tuple, tuple] = {}
         self.vae_scale = 2 ** (len(self.vae.decoder.up_blocks) - 1)
+
+    def _unet(self, x: torch.Tensor, t: torch.Tensor, ctx: torch.Tensor) -> torch.Tensor:
+        if not self.use_graphs:
+            return self.unet(x, t, ctx)
+        key = (tuple(x.shape), tuple(ctx.shape))
+        g = self._graphs.get(key)
+        if g is None:
+            out = self.unet(x, t, ctx)  # eager first call: kernel selection / workspaces happen outside capture
+            try:
+                sx, st, sc = x.clone(), t.clone(), ctx.clone()
+                graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(graph):
+                    so = self.unet(sx, st, sc)
+                self._graphs[key] = (graph, sx, st, sc, so)
+            except Exception as e:  # noqa: BLE001 - capture is an optimisation; eager stays correct
+                import logging
+                logging.getLogger(__name__).warning("sd: UNet graph capture failed (%r); running eager", e)
+                self.use_graphs = False
+            return out
+        graph, sx, st, sc, so = g
+        sx.copy_(x)
+        st.copy_(t)
+        sc.copy_(ctx)
+        graph.replay()
+        return so.clone()
 
     def _encode(self, prompts: List[str]) -> torch.Tensor:
         ids = self.tok(prompts, padding="max_length", max_length=self.max_len, truncation=True,
@@ -506,7 +534,7 @@ class StableDiffusion:
             xin = xin.to(self.dtype)
             if self.channels_last:
                 xin = xin.contiguous(memory_format=torch.channels_last)
-            out = self.unet(xin, tt, ctx).float()
+            out = self._unet(xin, tt, ctx).float()
             if cfg:
                 u, c = out.chunk(2)
                 out = u + guidance_scale * (c - u)

@@ -163,3 +163,14 @@ def test_groupnorm_nhwc_kernel_matches_fp32(shape, groups, silu):
     got = ops.groupnorm_nhwc(x, groups, None, None, 1e-5, silu)  # affine-free
     ref = F.group_norm(x.float(), groups, None, None, 1e-5)
     torch.testing.assert_close(got.float(), F.silu(ref) if silu else ref, atol=3e-2, rtol=2e-2)
+
+
+@pytest.mark.gpu
+def test_unet_graph_replay_matches_eager(pipe_dir):
+    p = StableDiffusion(pipe_dir, "cuda:0")
+    assert p.use_graphs and p.channels_last
+    a = p("a cat", "blurry", 32, 32, steps=3, seed=11)  # first step eager + capture, then replays
+    assert p._graphs, "UNet step was not captured"
+    p.use_graphs = False
+    b = p("a cat", "blurry", 32, 32, steps=3, seed=11)
+    assert (a.float() - b.float()).abs().max() <= 2
