@@ -42,7 +42,7 @@ def main():
         best = el if best is None else min(best, el)
         print(f"run {r}: {el:.3f} s", flush=True)
     print(json.dumps({"metric": "SD-1.5 txt2img, diffusers backend", "size": a.size, "steps": a.steps,
-                      "s_per_image": round(best, 3), "unet_it_s": round(a.steps / best, 2), "cfg": True, "layout": "nchw" if a.nchw else "nhwc",
+                      "s_per_image": round(best, 3), "unet_it_s": round(a.steps / best, 2), "cfg": True, "layout": "nchw" if a.nchw else "nhwc", "hipgraph": bool(p.use_graphs and p._graphs),
                       "dtype": str(p.dtype).replace("torch.", "")}), flush=True)
 
 
