@@ -138,9 +138,13 @@ class _Resnet(nn.Module):
             self.conv_shortcut = nn.Conv2d(cin, cout, 1)
 
     def forward(self, x, temb=None):
-        h = self.conv1(_gn(self.norm1, x, True))
+        h = _gn(self.norm1, x, True)
         if temb is not None:
-            h = h + self.time_emb_proj(F.silu(temb))[:, :, None, None]
+            # conv1's bias rides on the time-embedding add (one elementwise pass instead of two)
+            tb = self.conv1.bias + self.time_emb_proj(F.silu(temb))
+            h = F.conv2d(h, self.conv1.weight, None, padding=1) + tb[:, :, None, None]
+        else:
+            h = self.conv1(h)
         h = self.conv2(_gn(self.norm2, h, True))
         return (self.conv_shortcut(x) if hasattr(self, "conv_shortcut") else x) + h
 
