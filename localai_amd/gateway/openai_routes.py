@@ -497,10 +497,12 @@ def build_router(state) -> APIRouter:
         for _ in range(max(1, int(req.get("n") or 1))):
             name = f"b64{_u.uuid4().hex}.png"
             dst = os.path.join(state.cfg.image_dir, name)
-            await lm.handle.GenerateImage(pb.GenerateImageRequest(
+            res = await lm.handle.GenerateImage(pb.GenerateImageRequest(
                 width=int(w or 512), height=int(h or 512), mode=int(req.get("mode") or 0), step=int(req.get("step") or 15),
                 seed=int(req.get("seed") or 0), positive_prompt=pos, negative_prompt=neg, dst=dst,
                 src=str(req.get("file") or "")))
+            if res is not None and not getattr(res, "success", True):
+                raise APIError(res.message or "image generation failed", 500)
             if req.get("response_format") == "b64_json":
                 with open(dst, "rb") as f:
                     out.append({"b64_json": base64.b64encode(f.read()).decode()})

@@ -71,5 +71,9 @@ class DiffusersServicer:
             p.save(img, request.dst)
 
     async def GenerateImage(self, request, context=None):
+        if request.src:
+            # backend.py feeds `src` to img2img / ControlNet pipelines; the native pipeline is txt2img only
+            return pb.Result(success=False, message="img2img (src) is not supported by the native SD pipeline; "
+                                                    "register an external diffusers backend for it")
         await asyncio.get_running_loop().run_in_executor(None, self._generate, request)
         return pb.Result(message="Media generated", success=True)

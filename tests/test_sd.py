@@ -101,6 +101,8 @@ def test_servicer_generate_image(pipe_dir, tmp_path):
         # EnableParameters=none: pipeline defaults (sample_size * 2 px for the two-level toy VAE)
         await sv.GenerateImage(pb.GenerateImageRequest(positive_prompt="a boat", width=40, height=32, step=1,
                                                        EnableParameters="none", seed=3, dst=dst + ".2.png"))
+        r = await sv.GenerateImage(pb.GenerateImageRequest(positive_prompt="a boat", src="in.png", dst=dst + ".3.png"))
+        assert not r.success and "img2img" in r.message
     asyncio.run(go())
     assert sv.cfg_scale == 5.0 and sv.pipe.sched.kind == "euler"
     assert Image.open(dst).size == (40, 32)
