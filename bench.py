@@ -7,8 +7,12 @@ each with a synthetic ~`--prompt-len`-token user message and `--max-tokens` gene
 tokens (ignore_eos, temperature 0, mirostat 0 -- SURVEY §6 / BASELINE.md).  W untimed
 warm-up waves, then exactly K timed waves bracketed by barrier + synchronize.
 
-Multi-GPU (torchrun, one process per GPU): data-parallel engine replicas (weak scaling:
-fixed per-GPU load), aggregate tokens/s = sum over ranks / max wall time over ranks.
+Multi-GPU: one process per GPU over RCCL.  `python bench.py --gpus N` starts the N ranks
+itself (a torch.distributed.run child launched BEFORE this process touches the GPU) unless it
+already runs under torchrun (RANK / WORLD_SIZE set).  --tp T groups consecutive ranks into
+tensor-parallel replicas of T GPUs (BASELINE config 3: --preset llama3-70b --tp 8); the
+N / T replicas are data-parallel (weak scaling: fixed load per replica), aggregate tokens/s =
+sum over replicas / max wall time over replicas.
 
 --mode http   : requests go through the real gateway (FastAPI app on the native C++ HTTP
                 server, or uvicorn with --server uvicorn) from out-of-process aiohttp SSE
@@ -31,6 +35,8 @@ METRIC = "output tokens/sec + p50 TTFT, /v1/chat/completions Llama-3-8B GGUF, 1/
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--tp", type=int, default=int(os.environ.get("BENCH_TP", 1)),
+                    help="tensor-parallel degree per replica (consecutive ranks); replicas = gpus / tp")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--concurrency", type=int, default=int(os.environ.get("BENCH_CONCURRENCY", 256)))
@@ -77,10 +83,27 @@ def percentile(xs, p):
     return xs[f] + (xs[c] - xs[f]) * (k - f)
 
 
+def spawn_ranks(args) -> int:
+    """Start N ranks (torch.distributed.run, 127.0.0.1 rendezvous) as a CHILD process and return
+    its exit code.  Called before this process imports torch or touches a GPU."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd, env=dict(os.environ, BENCH_SPAWNED="1"))
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args))
     loadgen = None
-    if args.mode == "http":
+    tp_env = max(1, args.tp)
+    if args.mode == "http" and int(os.environ.get("RANK", "0")) % tp_env == 0:
         # client processes are started before this process touches the GPU (no fork/exec
         # from a GPU-initialised process)
         from localai_amd.utils.loadgen import LoadGen
@@ -96,14 +119,35 @@ def main():
     backend = os.environ.get("BENCH_BACKEND", "nccl")
     ndev = torch.cuda.device_count()
     gpu = local % max(1, ndev)
+    if args.gpus > 1 and world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    tp = max(1, args.tp)
+    if world % tp:
+        raise SystemExit(f"--tp {tp} does not divide the {world} ranks")
+    if not torch.cuda.is_available():
+        backend = "gloo"  # CPU rehearsal of the multi-rank path
     if world > 1:
-        torch.cuda.set_device(gpu)
+        if torch.cuda.is_available():
+            torch.cuda.set_device(gpu)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device(f"cuda:{gpu}"))
         else:
             dist.init_process_group(backend)
     dev = f"cuda:{gpu}" if torch.cuda.is_available() else "cpu"  # cpu: dev smoke runs only
     red_dev = dev if backend == "nccl" else "cpu"  # gloo reduces host tensors
+    # replica = tp consecutive ranks; its first rank ("leader") drives the load and the timing
+    replica, tp_rank = rank // tp, rank % tp
+    leader = tp_rank == 0
+    tp_group = ctrl = None
+    leaders = None
+    if world > 1:
+        for r0 in range(0, world, tp):   # new_group is collective: every rank creates every group
+            g = dist.new_group(list(range(r0, r0 + tp))) if tp > 1 else None
+            c = dist.new_group(list(range(r0, r0 + tp)), backend="gloo") if tp > 1 else None
+            if r0 == replica * tp:
+                tp_group, ctrl = g, c
+        leaders = dist.new_group(list(range(0, world, tp)), backend="gloo")
+    n_rep = world // tp
 
     def sync():
         if dev != "cpu":
@@ -122,7 +166,14 @@ def main():
     t_gen = time.time() - t_gen
 
     from localai_amd.engine.llm_engine import EngineConfig, LLMEngine
+    from localai_amd.models.decoder import TPInfo
 
+    tpi = None
+    if tp > 1:
+        tpi = TPInfo(rank=tp_rank, world=tp, group=tp_group)
+        if dev != "cpu":
+            from localai_amd.parallel.custom_ar import maybe_create
+            tpi.car = maybe_create(tp_group, tp_rank, tp, dev)
     t0 = time.time()
     extra = {"decode_steps": args.decode_steps, "decode_steps_wide": args.decode_steps} if args.decode_steps else {}
     cfg = EngineConfig(model_path=path, device=dev, context_size=args.context,
@@ -130,7 +181,7 @@ def main():
                        max_batched_tokens=args.batch_tokens or max(8192, args.prompt_len * 8),
                        use_graphs=not args.no_graphs,
                        max_kv_tokens=args.concurrency * (args.prompt_len + args.max_tokens + 64) + 4096, **extra)
-    eng = LLMEngine(cfg)
+    eng = LLMEngine(cfg, tp=tpi, ctrl_group=ctrl)
     t_load = time.time() - t0
     t0 = time.time()
     eng.warmup()
@@ -140,7 +191,17 @@ def main():
         for k, v in sorted(ops._GEMM_CHOICE.items(), key=str):
             print(f"gemm choice M={k[0]} K={k[1]} ws={k[2]} -> {v}", file=sys.stderr)
 
-    msgs = user_messages(eng.tokenizer, args.concurrency, args.prompt_len, seed=rank)
+    if not leader:
+        # tensor-parallel follower: mirror the leader's steps until its engine shuts down
+        eng.run_follower()
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        if loadgen is not None:
+            loadgen.close()
+        return
+
+    msgs = user_messages(eng.tokenizer, args.concurrency, args.prompt_len, seed=replica)
     if args.mode == "http":
         runner = HttpRunner(eng, args, loadgen)
     else:
@@ -152,38 +213,43 @@ def main():
         # would let the engine's prefix cache skip ~90 % of the prefill of every repeated wave)
         return runner.wave([f"(wave {w}) " + m for m in msgs])
 
+    def lbarrier():
+        if leaders is not None:
+            dist.barrier(group=leaders)
+
     for w in range(args.warmup):
         wave(-1 - w)
     sync()
-    if world > 1:
-        dist.barrier()
+    lbarrier()
     sync()
     t0 = time.perf_counter()
     ttfts, tokens = [], 0
-    for s in range(args.steps):
-        tt, nt = wave(s)
+    for s_ in range(args.steps):
+        tt, nt = wave(s_)
         ttfts += tt
         tokens += nt
     sync()
-    if world > 1:
-        dist.barrier()
+    lbarrier()
     sync()
     elapsed = time.perf_counter() - t0
 
     all_ttft, tot_tokens, max_el = ttfts, tokens, elapsed
-    if world > 1:
-        el = torch.tensor([elapsed], device=red_dev)
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-        nt = torch.tensor([float(tokens)], device=red_dev)
-        dist.all_reduce(nt)
-        gathered = [None] * world
-        dist.all_gather_object(gathered, ttfts)
+    if leaders is not None and n_rep > 1:
+        el = torch.tensor([elapsed])
+        dist.all_reduce(el, op=dist.ReduceOp.MAX, group=leaders)
+        nt = torch.tensor([float(tokens)])
+        dist.all_reduce(nt, group=leaders)
+        gathered = [None] * n_rep
+        dist.all_gather_object(gathered, ttfts, group=leaders)
         all_ttft = [x for g in gathered for x in g]
         max_el, tot_tokens = float(el.item()), int(nt.item())
     runner.close()
+    if tp > 1 and args.mode == "engine":
+        eng.shutdown()   # releases the followers (HttpRunner.close already did)
     if rank == 0:
         value = tot_tokens / max_el
         seq = args.prompt_len + args.max_tokens
+        par = f"dp{n_rep}" + (f"xtp{tp}" if tp > 1 else "")
         out = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -199,17 +265,23 @@ def main():
             "data": "synthetic",
             "p50_ttft_ms": round(percentile(all_ttft, 50) * 1000, 2),
             "p90_ttft_ms": round(percentile(all_ttft, 90) * 1000, 2),
-            "config": {"model": "Llama-3-8B-Instruct GGUF Q4_K_M (random-init)" if args.preset == "llama3-8b"
-                       else args.preset, "global_batch": args.concurrency * world, "seq_len": seq,
+            "config": {"model": MODEL_NAMES.get(args.preset, args.preset),
+                       "global_batch": args.concurrency * n_rep, "seq_len": seq,
                        "prompt_tokens": args.prompt_len, "max_tokens": args.max_tokens,
-                       "parallelism": f"dp{world}", "endpoint": "/v1/chat/completions (stream)",
+                       "parallelism": par, "endpoint": "/v1/chat/completions (stream)",
                        "mode": args.mode, "sampling": "greedy, mirostat 0, ignore_eos",
                        **({"n_draft": args.n_draft} if args.n_draft else {})},
             "setup_s": {"model_gen": round(t_gen, 1), "load": round(t_load, 1), "graph_capture": round(t_capture, 1)},
         }
         print(json.dumps(out), flush=True)
     if world > 1:
+        dist.barrier()
         dist.destroy_process_group()
+
+
+MODEL_NAMES = {"llama3-8b": "Llama-3-8B-Instruct GGUF Q4_K_M (random-init)",
+               "llama3-70b": "Llama-3-70B-Instruct GGUF Q4_K_M (random-init)",
+               "mixtral-8x7b": "Mixtral-8x7B GGUF Q4_K_M (random-init)"}
 
 
 class EngineRunner:

@@ -154,8 +154,10 @@ class LLMEngine:
                 raise ValueError(f"mmproj projects to {self.clip.out_dim}, the LLM embeds {self.hp.n_embd}")
         self.ctx = cfg.context_size
         bs = cfg.block_size
-        if self.device.type == "cuda":
-            # prefill / big decode batches run hipBLASLt on bf16 copies: materialise before any graph capture
+        if self.device.type == "cuda" and not ops.TILE_GEMM:
+            # legacy path (LOCALAI_AMD_TILE_GEMM=0): prefill / big decode batches run hipBLASLt on
+            # bf16 copies, materialised before any graph capture.  The default path multiplies the
+            # quantised weights directly (gemm_q.hip) and keeps no copy.
             self._materialize_bf16()
         num_blocks = self._num_kv_blocks()
         if faults.hit("kv_alloc"):
@@ -424,11 +426,17 @@ class LLMEngine:
         if self.tp.world > 1:
             # replicated scheduling: every rank applies the leader's new work in the same order,
             # so all ranks build identical batches and sample identical tokens
+            # one int per step over the gloo control group; the pickled items only when there are
+            # any (most decode steps have none).  group_src: the leader is rank 0 of its replica's
+            # group, not necessarily global rank 0 (data-parallel x tensor-parallel layouts)
             import torch.distributed as dist
-            box = [[self._to_wire(it) for it in items] if self.leader else None]
-            dist.broadcast_object_list(box, src=0, group=self.ctrl)
-            if not self.leader:
-                items = [self._from_wire(w) for w in box[0]]
+            n = torch.tensor([len(items)], dtype=torch.int64)
+            dist.broadcast(n, group_src=0, group=self.ctrl)
+            if int(n.item()):
+                box = [[self._to_wire(it) for it in items] if self.leader else None]
+                dist.broadcast_object_list(box, group_src=0, group=self.ctrl)
+                if not self.leader:
+                    items = [self._from_wire(w) for w in box[0]]
         mm = [it for it in items if isinstance(it, tuple) and it[0] == "mm"]
         if len(mm) > 1 and self.clip is not None:
             # every image that arrived this step goes through the vision tower in shared batches

@@ -70,12 +70,17 @@ def lib():
             "la_moe_router": [P, I, P, I, I, I, I, I, F, I, I, P, P, P],
             "la_moe_gemm": [I, I, P, I, I, I, P, P, I, P, I, I, I, P, P, I, LNG, I, P],
             "la_qw_size": [],
+            "la_gemm_scales": [I, P, P, I, I, P, P],
+            "la_qgemm_tile": [I, P, P, P, I, I, P, I, I, I, P, I, LNG, I, I, I, P],
+            "la_qgemm_tile_probe": [P, P, I, I, P, I, I, P, I, I, P],
             "la_decode_advance": [P, P, P, P, P, P, I, I, I, P, I, P, P, P],
         }
         for name, args in sig.items():
             fn = getattr(L, name)
             fn.argtypes = args
             fn.restype = I
+        L.la_gemm_scales_bytes.argtypes = [I, I]
+        L.la_gemm_scales_bytes.restype = LNG
         gv = os.environ.get("LOCALAI_AMD_GEMV_VARIANT")
         if gv is not None:
             _check(L.la_gemv_variant(int(gv)), "la_gemv_variant")
@@ -118,6 +123,7 @@ class QWeight:
     ref: Optional[torch.Tensor] = None            # fp32 [N, K] (CPU path / oracle)
     bf16: Optional[torch.Tensor] = None           # optional HBM-resident bf16 copy (prefill GEMMs)
     dq: Optional[Tuple[torch.Tensor, torch.Tensor]] = None  # fragment-ordered Q4_K copy (gemm_dq.hip)
+    gsc: Optional[torch.Tensor] = None            # blocked per-(column, K-step) scale plane (gemm_q.hip)
 
     @property
     def device(self) -> torch.device:
@@ -212,6 +218,33 @@ class QWeight:
                                        self.N, self.K, qsw.data_ptr(), ssw.data_ptr(), _stream()), "la_dq_swizzle")
             self.dq = (qsw, ssw)
         return self.dq
+
+    @property
+    def tile_ok(self) -> bool:
+        """Can feed the quantised tile GEMM (gemm_q.hip)."""
+        return self.K % 256 == 0 and self.fmt in (FMT_Q4_K, FMT_Q6_K, FMT_Q8_0, FMT_BF16) and self.planes[0] is not None
+
+    def tile_planes(self) -> Tuple[int, Optional[int], Optional[int]]:
+        """(p0, p1, gsc) pointers for la_qgemm_tile; the 8-byte-per-(column, K-step) scale plane
+        is built on the device on first use (0.125 B per weight)."""
+        if self.fmt == FMT_BF16:
+            return _ptr(self.planes[0]), None, None
+        if self.gsc is None:
+            nbytes = int(lib().la_gemm_scales_bytes(self.N, self.K))
+            g = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+            if self.fmt == FMT_Q4_K:
+                if self.planes[2] is None:
+                    raise ValueError("Q4_K weight without its unpacked scale planes")
+                a, b = self.planes[2], self.planes[3]
+            elif self.fmt == FMT_Q6_K:
+                a, b = self.planes[2], self.planes[3]
+            else:
+                a, b = self.planes[1], None
+            _check(lib().la_gemm_scales(self.fmt, _ptr(a), _ptr(b), self.N, self.K, g.data_ptr(), _stream()),
+                   "la_gemm_scales")
+            self.gsc = g
+        p1 = _ptr(self.planes[1]) if self.fmt == FMT_Q6_K else None
+        return _ptr(self.planes[0]), p1, self.gsc.data_ptr()
 
     def dequant_f32(self) -> torch.Tensor:
         if self.ref is not None:
@@ -596,7 +629,34 @@ def fuse_bf16(ws: Sequence[QWeight]) -> Optional[torch.Tensor]:
     return fused
 
 
+_SCRATCH: dict = {}
+
+
+def _run_scratch_blas(x, ws, Ntot):
+    """Large-M (prefill chunk) GEMM: dequantise the weights into ONE per-device bf16 scratch
+    buffer (reused by every call, sized by the largest fused weight seen), then a library GEMM
+    on it -- the reference's own large-batch path (ggml convert.cu dequant + hipBLAS GemmEx,
+    SURVEY K7), without a persistent bf16 copy of the model.  The dequant streams the quantised
+    bytes once and writes 2 B/weight: ~6 % of a 8192-row chunk's GEMM time."""
+    K = x.shape[1]
+    need = Ntot * K
+    buf = _SCRATCH.get(x.device)
+    if buf is None or buf.numel() < need:
+        buf = _SCRATCH[x.device] = torch.empty(need, dtype=torch.bfloat16, device=x.device)
+    wt = buf[:need].view(Ntot, K)
+    row = 0
+    for w in ws:
+        if w.fmt == FMT_BF16:
+            wt[row:row + w.N].copy_(w.planes[0].view(torch.bfloat16).view(w.N, w.K))
+        else:
+            _check(lib().la_dequant(w.fmt, *w.ptrs(), w.N, w.K, wt[row:row + w.N].data_ptr(), _stream()), "la_dequant")
+        row += w.N
+    return torch.matmul(x, wt.t())
+
+
 def _run_blas(x, ws, Ntot):
+    if TILE_GEMM and all(w.bf16 is None for w in ws) and getattr(ws[0], "_fused_bf16", None) is None:
+        return _run_scratch_blas(x, ws, Ntot)
     if len(ws) == 1:
         return torch.matmul(x, ws[0].materialize_bf16().t())
     fused = getattr(ws[0], "_fused_bf16", None)
@@ -624,27 +684,85 @@ def _cold_caches(device):
     buf.sum()
 
 
-def _autotune_mid(x, ws, key, Ntot):
-    """Time hipBLASLt (bf16 copy) against the quantised mid-M kernel at a few split-K factors
-    with COLD weights (caches flushed before every timed call: warm timings favour the 3.6x
-    larger bf16 copy), and remember the winner.  The slab variant is charged for the extra
-    fp32 bytes its consumer reads (at ~4 TB/s)."""
+# Quantised tile GEMM (gemm_q.hip): the M > SKINNY_MAX_M path.  Tile ids: (BM, BN).
+GQ_TILES = {0: (256, 256), 1: (256, 128), 2: (128, 256), 3: (128, 128), 4: (256, 64), 5: (64, 256), 6: (256, 256),
+            7: (128, 256)}
+# LOCALAI_AMD_TILE_GEMM=0 restores the round-2 path (hipBLASLt on bf16 weight copies + qgemm_mid)
+TILE_GEMM = os.environ.get("LOCALAI_AMD_TILE_GEMM", "1") == "1"
+# M > MID_MAX_M (prefill chunks): "blas" = dequantise into a scratch buffer + library GEMM (faster
+# than the tile kernel at M = 8192 today: profiles/r3_gemm_tile.md), "tile" = the tile kernel
+PREFILL_GEMM = os.environ.get("LOCALAI_AMD_PREFILL_GEMM", "blas")
+
+
+def _tile_split_ok(K: int, S: int) -> bool:
+    ks = K // 64
+    return S >= 1 and -(-ks // S) * (S - 1) < ks
+
+
+def _run_tile(x, ws, S, out, Ntot, tile):
+    """out: fp32 slabs [S, M, Ntot], or a bf16 [M, Ntot] matrix (S == 1)."""
     M, K = x.shape
-    tiles = (22, 21) if M <= 128 else (42, 41, 22, 21)
-    cands = [("blas", 0, 0)] + [("mid", S, t) for t in tiles for S in (1, 2, 4, 8) if _mid_split_ok(K, S)]
-    if M > 128:
-        cands += [("ws", S, 0) for S in (1, 2, 4, 8) if _ws_ok(ws, K, S)]
-    if GEMM_DQ:
-        cands += [("dq", S, 0) for S in (1, 2, 4, 8) if _dq_ok(ws, K, S)]
+    bf = out.dtype == torch.bfloat16
+    esz = 2 if bf else 4
+    col = 0
+    for w in ws:
+        p0, p1, g = w.tile_planes()
+        _check(lib().la_qgemm_tile(w.fmt, p0, p1, g, w.N, w.K, x.data_ptr(), K, M, S, out.data_ptr() + col * esz,
+                                   Ntot, 0 if bf else M * Ntot, int(bf), tile, 0, _stream()), "la_qgemm_tile")
+        col += w.N
+
+
+def _tile_grid(M: int, N: int, tile: int) -> int:
+    bm, bn = GQ_TILES[tile]
+    return -(-M // bm) * -(-N // bn)
+
+
+def pick_tile(M: int, Ns: Sequence[int], K: int) -> Tuple[int, int]:
+    """Heuristic (tile, split-K) for shapes the autotuner has not seen (prefill chunks): the
+    largest tile that still gives >= ~192 workgroups, else split K up to ~256 workgroups with
+    every split >= 8 K-steps."""
+    N = max(Ns)
+    ks = K // 64
+    for tile in ((6, 1, 3) if M > 128 else (7, 3, 5)):
+        tiles = _tile_grid(M, N, tile)
+        if tiles >= 192:
+            return tile, 1
+    tile = 1 if M > 128 else 3
+    tiles = _tile_grid(M, N, tile)
+    S = max(1, min(ks // 8, round(256 / tiles)))
+    while S > 1 and not _tile_split_ok(K, S):
+        S -= 1
+    return tile, S
+
+
+def _autotune_mid(x, ws, key, Ntot):
+    """Time the tile GEMM's (tile, split-K) candidates with COLD weights (caches flushed before
+    every timed call, as in decode where each step streams the whole model once) and remember
+    the winner.  A split variant is charged for the extra fp32 bytes its consumer reads (at
+    ~4 TB/s).  LOCALAI_AMD_BLAS_CANDIDATE=1 adds hipBLASLt on a bf16 copy (A/B only)."""
+    M, K = x.shape
+    N = max(w.N for w in ws)
+    cands = []
+    if all(w.tile_ok for w in ws):
+        tiles = (6, 0, 1, 4) if M > 128 else (7, 2, 3, 5)
+        for t in tiles:
+            g = _tile_grid(M, N, t)
+            base = max(1, round(256 / g))
+            for S in sorted({max(1, base // 2), base, base * 2}):
+                if S <= K // 256 and _tile_split_ok(K, S):
+                    cands.append(("tile", S, t))
+    if not cands or os.environ.get("LOCALAI_AMD_BLAS_CANDIDATE") == "1" or not TILE_GEMM:
+        cands.append(("blas", 0, 0))
+    if not TILE_GEMM:
+        cands = [("blas", 0, 0)] + [("mid", S, t) for t in ((22, 21) if M <= 128 else (42, 41, 22, 21))
+                                    for S in (1, 2, 4, 8) if _mid_split_ok(K, S)]
     outs = {S: torch.empty(S, M, Ntot, dtype=torch.float32, device=x.device) for _, S, _ in cands if S}
-    best, best_t = ("blas", 0, 0), float("inf")
+    best, best_t = cands[0], float("inf")
     for kind, S, t in cands:
         if kind == "blas":
             fn = lambda: _run_blas(x, ws, Ntot)  # noqa: E731
-        elif kind == "ws":
-            fn = lambda S=S: _run_ws(x, ws, S, outs[S], Ntot)  # noqa: E731
-        elif kind == "dq":
-            fn = lambda S=S: _run_dq(x, ws, S, outs[S], Ntot)  # noqa: E731
+        elif kind == "tile":
+            fn = lambda S=S, t=t: _run_tile(x, ws, S, outs[S], Ntot, t)  # noqa: E731
         else:
             fn = lambda S=S, t=t: _run_mid(x, ws, S, outs[S], Ntot, t)  # noqa: E731
         fn()
@@ -668,8 +786,8 @@ def _autotune_mid(x, ws, key, Ntot):
 
 def linear(x: torch.Tensor, w: QWeight, bias: Optional[torch.Tensor] = None,
            out_slabs: Optional[torch.Tensor] = None, force: Optional[str] = None) -> Partial:
-    """y = x @ W^T.  x: [M, K] bf16.  GPU: M <= 64 -> skinny MFMA kernel on the quantised
-    weights; larger M -> hipBLASLt on the HBM-resident bf16 copy."""
+    """y = x @ W^T.  x: [M, K] bf16.  GPU: M <= 2 -> int8-dot GEMV, M <= 64 -> skinny MFMA
+    kernel, larger M -> the quantised tile GEMM (gemm_q.hip); all on the quantised weights."""
     return linear_multi(x, [w], bias, out_slabs, force)
 
 
@@ -690,29 +808,45 @@ def linear_multi(x: torch.Tensor, ws: Sequence[QWeight], bias: Optional[torch.Te
     skinny_ok = all(w.K % 256 == 0 for w in ws)
     use_skinny = (M <= SKINNY_MAX_M and skinny_ok) if force is None else force == "skinny"
     mid_ok = skinny_ok and all(w.fmt in MID_FMTS for w in ws)
-    S, tile, use_ws, use_dq = 0, 0, False, False
+    tile_ok = TILE_GEMM and all(w.tile_ok for w in ws)
+    S, tile, kind = 0, 0, None
     if force == "ws":
-        S, use_ws = 1, True
-    if force == "mid":
-        S = min(pick_mid_splits(w.N, w.K, M) for w in ws)
-    elif force is None and not use_skinny and M <= MID_MAX_M and mid_ok:
+        S, kind = 1, "ws"
+    elif force == "mid":
+        S, kind = min(pick_mid_splits(w.N, w.K, M) for w in ws), "mid"
+    elif force is not None and force.startswith("tile"):
+        # "tile" (heuristic) or "tile:<id>:<S>"
+        parts = force.split(":")
+        tile, S = (int(parts[1]), int(parts[2])) if len(parts) == 3 else pick_tile(M, [w.N for w in ws], K)
+        kind = "tile"
+    elif force is None and not use_skinny and M <= MID_MAX_M and (tile_ok or mid_ok):
         # one tuned choice per 32-row bucket: prefill chunk / decode batch sizes vary per step
         # and must not re-run the (cache-flushing) autotune inside the serving loop
         key = ((M + 31) // 32 * 32, K, tuple((w.fmt, w.N) for w in ws))
         choice = _GEMM_CHOICE.get(key)
         if choice is None and GEMM_AUTOTUNE and not torch.cuda.is_current_stream_capturing():
             choice = _autotune_mid(x, ws, key, Ntot)
-        if choice is not None and choice[0] in ("mid", "ws", "dq"):
-            S, tile = choice[1], choice[2]
-            use_ws = choice[0] == "ws"
-            use_dq = choice[0] == "dq"
+        if choice is None and tile_ok:
+            t, s_ = pick_tile(M, [w.N for w in ws], K)
+            choice = ("tile", s_, t)
+        if choice is not None and choice[0] in ("mid", "ws", "dq", "tile"):
+            kind, S, tile = choice
+    elif force is None and not use_skinny and tile_ok and PREFILL_GEMM == "tile":
+        tile, S = pick_tile(M, [w.N for w in ws], K)   # prefill: heuristic, never tuned inline
+        kind = "tile"
+    if kind == "tile" and S == 1 and M > MID_MAX_M and out_slabs is None:
+        y = torch.empty(M, Ntot, dtype=torch.bfloat16, device=x.device)
+        _run_tile(x, ws, 1, y, Ntot, tile)
+        return Partial(y, bias)
     if S:
         out = out_slabs
         if out is None or out.shape != (S, M, Ntot):
             out = torch.empty(S, M, Ntot, dtype=torch.float32, device=x.device)
-        if use_ws:
+        if kind == "tile":
+            _run_tile(x, ws, S, out, Ntot, tile)
+        elif kind == "ws":
             _run_ws(x, ws, S, out, Ntot)
-        elif use_dq:
+        elif kind == "dq":
             _run_dq(x, ws, S, out, Ntot)
         else:
             _run_mid(x, ws, S, out, Ntot, tile)

@@ -1,0 +1,565 @@
+// Quantised tile GEMM for batched decode (M = 65..256) and prefill (M up to a chunk of 8192):
+//   out[s][m][n] = sum_{k in split s} X[m,k] * W[n,k]     (fp32 split-K slabs, or bf16 [M][N] at S = 1)
+// W is read in its GGUF quantisation (Q4_K, Q6_K, Q8_0) or bf16; no dequantised copy of it
+// exists in HBM.  SURVEY §2.8 K6 (ggml mmq / dequant + BLAS, llama.cpp @ d5cb868 [external]).
+//
+// Design (MI355X, one workgroup per CU):
+//   * tile BM x BN x 64 (K-step), 4 or 8 waves, each wave owns a (BM/WM) x (BN/WN) sub-tile of
+//     v_mfma_f32_16x16x32_bf16 accumulators (acc[MT][NT], up to 8 x 4 = 128 AGPRs);
+//   * every operand arrives by LDS-DMA (global_load_lds_dwordx4): X as bf16 rows of 128 B,
+//     XOR-swizzled on the SOURCE address so the A-fragment ds_read_b128 is conflict-free; W as
+//     its raw quant bytes (32 B / column / K-step for Q4_K) plus an 8-byte scale record per
+//     column per K-step from a 16-column-blocked plane built once per weight (la_gemm_scales).
+//     W is therefore never expanded in LDS: each wave dequantises its own B fragments in
+//     registers (ggml dequantize_row_* arithmetic in fp32, rounded once to bf16: the same
+//     weights as the former hipBLASLt bf16 copy), each fragment feeding MT MFMAs;
+//   * an NS-slot LDS ring: the DMAs of K-step t+NS-1 are issued right after the barrier of step
+//     t, each wave then waits only for its OWN DMAs of step t+1 with a counted vmcnt (never 0
+//     in steady state), raw s_barrier (no __syncthreads: that drains vmcnt);
+//   * split-K over the grid; tile -> block mapping is XCD-aware (each XCD gets a contiguous run
+//     of tiles, M fastest, so the M tiles that share a weight panel share one L2);
+//   * Q6_K: the 64 k of a K-step are a permutation of the super-block's k (ql byte b of a
+//     64-byte half holds two k 64 apart): K-step (hh, part) covers k in
+//     [128hh + 32part, +32) and [128hh + 64 + 32part, +32); X is staged with the same
+//     permutation, so every K-step reads exactly 32 B of ql per column.
+#include "qweight.h"
+
+namespace la {
+
+constexpr int GQ_BK = 64;
+
+LA_DEV void gq_glds16(const void* g, void* l) {
+  __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)l, 16, 0, 0);
+}
+
+template <int N>
+LA_DEV void gq_vmwait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// Wait until at most `ahead` stages of L loads each are outstanding (ahead in 0..2).
+template <int L>
+LA_DEV void gq_wait_stages(int ahead) {
+  if (ahead <= 0) gq_vmwait<0>();
+  else if (ahead == 1) gq_vmwait<L>();
+  else if (ahead == 2) gq_vmwait<2 * L>();
+  else gq_vmwait<3 * L>();
+}
+
+// ---------------------------------------------------------------- per-format W staging
+// LDS W area of a slot: [codes][scales]; scales = one 8-byte record per column (BN x 8 B, at
+// least 1 KiB so one DMA piece always fits).
+template <int FMT, int BN> struct GqW;
+
+template <int BN> struct GqScales {
+  static constexpr int BYTES = (BN * 8 > 1024) ? BN * 8 : 1024;
+  static constexpr int PIECES = (BN * 8 + 1023) / 1024;
+  // plane: [ceil(N/16)][K/64][16][8 B]; piece q covers columns 128q .. 128q+127 of the tile
+  LA_DEV static void issue(const uint8_t* gsc, int nblk, int KS, int n0, int q, int ks, uint8_t* dst, int lane) {
+    const int b = min((n0 >> 4) + 8 * q + (lane >> 3), nblk - 1);
+    gq_glds16(gsc + ((size_t)b * KS + ks) * 128 + 16 * (lane & 7), dst + q * 1024);
+  }
+};
+
+// 32 B per column per K-step, 16-B halves swapped on columns with bit 3 set (conflict-free
+// ds_read_b64 for lanes (n = l & 15, g = l >> 4) reading 8 B at logical offset 8g)
+LA_DEV void gq_issue32(const uint8_t* plane, int row_bytes, int N, int n0, int p, int kofs, uint8_t* dst, int lane) {
+  const int c = 32 * p + (lane >> 1);
+  const int n = min(n0 + c, N - 1);
+  const int lh = (lane & 1) ^ ((c >> 3) & 1);
+  gq_glds16(plane + (size_t)n * row_bytes + kofs + 16 * lh, dst + p * 1024);
+}
+LA_DEV u32x2 gq_read32(const uint8_t* area, int col, int g) {
+  return *(const u32x2*)(area + col * 32 + 16 * ((g >> 1) ^ ((col >> 3) & 1)) + 8 * (g & 1));
+}
+
+template <int BN> struct GqW<FMT_Q4_K, BN> {
+  static constexpr int CODES = BN * 32;
+  static constexpr int LDS = CODES + GqScales<BN>::BYTES;
+  static constexpr int PC = BN / 32;
+  static constexpr int PIECES = PC + GqScales<BN>::PIECES;
+  LA_DEV static void issue(const QW& w, int n0, int p, int ks, uint8_t* wl, int lane) {
+    if (p < PC) gq_issue32(w.p0, w.K >> 1, w.N, n0, p, 32 * ks, wl, lane);
+    else GqScales<BN>::issue(w.p2, (w.N + 15) >> 4, w.K >> 6, n0, p - PC, ks, wl + CODES, lane);
+  }
+  struct Frag {
+    u32x2 q;
+    float D[2], Mn[2];
+  };
+  LA_DEV static void load(const uint8_t* wl, int col, int g, int, Frag& f) {
+    f.q = gq_read32(wl, col, g);
+    const u32x2 s = *(const u32x2*)(wl + CODES + col * 8);
+    const float d = h2f(s.x & 0xFFFFu), dm = h2f(s.x >> 16);
+    f.D[0] = d * (float)(s.y & 0xFFu);
+    f.Mn[0] = -dm * (float)((s.y >> 8) & 0xFFu);
+    f.D[1] = d * (float)((s.y >> 16) & 0xFFu);
+    f.Mn[1] = -dm * (float)(s.y >> 24);
+  }
+  template <int S>
+  LA_DEV static bf16x8 deq(const Frag& f) {
+    uint32_t lo, hi;
+    // opaque masks keep one v_cvt_f32_ubyteN per weight (see gemm_dq.hip)
+    if constexpr (S == 0) {
+      asm("v_and_b32 %0, 0x0f0f0f0f, %1" : "=v"(lo) : "v"(f.q.x));
+      asm("v_and_b32 %0, 0x0f0f0f0f, %1" : "=v"(hi) : "v"(f.q.y));
+    } else {
+      asm("v_and_b32 %0, 0x0f0f0f0f, %1" : "=v"(lo) : "v"(f.q.x >> 4));
+      asm("v_and_b32 %0, 0x0f0f0f0f, %1" : "=v"(hi) : "v"(f.q.y >> 4));
+    }
+    bf16x8 r;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      r[b] = (bf16)fmaf(f.D[S], (float)((lo >> (8 * b)) & 0xFFu), f.Mn[S]);
+      r[b + 4] = (bf16)fmaf(f.D[S], (float)((hi >> (8 * b)) & 0xFFu), f.Mn[S]);
+    }
+    return r;
+  }
+};
+
+template <int BN> struct GqW<FMT_Q6_K, BN> {
+  static constexpr int CODES = BN * 64;  // ql [BN][32] then qh [BN][32]
+  static constexpr int LDS = CODES + GqScales<BN>::BYTES;
+  static constexpr int PC = BN / 32;
+  static constexpr int PIECES = 2 * PC + GqScales<BN>::PIECES;
+  LA_DEV static void issue(const QW& w, int n0, int p, int ks, uint8_t* wl, int lane) {
+    const int sb = ks >> 2, hh = (ks >> 1) & 1, part = ks & 1;
+    if (p < PC) gq_issue32(w.p0, w.K >> 1, w.N, n0, p, sb * 128 + 64 * hh + 32 * part, wl, lane);
+    else if (p < 2 * PC) gq_issue32(w.p1, w.K >> 2, w.N, n0, p - PC, sb * 64 + 32 * hh, wl + BN * 32, lane);
+    else GqScales<BN>::issue(w.p2, (w.N + 15) >> 4, w.K >> 6, n0, p - 2 * PC, ks, wl + CODES, lane);
+  }
+  struct Frag {
+    u32x2 ql, qh;
+    float S[2];
+    int sh;  // qh bit offset of this K-step's part
+  };
+  LA_DEV static void load(const uint8_t* wl, int col, int g, int ks, Frag& f) {
+    f.ql = gq_read32(wl, col, g);
+    f.qh = gq_read32(wl + BN * 32, col, g);
+    const u32x2 s = *(const u32x2*)(wl + CODES + col * 8);
+    const float d = h2f(s.x & 0xFFFFu);
+    const int i = g >> 1;  // 16-k scale group inside each 32-k run
+    f.S[0] = d * (float)(int8_t)((s.y >> (8 * i)) & 0xFFu);
+    f.S[1] = d * (float)(int8_t)((s.y >> (8 * (2 + i))) & 0xFFu);
+    f.sh = 2 * (ks & 1);
+  }
+  template <int S>
+  LA_DEV static bf16x8 deq(const Frag& f) {
+    bf16x8 r;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t l = (j < 4) ? f.ql.x : f.ql.y, h = (j < 4) ? f.qh.x : f.qh.y;
+      const int b = 8 * (j & 3);
+      const int q = (int)(((l >> (b + 4 * S)) & 0xFu) | (((h >> (b + f.sh + 4 * S)) & 3u) << 4)) - 32;
+      r[j] = (bf16)(f.S[S] * (float)q);
+    }
+    return r;
+  }
+};
+
+template <int BN> struct GqW<FMT_Q8_0, BN> {
+  static constexpr int CODES = BN * 64;
+  static constexpr int LDS = CODES + GqScales<BN>::BYTES;
+  static constexpr int PC = BN / 16;
+  static constexpr int PIECES = PC + GqScales<BN>::PIECES;
+  LA_DEV static void issue(const QW& w, int n0, int p, int ks, uint8_t* wl, int lane) {
+    if (p < PC) {
+      const int c = 16 * p + (lane >> 2);
+      const int n = min(n0 + c, w.N - 1);
+      const int lc = (lane & 3) ^ ((c >> 2) & 3);
+      gq_glds16(w.p0 + (size_t)n * w.K + 64 * ks + 16 * lc, wl + p * 1024);
+    } else {
+      GqScales<BN>::issue(w.p2, (w.N + 15) >> 4, w.K >> 6, n0, p - PC, ks, wl + CODES, lane);
+    }
+  }
+  struct Frag {
+    u32x2 q[2];
+    float d[2];
+  };
+  LA_DEV static void load(const uint8_t* wl, int col, int g, int, Frag& f) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int lc = 2 * s + (g >> 1);
+      f.q[s] = *(const u32x2*)(wl + col * 64 + 16 * (lc ^ ((col >> 2) & 3)) + 8 * (g & 1));
+    }
+    const uint32_t s = *(const uint32_t*)(wl + CODES + col * 8);
+    f.d[0] = h2f(s & 0xFFFFu);
+    f.d[1] = h2f(s >> 16);
+  }
+  template <int S>
+  LA_DEV static bf16x8 deq(const Frag& f) {
+    bf16x8 r;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t v = (j < 4) ? f.q[S].x : f.q[S].y;
+      r[j] = (bf16)(f.d[S] * (float)(int8_t)((v >> (8 * (j & 3))) & 0xFFu));
+    }
+    return r;
+  }
+};
+
+template <int BN> struct GqW<FMT_BF16, BN> {
+  static constexpr int LDS = BN * 128;
+  static constexpr int PIECES = BN / 8;
+  LA_DEV static void issue(const QW& w, int n0, int p, int ks, uint8_t* wl, int lane) {
+    const int c = 8 * p + (lane >> 3);
+    const int n = min(n0 + c, w.N - 1);
+    const int lc = (lane & 7) ^ ((c >> 1) & 7);
+    gq_glds16(w.p0 + ((size_t)n * w.K + 64 * ks + 8 * lc) * 2, wl + p * 1024);
+  }
+  struct Frag {
+    bf16x8 v[2];
+  };
+  LA_DEV static void load(const uint8_t* wl, int col, int g, int, Frag& f) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) f.v[s] = *(const bf16x8*)(wl + col * 128 + 16 * ((4 * s + g) ^ ((col >> 1) & 7)));
+  }
+  template <int S>
+  LA_DEV static bf16x8 deq(const Frag& f) {
+    return f.v[S];
+  }
+};
+
+// ---------------------------------------------------------------- kernel
+// ABL (probe builds only): bit0 no MFMA, bit1 no dequant arithmetic, bit2 no X DMA, bit3 no W DMA.
+template <int FMT, int BM, int BN, int WM, int WN, int NS, int ABL = 0>
+__global__ __launch_bounds__(WM* WN * 64, 1) void qgemm_tile_kernel(
+    QW w, const bf16* __restrict__ X, int ldx, int M, int per_split, int m_tiles, int n_tiles, int splits,
+    int real_tiles, float* __restrict__ out, bf16* __restrict__ outb, int ldo, long slab) {
+  using WS = GqW<FMT, BN>;
+  constexpr int NW = WM * WN;
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int MT = TM / 16, NT = TN / 16;
+  constexpr int XB = BM * 128;            // X bytes per slot
+  constexpr int SLOT = XB + WS::LDS;
+  constexpr int PX = BM / 8 / NW;         // X DMA pieces per wave per stage
+  constexpr int PW = WS::PIECES;
+  constexpr int PWA = PW / NW, PWR = PW % NW;  // waves < PWR issue one more W piece
+  constexpr int LA = PX + PWA + 1, LB = PX + PWA;
+  static_assert(BM % (8 * NW) == 0 && MT >= 1 && NT >= 1 && TM % 16 == 0 && TN % 16 == 0, "tile shape");
+  static_assert(NS >= 2 && NS <= 4, "ring depth");
+  __shared__ __attribute__((aligned(1024))) uint8_t lds[NS * SLOT];
+
+  // XCD-aware tile order: blocks b, b + 8, ... share an XCD; each XCD takes a contiguous run
+  const int nwg = gridDim.x;
+  const int xcd = blockIdx.x & 7, q8 = nwg >> 3;
+  const int tile = xcd * q8 + (blockIdx.x >> 3);
+  if (tile >= real_tiles) return;  // grid padded to a multiple of 8
+  const int mt_i = tile % m_tiles;
+  const int rest = tile / m_tiles;
+  const int nt_i = rest % n_tiles;
+  const int split = rest / n_tiles;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+  const int m0 = mt_i * BM, n0 = nt_i * BN;
+  const int KS = w.K / GQ_BK;
+  const int ks0 = split * per_split;
+  const int nk = min(KS, ks0 + per_split) - ks0;
+  if (nk <= 0) return;
+
+  // X DMA: piece j of this wave = rows 8(wave*PX + j) .. +8; lane -> (row, physical 16-B chunk)
+  uint32_t xoff[PX];
+#pragma unroll
+  for (int j = 0; j < PX; ++j) {
+    const int r = 8 * (wave * PX + j) + (lane >> 3);
+    const int c = (lane & 7) ^ ((r >> 1) & 7);  // logical chunk stored at this physical chunk
+    const int kc = (FMT == FMT_Q6_K) ? (8 * (c & 3) + 64 * (c >> 2)) : 8 * c;
+    xoff[j] = (uint32_t)min(m0 + r, M - 1) * ldx + kc;
+  }
+  auto xk_of = [&](int ks) -> int {
+    if constexpr (FMT == FMT_Q6_K) return 256 * (ks >> 2) + 128 * ((ks >> 1) & 1) + 32 * (ks & 1);
+    else return 64 * ks;
+  };
+  auto issue = [&](int t) {
+    const int ks = ks0 + t;
+    uint8_t* sl = lds + (t % NS) * SLOT;
+    if constexpr (!(ABL & 4)) {
+      const bf16* xk = X + xk_of(ks);
+#pragma unroll
+      for (int j = 0; j < PX; ++j) gq_glds16(xk + xoff[j], sl + (wave * PX + j) * 1024);
+    }
+    if constexpr (!(ABL & 8)) {
+#pragma unroll
+      for (int j = 0; j < PWA; ++j) WS::issue(w, n0, wave + NW * j, ks, sl + XB, lane);
+      if constexpr (PWR > 0) {
+        if (wave < PWR) WS::issue(w, n0, wave + NW * PWA, ks, sl + XB, lane);
+      }
+    }
+  };
+
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int a = 0; a < MT; ++a)
+#pragma unroll
+    for (int b = 0; b < NT; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int r16 = lane & 15, g = lane >> 4;
+  auto compute = [&](int t) {
+    const uint8_t* sl = lds + (t % NS) * SLOT;
+    const uint8_t* wl = sl + XB;
+    const int ks = ks0 + t;
+    typename WS::Frag f[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) WS::load(wl, wn * TN + nt * 16 + r16, g, ks, f[nt]);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      // all A fragments of this k32 sub-step first (one lgkmcnt wait per MFMA group, not per
+      // pair of reads), then the B fragments (dequantised in registers), then the MFMAs
+      bf16x8 a[MT], b[NT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int row = wm * TM + mt * 16 + r16;
+        a[mt] = *(const bf16x8*)(sl + row * 128 + 16 * ((4 * s + g) ^ ((row >> 1) & 7)));
+      }
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        if constexpr (ABL & 2) {
+          b[nt] = __builtin_bit_cast(bf16x8, u32x4{f[nt].q.x, f[nt].q.y, (uint32_t)s, 0u});
+        } else if (s == 0) {
+          b[nt] = WS::template deq<0>(f[nt]);
+        } else {
+          b[nt] = WS::template deq<1>(f[nt]);
+        }
+      }
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+          if constexpr (ABL & 1) {
+            acc[mt][nt][0] += (float)a[mt][nt & 7] * (float)b[nt][mt & 7];
+          } else {
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mt], b[nt], acc[mt][nt], 0, 0, 0);
+          }
+        }
+      }
+    }
+  };
+
+  constexpr int D = NS - 1;  // stages in flight ahead of the one being computed
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+    if (i < nk) issue(i);
+  const bool wa = wave < PWR;
+  for (int t = 0; t < nk; ++t) {
+    const int ahead = min(D - 1, nk - 1 - t);  // stages after t already issued
+    if (wa) gq_wait_stages<LA>(ahead);
+    else gq_wait_stages<LB>(ahead);
+    if constexpr (!(ABL & 32)) __builtin_amdgcn_s_barrier();  // every wave's DMAs of step t landed; slot (t-1) % NS free
+    asm volatile("" ::: "memory");
+    if (t + D < nk) issue(t + D);
+    compute(t);
+  }
+
+  // epilogue through LDS: acc[mt][nt][i] is (row wm*TM + 16mt + 4g + i, col wn*TN + 16nt + r16);
+  // each wave parks 64 rows x TN of its tile at a time in a private padded [64][TN + 4] f32 image,
+  // then every lane stores 16 contiguous bytes of one row (f32) or 8 (bf16): whole 256-B row
+  // segments per store instruction instead of 16 x 4 B pieces.
+  if constexpr (ABL & 64) {
+    // probe: keep the accumulators live, store nothing
+    float t = 0.f;
+#pragma unroll
+    for (int a = 0; a < MT; ++a)
+#pragma unroll
+      for (int b = 0; b < NT; ++b) t += acc[a][b][0] + acc[a][b][3];
+    if (t == 1.2345f) out[0] = t;
+    return;
+  }
+  constexpr int EW = TN + 4;                 // f32 per image row (pad: 4-row lane groups hit distinct banks)
+  constexpr int ERF = (NS * SLOT) / (NW * EW * 4) / 16 * 16;  // rows that fit per wave
+  constexpr int ER = ERF < 64 ? (ERF < TM ? ERF : TM) : (TM < 64 ? TM : 64);  // rows per pass
+  constexpr int EP = (TM + ER - 1) / ER;     // passes
+  static_assert(ER >= 16 && NW * ER * EW * 4 <= NS * SLOT, "epilogue image exceeds the ring");
+  __builtin_amdgcn_s_barrier();              // every wave has finished reading the ring
+  asm volatile("" ::: "memory");
+  float* img = (float*)lds + wave * ER * EW;
+  const bool f32out = outb == nullptr;
+  float* o = f32out ? out + (size_t)split * slab : nullptr;
+#pragma unroll
+  for (int pass = 0; pass < EP; ++pass) {
+#pragma unroll
+    for (int mt = pass * (ER / 16); mt < min(MT, (pass + 1) * (ER / 16)); ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) img[((mt % (ER / 16)) * 16 + 4 * g + i) * EW + nt * 16 + r16] = acc[mt][nt][i];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const int rows = min(ER, TM - pass * ER);
+    const int rbase = m0 + wm * TM + pass * ER;
+    const int cbase = n0 + wn * TN;
+    constexpr int CH = TN / 4;               // 16-B (4 x f32) chunks per row
+#pragma unroll
+    for (int it = 0; it < (ER * CH + 63) / 64; ++it) {
+      const int idx = it * 64 + lane;
+      const int r = idx / CH, c4 = idx % CH;
+      if (r < rows) {
+        const f32x4 v = *(const f32x4*)(img + r * EW + 4 * c4);
+        const int m = rbase + r, n = cbase + 4 * c4;
+        if (m < M) {
+          if (n + 3 < w.N) {
+            if (f32out) {
+              *(f32x4*)(o + (size_t)m * ldo + n) = v;
+            } else {
+              bf16x4 bv;
+              bv[0] = (bf16)v[0]; bv[1] = (bf16)v[1]; bv[2] = (bf16)v[2]; bv[3] = (bf16)v[3];
+              *(bf16x4*)(outb + (size_t)m * ldo + n) = bv;
+            }
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              if (n + e < w.N) {
+                if (f32out) o[(size_t)m * ldo + n + e] = v[e];
+                else outb[(size_t)m * ldo + n + e] = (bf16)v[e];
+              }
+          }
+        }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+}
+
+// Blocked scale plane for the tile GEMM: [ceil(N/16)][K/64][16 cols][8 B], one record per
+// (column, K-step).  Rows past N repeat row N-1.
+//   Q4_K: f16 d, f16 dmin, u8 sc, u8 m (sub-block 2(ks%4)), u8 sc, u8 m (sub-block 2(ks%4)+1)
+//         from the unpacked scm [N][K/256][16] and dd [N][K/256][2 x f16] planes
+//   Q6_K: f16 d, 2 B pad, i8 sc x4 = the 16-k groups of the K-step's two 32-k runs
+//   Q8_0: f16 d of the two 32-blocks, 4 B pad
+__global__ void gemm_scales_kernel(int fmt, const uint8_t* __restrict__ a, const uint8_t* __restrict__ b, int N,
+                                   int K, uint8_t* __restrict__ outp) {
+  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int KS = K >> 6;
+  const int NB = (N + 15) >> 4;
+  if (gid >= (long)NB * KS * 16) return;
+  const int c = (int)(gid & 15);
+  const long r = gid >> 4;
+  const int ks = (int)(r % KS), nb = (int)(r / KS);
+  const int n = min(nb * 16 + c, N - 1);
+  const int sb = ks >> 2;
+  uint32_t x = 0, y = 0;
+  if (fmt == FMT_Q4_K) {
+    const uint8_t* s = a + ((size_t)n * (K >> 8) + sb) * 16 + 4 * (ks & 3);  // sc, m, sc, m
+    x = *(const uint32_t*)(b + ((size_t)n * (K >> 8) + sb) * 4);             // d, dmin
+    y = (uint32_t)s[0] | ((uint32_t)s[1] << 8) | ((uint32_t)s[2] << 16) | ((uint32_t)s[3] << 24);
+  } else if (fmt == FMT_Q6_K) {
+    const int hh = (ks >> 1) & 1, part = ks & 1;
+    const uint8_t* s = a + (size_t)n * (K >> 4) + sb * 16 + 8 * hh + 2 * part;
+    x = *(const uint16_t*)(b + ((size_t)n * (K >> 8) + sb) * 2);
+    y = (uint32_t)s[0] | ((uint32_t)s[1] << 8) | ((uint32_t)s[4] << 16) | ((uint32_t)s[5] << 24);
+  } else {  // Q8_0: d plane [N][K/32] f16
+    x = *(const uint32_t*)(a + ((size_t)n * (K >> 5) + 2 * ks) * 2);
+  }
+  *(u32x2*)(outp + gid * 8) = u32x2{x, y};
+}
+
+template <int FMT, int BM, int BN, int WM, int WN, int NS, int ABL = 0>
+static void gq_launch(const QW& w, const bf16* X, int ldx, int M, int splits, float* out, bf16* outb, int ldo,
+                      long slab, hipStream_t st) {
+  const int KS = w.K / GQ_BK;
+  const int per = (KS + splits - 1) / splits;
+  const int m_tiles = (M + BM - 1) / BM, n_tiles = (w.N + BN - 1) / BN;
+  const int real = m_tiles * n_tiles * splits;
+  const int grid = (real + 7) / 8 * 8;
+  hipLaunchKernelGGL((qgemm_tile_kernel<FMT, BM, BN, WM, WN, NS, ABL>), dim3(grid), dim3(WM * WN * 64), 0, st, w, X,
+                     ldx, M, per, m_tiles, n_tiles, splits, real, out, outb, ldo, slab);
+}
+
+// tile ids (shared with ops/__init__.py GQ_TILES):
+//   0: 256 x 256 (8 waves 2x4)   1: 256 x 128 (8 waves 2x4)   2: 128 x 256 (8 waves 2x4)
+//   3: 128 x 128 (4 waves 2x2)   4: 256 x 64 (4 waves 4x1)    5: 64 x 256 (4 waves 1x4)
+//   6: 256 x 256 (8 waves 1x8: one dequantised B fragment feeds 16 MFMAs, A reads double)
+//   7: 128 x 256 (8 waves 1x8)
+template <int FMT, int ABL = 0>
+static int gq_dispatch(int tile, const QW& w, const bf16* X, int ldx, int M, int splits, float* out, bf16* outb,
+                       int ldo, long slab, hipStream_t st) {
+  // 3 slots where they fit in 160 KiB, else 2
+  constexpr int X1 = (ABL & 16) ? 1 : 0;  // probe: one more ring slot where it fits
+  constexpr int NS0 = ((256 * 128 + GqW<FMT, 256>::LDS) * (3 + X1) <= 163840) ? 3 + X1 : 2;
+  constexpr int NS1 = ((256 * 128 + GqW<FMT, 128>::LDS) * (3 + X1) <= 163840) ? 3 + X1 : 2;
+  constexpr int NS2 = ((128 * 128 + GqW<FMT, 256>::LDS) * (3 + X1) <= 163840) ? 3 + X1 : 2;
+  constexpr int NS3 = ((128 * 128 + GqW<FMT, 128>::LDS) * (3 + X1) <= 163840) ? 3 + X1 : 2;
+  switch (tile) {
+    case 0: gq_launch<FMT, 256, 256, 2, 4, NS0, ABL>(w, X, ldx, M, splits, out, outb, ldo, slab, st); break;
+    case 1: gq_launch<FMT, 256, 128, 2, 4, NS1, ABL>(w, X, ldx, M, splits, out, outb, ldo, slab, st); break;
+    case 2: gq_launch<FMT, 128, 256, 2, 4, NS2, ABL>(w, X, ldx, M, splits, out, outb, ldo, slab, st); break;
+    case 3: gq_launch<FMT, 128, 128, 2, 2, NS3, ABL>(w, X, ldx, M, splits, out, outb, ldo, slab, st); break;
+    case 4: gq_launch<FMT, 256, 64, 4, 1, 3, ABL>(w, X, ldx, M, splits, out, outb, ldo, slab, st); break;
+    case 5: gq_launch<FMT, 64, 256, 1, 4, 3, ABL>(w, X, ldx, M, splits, out, outb, ldo, slab, st); break;
+    case 6: gq_launch<FMT, 256, 256, 1, 8, NS0, ABL>(w, X, ldx, M, splits, out, outb, ldo, slab, st); break;
+    case 7: gq_launch<FMT, 128, 256, 1, 8, NS2, ABL>(w, X, ldx, M, splits, out, outb, ldo, slab, st); break;
+    default: return -1;
+  }
+  return 0;
+}
+
+}  // namespace la
+
+// C ABI ---------------------------------------------------------------------------
+extern "C" long la_gemm_scales_bytes(int N, int K) { return (long)((N + 15) / 16) * (K / 64) * 128; }
+
+// Build the blocked scale plane: Q4_K (a = scm, b = dd), Q6_K (a = sc, b = d), Q8_0 (a = d).
+extern "C" int la_gemm_scales(int fmt, const void* a, const void* b, int N, int K, void* outp, void* stream) {
+  using namespace la;
+  if (N < 1 || (K & 255) || !a || !outp) return -1;
+  if (fmt != FMT_Q4_K && fmt != FMT_Q6_K && fmt != FMT_Q8_0) return -2;
+  const long total = (long)((N + 15) / 16) * (K / 64) * 16;
+  hipLaunchKernelGGL(gemm_scales_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream, fmt,
+                     (const uint8_t*)a, (const uint8_t*)b, N, K, (uint8_t*)outp);
+  return (int)hipGetLastError();
+}
+
+// out: fp32 slabs [splits][M][ldo] (slab stride `slab`), or bf16 [M][ldo] when out_bf16 (splits == 1).
+// p0/p1: format planes (Q4_K: qs, -; Q6_K: ql, qh; Q8_0: qs, -; BF16: w), gsc: la_gemm_scales plane.
+// Every split must own >= 1 K-step: ceil(KS / splits) * (splits - 1) < KS.
+extern "C" int la_qgemm_tile(int fmt, const void* p0, const void* p1, const void* gsc, int N, int K, const void* X,
+                             int ldx, int M, int splits, void* out, int ldo, long slab, int out_bf16, int tile,
+                             int abl, void* stream) {
+  using namespace la;
+  if (M < 1 || N < 1 || (K & 255) || splits < 1 || ldo < N || ldx < K || (ldx & 7)) return -1;
+  if (out_bf16 && splits != 1) return -1;
+  if (!out_bf16 && slab < (long)M * ldo) return -1;
+  if ((long)M * ldx >= (1L << 31)) return -1;  // 32-bit X offsets
+  const int KS = K / 64, per = (KS + splits - 1) / splits;
+  if (per * (splits - 1) >= KS) return -1;
+  if (fmt != FMT_BF16 && !gsc) return -1;
+  QW w{(const uint8_t*)p0, (const uint8_t*)p1, (const uint8_t*)gsc, nullptr, N, K};
+  hipStream_t st = (hipStream_t)stream;
+  const bf16* x = (const bf16*)X;
+  float* o = out_bf16 ? nullptr : (float*)out;
+  bf16* ob = out_bf16 ? (bf16*)out : nullptr;
+  int rc = -2;
+#define GQ_CASE(F)                                                           \
+  case F:                                                                    \
+    if (abl == 0) rc = gq_dispatch<F, 0>(tile, w, x, ldx, M, splits, o, ob, ldo, slab, st); \
+    else return -3;                                                          \
+    break;
+  switch (fmt) {
+    GQ_CASE(FMT_Q4_K)
+    GQ_CASE(FMT_Q6_K)
+    GQ_CASE(FMT_Q8_0)
+    GQ_CASE(FMT_BF16)
+    default: return -2;
+  }
+#undef GQ_CASE
+  if (rc) return rc;
+  return (int)hipGetLastError();
+}
+
+// probe entry (scripts/gq_probe.py): Q4_K tile 0 / 1 with ablation bits; fp32 slabs, ldx = K, ldo = N
+extern "C" int la_qgemm_tile_probe(const void* p0, const void* gsc, int N, int K, const void* X, int M, int splits,
+                                   void* out, int tile, int abl, void* stream) {
+  using namespace la;
+  QW w{(const uint8_t*)p0, nullptr, (const uint8_t*)gsc, nullptr, N, K};
+  const long slab = (long)M * N;
+  hipStream_t st = (hipStream_t)stream;
+  const bf16* x = (const bf16*)X;
+  float* o = (float*)out;
+#define GQ_PROBE(A) \
+  case A: return gq_dispatch<FMT_Q4_K, A>(tile, w, x, K, M, splits, o, nullptr, N, slab, st) ? -1 : (int)hipGetLastError();
+  switch (abl) {
+    GQ_PROBE(1) GQ_PROBE(2) GQ_PROBE(3) GQ_PROBE(4) GQ_PROBE(8) GQ_PROBE(12) GQ_PROBE(15) GQ_PROBE(16)
+    GQ_PROBE(32) GQ_PROBE(47) GQ_PROBE(64) GQ_PROBE(79) GQ_PROBE(111)
+    default: return -1;
+  }
+#undef GQ_PROBE
+}

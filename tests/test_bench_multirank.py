@@ -1,0 +1,51 @@
+"""bench.py's multi-GPU launch contract, rehearsed on the CPU over gloo: `--gpus N` starts its
+own N ranks (a torch.distributed.run child), data-parallel replicas report one aggregate JSON
+line with n_gpus = N, and `--tp` groups ranks into tensor-parallel replicas."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench(tmp_path, *extra):
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", MASTER_ADDR="127.0.0.1")
+    env.pop("WORLD_SIZE", None)
+    env.pop("RANK", None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--preset", "tiny-llama", "--steps", "1", "--warmup", "1",
+           "--concurrency", "4", "--prompt-len", "16", "--max-tokens", "8", "--context", "256",
+           "--cache-dir", str(tmp_path), "--clients", "1", *extra]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("mode", ["engine", "http"])
+def test_bench_gpus2_data_parallel(tmp_path, mode):
+    out = _bench(tmp_path, "--gpus", "2", "--mode", mode)
+    assert out["n_gpus"] == 2
+    assert out["config"]["parallelism"] == "dp2"
+    assert out["config"]["global_batch"] == 8
+    assert out["steps"] == 1 and out["warmup"] == 1
+    # 2 replicas x 4 requests x 8 tokens in the timed wave
+    assert out["value"] > 0 and out["ms_per_step"] > 0
+    assert out["value"] * out["ms_per_step"] / 1000 == pytest.approx(64, rel=1e-3)
+
+
+def test_bench_tensor_parallel(tmp_path):
+    out = _bench(tmp_path, "--gpus", "2", "--tp", "2", "--mode", "engine")
+    assert out["n_gpus"] == 2
+    assert out["config"]["parallelism"] == "dp1xtp2"
+    assert out["value"] * out["ms_per_step"] / 1000 == pytest.approx(32, rel=1e-3)
+
+
+def test_bench_dp_times_tp_http(tmp_path):
+    out = _bench(tmp_path, "--gpus", "4", "--tp", "2", "--mode", "http")
+    assert out["n_gpus"] == 4
+    assert out["config"]["parallelism"] == "dp2xtp2"
+    assert out["value"] * out["ms_per_step"] / 1000 == pytest.approx(64, rel=1e-3)

@@ -1,0 +1,119 @@
+"""Quantised tile GEMM (ops/csrc/gemm_q.hip) against the plain fp32 PyTorch reference:
+every tile shape, every weight format, split-K, bf16 output, ragged M / N, and the
+Llama-3-8B production shapes at decode batch 256 through the engine's dispatch."""
+import numpy as np
+import pytest
+import torch
+
+from localai_amd import ops
+from localai_amd.gguf import GGMLType, quantize
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+FMTS = [GGMLType.Q4_K, GGMLType.Q6_K, GGMLType.Q8_0, GGMLType.F16]
+
+
+def _qw(N, K, t, seed=0, std=0.05):
+    rng = np.random.default_rng(seed)
+    w = rng.standard_normal((N, K)).astype(np.float32) * std
+    return ops.QWeight.from_raw(quantize(w, t), t, (N, K), DEV, keep_ref=True)
+
+
+def _run(w, x, tile, S, bf16=False):
+    M, K = x.shape
+    N = w.N
+    p0, p1, g = w.tile_planes()
+    if bf16:
+        out = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=DEV)
+        slab = 0
+    else:
+        out = torch.full((S, M, N), float("nan"), dtype=torch.float32, device=DEV)
+        slab = M * N
+    rc = ops.lib().la_qgemm_tile(w.fmt, p0, p1, g, N, K, x.data_ptr(), K, M, S, out.data_ptr(), N, slab, int(bf16),
+                                 tile, 0, ops._stream())
+    assert rc == 0, rc
+    torch.cuda.synchronize()
+    return out.float().cpu() if bf16 else out.sum(0).cpu()
+
+
+def _check(y, ref, tol=2e-2):
+    assert torch.isfinite(y).all()
+    err = (y - ref).abs().max().item()
+    assert err < tol * max(1.0, ref.abs().max().item()), err
+
+
+@pytest.mark.parametrize("t", FMTS)
+@pytest.mark.parametrize("tile", sorted(ops.GQ_TILES))
+def test_tile_gemm_formats(t, tile):
+    """N off every tile width, M off every tile height, K = 6 super-blocks."""
+    N, K, M = 200, 1536, 150
+    w = _qw(N, K, t, seed=tile)
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    ref = x.float().cpu() @ w.ref.t()
+    _check(_run(w, x, tile, 1), ref)
+
+
+@pytest.mark.parametrize("t", [GGMLType.Q4_K, GGMLType.Q6_K])
+def test_tile_gemm_splits(t):
+    """split-K at odd K-step boundaries (the Q6_K K-step permutation spans 4 K-steps)."""
+    N, K, M = 130, 3584, 256
+    w = _qw(N, K, t, seed=3)
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    ref = x.float().cpu() @ w.ref.t()
+    for tile in (0, 1, 4, 6):
+        for S in (1, 3, 5, 8, 14):
+            _check(_run(w, x, tile, S), ref, 3e-2)
+
+
+@pytest.mark.parametrize("t", [GGMLType.Q4_K, GGMLType.Q6_K, GGMLType.F16])
+def test_tile_gemm_bf16_out_large_m(t):
+    N, K, M = 384, 1024, 1100
+    w = _qw(N, K, t, seed=5)
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    ref = x.float().cpu() @ w.ref.t()
+    _check(_run(w, x, 0, 1, bf16=True), ref)
+
+
+def test_tile_gemm_deterministic():
+    w = _qw(512, 2048, GGMLType.Q4_K, seed=9)
+    x = torch.randn(256, 2048, device=DEV).to(torch.bfloat16)
+    a = _run(w, x, 0, 2)
+    b = _run(w, x, 0, 2)
+    assert torch.equal(a, b)
+
+
+def test_tile_gemm_asymmetric_identity():
+    """A = I (rows of the identity) with an asymmetric W: the output must be W^T exactly as
+    dequantised (catches a transposed C write / swapped fragment maps)."""
+    N, K = 64, 256
+    w = _qw(N, K, GGMLType.Q8_0, seed=2)
+    x = torch.zeros(K, K, dtype=torch.bfloat16, device=DEV)
+    x[torch.arange(K), torch.arange(K)] = 1
+    y = _run(w, x, 3, 1)
+    ref = w.ref.t().to(torch.bfloat16).float()
+    assert (y - ref).abs().max().item() < 1e-6
+
+
+@pytest.mark.parametrize("M", [96, 160, 256])
+def test_linear_dispatch_llama3_shapes(M):
+    """The engine's dispatch (autotuned tile choice) at decode batch sizes on the Llama-3-8B
+    projection shapes (q|k|v mixed Q4_K + Q6_K, o, gate|up, down) against fp32."""
+    K = 4096
+    shapes = {
+        "qkv": ([(4096, GGMLType.Q4_K), (1024, GGMLType.Q4_K), (1024, GGMLType.Q6_K)], K),
+        "o": ([(4096, GGMLType.Q4_K)], K),
+        "gate_up": ([(14336, GGMLType.Q4_K), (14336, GGMLType.Q4_K)], K),
+        "down": ([(4096, GGMLType.Q6_K)], 14336),
+    }
+    x_full = torch.randn(M, 14336, device=DEV).to(torch.bfloat16)
+    for name, (parts, k) in shapes.items():
+        ws = [_qw(n, k, t, seed=i) for i, (n, t) in enumerate(parts)]
+        x = x_full[:, :k].contiguous()
+        y = ops.linear_multi(x, ws).dense().cpu()
+        ref = torch.cat([x.float().cpu() @ w.ref.t() for w in ws], -1)
+        rel = ((y - ref).norm() / ref.norm()).item()
+        cos = torch.nn.functional.cosine_similarity(y.flatten(), ref.flatten(), dim=0).item()
+        assert rel < 1e-2 and cos > 0.9999, (name, rel, cos)
+        assert ops._GEMM_CHOICE, "autotune recorded no choice"
+        for key, ch in ops._GEMM_CHOICE.items():
+            assert ch[0] == "tile", (key, ch)
