@@ -408,6 +408,12 @@ class LLMEngine:
             if tr is not None:
                 tr.complete("decode", t0, t1, batch=len(d_ids), device_steps=K)
             did = True
+        if did and self.tp.car is not None:
+            try:
+                self.tp.check_custom_ar(self.ctrl)
+            except Exception:
+                self._graphs.clear()   # the captured decode graphs call the custom kernel
+                raise
         if tr is not None:
             tr.counter("sequences", time.perf_counter(), running=self.sched.num_running,
                        waiting=self.sched.num_waiting)
@@ -571,7 +577,15 @@ class LLMEngine:
         if self.device.type == "cuda":
             torch.cuda.set_device(self.device)
         while not self._stop:
-            self.step()
+            try:
+                self.step()
+            except Exception as e:  # noqa: BLE001 - mirror the leader's loop: fail the step, keep serving
+                log.exception("follower step failed")
+                self._fail_all(str(e))
+                if self._is_fatal(e):
+                    self.healthy = False
+                    self.fatal_error = str(e)
+                    raise
 
     def _dev(self, a: np.ndarray) -> torch.Tensor:
         t = torch.from_numpy(np.ascontiguousarray(a))

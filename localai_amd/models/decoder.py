@@ -37,6 +37,10 @@ FUSED_ROUTER_OFF = os.environ.get("LOCALAI_AMD_FUSED_ROUTER_OFF", "0") == "1"
 _ACT = {"swiglu": ops.ACT_SWIGLU, "gelu": ops.ACT_GELU, "geglu": ops.ACT_GEGLU}
 
 
+class CustomAllReduceTimeout(RuntimeError):
+    pass
+
+
 @dataclass
 class TPInfo:
     rank: int = 0
@@ -52,6 +56,22 @@ class TPInfo:
             import torch.distributed as dist
             dist.all_reduce(t, group=self.group)  # RCCL: prefill chunks, CPU (gloo)
         return t
+
+    def check_custom_ar(self, ctrl) -> None:
+        """Called once per engine step, at a host sync point that exists anyway: if ANY rank's
+        one-shot all-reduce hit its spin limit (a peer arrived too late: that call summed stale or
+        partial peer slots), every rank agrees over the gloo control group to drop the custom
+        path -- RCCL from then on -- and the step fails loudly instead of serving wrong sums."""
+        if self.world < 2 or self.car is None:
+            return
+        import torch.distributed as dist
+        bad = torch.tensor([1 if self.car.timed_out() else 0], dtype=torch.int32)
+        dist.all_reduce(bad, op=dist.ReduceOp.MAX, group=ctrl)
+        if int(bad.item()):
+            car, self.car = self.car, None
+            car.close()
+            raise CustomAllReduceTimeout("tensor-parallel one-shot all-reduce timed out on a late peer rank: this "
+                                         "step's results are invalid; the group continues on RCCL")
 
     def all_gather_cols(self, t: torch.Tensor) -> torch.Tensor:
         if self.world == 1:
@@ -256,6 +276,8 @@ class DecoderModel:
             router = experts = None
             gate_up, down, up_b, down_b = [], None, None, None
             moe_layer = hp.n_expert and i >= hp.n_layer_dense_lead and b + "ffn_gate_inp.weight" in T
+            if moe_layer and b + "exp_probs_b.bias" in T:
+                raise ValueError(f"{b}exp_probs_b: expert-selection bias (DeepSeek-V3 routing) is not supported")
             if moe_layer:
                 router = f32(b + "ffn_gate_inp.weight").view(hp.n_expert, hp.n_embd)
                 experts = []

@@ -81,6 +81,14 @@ class HParams:
         if a == "qwen2moe":  # the routed experts' width; no dense FFN
             n_ff = g("expert_feed_forward_length", n_ff)
         ds2 = a == "deepseek2"
+        if ds2:
+            # DeepSeek-V3 / R1 GGUFs also say arch deepseek2 but route with sigmoid gating, a
+            # selection bias (exp_probs_b) and normalised weights; the fused router implements
+            # V2's softmax routing only, so refuse those instead of routing experts wrongly
+            gating = int(g("expert_gating_func", 1) or 1)   # llama.cpp: 1 = softmax, 2 = sigmoid
+            if gating != 1 or bool(g("expert_weights_norm", False)):
+                raise ValueError("deepseek2 GGUF with sigmoid expert gating / normalised expert weights "
+                                 "(DeepSeek-V3/R1 routing) is not supported; only DeepSeek-V2 softmax routing")
         hp = HParams(
             arch=a,
             n_layer=int(g("block_count")),

@@ -29,6 +29,7 @@ from __future__ import annotations
 
 import json
 import math
+from collections import OrderedDict
 import os
 from typing import Dict, List, Optional, Sequence
 
@@ -237,7 +238,12 @@ class _Up(nn.Module):
         super().__init__()
         self.conv = nn.Conv2d(c, c, 3, padding=1)
 
-    def forward(self, x):
+    def forward(self, x, size=None):
+        # diffusers' forward_upsample_size: when the latent side is not a multiple of 2^(levels-1)
+        # the down path rounded up (stride-2 conv, padding 1), so the up path must land on the skip's
+        # size exactly, not on 2x (e.g. 520 px -> latent 65 -> 33 -> 17 -> 9; 9 -> 17, not 18)
+        if size is not None and (x.shape[-2] * 2 != size[0] or x.shape[-1] * 2 != size[1]):
+            return self.conv(F.interpolate(x, size=tuple(size), mode="nearest"))
         return self.conv(F.interpolate(x, scale_factor=2.0, mode="nearest"))
 
 
@@ -326,7 +332,7 @@ class UNet(nn.Module):
                 if hasattr(b, "attentions"):
                     h = b.attentions[j](h, ctx)
             if hasattr(b, "upsamplers"):
-                h = b.upsamplers[0](h)
+                h = b.upsamplers[0](h, skips[-1].shape[-2:] if skips else None)
         return self.conv_out(_gn(self.conv_norm_out, h, True))
 
 
@@ -488,7 +494,10 @@ class StableDiffusion:
         self.latent_ch = self.unet.conv_in.in_channels
         # one hipGraph per (batch, latent size) replays the whole UNet step (~1300 launches)
         self.use_graphs = self.device.type == "cuda" and os.environ.get("LOCALAI_AMD_SD_GRAPH", "1") != "0"
-        self._graphs: Dict[tuple, tuple] = {}
+        # bounded LRU: every captured graph owns its activation pool, so a stream of distinct image
+        # sizes must not grow device memory without limit
+        self._graphs: "OrderedDict[tuple, tuple]" = OrderedDict()
+        self.graph_cache = max(0, int(os.environ.get("LOCALAI_AMD_SD_GRAPH_CACHE", "4")))
         self.vae_scale = 2 ** (len(self.vae.decoder.up_blocks) - 1)
 
     def _unet(self, x: torch.Tensor, t: torch.Tensor, ctx: torch.Tensor) -> torch.Tensor:
@@ -496,8 +505,16 @@ class StableDiffusion:
             return self.unet(x, t, ctx)
         key = (tuple(x.shape), tuple(ctx.shape))
         g = self._graphs.get(key)
+        if g is not None:
+            self._graphs.move_to_end(key)
         if g is None:
             out = self.unet(x, t, ctx)  # eager first call: kernel selection / workspaces happen outside capture
+            if self.graph_cache == 0:
+                return out
+            while len(self._graphs) >= self.graph_cache:
+                _, old = self._graphs.popitem(last=False)   # least recently used size
+                del old
+                torch.cuda.empty_cache()
             try:
                 sx, st, sc = x.clone(), t.clone(), ctx.clone()
                 graph = torch.cuda.CUDAGraph()

@@ -129,56 +129,117 @@ class Registry:
         return dst
 
 
+def _rm(p: str) -> None:
+    if os.path.isdir(p) and not os.path.islink(p):
+        shutil.rmtree(p)
+    elif os.path.lexists(p):
+        os.remove(p)
+
+
+def _inside(root: str, p: str) -> bool:
+    return p.startswith(root + os.sep)
+
+
 def _safe_extract(tf: tarfile.TarFile, dest: str) -> None:
+    """Apply one layer to the image's private staging tree `dest`.  Whiteouts (`.wh.<name>`,
+    `.wh..wh..opq`) only ever delete entries of EARLIER LAYERS OF THIS IMAGE, because the staging
+    tree holds nothing else; a whiteout whose victim is empty, '.', '..', contains a separator or
+    resolves outside (or to) the staging root is ignored."""
     root = os.path.realpath(dest)
     for m in tf.getmembers():
         name = m.name.lstrip("/")
         target = os.path.realpath(os.path.join(root, name))
-        if target != root and not target.startswith(root + os.sep):
+        if target != root and not _inside(root, target):
             continue  # path traversal
         base = os.path.basename(name)
         if base.startswith(".wh."):  # whiteout: the layer deletes a path of a lower layer
-            victim = os.path.join(os.path.dirname(target), base[4:])
+            parent = os.path.realpath(os.path.dirname(os.path.join(root, name)))
+            if parent != root and not _inside(root, parent):
+                continue
             if base == ".wh..wh..opq":
-                for e in os.listdir(os.path.dirname(target)) if os.path.isdir(os.path.dirname(target)) else []:
-                    p = os.path.join(os.path.dirname(target), e)
-                    shutil.rmtree(p) if os.path.isdir(p) and not os.path.islink(p) else os.remove(p)
-            elif os.path.lexists(victim):
-                shutil.rmtree(victim) if os.path.isdir(victim) and not os.path.islink(victim) else os.remove(victim)
+                if os.path.isdir(parent) and not os.path.islink(parent):
+                    for e in os.listdir(parent):
+                        _rm(os.path.join(parent, e))
+                continue
+            vname = base[4:]
+            if vname in ("", ".", "..") or "/" in vname or os.sep in vname or vname.startswith(".wh."):
+                continue
+            victim = os.path.join(parent, vname)
+            if not _inside(root, os.path.realpath(victim)) and not _inside(root, os.path.abspath(victim)):
+                continue
+            if os.path.dirname(os.path.abspath(victim)) != parent:
+                continue
+            _rm(victim)
             continue
         if m.isdir():
             os.makedirs(target, exist_ok=True)
         elif m.isfile():
             os.makedirs(os.path.dirname(target), exist_ok=True)
             src = tf.extractfile(m)
+            if os.path.lexists(target) and (os.path.islink(target) or os.path.isdir(target)):
+                _rm(target)
             with open(target, "wb") as out:
                 shutil.copyfileobj(src, out)
             os.chmod(target, m.mode & 0o755 | 0o600)
         elif m.issym():
             link = os.path.realpath(os.path.join(os.path.dirname(target), m.linkname))
-            if link.startswith(root + os.sep):
+            if _inside(root, link):
                 os.makedirs(os.path.dirname(target), exist_ok=True)
                 if os.path.lexists(target):
-                    os.remove(target)
+                    _rm(target)
                 os.symlink(m.linkname, target)
         # hard links, devices, fifos: skipped
 
 
+def _merge_into(staging: str, dest: str) -> None:
+    """Move the flattened image into `dest`: files of the image replace same-named files, and
+    nothing that was already in `dest` is ever deleted (the reference's mutate.Extract +
+    archive.Apply behaviour)."""
+    for dirpath, dirnames, filenames in os.walk(staging):
+        rel = os.path.relpath(dirpath, staging)
+        out_dir = dest if rel == "." else os.path.join(dest, rel)
+        if os.path.lexists(out_dir) and not os.path.isdir(out_dir):
+            os.remove(out_dir)
+        os.makedirs(out_dir, exist_ok=True)
+        for d in list(dirnames):
+            sp = os.path.join(dirpath, d)
+            if os.path.islink(sp):  # symlinked dirs move as links, not walked
+                dirnames.remove(d)
+                filenames.append(d)
+        for f in filenames:
+            sp, dp = os.path.join(dirpath, f), os.path.join(out_dir, f)
+            if os.path.lexists(dp) and (os.path.isdir(dp) and not os.path.islink(dp)):
+                continue  # never replace a directory the user already has
+            if os.path.lexists(dp):
+                os.remove(dp)
+            os.replace(sp, dp)
+
+
 def pull_image(ref: str, dest: str, progress: Optional[Callable[[str, int, int], None]] = None) -> str:
-    """`oci://` model URIs: unpack every layer of the image (linux/amd64) into `dest` in order."""
+    """`oci://` model URIs: flatten every layer of the image (linux/amd64) in order in a private
+    staging tree, then move the result into `dest`."""
     registry, repo, tag = parse_reference(ref)
     reg = Registry(registry)
     man = reg.manifest(repo, tag)
     os.makedirs(dest, exist_ok=True)
-    for i, layer in enumerate(man.get("layers", [])):
-        tmp = os.path.join(dest, f".layer{i}.partial")
-        reg.fetch_blob(repo, layer["digest"], tmp, progress, int(layer.get("size") or 0))
-        try:
-            with tarfile.open(tmp, mode="r:*") as tf:  # plain or gzip tar, random access from disk
-                _safe_extract(tf, dest)
-        finally:
-            if os.path.exists(tmp):
-                os.remove(tmp)
+    staging = os.path.join(dest, f".oci-staging-{os.getpid()}")
+    if os.path.lexists(staging):
+        _rm(staging)
+    os.makedirs(staging)
+    try:
+        for i, layer in enumerate(man.get("layers", [])):
+            tmp = os.path.join(dest, f".layer{i}.partial")
+            reg.fetch_blob(repo, layer["digest"], tmp, progress, int(layer.get("size") or 0))
+            try:
+                with tarfile.open(tmp, mode="r:*") as tf:  # plain or gzip tar, random access from disk
+                    _safe_extract(tf, staging)
+            finally:
+                if os.path.exists(tmp):
+                    os.remove(tmp)
+        _merge_into(staging, dest)
+    finally:
+        if os.path.lexists(staging):
+            _rm(staging)
     return dest
 
 

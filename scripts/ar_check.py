@@ -76,6 +76,30 @@ def main():
     us = (time.perf_counter() - t0) / 200 * 1e6
     dist.barrier()
     car.close()
+    # a late peer: rank 1 arrives ~1.5 s after rank 0, whose spin limit is tiny -> rank 0's wait
+    # times out; the per-step agreement (TPInfo.check_custom_ar) must fail loudly on EVERY rank
+    # and drop the custom path, never hand out the stale sum silently
+    from localai_amd.models.decoder import CustomAllReduceTimeout, TPInfo
+    car2 = CustomAllReduce(dist.group.WORLD, rank, world, dev)
+    car2.SPIN_LIMIT = 1 << 8
+    tpi = TPInfo(rank=rank, world=world, group=dist.group.WORLD, car=car2)
+    t = inputs(rank, 4096, torch.float32, dev, 9)
+    dist.barrier()
+    if rank == 1:
+        time.sleep(1.5)
+    tpi.all_reduce(t)
+    torch.cuda.synchronize()
+    raised = False
+    try:
+        tpi.check_custom_ar(dist.group.WORLD)
+    except CustomAllReduceTimeout:
+        raised = True
+    assert raised and tpi.car is None, (rank, raised)
+    t2 = inputs(rank, 4096, torch.float32, dev, 10)
+    tpi.all_reduce(t2)          # now RCCL/gloo path: exact again
+    ref = expected(world, 4096, torch.float32, torch.device("cpu"), 10)
+    assert (t2.float().cpu() - ref).abs().max().item() < 1e-5, rank
+    dist.barrier()
     if rank == 0:
         print(f"AR_OK world={world} one-row all-reduce {us:.1f} us/call")
     dist.destroy_process_group()

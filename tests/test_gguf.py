@@ -49,3 +49,17 @@ def test_random_blocks_have_target_std(t):
     d = gguf.dequantize(raw, t, (64, 1024))
     assert np.isfinite(d).all()
     assert 0.005 < d.std() < 0.08
+
+
+def test_deepseek_v3_gating_is_refused(tmp_path):
+    """deepseek2 GGUFs carrying V3/R1 sigmoid gating load with a clear error, not wrong routing."""
+    from localai_amd.gguf import GGUFReader
+    from localai_amd.models import synth
+    from localai_amd.models.hparams import HParams
+    p = tmp_path / "ds.gguf"
+    synth.write_model(str(p), "tiny-deepseek2")
+    r = GGUFReader(str(p))
+    HParams.from_gguf(r)                      # V2 softmax routing loads
+    r.kv["deepseek2.expert_gating_func"] = 2  # V3 / R1: sigmoid
+    with pytest.raises(ValueError, match="sigmoid"):
+        HParams.from_gguf(r)

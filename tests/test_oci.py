@@ -169,3 +169,49 @@ def test_resumed_download(registry, tmp_path):
     (tmp_path / "b2.partial").write_bytes(payload)
     download_file(f"http://{host}/files/big.bin", str(tmp_path / "b2"), sha=hashlib.sha256(payload).hexdigest())
     assert (tmp_path / "b2").read_bytes() == payload
+
+
+def _apply_layers(staging, layers):
+    for data in layers:
+        with tarfile.open(fileobj=io.BytesIO(data), mode="r:*") as tf:
+            oci._safe_extract(tf, str(staging))
+
+
+def test_whiteout_cannot_delete_outside_its_own_image(tmp_path):
+    """`.wh..` / `.wh...` / a root-level opaque whiteout only touch entries of earlier layers of
+    the SAME image (private staging tree); the user's existing models survive the merge."""
+    dest = tmp_path / "models"
+    dest.mkdir()
+    (dest / "user-model.gguf").write_bytes(b"keep me")
+    (dest / "sub").mkdir()
+    (dest / "sub" / "keep.txt").write_bytes(b"keep")
+    staging = dest / ".oci-staging-test"
+    staging.mkdir()
+    l1 = _tar({"a.gguf": b"A", "dir/b.txt": b"B"})
+    l2 = _tar({".wh..": b"", ".wh...": b"", "dir/.wh..": b"", "dir/.wh...": b"", ".wh.": b""})
+    _apply_layers(staging, [l1, l2])
+    assert (staging / "a.gguf").read_bytes() == b"A" and (staging / "dir" / "b.txt").exists()
+    l3 = _tar({".wh..wh..opq": b"", "c.gguf": b"C"})      # opaque at the image root: drops a.gguf, dir/
+    _apply_layers(staging, [l3])
+    assert sorted(os.listdir(staging)) == ["c.gguf"]
+    oci._merge_into(str(staging), str(dest))
+    assert (dest / "user-model.gguf").read_bytes() == b"keep me"
+    assert (dest / "sub" / "keep.txt").read_bytes() == b"keep"
+    assert (dest / "c.gguf").read_bytes() == b"C"
+    assert tmp_path.exists() and dest.exists()
+
+
+def test_whiteout_of_lower_layer_symlink_removes_only_the_link(tmp_path):
+    staging = tmp_path / "st"
+    staging.mkdir()
+    outside = tmp_path / "outside"
+    outside.mkdir()
+    (outside / "precious").write_bytes(b"x")
+    link = tarfile.TarInfo("lnk")
+    link.type = tarfile.SYMTYPE
+    link.linkname = "a.gguf"
+    _apply_layers(staging, [_tar({"a.gguf": b"A"}, extra=[link])])
+    assert os.path.islink(staging / "lnk")
+    _apply_layers(staging, [_tar({".wh.lnk": b""})])
+    assert not os.path.lexists(staging / "lnk") and (staging / "a.gguf").exists()
+    assert (outside / "precious").exists()

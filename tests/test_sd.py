@@ -176,3 +176,22 @@ def test_unet_graph_replay_matches_eager(pipe_dir):
     p.use_graphs = False
     b = p("a cat", "blurry", 32, 32, steps=3, seed=11)
     assert (a.float() - b.float()).abs().max() <= 2
+
+
+@pytest.mark.parametrize("w,h", [(520, 72), (40, 24), (72, 56)])
+def test_pipeline_any_multiple_of_8(pipe_dir, w, h):
+    """Sides that are not a multiple of the UNet's total downsampling: the up path lands on each
+    skip's size (diffusers forward_upsample_size) instead of crashing at the concat."""
+    p = StableDiffusion(pipe_dir, "cpu")
+    img = p("a cat", "", w, h, steps=1, seed=3)
+    assert img.shape == (h, w, 3)
+
+
+@pytest.mark.gpu
+def test_unet_graph_cache_is_bounded(pipe_dir, monkeypatch):
+    monkeypatch.setenv("LOCALAI_AMD_SD_GRAPH_CACHE", "2")
+    p = StableDiffusion(pipe_dir, "cuda:0")
+    for side in (32, 40, 48, 56):
+        p("a cat", "", side, side, steps=2, seed=1)
+    assert len(p._graphs) == 2
+    assert [k[0][-1] for k in p._graphs] == [6, 7]   # the two most recent latent sizes
