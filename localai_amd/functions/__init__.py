@@ -362,8 +362,36 @@ def parse_text_content(s: str, fcfg: Optional[dict]) -> str:
     return ""
 
 
+class JSONTruncated(ValueError):
+    """parse.go ParseJSON's non-syntax error: the text ends inside a JSON value (io.ErrUnexpectedEOF)."""
+
+    def __init__(self, msg: str, objs: List[dict]):
+        super().__init__(msg)
+        self.objs = objs
+
+
+def _truncated_value(rest: str, e: json.JSONDecodeError) -> bool:
+    """Would Go's decoder report unexpected EOF (not a syntax error) on `rest`?  Either the error
+    sits at the very end of the input, or what is left is a proper prefix of null / true / false."""
+    if e.pos >= len(e.doc):
+        return True
+    r = rest.strip()
+    return bool(r) and any(lit.startswith(r) and lit != r for lit in ("null", "true", "false"))
+
+
+def parse_json_strict(s: str) -> List[dict]:
+    """parse.go ParseJSON including its error: raises JSONTruncated (carrying the objects decoded
+    so far) when the text ends inside a value."""
+    return _parse_json(s, True)
+
+
 def parse_json(s: str) -> List[dict]:
-    """Tolerant decoder of one or more JSON objects embedded in text (parse.go ParseJSON)."""
+    """Tolerant decoder of one or more JSON objects embedded in text (parse.go ParseJSON); the
+    callers (ParseFunctionCall) only log ParseJSON's error, so it is swallowed here."""
+    return _parse_json(s, False)
+
+
+def _parse_json(s: str, strict: bool) -> List[dict]:
     objs = []
     dec = json.JSONDecoder()
     off = 0
@@ -381,6 +409,8 @@ def parse_json(s: str) -> List[dict]:
                 objs.extend(o for o in obj if isinstance(o, dict))
             off = max(end, off + 1)
         except json.JSONDecodeError as e:
+            if strict and _truncated_value(s[off:], e):
+                raise JSONTruncated(f"unexpected end of JSON input at offset {off}", objs) from e
             off = max(e.pos, off + 1)
     return objs
 

@@ -88,12 +88,11 @@ template <int BN> struct GqW<FMT_Q4_K, BN> {
   };
   LA_DEV static void load(const uint8_t* wl, int col, int g, int, Frag& f) {
     f.q = gq_read32(wl, col, g);
-    const u32x2 s = *(const u32x2*)(wl + CODES + col * 8);
-    const float d = h2f(s.x & 0xFFFFu), dm = h2f(s.x >> 16);
-    f.D[0] = d * (float)(s.y & 0xFFu);
-    f.Mn[0] = -dm * (float)((s.y >> 8) & 0xFFu);
-    f.D[1] = d * (float)((s.y >> 16) & 0xFFu);
-    f.Mn[1] = -dm * (float)(s.y >> 24);
+    const u32x2 s = *(const u32x2*)(wl + CODES + col * 8);  // f16 D0, -M0, D1, -M1 (la_gemm_scales)
+    f.D[0] = h2f(s.x & 0xFFFFu);
+    f.Mn[0] = h2f(s.x >> 16);
+    f.D[1] = h2f(s.y & 0xFFFFu);
+    f.Mn[1] = h2f(s.y >> 16);
   }
   template <int S>
   LA_DEV static bf16x8 deq(const Frag& f) {
@@ -135,11 +134,10 @@ template <int BN> struct GqW<FMT_Q6_K, BN> {
   LA_DEV static void load(const uint8_t* wl, int col, int g, int ks, Frag& f) {
     f.ql = gq_read32(wl, col, g);
     f.qh = gq_read32(wl + BN * 32, col, g);
-    const u32x2 s = *(const u32x2*)(wl + CODES + col * 8);
-    const float d = h2f(s.x & 0xFFFFu);
+    const u32x2 s = *(const u32x2*)(wl + CODES + col * 8);  // f16 d*sc of the 4 16-k groups (la_gemm_scales)
     const int i = g >> 1;  // 16-k scale group inside each 32-k run
-    f.S[0] = d * (float)(int8_t)((s.y >> (8 * i)) & 0xFFu);
-    f.S[1] = d * (float)(int8_t)((s.y >> (8 * (2 + i))) & 0xFFu);
+    f.S[0] = h2f(i ? (s.x >> 16) : (s.x & 0xFFFFu));
+    f.S[1] = h2f(i ? (s.y >> 16) : (s.y & 0xFFFFu));
     f.sh = 2 * (ks & 1);
   }
   template <int S>
@@ -221,7 +219,7 @@ template <int BN> struct GqW<FMT_BF16, BN> {
 
 // ---------------------------------------------------------------- kernel
 // ABL (probe builds only): bit0 no MFMA, bit1 no dequant arithmetic, bit2 no X DMA, bit3 no W DMA.
-template <int FMT, int BM, int BN, int WM, int WN, int NS, int ABL = 0>
+template <int FMT, int BM, int BN, int WM, int WN, int NS, int ABL = 0, int PIPE = 0>
 __global__ __launch_bounds__(WM* WN * 64, 1) void qgemm_tile_kernel(
     QW w, const bf16* __restrict__ X, int ldx, int M, int per_split, int m_tiles, int n_tiles, int splits,
     int real_tiles, float* __restrict__ out, bf16* __restrict__ outb, int ldo, long slab) {
@@ -336,19 +334,99 @@ __global__ __launch_bounds__(WM* WN * 64, 1) void qgemm_tile_kernel(
     }
   };
 
-  constexpr int D = NS - 1;  // stages in flight ahead of the one being computed
+  if constexpr (PIPE) {
+    // Software-pipelined schedule: a K-step is P phases (k32 sub-step x group of MG A fragments);
+    // each phase first ISSUES the LDS reads of the next phase, then runs its own MFMAs, so LDS
+    // latency hides under MFMA inside every wave.  The barrier sits in the last phase, before the
+    // reads of step t+1: it needs only stage t+1 landed, and frees slot t for the DMA of t+NS.
+    // A fragments per phase: 8, or 4 when NT = 4 (two phase sets of 8 + 4 B fragments + 128
+    // accumulators would not fit 256 VGPRs)
+    constexpr int MG = (NT >= 4 && MT >= 4) ? 4 : (MT < 8 ? MT : 8);
+    constexpr int NG = MT / MG;           // phases per k32 sub-step
+    constexpr int P = 2 * NG;             // phases per K-step
+    static_assert(MT % MG == 0, "phase grouping");
 #pragma unroll
-  for (int i = 0; i < D; ++i)
-    if (i < nk) issue(i);
-  const bool wa = wave < PWR;
-  for (int t = 0; t < nk; ++t) {
-    const int ahead = min(D - 1, nk - 1 - t);  // stages after t already issued
-    if (wa) gq_wait_stages<LA>(ahead);
-    else gq_wait_stages<LB>(ahead);
-    if constexpr (!(ABL & 32)) __builtin_amdgcn_s_barrier();  // every wave's DMAs of step t landed; slot (t-1) % NS free
+    for (int i = 0; i < NS; ++i)
+      if (i < nk) issue(i);
+    const bool wa = wave < PWR;
+    {
+      const int ahead = min(NS - 1, nk - 1);
+      if (wa) gq_wait_stages<LA>(ahead);
+      else gq_wait_stages<LB>(ahead);
+    }
+    __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (t + D < nk) issue(t + D);
-    compute(t);
+    auto read_a = [&](bf16x8* dst, int t, int s, int grp) {
+      const uint8_t* sl = lds + (t % NS) * SLOT;
+#pragma unroll
+      for (int j = 0; j < MG; ++j) {
+        const int row = wm * TM + (grp * MG + j) * 16 + r16;
+        dst[j] = *(const bf16x8*)(sl + row * 128 + 16 * ((4 * s + g) ^ ((row >> 1) & 7)));
+      }
+    };
+    auto read_b = [&](typename WS::Frag* dst, int t) {
+      const uint8_t* wl = lds + (t % NS) * SLOT + XB;
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) WS::load(wl, wn * TN + nt * 16 + r16, g, ks0 + t, dst[nt]);
+    };
+    typename WS::Frag f[NT], fn[NT];
+    bf16x8 a[MG], an[MG], b[NT];
+    read_b(f, 0);
+    read_a(a, 0, 0, 0);
+    for (int t = 0; t < nk; ++t) {
+#pragma unroll
+      for (int p = 0; p < P; ++p) {
+        const int s = p / NG, grp = p % NG;
+        if (p + 1 < P) {
+          read_a(an, t, (p + 1) / NG, (p + 1) % NG);
+        } else if (t + 1 < nk) {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of slot t are done
+          const int ahead = min(NS - 2, nk - 2 - t);           // stages after t+1 still in flight
+          if (wa) gq_wait_stages<LA>(ahead);
+          else gq_wait_stages<LB>(ahead);
+          if constexpr (!(ABL & 32)) __builtin_amdgcn_s_barrier();  // stage t+1 visible; slot t free
+          asm volatile("" ::: "memory");
+          if (t + NS < nk) issue(t + NS);
+          read_b(fn, t + 1);
+          read_a(an, t + 1, 0, 0);
+        }
+        if (grp == 0) {
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt) {
+            if constexpr (ABL & 2) b[nt] = __builtin_bit_cast(bf16x8, u32x4{(uint32_t)nt, (uint32_t)s, 0u, 0u});
+            else if (s == 0) b[nt] = WS::template deq<0>(f[nt]);
+            else b[nt] = WS::template deq<1>(f[nt]);
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < MG; ++j)
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt) {
+            if constexpr (ABL & 1) acc[grp * MG + j][nt][0] += (float)a[j][nt & 7] * (float)b[nt][j & 7];
+            else acc[grp * MG + j][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[j], b[nt], acc[grp * MG + j][nt], 0, 0, 0);
+          }
+#pragma unroll
+        for (int j = 0; j < MG; ++j) a[j] = an[j];
+      }
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) f[nt] = fn[nt];
+    }
+  } else {
+    constexpr int D = NS - 1;  // stages in flight ahead of the one being computed
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+      if (i < nk) issue(i);
+    const bool wa = wave < PWR;
+    for (int t = 0; t < nk; ++t) {
+      const int ahead = min(D - 1, nk - 1 - t);  // stages after t already issued
+      if (wa) gq_wait_stages<LA>(ahead);
+      else gq_wait_stages<LB>(ahead);
+      if constexpr (!(ABL & 32)) __builtin_amdgcn_s_barrier();  // every wave's DMAs of step t landed; slot (t-1) % NS free
+      asm volatile("" ::: "memory");
+      if (t + D < nk) issue(t + D);
+      compute(t);
+    }
+
   }
 
   // epilogue through LDS: acc[mt][nt][i] is (row wm*TM + 16mt + 4g + i, col wn*TN + 16nt + r16);
@@ -421,9 +499,9 @@ __global__ __launch_bounds__(WM* WN * 64, 1) void qgemm_tile_kernel(
 
 // Blocked scale plane for the tile GEMM: [ceil(N/16)][K/64][16 cols][8 B], one record per
 // (column, K-step).  Rows past N repeat row N-1.
-//   Q4_K: f16 d, f16 dmin, u8 sc, u8 m (sub-block 2(ks%4)), u8 sc, u8 m (sub-block 2(ks%4)+1)
-//         from the unpacked scm [N][K/256][16] and dd [N][K/256][2 x f16] planes
-//   Q6_K: f16 d, 2 B pad, i8 sc x4 = the 16-k groups of the K-step's two 32-k runs
+//   Q4_K: f16 d*sc, f16 -dmin*m of sub-block 2(ks%4), then of sub-block 2(ks%4)+1, from the
+//         unpacked scm [N][K/256][16] and dd [N][K/256][2 x f16] planes
+//   Q6_K: f16 d*sc of the 16-k groups of the K-step's two 32-k runs (4 x f16)
 //   Q8_0: f16 d of the two 32-blocks, 4 B pad
 __global__ void gemm_scales_kernel(int fmt, const uint8_t* __restrict__ a, const uint8_t* __restrict__ b, int N,
                                    int K, uint8_t* __restrict__ outp) {
@@ -437,22 +515,32 @@ __global__ void gemm_scales_kernel(int fmt, const uint8_t* __restrict__ a, const
   const int n = min(nb * 16 + c, N - 1);
   const int sb = ks >> 2;
   uint32_t x = 0, y = 0;
+  auto f2h = [](float v) -> uint32_t {
+    const _Float16 h = (_Float16)v;
+    uint16_t b;
+    __builtin_memcpy(&b, &h, 2);
+    return b;
+  };
   if (fmt == FMT_Q4_K) {
+    // ggml dequantize_row_q4_K: y = (d * sc) * q - (dmin * m); the two products in f16
     const uint8_t* s = a + ((size_t)n * (K >> 8) + sb) * 16 + 4 * (ks & 3);  // sc, m, sc, m
-    x = *(const uint32_t*)(b + ((size_t)n * (K >> 8) + sb) * 4);             // d, dmin
-    y = (uint32_t)s[0] | ((uint32_t)s[1] << 8) | ((uint32_t)s[2] << 16) | ((uint32_t)s[3] << 24);
+    const uint32_t dd = *(const uint32_t*)(b + ((size_t)n * (K >> 8) + sb) * 4);  // d, dmin
+    const float d = h2f(dd & 0xFFFFu), dm = h2f(dd >> 16);
+    x = f2h(d * (float)s[0]) | (f2h(-dm * (float)s[1]) << 16);
+    y = f2h(d * (float)s[2]) | (f2h(-dm * (float)s[3]) << 16);
   } else if (fmt == FMT_Q6_K) {
     const int hh = (ks >> 1) & 1, part = ks & 1;
-    const uint8_t* s = a + (size_t)n * (K >> 4) + sb * 16 + 8 * hh + 2 * part;
-    x = *(const uint16_t*)(b + ((size_t)n * (K >> 8) + sb) * 2);
-    y = (uint32_t)s[0] | ((uint32_t)s[1] << 8) | ((uint32_t)s[4] << 16) | ((uint32_t)s[5] << 24);
+    const int8_t* s = (const int8_t*)(a + (size_t)n * (K >> 4) + sb * 16 + 8 * hh + 2 * part);
+    const float d = h2f(*(const uint16_t*)(b + ((size_t)n * (K >> 8) + sb) * 2));
+    x = f2h(d * (float)s[0]) | (f2h(d * (float)s[1]) << 16);
+    y = f2h(d * (float)s[4]) | (f2h(d * (float)s[5]) << 16);
   } else {  // Q8_0: d plane [N][K/32] f16
     x = *(const uint32_t*)(a + ((size_t)n * (K >> 5) + 2 * ks) * 2);
   }
   *(u32x2*)(outp + gid * 8) = u32x2{x, y};
 }
 
-template <int FMT, int BM, int BN, int WM, int WN, int NS, int ABL = 0>
+template <int FMT, int BM, int BN, int WM, int WN, int NS, int ABL = 0, int PIPE = 0>
 static void gq_launch(const QW& w, const bf16* X, int ldx, int M, int splits, float* out, bf16* outb, int ldo,
                       long slab, hipStream_t st) {
   const int KS = w.K / GQ_BK;
@@ -460,7 +548,7 @@ static void gq_launch(const QW& w, const bf16* X, int ldx, int M, int splits, fl
   const int m_tiles = (M + BM - 1) / BM, n_tiles = (w.N + BN - 1) / BN;
   const int real = m_tiles * n_tiles * splits;
   const int grid = (real + 7) / 8 * 8;
-  hipLaunchKernelGGL((qgemm_tile_kernel<FMT, BM, BN, WM, WN, NS, ABL>), dim3(grid), dim3(WM * WN * 64), 0, st, w, X,
+  hipLaunchKernelGGL((qgemm_tile_kernel<FMT, BM, BN, WM, WN, NS, ABL, PIPE>), dim3(grid), dim3(WM * WN * 64), 0, st, w, X,
                      ldx, M, per, m_tiles, n_tiles, splits, real, out, outb, ldo, slab);
 }
 
@@ -468,7 +556,8 @@ static void gq_launch(const QW& w, const bf16* X, int ldx, int M, int splits, fl
 //   0: 256 x 256 (8 waves 2x4)   1: 256 x 128 (8 waves 2x4)   2: 128 x 256 (8 waves 2x4)
 //   3: 128 x 128 (4 waves 2x2)   4: 256 x 64 (4 waves 4x1)    5: 64 x 256 (4 waves 1x4)
 //   6: 256 x 256 (8 waves 1x8: one dequantised B fragment feeds 16 MFMAs, A reads double)
-//   7: 128 x 256 (8 waves 1x8)
+//   7: 128 x 256 (8 waves 1x8)   8: 256 x 128 (8 waves 2x4, 2 ring slots)   12: 128 x 128 (8 waves 2x4)
+//   14: 64 x 256 (8 waves 1x8)
 template <int FMT, int ABL = 0>
 static int gq_dispatch(int tile, const QW& w, const bf16* X, int ldx, int M, int splits, float* out, bf16* outb,
                        int ldo, long slab, hipStream_t st) {
@@ -487,6 +576,17 @@ static int gq_dispatch(int tile, const QW& w, const bf16* X, int ldx, int M, int
     case 5: gq_launch<FMT, 64, 256, 1, 4, 3, ABL>(w, X, ldx, M, splits, out, outb, ldo, slab, st); break;
     case 6: gq_launch<FMT, 256, 256, 1, 8, NS0, ABL>(w, X, ldx, M, splits, out, outb, ldo, slab, st); break;
     case 7: gq_launch<FMT, 128, 256, 1, 8, NS2, ABL>(w, X, ldx, M, splits, out, outb, ldo, slab, st); break;
+    // two or three workgroups per CU (<= 80 / 53 KiB LDS, <= 128 / 85 VGPRs): independent
+    // barrier domains on one CU hide each other's DMA / barrier waits
+    case 8: gq_launch<FMT, 256, 128, 2, 4, 2, ABL>(w, X, ldx, M, splits, out, outb, ldo, slab, st); break;
+    case 12: gq_launch<FMT, 128, 128, 2, 4, 3, ABL>(w, X, ldx, M, splits, out, outb, ldo, slab, st); break;
+    case 14: gq_launch<FMT, 64, 256, 1, 8, 3, ABL>(w, X, ldx, M, splits, out, outb, ldo, slab, st); break;
+    // software-pipelined schedule (PIPE = 1) of tiles 0, 1, 3, 6
+    case 10: gq_launch<FMT, 256, 256, 2, 4, NS0, ABL, 1>(w, X, ldx, M, splits, out, outb, ldo, slab, st); break;
+    case 11: gq_launch<FMT, 256, 128, 2, 4, NS1, ABL, 1>(w, X, ldx, M, splits, out, outb, ldo, slab, st); break;
+    case 13: gq_launch<FMT, 128, 128, 2, 2, NS3, ABL, 1>(w, X, ldx, M, splits, out, outb, ldo, slab, st); break;
+    case 16: gq_launch<FMT, 256, 256, 1, 8, NS0, ABL, 1>(w, X, ldx, M, splits, out, outb, ldo, slab, st); break;
+    case 17: gq_launch<FMT, 128, 256, 1, 8, NS2, ABL, 1>(w, X, ldx, M, splits, out, outb, ldo, slab, st); break;
     default: return -1;
   }
   return 0;

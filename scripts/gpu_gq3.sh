@@ -1,0 +1,12 @@
+#!/bin/bash
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 500 python -u -m pytest -x -q --timeout 180 --timeout-method thread tests/test_gemm_tile_gpu.py > gpurun_out/gq_tests.log 2>&1
+rc=$?
+tail -3 gpurun_out/gq_tests.log
+if [ $rc -ne 0 ]; then echo "tests rc=$rc: stopping"; exit $rc; fi
+timeout -k 10 400 python -u scripts/gq_bench.py --m 256 128 --shapes qkv,o,gate_up,down,down6,lm_head --blas > gpurun_out/gq_bench3.log 2>&1
+rc=$?
+cat gpurun_out/gq_bench3.log
+exit $rc

@@ -82,9 +82,9 @@ def main():
             x = (torch.randn(M, K, device=DEV) * 0.5).to(torch.bfloat16)
             flops = 2.0 * M * Ntot * K
             res = {}
-            tiles = (0, 6, 1, 4) if M > 128 else (7, 2, 3, 5, 1)
+            tiles = (6, 1, 7, 8, 12) if M > 128 else (7, 12, 14, 3)
             if M > 256:
-                tiles = (0, 6, 1, 2)
+                tiles = (6, 16, 10)
             for t in tiles:
                 g = ops._tile_grid(M, max(w.N for w in ws), t)
                 base = max(1, round(256 / g))
@@ -119,7 +119,7 @@ def main():
         p0, _, g = w.tile_planes()
         for M in a.m:
             x = (torch.randn(M, K, device=DEV) * 0.5).to(torch.bfloat16)
-            for tile, S in ((0, 2), (6, 2), (1, 1)):
+            for tile, S in ((16, 2), (10, 2), (11, 1)):
                 out = torch.empty(S, M, w.N, dtype=torch.float32, device=DEV)
                 line = []
                 for abl in (0, 1, 2, 3, 4, 8, 12, 15, 32, 47, 64, 79, 111):
