@@ -370,6 +370,23 @@ class LLMEngine:
             self._finish(self.requests[rid], "error", error=msg)
 
     # ------------------------------------------------------------------ step
+    def active_slot_stats(self) -> Optional[dict]:
+        """The reference's GetMetrics view (grpc-server.cpp:2434-2457, llama.get_active_slot()):
+        live numbers of one in-flight request -- the oldest one that is generating -- or None when
+        nothing is in flight.  Read from the serving thread's dict without locking: a snapshot."""
+        now = time.perf_counter()
+        best = None
+        for r in list(self.requests.values()):
+            if r.done or r.cancelled:
+                continue
+            if best is None or r.arrival < best.arrival:
+                best = r
+        if best is None:
+            return None
+        gen_s = (now - best.first_token_t) if best.first_token_t else 0.0
+        return {"id": best.id, "prompt_tokens": best.n_prompt or len(best.prompt), "completion_tokens": best.n_gen,
+                "tokens_per_second": (best.n_gen / gen_s) if gen_s > 0 else 0.0, "prompt": list(best.prompt)}
+
     def has_work(self) -> bool:
         return bool(self.requests) or not self._inbox.empty()
 

@@ -31,6 +31,21 @@ def build_router(state) -> APIRouter:
 
     r.add_api_route("/version", version, methods=["GET"])
 
+    # ---------------------------------------------------------------- generated media
+    # core/http/routes/openai.go:75,79: app.Static("/generated-images", ImageDir) and
+    # ("/generated-audio", AudioDir) -- the URLs /v1/images/generations returns (response_format url)
+    def _static(root_attr: str):
+        async def serve(name: str):
+            root = os.path.realpath(getattr(state.cfg, root_attr))
+            p = os.path.realpath(os.path.join(root, name))
+            if not p.startswith(root + os.sep) or not os.path.isfile(p):
+                return JSONResponse({"error": {"code": 404, "message": "not found", "type": ""}}, status_code=404)
+            return FileResponse(p)
+        return serve
+
+    r.add_api_route("/generated-images/{name:path}", _static("image_dir"), methods=["GET", "HEAD"])
+    r.add_api_route("/generated-audio/{name:path}", _static("audio_dir"), methods=["GET", "HEAD"])
+
     async def system():
         backends = sorted(set(b for b in ENGINE_BACKENDS if b) | HF_BACKENDS | SD_BACKENDS |
                           {MAMBA_BACKEND, RWKV_BACKEND}) + \

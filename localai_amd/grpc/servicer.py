@@ -332,14 +332,19 @@ class EngineServicer:
         return st
 
     async def GetMetrics(self, request, context=None):
+        """Metrics of the ACTIVE slot, as the reference's llama backend reports them
+        (grpc-server.cpp:2434-2457): an in-flight request's id, prompt, generated tokens and
+        decode rate; all zero / empty when nothing is in flight."""
         r = pb.MetricsResponse()
-        if self.engine is not None:
-            s = self.engine.last_request_stats or {}
-            r.slot_id = int(s.get("id", 0))
-            r.tokens_per_second = float(s.get("tokens_per_second", 0.0))
-            r.tokens_generated = int(s.get("completion_tokens", 0))
-            r.prompt_tokens_processed = int(s.get("prompt_tokens", 0))
-            r.prompt_json_for_slot = json.dumps({"ttft_s": s.get("ttft_s", 0.0)})
+        s = None
+        if self.engine is not None and hasattr(self.engine, "active_slot_stats"):
+            s = self.engine.active_slot_stats()
+        if s:
+            r.slot_id = int(s["id"])
+            r.tokens_per_second = float(s["tokens_per_second"])
+            r.tokens_generated = int(s["completion_tokens"])
+            r.prompt_tokens_processed = int(s["prompt_tokens"])
+            r.prompt_json_for_slot = json.dumps(s["prompt"])
         return r
 
     # ------------------------------------------------------------------ vector store (local-store backend)

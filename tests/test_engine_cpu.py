@@ -369,3 +369,29 @@ def test_batched_vision_tower_matches_single(tiny_model_path, tmp_path):
         n_img = cv.embed_image(im).shape[0]
         assert got[i][2] == "" and got[i][1] == 2
         assert got[i][0] == n_img + len(e.tokenize(f"request {i}"))
+
+
+def test_get_metrics_reports_the_active_slot(eng):
+    """GetMetrics = the reference's get_active_slot() view (grpc-server.cpp:2434-2457): a request
+    in flight is reported with its id, prompt and generated-token count; idle -> zeros."""
+    import asyncio
+    import json as _json
+
+    from localai_amd.grpc import backend_pb as pb
+    from localai_amd.grpc.servicer import EngineServicer
+    sv = EngineServicer(device="cpu")
+    sv.engine = eng
+    idle = asyncio.run(sv.GetMetrics(pb.MetricsRequest()))
+    assert idle.slot_id == 0 and idle.tokens_generated == 0 and idle.prompt_json_for_slot == ""
+    ids = eng.tokenize("metrics probe")
+    rid = eng.add_request(ids, SamplingParams(max_tokens=6, temperature=0.0, ignore_eos=True), lambda ev: None)
+    for _ in range(4):
+        eng.step()
+    m = asyncio.run(sv.GetMetrics(pb.MetricsRequest()))
+    assert m.slot_id == rid
+    assert 0 < m.tokens_generated <= 6
+    assert m.prompt_tokens_processed == len(ids)
+    assert _json.loads(m.prompt_json_for_slot) == list(ids)
+    while eng.has_work():
+        eng.step()
+    assert asyncio.run(sv.GetMetrics(pb.MetricsRequest())).slot_id == 0

@@ -31,3 +31,20 @@ def test_install_embedded_configs(tmp_path):
 def test_unknown_name_is_reported(tmp_path):
     errs = install_models([], str(tmp_path), ["definitely-not-a-model"])
     assert len(errs) == 1
+
+
+def test_library_covers_every_reference_embedded_model():
+    """Every embedded/models/*.yaml name of the reference resolves to a loadable config here."""
+    import os
+
+    import yaml
+
+    from localai_amd import library
+    from localai_amd.config.backend_config import BackendConfig
+    ref = "/root/reference/embedded/models"
+    names = sorted(f[:-5] for f in os.listdir(ref)) if os.path.isdir(ref) else sorted(library.EMBEDDED)
+    assert len(names) >= 27
+    for n in names:
+        assert library.exists_in_library(n), n
+        cfg = BackendConfig(yaml.safe_load(library.resolve_content(n)))
+        assert cfg.name and cfg.validate(), n

@@ -136,6 +136,16 @@ def test_gateway_images_endpoint(pipe_dir, tmp_path):
         img = Image.open(io.BytesIO(base64.b64decode(r.json()["data"][0]["b64_json"])))
         assert img.size == (32, 32)
         assert "diffusers" in c.get("/system").json()["backends"]
+        # default response_format (url): the returned URL is served (core/http/routes/openai.go:75)
+        r = c.post("/v1/images/generations", json={"model": "sd", "prompt": "a lighthouse", "size": "32x32",
+                                                   "step": 1})
+        assert r.status_code == 200, r.text
+        url = r.json()["data"][0]["url"]
+        path = url[url.index("/generated-images/"):]
+        got = c.get(path)
+        assert got.status_code == 200 and Image.open(io.BytesIO(got.content)).size == (32, 32)
+        assert c.get("/generated-images/../../etc/passwd").status_code == 404
+        assert c.get("/generated-audio/nope.wav").status_code == 404
 
 
 @pytest.mark.gpu
