@@ -446,9 +446,10 @@ class DecoderModel:
         hp = self.hp
         T = xn.shape[0]
         El, base = self.E_local, self.ep_base
-        if L.moe_gu is not None and T <= 64 and xn.is_cuda and not FUSED_ROUTER_OFF:
-            # decode batches: one fused router launch (softmax, top-k, renorm, EP remap) feeds the
-            # grouped expert GEMMs; no host round trip anywhere (graph-capturable)
+        if L.moe_gu is not None and xn.is_cuda and not FUSED_ROUTER_OFF:
+            # any batch: one fused router launch (softmax, top-k, renorm, EP remap) feeds the
+            # grouped expert GEMMs (row-chunked past 64 rows per expert); no host round trip
+            # anywhere, so decode steps at every batch size capture into graphs
             k = hp.n_expert_used
             ids, wts = ops.moe_router(xn, L.router, k, hp.moe_renorm, hp.expert_weights_scale,
                                       base if self.ep else 0, El if self.ep else 0)
@@ -471,7 +472,7 @@ class DecoderModel:
             idx_l = torch.where((loc >= 0) & (loc < El), loc, torch.full_like(loc, El))
         else:
             idx_l = idx
-        if L.moe_gu is not None and T <= 64 and xn.is_cuda:
+        if L.moe_gu is not None and xn.is_cuda:
             # graph-capturable grouped path: device routing, one weight stream per active expert,
             # routing-weighted outputs land as extra slabs summed by the next kernel
             k = hp.n_expert_used

@@ -73,6 +73,7 @@ def lib():
             "la_gemm_scales": [I, P, P, I, I, P, P],
             "la_qgemm_tile": [I, P, P, P, I, I, P, I, I, I, P, I, LNG, I, I, I, P],
             "la_qgemm_tile_probe": [P, P, I, I, P, I, I, P, I, I, P],
+            "la_qgemm_tile2": [I, P, P, P, I, I, P, P, P, I, I, P, I, I, I, P, I, LNG, I, I, P],
             "la_decode_advance": [P, P, P, P, P, P, I, I, I, P, I, P, P, P],
         }
         for name, args in sig.items():
@@ -701,11 +702,23 @@ def _tile_split_ok(K: int, S: int) -> bool:
     return S >= 1 and -(-ks // S) * (S - 1) < ks
 
 
+_TILE2_PAIRS = {(FMT_Q4_K, FMT_Q6_K), (FMT_Q6_K, FMT_Q4_K)}
+_TILE2_TILES = (7, 8, 12)
+
+
 def _run_tile(x, ws, S, out, Ntot, tile):
-    """out: fp32 slabs [S, M, Ntot], or a bf16 [M, Ntot] matrix (S == 1)."""
+    """out: fp32 slabs [S, M, Ntot], or a bf16 [M, Ntot] matrix (S == 1).  Two weights of a
+    Q4_K/Q6_K mix (q|k + v) run as ONE launch (la_qgemm_tile2)."""
     M, K = x.shape
     bf = out.dtype == torch.bfloat16
     esz = 2 if bf else 4
+    if len(ws) == 2 and (ws[0].fmt, ws[1].fmt) in _TILE2_PAIRS and tile in _TILE2_TILES:
+        a0, a1, ag = ws[0].tile_planes()
+        b0, b1, bg = ws[1].tile_planes()
+        _check(lib().la_qgemm_tile2(ws[0].fmt, a0, a1, ag, ws[0].N, ws[1].fmt, b0, b1, bg, ws[1].N, K, x.data_ptr(), K,
+                                    M, S, out.data_ptr(), Ntot, 0 if bf else M * Ntot, int(bf), tile, _stream()),
+               "la_qgemm_tile2")
+        return
     col = 0
     for w in ws:
         p0, p1, g = w.tile_planes()
@@ -750,15 +763,19 @@ def _autotune_mid(x, ws, key, Ntot):
         for t in tiles:
             g = _tile_grid(M, N, t)
             base = max(1, round(256 / g))
-            for S in sorted({max(1, base // 2), base, base * 2}):
-                if S <= K // 256 and _tile_split_ok(K, S):
+            # split-K <= 8: every split costs its consumer another fp32 [M, N] slab read
+            for S in sorted({1, max(1, base // 2), base, base * 2}):
+                if S <= min(8, K // 256) and _tile_split_ok(K, S):
                     cands.append(("tile", S, t))
     if not cands or os.environ.get("LOCALAI_AMD_BLAS_CANDIDATE") == "1" or not TILE_GEMM:
         cands.append(("blas", 0, 0))
     if not TILE_GEMM:
         cands = [("blas", 0, 0)] + [("mid", S, t) for t in ((22, 21) if M <= 128 else (42, 41, 22, 21))
                                     for S in (1, 2, 4, 8) if _mid_split_ok(K, S)]
-    outs = {S: torch.empty(S, M, Ntot, dtype=torch.float32, device=x.device) for _, S, _ in cands if S}
+    outs = {S: torch.empty(S, M, Ntot, dtype=torch.float32, device=x.device) for _, S, _ in cands
+            if S > 1 or (S == 1 and not TILE_GEMM)}
+    if TILE_GEMM:
+        outs[1] = torch.empty(M, Ntot, dtype=torch.bfloat16, device=x.device)   # S = 1: one bf16 matrix
     best, best_t = cands[0], float("inf")
     for kind, S, t in cands:
         if kind == "blas":
@@ -778,8 +795,9 @@ def _autotune_mid(x, ws, key, Ntot):
             e1.synchronize()
             ts.append(e0.elapsed_time(e1) * 1000)
         tt = sorted(ts)[1]
-        if kind != "blas":
-            tt += (S * M * Ntot * 4 - M * Ntot * 2) / 4e6
+        if kind != "blas" and S > 1:
+            # fp32 slabs: written here and read back by the consumer (vs one bf16 matrix), ~4 TB/s each way
+            tt += 2 * (S * M * Ntot * 4 - M * Ntot * 2) / 4e6
         if tt < best_t:
             best, best_t = (kind, S, t), tt
     _GEMM_CHOICE[key] = best
@@ -836,7 +854,7 @@ def linear_multi(x: torch.Tensor, ws: Sequence[QWeight], bias: Optional[torch.Te
     elif force is None and not use_skinny and tile_ok and PREFILL_GEMM == "tile":
         tile, S = pick_tile(M, [w.N for w in ws], K)   # prefill: heuristic, never tuned inline
         kind = "tile"
-    if kind == "tile" and S == 1 and M > MID_MAX_M and out_slabs is None:
+    if kind == "tile" and S == 1 and out_slabs is None:
         y = torch.empty(M, Ntot, dtype=torch.bfloat16, device=x.device)
         _run_tile(x, ws, 1, y, Ntot, tile)
         return Partial(y, bias)
@@ -1491,9 +1509,7 @@ def moe_linear(x: torch.Tensor, mw: MoEWeights, order: torch.Tensor, off: torch.
         return Partial(out)
     if x.dtype != torch.bfloat16 or not x.is_contiguous():
         raise ValueError("moe_linear: x must be contiguous bf16")
-    maxM = T  # a token picks an expert at most once
-    if maxM > 64:
-        raise ValueError("moe_linear: grouped decode path supports T <= 64")
+    maxM = T  # a token picks an expert at most once; above 64 rows the launch adds row chunks
     S = pick_splits(mw.N, mw.K, maxM)
     nsb = mw.K // 256
     while nsb % S:

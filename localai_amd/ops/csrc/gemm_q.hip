@@ -219,10 +219,13 @@ template <int BN> struct GqW<FMT_BF16, BN> {
 
 // ---------------------------------------------------------------- kernel
 // ABL (probe builds only): bit0 no MFMA, bit1 no dequant arithmetic, bit2 no X DMA, bit3 no W DMA.
+// One (M tile, N tile, K split) of one weight; `tile` is the segment-local tile id and out/outb
+// already point at the segment's first output column.  Returns without touching memory when
+// the tile's K range is empty.
 template <int FMT, int BM, int BN, int WM, int WN, int NS, int ABL = 0, int PIPE = 0>
-__global__ __launch_bounds__(WM* WN * 64, 1) void qgemm_tile_kernel(
-    QW w, const bf16* __restrict__ X, int ldx, int M, int per_split, int m_tiles, int n_tiles, int splits,
-    int real_tiles, float* __restrict__ out, bf16* __restrict__ outb, int ldo, long slab) {
+LA_DEV void gq_tile(uint8_t* __restrict__ lds, const QW& w, int tile, const bf16* __restrict__ X, int ldx, int M,
+                    int per_split, int m_tiles, int n_tiles, float* __restrict__ out, bf16* __restrict__ outb,
+                    int ldo, long slab) {
   using WS = GqW<FMT, BN>;
   constexpr int NW = WM * WN;
   constexpr int TM = BM / WM, TN = BN / WN;
@@ -235,13 +238,6 @@ __global__ __launch_bounds__(WM* WN * 64, 1) void qgemm_tile_kernel(
   constexpr int LA = PX + PWA + 1, LB = PX + PWA;
   static_assert(BM % (8 * NW) == 0 && MT >= 1 && NT >= 1 && TM % 16 == 0 && TN % 16 == 0, "tile shape");
   static_assert(NS >= 2 && NS <= 4, "ring depth");
-  __shared__ __attribute__((aligned(1024))) uint8_t lds[NS * SLOT];
-
-  // XCD-aware tile order: blocks b, b + 8, ... share an XCD; each XCD takes a contiguous run
-  const int nwg = gridDim.x;
-  const int xcd = blockIdx.x & 7, q8 = nwg >> 3;
-  const int tile = xcd * q8 + (blockIdx.x >> 3);
-  if (tile >= real_tiles) return;  // grid padded to a multiple of 8
   const int mt_i = tile % m_tiles;
   const int rest = tile / m_tiles;
   const int nt_i = rest % n_tiles;
@@ -497,6 +493,39 @@ __global__ __launch_bounds__(WM* WN * 64, 1) void qgemm_tile_kernel(
   }
 }
 
+// Single weight: tiles (M fastest, then N, then split) in XCD-contiguous runs (blocks b, b + 8, ...
+// share an XCD; each XCD takes a contiguous run, so the M tiles of one weight panel share an L2).
+template <int FMT, int BM, int BN, int WM, int WN, int NS, int ABL = 0, int PIPE = 0>
+__global__ __launch_bounds__(WM* WN * 64, 1) void qgemm_tile_kernel(
+    QW w, const bf16* __restrict__ X, int ldx, int M, int per_split, int m_tiles, int n_tiles, int splits,
+    int real_tiles, float* __restrict__ out, bf16* __restrict__ outb, int ldo, long slab) {
+  __shared__ __attribute__((aligned(1024))) uint8_t lds[NS * (BM * 128 + GqW<FMT, BN>::LDS)];
+  const int tile = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+  if (tile >= real_tiles) return;  // grid padded to a multiple of 8
+  gq_tile<FMT, BM, BN, WM, WN, NS, ABL, PIPE>(lds, w, tile, X, ldx, M, per_split, m_tiles, n_tiles, out, outb, ldo,
+                                               slab);
+}
+
+// Two weights of one fused output (a Q4_K q|k beside a Q6_K v, a Q4_K gate beside a Q6_K up...)
+// in ONE launch: segment B's tiles follow segment A's, so the small segment's tiles run beside
+// the large one's instead of as a separate low-occupancy launch.
+template <int FA, int FB, int BM, int BN, int WM, int WN, int NS>
+__global__ __launch_bounds__(WM* WN * 64, 1) void qgemm_tile2_kernel(
+    QW wa, QW wb, int col_b, const bf16* __restrict__ X, int ldx, int M, int per_split, int m_tiles, int n_tiles_a,
+    int n_tiles_b, int tiles_a, int real_tiles, float* __restrict__ out, bf16* __restrict__ outb, int ldo,
+    long slab) {
+  constexpr int LA_ = NS * (BM * 128 + GqW<FA, BN>::LDS), LB_ = NS * (BM * 128 + GqW<FB, BN>::LDS);
+  __shared__ __attribute__((aligned(1024))) uint8_t lds[LA_ > LB_ ? LA_ : LB_];
+  const int tile = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+  if (tile >= real_tiles) return;
+  if (tile < tiles_a) {
+    gq_tile<FA, BM, BN, WM, WN, NS>(lds, wa, tile, X, ldx, M, per_split, m_tiles, n_tiles_a, out, outb, ldo, slab);
+  } else {
+    gq_tile<FB, BM, BN, WM, WN, NS>(lds, wb, tile - tiles_a, X, ldx, M, per_split, m_tiles, n_tiles_b,
+                                    out ? out + col_b : nullptr, outb ? outb + col_b : nullptr, ldo, slab);
+  }
+}
+
 // Blocked scale plane for the tile GEMM: [ceil(N/16)][K/64][16 cols][8 B], one record per
 // (column, K-step).  Rows past N repeat row N-1.
 //   Q4_K: f16 d*sc, f16 -dmin*m of sub-block 2(ks%4), then of sub-block 2(ks%4)+1, from the
@@ -550,6 +579,32 @@ static void gq_launch(const QW& w, const bf16* X, int ldx, int M, int splits, fl
   const int grid = (real + 7) / 8 * 8;
   hipLaunchKernelGGL((qgemm_tile_kernel<FMT, BM, BN, WM, WN, NS, ABL, PIPE>), dim3(grid), dim3(WM * WN * 64), 0, st, w, X,
                      ldx, M, per, m_tiles, n_tiles, splits, real, out, outb, ldo, slab);
+}
+
+template <int FA, int FB, int BM, int BN, int WM, int WN, int NS>
+static void gq_launch2(const QW& wa, const QW& wb, const bf16* X, int ldx, int M, int splits, float* out,
+                       bf16* outb, int ldo, long slab, hipStream_t st) {
+  const int KS = wa.K / GQ_BK;
+  const int per = (KS + splits - 1) / splits;
+  const int m_tiles = (M + BM - 1) / BM;
+  const int nta = (wa.N + BN - 1) / BN, ntb = (wb.N + BN - 1) / BN;
+  const int tiles_a = m_tiles * nta * splits;
+  const int real = tiles_a + m_tiles * ntb * splits;
+  const int grid = (real + 7) / 8 * 8;
+  hipLaunchKernelGGL((qgemm_tile2_kernel<FA, FB, BM, BN, WM, WN, NS>), dim3(grid), dim3(WM * WN * 64), 0, st, wa, wb,
+                     wa.N, X, ldx, M, per, m_tiles, nta, ntb, tiles_a, real, out, outb, ldo, slab);
+}
+
+template <int FA, int FB>
+static int gq_dispatch2(int tile, const QW& wa, const QW& wb, const bf16* X, int ldx, int M, int splits, float* out,
+                        bf16* outb, int ldo, long slab, hipStream_t st) {
+  switch (tile) {
+    case 7: gq_launch2<FA, FB, 128, 256, 1, 8, 3>(wa, wb, X, ldx, M, splits, out, outb, ldo, slab, st); break;
+    case 8: gq_launch2<FA, FB, 256, 128, 2, 4, 2>(wa, wb, X, ldx, M, splits, out, outb, ldo, slab, st); break;
+    case 12: gq_launch2<FA, FB, 128, 128, 2, 4, 3>(wa, wb, X, ldx, M, splits, out, outb, ldo, slab, st); break;
+    default: return -1;
+  }
+  return 0;
 }
 
 // tile ids (shared with ops/__init__.py GQ_TILES):
@@ -641,6 +696,34 @@ extern "C" int la_qgemm_tile(int fmt, const void* p0, const void* p1, const void
     default: return -2;
   }
 #undef GQ_CASE
+  if (rc) return rc;
+  return (int)hipGetLastError();
+}
+
+// Two weights (same K) side by side in one output [M][ldo]: columns [0, Na) from (fa, pa*) and
+// [Na, Na+Nb) from (fb, pb*).  Pairs: Q4_K + Q6_K, Q6_K + Q4_K.  Tiles 7, 8, 12.
+extern "C" int la_qgemm_tile2(int fa, const void* pa0, const void* pa1, const void* ga, int Na, int fb,
+                              const void* pb0, const void* pb1, const void* gb, int Nb, int K, const void* X,
+                              int ldx, int M, int splits, void* out, int ldo, long slab, int out_bf16, int tile,
+                              void* stream) {
+  using namespace la;
+  if (M < 1 || Na < 1 || Nb < 1 || (K & 255) || splits < 1 || ldo < Na + Nb || ldx < K || (ldx & 7)) return -1;
+  if (out_bf16 && splits != 1) return -1;
+  if (!out_bf16 && slab < (long)M * ldo) return -1;
+  if ((long)M * ldx >= (1L << 31)) return -1;
+  const int KS = K / 64, per = (KS + splits - 1) / splits;
+  if (per * (splits - 1) >= KS) return -1;
+  if (!ga || !gb) return -1;
+  QW wa{(const uint8_t*)pa0, (const uint8_t*)pa1, (const uint8_t*)ga, nullptr, Na, K};
+  QW wb{(const uint8_t*)pb0, (const uint8_t*)pb1, (const uint8_t*)gb, nullptr, Nb, K};
+  hipStream_t st = (hipStream_t)stream;
+  const bf16* x = (const bf16*)X;
+  float* o = out_bf16 ? nullptr : (float*)out;
+  bf16* ob = out_bf16 ? (bf16*)out : nullptr;
+  int rc;
+  if (fa == FMT_Q4_K && fb == FMT_Q6_K) rc = gq_dispatch2<FMT_Q4_K, FMT_Q6_K>(tile, wa, wb, x, ldx, M, splits, o, ob, ldo, slab, st);
+  else if (fa == FMT_Q6_K && fb == FMT_Q4_K) rc = gq_dispatch2<FMT_Q6_K, FMT_Q4_K>(tile, wa, wb, x, ldx, M, splits, o, ob, ldo, slab, st);
+  else return -2;
   if (rc) return rc;
   return (int)hipGetLastError();
 }

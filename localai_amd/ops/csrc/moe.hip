@@ -19,8 +19,8 @@ constexpr int MOE_WAVES = 4;
 constexpr int MOE_THREADS = 64 * MOE_WAVES;
 constexpr int MOE_LDS_STRIDE = 256 + 8;
 
-__global__ __launch_bounds__(256) void moe_route_kernel(const int* __restrict__ ids, int T, int topk, int E,
-                                                        int* __restrict__ order, int* __restrict__ off) {
+__global__ __launch_bounds__(1024) void moe_route_kernel(const int* __restrict__ ids, int T, int topk, int E,
+                                                         int* __restrict__ order, int* __restrict__ off) {
   __shared__ int cnt[256];
   __shared__ int base[257];
   const int P = T * topk;
@@ -34,11 +34,18 @@ __global__ __launch_bounds__(256) void moe_route_kernel(const int* __restrict__ 
   }
   __syncthreads();
   for (int e = threadIdx.x; e <= E; e += blockDim.x) off[e] = base[e];
-  // stable placement: expert e's pairs in increasing pair order (one thread per expert)
-  for (int e = threadIdx.x; e < E; e += blockDim.x) {
+  // stable placement, one wave per expert: 64 pairs per ballot, each hit's slot = its rank
+  // among the hits of lower lanes (expert e's pairs land in increasing pair order)
+  const int lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+  for (int e = threadIdx.x >> 6; e < E; e += nw) {
     int o = base[e];
-    for (int p = 0; p < P; ++p)
-      if (min(max(ids[p], 0), E - 1) == e) order[o++] = p;
+    for (int p0 = 0; p0 < P; p0 += 64) {
+      const int p = p0 + lane;
+      const bool hit = p < P && min(max(ids[p], 0), E - 1) == e;
+      const unsigned long long m = __ballot(hit);
+      if (hit) order[o + __popcll(m & ((1ull << lane) - 1ull))] = p;
+      o += __popcll(m);
+    }
   }
 }
 
@@ -108,13 +115,15 @@ template <int FMT, int MT, bool DOWN>
 __global__ __launch_bounds__(MOE_THREADS, 2) void moe_gemm_kernel(
     const QW* __restrict__ qws, const int* __restrict__ order, const int* __restrict__ off, int topk,
     const bf16* __restrict__ X, int ldx, int k_per_split, const float* __restrict__ wts, float* __restrict__ out,
-    int ldo, long slab, int T) {
+    int ldo, long slab, int T, int nchunk) {
   constexpr int MP = 16 * MT;
   __shared__ __attribute__((aligned(16))) bf16 xs[MP * MOE_LDS_STRIDE];
   __shared__ int prow[MP];
 
-  const int e = blockIdx.z;
-  const int o0 = off[e];
+  // blockIdx.z = expert * nchunk + chunk: chunk c takes the expert's rows [c*MP, c*MP + MP), so any
+  // batch size is one fixed-shape launch (chunks past an expert's row count exit at once)
+  const int e = blockIdx.z / nchunk, chunk = blockIdx.z - e * nchunk;
+  const int o0 = off[e] + chunk * MP;
   const int M = min(off[e + 1] - o0, MP);
   if (M <= 0) return;
   const QW w = qws[e];
@@ -215,13 +224,17 @@ static void launch_moe(const QW* qws, int N, int K, int E, const int* order, con
                        const bf16* X, int ldx, int maxM, int splits, const float* wts, float* out, int ldo, long slab,
                        int T, hipStream_t st) {
   const int per = (K >> 8) / splits;
-  dim3 grid((N + 16 * MOE_WAVES - 1) / (16 * MOE_WAVES), splits, E);
-#define MOE_L(MT)                                                                                            \
-  hipLaunchKernelGGL((moe_gemm_kernel<FMT, MT, DOWN>), grid, dim3(MOE_THREADS), 0, st, qws, order, off, topk, X, \
-                     ldx, per * 256, wts, out, ldo, slab, T)
-  if (maxM <= 16) MOE_L(1);
-  else if (maxM <= 32) MOE_L(2);
-  else MOE_L(4);
+  const int gx = (N + 16 * MOE_WAVES - 1) / (16 * MOE_WAVES);
+#define MOE_L(MT)                                                                                                \
+  {                                                                                                              \
+    const int nch = (maxM + 16 * (MT)-1) / (16 * (MT));                                                          \
+    hipLaunchKernelGGL((moe_gemm_kernel<FMT, MT, DOWN>), dim3(gx, splits, E * nch), dim3(MOE_THREADS), 0, st, qws, \
+                       order, off, topk, X, ldx, per * 256, wts, out, ldo, slab, T, nch);                        \
+  }
+  if (maxM <= 16) MOE_L(1)
+  else if (maxM <= 32) MOE_L(2)
+  else if (maxM <= 64) MOE_L(4)
+  else MOE_L(8)
 #undef MOE_L
 }
 
@@ -237,17 +250,18 @@ extern "C" int la_moe_router(const void* x, int ldx, const float* wr, int E, int
 
 extern "C" int la_moe_route(const int* ids, int T, int topk, int E, int* order, int* off, void* stream) {
   if (E > 256 || E < 1) return -1;
-  hipLaunchKernelGGL(la::moe_route_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, ids, T, topk, E, order, off);
+  hipLaunchKernelGGL(la::moe_route_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, ids, T, topk, E, order, off);
   return (int)hipGetLastError();
 }
 
 // qws: device array of E QW descriptors (all experts share fmt, N, K).  maxM = max rows per expert
-// (<= T for GATE_UP / DOWN since a token picks an expert at most once) must be <= 64.
+// (<= T for GATE_UP / DOWN since a token picks an expert at most once); above 64 the launch covers
+// ceil(maxM / 128) row chunks per expert.
 extern "C" int la_moe_gemm(int fmt, int down, const void* qws, int N, int K, int E, const int* order, const int* off,
                            int topk, const void* X, int ldx, int maxM, int splits, const float* wts, void* out,
                            int ldo, long slab, int T, void* stream) {
   using namespace la;
-  if (maxM < 1 || maxM > 64 || (K & 255) || splits < 1 || ((K >> 8) % splits) || ldo < N) return -1;
+  if (maxM < 1 || E * ((maxM + 127) / 128) > 65535 || (K & 255) || splits < 1 || ((K >> 8) % splits) || ldo < N) return -1;
   hipStream_t st = (hipStream_t)stream;
   const QW* q = (const QW*)qws;
   const bf16* x = (const bf16*)X;

@@ -84,6 +84,31 @@ def test_mixtral_moe_graph_decode(tmp_path):
     assert first == int(top.indices[0]) or float(top.values[0] - ref[first]) < 0.05
 
 
+def test_mixtral_moe_wide_batch_graph_decode(tmp_path):
+    """Decode batches past 64 tokens run the row-chunked grouped expert GEMM inside the captured
+    graph (no per-expert host loop): 100 concurrent requests, multi-step == single-step, and a
+    graph was captured for the padded batch."""
+    from localai_amd.models import synth
+    p = str(tmp_path / "tiny-mixtral.gguf")
+    synth.write_model(p, "tiny-mixtral", exact=True)
+
+    def eng(K):
+        return LLMEngine(EngineConfig(model_path=p, device="cuda:0", context_size=256, max_num_seqs=128,
+                                      max_batched_tokens=2048, decode_steps=K))
+    prompts = [f"expert wave {i}" for i in range(100)]
+    e1 = eng(1)
+    a = _run(e1, prompts, max_tokens=6, temperature=0.0, ignore_eos=True)
+    e8 = eng(8)
+    b = _run(e8, prompts, max_tokens=6, temperature=0.0, ignore_eos=True)
+    assert all(x[1] == 6 for x in a) and a == b
+    assert any(bp > 64 for bp in e8._graphs), sorted(e8._graphs)
+    ids = e8.tokenize(prompts[7])
+    ref = e8.model.reference_logits(ids)[-1]
+    first = e8.tokenize(prompts[7] + a[7][0].decode("utf-8", "replace"))[len(ids)]
+    top = torch.topk(ref, 2)
+    assert first == int(top.indices[0]) or float(top.values[0] - ref[first]) < 0.05
+
+
 @pytest.mark.parametrize("preset", ["tiny-qwen2", "tiny-phi3", "tiny-gemma", "tiny-gemma2", "tiny-command-r",
                                     "tiny-starcoder2", "tiny-qwen2moe", "tiny-deepseek2"])
 def test_model_families_graph_decode(preset, tmp_path):

@@ -117,3 +117,21 @@ def test_linear_dispatch_llama3_shapes(M):
         assert ops._GEMM_CHOICE, "autotune recorded no choice"
         for key, ch in ops._GEMM_CHOICE.items():
             assert ch[0] == "tile", (key, ch)
+
+
+@pytest.mark.parametrize("tile", [7, 8, 12])
+@pytest.mark.parametrize("S", [1, 3])
+def test_tile_gemm_two_segments_one_launch(tile, S):
+    """Q4_K q|k beside a Q6_K v (and the reverse) in one la_qgemm_tile2 launch."""
+    K, M = 1536, 200
+    for fa, fb in ((GGMLType.Q4_K, GGMLType.Q6_K), (GGMLType.Q6_K, GGMLType.Q4_K)):
+        ws = [_qw(320, K, fa, seed=1), _qw(96, K, fb, seed=2)]
+        x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+        Ntot = 416
+        out = (torch.full((M, Ntot), float("nan"), dtype=torch.bfloat16, device=DEV) if S == 1 else
+               torch.full((S, M, Ntot), float("nan"), dtype=torch.float32, device=DEV))
+        ops._run_tile(x, ws, S, out, Ntot, tile)
+        torch.cuda.synchronize()
+        y = out.float().cpu() if S == 1 else out.sum(0).cpu()
+        ref = torch.cat([x.float().cpu() @ w.ref.t() for w in ws], -1)
+        _check(y, ref)

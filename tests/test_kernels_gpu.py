@@ -527,8 +527,9 @@ def test_decode_advance_kernel():
     assert int(g[5].item()) == 1 and list(g[4][0].cpu()) == [7, 8, 9, 10, 11]
 
 
-@pytest.mark.parametrize("T", [1, 5, 33])
+@pytest.mark.parametrize("T", [1, 5, 33, 100, 300])
 def test_moe_grouped_gemm(T):
+    """Grouped expert GEMM at decode and wide / prefill batch sizes (T > 64: row-chunked grid)."""
     E, topk, D, F = 8, 2, 512, 768
     gu = [_qw(2 * F, D, GGMLType.Q4_K, seed=10 + e) for e in range(E)]
     dn = [_qw(D, F, GGMLType.Q6_K, seed=30 + e) for e in range(E)]
@@ -539,20 +540,34 @@ def test_moe_grouped_gemm(T):
     order, off = ops.moe_route(ids, E)
     o = order.cpu().tolist()
     assert sorted(o) == list(range(T * topk))
-    y = ops.moe_linear(x, mg, order, off, topk, T).dense()          # [T*topk, 2F]
-    idc = ids.cpu()
-    for p in range(T * topk):
-        e = int(idc.view(-1)[p])
-        ref = x[p // topk].float().cpu() @ gu[e].ref.t()
-        assert (y[p].cpu() - ref).abs().max() < 2e-2 * max(1.0, ref.abs().max())
+    idc = ids.cpu().view(-1).long()
+    offc = off.cpu().tolist()
+    for e in range(E):  # grouped by expert, stable (increasing pair id) inside each group
+        grp = o[offc[e]:offc[e + 1]]
+        assert grp == sorted(grp) and all(int(idc[p]) == e for p in grp)
+    y = ops.moe_linear(x, mg, order, off, topk, T).dense().cpu()          # [T*topk, 2F]
+    xc = x.float().cpu()
+    ref = torch.stack([xc[p // topk] for p in range(T * topk)])
+    ref = torch.stack([ref[p] @ gu[int(idc[p])].ref.t() for p in range(T * topk)])
+    assert (y - ref).abs().max() < 2e-2 * max(1.0, ref.abs().max())
     h = torch.randn(T * topk, F, device=DEV).to(torch.bfloat16)
     z = ops.moe_linear(h, md, order, off, topk, T, down=True, wts=wts.reshape(-1).contiguous()).dense()  # [T, D]
+    hc, wc = h.float().cpu(), wts.cpu().view(-1)
     ref = torch.zeros(T, D)
     for p in range(T * topk):
-        t, slot = divmod(p, topk)
-        e = int(idc.view(-1)[p])
-        ref[t] += float(wts.view(-1)[p]) * (h[p].float().cpu() @ dn[e].ref.t())
+        ref[p // topk] += float(wc[p]) * (hc[p] @ dn[int(idc[p])].ref.t())
     assert (z.cpu() - ref).abs().max() < 2e-2 * max(1.0, ref.abs().max())
+
+
+def test_moe_route_skewed_large():
+    """Every pair on one expert (the row-chunk grid's worst case) and 4096 pairs over 64 experts."""
+    for T, topk, E in ((200, 1, 8), (2048, 2, 64)):
+        ids = (torch.zeros(T, topk, dtype=torch.int32) if E == 8 else
+               torch.randint(0, E, (T, topk), dtype=torch.int32))
+        order, off = ops.moe_route(ids.to(DEV), E)
+        ref = torch.sort(ids.view(-1).long(), stable=True).indices
+        assert torch.equal(order.cpu().long(), ref)
+        assert off.cpu().tolist() == [0] + torch.bincount(ids.view(-1).long(), minlength=E).cumsum(0).tolist()
 
 
 @pytest.mark.parametrize("M", [1, 100, 256, 300])
