@@ -13,7 +13,8 @@ from .. import __version__
 from ..config.backend_config import BackendConfig
 from ..grpc import backend_pb as pb
 from .metrics import CONTENT_TYPE
-from .model_manager import ENGINE_BACKENDS, HF_BACKENDS, MAMBA_BACKEND, RWKV_BACKEND, SD_BACKENDS, STORE_BACKEND
+from .model_manager import (BARK_BACKENDS, ENGINE_BACKENDS, HF_BACKENDS, MAMBA_BACKEND, MUSICGEN_BACKENDS, RWKV_BACKEND,
+                            SD_BACKENDS, STORE_BACKEND, VITS_BACKENDS)
 from .openai_routes import APIError, merge_request_with_config, model_from_context, read_request
 
 
@@ -47,8 +48,8 @@ def build_router(state) -> APIRouter:
     r.add_api_route("/generated-audio/{name:path}", _static("audio_dir"), methods=["GET", "HEAD"])
 
     async def system():
-        backends = sorted(set(b for b in ENGINE_BACKENDS if b) | HF_BACKENDS | SD_BACKENDS |
-                          {MAMBA_BACKEND, RWKV_BACKEND}) + \
+        backends = sorted(set(b for b in ENGINE_BACKENDS if b) | HF_BACKENDS | SD_BACKENDS | VITS_BACKENDS |
+                          MUSICGEN_BACKENDS | BARK_BACKENDS | {MAMBA_BACKEND, RWKV_BACKEND}) + \
             [STORE_BACKEND] + list(state.cfg.external_grpc_backends)
         from ..utils.sysinfo import system_info
         return {"backends": backends, "loaded_models": [{"id": m.id} for m in state.manager.list_loaded()],
@@ -196,6 +197,8 @@ def build_router(state) -> APIRouter:
         cfg = merge_request_with_config(state, model, {"model": model})
         if backend:
             cfg.backend = backend
+        elif not cfg.backend:
+            cfg.backend = "piper"  # core/backend/tts.go: piper when neither the request nor the config names one
         lm = await state.manager.load(cfg)
         os.makedirs(state.cfg.audio_dir, exist_ok=True)
         dst = os.path.join(state.cfg.audio_dir, f"tts_{uuid.uuid4().hex}.wav")

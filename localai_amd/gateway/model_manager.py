@@ -41,6 +41,9 @@ HF_BACKENDS = {"huggingface", "langchain-huggingface"}  # remote Inference API (
 MAMBA_BACKEND = "mamba"  # selective state-space LMs (models/mamba.py, ops/csrc/mamba.hip)
 RWKV_BACKEND = "rwkv"    # RWKV-4 recurrent LMs (models/rwkv.py)
 SD_BACKENDS = {"diffusers", "stablediffusion"}  # Stable Diffusion 1.x / 2.x pipelines (models/sd.py)
+VITS_BACKENDS = {"piper", "vits", "mms-tts"}    # VITS text-to-speech voices (models/tts.py)
+MUSICGEN_BACKENDS = {"transformers-musicgen", "musicgen"}  # text-to-music (models/musicgen.py)
+BARK_BACKENDS = {"bark"}                         # text-to-speech/audio (models/bark.py)
 
 
 def free_port() -> int:
@@ -202,6 +205,15 @@ class ModelManager:
         if backend in SD_BACKENDS:
             from ..grpc.diffusers_servicer import DiffusersServicer
             sv = DiffusersServicer(device=self._pick_device(cfg))
+            res = await sv.LoadModel(grpc_model_options(cfg, self.app, self.models_path), None)
+            if not res.success:
+                raise RuntimeError(f"could not load model: {res.message}")
+            return LoadedModel(mid, backend, EmbeddedBackend(sv), servicer=sv)
+        if backend in VITS_BACKENDS | MUSICGEN_BACKENDS | BARK_BACKENDS:
+            from ..grpc import audio_servicer as au
+            cls = (au.VitsServicer if backend in VITS_BACKENDS else
+                   au.MusicgenServicer if backend in MUSICGEN_BACKENDS else au.BarkServicer)
+            sv = cls(device=self._pick_device(cfg))
             res = await sv.LoadModel(grpc_model_options(cfg, self.app, self.models_path), None)
             if not res.success:
                 raise RuntimeError(f"could not load model: {res.message}")

@@ -1,0 +1,95 @@
+"""Text-to-speech / sound-generation backend servicers (backend.proto LoadModel + TTS /
+SoundGeneration) over the native audio models.
+
+  piper / vits / mms-tts     VITS voices (models/tts.py)        -- backend/go/tts/piper.go:30-49
+  transformers-musicgen      MusicGen (models/musicgen.py)      -- backend/python/transformers-musicgen/backend.py:66,121
+  bark                       Bark (models/bark.py)              -- backend/python/bark/backend.py:44
+
+TTS writes a 16-bit PCM wav to `request.dst` and answers `Result(success=True)`, as the
+reference backends do.  `voice` selects a speaker id of a multi-speaker VITS voice (a number) or
+a Bark history prompt name; `language` is accepted and ignored (the voice fixes the language).
+"""
+from __future__ import annotations
+
+import asyncio
+import os
+import threading
+
+from . import backend_pb as pb
+
+
+class _AudioBase:
+    kind = "audio"
+
+    def __init__(self, device: str = ""):
+        self.device = device
+        self.model = None
+        self.state = pb.StatusResponse.UNINITIALIZED
+        self._lock = threading.Lock()
+
+    def _dev(self) -> str:
+        if self.device:
+            return self.device
+        import torch
+        return "cuda:0" if torch.cuda.is_available() else "cpu"
+
+    async def Health(self, request, context=None):
+        return pb.Reply(message=b"OK")
+
+    async def Status(self, request, context=None):
+        return pb.StatusResponse(state=self.state)
+
+    def shutdown(self):
+        self.model, self.state = None, pb.StatusResponse.UNINITIALIZED
+
+    def _load(self, path: str):
+        raise NotImplementedError
+
+    async def LoadModel(self, request, context=None):
+        path = request.ModelFile or request.Model
+        try:
+            m = await asyncio.get_running_loop().run_in_executor(None, self._load, path)
+        except Exception as e:  # noqa: BLE001 - reported to the caller like the reference
+            return pb.Result(success=False, message=f"{self.kind}: could not load {path}: {e}")
+        self.model, self.state = m, pb.StatusResponse.READY
+        return pb.Result(success=True, message="Model loaded successfully")
+
+    async def TTS(self, request, context=None):
+        return pb.Result(success=False, message=f"TTS is not supported by the {self.kind} backend")
+
+    async def SoundGeneration(self, request, context=None):
+        return pb.Result(success=False, message=f"SoundGeneration is not supported by the {self.kind} backend")
+
+    async def _run(self, fn, *a):
+        try:
+            await asyncio.get_running_loop().run_in_executor(None, fn, *a)
+        except Exception as e:  # noqa: BLE001
+            return pb.Result(success=False, message=f"{self.kind}: {e}")
+        return pb.Result(success=True, message="Media generated")
+
+
+class VitsServicer(_AudioBase):
+    """piper / vits / mms-tts voices."""
+    kind = "vits"
+
+    def _load(self, path):
+        from ..models.tts import VitsVoice, is_vits_dir
+        if path.endswith(".onnx"):
+            raise ValueError("ONNX piper voices are not loadable here (no ONNX runtime): use the voice's VITS "
+                             "checkpoint in the Hugging Face layout (config.json + vocab.json + model.safetensors)")
+        if not is_vits_dir(path):
+            raise ValueError("not a VITS checkpoint directory (config.json model_type 'vits')")
+        return VitsVoice(path, self._dev())
+
+    def _tts(self, request):
+        from ..models.tts import write_wav
+        v = self.model
+        if v is None:
+            raise RuntimeError("no model loaded")
+        sid = int(request.voice) if request.voice.strip().isdigit() else None
+        with self._lock:
+            audio = v.synthesize(request.text, speaker_id=sid)
+        write_wav(request.dst, audio, v.sampling_rate)
+
+    async def TTS(self, request, context=None):
+        return await self._run(self._tts, request)

@@ -436,8 +436,12 @@ class DecoderModel:
         hp = self.hp
         if L.experts is not None:
             return self._moe(L, xn)
+        F, mode = L.F or self.F, _ACT[hp.act]
+        h = ops.glu_linear(xn, L.gate_up, F, mode, L.up_bias)  # decode batches: act in the GEMM epilogue
+        if h is not None:
+            return self._row_parallel_out(ops.linear(h, L.down), L.down_bias)
         gu = ops.linear_multi(xn, L.gate_up, bias=L.up_bias)
-        d = ops.act_linear(gu, L.F or self.F, _ACT[hp.act], L.down)
+        d = ops.act_linear(gu, F, mode, L.down)
         return self._row_parallel_out(d, L.down_bias)
 
     def _moe(self, L: Layer, xn: torch.Tensor) -> ops.Partial:

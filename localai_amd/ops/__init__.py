@@ -15,7 +15,7 @@ import math
 import os
 import threading
 from dataclasses import dataclass
-from typing import List, Optional, Sequence, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -74,6 +74,7 @@ def lib():
             "la_qgemm_tile": [I, P, P, P, I, I, P, I, I, I, P, I, LNG, I, I, I, P],
             "la_qgemm_tile_probe": [P, P, I, I, P, I, I, P, I, I, P],
             "la_qgemm_tile2": [I, P, P, P, I, I, P, P, P, I, I, P, I, I, I, P, I, LNG, I, I, P],
+            "la_qgemm_glu": [I, P, P, P, I, P, P, P, I, I, I, P, I, I, P, I, I, I, P],
             "la_decode_advance": [P, P, P, P, P, P, I, I, I, P, I, P, P, P],
         }
         for name, args in sig.items():
@@ -898,6 +899,80 @@ def linear_multi(x: torch.Tensor, ws: Sequence[QWeight], bias: Optional[torch.Te
             col += w.N
         return Partial(out, bias)
     return Partial(_run_blas(x, ws, Ntot), bias)
+
+
+GLU_FUSE = os.environ.get("LOCALAI_AMD_GLU_FUSE", "1") == "1"
+_GLU_CHOICE: Dict[tuple, Optional[int]] = {}
+
+
+def _glu_pair(ws: Sequence[QWeight], F: int):
+    """(gate weight, row offset, up weight, row offset) of a gate|up projection, or None."""
+    if not all(w.tile_ok for w in ws):
+        return None
+    if len(ws) == 2 and ws[0].N == F and ws[1].N == F and ws[0].fmt == ws[1].fmt:
+        return ws[0], 0, ws[1], 0
+    if len(ws) == 1 and ws[0].N == 2 * F and F % 16 == 0:
+        return ws[0], 0, ws[0], F
+    return None
+
+
+def _run_glu(x: torch.Tensor, pair, F: int, mode: int, tile: int, out: torch.Tensor) -> None:
+    M, K = x.shape
+    wa, oa, wb, ob = pair
+    a0, a1, ag = wa.tile_planes()
+    b0, b1, bg = wb.tile_planes()
+    _check(lib().la_qgemm_glu(wa.fmt, a0, a1, ag, oa, b0, b1, bg, ob, F, K, x.data_ptr(), K, M, out.data_ptr(), F,
+                              mode, tile, _stream()), "la_qgemm_glu")
+
+
+def _time_cold(fn) -> float:
+    fn()
+    ts = []
+    for _ in range(3):
+        _cold_caches(torch.device("cuda", torch.cuda.current_device()))
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        fn()
+        e1.record()
+        e1.synchronize()
+        ts.append(e0.elapsed_time(e1) * 1000)
+    return sorted(ts)[1]
+
+
+def glu_linear(x: torch.Tensor, ws: Sequence[QWeight], F: int, mode: int,
+               bias: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+    """act(x Wg^T) * (x Wu^T) -> bf16 [M, F] in ONE tile-GEMM launch with the GLU activation in
+    its epilogue (gate and up columns of the same index share a tile), for decode batches.  The
+    autotuner times it against the unfused pair (tuned GEMM + activation kernel) once per
+    32-row bucket; returns None where the fused kernel does not apply or loses."""
+    if not (GLU_FUSE and TILE_GEMM and x.is_cuda and bias is None and mode in GLU_ACTS):
+        return None
+    M, K = x.shape
+    if M <= SKINNY_MAX_M or M > MID_MAX_M:
+        return None
+    pair = _glu_pair(ws, F)
+    if pair is None:
+        return None
+    key = ((M + 31) // 32 * 32, K, F, mode, tuple((w.fmt, w.N) for w in ws))
+    if key not in _GLU_CHOICE:
+        if not GEMM_AUTOTUNE or torch.cuda.is_current_stream_capturing():
+            return None
+        out = torch.empty(M, F, dtype=torch.bfloat16, device=x.device)
+        t_ref = _time_cold(lambda: act(linear_multi(x, ws), F, mode))
+        best, best_t = None, t_ref
+        for t in ((6, 7, 8) if M > 128 else (7, 12, 14)):
+            tt = _time_cold(lambda t=t: _run_glu(x, pair, F, mode, t, out))
+            if tt < best_t:
+                best, best_t = t, tt
+        _GLU_CHOICE[key] = best
+        if os.environ.get("BENCH_DUMP_GEMM"):
+            print(f"glu choice M={M} K={K} F={F} -> {best} ({best_t:.1f} us vs unfused {t_ref:.1f} us)", flush=True)
+    tile = _GLU_CHOICE[key]
+    if tile is None:
+        return None
+    out = torch.empty(M, F, dtype=torch.bfloat16, device=x.device)
+    _run_glu(x, pair, F, mode, tile, out)
+    return out
 
 
 # ---------------------------------------------------------------------------------------

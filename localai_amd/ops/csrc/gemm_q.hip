@@ -51,23 +51,46 @@ LA_DEV void gq_wait_stages(int ahead) {
 // least 1 KiB so one DMA piece always fits).
 template <int FMT, int BN> struct GqW;
 
+// Tile column c -> (weight plane, weight row).  One weight: row n0 + c.  GLU pair (gate|up fused
+// into one tile): columns [0, half) are gate rows oa + j0 + c, columns [half, 2 half) the up rows
+// ob + j0 + (c - half) -- two weights, or two row ranges of one [2F, K] weight.  Rows clamp to
+// the last valid one (their results are never stored).
+template <bool GLU> struct GqCols;
+template <> struct GqCols<false> {
+  QW w;
+  int n0;
+  template <int P> LA_DEV const uint8_t* plane(int) const { return P == 0 ? w.p0 : P == 1 ? w.p1 : w.p2; }
+  LA_DEV int n(int c) const { return min(n0 + c, w.N - 1); }
+};
+template <> struct GqCols<true> {
+  QW a, b;
+  int oa, ob, j0, half, lim;  // lim = F - 1
+  template <int P> LA_DEV const uint8_t* plane(int c) const {
+    const QW& q = c < half ? a : b;
+    return P == 0 ? q.p0 : P == 1 ? q.p1 : q.p2;
+  }
+  LA_DEV int n(int c) const { return c < half ? oa + min(j0 + c, lim) : ob + min(j0 + c - half, lim); }
+};
+
 template <int BN> struct GqScales {
   static constexpr int BYTES = (BN * 8 > 1024) ? BN * 8 : 1024;
   static constexpr int PIECES = (BN * 8 + 1023) / 1024;
   // plane: [ceil(N/16)][K/64][16][8 B]; piece q covers columns 128q .. 128q+127 of the tile
-  LA_DEV static void issue(const uint8_t* gsc, int nblk, int KS, int n0, int q, int ks, uint8_t* dst, int lane) {
-    const int b = min((n0 >> 4) + 8 * q + (lane >> 3), nblk - 1);
-    gq_glds16(gsc + ((size_t)b * KS + ks) * 128 + 16 * (lane & 7), dst + q * 1024);
+  template <class CM>
+  LA_DEV static void issue(const CM& cm, int KS, int q, int ks, uint8_t* dst, int lane) {
+    const int c = 128 * q + 16 * (lane >> 3);  // this lane's 16-column block
+    const int b = cm.n(c) >> 4;
+    gq_glds16(cm.template plane<2>(c) + ((size_t)b * KS + ks) * 128 + 16 * (lane & 7), dst + q * 1024);
   }
 };
 
 // 32 B per column per K-step, 16-B halves swapped on columns with bit 3 set (conflict-free
 // ds_read_b64 for lanes (n = l & 15, g = l >> 4) reading 8 B at logical offset 8g)
-LA_DEV void gq_issue32(const uint8_t* plane, int row_bytes, int N, int n0, int p, int kofs, uint8_t* dst, int lane) {
+template <int P, class CM>
+LA_DEV void gq_issue32(const CM& cm, int row_bytes, int p, int kofs, uint8_t* dst, int lane) {
   const int c = 32 * p + (lane >> 1);
-  const int n = min(n0 + c, N - 1);
   const int lh = (lane & 1) ^ ((c >> 3) & 1);
-  gq_glds16(plane + (size_t)n * row_bytes + kofs + 16 * lh, dst + p * 1024);
+  gq_glds16(cm.template plane<P>(c) + (size_t)cm.n(c) * row_bytes + kofs + 16 * lh, dst + p * 1024);
 }
 LA_DEV u32x2 gq_read32(const uint8_t* area, int col, int g) {
   return *(const u32x2*)(area + col * 32 + 16 * ((g >> 1) ^ ((col >> 3) & 1)) + 8 * (g & 1));
@@ -78,9 +101,10 @@ template <int BN> struct GqW<FMT_Q4_K, BN> {
   static constexpr int LDS = CODES + GqScales<BN>::BYTES;
   static constexpr int PC = BN / 32;
   static constexpr int PIECES = PC + GqScales<BN>::PIECES;
-  LA_DEV static void issue(const QW& w, int n0, int p, int ks, uint8_t* wl, int lane) {
-    if (p < PC) gq_issue32(w.p0, w.K >> 1, w.N, n0, p, 32 * ks, wl, lane);
-    else GqScales<BN>::issue(w.p2, (w.N + 15) >> 4, w.K >> 6, n0, p - PC, ks, wl + CODES, lane);
+  template <class CM>
+  LA_DEV static void issue(const CM& cm, int K, int p, int ks, uint8_t* wl, int lane) {
+    if (p < PC) gq_issue32<0>(cm, K >> 1, p, 32 * ks, wl, lane);
+    else GqScales<BN>::issue(cm, K >> 6, p - PC, ks, wl + CODES, lane);
   }
   struct Frag {
     u32x2 q;
@@ -120,16 +144,17 @@ template <int BN> struct GqW<FMT_Q6_K, BN> {
   static constexpr int LDS = CODES + GqScales<BN>::BYTES;
   static constexpr int PC = BN / 32;
   static constexpr int PIECES = 2 * PC + GqScales<BN>::PIECES;
-  LA_DEV static void issue(const QW& w, int n0, int p, int ks, uint8_t* wl, int lane) {
+  template <class CM>
+  LA_DEV static void issue(const CM& cm, int K, int p, int ks, uint8_t* wl, int lane) {
     const int sb = ks >> 2, hh = (ks >> 1) & 1, part = ks & 1;
-    if (p < PC) gq_issue32(w.p0, w.K >> 1, w.N, n0, p, sb * 128 + 64 * hh + 32 * part, wl, lane);
-    else if (p < 2 * PC) gq_issue32(w.p1, w.K >> 2, w.N, n0, p - PC, sb * 64 + 32 * hh, wl + BN * 32, lane);
-    else GqScales<BN>::issue(w.p2, (w.N + 15) >> 4, w.K >> 6, n0, p - 2 * PC, ks, wl + CODES, lane);
+    if (p < PC) gq_issue32<0>(cm, K >> 1, p, sb * 128 + 64 * hh + 32 * part, wl, lane);
+    else if (p < 2 * PC) gq_issue32<1>(cm, K >> 2, p - PC, sb * 64 + 32 * hh, wl + BN * 32, lane);
+    else GqScales<BN>::issue(cm, K >> 6, p - 2 * PC, ks, wl + CODES, lane);
   }
   struct Frag {
     u32x2 ql, qh;
-    float S[2];
-    int sh;  // qh bit offset of this K-step's part
+    float S[2], O[2];  // d*sc and -32*d*sc of this lane's 16-k scale group, per 32-k run
+    int sh;            // qh bit offset of this K-step's part
   };
   LA_DEV static void load(const uint8_t* wl, int col, int g, int ks, Frag& f) {
     f.ql = gq_read32(wl, col, g);
@@ -138,17 +163,32 @@ template <int BN> struct GqW<FMT_Q6_K, BN> {
     const int i = g >> 1;  // 16-k scale group inside each 32-k run
     f.S[0] = h2f(i ? (s.x >> 16) : (s.x & 0xFFFFu));
     f.S[1] = h2f(i ? (s.y >> 16) : (s.y & 0xFFFFu));
+    f.O[0] = -32.0f * f.S[0];
+    f.O[1] = -32.0f * f.S[1];
     f.sh = 2 * (ks & 1);
   }
+  // byte-parallel 6-bit codes: 4 weights per dword op (low nibble | 2 high bits << 4), then one
+  // v_cvt_f32_ubyteN + fma per weight: w = d*sc*q - 32*d*sc
   template <int S>
   LA_DEV static bf16x8 deq(const Frag& f) {
+    uint32_t lo0, lo1, q0, q1;
+    if constexpr (S == 0) {
+      asm("v_and_b32 %0, 0x0f0f0f0f, %1" : "=v"(lo0) : "v"(f.ql.x));
+      asm("v_and_b32 %0, 0x0f0f0f0f, %1" : "=v"(lo1) : "v"(f.ql.y));
+      const int up = 4 - f.sh;
+      asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(q0) : "v"(f.qh.x << up), "s"(0x30303030u), "v"(lo0));
+      asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(q1) : "v"(f.qh.y << up), "s"(0x30303030u), "v"(lo1));
+    } else {
+      asm("v_and_b32 %0, 0x0f0f0f0f, %1" : "=v"(lo0) : "v"(f.ql.x >> 4));
+      asm("v_and_b32 %0, 0x0f0f0f0f, %1" : "=v"(lo1) : "v"(f.ql.y >> 4));
+      asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(q0) : "v"(f.qh.x >> f.sh), "s"(0x30303030u), "v"(lo0));
+      asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(q1) : "v"(f.qh.y >> f.sh), "s"(0x30303030u), "v"(lo1));
+    }
     bf16x8 r;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const uint32_t l = (j < 4) ? f.ql.x : f.ql.y, h = (j < 4) ? f.qh.x : f.qh.y;
-      const int b = 8 * (j & 3);
-      const int q = (int)(((l >> (b + 4 * S)) & 0xFu) | (((h >> (b + f.sh + 4 * S)) & 3u) << 4)) - 32;
-      r[j] = (bf16)(f.S[S] * (float)q);
+    for (int b = 0; b < 4; ++b) {
+      r[b] = (bf16)fmaf(f.S[S], (float)((q0 >> (8 * b)) & 0xFFu), f.O[S]);
+      r[b + 4] = (bf16)fmaf(f.S[S], (float)((q1 >> (8 * b)) & 0xFFu), f.O[S]);
     }
     return r;
   }
@@ -159,14 +199,14 @@ template <int BN> struct GqW<FMT_Q8_0, BN> {
   static constexpr int LDS = CODES + GqScales<BN>::BYTES;
   static constexpr int PC = BN / 16;
   static constexpr int PIECES = PC + GqScales<BN>::PIECES;
-  LA_DEV static void issue(const QW& w, int n0, int p, int ks, uint8_t* wl, int lane) {
+  template <class CM>
+  LA_DEV static void issue(const CM& cm, int K, int p, int ks, uint8_t* wl, int lane) {
     if (p < PC) {
       const int c = 16 * p + (lane >> 2);
-      const int n = min(n0 + c, w.N - 1);
       const int lc = (lane & 3) ^ ((c >> 2) & 3);
-      gq_glds16(w.p0 + (size_t)n * w.K + 64 * ks + 16 * lc, wl + p * 1024);
+      gq_glds16(cm.template plane<0>(c) + (size_t)cm.n(c) * K + 64 * ks + 16 * lc, wl + p * 1024);
     } else {
-      GqScales<BN>::issue(w.p2, (w.N + 15) >> 4, w.K >> 6, n0, p - PC, ks, wl + CODES, lane);
+      GqScales<BN>::issue(cm, K >> 6, p - PC, ks, wl + CODES, lane);
     }
   }
   struct Frag {
@@ -198,11 +238,11 @@ template <int BN> struct GqW<FMT_Q8_0, BN> {
 template <int BN> struct GqW<FMT_BF16, BN> {
   static constexpr int LDS = BN * 128;
   static constexpr int PIECES = BN / 8;
-  LA_DEV static void issue(const QW& w, int n0, int p, int ks, uint8_t* wl, int lane) {
+  template <class CM>
+  LA_DEV static void issue(const CM& cm, int K, int p, int ks, uint8_t* wl, int lane) {
     const int c = 8 * p + (lane >> 3);
-    const int n = min(n0 + c, w.N - 1);
     const int lc = (lane & 7) ^ ((c >> 1) & 7);
-    gq_glds16(w.p0 + ((size_t)n * w.K + 64 * ks + 8 * lc) * 2, wl + p * 1024);
+    gq_glds16(cm.template plane<0>(c) + ((size_t)cm.n(c) * K + 64 * ks + 8 * lc) * 2, wl + p * 1024);
   }
   struct Frag {
     bf16x8 v[2];
@@ -222,10 +262,18 @@ template <int BN> struct GqW<FMT_BF16, BN> {
 // One (M tile, N tile, K split) of one weight; `tile` is the segment-local tile id and out/outb
 // already point at the segment's first output column.  Returns without touching memory when
 // the tile's K range is empty.
-template <int FMT, int BM, int BN, int WM, int WN, int NS, int ABL = 0, int PIPE = 0>
+// GLU (gate|up fused): the second weight, row offsets, F and the activation (0 SwiGLU, 3 GeGLU)
+struct GqGlu {
+  QW b;
+  int oa, ob, F, act;
+};
+
+LA_DEV float gq_gelu_tanh(float x) { return 0.5f * x * (1.f + tanhf(0.7978845608f * (x + 0.044715f * x * x * x))); }
+
+template <int FMT, int BM, int BN, int WM, int WN, int NS, int ABL = 0, int PIPE = 0, bool GLU = false>
 LA_DEV void gq_tile(uint8_t* __restrict__ lds, const QW& w, int tile, const bf16* __restrict__ X, int ldx, int M,
                     int per_split, int m_tiles, int n_tiles, float* __restrict__ out, bf16* __restrict__ outb,
-                    int ldo, long slab) {
+                    int ldo, long slab, const GqGlu& glu = GqGlu{}) {
   using WS = GqW<FMT, BN>;
   constexpr int NW = WM * WN;
   constexpr int TM = BM / WM, TN = BN / WN;
@@ -251,6 +299,10 @@ LA_DEV void gq_tile(uint8_t* __restrict__ lds, const QW& w, int tile, const bf16
   const int ks0 = split * per_split;
   const int nk = min(KS, ks0 + per_split) - ks0;
   if (nk <= 0) return;
+  static_assert(!GLU || (WN % 2 == 0 && (BN / 2) % 16 == 0), "GLU tile: gate and up halves of whole waves");
+  GqCols<GLU> cm;
+  if constexpr (GLU) cm = GqCols<true>{w, glu.b, glu.oa, glu.ob, nt_i * (BN / 2), BN / 2, glu.F - 1};
+  else cm = GqCols<false>{w, n0};
 
   // X DMA: piece j of this wave = rows 8(wave*PX + j) .. +8; lane -> (row, physical 16-B chunk)
   uint32_t xoff[PX];
@@ -275,9 +327,9 @@ LA_DEV void gq_tile(uint8_t* __restrict__ lds, const QW& w, int tile, const bf16
     }
     if constexpr (!(ABL & 8)) {
 #pragma unroll
-      for (int j = 0; j < PWA; ++j) WS::issue(w, n0, wave + NW * j, ks, sl + XB, lane);
+      for (int j = 0; j < PWA; ++j) WS::issue(cm, w.K, wave + NW * j, ks, sl + XB, lane);
       if constexpr (PWR > 0) {
-        if (wave < PWR) WS::issue(w, n0, wave + NW * PWA, ks, sl + XB, lane);
+        if (wave < PWR) WS::issue(cm, w.K, wave + NW * PWA, ks, sl + XB, lane);
       }
     }
   };
@@ -447,6 +499,54 @@ LA_DEV void gq_tile(uint8_t* __restrict__ lds, const QW& w, int tile, const bf16
   __builtin_amdgcn_s_barrier();              // every wave has finished reading the ring
   asm volatile("" ::: "memory");
   float* img = (float*)lds + wave * ER * EW;
+  if constexpr (GLU) {
+    // wave (wm, wn < WN/2) holds gate columns j0 + wn*TN .., its partner (wm, wn + WN/2) the same
+    // up columns: both park a pass of rows, the gate wave writes act(g) * u as bf16 [M][F]
+    constexpr int HW = WN / 2;
+    constexpr int CH = TN / 4;
+    const float* pimg = (const float*)lds + (wave + HW) * ER * EW;
+    const int cbase = nt_i * (BN / 2) + wn * TN;
+#pragma unroll
+    for (int pass = 0; pass < EP; ++pass) {
+#pragma unroll
+      for (int mt = pass * (ER / 16); mt < min(MT, (pass + 1) * (ER / 16)); ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) img[((mt % (ER / 16)) * 16 + 4 * g + i) * EW + nt * 16 + r16] = acc[mt][nt][i];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();            // the partner's rows are parked
+      asm volatile("" ::: "memory");
+      if (wn < HW) {
+        const int rows = min(ER, TM - pass * ER);
+        const int rbase = m0 + wm * TM + pass * ER;
+#pragma unroll
+        for (int it = 0; it < (ER * CH + 63) / 64; ++it) {
+          const int idx = it * 64 + lane;
+          const int r = idx / CH, c4 = idx % CH;
+          const int m = rbase + r, j = cbase + 4 * c4;
+          if (r < rows && m < M) {
+            const f32x4 gv = *(const f32x4*)(img + r * EW + 4 * c4);
+            const f32x4 uv = *(const f32x4*)(pimg + r * EW + 4 * c4);
+            bf16x4 hv;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) hv[e] = (bf16)((glu.act == 0 ? silu(gv[e]) : gq_gelu_tanh(gv[e])) * uv[e]);
+            if (j + 3 < glu.F) {
+              *(bf16x4*)(outb + (size_t)m * ldo + j) = hv;
+            } else {
+#pragma unroll
+              for (int e = 0; e < 4; ++e)
+                if (j + e < glu.F) outb[(size_t)m * ldo + j + e] = hv[e];
+            }
+          }
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();            // images read before the next pass overwrites them
+      asm volatile("" ::: "memory");
+    }
+    return;
+  }
   const bool f32out = outb == nullptr;
   float* o = f32out ? out + (size_t)split * slab : nullptr;
 #pragma unroll
@@ -526,6 +626,19 @@ __global__ __launch_bounds__(WM* WN * 64, 1) void qgemm_tile2_kernel(
   }
 }
 
+// gate|up GEMM with the GLU activation in the epilogue: out = act(x Wg^T) * (x Wu^T), bf16 [M][F]
+// (tile n covers gate and up rows j0 .. j0 + BN/2; no split-K, no fp32 intermediate)
+template <int FMT, int BM, int BN, int WM, int WN, int NS>
+__global__ __launch_bounds__(WM* WN * 64, 1) void qgemm_glu_kernel(QW wa, GqGlu glu, const bf16* __restrict__ X,
+                                                                   int ldx, int M, int m_tiles, int n_tiles,
+                                                                   int real_tiles, bf16* __restrict__ outb, int ldo) {
+  __shared__ __attribute__((aligned(1024))) uint8_t lds[NS * (BM * 128 + GqW<FMT, BN>::LDS)];
+  const int tile = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+  if (tile >= real_tiles) return;
+  gq_tile<FMT, BM, BN, WM, WN, NS, 0, 0, true>(lds, wa, tile, X, ldx, M, wa.K / GQ_BK, m_tiles, n_tiles, nullptr,
+                                                 outb, ldo, 0, glu);
+}
+
 // Blocked scale plane for the tile GEMM: [ceil(N/16)][K/64][16 cols][8 B], one record per
 // (column, K-step).  Rows past N repeat row N-1.
 //   Q4_K: f16 d*sc, f16 -dmin*m of sub-block 2(ks%4), then of sub-block 2(ks%4)+1, from the
@@ -602,6 +715,32 @@ static int gq_dispatch2(int tile, const QW& wa, const QW& wb, const bf16* X, int
     case 7: gq_launch2<FA, FB, 128, 256, 1, 8, 3>(wa, wb, X, ldx, M, splits, out, outb, ldo, slab, st); break;
     case 8: gq_launch2<FA, FB, 256, 128, 2, 4, 2>(wa, wb, X, ldx, M, splits, out, outb, ldo, slab, st); break;
     case 12: gq_launch2<FA, FB, 128, 128, 2, 4, 3>(wa, wb, X, ldx, M, splits, out, outb, ldo, slab, st); break;
+    default: return -1;
+  }
+  return 0;
+}
+
+template <int FMT, int BM, int BN, int WM, int WN, int NS>
+static void gq_launch_glu(const QW& wa, const GqGlu& glu, const bf16* X, int ldx, int M, bf16* outb, int ldo,
+                          hipStream_t st) {
+  const int m_tiles = (M + BM - 1) / BM, n_tiles = (glu.F + BN / 2 - 1) / (BN / 2);
+  const int real = m_tiles * n_tiles;
+  const int grid = (real + 7) / 8 * 8;
+  hipLaunchKernelGGL((qgemm_glu_kernel<FMT, BM, BN, WM, WN, NS>), dim3(grid), dim3(WM * WN * 64), 0, st, wa, glu, X,
+                     ldx, M, m_tiles, n_tiles, real, outb, ldo);
+}
+
+template <int FMT>
+static int gq_dispatch_glu(int tile, const QW& wa, const GqGlu& glu, const bf16* X, int ldx, int M, bf16* outb,
+                           int ldo, hipStream_t st) {
+  constexpr int NS0 = ((256 * 128 + GqW<FMT, 256>::LDS) * 3 <= 163840) ? 3 : 2;
+  constexpr int NS2 = ((128 * 128 + GqW<FMT, 256>::LDS) * 3 <= 163840) ? 3 : 2;
+  switch (tile) {
+    case 6: gq_launch_glu<FMT, 256, 256, 1, 8, NS0>(wa, glu, X, ldx, M, outb, ldo, st); break;
+    case 7: gq_launch_glu<FMT, 128, 256, 1, 8, NS2>(wa, glu, X, ldx, M, outb, ldo, st); break;
+    case 8: gq_launch_glu<FMT, 256, 128, 2, 4, 2>(wa, glu, X, ldx, M, outb, ldo, st); break;
+    case 12: gq_launch_glu<FMT, 128, 128, 2, 4, 3>(wa, glu, X, ldx, M, outb, ldo, st); break;
+    case 14: gq_launch_glu<FMT, 64, 256, 1, 8, 3>(wa, glu, X, ldx, M, outb, ldo, st); break;
     default: return -1;
   }
   return 0;
@@ -724,6 +863,35 @@ extern "C" int la_qgemm_tile2(int fa, const void* pa0, const void* pa1, const vo
   if (fa == FMT_Q4_K && fb == FMT_Q6_K) rc = gq_dispatch2<FMT_Q4_K, FMT_Q6_K>(tile, wa, wb, x, ldx, M, splits, o, ob, ldo, slab, st);
   else if (fa == FMT_Q6_K && fb == FMT_Q4_K) rc = gq_dispatch2<FMT_Q6_K, FMT_Q4_K>(tile, wa, wb, x, ldx, M, splits, o, ob, ldo, slab, st);
   else return -2;
+  if (rc) return rc;
+  return (int)hipGetLastError();
+}
+
+// h = act(x Wg^T) * (x Wu^T) -> bf16 [M][ldo], F columns.  Gate rows oa .. oa+F of (pa*, ga), up
+// rows ob .. ob+F of (pb*, gb): two weights (oa = ob = 0) or the halves of one [2F, K] weight
+// (same planes, ob = F).  act: 0 SwiGLU, 3 GeGLU (ops.ACT_*).  Tiles 6, 7, 8, 12, 14.
+extern "C" int la_qgemm_glu(int fmt, const void* pa0, const void* pa1, const void* ga, int oa, const void* pb0,
+                            const void* pb1, const void* gb, int ob, int F, int K, const void* X, int ldx, int M,
+                            void* out, int ldo, int act, int tile, void* stream) {
+  using namespace la;
+  if (M < 1 || F < 1 || (K & 255) || ldo < F || ldx < K || (ldx & 7) || (oa & 15) || (ob & 15)) return -1;
+  if (act != 0 && act != 3) return -1;
+  if ((long)M * ldx >= (1L << 31)) return -1;
+  if (fmt != FMT_BF16 && (!ga || !gb)) return -1;
+  // the column maps clamp rows to oa/ob + F - 1, so each weight must hold rows up to that
+  QW wa{(const uint8_t*)pa0, (const uint8_t*)pa1, (const uint8_t*)ga, nullptr, oa + F, K};
+  GqGlu glu{QW{(const uint8_t*)pb0, (const uint8_t*)pb1, (const uint8_t*)gb, nullptr, ob + F, K}, oa, ob, F, act};
+  hipStream_t st = (hipStream_t)stream;
+  const bf16* x = (const bf16*)X;
+  bf16* o = (bf16*)out;
+  int rc;
+  switch (fmt) {
+    case FMT_Q4_K: rc = gq_dispatch_glu<FMT_Q4_K>(tile, wa, glu, x, ldx, M, o, ldo, st); break;
+    case FMT_Q6_K: rc = gq_dispatch_glu<FMT_Q6_K>(tile, wa, glu, x, ldx, M, o, ldo, st); break;
+    case FMT_Q8_0: rc = gq_dispatch_glu<FMT_Q8_0>(tile, wa, glu, x, ldx, M, o, ldo, st); break;
+    case FMT_BF16: rc = gq_dispatch_glu<FMT_BF16>(tile, wa, glu, x, ldx, M, o, ldo, st); break;
+    default: return -2;
+  }
   if (rc) return rc;
   return (int)hipGetLastError();
 }

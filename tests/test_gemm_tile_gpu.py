@@ -135,3 +135,44 @@ def test_tile_gemm_two_segments_one_launch(tile, S):
         y = out.float().cpu() if S == 1 else out.sum(0).cpu()
         ref = torch.cat([x.float().cpu() @ w.ref.t() for w in ws], -1)
         _check(y, ref)
+
+
+@pytest.mark.parametrize("t", FMTS)
+@pytest.mark.parametrize("tile", [6, 7, 8, 12, 14])
+def test_glu_fused_gate_up(t, tile):
+    """gate|up with SwiGLU / GeGLU in the tile epilogue (la_qgemm_glu) vs fp32: two weights, and
+    the halves of one fused [2F, K] weight; F off every half-tile width, ragged M."""
+    F, K, M = 200, 768, 150
+    g, u = _qw(F, K, t, seed=40 + tile), _qw(F, K, t, seed=41 + tile)
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    xc = x.float().cpu()
+    for mode in (ops.ACT_SWIGLU, ops.ACT_GEGLU):
+        gr, ur = xc @ g.ref.t(), xc @ u.ref.t()
+        act = (torch.nn.functional.silu(gr) if mode == ops.ACT_SWIGLU
+               else torch.nn.functional.gelu(gr, approximate="tanh"))
+        ref = act * ur
+        out = torch.full((M, F), float("nan"), dtype=torch.bfloat16, device=DEV)
+        ops._run_glu(x, (g, 0, u, 0), F, mode, tile, out)
+        torch.cuda.synchronize()
+        _check(out.float().cpu(), ref, 3e-2)
+    # one [2F, K] weight (Phi-3 style fused gate_up): up rows start at F (F % 16 == 0)
+    F2 = 208
+    w = _qw(2 * F2, K, t, seed=50 + tile)
+    out = torch.full((M, F2), float("nan"), dtype=torch.bfloat16, device=DEV)
+    ops._run_glu(x, (w, 0, w, F2), F2, ops.ACT_SWIGLU, tile, out)
+    torch.cuda.synchronize()
+    full = xc @ w.ref.t()
+    _check(out.float().cpu(), torch.nn.functional.silu(full[:, :F2]) * full[:, F2:], 3e-2)
+
+
+def test_glu_linear_dispatch():
+    """ops.glu_linear (autotuned fused vs unfused) returns act(gate) * up at a decode batch."""
+    F, K, M = 1024, 1024, 200
+    ws = [_qw(F, K, GGMLType.Q4_K, seed=61), _qw(F, K, GGMLType.Q4_K, seed=62)]
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    h = ops.glu_linear(x, ws, F, ops.ACT_SWIGLU)
+    if h is None:  # unfused won the autotune: the decoder then runs GEMM + act
+        h = ops.act(ops.linear_multi(x, ws), F, ops.ACT_SWIGLU)
+    xc = x.float().cpu()
+    ref = torch.nn.functional.silu(xc @ ws[0].ref.t()) * (xc @ ws[1].ref.t())
+    _check(h.float().cpu(), ref, 3e-2)
