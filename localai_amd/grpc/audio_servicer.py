@@ -93,3 +93,61 @@ class VitsServicer(_AudioBase):
 
     async def TTS(self, request, context=None):
         return await self._run(self._tts, request)
+
+
+class MusicgenServicer(_AudioBase):
+    """transformers-musicgen: SoundGeneration (and the older TTS entry point)."""
+    kind = "transformers-musicgen"
+
+    def _load(self, path):
+        from ..models.musicgen import MusicGen, is_musicgen_dir
+        if not is_musicgen_dir(path):
+            raise ValueError("not a MusicGen checkpoint directory (config.json model_type 'musicgen')")
+        return MusicGen(path, self._dev())
+
+    def _sound(self, request, tts: bool):
+        from ..models.tts import write_wav
+        m = self.model
+        if m is None:
+            raise RuntimeError("no model loaded")
+        if tts:
+            tokens, guidance, sample = 512, 3.0, True     # backend.py TTS: 10 s, generation defaults
+        else:
+            tokens = int(request.duration * 51.2) if request.HasField("duration") else 256
+            guidance = request.temperature if request.HasField("temperature") else 3.0
+            sample = request.sample if request.HasField("sample") else True
+        with self._lock:
+            audio = m.generate(request.text, max_new_tokens=max(tokens, m.dec["num_codebooks"]),
+                               guidance_scale=guidance, do_sample=sample)
+        write_wav(request.dst, audio, m.sampling_rate)
+
+    async def SoundGeneration(self, request, context=None):
+        if request.HasField("src"):
+            return pb.Result(success=False, message="audio-prompted generation (src) is not supported")
+        return await self._run(self._sound, request, False)
+
+    async def TTS(self, request, context=None):
+        return await self._run(self._sound, request, True)
+
+
+class BarkServicer(_AudioBase):
+    """bark: TTS with an optional speaker preset (`voice`)."""
+    kind = "bark"
+
+    def _load(self, path):
+        from ..models.bark import Bark, is_bark_dir
+        if not is_bark_dir(path):
+            raise ValueError("not a Bark checkpoint directory (config.json model_type 'bark')")
+        return Bark(path, self._dev())
+
+    def _tts(self, request):
+        from ..models.tts import write_wav
+        m = self.model
+        if m is None:
+            raise RuntimeError("no model loaded")
+        with self._lock:
+            audio = m.generate(request.text, voice=request.voice)
+        write_wav(request.dst, audio, m.sampling_rate)
+
+    async def TTS(self, request, context=None):
+        return await self._run(self._tts, request)

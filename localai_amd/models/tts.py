@@ -363,11 +363,12 @@ class VitsVoice:
 
 
 def write_wav(path: str, audio: np.ndarray, sampling_rate: int) -> None:
-    """16-bit PCM mono."""
-    pcm = (np.clip(audio, -1.0, 1.0) * 32767.0).astype("<i2")
+    """16-bit PCM; audio [samples] (mono) or [channels, samples] (interleaved on write)."""
+    ch = 1 if audio.ndim == 1 else audio.shape[0]
+    pcm = (np.clip(audio if audio.ndim == 1 else audio.T, -1.0, 1.0) * 32767.0).astype("<i2")
     os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
     with wave.open(path, "wb") as w:
-        w.setnchannels(1)
+        w.setnchannels(ch)
         w.setsampwidth(2)
         w.setframerate(int(sampling_rate))
         w.writeframes(pcm.tobytes())
