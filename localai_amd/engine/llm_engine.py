@@ -70,6 +70,7 @@ class EngineConfig:
     bias_capacity: int = 16           # logit-bias / EOS-ban entries per sequence inside the graph
     blas_tune: bool = True            # tune the hipBLASLt/rocBLAS solution per decode GEMM shape at warm-up
     lora_adapters: tuple = ()         # ((adapter GGUF path, scale), ...) merged into the weights at load
+    record_tokens: bool = False       # final Event carries the generated token ids (numerics tests)
 
 
 @dataclass
@@ -81,6 +82,7 @@ class Event:
     prompt_tokens: int = 0
     completion_tokens: int = 0
     error: str = ""
+    token_ids: Optional[List[int]] = None   # final event, with EngineConfig.record_tokens
 
 
 @dataclass
@@ -104,6 +106,7 @@ class Request:
     spec_drafted: int = 0        # n-gram speculation bookkeeping (adaptive back-off)
     spec_accepted: int = 0
     spec_off: bool = False
+    out_ids: Optional[List[int]] = None  # generated ids (EngineConfig.record_tokens)
 
 
 def _noop_callback(ev):  # follower ranks: the leader talks to the client
@@ -245,6 +248,8 @@ class LLMEngine:
         params.resolved_seed()
         stops = list(params.stop)
         r = Request(rid, toks, params, callback, n_prompt=len(toks), mu=2.0 * params.mirostat_tau)
+        if self.cfg.record_tokens:
+            r.out_ids = []
         r.stream = core.TextStream(self.vocab, stops)
         if params.grammar:
             r.grammar = core.GrammarState(self._grammar(params.grammar), self.gvocab)
@@ -579,6 +584,8 @@ class LLMEngine:
         if len(toks) >= self.ctx:
             raise ValueError(f"prompt with images is {len(toks)} tokens, context is {self.ctx}")
         r = Request(rid, toks, params, callback, n_prompt=len(toks), mu=2.0 * params.mirostat_tau)
+        if self.cfg.record_tokens:
+            r.out_ids = []
         r.stream = core.TextStream(self.vocab, list(params.stop))
         if params.grammar:
             r.grammar = core.GrammarState(self._grammar(params.grammar), self.gvocab)
@@ -810,6 +817,8 @@ class LLMEngine:
                                         correlation_id=r.params.correlation_id)
             r.n_gen += n
             self.metrics["gen_tokens"] += n
+            if r.out_ids is not None:
+                r.out_ids.extend(int(t) for t in hist[:n, j])
             if texts[j]:
                 r.callback(Event(text=texts[j], token=-1))
             rs = int(reason[j])
@@ -1114,6 +1123,8 @@ class LLMEngine:
                 return
         if append:
             self.sched.append(r.id, tok)
+        if r.out_ids is not None:
+            r.out_ids.append(tok)
         r.n_gen += 1
         self.metrics["gen_tokens"] += 1
         if r.first_token_t == 0.0:
@@ -1183,7 +1194,7 @@ class LLMEngine:
                       self.last_request_stats["tokens_per_second"])
         try:
             r.callback(Event(text=tail, finished=True, finish_reason=reason, prompt_tokens=r.n_prompt,
-                             completion_tokens=r.n_gen, error=error))
+                             completion_tokens=r.n_gen, error=error, token_ids=r.out_ids))
         except Exception:
             log.exception("callback failed")
 

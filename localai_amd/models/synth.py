@@ -74,6 +74,9 @@ class Preset:
 PRESETS: Dict[str, Preset] = {
     "llama3-8b": Preset(name="Meta-Llama-3-8B-Instruct (random-init)"),
     "llama3-8b-q8_0": Preset(qtype="Q8_0", name="Meta-Llama-3-8B-Instruct Q8_0 (random-init)"),
+    # the Llama-3-8B layer shapes (4096 wide, GQA 32/8, 14336 FFN, Q4_K_M mixed Q4_K/Q6_K, 128256 vocab)
+    # on 2 layers: the headline decode path at a size the fp32 oracle can check (tests/test_engine_gpu.py)
+    "llama3-8b-2l": Preset(n_layer=2, ctx=1024, name="Llama-3-8B shapes, 2 layers (random-init)"),
     "llama3-70b": Preset(n_layer=80, n_embd=8192, n_head=64, n_head_kv=8, n_ff=28672,
                          name="Meta-Llama-3-70B-Instruct (random-init)"),
     "mixtral-8x7b": Preset(n_layer=32, n_embd=4096, n_head=32, n_head_kv=8, n_ff=14336, n_vocab=32000,

@@ -84,6 +84,46 @@ def test_mixtral_moe_graph_decode(tmp_path):
     assert first == int(top.indices[0]) or float(top.values[0] - ref[first]) < 0.05
 
 
+def test_headline_path_against_fp32_oracle(tmp_path):
+    """The C=256 headline decode path -- Llama-3-8B layer shapes with Q4_K_M mixed formats,
+    decode batches up to 200 through the autotuned tile GEMMs, wide-batch 16-step graphs, paged
+    attention -- against the fp32 PyTorch oracle, teacher-forced on the engine's own tokens:
+    every greedy token is the oracle's argmax or within bf16 noise of it."""
+    from localai_amd.models import synth
+    p = str(tmp_path / "l3-2l.gguf")
+    synth.write_model(p, "llama3-8b-2l")
+    eng = LLMEngine(EngineConfig(model_path=p, device="cuda:0", context_size=256, max_num_seqs=256,
+                                 max_batched_tokens=4096, decode_steps=8, decode_steps_wide=16, wide_batch=128,
+                                 record_tokens=True))
+    prompts = [f"numerics check {i} " + "word " * (i % 13) for i in range(200)]
+    got = {}
+
+    def mk(i):
+        def cb(ev):
+            if ev.finished:
+                got[i] = ev.token_ids
+        return cb
+    for i, pr in enumerate(prompts):
+        eng.add_request(pr, SamplingParams(max_tokens=6, temperature=0.0, ignore_eos=True), mk(i))
+    while len(got) < len(prompts):
+        eng.step()
+    assert all(len(got[i]) == 6 for i in got)
+    exact, worst = 0, 0.0
+    n = 0
+    for i in (0, 57, 123, 199):
+        ids = eng.tokenize(prompts[i])
+        gen = got[i]
+        ref = eng.model.reference_logits(ids + gen[:-1])
+        for j, t in enumerate(gen):
+            row = ref[len(ids) - 1 + j].float()
+            gap = float(row.max() - row[t]) / float(row.std())
+            exact += int(t == int(row.argmax()))
+            worst = max(worst, gap)
+            n += 1
+    print(f"headline numerics: {exact}/{n} exact argmax, worst gap {worst:.4f} logit-std")
+    assert exact >= 0.75 * n and worst < 0.05, (exact, n, worst)
+
+
 def test_mixtral_moe_wide_batch_graph_decode(tmp_path):
     """Decode batches past 64 tokens run the row-chunked grouped expert GEMM inside the captured
     graph (no per-expert host loop): 100 concurrent requests, multi-step == single-step, and a

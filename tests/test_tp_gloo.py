@@ -39,7 +39,7 @@ def _worker(rank, world, port, path, q, ep=False):
             emb = eng.embed(["embed me"])[0]
             n_exp = len(eng.model.layers[0].experts or [])
             eng.shutdown()
-            q.put((rank, outs, len(emb), n_exp))
+            q.put((rank, outs, [float(v) for v in emb], n_exp))
         else:
             eng.run_follower()
             q.put((rank, eng.metrics["requests"], eng.metrics["gen_tokens"]))
@@ -105,12 +105,19 @@ def _run_tp2(tp_model_path, ep=False, world=2):
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
-    _, outs, emb_len, n_exp = out[0]
+    _, outs, emb, n_exp = out[0]
     assert [n for _, n in outs] == [5, 5]
     for r in range(1, world):
         _, f_requests, f_tokens = out[r]
         assert f_requests == 2 and f_tokens == 10  # every follower ran the same two requests
-    assert emb_len == single.model.hp.n_embd
+    assert len(emb) == single.model.hp.n_embd
+    # hidden states through every sharded layer (column/row-parallel GEMMs, the all-reduces, the
+    # sharded attention / experts) against the unsharded model: numerically, not just the argmax
+    import torch
+    a, b = torch.tensor(emb), torch.tensor(single.embed(["embed me"])[0], dtype=torch.float32)
+    rel = float((a - b).norm() / b.norm())
+    cos = float(torch.nn.functional.cosine_similarity(a, b, dim=0))
+    assert rel < 2e-2 and cos > 0.9998, (rel, cos)
     # sharded reductions change bf16 summation order; the first token must agree
     assert outs[0][0][:1] == ref["text"][:1]
     return n_exp
