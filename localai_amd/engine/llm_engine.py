@@ -657,11 +657,17 @@ class LLMEngine:
         self._sample_and_emit(seqs, logits)
 
     # ------------------------------------------------------------------ decode
+    PEN_CAP = 256  # longest penalty window (repeat_last_n) the captured decode graphs keep on the device
+
     def _needs_host_sampling(self, r: Request) -> bool:
+        """Sampler features the captured decode graph cannot run: mirostat v1, grammars, more logit
+        biases than its table holds, or a penalty window longer than PEN_CAP tokens.  Penalties
+        over shorter windows run in the graph (penalty ring), so they keep multi-step decode."""
         p = r.params
-        return (p.repeat_penalty != 1.0 or p.frequency_penalty != 0.0 or p.presence_penalty != 0.0
-                or p.mirostat == 1 or bool(p.grammar) or len(p.logit_bias) + len(self.tokenizer.eog) >
-                self.cfg.bias_capacity)
+        pen = p.repeat_penalty != 1.0 or p.frequency_penalty != 0.0 or p.presence_penalty != 0.0
+        window = p.repeat_last_n if p.repeat_last_n >= 0 else self.ctx
+        return ((pen and window > self.PEN_CAP) or p.mirostat == 1 or bool(p.grammar)
+                or len(p.logit_bias) + len(self.tokenizer.eog) > self.cfg.bias_capacity)
 
     def _lookahead(self) -> int:
         """Decode steps to run on the device before coming back to the host."""
@@ -864,6 +870,32 @@ class LLMEngine:
             for j, r in enumerate(reqs):
                 mu[j] = r.mu
             h["mu"][:] = torch.from_numpy(mu)
+        # penalty windows: neutral unless a device-sampled row asks for penalties
+        pen = np.zeros((Bp, 3), dtype=np.float32)
+        pen[:, 0] = 1.0
+        pcap = np.zeros(Bp, dtype=np.int32)
+        pcnt = np.zeros(Bp, dtype=np.int32)
+        pnl = np.ones(Bp, dtype=np.int32)
+        if device_sampling:
+            for j, r in enumerate(reqs):
+                p = r.params
+                if p.repeat_penalty == 1.0 and p.frequency_penalty == 0.0 and p.presence_penalty == 0.0:
+                    continue
+                ln = p.repeat_last_n if p.repeat_last_n >= 0 else self.ctx
+                if ln <= 0:
+                    continue
+                toks = self.sched.tokens(r.id)[-ln:]
+                pen[j] = (p.repeat_penalty, p.frequency_penalty, p.presence_penalty)
+                pcap[j] = ln
+                pcnt[j] = len(toks)
+                pnl[j] = 1 if p.penalize_nl else 0
+                if toks:
+                    h["phist"][j, :len(toks)] = torch.tensor(toks, dtype=torch.int32)
+        h["pen"][:] = torch.from_numpy(pen)
+        h["pcap"][:] = torch.from_numpy(pcap)
+        h["pcnt"][:] = torch.from_numpy(pcnt)
+        h["phl"][:] = torch.from_numpy(np.minimum(pcnt, pcap))
+        h["pnl"][:] = torch.from_numpy(pnl)
         h["bias_n"][0] = n_bias
         st["dev_block"].copy_(st["host_block"], non_blocking=True)
 
@@ -875,9 +907,11 @@ class LLMEngine:
         K = max(1, self.cfg.decode_steps, self.cfg.decode_steps_wide)
         # all per-run inputs live in one int32 block (uploaded with a single copy)
         prm_words = Bp * ops.SAMPLE_ROW_DTYPE.itemsize // 4
+        PL = self.PEN_CAP
         layout = [("tokens", Bp), ("pos", Bp), ("slots", Bp), ("lens", Bp), ("bt", Bp * MB), ("step", 1),
                   ("prm", prm_words), ("bias_rows", cap), ("bias_cols", cap), ("bias_vals", cap), ("bias_n", 1),
-                  ("mu", Bp)]
+                  ("mu", Bp), ("phist", Bp * PL), ("pcnt", Bp), ("phl", Bp), ("pcap", Bp), ("pen", Bp * 3),
+                  ("pnl", Bp)]
         total = sum(n for _, n in layout)
         host_block = torch.zeros(total, dtype=torch.int32).pin_memory()
         dev_block = torch.zeros(total, dtype=torch.int32, device=dev)
@@ -886,6 +920,10 @@ class LLMEngine:
             hv, dv = host_block[o:o + n], dev_block[o:o + n]
             if name == "bt":
                 hv, dv = hv.view(Bp, MB), dv.view(Bp, MB)
+            elif name == "phist":
+                hv, dv = hv.view(Bp, PL), dv.view(Bp, PL)
+            elif name == "pen":
+                hv, dv = hv.view(torch.float32).view(Bp, 3), dv.view(torch.float32).view(Bp, 3)
             elif name in ("bias_vals", "mu"):
                 hv, dv = hv.view(torch.float32), dv.view(torch.float32)
             elif name == "prm":
@@ -908,7 +946,11 @@ class LLMEngine:
         def body():
             lg = self.model.forward(fb, self.kv, attn_workspace=ws)
             ops.logit_bias(lg, st["bias_rows"], st["bias_cols"], st["bias_vals"], st["bias_n"])
+            # repeat / frequency / presence penalties over each row's last-n window, kept on the
+            # device across the run's steps (rows without penalties return at once)
+            ops.penalties(lg, st["phist"], st["phl"], st["pen"], self.tokenizer.nl_id, st["pnl"])
             ops.sample(lg, st["prm_np"], mu=st["mu"], params_dev=st["prm"], out=st["next"])
+            ops.penalty_push(st["next"], st["phist"], st["pcnt"], st["phl"], st["pcap"])
             ops.decode_advance(st["next"], st["tokens"], st["pos"], st["lens"], st["slots"], st["bt"], bs,
                                st["hist"], st["step"], st["prm"])
             return lg

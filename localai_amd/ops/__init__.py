@@ -74,6 +74,7 @@ def lib():
             "la_qgemm_tile": [I, P, P, P, I, I, P, I, I, I, P, I, LNG, I, I, I, P],
             "la_qgemm_tile_probe": [P, P, I, I, P, I, I, P, I, I, P],
             "la_qgemm_tile2": [I, P, P, P, I, I, P, P, P, I, I, P, I, I, I, P, I, LNG, I, I, P],
+            "la_pen_push": [P, I, P, I, P, P, P, P],
             "la_qgemm_glu": [I, P, P, P, I, P, P, P, I, I, I, P, I, I, P, I, I, I, P],
             "la_decode_advance": [P, P, P, P, P, P, I, I, I, P, I, P, P, P],
         }
@@ -1628,6 +1629,25 @@ def penalties(logits: torch.Tensor, hist: torch.Tensor, hist_len: torch.Tensor, 
                               hist_len.data_ptr(), pen.data_ptr(), nl_token, _ptr(penalize_nl), _stream()),
            "la_penalties")
     return logits
+
+
+def penalty_push(nxt: torch.Tensor, hist: torch.Tensor, cnt: torch.Tensor, hl: torch.Tensor,
+                 cap: torch.Tensor) -> None:
+    """Append the sampled tokens to each row's penalty ring (hist [B, L] i32, ring size cap[b])
+    and refresh hist_len = min(count, cap) -- the in-graph history the penalties kernel reads."""
+    B = nxt.shape[0]
+    if not nxt.is_cuda:
+        for b in range(B):
+            k = int(cap[b])
+            if k <= 0:
+                continue
+            c = int(cnt[b])
+            hist[b, c % k] = nxt[b]
+            cnt[b] = c + 1
+            hl[b] = min(c + 1, k)
+        return
+    _check(lib().la_pen_push(nxt.data_ptr(), B, hist.data_ptr(), hist.stride(0), cnt.data_ptr(), hl.data_ptr(),
+                             cap.data_ptr(), _stream()), "la_pen_push")
 
 
 # ---------------------------------------------------------------------------------------

@@ -479,7 +479,28 @@ __global__ __launch_bounds__(256) void penalties_kernel(float* __restrict__ logi
   }
 }
 
+// In-graph penalty window: append each row's sampled token to its ring of the last pcap[b]
+// tokens (order is irrelevant to the penalties, which count occurrences) and refresh the
+// window length the penalties kernel reads.
+__global__ void pen_push_kernel(const int* __restrict__ next, int B, int* __restrict__ hist, int hist_ld,
+                                int* __restrict__ cnt, int* __restrict__ len, const int* __restrict__ cap) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const int c = cnt[b], k = cap[b];
+  if (k <= 0) return;
+  hist[(long)b * hist_ld + c % k] = next[b];
+  cnt[b] = c + 1;
+  len[b] = min(c + 1, k);
+}
+
 }  // namespace la
+
+extern "C" int la_pen_push(const int* next, int B, int* hist, int hist_ld, int* cnt, int* len, const int* cap,
+                           void* stream) {
+  hipLaunchKernelGGL(la::pen_push_kernel, dim3((B + 255) / 256), dim3(256), 0, (hipStream_t)stream, next, B, hist,
+                     hist_ld, cnt, len, cap);
+  return (int)hipGetLastError();
+}
 
 extern "C" int la_sample(const float* logits, long ld, int B, int V, const void* params, float* mu, int* out_tok,
                          float* out_p, void* stream) {

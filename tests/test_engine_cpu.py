@@ -395,3 +395,36 @@ def test_get_metrics_reports_the_active_slot(eng):
     while eng.has_work():
         eng.step()
     assert asyncio.run(sv.GetMetrics(pb.MetricsRequest())).slot_id == 0
+
+
+def test_penalties_keep_device_sampling_within_the_ring(tiny_model_path):
+    """Penalty windows up to PEN_CAP stay on the device (multi-step graphs); longer ones, mirostat
+    v1 and grammars fall back to host-driven sampling."""
+    from localai_amd.engine.llm_engine import EngineConfig, LLMEngine, Request
+    from localai_amd.engine.sampling_params import SamplingParams
+    eng = LLMEngine(EngineConfig(model_path=tiny_model_path, device="cpu", context_size=512, max_num_seqs=2,
+                                 use_graphs=False))
+
+    def need(**kw):
+        return eng._needs_host_sampling(Request(0, [1], SamplingParams(**kw), lambda e: None))
+    assert not need(repeat_penalty=1.3, repeat_last_n=64)
+    assert not need(frequency_penalty=0.5, presence_penalty=0.5, repeat_last_n=256)
+    assert need(repeat_penalty=1.3, repeat_last_n=257)
+    assert need(repeat_penalty=1.3, repeat_last_n=-1)  # whole context (512 > 256)
+    assert not need(repeat_last_n=-1)                   # no penalty asked
+    assert need(mirostat=1)
+
+
+def test_penalty_ring_push_cpu():
+    import torch
+
+    from localai_amd import ops
+    hist = torch.full((2, 4), -1, dtype=torch.int32)
+    cnt = torch.tensor([0, 3], dtype=torch.int32)
+    hl = torch.zeros(2, dtype=torch.int32)
+    cap = torch.tensor([4, 3], dtype=torch.int32)
+    hist[1, :3] = torch.tensor([7, 8, 9])
+    for t in (5, 6):
+        ops.penalty_push(torch.tensor([t, t], dtype=torch.int32), hist, cnt, hl, cap)
+    assert hist[0].tolist() == [5, 6, -1, -1] and hl.tolist() == [2, 3]
+    assert sorted(hist[1, :3].tolist()) == [5, 6, 9]   # the two oldest (7, 8) dropped out of the window

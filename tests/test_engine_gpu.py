@@ -215,3 +215,21 @@ def test_llava_on_gpu(tiny_model_path, tmp_path):
         eng.step()
     assert got["err"] == "" and got["n"] == 6
     assert got["n_prompt"] == len(eng.tokenize(" describe")) + 16
+
+
+def test_penalties_in_graph_match_host_sampling(tiny_model_path):
+    """repeat / frequency / presence penalties run inside the captured multi-step decode graph
+    (device penalty ring) and give the token stream of the host-driven eager path."""
+    # negative frequency / presence penalties pull the window's tokens up, so the stream visibly
+    # depends on the window (a random model's greedy stream rarely repeats on its own)
+    sp = dict(max_tokens=24, temperature=0.0, repeat_penalty=1.6, repeat_last_n=16, frequency_penalty=-1.5,
+              presence_penalty=-2.0, ignore_eos=True)
+    prompts = ["one", "two three", "four five six", "seven"]
+    eager = LLMEngine(EngineConfig(model_path=tiny_model_path, device="cuda:0", context_size=256, max_num_seqs=8,
+                                   max_batched_tokens=512, use_graphs=False))
+    a = _run(eager, prompts, **sp)
+    g = _eng(tiny_model_path, 8)
+    b = _run(g, prompts, **sp)
+    assert a == b and all(x[1] == 24 for x in b)
+    plain = _run(_eng(tiny_model_path, 8), prompts, max_tokens=24, temperature=0.0, ignore_eos=True)
+    assert plain != b  # the penalties changed the greedy stream
