@@ -13,9 +13,12 @@ are dequantised at load.
 
 Compute: the log-mel front end (STFT n_fft 400 / hop 160, Hann, log10, 8-decade floor,
 (x + 4) / 4), the conv stem + pre-LN transformer encoder over 30-s windows, and the decoder with
-self-attention KV caches and per-window cross-attention K/V, greedily decoded without
-timestamps (one segment per 30-s window; whisper.cpp's timestamp-token segmentation is not
-reproduced).  The GEMMs run through torch.matmul (hipBLASLt on the GPU, bf16 weights); whisper
+self-attention KV caches and per-window cross-attention K/V, greedily decoded with timestamp
+tokens (whisper.cpp / OpenAI rules: a window opens with a timestamp <= 1 s, timestamps come in
+pairs and never decrease, a timestamp wins when the timestamps' total probability beats the best
+text token, no <|notimestamps|>); text between a timestamp pair is one segment with its start /
+end, and a window that ends on a lone timestamp seeks the next window to it.  `timestamps=False`
+keeps the single-segment-per-window mode.  The GEMMs run through torch.matmul (hipBLASLt on the GPU, bf16 weights); whisper
 is a side workload next to the LLM path, whose hot ops are the hand-written kernels.
 """
 from __future__ import annotations
@@ -262,6 +265,80 @@ class WhisperModel:
             logits = step([t])
         return out
 
+    TS_STEP = 0.02          # seconds per timestamp token
+    MAX_INITIAL_TS = 1.0    # the first timestamp of a window is at most this (seconds)
+
+    def _timestamp_rules(self, logits: torch.Tensor, out: List[int]) -> None:
+        """In-place logit masks of timestamp decoding (OpenAI ApplyTimestampRules / whisper.cpp
+        whisper_process_logits)."""
+        tb, eot = self.timestamp_begin, self.eot
+        logits[self.no_timestamps] = float("-inf")
+        logits[eot + 1:tb] = float("-inf")                       # other specials
+        if not out:
+            logits[:tb] = float("-inf")                           # a window opens with a timestamp ...
+            logits[tb + int(round(self.MAX_INITIAL_TS / self.TS_STEP)) + 1:] = float("-inf")  # ... <= 1 s
+            return
+        last_ts = out[-1] >= tb
+        prev_ts = len(out) < 2 or out[-2] >= tb
+        if last_ts:
+            if prev_ts:
+                logits[tb:] = float("-inf")                       # a pair is complete: text next
+            else:
+                logits[:eot] = float("-inf")                      # close the pair (or end)
+        ts = [t for t in out if t >= tb]
+        if ts:
+            # never decrease; a segment has nonzero length; after a closing timestamp the next one
+            # may repeat it (the next segment's start)
+            floor = ts[-1] if (last_ts and not prev_ts) else ts[-1] + 1
+            logits[tb:floor] = float("-inf")
+        lp = torch.log_softmax(logits.float(), -1)
+        if torch.logsumexp(lp[tb:], 0) > lp[:tb].max():
+            logits[:tb] = float("-inf")                           # timestamps together beat any text token
+
+    def decode_window_ts(self, enc: torch.Tensor, lang_id: Optional[int], translate: bool,
+                         max_tokens: int) -> List[int]:
+        prompt = [self.sot]
+        if self.multilingual:
+            prompt += [self.sot + 1 + (lang_id or 0), self.tok_translate if translate else self.tok_transcribe]
+        step = self._decoder(enc)
+        logits = step(prompt)
+        out: List[int] = []
+        for _ in range(min(max_tokens, self.hp.n_text_ctx // 2)):
+            self._timestamp_rules(logits, out)
+            t = int(torch.argmax(logits))
+            if t == self.eot:
+                break
+            out.append(t)
+            logits = step([t])
+        return out
+
+    def split_segments(self, toks: List[int], t0: float, dur: float):
+        """Window tokens -> ([(start_s, end_s, text tokens)], seek_s): text between timestamps is a
+        segment (absolute times from the window start t0); a trailing lone timestamp closing a
+        segment moves the next window to it, otherwise the whole window was consumed."""
+        tb = self.timestamp_begin
+        segs, start, text = [], None, []
+        for t in toks:
+            if t >= tb:
+                ts = (t - tb) * self.TS_STEP
+                if start is not None and text:
+                    segs.append((t0 + start, t0 + min(ts, dur), text))
+                    text, start = [], None
+                else:
+                    start = ts
+            else:
+                if start is None:
+                    start = 0.0
+                text.append(t)
+        if text:
+            segs.append((t0 + start, t0 + dur, text))
+        seek = dur
+        if len(toks) >= 2 and toks[-1] >= tb and toks[-2] < tb:
+            last = (toks[-1] - tb) * self.TS_STEP
+            if 0 < last < dur:
+                seek = last
+        return segs, seek
+
     def shutdown(self):
         self.w.clear()
 
@@ -270,7 +347,7 @@ class WhisperModel:
 
     @torch.no_grad()
     def transcribe(self, audio: np.ndarray, language: str = "", translate: bool = False,
-                   max_tokens_per_window: int = 224) -> Tuple[List[Segment], str]:
+                   max_tokens_per_window: int = 224, timestamps: bool = True) -> Tuple[List[Segment], str]:
         x = torch.from_numpy(np.asarray(audio, dtype=np.float32))
         segs: List[Segment] = []
         lang_id = None
@@ -278,18 +355,35 @@ class WhisperModel:
             if language not in LANGUAGES[:self.n_lang]:
                 raise ValueError(f"unsupported language {language!r}")
             lang_id = LANGUAGES.index(language)
-        n = max(1, math.ceil(x.shape[0] / N_SAMPLES))
-        for wi in range(n):
-            chunk = x[wi * N_SAMPLES:(wi + 1) * N_SAMPLES]
-            if chunk.numel() == 0:
+        if not timestamps:
+            n = max(1, math.ceil(x.shape[0] / N_SAMPLES))
+            for wi in range(n):
+                chunk = x[wi * N_SAMPLES:(wi + 1) * N_SAMPLES]
+                if chunk.numel() == 0:
+                    break
+                enc = self.encode(self.log_mel(chunk))
+                if self.multilingual and lang_id is None:
+                    lang_id = self.detect_language(enc)
+                toks = self.decode_window(enc, lang_id, translate, max_tokens_per_window)
+                start = wi * CHUNK_S * 10 ** 9
+                end = start + int(chunk.numel() / SAMPLE_RATE * 1e9)
+                segs.append(Segment(wi, start, end, self.text(toks), toks))
+            return segs, "".join(s.text for s in segs)
+        seek = 0                                                   # samples
+        total = max(1, x.shape[0])
+        while seek < total:
+            chunk = x[seek:seek + N_SAMPLES]
+            if chunk.numel() < HOP:                                # less than one frame left
                 break
             enc = self.encode(self.log_mel(chunk))
             if self.multilingual and lang_id is None:
                 lang_id = self.detect_language(enc)
-            toks = self.decode_window(enc, lang_id, translate, max_tokens_per_window)
-            start = wi * CHUNK_S * 10 ** 9
-            end = start + int(chunk.numel() / SAMPLE_RATE * 1e9)
-            segs.append(Segment(wi, start, end, self.text(toks), toks))
+            toks = self.decode_window_ts(enc, lang_id, translate, max_tokens_per_window)
+            dur = chunk.numel() / SAMPLE_RATE
+            parts, adv = self.split_segments(toks, seek / SAMPLE_RATE, dur)
+            for s0, s1, tt in parts:
+                segs.append(Segment(len(segs), int(round(s0 * 1e9)), int(round(max(s1, s0) * 1e9)), self.text(tt), tt))
+            seek += max(HOP, int(round(adv * SAMPLE_RATE)))
         return segs, "".join(s.text for s in segs)
 
 

@@ -48,20 +48,61 @@ def test_log_mel_and_transcribe_deterministic(wpath, tmp_path):
     audio = load_audio(_wav(str(tmp_path / "b.wav")))
     mel = m.log_mel(torch.from_numpy(audio))
     assert mel.shape == (80, N_FRAMES) and float(mel.max()) <= 2.0 and float(mel.max() - mel.min()) <= 2.0 + 1e-5
-    s1, text1 = m.transcribe(audio, max_tokens_per_window=12)
-    s2, text2 = m.transcribe(audio, max_tokens_per_window=12)
+    # no-timestamp mode: one segment per 30-s window
+    s1, text1 = m.transcribe(audio, max_tokens_per_window=12, timestamps=False)
+    s2, text2 = m.transcribe(audio, max_tokens_per_window=12, timestamps=False)
     assert text1 == text2 and len(s1) == 1 and s1[0].tokens == s2[0].tokens and len(s1[0].tokens) >= 1
     assert s1[0].start_ns == 0 and s1[0].end_ns == 2 * 10 ** 9
     assert all(t < m.eot for t in s1[0].tokens)
     # explicit language and the translate task take other prompt tokens
-    s3, _ = m.transcribe(audio, language="de", translate=True, max_tokens_per_window=12)
+    s3, _ = m.transcribe(audio, language="de", translate=True, max_tokens_per_window=12, timestamps=False)
     assert len(s3) == 1
     with pytest.raises(ValueError):
         m.transcribe(audio, language="xx")
     # > 30 s of audio: one segment per window
     long = np.concatenate([audio] * 16)
-    s4, _ = m.transcribe(long, max_tokens_per_window=4)
+    s4, _ = m.transcribe(long, max_tokens_per_window=4, timestamps=False)
     assert [s.id for s in s4] == [0, 1] and s4[1].start_ns == 30 * 10 ** 9
+    # timestamp mode (the default, as whisper.cpp): segments in order, inside the audio, text only
+    for a, cap in ((audio, 24), (long, 16)):
+        segs, text = m.transcribe(a, max_tokens_per_window=cap)
+        again, _ = m.transcribe(a, max_tokens_per_window=cap)
+        assert [s.tokens for s in segs] == [s.tokens for s in again]
+        assert segs and [s.id for s in segs] == list(range(len(segs))) and text == "".join(s.text for s in segs)
+        dur = int(a.shape[0] / 16000 * 1e9) + 1
+        for x, y in zip(segs, segs[1:]):
+            assert x.start_ns <= y.start_ns
+        assert all(0 <= s.start_ns <= s.end_ns <= dur and all(t < m.eot for t in s.tokens) for s in segs)
+
+
+def test_timestamp_rules_and_segments(wpath):
+    """The decoding rules on synthetic logits and the segment split on synthetic token streams."""
+    m = WhisperModel(wpath, "cpu")
+    tb, V = m.timestamp_begin, m.hp.n_vocab
+    lg = torch.zeros(V)
+    m._timestamp_rules(lg, [])
+    allowed = torch.isfinite(lg).nonzero().flatten().tolist()
+    assert allowed == list(range(tb, tb + 51))                     # first token: a timestamp <= 1.00 s
+    lg = torch.zeros(V)
+    m._timestamp_rules(lg, [tb + 10, 300])
+    # text after an opening timestamp: the closing one must be later (nonzero-length segment)
+    assert torch.isinf(lg[tb:tb + 11]).all() and torch.isfinite(lg[tb + 11]) and torch.isinf(lg[m.no_timestamps])
+    lg = torch.zeros(V)
+    m._timestamp_rules(lg, [tb + 10, 300, tb + 40])               # pair open after text: close it
+    assert torch.isinf(lg[:m.eot]).all() and torch.isfinite(lg[tb + 40])
+    lg = torch.zeros(V)
+    m._timestamp_rules(lg, [tb + 10, 300, tb + 40, tb + 40])      # pair complete: text next
+    assert torch.isinf(lg[tb:]).all() and torch.isfinite(lg[300])
+    lg = torch.full((V,), -5.0)
+    lg[tb:] = 0.0                                                  # timestamps' mass beats any text token
+    m._timestamp_rules(lg, [tb, 300])
+    assert torch.isinf(lg[:tb]).all()
+    # "<|0.00|> a b <|1.00|><|1.00|> c <|2.50|>" in a window starting at 30 s
+    segs, seek = m.split_segments([tb, 11, 12, tb + 50, tb + 50, 13, tb + 125], 30.0, 30.0)
+    assert [(a, b, t) for a, b, t in segs] == [(30.0, 31.0, [11, 12]), (31.0, 32.5, [13])]
+    assert seek == pytest.approx(2.5)                              # ended on a lone timestamp: seek to it
+    segs, seek = m.split_segments([tb, 11, tb + 50, tb + 50, 12], 0.0, 7.0)
+    assert segs[-1] == (1.0, 7.0, [12]) and seek == 7.0            # unterminated: runs to the window end
 
 
 def test_transcription_endpoint(wpath, tmp_path):
@@ -89,8 +130,9 @@ def test_transcription_endpoint(wpath, tmp_path):
                    files={"file": ("c.wav", wav, "audio/wav")})
         assert r.status_code == 200, r.text
         j = r.json()
-        assert len(j["segments"]) == 1 and j["text"] == j["segments"][0]["text"]
-        assert j["segments"][0]["end"] == 2 * 10 ** 9 and j["segments"][0]["tokens"]
+        assert j["segments"] and j["text"] == "".join(s["text"] for s in j["segments"])
+        assert all(s["end"] <= 2 * 10 ** 9 + 1 and s["start"] <= s["end"] for s in j["segments"])
+        assert [s["id"] for s in j["segments"]] == list(range(len(j["segments"])))
 
 
 @pytest.mark.gpu
@@ -110,4 +152,4 @@ def test_whisper_on_gpu_matches_cpu(wpath, tmp_path):
     res = asyncio.run(sv.LoadModel(pb.ModelOptions(ModelFile=wpath, Model=wpath)))
     assert res.success, res.message
     out = asyncio.run(sv.AudioTranscription(pb.TranscriptRequest(dst=str(tmp_path / "g.wav"), language="en")))
-    assert len(out.segments) == 1 and out.text == out.segments[0].text and len(out.segments[0].tokens) >= 1
+    assert out.segments and out.text == "".join(s.text for s in out.segments)
