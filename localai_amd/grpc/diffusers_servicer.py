@@ -6,7 +6,9 @@ Mirrors `backend/python/diffusers/backend.py`: LoadModel keeps `CFGScale` (7 whe
 `negative_prompt`, seeds its generator when `seed > 0`, and honours `EnableParameters` (a comma
 list naming which of negative_prompt / width / height / num_inference_steps reach the pipeline,
 "none" for none of them -- the rest take the pipeline defaults: sample_size * 8 pixels, 50 steps).
-One image at a time (the reference runs one gRPC worker per backend).
+`src` makes the call img2img (strength 0.8, the diffusers default); `SchedulerType` takes every
+scheduler name of the reference's mapping (models/schedulers.py).  One image at a time (the
+reference runs one gRPC worker per backend).
 """
 from __future__ import annotations
 
@@ -64,16 +66,20 @@ class DiffusersServicer:
         kw = {k: options[k] for k in keys if k in options}
         w = int(kw.get("width") or default_px)
         h = int(kw.get("height") or default_px)
+        image = request.src or None   # backend.py: options["image"] = Image.open(request.src) -> img2img
+        if image is not None:
+            # the reference passes width / height only when asked; img2img keeps the source's size otherwise
+            w = int(kw["width"]) if kw.get("width") else 0
+            h = int(kw["height"]) if kw.get("height") else 0
         with self._lock:
             img = p(request.positive_prompt, kw.get("negative_prompt", ""), w, h,
                     steps=int(kw.get("num_inference_steps", 50)), guidance_scale=self.cfg_scale,
-                    seed=request.seed if request.seed > 0 else None)
+                    seed=request.seed if request.seed > 0 else None, image=image)
             p.save(img, request.dst)
 
     async def GenerateImage(self, request, context=None):
-        if request.src:
-            # backend.py feeds `src` to img2img / ControlNet pipelines; the native pipeline is txt2img only
-            return pb.Result(success=False, message="img2img (src) is not supported by the native SD pipeline; "
-                                                    "register an external diffusers backend for it")
-        await asyncio.get_running_loop().run_in_executor(None, self._generate, request)
+        try:
+            await asyncio.get_running_loop().run_in_executor(None, self._generate, request)
+        except (ValueError, OSError) as e:
+            return pb.Result(success=False, message=f"Unexpected {e!r}")
         return pb.Result(message="Media generated", success=True)

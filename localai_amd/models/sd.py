@@ -21,9 +21,11 @@ PyTorch path (profiles/r2c_sd15.md).
 
 Classifier-free guidance runs conditional and unconditional branches as one batch of 2.  On
 the GPU everything is bf16 (convolutions through MIOpen, attention through PyTorch's fused SDPA,
-the GEMMs through hipBLASLt); the schedulers keep latents in fp32.  Schedulers: DDIM
-(eta 0, "leading" spacing with `steps_offset`) and Euler (discrete, "leading"), the two
-`SchedulerType` values `ddim` / `euler` of backend.py:74-143; anything else falls back to DDIM.
+the GEMMs through hipBLASLt); the schedulers keep latents in fp32.  Schedulers: every
+`SchedulerType` of backend.py:74-143 (models/schedulers.py: DDIM, PNDM/PLMS, and the sigma-space
+samplers euler, euler_a, heun, lms, dpm_2, dpm_2_a, dpmpp_2m, dpmpp_sde, dpmpp_2m_sde, unipc, with
+`k_` Karras variants); an unknown name is refused, as the reference's get_scheduler does.
+img2img: the KL-VAE encoder half samples the source image's latents, noised to `strength`.
 """
 from __future__ import annotations
 
@@ -33,6 +35,7 @@ from collections import OrderedDict
 import os
 from typing import Dict, List, Optional, Sequence
 
+import numpy as np
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -390,6 +393,67 @@ class VaeDecoder(nn.Module):
         return d.conv_out(_gn(d.conv_norm_out, h, True))
 
 
+class VaeEncoder(nn.Module):
+    """KL-VAE encoder (img2img): conv stem, DownEncoderBlock2D stages (right/bottom-padded stride-2
+    convs), mid block, then the latent distribution's mean / log-variance through quant_conv."""
+
+    def __init__(self, c: dict):
+        super().__init__()
+        ch = list(c["block_out_channels"])
+        lpb = int(c.get("layers_per_block", 2))
+        g = int(c.get("norm_num_groups", 32))
+        lat = int(c.get("latent_channels", 4))
+        self.scaling = float(c.get("scaling_factor", 0.18215))
+        e = nn.Module()
+        e.conv_in = nn.Conv2d(c.get("in_channels", 3), ch[0], 3, padding=1)
+        downs, prev = [], ch[0]
+        for i in range(len(ch)):
+            b = nn.Module()
+            b.resnets = nn.ModuleList(_Resnet(prev if j == 0 else ch[i], ch[i], g, 1e-6, None) for j in range(lpb))
+            if i < len(ch) - 1:
+                b.downsamplers = nn.ModuleList([_Down(ch[i], pad=0)])
+            downs.append(b)
+            prev = ch[i]
+        e.down_blocks = nn.ModuleList(downs)
+        e.mid_block = nn.Module()
+        e.mid_block.resnets = nn.ModuleList([_Resnet(ch[-1], ch[-1], g, 1e-6, None) for _ in range(2)])
+        e.mid_block.attentions = nn.ModuleList([_VaeAttn(ch[-1], g, 1e-6)])
+        e.conv_norm_out = nn.GroupNorm(g, ch[-1], eps=1e-6)
+        e.conv_out = nn.Conv2d(ch[-1], 2 * lat, 3, padding=1)
+        self.encoder = e
+        self.quant_conv = nn.Conv2d(2 * lat, 2 * lat, 1)
+
+    def forward(self, img: torch.Tensor, gen: Optional[torch.Generator] = None) -> torch.Tensor:
+        """img [B, 3, H, W] in [-1, 1] -> scaled latents (a sample of the latent distribution)."""
+        e = self.encoder
+        h = e.conv_in(img)
+        for b in e.down_blocks:
+            for r in b.resnets:
+                h = r(h)
+            if hasattr(b, "downsamplers"):
+                h = b.downsamplers[0](h)
+        h = e.mid_block.resnets[1](e.mid_block.attentions[0](e.mid_block.resnets[0](h)))
+        m = self.quant_conv(e.conv_out(_gn(e.conv_norm_out, h, True))).float()
+        mean, logvar = m.chunk(2, dim=1)
+        std = torch.exp(0.5 * logvar.clamp(-30.0, 20.0))
+        eps = torch.randn(mean.shape, generator=gen).to(mean.device)
+        return (mean + std * eps) * self.scaling
+
+
+def _vae_enc_names(sd: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
+    ren = {".query.": ".to_q.", ".key.": ".to_k.", ".value.": ".to_v.", ".proj_attn.": ".to_out.0."}
+    out = {}
+    for k, v in sd.items():
+        if not (k.startswith("encoder.") or k.startswith("quant_conv.")):
+            continue
+        for a, b in ren.items():
+            k = k.replace(a, b)
+        if ".attentions." in k and k.endswith(".weight") and v.dim() == 4:
+            v = v[:, :, 0, 0]
+        out[k] = v
+    return out
+
+
 def _vae_names(sd: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
     """Decoder tensors only; older VAE checkpoints name the attention `query/key/value/proj_attn`
     and store them as 1x1 convolutions."""
@@ -478,8 +542,16 @@ class StableDiffusion:
         self.unet_sample_size = int(ucfg.get("sample_size", 64))
         self.unet = UNet(ucfg)
         self.unet.load_state_dict(_load_weights(os.path.join(path, "unet")), strict=True)
-        self.vae = VaeDecoder(_cfg(os.path.join(path, "vae", "config.json")))
-        self.vae.load_state_dict(_vae_names(_load_weights(os.path.join(path, "vae"))), strict=True)
+        vcfg = _cfg(os.path.join(path, "vae", "config.json"))
+        vae_sd = _load_weights(os.path.join(path, "vae"))
+        self.vae = VaeDecoder(vcfg)
+        self.vae.load_state_dict(_vae_names(vae_sd), strict=True)
+        enc = _vae_enc_names(vae_sd)
+        self.vae_enc = None
+        if enc:  # img2img needs the encoder half (decoder-only VAE checkpoints stay txt2img)
+            self.vae_enc = VaeEncoder(vcfg)
+            self.vae_enc.load_state_dict(enc, strict=True)
+            self.vae_enc.to(self.device, self.dtype).eval().requires_grad_(False)
         for m in (self.text, self.unet, self.vae):
             m.to(self.device, self.dtype).eval().requires_grad_(False)
         if self.channels_last:
@@ -487,7 +559,12 @@ class StableDiffusion:
             self.vae.to(memory_format=torch.channels_last)
         sc = os.path.join(path, "scheduler", "scheduler_config.json")
         self.sched_cfg = _cfg(sc) if os.path.isfile(sc) else {}
-        self.sched = Scheduler(self.sched_cfg, (scheduler or "ddim").lower())
+        from .schedulers import PLMS, KSampler, parse_name
+        self.sched_name, karras = parse_name(scheduler or "ddim")
+        self.sched = Scheduler(self.sched_cfg, "ddim")
+        self.ksampler = KSampler(self.sched_cfg, scheduler) if self.sched_name not in ("ddim", "pndm") else None
+        self.plms = PLMS(self.sched_cfg) if self.sched_name == "pndm" else None
+        self.pred = self.sched_cfg.get("prediction_type", "epsilon")
         from transformers import CLIPTokenizer
         self.tok = CLIPTokenizer.from_pretrained(os.path.join(path, "tokenizer"))
         self.max_len = self.text.text_model.embeddings.position_embedding.weight.shape[0]
@@ -538,31 +615,85 @@ class StableDiffusion:
                        return_tensors="pt").input_ids.to(self.device)
         return self.text(ids, self.clip_skip)
 
+    def _eps(self, x: torch.Tensor, t: float, ctx: torch.Tensor, cfg: bool, guidance_scale: float) -> torch.Tensor:
+        """Model output (eps or v) at timestep t with classifier-free guidance as one batch of 2."""
+        xin = torch.cat([x, x]) if cfg else x
+        tt = torch.full((xin.shape[0],), float(t), device=self.device)
+        xin = xin.to(self.dtype)
+        if self.channels_last:
+            xin = xin.contiguous(memory_format=torch.channels_last)
+        out = self._unet(xin, tt, ctx).float()
+        if cfg:
+            u, c = out.chunk(2)
+            out = u + guidance_scale * (c - u)
+        return out
+
+    def _init_latents(self, image, w: int, h: int, g: torch.Generator) -> torch.Tensor:
+        """img2img source -> scaled latents of the requested size."""
+        from PIL import Image
+        if self.vae_enc is None:
+            raise ValueError("this VAE checkpoint has no encoder: img2img is unavailable")
+        im = image if isinstance(image, Image.Image) else Image.open(image)
+        im = im.convert("RGB").resize((w * self.vae_scale, h * self.vae_scale), Image.BICUBIC)
+        a = torch.from_numpy(np.asarray(im, dtype=np.float32)).permute(2, 0, 1)[None] / 127.5 - 1.0
+        a = a.to(self.device, self.dtype)
+        if self.channels_last:
+            a = a.contiguous(memory_format=torch.channels_last)
+        return self.vae_enc(a, g).float()
+
     @torch.inference_mode()
     def __call__(self, prompt: str, negative_prompt: str = "", width: int = 512, height: int = 512,
-                 steps: int = 1, guidance_scale: float = 7.0, seed: Optional[int] = None) -> torch.Tensor:
-        """-> uint8 image [H, W, 3] on the CPU."""
+                 steps: int = 1, guidance_scale: float = 7.0, seed: Optional[int] = None,
+                 image=None, strength: float = 0.8) -> torch.Tensor:
+        """-> uint8 image [H, W, 3] on the CPU.  `image` (a path or PIL image) turns the call into
+        img2img: its latents are noised to `strength` of the schedule and denoised from there."""
         g = torch.Generator().manual_seed(seed if seed is not None else int.from_bytes(os.urandom(4), "little"))
+        if image is not None and not (width and height):
+            from PIL import Image
+            im = image if isinstance(image, Image.Image) else Image.open(image)
+            width, height = im.size
         h, w = max(1, height // self.vae_scale), max(1, width // self.vae_scale)
         cfg = guidance_scale > 1.0
         ctx = self._encode([negative_prompt, prompt] if cfg else [prompt])
-        ts = self.sched.timesteps(max(1, steps))
-        x = torch.randn(1, self.latent_ch, h, w, generator=g).to(self.device) * self.sched.init_sigma(ts)
-        for i, t in enumerate(ts):
-            xin = self.sched.scale_input(x, t)
-            xin = torch.cat([xin, xin]) if cfg else xin
-            tt = torch.full((xin.shape[0],), t, device=self.device)
-            xin = xin.to(self.dtype)
-            if self.channels_last:
-                xin = xin.contiguous(memory_format=torch.channels_last)
-            out = self._unet(xin, tt, ctx).float()
-            if cfg:
-                u, c = out.chunk(2)
-                out = u + guidance_scale * (c - u)
-            x = self.sched.step(out, t, ts[i + 1] if i + 1 < len(ts) else None, x)
+        steps = max(1, steps)
+        x0 = self._init_latents(image, w, h, g) if image is not None else None
+        # img2img: skip the first (1 - strength) of the schedule (diffusers get_timesteps)
+        skip = max(steps - min(int(steps * strength), steps), 0) if x0 is not None else 0
+        noise = torch.randn(1, self.latent_ch, h, w, generator=g).to(self.device)
+        if x0 is not None and skip >= steps:
+            x = x0                                 # strength 0: nothing to denoise
+        elif self.ksampler is not None:
+            ks = self.ksampler
+            sig = ks.sigmas(steps)[skip:]
+            x = noise * sig[0] if x0 is None else x0 + noise * sig[0]
+
+            def denoise(xv, sigma):
+                c_in = 1.0 / math.sqrt(sigma * sigma + 1.0)
+                out = self._eps(xv * c_in, ks.sched.sigma_to_t(sigma), ctx, cfg, guidance_scale)
+                if self.pred == "v_prediction":
+                    return xv / (sigma * sigma + 1.0) - out * (sigma * c_in)
+                return xv - sigma * out
+            x = ks.sample(denoise, x, sig, g)
+        elif self.plms is not None:
+            ts = self.plms.timesteps(steps)
+            self.plms.reset(steps)
+            ts = ts[skip:] if skip else ts
+            x = noise if x0 is None else self._add_noise(x0, noise, ts[0])
+            for t in ts:
+                x = self.plms.step(self._eps(x, t, ctx, cfg, guidance_scale), t, x)
+        else:
+            ts = self.sched.timesteps(steps)[skip:]
+            x = noise if x0 is None else self._add_noise(x0, noise, ts[0])
+            for i, t in enumerate(ts):
+                out = self._eps(x, t, ctx, cfg, guidance_scale)
+                x = self.sched.step(out, t, ts[i + 1] if i + 1 < len(ts) else None, x)
         img = self.vae(x.to(self.dtype)).float()
         img = ((img[0] / 2 + 0.5).clamp(0, 1) * 255).round().to(torch.uint8)
         return img.permute(1, 2, 0).cpu()
+
+    def _add_noise(self, x0: torch.Tensor, noise: torch.Tensor, t: int) -> torch.Tensor:
+        a = float(self.sched.ac[t])
+        return math.sqrt(a) * x0 + math.sqrt(1 - a) * noise
 
     def save(self, img: torch.Tensor, dst: str):
         from PIL import Image

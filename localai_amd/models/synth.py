@@ -844,7 +844,7 @@ def write_sd_pipeline(out_dir: str, size: str = "tiny", seed: int = 0, v_predict
     import transformers as tf
     from safetensors.torch import save_file
 
-    from .sd import UNet, VaeDecoder
+    from .sd import UNet, VaeDecoder, VaeEncoder
     if size == "sd15":
         uc, vc, tc = dict(SD15_UNET), dict(SD15_VAE), dict(SD15_TEXT)
     else:
@@ -867,7 +867,10 @@ def write_sd_pipeline(out_dir: str, size: str = "tiny", seed: int = 0, v_predict
         with open(os.path.join(out_dir, sub, "config.json"), "w") as f:
             json.dump(dict(c, _class_name="UNet2DConditionModel" if sub == "unet" else "AutoencoderKL"), f)
         dt = torch.bfloat16 if size == "sd15" else torch.float32  # halves the 3.4 GB SD-1.5 UNet file
-        save_file({k: v.to(dt).contiguous() for k, v in m.state_dict().items()},
+        sd = m.state_dict()
+        if sub == "vae":  # the full AutoencoderKL: the encoder half too (img2img)
+            sd.update(VaeEncoder(c).state_dict())
+        save_file({k: v.to(dt).contiguous() for k, v in sd.items()},
                   os.path.join(out_dir, sub, "diffusion_pytorch_model.safetensors"))
     te = tf.CLIPTextModel(tf.CLIPTextConfig(**tc))
     te.save_pretrained(os.path.join(out_dir, "text_encoder"), safe_serialization=True)

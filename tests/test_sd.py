@@ -102,9 +102,15 @@ def test_servicer_generate_image(pipe_dir, tmp_path):
         await sv.GenerateImage(pb.GenerateImageRequest(positive_prompt="a boat", width=40, height=32, step=1,
                                                        EnableParameters="none", seed=3, dst=dst + ".2.png"))
         r = await sv.GenerateImage(pb.GenerateImageRequest(positive_prompt="a boat", src="in.png", dst=dst + ".3.png"))
-        assert not r.success and "img2img" in r.message
+        assert not r.success and "No such file" in r.message
+        # img2img from a real source keeps the source's size (no width / height asked)
+        Image.new("RGB", (24, 16), (200, 30, 30)).save(tmp_path / "src.png")
+        r = await sv.GenerateImage(pb.GenerateImageRequest(positive_prompt="a boat", src=str(tmp_path / "src.png"),
+                                                           step=4, seed=1, dst=dst + ".4.png"))
+        assert r.success, r.message
     asyncio.run(go())
-    assert sv.cfg_scale == 5.0 and sv.pipe.sched.kind == "euler"
+    assert sv.cfg_scale == 5.0 and sv.pipe.sched_name == "euler" and sv.pipe.ksampler is not None
+    assert Image.open(dst + ".4.png").size == (24, 16)
     assert Image.open(dst).size == (40, 32)
     px = sv.pipe.unet_sample_size * sv.pipe.vae_scale
     assert Image.open(dst + ".2.png").size == (px, px)
@@ -205,3 +211,47 @@ def test_unet_graph_cache_is_bounded(pipe_dir, monkeypatch):
         p("a cat", "", side, side, steps=2, seed=1)
     assert len(p._graphs) == 2
     assert [k[0][-1] for k in p._graphs] == [6, 7]   # the two most recent latent sizes
+
+
+@pytest.mark.parametrize("name", ["pndm", "heun", "unipc", "euler_a", "lms", "dpm_2", "dpm_2_a", "dpmpp_2m",
+                                  "dpmpp_sde", "dpmpp_2m_sde", "k_dpmpp_2m", "k_lms"])
+def test_every_reference_scheduler_runs_the_pipeline(pipe_dir, name):
+    """Each SchedulerType of the reference's mapping drives the pipeline end to end; seeded runs are
+    reproducible; unknown names are refused at load."""
+    p = StableDiffusion(pipe_dir, "cpu", scheduler=name)
+    a = p("a lighthouse", "", 32, 32, steps=3, seed=5)
+    b = p("a lighthouse", "", 32, 32, steps=3, seed=5)
+    assert a.shape == (32, 32, 3) and torch.equal(a, b)
+
+
+def test_unknown_scheduler_refused(pipe_dir):
+    with pytest.raises(ValueError, match="Invalid scheduler"):
+        StableDiffusion(pipe_dir, "cpu", scheduler="k_bogus")
+
+
+def test_img2img_strength(pipe_dir, tmp_path):
+    """img2img: strength 0 returns (a VAE round trip of) the source; full strength ignores it."""
+    from PIL import Image
+    p = StableDiffusion(pipe_dir, "cpu", scheduler="ddim")
+    src = Image.new("RGB", (32, 32), (10, 200, 40))
+    lo = p("x", "", 32, 32, steps=4, seed=2, image=src, strength=0.0)
+    hi = p("x", "", 32, 32, steps=4, seed=2, image=src, strength=1.0)
+    txt = p("x", "", 32, 32, steps=4, seed=2)
+    assert lo.shape == hi.shape == (32, 32, 3)
+    assert not torch.equal(lo, hi) and not torch.equal(lo, txt)
+
+
+@pytest.mark.gpu
+def test_k_sampler_and_img2img_on_gpu(pipe_dir):
+    """Sigma-space sampler (fractional timesteps through the captured UNet graph) and img2img on
+    the device: seeded runs reproduce, and match the CPU pipeline's layout."""
+    from PIL import Image
+    g = StableDiffusion(pipe_dir, "cuda:0", scheduler="k_dpmpp_2m")
+    a = g("a cat", "", 32, 32, steps=4, seed=7)
+    b = g("a cat", "", 32, 32, steps=4, seed=7)
+    assert torch.equal(a, b)
+    c = StableDiffusion(pipe_dir, "cpu", scheduler="k_dpmpp_2m")("a cat", "", 32, 32, steps=4, seed=7)
+    assert (a.float() - c.float()).abs().mean() < 4.0
+    src = Image.new("RGB", (32, 32), (10, 200, 40))
+    i2i = g("a cat", "", 32, 32, steps=4, seed=7, image=src, strength=0.6)
+    assert i2i.shape == (32, 32, 3)
