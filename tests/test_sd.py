@@ -210,7 +210,8 @@ def test_unet_graph_cache_is_bounded(pipe_dir, monkeypatch):
     for side in (32, 40, 48, 56):
         p("a cat", "", side, side, steps=2, seed=1)
     assert len(p._graphs) == 2
-    assert [k[0][-1] for k in p._graphs] == [6, 7]   # the two most recent latent sizes
+    # the two most recent latent sizes (side / the VAE's downscale)
+    assert [k[0][-1] for k in p._graphs] == [48 // p.vae_scale, 56 // p.vae_scale]
 
 
 @pytest.mark.parametrize("name", ["pndm", "heun", "unipc", "euler_a", "lms", "dpm_2", "dpm_2_a", "dpmpp_2m",
