@@ -105,11 +105,14 @@ def build_router(state) -> APIRouter:
             raise APIError(f"backend {name} is not currently loaded", 500)
         try:
             st = await lm.handle.Status(pb.HealthMessage())
-            return {"state": int(st.state), "memory": {"total": st.memory.total,
-                                                        "breakdown": dict(st.memory.breakdown)}}
+            out = {"state": int(st.state), "memory": {"total": st.memory.total,
+                                                       "breakdown": dict(st.memory.breakdown)}}
+            if hasattr(lm.handle, "stats"):  # data-parallel replicas: per-replica load
+                out["replicas"] = lm.handle.stats()
+            return out
         except Exception:
             import psutil
-            p = psutil.Process(lm.process.pid) if lm.process is not None else psutil.Process()
+            p = psutil.Process(lm.process.pid) if getattr(lm.process, "pid", None) else psutil.Process()
             mi = p.memory_info()
             return {"MemoryInfo": {"rss": mi.rss, "vms": mi.vms}, "MemoryPercent": p.memory_percent(),
                     "CPUPercent": p.cpu_percent(interval=None)}

@@ -101,6 +101,46 @@ def grpc_model_options(c: BackendConfig, app, model_path: str) -> pb.ModelOption
     return o
 
 
+class _ReplicaServicers:
+    """The in-process servicers of a replicated model, shut down together."""
+
+    def __init__(self, servicers):
+        self.servicers = list(servicers)
+        self.engine = servicers[0].engine if servicers and hasattr(servicers[0], "engine") else None
+
+    def shutdown(self):
+        for sv in self.servicers:
+            sv.shutdown()
+
+
+class _ProcessGroup:
+    """The worker processes of a replicated model: poll() reports the first one that died."""
+
+    def __init__(self, procs):
+        self.procs = [p for p in procs if p is not None]
+        self.returncode = None
+
+    def poll(self):
+        for p in self.procs:
+            rc = p.poll()
+            if rc is not None:
+                self.returncode = rc
+                return rc
+        return None
+
+    def terminate(self):
+        for p in self.procs:
+            p.terminate()
+
+    def kill(self):
+        for p in self.procs:
+            p.kill()
+
+    def wait(self, timeout=None):
+        for p in self.procs:
+            p.wait(timeout)
+
+
 class ModelManager:
     def __init__(self, app_config, models_path: str):
         self.app = app_config
@@ -229,6 +269,9 @@ class ModelManager:
         if not (os.path.isfile(opts.ModelFile) or is_hf_checkpoint(opts.ModelFile)):
             raise RuntimeError(f"could not load model: model file {opts.ModelFile} not found")
         tp = int(cfg.raw.get("tensor_parallel_size") or 0)
+        dp = int(cfg.raw.get("data_parallel_size") or cfg.raw.get("replicas") or 0)
+        if dp > 1:
+            return await self._start_replicas(mid, cfg, opts, dp, tp)
         if tp > 1:
             return await self._start_tp_group(mid, cfg, opts, tp)
         if self.app.engine_mode == "process":
@@ -254,9 +297,84 @@ class ModelManager:
             raise RuntimeError(res.message)
         return LoadedModel(mid, "localai-amd", EmbeddedBackend(sv), servicer=sv)
 
-    async def _start_tp_group(self, mid: str, cfg: BackendConfig, opts, tp: int) -> LoadedModel:
+    def _replica_devices(self, cfg: BackendConfig, n: int, per: int) -> list:
+        """Devices of n replicas of `per` GPUs each: consecutive GPUs from main_gpu (default 0);
+        every replica on the CPU when there is no GPU."""
+        try:
+            import torch
+            ngpu = torch.cuda.device_count() if torch.cuda.is_available() else 0
+        except Exception:
+            ngpu = 0
+        if ngpu == 0:
+            return ["cpu"] * n
+        mg = str(cfg.raw.get("main_gpu") or "0")
+        base = int(mg) if mg.isdigit() else 0
+        if base + n * per > ngpu:
+            raise RuntimeError(f"data_parallel_size {n} x {per} GPU(s) from GPU {base} needs {base + n * per} GPUs, "
+                               f"{ngpu} visible")
+        return [f"cuda:{base + i * per}" for i in range(n)]
+
+    async def _start_replicas(self, mid: str, cfg: BackendConfig, opts, dp: int, tp: int) -> LoadedModel:
+        """data_parallel_size = N > 1: N engine replicas of the model (one per GPU, or one per
+        tensor-parallel group of tensor_parallel_size GPUs), served through ONE handle that sends
+        each request to the least-busy replica, preferring the replica that holds the request's
+        prompt prefix in its cache (parallel/replicas.py)."""
+        from ..parallel.replicas import ReplicaBackend
+        per = max(1, tp)
+        devs = self._replica_devices(cfg, dp, per)
+        handles, procs, servicers, names = [], [], [], []
+        try:
+            for i, dev in enumerate(devs):
+                if per > 1:
+                    first = int(dev.split(":")[1])
+                    vis = ",".join(str(first + j) for j in range(per))
+                    lm = await self._start_tp_group(f"{mid}#{i}", cfg, opts, per, visible=vis)
+                    handles.append(lm.handle)
+                    procs.append(lm.process)
+                    names.append(f"{lm.addr}[gpus {vis}]")
+                elif self.app.engine_mode == "process":
+                    addr = f"127.0.0.1:{free_port()}"
+                    env = dict(os.environ)
+                    if dev.startswith("cuda:"):
+                        env["LOCALAI_DEVICE"] = dev
+                    proc = subprocess.Popen([sys.executable, "-m", "localai_amd.worker", "--addr", addr], env=env)
+                    procs.append(proc)
+                    h = GRPCBackend(addr)
+                    await self._wait_healthy(h, cfg, proc)
+                    res = await h.LoadModel(opts, timeout=3600)
+                    if not res.success:
+                        raise RuntimeError(f"could not load model: {res.message}")
+                    handles.append(h)
+                    names.append(f"{addr}[{dev}]")
+                else:
+                    from ..grpc.servicer import EngineServicer
+                    sv = EngineServicer(device=dev)
+                    res = await sv.LoadModel(opts)
+                    if not res.success:
+                        raise RuntimeError(res.message)
+                    servicers.append(sv)
+                    handles.append(EmbeddedBackend(sv))
+                    names.append(f"embedded[{dev}]#{i}")
+        except Exception:
+            for sv in servicers:
+                sv.shutdown()
+            for h in handles:
+                if isinstance(h, GRPCBackend):
+                    await h.close()
+            for p in procs:
+                if p is not None:
+                    p.terminate()
+            raise
+        rb = ReplicaBackend(handles, names, affinity_chars=int(cfg.raw.get("replica_affinity_chars") or 512))
+        log.info("model %s: %d replicas %s", mid, dp, names)
+        return LoadedModel(mid, f"localai-amd-dp{dp}" + (f"xtp{per}" if per > 1 else ""), rb,
+                           servicer=_ReplicaServicers(servicers) if servicers else None,
+                           process=_ProcessGroup(procs) if procs else None, addr=rb.addr)
+
+    async def _start_tp_group(self, mid: str, cfg: BackendConfig, opts, tp: int, visible: str = "") -> LoadedModel:
         """tensor_parallel_size > 1: one process per GPU via torch.distributed.run (RCCL over xGMI);
-        rank 0 serves backend.proto and the gateway talks to it like any other backend."""
+        rank 0 serves backend.proto and the gateway talks to it like any other backend.
+        `visible`: the group's GPUs (HIP_VISIBLE_DEVICES) when several groups share a node."""
         port, mport = free_port(), free_port()
         addr = f"127.0.0.1:{port}"
         ctx = int(cfg.raw.get("context_size") or opts.ContextSize or 4096)
@@ -268,7 +386,10 @@ class ModelManager:
             cmd.append("--eager")
         if cfg.raw.get("expert_parallel"):  # model-config extension (not in the reference schema)
             cmd.append("--expert-parallel")
-        proc = subprocess.Popen(cmd, env=dict(os.environ))
+        env = dict(os.environ)
+        if visible:
+            env["HIP_VISIBLE_DEVICES"] = visible
+        proc = subprocess.Popen(cmd, env=env)
         h = GRPCBackend(addr)
         g = dict(cfg.raw.get("grpc") or {})
         g.setdefault("attempts", 300)  # sharded load of a 70B model takes a while
