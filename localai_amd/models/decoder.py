@@ -31,6 +31,10 @@ from .hparams import HParams
 
 # batch-1/2 decode: q|k|v GEMV with RoPE + KV append in its epilogue (ops.qkv_rope_dp4)
 FUSED_QKV_ROPE = os.environ.get("LOCALAI_AMD_QKV_ROPE", "1") == "1"
+# tensor parallelism: row-parallel outputs of at least this many rows (prefill chunks) all-reduce
+# chunk by chunk on a comm stream, overlapped with the next chunk's GEMM
+TP_OVERLAP_ROWS = int(os.environ.get("LOCALAI_AMD_TP_OVERLAP_ROWS", "1024"))
+TP_OVERLAP_CHUNKS = int(os.environ.get("LOCALAI_AMD_TP_OVERLAP_CHUNKS", "4"))
 # MoE decode batches route with the fused router kernel (moe.hip); =1 falls back to the torch ops
 FUSED_ROUTER_OFF = os.environ.get("LOCALAI_AMD_FUSED_ROUTER_OFF", "0") == "1"
 
@@ -72,6 +76,13 @@ class TPInfo:
             car.close()
             raise CustomAllReduceTimeout("tensor-parallel one-shot all-reduce timed out on a late peer rank: this "
                                          "step's results are invalid; the group continues on RCCL")
+
+    def comm_stream(self, device) -> "torch.cuda.Stream":
+        """The TP collectives' own HIP stream (prefill all-reduces overlapped with GEMMs)."""
+        st = getattr(self, "_comm", None)
+        if st is None:
+            st = self._comm = torch.cuda.Stream(device=device)
+        return st
 
     def all_gather_cols(self, t: torch.Tensor) -> torch.Tensor:
         if self.world == 1:
@@ -408,7 +419,7 @@ class DecoderModel:
             a = a.view(T, self.Hq, self.Dh)[:, :, :self.hp.head_dim_v].reshape(T, -1).contiguous()
         else:
             a = a.view(T, self.Hq * self.Dh)
-        return self._row_parallel_out(ops.linear(a, L.wo), L.wo_bias)
+        return self._row_parallel(a, L.wo, L.wo_bias)
 
     def _expert_slice(self, t, e, rows=None, cols=None):
         E = t.shape[0]
@@ -432,6 +443,40 @@ class DecoderModel:
         self.tp.all_reduce(dense)
         return ops.Partial(dense.unsqueeze(0), bias)
 
+    def _row_parallel(self, x: torch.Tensor, w, bias) -> ops.Partial:
+        """x @ w^T for a row-parallel weight (its input features sharded over the TP ranks),
+        summed over the ranks.  Prefill-size inputs (>= TP_OVERLAP_ROWS rows) run in row chunks:
+        chunk k's all-reduce runs on the TP comm stream while chunk k+1's GEMM runs on the compute
+        stream, so the ~64-128 MB prefill all-reduces over xGMI hide under the GEMMs (SURVEY
+        §2.11); decode batches keep the single latency-bound call (custom one-shot AR)."""
+        tp = self.tp
+        T = x.shape[0]
+        if tp.world == 1 or T < TP_OVERLAP_ROWS or TP_OVERLAP_CHUNKS < 2:
+            return self._row_parallel_out(ops.linear(x, w), bias)
+        step = -(-T // TP_OVERLAP_CHUNKS)
+        step = -(-step // 64) * 64
+        out = torch.empty(T, w.N, dtype=torch.float32, device=x.device)
+        cuda = x.is_cuda
+        if cuda:
+            cs = torch.cuda.current_stream(x.device)
+            comm = tp.comm_stream(x.device)
+        for r0 in range(0, T, step):
+            r1 = min(T, r0 + step)
+            p = ops.linear(x[r0:r1], w)
+            ops.reduce(p, out=out[r0:r1])
+            if cuda:
+                ev = torch.cuda.Event()
+                ev.record(cs)
+                comm.wait_event(ev)
+                with torch.cuda.stream(comm):
+                    tp.all_reduce(out[r0:r1])
+            else:
+                tp.all_reduce(out[r0:r1])
+        if cuda:
+            cs.wait_stream(comm)
+            out.record_stream(comm)
+        return ops.Partial(out.unsqueeze(0), bias)
+
     def _mlp(self, L: Layer, xn: torch.Tensor) -> ops.Partial:
         hp = self.hp
         if L.experts is not None:
@@ -439,7 +484,7 @@ class DecoderModel:
         F, mode = L.F or self.F, _ACT[hp.act]
         h = ops.glu_linear(xn, L.gate_up, F, mode, L.up_bias)  # decode batches: act in the GEMM epilogue
         if h is not None:
-            return self._row_parallel_out(ops.linear(h, L.down), L.down_bias)
+            return self._row_parallel(h, L.down, L.down_bias)
         gu = ops.linear_multi(xn, L.gate_up, bias=L.up_bias)
         d = ops.act_linear(gu, F, mode, L.down)
         return self._row_parallel_out(d, L.down_bias)

@@ -1134,11 +1134,21 @@ def act_linear(src: Partial, F: int, mode: int, w: QWeight) -> Partial:
     return linear(act(src, F, mode), w)
 
 
-def reduce(src: Partial, dtype=torch.float32) -> torch.Tensor:
+def reduce(src: Partial, dtype=torch.float32, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Sum of the split-K slabs (+ bias) as one dense [M, N] matrix (into `out`, a contiguous
+    [M, N] tensor of `dtype`, when given)."""
+    if out is not None:
+        dtype = out.dtype
+        assert out.is_contiguous() and tuple(out.shape) == (src.M, src.N)
     if not src.t.is_cuda:
-        return src.dense().to(dtype)
+        d = src.dense().to(dtype)
+        if out is None:
+            return d
+        out.copy_(d)
+        return out
     T, N = src.M, src.N
-    out = torch.empty(T, N, dtype=dtype, device=src.t.device)
+    if out is None:
+        out = torch.empty(T, N, dtype=dtype, device=src.t.device)
     a = src.src_args()
     f32 = out.data_ptr() if dtype == torch.float32 else None
     b16 = out.data_ptr() if dtype == torch.bfloat16 else None

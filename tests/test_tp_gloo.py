@@ -127,3 +127,12 @@ def test_tp4_replicated_kv_heads(tiny_model_path):
     """TP=4 over a model with 2 kv heads: each kv head lives on the 2 ranks whose query heads read
     it (DecoderModel.kv_rep), so TP degrees above the kv-head count (Qwen2-7B at TP=8) work."""
     _run_tp2(tiny_model_path, world=4)
+
+
+def test_tp2_chunked_row_parallel(tiny_model_path, monkeypatch):
+    """Row-parallel outputs all-reduced chunk by chunk (the prefill overlap path: GEMM of chunk
+    k+1 beside the all-reduce of chunk k on the comm stream) give the unsharded hidden states:
+    forced on for every prefill of >= 2 rows, in 3 chunks."""
+    monkeypatch.setenv("LOCALAI_AMD_TP_OVERLAP_ROWS", "2")
+    monkeypatch.setenv("LOCALAI_AMD_TP_OVERLAP_CHUNKS", "3")
+    _run_tp2(tiny_model_path)

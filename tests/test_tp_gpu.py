@@ -11,12 +11,18 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 @pytest.mark.gpu
-def test_tp2_engine_two_ranks_one_gpu(tmp_path):
+@pytest.mark.parametrize("overlap", [False, True])
+def test_tp2_engine_two_ranks_one_gpu(tmp_path, overlap):
+    """overlap: every prefill's row-parallel outputs all-reduced in chunks on the TP comm stream
+    (the prefill overlap path, forced on at 2 rows)."""
     from localai_amd.models import synth
     p = synth.write_model(str(tmp_path / "tp.gguf"), "tiny-llama", exact=True)
+    env = dict(os.environ)
+    if overlap:
+        env.update(LOCALAI_AMD_TP_OVERLAP_ROWS="2", LOCALAI_AMD_TP_OVERLAP_CHUNKS="3")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-                        "--master-addr", "127.0.0.1", "--master-port", "29541",
+                        "--master-addr", "127.0.0.1", "--master-port", "29542" if overlap else "29541",
                         os.path.join(ROOT, "scripts", "tp_rehearsal.py"), p],
-                       cwd=ROOT, env=dict(os.environ), capture_output=True, text=True, timeout=300)
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "TP_OK" in r.stdout, r.stdout[-2000:]
