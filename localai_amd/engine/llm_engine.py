@@ -37,7 +37,7 @@ from ..native import core
 from ..tokenizer import Tokenizer
 from .prompt_cache import PromptCacheFiles
 from .sampling_params import SamplingParams
-from .speculative import ngram_draft
+from .speculative import DraftModel, ngram_draft
 from ..utils import faults
 from ..utils.trace import get_tracer, roctx
 
@@ -71,6 +71,8 @@ class EngineConfig:
     blas_tune: bool = True            # tune the hipBLASLt/rocBLAS solution per decode GEMM shape at warm-up
     lora_adapters: tuple = ()         # ((adapter GGUF path, scale), ...) merged into the weights at load
     record_tokens: bool = False       # final Event carries the generated token ids (numerics tests)
+    draft_model: str = ""             # speculative decoding: draft LM GGUF (engine/speculative.DraftModel)
+    draft_max_seqs: int = 16          # draft-model KV cache capacity in sequences of context_size
 
 
 @dataclass
@@ -166,6 +168,9 @@ class LLMEngine:
         if faults.hit("kv_alloc"):
             raise faults.InjectedFault("hipMalloc failed for the KV cache (injected fault): out of memory")
         self.kv = self.model.new_kv_cache(num_blocks, bs)
+        self.drafter = None
+        if cfg.draft_model:
+            self.drafter = DraftModel(cfg.draft_model, self.device, cfg.draft_max_seqs, self.ctx, self.hp.n_vocab)
         self.sched = core.Scheduler(num_blocks, bs, cfg.max_num_seqs, cfg.max_batched_tokens, self.ctx,
                                     cfg.prefix_cache, 1 if (cfg.use_graphs and self.device.type == "cuda") else 0)
         self.max_blocks = (self.ctx + bs - 1) // bs
@@ -691,6 +696,7 @@ class LLMEngine:
 
     SPEC_MAX_BATCH = 8   # speculation pays while decode streams weights (small batches)
     SPEC_MAX_DRAFT = 16
+    DRAFT_DEFAULT_K = 8  # draft-model tokens per verify when the request sets no n_draft
 
     def _spec_k(self) -> int:
         """Draft length for an n-gram speculative step (engine/speculative.py), or 0: every
@@ -701,11 +707,12 @@ class LLMEngine:
         k = 0
         for r in self.requests.values():
             p = r.params
-            if (p.n_draft <= 0 or r.n_gen == 0 or r.spec_off or r.grammar is not None or p.mirostat
+            nd = p.n_draft if p.n_draft > 0 else (self.DRAFT_DEFAULT_K if self.drafter is not None else 0)
+            if (nd <= 0 or r.n_gen == 0 or r.spec_off or r.grammar is not None or p.mirostat
                     or not (p.temperature <= 0.0 or p.top_k == 1) or p.logit_bias or p.repeat_penalty != 1.0
                     or p.frequency_penalty != 0.0 or p.presence_penalty != 0.0):
                 return 0
-            k = max(k, min(p.n_draft, self.SPEC_MAX_DRAFT))
+            k = max(k, min(nd, self.SPEC_MAX_DRAFT))
         return k
 
     def _run_spec(self, plan, k: int):
@@ -716,11 +723,14 @@ class LLMEngine:
         reqs = [self.requests[i] for i in ids]
         bm = self.sched.blocks()
         toks, pos, slots, cu, ctxl, drafts, tabs = [], [], [], [0], [], [], []
-        for r in reqs:
-            seq = self.sched.tokens(r.id)
+        seqs = [self.sched.tokens(r.id) for r in reqs]
+        kk = [min(k, max(0, min(self.ctx - len(s), (r.params.max_tokens - r.n_gen) if r.params.max_tokens > 0
+                                else self.ctx) - 1)) for r, s in zip(reqs, seqs)]
+        dm = self.drafter.draft([r.id for r in reqs], seqs, kk) if self.drafter is not None else None
+        for i, r in enumerate(reqs):
+            seq = seqs[i]
             L = len(seq)
-            room = min(self.ctx - L, (r.params.max_tokens - r.n_gen) if r.params.max_tokens > 0 else self.ctx)
-            d = ngram_draft(seq, min(k, max(0, room - 1)))
+            d = dm[i] if dm is not None else ngram_draft(seq, kk[i])
             for j, t in enumerate([seq[-1]] + d):
                 toks.append(t)
                 pos.append(L - 1 + j)
@@ -1220,6 +1230,8 @@ class LLMEngine:
                 log.exception("saving prompt cache %s", p.prompt_cache_path)
         self.sched.finish(r.id)
         self.requests.pop(r.id, None)
+        if self.drafter is not None:
+            self.drafter.release(r.id)
         end = time.perf_counter()
         ttft = (r.first_token_t - r.arrival) if r.first_token_t else 0.0
         gen_s = end - r.first_token_t if r.first_token_t else 0.0

@@ -38,3 +38,134 @@ def ngram_draft(seq: Sequence[int], k: int, max_n: int = 3, min_n: int = 1) -> L
             if len(d):
                 return d.tolist()
     return []
+
+
+class DraftModel:
+    """A small draft LM (config `draft_model`, path relative to the main model's directory as in
+    the reference's `llama.go:89-95`) that proposes k greedy tokens per sequence; the engine
+    verifies them with the main model in one forward (LLMEngine._run_spec), so the output stays
+    exactly the main model's greedy output.
+
+    The draft model keeps its own paged KV cache.  Per request it remembers which tokens its cache
+    holds (`_cached`); a draft call first feeds every sequence the tokens it has not seen (the
+    accepted tokens of the last verify, or the whole prompt the first time) in ONE chunked-prefill
+    forward over all sequences, then k-1 batched single-token decode forwards.  Cache entries past
+    the accepted prefix are simply overwritten by the next call (longest-common-prefix rule)."""
+
+    def __init__(self, path: str, device, max_seqs: int, context_size: int, vocab_size: int,
+                 block_size: int = 32):
+        import torch
+
+        from ..models.decoder import DecoderModel
+        from ..models.hf_checkpoint import open_model
+        self.torch = torch
+        self.device = torch.device(device)
+        self.reader = open_model(path)
+        self.model = DecoderModel(self.reader, self.device, max_pos=context_size)
+        if self.model.hp.n_vocab != vocab_size:
+            raise ValueError(f"draft model vocabulary {self.model.hp.n_vocab} != main model {vocab_size}")
+        self.bs = block_size
+        self.ctx = context_size
+        self.max_blocks = (context_size + block_size - 1) // block_size
+        nblk = max(1, max_seqs) * self.max_blocks + 1
+        self.kv = self.model.new_kv_cache(nblk, block_size)
+        self._free = list(range(nblk - 1, -1, -1))
+        self._pages: dict = {}     # request id -> [page, ...]
+        self._cached: dict = {}    # request id -> token ids whose K/V the cache holds
+        self.ws = None
+
+    def release(self, rid: int) -> None:
+        self._free.extend(self._pages.pop(rid, []))
+        self._cached.pop(rid, None)
+
+    def _ensure_pages(self, rid: int, n_tokens: int, keep=()) -> list:
+        pages = self._pages.setdefault(rid, [])
+        need = (n_tokens + self.bs - 1) // self.bs
+        while len(pages) < need:
+            if not self._free:
+                # evict a request that is not drafting now (it re-feeds its tokens next time)
+                victim = next((r for r in self._pages if r != rid and r not in keep), None)
+                if victim is None:
+                    raise RuntimeError("draft model KV cache exhausted")
+                self.release(victim)
+                continue
+            pages.append(self._free.pop())
+        return pages
+
+    def _slot(self, pages, p: int) -> int:
+        return pages[p // self.bs] * self.bs + p % self.bs
+
+    def _i32(self, a):
+        return self.torch.tensor(np.asarray(a, dtype=np.int32), device=self.device)
+
+    def _table(self, rids):
+        bt = np.zeros((len(rids), max(len(self._pages[r]) for r in rids)), dtype=np.int32)
+        for i, r in enumerate(rids):
+            bt[i, :len(self._pages[r])] = self._pages[r]
+        return self._i32(bt)
+
+    def draft(self, rids: Sequence[int], seqs: Sequence[Sequence[int]], ks: Sequence[int]) -> List[List[int]]:
+        """Greedy drafts of ks[i] tokens continuing seqs[i] (request rids[i])."""
+        from .. import ops
+        from ..models.decoder import ForwardBatch
+        torch = self.torch
+        live = [i for i, k in enumerate(ks) if k > 0 and len(seqs[i]) + k <= self.ctx]
+        out: List[List[int]] = [[] for _ in seqs]
+        if not live:
+            return out
+        # 1) catch-up: tokens the draft cache has not seen, one chunked-prefill forward
+        toks, pos, slots, cu, ctxl = [], [], [], [0], []
+        for i in live:
+            rid, seq = rids[i], list(seqs[i])
+            old = self._cached.get(rid, [])
+            lcp = 0
+            m = min(len(old), len(seq) - 1)  # always re-feed at least the last token
+            while lcp < m and old[lcp] == seq[lcp]:
+                lcp += 1
+            pages = self._ensure_pages(rid, len(seq) + ks[i], keep=set(rids))
+            for p in range(lcp, len(seq)):
+                toks.append(seq[p])
+                pos.append(p)
+                slots.append(self._slot(pages, p))
+            cu.append(len(toks))
+            ctxl.append(len(seq))
+            self._cached[rid] = seq
+        qlens = [cu[j + 1] - cu[j] for j in range(len(live))]
+        rl = [rids[i] for i in live]
+        last = self._i32([c - 1 for c in cu[1:]])
+        fb = ForwardBatch(tokens=self._i32(toks), pos=self._i32(pos), slots=self._i32(slots), decode=False,
+                          block_tables=self._table(rl), cu_q=self._i32(cu), ctx_lens=self._i32(ctxl),
+                          tiles=ops.prefill_tiles(qlens, self.device) if self.device.type == "cuda" else None,
+                          logits_idx=last)
+        cur = self.model.forward(fb, self.kv).argmax(-1)
+        nxt = [int(t) for t in cur.tolist()]
+        for j, i in enumerate(live):
+            out[i].append(nxt[j])
+        # 2) k-1 batched single-token decode forwards over the sequences still drafting
+        kmax = max(ks[i] for i in live)
+        for step in range(1, kmax):
+            act = [j for j, i in enumerate(live) if ks[i] > step]
+            if not act:
+                break
+            ids = [live[j] for j in act]
+            tk = [out[i][-1] for i in ids]
+            ps = [len(seqs[i]) + step - 1 for i in ids]
+            sl = [self._slot(self._pages[rids[i]], p) for i, p in zip(ids, ps)]
+            lens = [p + 1 for p in ps]
+            fb = ForwardBatch(tokens=self._i32(tk), pos=self._i32(ps), slots=self._i32(sl), decode=True,
+                              block_tables=self._table([rids[i] for i in ids]), seq_lens=self._i32(lens),
+                              max_len=max(lens))
+            am = self.model.forward(fb, self.kv, attn_workspace=self._workspace(len(ids))).argmax(-1).tolist()
+            for i, t, p in zip(ids, am, ps):
+                out[i].append(int(t))
+                self._cached[rids[i]] = self._cached[rids[i]] + [out[i][-2]]  # K/V of p now cached
+        return out
+
+    def _workspace(self, B: int):
+        if self.device.type != "cuda":
+            return None
+        from .. import ops
+        if self.ws is None or self.ws[0] < B:
+            hp = self.model
+            self.ws = (B, ops.decode_workspace(B, hp.Hq, hp.Hkv, hp.Dh, self.ctx, self.device, self.bs))
+        return self.ws[1]

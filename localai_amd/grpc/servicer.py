@@ -169,7 +169,8 @@ class EngineServicer:
                 rope_freq_scale=request.RopeFreqScale, rope_scaling=request.RopeScaling,
                 use_graphs=not request.EnforceEager,
                 mmproj=self._mmproj_path(request, path),
-                lora_adapters=self._lora(request, path))
+                lora_adapters=self._lora(request, path),
+                draft_model=self._draft_path(request, path))
             loop = asyncio.get_running_loop()
             eng = await loop.run_in_executor(None, lambda: LLMEngine(cfg, tp=self.tp))
             await loop.run_in_executor(None, eng.warmup)
@@ -197,6 +198,18 @@ class EngineServicer:
         return ((adapter_path(model_path, request.LoraAdapter), float(request.LoraScale or 1.0)),)
 
     @staticmethod
+    @staticmethod
+    def _draft_path(request, model_path: str) -> str:
+        """DraftModel, relative to the main model's directory (reference llama.go:89-95)."""
+        d = str(request.DraftModel or "")
+        if not d:
+            return ""
+        if not os.path.isabs(d):
+            d = os.path.join(os.path.dirname(model_path), d)
+        if not os.path.exists(d):
+            raise FileNotFoundError(f"draft model {d} not found")
+        return d
+
     def _mmproj_path(request, model_path: str) -> str:
         mm = request.MMProj
         if not mm:

@@ -233,3 +233,18 @@ def test_penalties_in_graph_match_host_sampling(tiny_model_path):
     assert a == b and all(x[1] == 24 for x in b)
     plain = _run(_eng(tiny_model_path, 8), prompts, max_tokens=24, temperature=0.0, ignore_eos=True)
     assert plain != b  # the penalties changed the greedy stream
+
+
+def test_draft_model_speculation_on_gpu(tiny_model_path):
+    """draft_model speculation on the HIP path (draft catch-up prefill + batched draft decode
+    forwards, one verify forward of the main model per round): the streams equal plain greedy
+    decoding for several concurrent requests, and a self-draft is always accepted."""
+    prompts = ["draft on the gpu", "second speculative stream", "third"]
+    sp = dict(max_tokens=18, temperature=0.0, ignore_eos=True)
+    base = _run(_eng(tiny_model_path, 1), prompts, **sp)
+    eng = LLMEngine(EngineConfig(model_path=tiny_model_path, device="cuda:0", context_size=256, max_num_seqs=8,
+                                 max_batched_tokens=512, draft_model=tiny_model_path))
+    got = _run(eng, prompts, **sp)
+    assert got == base
+    m = eng.metrics
+    assert m["spec_steps"] > 0 and m["spec_accepted"] == m["spec_drafted"] > 0

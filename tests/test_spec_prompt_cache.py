@@ -104,3 +104,41 @@ def test_prompt_cache_read_only_never_writes(tiny_model_path, tmp_path, ro):
                               prompt_cache_ro=ro))
     e._pcache.flush()
     assert os.path.exists(path) is (not ro)
+
+
+def test_draft_model_speculation_is_exact(tiny_model_path, tmp_path):
+    """draft_model: a second LM proposes the drafts.  With the main model itself as the draft every
+    draft token is accepted (k+1 tokens per verify pass); with an unrelated draft model (other
+    weights, same vocabulary, fewer layers) drafts are mostly rejected; either way the text is the
+    main model's greedy text, and finished requests give their draft KV pages back."""
+    from localai_amd.models import synth
+    prompt = "speculative decoding with a draft model"
+    sp = lambda **kw: SamplingParams(max_tokens=20, temperature=0.0, ignore_eos=True, **kw)  # noqa: E731
+    base = _engine(tiny_model_path).generate(prompt, sp())
+    eng = _engine(tiny_model_path, draft_model=tiny_model_path)
+    out = eng.generate(prompt, sp())
+    assert out["text"] == base["text"] and out["completion_tokens"] == 20
+    m = eng.metrics
+    assert m["spec_steps"] > 0 and m["spec_accepted"] == m["spec_drafted"] > 0
+    assert m["spec_steps"] <= 20 // (eng.DRAFT_DEFAULT_K + 1) + 2  # ~k+1 tokens per main-model pass
+    assert not eng.drafter._pages  # released on finish
+    # a second request reuses the draft cache pages (and n_draft from the request wins)
+    out2 = eng.generate(prompt + " again", sp(n_draft=3))
+    assert out2["text"] == _engine(tiny_model_path).generate(prompt + " again", sp())["text"]
+
+    other = str(tmp_path / "draft.gguf")
+    synth.write_model(other, "tiny-llama", seed=7, exact=True, n_layer=1)
+    eng2 = _engine(tiny_model_path, draft_model=other)
+    outs = [eng2.generate(p, sp()) for p in (prompt, "a different prompt entirely")]
+    assert outs[0]["text"] == base["text"]
+    assert outs[1]["text"] == _engine(tiny_model_path).generate("a different prompt entirely", sp())["text"]
+    assert eng2.metrics["spec_drafted"] > eng2.metrics["spec_accepted"]
+
+
+def test_draft_model_vocab_mismatch_is_a_load_error(tiny_model_path, tmp_path):
+    from localai_amd.models import synth
+    from localai_amd.models.synth import PRESETS
+    other = str(tmp_path / "small-vocab.gguf")
+    synth.write_model(other, "tiny-llama", exact=True, n_vocab=PRESETS["tiny-llama"].n_vocab - 64)
+    with pytest.raises(ValueError, match="vocabulary"):
+        _engine(tiny_model_path, draft_model=other)
