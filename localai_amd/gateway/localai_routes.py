@@ -15,7 +15,8 @@ from ..grpc import backend_pb as pb
 from .metrics import CONTENT_TYPE
 from .model_manager import (BARK_BACKENDS, ENGINE_BACKENDS, HF_BACKENDS, MAMBA_BACKEND, MUSICGEN_BACKENDS, RWKV_BACKEND,
                             SD_BACKENDS, STORE_BACKEND, VITS_BACKENDS)
-from .openai_routes import APIError, merge_request_with_config, model_from_context, read_request
+from . import schema as sc
+from .openai_routes import APIError, merge_request_with_config, model_from_context, read_request, typed_body
 
 
 def build_router(state) -> APIRouter:
@@ -66,16 +67,16 @@ def build_router(state) -> APIRouter:
 
     # ---------------------------------------------------------------- tokenize / token metrics
     async def tokenize(request: Request):
-        model, req = await read_request(request, state)
+        model, req = await read_request(request, state, schema=sc.TokenizeRequest)
         cfg = merge_request_with_config(state, model, req)
         lm = await state.manager.load(cfg)
         res = await lm.handle.TokenizeString(pb.PredictOptions(Prompt=str(req.get("content") or "")))
         return {"tokens": list(res.tokens)}
 
-    r.add_api_route("/v1/tokenize", tokenize, methods=["POST"])
+    r.add_api_route("/v1/tokenize", tokenize, methods=["POST"], openapi_extra=sc.body_doc(sc.TokenizeRequest))
 
     async def token_metrics(request: Request):
-        model, req = await read_request(request, state)
+        model, req = await read_request(request, state, schema=sc.TokenMetricsRequest)
         cfg = merge_request_with_config(state, model, req)
         lm = await state.manager.load(cfg)
         res = await lm.handle.GetMetrics(pb.MetricsRequest())
@@ -142,7 +143,7 @@ def build_router(state) -> APIRouter:
         return [pb.StoresKey(Floats=[float(x) for x in k]) for k in (ks or [])]
 
     async def stores_set(request: Request):
-        b = await request.json()
+        b = await typed_body(request, sc.StoresSet)
         keys, vals = b.get("keys") or [], b.get("values") or []
         if len(keys) != len(vals):
             raise APIError("keys and values must have the same length", 400)
@@ -154,7 +155,7 @@ def build_router(state) -> APIRouter:
         return Response(status_code=200)
 
     async def stores_delete(request: Request):
-        b = await request.json()
+        b = await typed_body(request, sc.StoresDelete)
         lm = await _store(b.get("store", ""))
         res = await lm.handle.StoresDelete(pb.StoresDeleteOptions(Keys=_keys(b.get("keys"))))
         if not res.success:
@@ -162,14 +163,14 @@ def build_router(state) -> APIRouter:
         return Response(status_code=200)
 
     async def stores_get(request: Request):
-        b = await request.json()
+        b = await typed_body(request, sc.StoresGet)
         lm = await _store(b.get("store", ""))
         res = await lm.handle.StoresGet(pb.StoresGetOptions(Keys=_keys(b.get("keys"))))
         return {"keys": [list(k.Floats) for k in res.Keys],
                 "values": [bytes(v.Bytes).decode("utf-8", "replace") for v in res.Values]}
 
     async def stores_find(request: Request):
-        b = await request.json()
+        b = await typed_body(request, sc.StoresFind)
         lm = await _store(b.get("store", ""))
         res = await lm.handle.StoresFind(pb.StoresFindOptions(Key=pb.StoresKey(Floats=b.get("key") or []),
                                                               TopK=int(b.get("topk") or 0)))
@@ -177,12 +178,13 @@ def build_router(state) -> APIRouter:
                 "values": [bytes(v.Bytes).decode("utf-8", "replace") for v in res.Values],
                 "similarities": list(res.Similarities)}
 
-    for path, fn in (("set", stores_set), ("delete", stores_delete), ("get", stores_get), ("find", stores_find)):
-        r.add_api_route(f"/stores/{path}", fn, methods=["POST"])
+    for path, fn, m in (("set", stores_set, sc.StoresSet), ("delete", stores_delete, sc.StoresDelete),
+                        ("get", stores_get, sc.StoresGet), ("find", stores_find, sc.StoresFind)):
+        r.add_api_route(f"/stores/{path}", fn, methods=["POST"], openapi_extra=sc.body_doc(m))
 
     # ---------------------------------------------------------------- rerank (Jina)
     async def rerank(request: Request):
-        model, req = await read_request(request, state)
+        model, req = await read_request(request, state, schema=sc.JINARerankRequest)
         cfg = merge_request_with_config(state, model, req)
         lm = await state.manager.load(cfg)
         res = await lm.handle.Rerank(pb.RerankRequest(query=str(req.get("query") or ""),
@@ -193,7 +195,7 @@ def build_router(state) -> APIRouter:
                 "results": [{"index": d.index, "document": {"text": d.text}, "relevance_score": d.relevance_score}
                             for d in res.results]}
 
-    r.add_api_route("/v1/rerank", rerank, methods=["POST"])
+    r.add_api_route("/v1/rerank", rerank, methods=["POST"], openapi_extra=sc.body_doc(sc.JINARerankRequest))
 
     # ---------------------------------------------------------------- TTS / sound generation
     async def _tts(model: str, backend: str, text: str, voice: str, language: str):
@@ -212,17 +214,17 @@ def build_router(state) -> APIRouter:
         return FileResponse(dst, media_type="audio/wav")
 
     async def tts(request: Request):
-        b = await request.json()
+        b = await typed_body(request, sc.TTSRequest)
         model = model_from_context(request, state, b.get("model", ""), False)
         return await _tts(model, b.get("backend", ""), b.get("input", ""), b.get("voice", ""), b.get("language", ""))
 
     async def tts_eleven(request: Request, voice_id: str):
-        b = await request.json()
+        b = await typed_body(request, sc.ElevenLabsTTSRequest)
         model = model_from_context(request, state, b.get("model_id", ""), False)
         return await _tts(model, "", b.get("text", ""), voice_id, "")
 
     async def sound_generation(request: Request):
-        b = await request.json()
+        b = await typed_body(request, sc.ElevenLabsSoundGenerationRequest)
         model = model_from_context(request, state, b.get("model_id", ""), False)
         cfg = merge_request_with_config(state, model, {"model": model})
         lm = await state.manager.load(cfg)
@@ -240,9 +242,11 @@ def build_router(state) -> APIRouter:
             raise APIError(res.message, 500)
         return FileResponse(dst, media_type="audio/wav")
 
-    r.add_api_route("/tts", tts, methods=["POST"])
-    r.add_api_route("/v1/audio/speech", tts, methods=["POST"])
-    r.add_api_route("/v1/text-to-speech/{voice_id}", tts_eleven, methods=["POST"])
-    r.add_api_route("/v1/sound-generation", sound_generation, methods=["POST"])
+    r.add_api_route("/tts", tts, methods=["POST"], openapi_extra=sc.body_doc(sc.TTSRequest))
+    r.add_api_route("/v1/audio/speech", tts, methods=["POST"], openapi_extra=sc.body_doc(sc.TTSRequest))
+    r.add_api_route("/v1/text-to-speech/{voice_id}", tts_eleven, methods=["POST"],
+                    openapi_extra=sc.body_doc(sc.ElevenLabsTTSRequest))
+    r.add_api_route("/v1/sound-generation", sound_generation, methods=["POST"],
+                    openapi_extra=sc.body_doc(sc.ElevenLabsSoundGenerationRequest))
 
     return r

@@ -20,9 +20,11 @@ from .. import functions as fn
 from ..config.backend_config import FLAG_CHAT, FLAG_COMPLETION, FLAG_EMBEDDINGS
 from ..config.loader import build_name_filter, build_usecase_filter
 from ..templates import CHAT_MESSAGE, CHAT_PROMPT, COMPLETION_PROMPT, EDIT_PROMPT
+from . import schema as sc
 from .inference import Inference, TokenUsage, finetune, update_request_config
 
 log = logging.getLogger("localai_amd.api")
+_DOC = sc.body_doc(sc.OpenAIRequest)
 
 
 def _sse(obj) -> bytes:
@@ -39,13 +41,22 @@ class APIError(Exception):
         self.code = code
 
 
-async def read_request(request: Request, state, first_model: bool = True, path_model: str = ""):
+async def typed_body(request: Request, model=sc.OpenAIRequest) -> dict:
+    """The JSON body, checked against its request struct (gateway/schema.py): a field of the
+    wrong type is a 400, as the reference's struct decoding makes it."""
     try:
         body = await request.json()
     except Exception:
         body = {}
-    if not isinstance(body, dict):
-        raise APIError("failed reading parameters from request: body must be a JSON object", 400)
+    try:
+        return sc.validate(model, body)
+    except sc.SchemaError as e:
+        raise APIError(str(e), 400)
+
+
+async def read_request(request: Request, state, first_model: bool = True, path_model: str = "",
+                       schema=sc.OpenAIRequest):
+    body = await typed_body(request, schema)
     body["_correlation_id"] = request.headers.get("X-Correlation-ID") or str(uuid.uuid4())
     model = model_from_context(request, state, body.get("model", ""), first_model, path_model)
     return model, body
@@ -305,7 +316,7 @@ def build_router(state) -> APIRouter:
                              "choices": choices, "usage": _usage(usage)}, headers=headers)
 
     for p in ("/v1/chat/completions", "/chat/completions"):
-        r.add_api_route(p, chat, methods=["POST"])
+        r.add_api_route(p, chat, methods=["POST"], openapi_extra=_DOC)
 
     # ------------------------------------------------------------------------ completion
     async def completion(request: Request, model_path: str = ""):
@@ -372,7 +383,7 @@ def build_router(state) -> APIRouter:
         return await completion(request, model_path=model)
 
     for p in ("/v1/completions", "/completions"):
-        r.add_api_route(p, completion, methods=["POST"])
+        r.add_api_route(p, completion, methods=["POST"], openapi_extra=_DOC)
     r.add_api_route("/v1/engines/{model}/completions", completion_engine, methods=["POST"])
 
     # ------------------------------------------------------------------------ edits
@@ -404,7 +415,7 @@ def build_router(state) -> APIRouter:
                              "choices": choices, "usage": _usage(usage)})
 
     for p in ("/v1/edits", "/edits"):
-        r.add_api_route(p, edit, methods=["POST"])
+        r.add_api_route(p, edit, methods=["POST"], openapi_extra=_DOC)
 
     # ------------------------------------------------------------------------ embeddings
     async def embeddings(request: Request, model_path: str = ""):
@@ -434,7 +445,7 @@ def build_router(state) -> APIRouter:
         return await embeddings(request, model_path=model)
 
     for p in ("/v1/embeddings", "/embeddings"):
-        r.add_api_route(p, embeddings, methods=["POST"])
+        r.add_api_route(p, embeddings, methods=["POST"], openapi_extra=_DOC)
     r.add_api_route("/v1/engines/{model}/embeddings", embeddings_engine, methods=["POST"])
 
     # ------------------------------------------------------------------------ models
@@ -511,7 +522,7 @@ def build_router(state) -> APIRouter:
                 out.append({"url": f"{base}/generated-images/{name}"})
         return {"created": int(time.time()), "id": str(uuid.uuid4()), "data": out}
 
-    r.add_api_route("/v1/images/generations", images, methods=["POST"])
+    r.add_api_route("/v1/images/generations", images, methods=["POST"], openapi_extra=_DOC)
     return r
 
 

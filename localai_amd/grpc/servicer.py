@@ -198,7 +198,6 @@ class EngineServicer:
         return ((adapter_path(model_path, request.LoraAdapter), float(request.LoraScale or 1.0)),)
 
     @staticmethod
-    @staticmethod
     def _draft_path(request, model_path: str) -> str:
         """DraftModel, relative to the main model's directory (reference llama.go:89-95)."""
         d = str(request.DraftModel or "")
@@ -210,6 +209,7 @@ class EngineServicer:
             raise FileNotFoundError(f"draft model {d} not found")
         return d
 
+    @staticmethod
     def _mmproj_path(request, model_path: str) -> str:
         mm = request.MMProj
         if not mm:

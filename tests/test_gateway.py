@@ -189,6 +189,34 @@ def test_metrics_endpoint(client):
     assert "api_call" in txt and "localai_output_tokens_total" in txt
 
 
+def test_typed_request_schema(client):
+    """Bodies are checked against the reference's request structs (core/schema): a field of the
+    wrong JSON type is a 400 naming the field; unknown fields and nulls pass; /swagger's OpenAPI
+    document carries the typed bodies."""
+    m = client.model_name
+    r = client.post("/v1/chat/completions", json={"model": m, "temperature": "hot",
+                                                 "messages": [{"role": "user", "content": "hi"}]})
+    assert r.status_code == 400 and "temperature" in r.json()["error"]["message"]
+    r = client.post("/v1/chat/completions", json={"model": m, "messages": [{"role": 7, "content": "hi"}]})
+    assert r.status_code == 400 and "messages.0.role" in r.json()["error"]["message"]
+    r = client.post("/v1/completions", json={"model": m, "prompt": "x", "max_tokens": {"n": 3}})
+    assert r.status_code == 400 and "max_tokens" in r.json()["error"]["message"]
+    r = client.post("/v1/chat/completions", json={"model": m, "max_tokens": 2, "temperature": 0, "top_k": None,
+                                                 "some_future_field": {"x": 1},
+                                                 "messages": [{"role": "user", "content": [{"type": "text", "text": "hi"}]}]})
+    assert r.status_code == 200, r.text
+    r = client.post("/stores/find", json={"key": "not-a-vector"})
+    assert r.status_code == 400
+    r = client.post("/v1/tokenize", json={"model": m, "content": 42})
+    assert r.status_code == 400 and "content" in r.json()["error"]["message"]
+    spec = client.get("/swagger/doc.json").json()
+    chat = spec["paths"]["/v1/chat/completions"]["post"]["requestBody"]["content"]["application/json"]["schema"]
+    assert "messages" in chat["properties"] and "temperature" in chat["properties"]
+    tts = spec["paths"]["/tts"]["post"]["requestBody"]["content"]["application/json"]["schema"]
+    assert set(tts["properties"]) >= {"model", "input", "voice", "backend", "language"}
+    assert "$ref" not in json.dumps(chat)
+
+
 def test_api_key_auth(engine, tmp_path_factory):
     from fastapi.testclient import TestClient
     from localai_amd.gateway.app import create_app_for_engine
@@ -236,3 +264,4 @@ def test_browse_page_escapes_gallery_names(engine, tmp_path_factory):
     assert "fetch(&#x27;/evil&#x27;)" in page, page[page.find("<main>"):][:600]  # escaped attribute text only
     assert "install(this)" in page and "install('" not in page
     assert "onclick=\"install" not in page
+
