@@ -1,4 +1,4 @@
-"""Stable Diffusion 1.x / 2.x text-to-image, served by the `diffusers` / `stablediffusion`
+"""Stable Diffusion 1.x / 2.x / XL text-to-image, served by the `diffusers` / `stablediffusion`
 backends (reference: `backend/python/diffusers/backend.py:147-471` -- LoadModel keeps
 `CFGScale` (default 7), `CLIPSkip`, `SchedulerType`; GenerateImage takes `step` (default 1),
 width / height, `negative_prompt`, `seed` and `EnableParameters`, runs the pipeline and saves a
@@ -103,18 +103,40 @@ class ClipTextEncoder(nn.Module):
                                                      c.get("hidden_act", "quick_gelu"))
                                           for _ in range(c["num_hidden_layers"]))
         tm.final_layer_norm = nn.LayerNorm(d)
+        self.eos_id = int(c.get("eos_token_id", 2))
+        if c.get("projection_dim") and "CLIPTextModelWithProjection" in (c.get("architectures") or []):
+            # SDXL's second encoder: the pooled (EOS) state through text_projection
+            self.text_projection = nn.Linear(d, int(c["projection_dim"]), bias=False)
         for m in self.modules():
             if isinstance(m, nn.LayerNorm):
                 m.eps = self.eps
 
-    def forward(self, ids: torch.Tensor, clip_skip: int = 0) -> torch.Tensor:
+    def _run(self, ids: torch.Tensor, n_layers: int) -> torch.Tensor:
         tm = self.text_model
         x = tm.embeddings.token_embedding(ids) + tm.embeddings.position_embedding.weight[: ids.shape[1]]
-        layers = tm.encoder.layers
-        # diffusers' clip_skip: the hidden state `clip_skip` layers before the last, then final LN
-        for ly in layers[: len(layers) - clip_skip]:
+        for ly in tm.encoder.layers[:n_layers]:
             x = ly(x)
-        return tm.final_layer_norm(x)
+        return x
+
+    def forward(self, ids: torch.Tensor, clip_skip: int = 0) -> torch.Tensor:
+        # diffusers' clip_skip: the hidden state `clip_skip` layers before the last, then final LN
+        return self.text_model.final_layer_norm(self._run(ids, len(self.text_model.encoder.layers) - clip_skip))
+
+    def sdxl(self, ids: torch.Tensor, clip_skip: int = 0, pooled: bool = False):
+        """SDXL conditioning: hidden_states[-(clip_skip + 2)] (no final LN) and, for the
+        projection encoder, the final-LN state at the first EOS token through text_projection
+        (transformers CLIPTextModelWithProjection.text_embeds)."""
+        n = len(self.text_model.encoder.layers)
+        h = self._run(ids, n - 1)
+        pen = self._run(ids, n - 1 - clip_skip) if clip_skip else h
+        if not pooled:
+            return pen, None
+        fin = self.text_model.final_layer_norm(self.text_model.encoder.layers[n - 1](h))
+        eos = (ids == self.eos_id).int().argmax(-1)
+        pool = fin[torch.arange(ids.shape[0], device=ids.device), eos]
+        if hasattr(self, "text_projection"):
+            pool = self.text_projection(pool)
+        return pen, pool
 
 
 # ------------------------------------------------------------------ UNet / VAE building blocks
@@ -198,12 +220,12 @@ class _TBlock(nn.Module):
 
 
 class _Transformer2D(nn.Module):
-    def __init__(self, c: int, heads: int, ctx: int, groups: int, linear_proj: bool):
+    def __init__(self, c: int, heads: int, ctx: int, groups: int, linear_proj: bool, depth: int = 1):
         super().__init__()
         self.linear = linear_proj
         self.norm = nn.GroupNorm(groups, c, eps=1e-6)
         self.proj_in = nn.Linear(c, c) if linear_proj else nn.Conv2d(c, c, 1)
-        self.transformer_blocks = nn.ModuleList([_TBlock(c, heads, ctx)])
+        self.transformer_blocks = nn.ModuleList([_TBlock(c, heads, ctx) for _ in range(depth)])
         self.proj_out = nn.Linear(c, c) if linear_proj else nn.Conv2d(c, c, 1)
 
     def forward(self, x, ctx):
@@ -265,6 +287,9 @@ class UNet(nn.Module):
         # diffusers: `attention_head_dim` holds the number of heads when num_attention_heads is unset
         heads = _per_block(c.get("num_attention_heads") or c.get("attention_head_dim", 8), n)
         lin = bool(c.get("use_linear_projection", False))
+        # SDXL: several transformer blocks per attention (transformer_layers_per_block, e.g. 1/2/10)
+        depth = _per_block(c.get("transformer_layers_per_block", 1), n)
+        rdepth = c.get("reverse_transformer_layers_per_block")
         self.flip = bool(c.get("flip_sin_to_cos", True))
         self.shift = float(c.get("freq_shift", 0))
         temb = ch[0] * 4
@@ -272,12 +297,22 @@ class UNet(nn.Module):
         self.time_embedding = nn.Module()
         self.time_embedding.linear_1 = nn.Linear(ch[0], temb)
         self.time_embedding.linear_2 = nn.Linear(temb, temb)
+        # SDXL micro-conditioning (addition_embed_type "text_time"): sinusoidal embeddings of the 6
+        # size / crop time ids, concatenated with the pooled text embedding, through add_embedding
+        self.text_time = c.get("addition_embed_type") == "text_time"
+        if self.text_time:
+            self.add_time_dim = int(c["addition_time_embed_dim"])
+            self.add_embedding = nn.Module()
+            self.add_embedding.linear_1 = nn.Linear(int(c["projection_class_embeddings_input_dim"]), temb)
+            self.add_embedding.linear_2 = nn.Linear(temb, temb)
+        elif c.get("addition_embed_type"):
+            raise ValueError(f"unsupported UNet addition_embed_type {c.get('addition_embed_type')!r}")
         downs, prev = [], ch[0]
         for i, t in enumerate(c["down_block_types"]):
             b = nn.Module()
             b.resnets = nn.ModuleList(_Resnet(prev if j == 0 else ch[i], ch[i], g, eps, temb) for j in range(lpb))
             if "CrossAttn" in t:
-                b.attentions = nn.ModuleList(_Transformer2D(ch[i], heads[i], ctx, g, lin) for _ in range(lpb))
+                b.attentions = nn.ModuleList(_Transformer2D(ch[i], heads[i], ctx, g, lin, depth[i]) for _ in range(lpb))
             if i < n - 1:
                 b.downsamplers = nn.ModuleList([_Down(ch[i])])
             downs.append(b)
@@ -285,8 +320,9 @@ class UNet(nn.Module):
         self.down_blocks = nn.ModuleList(downs)
         self.mid_block = nn.Module()
         self.mid_block.resnets = nn.ModuleList([_Resnet(ch[-1], ch[-1], g, eps, temb) for _ in range(2)])
-        self.mid_block.attentions = nn.ModuleList([_Transformer2D(ch[-1], heads[-1], ctx, g, lin)])
+        self.mid_block.attentions = nn.ModuleList([_Transformer2D(ch[-1], heads[-1], ctx, g, lin, depth[-1])])
         rch, rheads = ch[::-1], heads[::-1]
+        rdep = _per_block(rdepth, n) if rdepth is not None else depth[::-1]
         ups, prev = [], ch[-1]
         for i, t in enumerate(c["up_block_types"]):
             out, skip_in = rch[i], rch[min(i + 1, n - 1)]
@@ -295,7 +331,7 @@ class UNet(nn.Module):
                 _Resnet((prev if j == 0 else out) + (skip_in if j == lpb else out), out, g, eps, temb)
                 for j in range(lpb + 1))
             if "CrossAttn" in t:
-                b.attentions = nn.ModuleList(_Transformer2D(out, rheads[i], ctx, g, lin) for _ in range(lpb + 1))
+                b.attentions = nn.ModuleList(_Transformer2D(out, rheads[i], ctx, g, lin, rdep[i]) for _ in range(lpb + 1))
             if i < n - 1:
                 b.upsamplers = nn.ModuleList([_Up(out)])
             ups.append(b)
@@ -305,16 +341,23 @@ class UNet(nn.Module):
         self.conv_out = nn.Conv2d(ch[0], c.get("out_channels", 4), 3, padding=1)
         self.ch0 = ch[0]
 
-    def _tproj(self, t: torch.Tensor) -> torch.Tensor:
-        half = self.ch0 // 2
+    def _tproj(self, t: torch.Tensor, dim: int = 0) -> torch.Tensor:
+        half = (dim or self.ch0) // 2
         f = torch.exp(-math.log(10000) * torch.arange(half, dtype=torch.float32, device=t.device) / (half - self.shift))
         e = t.float()[:, None] * f[None]
         e = torch.cat([torch.cos(e), torch.sin(e)] if self.flip else [torch.sin(e), torch.cos(e)], dim=-1)
         return e
 
-    def forward(self, x, t, ctx):
+    def forward(self, x, t, ctx, text_embeds=None, time_ids=None):
         temb = self._tproj(t).to(x.dtype)
         temb = self.time_embedding.linear_2(F.silu(self.time_embedding.linear_1(temb)))
+        if self.text_time:
+            if text_embeds is None or time_ids is None:
+                raise ValueError("this UNet (SDXL) needs text_embeds and time_ids")
+            B = x.shape[0]
+            tid = self._tproj(time_ids.reshape(-1), self.add_time_dim).reshape(B, -1)
+            a = torch.cat([text_embeds.to(x.dtype), tid.to(x.dtype)], dim=-1)
+            temb = temb + self.add_embedding.linear_2(F.silu(self.add_embedding.linear_1(a)))
         h = self.conv_in(x)
         skips = [h]
         for b in self.down_blocks:
@@ -533,11 +576,13 @@ class StableDiffusion:
         self.channels_last = channels_last and self.device.type == "cuda"
         self.dtype = torch.bfloat16 if self.device.type == "cuda" else torch.float32
         self.clip_skip = clip_skip
-        self.text = ClipTextEncoder(_cfg(os.path.join(path, "text_encoder", "config.json")))
-        # transformers 4 keeps the `text_model.` prefix, transformers 5 drops it
-        self.text.load_state_dict({(k if k.startswith("text_model.") else "text_model." + k): v
-                                   for k, v in _load_weights(os.path.join(path, "text_encoder")).items()
-                                   if "position_ids" not in k}, strict=True)
+        self.text = self._load_text(os.path.join(path, "text_encoder"))
+        # SDXL: a second (OpenCLIP bigG, projected) text encoder; prompt embeddings are the two
+        # encoders' penultimate states side by side, the pooled projection conditions add_embedding
+        self.xl = os.path.isdir(os.path.join(path, "text_encoder_2"))
+        self.text2 = self._load_text(os.path.join(path, "text_encoder_2")) if self.xl else None
+        mi = os.path.join(path, "model_index.json")
+        self.zero_neg = bool((_cfg(mi) if os.path.isfile(mi) else {}).get("force_zeros_for_empty_prompt", True))
         ucfg = _cfg(os.path.join(path, "unet", "config.json"))
         self.unet_sample_size = int(ucfg.get("sample_size", 64))
         self.unet = UNet(ucfg)
@@ -552,8 +597,11 @@ class StableDiffusion:
             self.vae_enc = VaeEncoder(vcfg)
             self.vae_enc.load_state_dict(enc, strict=True)
             self.vae_enc.to(self.device, self.dtype).eval().requires_grad_(False)
-        for m in (self.text, self.unet, self.vae):
-            m.to(self.device, self.dtype).eval().requires_grad_(False)
+        for m in (self.text, self.text2, self.unet, self.vae):
+            if m is not None:
+                m.to(self.device, self.dtype).eval().requires_grad_(False)
+        if self.xl and not self.unet.text_time:
+            raise ValueError("SDXL pipeline (text_encoder_2) with a UNet lacking text_time conditioning")
         if self.channels_last:
             self.unet.to(memory_format=torch.channels_last)
             self.vae.to(memory_format=torch.channels_last)
@@ -567,6 +615,7 @@ class StableDiffusion:
         self.pred = self.sched_cfg.get("prediction_type", "epsilon")
         from transformers import CLIPTokenizer
         self.tok = CLIPTokenizer.from_pretrained(os.path.join(path, "tokenizer"))
+        self.tok2 = CLIPTokenizer.from_pretrained(os.path.join(path, "tokenizer_2")) if self.xl else None
         self.max_len = self.text.text_model.embeddings.position_embedding.weight.shape[0]
         self.latent_ch = self.unet.conv_in.in_channels
         # one hipGraph per (batch, latent size) replays the whole UNet step (~1300 launches)
@@ -577,7 +626,18 @@ class StableDiffusion:
         self.graph_cache = max(0, int(os.environ.get("LOCALAI_AMD_SD_GRAPH_CACHE", "4")))
         self.vae_scale = 2 ** (len(self.vae.decoder.up_blocks) - 1)
 
-    def _unet(self, x: torch.Tensor, t: torch.Tensor, ctx: torch.Tensor) -> torch.Tensor:
+    @staticmethod
+    def _load_text(d: str) -> ClipTextEncoder:
+        te = ClipTextEncoder(_cfg(os.path.join(d, "config.json")))
+        # transformers 4 keeps the `text_model.` prefix, transformers 5 drops it
+        te.load_state_dict({(k if k.startswith(("text_model.", "text_projection")) else "text_model." + k): v
+                            for k, v in _load_weights(d).items() if "position_ids" not in k}, strict=True)
+        return te
+
+    def _unet(self, x: torch.Tensor, t: torch.Tensor, ctx: torch.Tensor, add=None) -> torch.Tensor:
+        """add: SDXL (text_embeds, time_ids) or None."""
+        if add is not None:
+            return self._unet_xl(x, t, ctx, add)
         if not self.use_graphs:
             return self.unet(x, t, ctx)
         key = (tuple(x.shape), tuple(ctx.shape))
@@ -610,19 +670,71 @@ class StableDiffusion:
         graph.replay()
         return so.clone()
 
+    def _unet_xl(self, x, t, ctx, add):
+        """SDXL step: the same graph cache, with the pooled text embeds and time ids as two more
+        static inputs of the captured graph."""
+        te, ti = add
+        if not self.use_graphs:
+            return self.unet(x, t, ctx, te, ti)
+        key = ("xl", tuple(x.shape), tuple(ctx.shape), tuple(te.shape))
+        g = self._graphs.get(key)
+        if g is None:
+            out = self.unet(x, t, ctx, te, ti)
+            if self.graph_cache == 0:
+                return out
+            while len(self._graphs) >= self.graph_cache:
+                _, old = self._graphs.popitem(last=False)
+                del old
+                torch.cuda.empty_cache()
+            try:
+                st = tuple(v.clone() for v in (x, t, ctx, te, ti))
+                graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(graph):
+                    so = self.unet(*st)
+                self._graphs[key] = (graph, st, so)
+            except Exception as e:  # noqa: BLE001
+                import logging
+                logging.getLogger(__name__).warning("sd: SDXL UNet graph capture failed (%r); running eager", e)
+                self.use_graphs = False
+            return out
+        self._graphs.move_to_end(key)
+        graph, st, so = g
+        for dst, src in zip(st, (x, t, ctx, te, ti)):
+            dst.copy_(src)
+        graph.replay()
+        return so.clone()
+
     def _encode(self, prompts: List[str]) -> torch.Tensor:
         ids = self.tok(prompts, padding="max_length", max_length=self.max_len, truncation=True,
                        return_tensors="pt").input_ids.to(self.device)
         return self.text(ids, self.clip_skip)
 
-    def _eps(self, x: torch.Tensor, t: float, ctx: torch.Tensor, cfg: bool, guidance_scale: float) -> torch.Tensor:
+    def _encode_xl(self, prompts: List[str]):
+        """SDXL: (prompt embeds [B, 77, d1 + d2], pooled projection [B, p]); an empty prompt is all
+        zeros when the pipeline sets force_zeros_for_empty_prompt (diffusers encode_prompt)."""
+        outs = []
+        for tok, te, pooled in ((self.tok, self.text, False), (self.tok2, self.text2, True)):
+            ids = tok(prompts, padding="max_length", max_length=self.max_len, truncation=True,
+                      return_tensors="pt").input_ids.to(self.device)
+            outs.append(te.sdxl(ids, self.clip_skip, pooled))
+        ctx = torch.cat([outs[0][0], outs[1][0]], dim=-1)
+        pool = outs[1][1]
+        if self.zero_neg:
+            for i, p in enumerate(prompts):
+                if p == "" and len(prompts) > 1 and i == 0:  # the negative branch of CFG
+                    ctx[i] = 0
+                    pool[i] = 0
+        return ctx, pool
+
+    def _eps(self, x: torch.Tensor, t: float, ctx: torch.Tensor, cfg: bool, guidance_scale: float,
+             add=None) -> torch.Tensor:
         """Model output (eps or v) at timestep t with classifier-free guidance as one batch of 2."""
         xin = torch.cat([x, x]) if cfg else x
         tt = torch.full((xin.shape[0],), float(t), device=self.device)
         xin = xin.to(self.dtype)
         if self.channels_last:
             xin = xin.contiguous(memory_format=torch.channels_last)
-        out = self._unet(xin, tt, ctx).float()
+        out = self._unet(xin, tt, ctx, add).float()
         if cfg:
             u, c = out.chunk(2)
             out = u + guidance_scale * (c - u)
@@ -654,7 +766,15 @@ class StableDiffusion:
             width, height = im.size
         h, w = max(1, height // self.vae_scale), max(1, width // self.vae_scale)
         cfg = guidance_scale > 1.0
-        ctx = self._encode([negative_prompt, prompt] if cfg else [prompt])
+        prompts = [negative_prompt, prompt] if cfg else [prompt]
+        add = None
+        if self.xl:
+            ctx, pool = self._encode_xl(prompts)
+            H, W = h * self.vae_scale, w * self.vae_scale   # original = target size, no crop
+            tid = torch.tensor([[H, W, 0, 0, H, W]] * len(prompts), dtype=torch.float32, device=self.device)
+            add = (pool, tid)
+        else:
+            ctx = self._encode(prompts)
         steps = max(1, steps)
         x0 = self._init_latents(image, w, h, g) if image is not None else None
         # img2img: skip the first (1 - strength) of the schedule (diffusers get_timesteps)
@@ -669,7 +789,7 @@ class StableDiffusion:
 
             def denoise(xv, sigma):
                 c_in = 1.0 / math.sqrt(sigma * sigma + 1.0)
-                out = self._eps(xv * c_in, ks.sched.sigma_to_t(sigma), ctx, cfg, guidance_scale)
+                out = self._eps(xv * c_in, ks.sched.sigma_to_t(sigma), ctx, cfg, guidance_scale, add)
                 if self.pred == "v_prediction":
                     return xv / (sigma * sigma + 1.0) - out * (sigma * c_in)
                 return xv - sigma * out
@@ -680,12 +800,12 @@ class StableDiffusion:
             ts = ts[skip:] if skip else ts
             x = noise if x0 is None else self._add_noise(x0, noise, ts[0])
             for t in ts:
-                x = self.plms.step(self._eps(x, t, ctx, cfg, guidance_scale), t, x)
+                x = self.plms.step(self._eps(x, t, ctx, cfg, guidance_scale, add), t, x)
         else:
             ts = self.sched.timesteps(steps)[skip:]
             x = noise if x0 is None else self._add_noise(x0, noise, ts[0])
             for i, t in enumerate(ts):
-                out = self._eps(x, t, ctx, cfg, guidance_scale)
+                out = self._eps(x, t, ctx, cfg, guidance_scale, add)
                 x = self.sched.step(out, t, ts[i + 1] if i + 1 < len(ts) else None, x)
         img = self.vae(x.to(self.dtype)).float()
         img = ((img[0] / 2 + 0.5).clamp(0, 1) * 255).round().to(torch.uint8)

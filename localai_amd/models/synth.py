@@ -819,6 +819,17 @@ SD15_VAE = dict(block_out_channels=[128, 256, 512, 512], layers_per_block=2, lat
                 in_channels=3, out_channels=3, scaling_factor=0.18215)
 SD15_TEXT = dict(hidden_size=768, num_hidden_layers=12, num_attention_heads=12, intermediate_size=3072,
                  vocab_size=49408, max_position_embeddings=77, hidden_act="quick_gelu")
+# Stable Diffusion XL base 1.0 (diffusers configs): 2.6 B-parameter UNet, CLIP-L + OpenCLIP bigG
+SDXL_UNET = dict(block_out_channels=[320, 640, 1280], layers_per_block=2, cross_attention_dim=2048,
+                 attention_head_dim=[5, 10, 20], transformer_layers_per_block=[1, 2, 10], norm_num_groups=32,
+                 in_channels=4, out_channels=4, sample_size=128, use_linear_projection=True,
+                 down_block_types=["DownBlock2D", "CrossAttnDownBlock2D", "CrossAttnDownBlock2D"],
+                 up_block_types=["CrossAttnUpBlock2D", "CrossAttnUpBlock2D", "UpBlock2D"],
+                 addition_embed_type="text_time", addition_time_embed_dim=256,
+                 projection_class_embeddings_input_dim=2816, flip_sin_to_cos=True, freq_shift=0)
+SDXL_VAE = dict(SD15_VAE, scaling_factor=0.13025, sample_size=1024)
+SDXL_TEXT2 = dict(hidden_size=1280, num_hidden_layers=32, num_attention_heads=20, intermediate_size=5120,
+                  vocab_size=49408, max_position_embeddings=77, hidden_act="gelu", projection_dim=1280)
 
 
 def _clip_byte_vocab():
@@ -838,15 +849,34 @@ def _clip_byte_vocab():
 
 def write_sd_pipeline(out_dir: str, size: str = "tiny", seed: int = 0, v_prediction: bool = False) -> str:
     """Random-init Stable Diffusion pipeline directory in the diffusers layout (model_index.json,
-    unet/, vae/, text_encoder/ (transformers CLIPTextModel), tokenizer/, scheduler/).
-    size="sd15": the SD-1.5 architecture (860M-parameter UNet); "tiny": a two-level toy."""
+    unet/, vae/, text_encoder/ (transformers CLIPTextModel), tokenizer/, scheduler/; SDXL adds
+    text_encoder_2/ (CLIPTextModelWithProjection) and tokenizer_2/).
+    size="sd15": the SD-1.5 architecture (860M-parameter UNet); "sdxl": SDXL base 1.0;
+    "tiny": a two-level toy; "tiny-xl": a two-level SDXL-shaped toy."""
     import torch
     import transformers as tf
     from safetensors.torch import save_file
 
     from .sd import UNet, VaeDecoder, VaeEncoder
+    xl = size in ("sdxl", "tiny-xl")
+    tc2 = None
     if size == "sd15":
         uc, vc, tc = dict(SD15_UNET), dict(SD15_VAE), dict(SD15_TEXT)
+    elif size == "sdxl":
+        uc, vc, tc, tc2 = dict(SDXL_UNET), dict(SDXL_VAE), dict(SD15_TEXT), dict(SDXL_TEXT2)
+    elif size == "tiny-xl":
+        vocab = _clip_byte_vocab()
+        sp = dict(vocab_size=len(vocab), bos_token_id=vocab["<|startoftext|>"], eos_token_id=vocab["<|endoftext|>"],
+                  pad_token_id=vocab["<|endoftext|>"])
+        tc = dict(SD15_TEXT, hidden_size=32, num_hidden_layers=2, num_attention_heads=2, intermediate_size=64, **sp)
+        tc2 = dict(SDXL_TEXT2, hidden_size=48, num_hidden_layers=3, num_attention_heads=2, intermediate_size=96,
+                   projection_dim=16, **sp)
+        uc = dict(SDXL_UNET, block_out_channels=[32, 64], layers_per_block=1, cross_attention_dim=32 + 48,
+                  attention_head_dim=[2, 4], transformer_layers_per_block=[1, 2], norm_num_groups=8, sample_size=8,
+                  down_block_types=["DownBlock2D", "CrossAttnDownBlock2D"],
+                  up_block_types=["CrossAttnUpBlock2D", "UpBlock2D"], addition_time_embed_dim=8,
+                  projection_class_embeddings_input_dim=16 + 6 * 8)
+        vc = dict(SDXL_VAE, block_out_channels=[16, 32], layers_per_block=1, norm_num_groups=8)
     else:
         uc = dict(SD15_UNET, block_out_channels=[32, 64], layers_per_block=1, cross_attention_dim=32,
                   attention_head_dim=[2, 4], norm_num_groups=8, sample_size=8,
@@ -860,13 +890,14 @@ def write_sd_pipeline(out_dir: str, size: str = "tiny", seed: int = 0, v_predict
     if v_prediction:
         uc["use_linear_projection"] = True
     torch.manual_seed(seed)
-    for sub in ("unet", "vae", "text_encoder", "tokenizer", "scheduler"):
+    subs = ["unet", "vae", "text_encoder", "tokenizer", "scheduler"] + (["text_encoder_2", "tokenizer_2"] if xl else [])
+    for sub in subs:
         os.makedirs(os.path.join(out_dir, sub), exist_ok=True)
     for sub, cls, c in (("unet", UNet, uc), ("vae", VaeDecoder, vc)):
         m = cls(c)
         with open(os.path.join(out_dir, sub, "config.json"), "w") as f:
             json.dump(dict(c, _class_name="UNet2DConditionModel" if sub == "unet" else "AutoencoderKL"), f)
-        dt = torch.bfloat16 if size == "sd15" else torch.float32  # halves the 3.4 GB SD-1.5 UNet file
+        dt = torch.bfloat16 if size in ("sd15", "sdxl") else torch.float32  # halves the multi-GB UNet files
         sd = m.state_dict()
         if sub == "vae":  # the full AutoencoderKL: the encoder half too (img2img)
             sd.update(VaeEncoder(c).state_dict())
@@ -874,16 +905,23 @@ def write_sd_pipeline(out_dir: str, size: str = "tiny", seed: int = 0, v_predict
                   os.path.join(out_dir, sub, "diffusion_pytorch_model.safetensors"))
     te = tf.CLIPTextModel(tf.CLIPTextConfig(**tc))
     te.save_pretrained(os.path.join(out_dir, "text_encoder"), safe_serialization=True)
+    if tc2 is not None:
+        te2 = tf.CLIPTextModelWithProjection(tf.CLIPTextConfig(**tc2))
+        if size == "sdxl":
+            te2 = te2.to(torch.bfloat16)
+        te2.save_pretrained(os.path.join(out_dir, "text_encoder_2"), safe_serialization=True)
     vocab = _clip_byte_vocab()
-    with open(os.path.join(out_dir, "tokenizer", "vocab.json"), "w") as f:
-        json.dump(vocab, f)
-    with open(os.path.join(out_dir, "tokenizer", "merges.txt"), "w") as f:
-        f.write("#version: 0.2\n")
+    for tk in ("tokenizer", "tokenizer_2") if xl else ("tokenizer",):
+        with open(os.path.join(out_dir, tk, "vocab.json"), "w") as f:
+            json.dump(vocab, f)
+        with open(os.path.join(out_dir, tk, "merges.txt"), "w") as f:
+            f.write("#version: 0.2\n")
     with open(os.path.join(out_dir, "scheduler", "scheduler_config.json"), "w") as f:
         json.dump({"_class_name": "DDIMScheduler", "beta_start": 0.00085, "beta_end": 0.012,
                    "beta_schedule": "scaled_linear", "num_train_timesteps": 1000, "steps_offset": 1,
                    "set_alpha_to_one": False, "clip_sample": False,
                    "prediction_type": "v_prediction" if v_prediction else "epsilon"}, f)
     with open(os.path.join(out_dir, "model_index.json"), "w") as f:
-        json.dump({"_class_name": "StableDiffusionPipeline"}, f)
+        json.dump({"_class_name": "StableDiffusionXLPipeline", "force_zeros_for_empty_prompt": True} if xl
+                  else {"_class_name": "StableDiffusionPipeline"}, f)
     return out_dir
