@@ -40,7 +40,7 @@ STORE_BACKEND = "local-store"
 HF_BACKENDS = {"huggingface", "langchain-huggingface"}  # remote Inference API (grpc/huggingface.py)
 MAMBA_BACKEND = "mamba"  # selective state-space LMs (models/mamba.py, ops/csrc/mamba.hip)
 RWKV_BACKEND = "rwkv"    # RWKV-4 recurrent LMs (models/rwkv.py)
-SD_BACKENDS = {"diffusers", "stablediffusion"}  # Stable Diffusion 1.x / 2.x pipelines (models/sd.py)
+SD_BACKENDS = {"diffusers", "stablediffusion", "tinydream"}  # Stable Diffusion 1.x / 2.x / XL pipelines (models/sd.py)
 VITS_BACKENDS = {"piper", "vits", "mms-tts"}    # VITS text-to-speech voices (models/tts.py)
 MUSICGEN_BACKENDS = {"transformers-musicgen", "musicgen"}  # text-to-music (models/musicgen.py)
 BARK_BACKENDS = {"bark"}                         # text-to-speech/audio (models/bark.py)

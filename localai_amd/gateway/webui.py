@@ -1,6 +1,9 @@
 """Built-in web UI (`core/http/routes/ui.go:87-432`, `core/http/views/*.html` -- behaviour, not
-assets): home page with the installed models, model gallery browser with install/delete and
-job progress, streaming chat, text-to-speech and text-to-image pages.
+assets): home page with the installed models (loaded state, backend monitor, unload), model
+gallery browser with search, install/delete and job progress, streaming chat (system prompt,
+sampling knobs, image attachments for vision models, code blocks), text-to-speech (voice /
+backend), text-to-image (size, steps, seed, negative prompt, result gallery), sound generation
+and the push-to-talk loop; the P2P page lives with the p2p routes (gateway/p2p.py).
 
 Self-contained HTML + vanilla JS served by the gateway (no build step, no CDN: the server may
 run air-gapped).  Every page talks to the public REST API (/v1/chat/completions with SSE,
@@ -30,10 +33,14 @@ button{cursor:pointer}button:hover{background:#2b3242}
 #log{white-space:pre-wrap;background:#151821;border:1px solid #2a2f3a;border-radius:8px;padding:1em;min-height:260px}
 .u{color:#8ab4ff}.a{color:#e6e6e6}.muted{color:#8a93a5;font-size:.9em}
 .row{display:flex;gap:.6em;margin:.8em 0}.row>*{flex:1}.row>button,.row>select{flex:0 0 auto}
+pre.code{background:#0b0d12;border:1px solid #2a2f3a;border-radius:6px;padding:.6em;overflow-x:auto}
+.grid{display:grid;grid-template-columns:repeat(auto-fill,minmax(220px,1fr));gap:.8em}.grid img{width:100%;border-radius:6px}
+label{color:#8a93a5;font-size:.9em;align-self:center}
 """
 
 _NAV = ('<header><b>LocalAI · MI355X</b><a href="/">Home</a><a href="/browse">Models</a>'
         '<a href="/chat/">Chat</a><a href="/tts/">TTS</a><a href="/text2image/">Text→Image</a>'
+        '<a href="/sound/">Sound</a><a href="/talk/">Talk</a><a href="/p2p">P2P</a>'
         '<a href="/swagger">API</a></header>')
 
 
@@ -55,15 +62,31 @@ function hdrs(){const h={'Content-Type':'application/json'}; if(KEY) h['Authoriz
 
 _CHAT_JS = _AUTH_JS + """
 const log = document.getElementById('log'), inp = document.getElementById('msg');
-const history = [];
+let history = [], image = null;
 function add(cls, text){const d=document.createElement('div'); d.className=cls; d.textContent=text; log.appendChild(d); return d;}
+// fenced code blocks of a reply as <pre> elements; everything stays text (no HTML injection)
+function render(el, text){
+  el.textContent = ''; const parts = text.split('```');
+  parts.forEach((p, i) => { const n = document.createElement(i % 2 ? 'pre' : 'span');
+    n.textContent = i % 2 ? p.replace(/^[a-zA-Z0-9_+-]*\n/, '') : p; if(i % 2) n.className = 'code'; el.appendChild(n); });
+}
+function num(id){ const v = document.getElementById(id).value; return v === '' ? undefined : parseFloat(v); }
+function clearChat(){ history = []; log.textContent = ''; image = null; document.getElementById('img').value = ''; }
+document.getElementById('img').addEventListener('change', e => {
+  const f = e.target.files[0]; if(!f) { image = null; return; }
+  const r = new FileReader(); r.onload = () => { image = r.result; }; r.readAsDataURL(f);
+});
 async function send(){
   const text = inp.value.trim(); if(!text) return; inp.value='';
-  history.push({role:'user', content:text}); add('u', '> '+text);
+  const sys = document.getElementById('sys').value.trim();
+  const content = image ? [{type:'text', text}, {type:'image_url', image_url:{url:image}}] : text;
+  history.push({role:'user', content}); add('u', '> ' + text + (image ? '  [image]' : ''));
+  image = null; document.getElementById('img').value = '';
+  const msgs = sys ? [{role:'system', content:sys}].concat(history) : history;
   const out = add('a', ''); const t0 = performance.now(); let first = 0, n = 0;
   const res = await fetch('/v1/chat/completions', {method:'POST', headers:hdrs(), body: JSON.stringify({
-    model: document.getElementById('model').value, messages: history, stream: true,
-    temperature: parseFloat(document.getElementById('temp').value)})});
+    model: document.getElementById('model').value, messages: msgs, stream: true,
+    temperature: num('temp'), top_p: num('topp'), max_tokens: num('maxt') && Math.round(num('maxt'))})});
   if(!res.ok){out.textContent = 'error: ' + res.status + ' ' + await res.text(); return;}
   const rd = res.body.getReader(), dec = new TextDecoder(); let buf = '', full = '';
   for(;;){
@@ -74,7 +97,7 @@ async function send(){
       if(!line.startsWith('data:')) continue; const data = line.slice(5).trim();
       if(data === '[DONE]') continue;
       try{const j = JSON.parse(data); const d = (j.choices && j.choices[0].delta) || {};
-          if(d.content){ if(!first) first = performance.now(); n++; full += d.content; out.textContent = full; }}catch(e){}
+          if(d.content){ if(!first) first = performance.now(); n++; full += d.content; render(out, full); }}catch(e){}
     }
   }
   history.push({role:'assistant', content: full});
@@ -110,8 +133,10 @@ function filter(){const q = document.getElementById('q').value.toLowerCase();
 
 _TTS_JS = _AUTH_JS + """
 async function speak(){
-  const r = await fetch('/tts', {method:'POST', headers:hdrs(), body: JSON.stringify({
-    model: document.getElementById('model').value, input: document.getElementById('txt').value})});
+  const body = {model: document.getElementById('model').value, input: document.getElementById('txt').value};
+  const v = document.getElementById('voice').value, b = document.getElementById('backend').value;
+  if(v) body.voice = v; if(b) body.backend = b;
+  const r = await fetch('/tts', {method:'POST', headers:hdrs(), body: JSON.stringify(body)});
   if(!r.ok){document.getElementById('st').textContent = 'error: ' + r.status + ' ' + await r.text(); return;}
   const a = document.getElementById('audio'); a.src = URL.createObjectURL(await r.blob()); a.play();
 }
@@ -120,12 +145,39 @@ async function speak(){
 _IMG_JS = _AUTH_JS + """
 async function gen(){
   const st = document.getElementById('st'); st.textContent = 'generating...';
+  // the reference's prompt syntax: "positive|negative"
+  const neg = document.getElementById('neg').value.trim(), pos = document.getElementById('txt').value;
+  const t0 = performance.now();
   const r = await fetch('/v1/images/generations', {method:'POST', headers:hdrs(), body: JSON.stringify({
-    model: document.getElementById('model').value, prompt: document.getElementById('txt').value,
-    size: '512x512', response_format: 'b64_json'})});
+    model: document.getElementById('model').value, prompt: neg ? pos + '|' + neg : pos,
+    size: document.getElementById('size').value, step: parseInt(document.getElementById('steps').value) || undefined,
+    seed: parseInt(document.getElementById('seed').value) || undefined, response_format: 'b64_json'})});
   if(!r.ok){st.textContent = 'error: ' + r.status + ' ' + await r.text(); return;}
-  const j = await r.json(); st.textContent = '';
-  document.getElementById('img').src = 'data:image/png;base64,' + j.data[0].b64_json;
+  const j = await r.json(); st.textContent = ((performance.now() - t0) / 1000).toFixed(2) + ' s';
+  const im = document.createElement('img'); im.src = 'data:image/png;base64,' + j.data[0].b64_json; im.title = pos;
+  const g = document.getElementById('gallery'); g.insertBefore(im, g.firstChild);
+}
+"""
+
+_SOUND_JS = _AUTH_JS + """
+async function gen(){
+  const st = document.getElementById('st'); st.textContent = 'generating...';
+  const body = {model_id: document.getElementById('model').value, text: document.getElementById('txt').value};
+  const d = parseFloat(document.getElementById('dur').value); if(d) body.duration_seconds = d;
+  const r = await fetch('/v1/sound-generation', {method:'POST', headers:hdrs(), body: JSON.stringify(body)});
+  if(!r.ok){st.textContent = 'error: ' + r.status + ' ' + await r.text(); return;}
+  st.textContent = ''; const a = document.getElementById('audio'); a.src = URL.createObjectURL(await r.blob()); a.play();
+}
+"""
+
+_HOME_JS = _AUTH_JS + """
+async function unload(btn){
+  await fetch('/backend/shutdown', {method:'POST', headers:hdrs(), body: JSON.stringify({model: btn.dataset.model})});
+  location.reload();
+}
+async function monitor(btn){
+  const r = await fetch('/backend/monitor?model=' + encodeURIComponent(btn.dataset.model), {headers:hdrs()});
+  btn.closest('tr').querySelector('td.mon').textContent = r.ok ? JSON.stringify(await r.json()) : 'error ' + r.status;
 }
 """
 
@@ -177,15 +229,23 @@ def build_router(state) -> APIRouter:
             return JSONResponse({"version": __version__, "models": models(),
                                  "loaded": [m.id for m in state.manager.list_loaded()],
                                  "uptime_s": round(time.time() - state.start_time, 1)})
-        loaded = {m.id for m in state.manager.list_loaded()}
-        rows = "".join(
-            f"<tr><td>{html.escape(m)}</td><td>{'loaded' if m in loaded else ''}</td>"
-            f"<td><a href='/chat/{html.escape(urllib.parse.quote(m, safe=''))}'>chat</a></td></tr>" for m in models())
-        body = (f"<h2>Installed models</h2><table><thead><tr><th>model</th><th>state</th><th></th></tr></thead>"
-                f"<tbody>{rows or '<tr><td colspan=3 class=muted>no models yet: install one from the gallery</td></tr>'}"
+        loaded = {m.id: m for m in state.manager.list_loaded()}
+
+        def row(m):
+            q = html.escape(urllib.parse.quote(m, safe=""))
+            lm = loaded.get(m)
+            acts = (f"<a href='/chat/{q}'>chat</a> · <a href='/tts/{q}'>tts</a> · <a href='/text2image/{q}'>image</a>")
+            if lm is not None:
+                acts += (f" · <button data-model=\"{html.escape(m)}\" onclick='monitor(this)'>monitor</button>"
+                         f" <button data-model=\"{html.escape(m)}\" onclick='unload(this)'>unload</button>")
+            state_ = f"loaded ({html.escape(lm.backend_name)})" if lm is not None else ""
+            return f"<tr><td>{html.escape(m)}</td><td>{state_}</td><td>{acts}</td><td class='mon muted'></td></tr>"
+        rows = "".join(row(m) for m in models())
+        body = (f"<h2>Installed models</h2><table><thead><tr><th>model</th><th>state</th><th></th><th></th></tr></thead>"
+                f"<tbody>{rows or '<tr><td colspan=4 class=muted>no models yet: install one from the gallery</td></tr>'}"
                 f"</tbody></table><p class=muted>version {html.escape(__version__)} · "
-                f"<a href='/metrics'>metrics</a> · <a href='/system'>system</a></p>")
-        return _page("LocalAI", body)
+                f"<a href='/metrics'>metrics</a> · <a href='/system'>system</a> · <a href='/swagger'>API docs</a></p>")
+        return _page("LocalAI", body, _HOME_JS)
 
     async def browse():
         import asyncio
@@ -219,9 +279,15 @@ def build_router(state) -> APIRouter:
         ms = models()
         model = model or (ms[0] if ms else "")
         body = (f"<h2>Chat</h2><div class=row>{_model_select(ms, model)}"
-                f"<input id=temp type=number step=0.1 value=0.7 title=temperature style='max-width:90px'></div>"
+                f"<label>temperature</label><input id=temp type=number step=0.1 value=0.7 style='max-width:80px'>"
+                f"<label>top_p</label><input id=topp type=number step=0.05 placeholder=default style='max-width:80px'>"
+                f"<label>max tokens</label><input id=maxt type=number step=1 placeholder=default style='max-width:90px'>"
+                f"<button onclick='clearChat()'>Clear</button></div>"
+                f"<div class=row><input id=sys placeholder='system prompt (optional)'></div>"
                 f"<div id=log></div><div class=row><textarea id=msg rows=3 placeholder='message (Enter to send)'>"
-                f"</textarea><button onclick='send()'>Send</button></div><div id=stats class=muted></div>")
+                f"</textarea><button onclick='send()'>Send</button></div>"
+                f"<div class=row><label>attach image (vision models)</label><input id=img type=file accept='image/*'></div>"
+                f"<div id=stats class=muted></div>")
         return _page("Chat", body, _CHAT_JS)
 
     async def chat_model(model: str):
@@ -229,7 +295,8 @@ def build_router(state) -> APIRouter:
 
     async def tts(model: str = ""):
         ms = models()
-        body = (f"<h2>Text to speech</h2><div class=row>{_model_select(ms, model or (ms[0] if ms else ''))}</div>"
+        body = (f"<h2>Text to speech</h2><div class=row>{_model_select(ms, model or (ms[0] if ms else ''))}"
+                f"<input id=voice placeholder='voice (optional)'><input id=backend placeholder='backend (optional)'></div>"
                 f"<div class=row><textarea id=txt rows=3></textarea><button onclick='speak()'>Speak</button></div>"
                 f"<audio id=audio controls></audio><div id=st class=muted></div>")
         return _page("TTS", body, _TTS_JS)
@@ -239,13 +306,31 @@ def build_router(state) -> APIRouter:
 
     async def text2image(model: str = ""):
         ms = models()
-        body = (f"<h2>Text to image</h2><div class=row>{_model_select(ms, model or (ms[0] if ms else ''))}</div>"
+        sizes = "".join(f"<option>{z}</option>" for z in ("512x512", "256x256", "768x768", "1024x1024", "768x512",
+                                                          "512x768"))
+        body = (f"<h2>Text to image</h2><div class=row>{_model_select(ms, model or (ms[0] if ms else ''))}"
+                f"<select id=size>{sizes}</select><label>steps</label>"
+                f"<input id=steps type=number value=20 style='max-width:70px'><label>seed</label>"
+                f"<input id=seed type=number placeholder=random style='max-width:100px'></div>"
                 f"<div class=row><input id=txt placeholder=prompt><button onclick='gen()'>Generate</button></div>"
-                f"<div id=st class=muted></div><img id=img style='max-width:100%'>")
+                f"<div class=row><input id=neg placeholder='negative prompt (optional)'></div>"
+                f"<div id=st class=muted></div><div id=gallery class=grid></div>")
         return _page("Text to image", body, _IMG_JS)
 
     async def text2image_model(model: str):
         return await text2image(model)
+
+    async def sound(model: str = ""):
+        ms = models()
+        body = (f"<h2>Sound generation</h2><div class=row>{_model_select(ms, model or (ms[0] if ms else ''))}"
+                f"<label>seconds</label><input id=dur type=number step=0.5 placeholder=default style='max-width:90px'>"
+                f"</div><div class=row><input id=txt placeholder='describe the sound or music'>"
+                f"<button onclick='gen()'>Generate</button></div><audio id=audio controls></audio>"
+                f"<div id=st class=muted></div>")
+        return _page("Sound generation", body, _SOUND_JS)
+
+    async def sound_model(model: str):
+        return await sound(model)
 
     async def talk():
         ms = models()
@@ -266,5 +351,7 @@ def build_router(state) -> APIRouter:
         r.add_api_route("/text2image/", text2image, methods=["GET"])
         r.add_api_route("/text2image/{model}", text2image_model, methods=["GET"])
         r.add_api_route("/talk/", talk, methods=["GET"])
+        r.add_api_route("/sound/", sound, methods=["GET"])
+        r.add_api_route("/sound/{model}", sound_model, methods=["GET"])
     return r
 

@@ -84,11 +84,16 @@ def test_web_ui_pages(client):
     assert client.model_name in w["models"]
     page = client.get("/", headers={"accept": "text/html"})
     assert page.status_code == 200 and "Installed models" in page.text and client.model_name in page.text
-    for path in ("/chat/", f"/chat/{client.model_name}", "/tts/", "/text2image/", "/browse", "/talk/"):
+    for path in ("/chat/", f"/chat/{client.model_name}", "/tts/", "/text2image/", "/browse", "/talk/", "/sound/",
+                 f"/sound/{client.model_name}"):
         r = client.get(path, headers={"accept": "text/html"})
         assert r.status_code == 200, path
         assert "<main>" in r.text
-    assert "/v1/chat/completions" in client.get("/chat/").text  # the page streams through the public API
+    chat = client.get("/chat/").text
+    assert "/v1/chat/completions" in chat  # the page streams through the public API
+    assert "image_url" in chat and "id=sys" in chat  # vision attachments, system prompt
+    assert "/v1/sound-generation" in client.get("/sound/").text
+    assert "negative" in client.get("/text2image/").text
 
 
 def test_chat_completion_greedy_is_deterministic(client):
