@@ -72,6 +72,7 @@ class EngineConfig:
     lora_adapters: tuple = ()         # ((adapter GGUF path, scale), ...) merged into the weights at load
     record_tokens: bool = False       # final Event carries the generated token ids (numerics tests)
     draft_model: str = ""             # speculative decoding: draft LM GGUF (engine/speculative.DraftModel)
+    quantization: str = ""            # HF checkpoints: load-time quantisation (bnb_4bit / bnb_8bit / ...)
     draft_max_seqs: int = 16          # draft-model KV cache capacity in sequences of context_size
 
 
@@ -130,7 +131,7 @@ class LLMEngine:
         if self.device.type == "cuda":
             torch.cuda.set_device(self.device)
             ops.lib()  # fail loudly if the kernel library is missing on a GPU box
-        self.reader = open_model(cfg.model_path)  # GGUF file or HF checkpoint directory
+        self.reader = open_model(cfg.model_path, cfg.quantization)  # GGUF file or HF checkpoint directory
         self.tokenizer = Tokenizer.from_gguf(self.reader)
         ro = {}
         if cfg.rope_freq_base:

@@ -170,7 +170,8 @@ class EngineServicer:
                 use_graphs=not request.EnforceEager,
                 mmproj=self._mmproj_path(request, path),
                 lora_adapters=self._lora(request, path),
-                draft_model=self._draft_path(request, path))
+                draft_model=self._draft_path(request, path),
+                quantization=str(request.Quantization or "") if is_hf_checkpoint(path) else "")
             loop = asyncio.get_running_loop()
             eng = await loop.run_in_executor(None, lambda: LLMEngine(cfg, tp=self.tp))
             await loop.run_in_executor(None, eng.warmup)

@@ -53,11 +53,21 @@ def hf_architecture(path: str) -> str:
     return ARCH_OF.get(archs[0], "") if archs else ""
 
 
-def open_model(path: str):
+# `quantization` of the transformers backend (backend/python/transformers/backend.py:93-106:
+# bitsandbytes nf4 / int8, XPU 4 / 8 bit) -> the GGML block formats the engine's HIP GEMMs read
+# directly: the checkpoint's linear weights are quantised once at load (llama.cpp's Q4_K_M recipe
+# for the 4-bit modes: Q4_K projections, Q6_K for the output head and ffn_down / attn_v; Q8_0 for
+# the 8-bit modes).  Same memory class and the same load-time semantics as bnb (quantise on load,
+# compute in bf16); the numbers are the GGML formats', not bnb's.
+QUANT_MODES = {"bnb_4bit": "q4_k_m", "xpu_4bit": "q4_k_m", "q4_k_m": "q4_k_m", "q4_k": "q4_k_m",
+               "bnb_8bit": "q8_0", "xpu_8bit": "q8_0", "q8_0": "q8_0"}
+
+
+def open_model(path: str, quantization: str = ""):
     """GGUF file, HF checkpoint directory or pre-GGUF ggjt v3 file -> reader with the GGUFReader
-    interface."""
+    interface.  `quantization`: load-time quantisation of an HF checkpoint (QUANT_MODES)."""
     if is_hf_checkpoint(path):
-        return HFCheckpointReader(path)
+        return HFCheckpointReader(path, quantization=quantization)
     from .ggml_legacy import GGJTReader, is_ggjt
     if is_ggjt(path):
         return GGJTReader(path)
@@ -93,8 +103,12 @@ def _llama3_rope_freqs(rs: dict, head_dim: int, theta: float) -> np.ndarray:
 
 
 class HFCheckpointReader:
-    def __init__(self, path: str):
+    def __init__(self, path: str, quantization: str = ""):
         self.path = path
+        q = (quantization or "").lower()
+        if q and q not in QUANT_MODES:
+            raise ValueError(f"quantization {quantization!r} is not supported; one of {', '.join(sorted(QUANT_MODES))}")
+        self.quant = QUANT_MODES.get(q, "")
         with open(os.path.join(path, "config.json")) as f:
             self.config: Dict[str, Any] = json.load(f)
         archs = self.config.get("architectures") or []
@@ -287,9 +301,37 @@ class HFCheckpointReader:
                 put(b + "ffn_down.weight", p + "mlp.down_proj.weight")
         if self._rope_freqs is not None:
             self._put("rope_freqs.weight", self._rope_freqs, GGMLType.F32)
+        if self.quant:
+            self._quantize_weights()
         rest = [k for k in hf if not k.endswith("rotary_emb.inv_freq")]
         if rest:
             raise ValueError(f"{self.path}: unmapped tensors {rest[:5]}")
+
+    _QUANT_TARGETS = ("attn_q.weight", "attn_k.weight", "attn_v.weight", "attn_output.weight", "ffn_gate.weight",
+                      "ffn_up.weight", "ffn_down.weight", "ffn_gate_exps.weight", "ffn_up_exps.weight",
+                      "ffn_down_exps.weight", "output.weight")
+
+    def _quantize_weights(self):
+        """Linear weights -> Q4_K_M mix or Q8_0 (QUANT_MODES); norms, embeddings, biases stay."""
+        from ..gguf import quantize
+        for name, t in list(self.tensors.items()):
+            if not name.endswith(self._QUANT_TARGETS):
+                continue
+            K = t.shape[-1]
+            if self.quant == "q8_0":
+                gt = GGMLType.Q8_0 if K % 32 == 0 else None
+            else:
+                six = name.endswith(("output.weight", "ffn_down.weight", "ffn_down_exps.weight", "attn_v.weight")) \
+                    and not name.endswith("attn_output.weight")
+                gt = (GGMLType.Q6_K if six else GGMLType.Q4_K) if K % 256 == 0 else \
+                    (GGMLType.Q8_0 if K % 32 == 0 else None)
+            if gt is None:
+                continue
+            src = {GGMLType.BF16: lambda d: (d.view(np.uint16).astype(np.uint32) << 16).view(np.float32),
+                   GGMLType.F16: lambda d: d.view(np.float16).astype(np.float32),
+                   GGMLType.F32: lambda d: d.view(np.float32)}[GGMLType(t.ggml_type)](t.data)
+            q = quantize(src.reshape(t.shape), gt)
+            self.tensors[name] = GGUFTensor(name, t.shape, int(gt), 0, q.nbytes, q)
 
     # ---- tokenizer -------------------------------------------------------------------------
     def _json(self, name: str) -> dict:

@@ -138,3 +138,30 @@ def test_gptq_checkpoint(tmp_path, act_order):
     ref = _hf_logits(str(tmp_path / "oracle"), ids)
     err = float((ours - ref).abs().max() / ref.abs().max())
     assert err < 3e-3, err  # the loader rounds dequantised weights to f16
+
+
+@pytest.mark.parametrize("mode,types", [("bnb_4bit", {"attn_q": 12, "ffn_down": 14, "output": 14, "attn_v": 14}),
+                                        ("bnb_8bit", {"attn_q": 8, "ffn_down": 8, "output": 8})])
+def test_transformers_quantization_modes(tmp_path, mode, types):
+    """`quantization: bnb_4bit / bnb_8bit` (reference transformers backend) quantise the HF
+    checkpoint's linear weights at load into the GGML formats the HIP GEMMs read (Q4_K_M mix /
+    Q8_0); the quantised model stays close to the float one (transformers oracle)."""
+    d = str(tmp_path / "ck")
+    synth.write_hf_checkpoint(d, kind="llama", hidden=256, heads=4, kv_heads=2, ffn=512)
+    r = HFCheckpointReader(d, quantization=mode)
+    for short, gt in types.items():
+        name = "output.weight" if short == "output" else f"blk.0.{short}.weight"
+        assert r.tensors[name].ggml_type == gt, (name, r.tensors[name].ggml_type)
+    assert r.tensors["token_embd.weight"].ggml_type in (0, 1, 30)  # embeddings / norms stay float
+    e = LLMEngine(EngineConfig(model_path=d, device="cpu", context_size=256, max_num_seqs=4, use_graphs=False,
+                               quantization=mode))
+    ids = e.tokenize(TEXT)
+    ours = e.model.reference_logits(ids).float()
+    ref = _hf_logits(d, ids)
+    cos = float(torch.nn.functional.cosine_similarity(ours.flatten(), ref.flatten(), dim=0))
+    # random-init gaussian weights are the worst case for 4-bit codes (no outlier structure)
+    assert cos > (0.93 if mode == "bnb_4bit" else 0.999), cos
+    out = e.generate(TEXT, SamplingParams(max_tokens=4, temperature=0.0, ignore_eos=True))
+    assert out["completion_tokens"] == 4
+    with pytest.raises(ValueError, match="quantization"):
+        HFCheckpointReader(d, quantization="awq_3bit")
