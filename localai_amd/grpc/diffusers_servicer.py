@@ -6,13 +6,16 @@ Mirrors `backend/python/diffusers/backend.py`: LoadModel keeps `CFGScale` (7 whe
 `negative_prompt`, seeds its generator when `seed > 0`, and honours `EnableParameters` (a comma
 list naming which of negative_prompt / width / height / num_inference_steps reach the pipeline,
 "none" for none of them -- the rest take the pipeline defaults: sample_size * 8 pixels, 50 steps).
-`src` makes the call img2img (strength 0.8, the diffusers default); `SchedulerType` takes every
+`src` makes the call img2img (strength 0.8, the diffusers default) -- or, when LoadModel named a
+`ControlNet` (a ControlNetModel directory, relative to the pipeline's parent directory), the
+control image of a ControlNet-conditioned txt2img (backend.py:292-296, 403-405); `SchedulerType` takes every
 scheduler name of the reference's mapping (models/schedulers.py).  One image at a time (the
 reference runs one gRPC worker per backend).
 """
 from __future__ import annotations
 
 import asyncio
+import os
 import threading
 
 from . import backend_pb as pb
@@ -41,9 +44,15 @@ class DiffusersServicer:
         if not dev:
             import torch
             dev = "cuda:0" if torch.cuda.is_available() else "cpu"
+        cn = str(request.ControlNet or "")
+        if cn and not os.path.isabs(cn) and not os.path.isdir(cn):
+            cn = os.path.join(os.path.dirname(os.path.normpath(path)), cn)  # next to the pipeline directory
+        if cn and not os.path.isfile(os.path.join(cn, "config.json")):
+            return pb.Result(success=False, message=f"ControlNet model not found: {request.ControlNet}")
         try:
             p = await asyncio.get_running_loop().run_in_executor(
-                None, lambda: StableDiffusion(path, dev, request.SchedulerType, int(request.CLIPSkip or 0)))
+                None, lambda: StableDiffusion(path, dev, request.SchedulerType, int(request.CLIPSkip or 0),
+                                              controlnet=cn))
         except Exception as e:  # noqa: BLE001 - reported to the caller like the reference
             return pb.Result(success=False, message=f"Unexpected {e!r}")
         self.pipe, self.state = p, pb.StatusResponse.READY
@@ -67,6 +76,9 @@ class DiffusersServicer:
         w = int(kw.get("width") or default_px)
         h = int(kw.get("height") or default_px)
         image = request.src or None   # backend.py: options["image"] = Image.open(request.src) -> img2img
+        control = None
+        if image is not None and p.controlnet is not None:
+            control, image = image, None  # backend.py:403: with a ControlNet, src is the control image
         if image is not None:
             # the reference passes width / height only when asked; img2img keeps the source's size otherwise
             w = int(kw["width"]) if kw.get("width") else 0
@@ -74,7 +86,7 @@ class DiffusersServicer:
         with self._lock:
             img = p(request.positive_prompt, kw.get("negative_prompt", ""), w, h,
                     steps=int(kw.get("num_inference_steps", 50)), guidance_scale=self.cfg_scale,
-                    seed=request.seed if request.seed > 0 else None, image=image)
+                    seed=request.seed if request.seed > 0 else None, image=image, control_image=control)
             p.save(img, request.dst)
 
     async def GenerateImage(self, request, context=None):

@@ -348,7 +348,7 @@ class UNet(nn.Module):
         e = torch.cat([torch.cos(e), torch.sin(e)] if self.flip else [torch.sin(e), torch.cos(e)], dim=-1)
         return e
 
-    def forward(self, x, t, ctx, text_embeds=None, time_ids=None):
+    def _temb(self, x, t, text_embeds=None, time_ids=None):
         temb = self._tproj(t).to(x.dtype)
         temb = self.time_embedding.linear_2(F.silu(self.time_embedding.linear_1(temb)))
         if self.text_time:
@@ -358,7 +358,10 @@ class UNet(nn.Module):
             tid = self._tproj(time_ids.reshape(-1), self.add_time_dim).reshape(B, -1)
             a = torch.cat([text_embeds.to(x.dtype), tid.to(x.dtype)], dim=-1)
             temb = temb + self.add_embedding.linear_2(F.silu(self.add_embedding.linear_1(a)))
-        h = self.conv_in(x)
+        return temb
+
+    def _down_mid(self, h, temb, ctx):
+        """conv_in output -> (mid-block output, skip tensors of the down path)."""
         skips = [h]
         for b in self.down_blocks:
             for j, r in enumerate(b.resnets):
@@ -371,7 +374,17 @@ class UNet(nn.Module):
                 skips.append(h)
         m = self.mid_block
         h = m.attentions[0](m.resnets[0](h, temb), ctx)
-        h = m.resnets[1](h, temb)
+        return m.resnets[1](h, temb), skips
+
+    def forward(self, x, t, ctx, text_embeds=None, time_ids=None, down_res=None, mid_res=None):
+        """down_res / mid_res: ControlNet residuals added to the skips / the mid-block output
+        (diffusers' down_block_additional_residuals / mid_block_additional_residual)."""
+        temb = self._temb(x, t, text_embeds, time_ids)
+        h, skips = self._down_mid(self.conv_in(x), temb, ctx)
+        if down_res is not None:
+            skips = [s_ + r_ for s_, r_ in zip(skips, down_res)]
+        if mid_res is not None:
+            h = h + mid_res
         for b in self.up_blocks:
             for j, r in enumerate(b.resnets):
                 h = r(torch.cat([h, skips.pop()], dim=1), temb)
@@ -380,6 +393,50 @@ class UNet(nn.Module):
             if hasattr(b, "upsamplers"):
                 h = b.upsamplers[0](h, skips[-1].shape[-2:] if skips else None)
         return self.conv_out(_gn(self.conv_norm_out, h, True))
+
+
+class ControlNet(UNet):
+    """diffusers ControlNetModel: the UNet's encoder half (conv_in, time embedding, down blocks,
+    mid block -- named like the UNet's) plus a conditioning-image embedding added after conv_in
+    and zero-initialised 1x1 convolutions that turn every skip and the mid output into residuals
+    for the UNet (reference: `backend/python/diffusers/backend.py:292-296`, ControlNetModel with
+    the control image as `image`)."""
+
+    def __init__(self, c: dict):
+        n = len(c["block_out_channels"])
+        super().__init__(dict(c, up_block_types=c.get("up_block_types") or ["UpBlock2D"] * n))
+        del self.up_blocks, self.conv_norm_out, self.conv_out
+        ch = list(c["block_out_channels"])
+        lpb = int(c.get("layers_per_block", 2))
+        emb = list(c.get("conditioning_embedding_out_channels") or [16, 32, 96, 256])
+        self.bgr = str(c.get("controlnet_conditioning_channel_order", "rgb")) == "bgr"
+        ce = nn.Module()
+        ce.conv_in = nn.Conv2d(int(c.get("conditioning_channels", 3)), emb[0], 3, padding=1)
+        ce.blocks = nn.ModuleList()
+        for i in range(len(emb) - 1):
+            ce.blocks.append(nn.Conv2d(emb[i], emb[i], 3, padding=1))
+            ce.blocks.append(nn.Conv2d(emb[i], emb[i + 1], 3, padding=1, stride=2))
+        ce.conv_out = nn.Conv2d(emb[-1], ch[0], 3, padding=1)
+        self.controlnet_cond_embedding = ce
+        skip_ch = [ch[0]]
+        for i in range(n):
+            skip_ch += [ch[i]] * lpb + ([ch[i]] if i < n - 1 else [])
+        self.controlnet_down_blocks = nn.ModuleList(nn.Conv2d(k, k, 1) for k in skip_ch)
+        self.controlnet_mid_block = nn.Conv2d(ch[-1], ch[-1], 1)
+
+    def forward(self, x, t, ctx, cond, scale: float = 1.0, text_embeds=None, time_ids=None):
+        """cond: the control image in [0, 1], [B, 3, 8h, 8w] -> (skip residuals, mid residual)."""
+        temb = self._temb(x, t, text_embeds, time_ids)
+        ce = self.controlnet_cond_embedding
+        if self.bgr:
+            cond = cond.flip(1)
+        e = F.silu(ce.conv_in(cond))
+        for blk in ce.blocks:
+            e = F.silu(blk(e))
+        h = self.conv_in(x) + ce.conv_out(e)
+        h, skips = self._down_mid(h, temb, ctx)
+        down = [conv(s_) * scale for conv, s_ in zip(self.controlnet_down_blocks, skips)]
+        return down, self.controlnet_mid_block(h) * scale
 
 
 class _VaeAttn(nn.Module):
@@ -568,7 +625,7 @@ class Scheduler:
 # ------------------------------------------------------------------ pipeline
 class StableDiffusion:
     def __init__(self, path: str, device: str = "cpu", scheduler: str = "", clip_skip: int = 0,
-                 channels_last: Optional[bool] = None):
+                 channels_last: Optional[bool] = None, controlnet: str = "", controlnet_scale: float = 1.0):
         self.device = torch.device(device)
         # NHWC activations for the MIOpen convolutions (LOCALAI_AMD_SD_NHWC=0 keeps NCHW)
         if channels_last is None:
@@ -597,7 +654,13 @@ class StableDiffusion:
             self.vae_enc = VaeEncoder(vcfg)
             self.vae_enc.load_state_dict(enc, strict=True)
             self.vae_enc.to(self.device, self.dtype).eval().requires_grad_(False)
-        for m in (self.text, self.text2, self.unet, self.vae):
+        # ControlNet (diffusers ControlNetModel directory: config.json + weights)
+        self.controlnet = None
+        self.cn_scale = float(controlnet_scale)
+        if controlnet:
+            self.controlnet = ControlNet(_cfg(os.path.join(controlnet, "config.json")))
+            self.controlnet.load_state_dict(_load_weights(controlnet), strict=True)
+        for m in (self.text, self.text2, self.unet, self.vae, self.controlnet):
             if m is not None:
                 m.to(self.device, self.dtype).eval().requires_grad_(False)
         if self.xl and not self.unet.text_time:
@@ -605,6 +668,8 @@ class StableDiffusion:
         if self.channels_last:
             self.unet.to(memory_format=torch.channels_last)
             self.vae.to(memory_format=torch.channels_last)
+            if self.controlnet is not None:
+                self.controlnet.to(memory_format=torch.channels_last)
         sc = os.path.join(path, "scheduler", "scheduler_config.json")
         self.sched_cfg = _cfg(sc) if os.path.isfile(sc) else {}
         from .schedulers import PLMS, KSampler, parse_name
@@ -634,73 +699,47 @@ class StableDiffusion:
                             for k, v in _load_weights(d).items() if "position_ids" not in k}, strict=True)
         return te
 
-    def _unet(self, x: torch.Tensor, t: torch.Tensor, ctx: torch.Tensor, add=None) -> torch.Tensor:
-        """add: SDXL (text_embeds, time_ids) or None."""
-        if add is not None:
-            return self._unet_xl(x, t, ctx, add)
+    def _model(self, x, t, ctx, te=None, ti=None, cond=None):
+        """One denoiser evaluation: ControlNet residuals (when a control image is given) + UNet."""
+        dr = mr = None
+        if cond is not None:
+            dr, mr = self.controlnet(x, t, ctx, cond, self.cn_scale, te, ti)
+        return self.unet(x, t, ctx, te, ti, dr, mr)
+
+    def _unet(self, x: torch.Tensor, t: torch.Tensor, ctx: torch.Tensor, add=None, cond=None) -> torch.Tensor:
+        """add: SDXL (text_embeds, time_ids) or None; cond: ControlNet image or None.  On the GPU
+        the whole step (ControlNet + UNet, ~1300 launches) replays from one hipGraph per input
+        shape set, kept in a bounded LRU (each graph owns its activation pool)."""
+        te, ti = add if add is not None else (None, None)
+        ins = (x, t, ctx, te, ti, cond)
         if not self.use_graphs:
-            return self.unet(x, t, ctx)
-        key = (tuple(x.shape), tuple(ctx.shape))
+            return self._model(*ins)
+        key = tuple(None if v is None else tuple(v.shape) for v in ins)
         g = self._graphs.get(key)
-        if g is not None:
-            self._graphs.move_to_end(key)
         if g is None:
-            out = self.unet(x, t, ctx)  # eager first call: kernel selection / workspaces happen outside capture
+            out = self._model(*ins)  # eager first call: kernel selection / workspaces happen outside capture
             if self.graph_cache == 0:
                 return out
             while len(self._graphs) >= self.graph_cache:
-                _, old = self._graphs.popitem(last=False)   # least recently used size
+                _, old = self._graphs.popitem(last=False)   # least recently used shape set
                 del old
                 torch.cuda.empty_cache()
             try:
-                sx, st, sc = x.clone(), t.clone(), ctx.clone()
+                st = tuple(None if v is None else v.clone() for v in ins)
                 graph = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(graph):
-                    so = self.unet(sx, st, sc)
-                self._graphs[key] = (graph, sx, st, sc, so)
+                    so = self._model(*st)
+                self._graphs[key] = (graph, st, so)
             except Exception as e:  # noqa: BLE001 - capture is an optimisation; eager stays correct
                 import logging
                 logging.getLogger(__name__).warning("sd: UNet graph capture failed (%r); running eager", e)
                 self.use_graphs = False
             return out
-        graph, sx, st, sc, so = g
-        sx.copy_(x)
-        st.copy_(t)
-        sc.copy_(ctx)
-        graph.replay()
-        return so.clone()
-
-    def _unet_xl(self, x, t, ctx, add):
-        """SDXL step: the same graph cache, with the pooled text embeds and time ids as two more
-        static inputs of the captured graph."""
-        te, ti = add
-        if not self.use_graphs:
-            return self.unet(x, t, ctx, te, ti)
-        key = ("xl", tuple(x.shape), tuple(ctx.shape), tuple(te.shape))
-        g = self._graphs.get(key)
-        if g is None:
-            out = self.unet(x, t, ctx, te, ti)
-            if self.graph_cache == 0:
-                return out
-            while len(self._graphs) >= self.graph_cache:
-                _, old = self._graphs.popitem(last=False)
-                del old
-                torch.cuda.empty_cache()
-            try:
-                st = tuple(v.clone() for v in (x, t, ctx, te, ti))
-                graph = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(graph):
-                    so = self.unet(*st)
-                self._graphs[key] = (graph, st, so)
-            except Exception as e:  # noqa: BLE001
-                import logging
-                logging.getLogger(__name__).warning("sd: SDXL UNet graph capture failed (%r); running eager", e)
-                self.use_graphs = False
-            return out
         self._graphs.move_to_end(key)
         graph, st, so = g
-        for dst, src in zip(st, (x, t, ctx, te, ti)):
-            dst.copy_(src)
+        for dst, src in zip(st, ins):
+            if dst is not None:
+                dst.copy_(src)
         graph.replay()
         return so.clone()
 
@@ -727,14 +766,14 @@ class StableDiffusion:
         return ctx, pool
 
     def _eps(self, x: torch.Tensor, t: float, ctx: torch.Tensor, cfg: bool, guidance_scale: float,
-             add=None) -> torch.Tensor:
+             add=None, cond=None) -> torch.Tensor:
         """Model output (eps or v) at timestep t with classifier-free guidance as one batch of 2."""
         xin = torch.cat([x, x]) if cfg else x
         tt = torch.full((xin.shape[0],), float(t), device=self.device)
         xin = xin.to(self.dtype)
         if self.channels_last:
             xin = xin.contiguous(memory_format=torch.channels_last)
-        out = self._unet(xin, tt, ctx, add).float()
+        out = self._unet(xin, tt, ctx, add, cond).float()
         if cfg:
             u, c = out.chunk(2)
             out = u + guidance_scale * (c - u)
@@ -753,12 +792,25 @@ class StableDiffusion:
             a = a.contiguous(memory_format=torch.channels_last)
         return self.vae_enc(a, g).float()
 
+    def _control_image(self, image, W: int, H: int, batch: int) -> torch.Tensor:
+        """ControlNet conditioning image -> [batch, 3, H, W] in [0, 1] (diffusers'
+        control_image_processor: RGB, resized to the output size, not normalised)."""
+        from PIL import Image
+        im = image if isinstance(image, Image.Image) else Image.open(image)
+        im = im.convert("RGB").resize((W, H), Image.LANCZOS)
+        a = torch.from_numpy(np.asarray(im, dtype=np.float32) / 255.0).permute(2, 0, 1)[None]
+        a = a.expand(batch, -1, -1, -1).to(self.device, self.dtype)
+        return a.contiguous(memory_format=torch.channels_last) if self.channels_last else a.contiguous()
+
     @torch.inference_mode()
     def __call__(self, prompt: str, negative_prompt: str = "", width: int = 512, height: int = 512,
                  steps: int = 1, guidance_scale: float = 7.0, seed: Optional[int] = None,
-                 image=None, strength: float = 0.8) -> torch.Tensor:
+                 image=None, strength: float = 0.8, control_image=None) -> torch.Tensor:
         """-> uint8 image [H, W, 3] on the CPU.  `image` (a path or PIL image) turns the call into
-        img2img: its latents are noised to `strength` of the schedule and denoised from there."""
+        img2img: its latents are noised to `strength` of the schedule and denoised from there.
+        `control_image` conditions every step through the ControlNet (pipelines loaded with one)."""
+        if control_image is not None and self.controlnet is None:
+            raise ValueError("control_image given but no ControlNet is loaded")
         g = torch.Generator().manual_seed(seed if seed is not None else int.from_bytes(os.urandom(4), "little"))
         if image is not None and not (width and height):
             from PIL import Image
@@ -775,6 +827,9 @@ class StableDiffusion:
             add = (pool, tid)
         else:
             ctx = self._encode(prompts)
+        cond = None
+        if control_image is not None:
+            cond = self._control_image(control_image, w * self.vae_scale, h * self.vae_scale, len(prompts))
         steps = max(1, steps)
         x0 = self._init_latents(image, w, h, g) if image is not None else None
         # img2img: skip the first (1 - strength) of the schedule (diffusers get_timesteps)
@@ -789,7 +844,7 @@ class StableDiffusion:
 
             def denoise(xv, sigma):
                 c_in = 1.0 / math.sqrt(sigma * sigma + 1.0)
-                out = self._eps(xv * c_in, ks.sched.sigma_to_t(sigma), ctx, cfg, guidance_scale, add)
+                out = self._eps(xv * c_in, ks.sched.sigma_to_t(sigma), ctx, cfg, guidance_scale, add, cond)
                 if self.pred == "v_prediction":
                     return xv / (sigma * sigma + 1.0) - out * (sigma * c_in)
                 return xv - sigma * out
@@ -800,12 +855,12 @@ class StableDiffusion:
             ts = ts[skip:] if skip else ts
             x = noise if x0 is None else self._add_noise(x0, noise, ts[0])
             for t in ts:
-                x = self.plms.step(self._eps(x, t, ctx, cfg, guidance_scale, add), t, x)
+                x = self.plms.step(self._eps(x, t, ctx, cfg, guidance_scale, add, cond), t, x)
         else:
             ts = self.sched.timesteps(steps)[skip:]
             x = noise if x0 is None else self._add_noise(x0, noise, ts[0])
             for i, t in enumerate(ts):
-                out = self._eps(x, t, ctx, cfg, guidance_scale, add)
+                out = self._eps(x, t, ctx, cfg, guidance_scale, add, cond)
                 x = self.sched.step(out, t, ts[i + 1] if i + 1 < len(ts) else None, x)
         img = self.vae(x.to(self.dtype)).float()
         img = ((img[0] / 2 + 0.5).clamp(0, 1) * 255).round().to(torch.uint8)

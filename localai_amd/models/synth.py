@@ -925,3 +925,33 @@ def write_sd_pipeline(out_dir: str, size: str = "tiny", seed: int = 0, v_predict
         json.dump({"_class_name": "StableDiffusionXLPipeline", "force_zeros_for_empty_prompt": True} if xl
                   else {"_class_name": "StableDiffusionPipeline"}, f)
     return out_dir
+
+
+def write_controlnet(out_dir: str, pipe_dir: str, seed: int = 0, zero: bool = True) -> str:
+    """Random-init diffusers ControlNetModel directory matching the UNet of `pipe_dir` (same block
+    layout; conditioning_embedding_out_channels scaled down for toy pipelines).  zero=True keeps
+    the zero-initialised output convolutions of a fresh ControlNet (its residuals are exactly 0)."""
+    import torch
+    from safetensors.torch import save_file
+
+    from .sd import ControlNet
+    with open(os.path.join(pipe_dir, "unet", "config.json")) as f:
+        uc = json.load(f)
+    c = {k: v for k, v in uc.items() if k not in ("up_block_types", "out_channels", "sample_size", "_class_name")}
+    small = uc["block_out_channels"][0] < 128
+    c["conditioning_embedding_out_channels"] = [4, 8] if small else [16, 32, 96, 256]
+    if small and len(uc["block_out_channels"]) > 2:
+        c["conditioning_embedding_out_channels"] = [4, 8, 8]
+    c["_class_name"] = "ControlNetModel"
+    torch.manual_seed(seed)
+    m = ControlNet(c)
+    if zero:
+        for conv in list(m.controlnet_down_blocks) + [m.controlnet_mid_block, m.controlnet_cond_embedding.conv_out]:
+            torch.nn.init.zeros_(conv.weight)
+            torch.nn.init.zeros_(conv.bias)
+    os.makedirs(out_dir, exist_ok=True)
+    with open(os.path.join(out_dir, "config.json"), "w") as f:
+        json.dump(c, f)
+    save_file({k: v.contiguous() for k, v in m.state_dict().items()},
+              os.path.join(out_dir, "diffusion_pytorch_model.safetensors"))
+    return out_dir

@@ -256,3 +256,73 @@ def test_k_sampler_and_img2img_on_gpu(pipe_dir):
     src = Image.new("RGB", (32, 32), (10, 200, 40))
     i2i = g("a cat", "", 32, 32, steps=4, seed=7, image=src, strength=0.6)
     assert i2i.shape == (32, 32, 3)
+
+
+def test_controlnet(pipe_dir, tmp_path):
+    """ControlNetModel (diffusers layout) conditioning the UNet: a fresh ControlNet (zero output
+    convolutions) leaves the image unchanged exactly; a trained-looking one (random output convs)
+    changes it, and the control image matters; weight names follow diffusers
+    (controlnet_cond_embedding.*, controlnet_down_blocks.N, controlnet_mid_block)."""
+    from PIL import Image
+
+    from localai_amd.models.sd import ControlNet
+    ctrl = tmp_path / "ctrl.png"
+    Image.fromarray((torch.rand(32, 32, 3) * 255).to(torch.uint8).numpy()).save(ctrl)
+    ctrl2 = tmp_path / "ctrl2.png"
+    Image.fromarray((torch.rand(32, 32, 3) * 255).to(torch.uint8).numpy()).save(ctrl2)
+    base = StableDiffusion(pipe_dir, "cpu")("a cat", "", 32, 32, steps=2, seed=3)
+    zdir = synth.write_controlnet(str(tmp_path / "cn-zero"), pipe_dir, zero=True)
+    pz = StableDiffusion(pipe_dir, "cpu", controlnet=zdir)
+    names = set(pz.controlnet.state_dict())
+    n_skips = sum(1 for k in names if k.startswith("controlnet_down_blocks.") and k.endswith(".weight"))
+    assert n_skips == 1 + 2 + 1  # conv_in + (resnet, downsampler) + resnet of the 2-level toy UNet
+    assert {"controlnet_mid_block.weight", "controlnet_cond_embedding.conv_out.weight"} <= names
+    assert not any(k.startswith("up_blocks") for k in names)
+    assert torch.equal(pz("a cat", "", 32, 32, steps=2, seed=3, control_image=str(ctrl)), base)
+    rdir = synth.write_controlnet(str(tmp_path / "cn-rand"), pipe_dir, zero=False, seed=5)
+    pr = StableDiffusion(pipe_dir, "cpu", controlnet=rdir)
+    a = pr("a cat", "", 32, 32, steps=2, seed=3, control_image=str(ctrl))
+    b = pr("a cat", "", 32, 32, steps=2, seed=3, control_image=str(ctrl2))
+    assert not torch.equal(a, base) and not torch.equal(a, b)
+    pr.cn_scale = 0.0
+    assert torch.equal(pr("a cat", "", 32, 32, steps=2, seed=3, control_image=str(ctrl)), base)
+    with pytest.raises(ValueError, match="ControlNet"):
+        StableDiffusion(pipe_dir, "cpu")("a cat", "", 32, 32, steps=1, seed=3, control_image=str(ctrl))
+    assert isinstance(pr.controlnet, ControlNet)
+
+
+def test_controlnet_through_backend(pipe_dir, tmp_path):
+    from PIL import Image
+
+    from localai_amd.grpc.diffusers_servicer import DiffusersServicer
+    synth.write_controlnet(os.path.join(os.path.dirname(pipe_dir), "cn-backend"), pipe_dir, zero=False, seed=2)
+    ctrl = tmp_path / "pose.png"
+    Image.fromarray((torch.rand(32, 32, 3) * 255).to(torch.uint8).numpy()).save(ctrl)
+    sv = DiffusersServicer(device="cpu")
+
+    async def go():
+        r = await sv.LoadModel(pb.ModelOptions(ModelFile=pipe_dir, ControlNet="cn-backend"), None)
+        assert r.success, r.message
+        dst = str(tmp_path / "out.png")
+        r = await sv.GenerateImage(pb.GenerateImageRequest(positive_prompt="a dancer", width=32, height=32, step=2,
+                                                           seed=4, src=str(ctrl), dst=dst), None)
+        assert r.success, r.message
+        assert Image.open(dst).size == (32, 32)  # control image, not img2img: the requested size
+        r = await sv.LoadModel(pb.ModelOptions(ModelFile=pipe_dir, ControlNet="no-such-controlnet"), None)
+        assert not r.success and "ControlNet" in r.message
+    asyncio.run(go())
+
+
+@pytest.mark.gpu
+def test_controlnet_on_gpu_graph(pipe_dir, tmp_path):
+    from PIL import Image
+    cdir = synth.write_controlnet(str(tmp_path / "cn"), pipe_dir, zero=False, seed=5)
+    ctrl = tmp_path / "ctrl.png"
+    Image.fromarray((torch.rand(32, 32, 3) * 255).to(torch.uint8).numpy()).save(ctrl)
+    p = StableDiffusion(pipe_dir, "cuda:0", controlnet=cdir)
+    a = p("a cat", "", 32, 32, steps=3, seed=3, control_image=str(ctrl))
+    b = p("a cat", "", 32, 32, steps=3, seed=3, control_image=str(ctrl))
+    assert p._graphs and (a.float() - b.float()).abs().max() <= 3
+    p.use_graphs = False
+    c = p("a cat", "", 32, 32, steps=3, seed=3, control_image=str(ctrl))
+    assert (b.float() - c.float()).abs().max() <= 3
