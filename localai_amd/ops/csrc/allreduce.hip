@@ -131,9 +131,160 @@ __global__ __launch_bounds__(AR_T) void allreduce_oneshot_kernel(ARArgs a) {
   if (tid == 0) *counter = ep;
 }
 
+// ----------------------------------------------------------------------------- two-shot
+// Reduce-scatter + all-gather over the same kind of peer-mapped region, for messages past the
+// one-shot's 256 K elements (decode rows of a wide TP batch: 256 x 4096 fp32 = 4 MiB; prefill
+// chunks up to 4 M elements).  One-shot makes every rank read all R copies of the message (R x n
+// bytes per rank); two-shot reads ~2n: rank r reduces only its 1/R sub-range of each 1024-element
+// block (reading that sub-range from every rank), stores the sum in its own result slot, and then
+// every rank gathers the R reduced sub-ranges.  Same per-block channels, epochs and parity slots
+// as the one-shot; a second flag row per block orders phase 2 after phase 1 on every rank.
+//   region: [flags1 | flags2 : AR2_MAXB x AR_MAXR int32] [counter : AR2_MAXB] [err]
+//           [data : 2 parity slots x 16 MiB] [result : 2 parity slots x 16 MiB]
+// Slot reuse is safe for the reason given above: a peer signals epoch e+1 only after its epoch-e
+// kernel (every read of this rank's epoch-e slots) has finished.  Every element is reduced once,
+// by its owner, in rank order (fp32), so all ranks hold identical bits.
+constexpr int AR2_MAXB = 4096;
+constexpr long AR2_F1 = 0, AR2_F2 = (long)AR2_MAXB * AR_MAXR * 4, AR2_CNT = 2 * AR2_F2,
+               AR2_ERR = AR2_CNT + AR2_MAXB * 4;
+constexpr long AR2_DATA = 524288;                 // header rounded up (512 KiB)
+constexpr long AR2_SLOT = (long)AR2_MAXB * AR_CHUNK * 4;  // 16 MiB per parity slot
+static_assert(AR2_ERR + 64 <= AR2_DATA, "two-shot header");
+
+LA_DEV void ar_signal(uint8_t* const* bufs, int world, int rank, long flags_off, int b, int ep, int tid) {
+  if (tid < world && tid != rank) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int* f = (int*)(bufs[tid] + flags_off) + b * AR_MAXR + rank;
+    __hip_atomic_store(f, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+LA_DEV void ar_wait(uint8_t* own, int world, int rank, long flags_off, long err_off, int b, int ep, int tid,
+                    long spin_limit) {
+  if (tid < world && tid != rank) {
+    const int* f = (const int*)(own + flags_off) + b * AR_MAXR + tid;
+    long spins = 0;
+    while (ar_load_flag(f) < ep) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > spin_limit) {
+        __hip_atomic_store((int*)(own + err_off), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(AR_T) void allreduce_twoshot_kernel(ARArgs a) {
+  const int b = blockIdx.x, tid = threadIdx.x, R = a.world;
+  const long e0 = (long)b * AR_CHUNK;
+  const long e1 = min(a.n, e0 + AR_CHUNK);
+  uint8_t* own = a.bufs[a.rank];
+  int* counter = (int*)(own + AR2_CNT) + b;
+  const int ep = *counter + 1;
+  const long boff = (long)b * AR_CHUNK * 4;                        // this block's bytes in a slot
+  const long dslot = AR2_DATA + (long)(ep & 1) * AR2_SLOT + boff;   // inputs
+  const long rslot = AR2_DATA + (long)(2 + (ep & 1)) * AR2_SLOT + boff;  // reduced sub-ranges
+  const int esz = a.bf16 ? 2 : 4;
+  // 1. local chunk -> own data slot
+  {
+    const uint8_t* src = (const uint8_t*)a.in + e0 * esz;
+    uint8_t* dst = own + dslot;
+    const long bytes = (e1 - e0) * esz, v16 = bytes >> 4;
+    for (long i = tid; i < v16; i += AR_T) ((u32x4*)dst)[i] = ((const u32x4*)src)[i];
+    for (long i = (v16 << 4) + tid; i < bytes; i += AR_T) dst[i] = src[i];
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  ar_signal(a.bufs, R, a.rank, AR2_F1, b, ep, tid);
+  ar_wait(own, R, a.rank, AR2_F1, AR2_ERR, b, ep, tid, a.spin_limit);
+  // 2. reduce-scatter: this rank's sub-range of the block (multiples of 8 elements)
+  const long sub = ((AR_CHUNK / R) + 7) & ~7L;
+  const long s0 = min(e1, e0 + (long)a.rank * sub), s1 = min(e1, s0 + sub);
+  for (long i = s0 + tid * 8; i < s1; i += AR_T * 8) {
+    const int cnt = (int)min(8L, s1 - i);
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int r = 0; r < R; ++r) {
+      const uint8_t* src = a.bufs[r] + dslot + (i - e0) * esz;
+      if (a.bf16) {
+        if (cnt == 8) {
+          const bf16x8 v = *(const bf16x8*)src;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[j] += (float)v[j];
+        } else {
+          for (int j = 0; j < cnt; ++j) acc[j] += (float)((const bf16*)src)[j];
+        }
+      } else {
+        if (cnt == 8) {
+          const f32x4 v0 = *(const f32x4*)src, v1 = *(const f32x4*)(src + 16);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            acc[j] += v0[j];
+            acc[j + 4] += v1[j];
+          }
+        } else {
+          for (int j = 0; j < cnt; ++j) acc[j] += ((const float*)src)[j];
+        }
+      }
+    }
+    uint8_t* dst = own + rslot + (i - e0) * esz;
+    if (a.bf16) {
+      for (int j = 0; j < cnt; ++j) ((bf16*)dst)[j] = (bf16)acc[j];
+    } else {
+      for (int j = 0; j < cnt; ++j) ((float*)dst)[j] = acc[j];
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  ar_signal(a.bufs, R, a.rank, AR2_F2, b, ep, tid);
+  ar_wait(own, R, a.rank, AR2_F2, AR2_ERR, b, ep, tid, a.spin_limit);
+  // 3. all-gather: every rank's reduced sub-range, from its result slot, into out
+  {
+    const long bytes = (e1 - e0) * esz, v16 = bytes >> 4;
+    const long subb = sub * esz;  // a sub-range is a multiple of 16 bytes
+    for (long i = tid; i < v16; i += AR_T) {
+      const int q = (int)min((long)R - 1, (i << 4) / subb);
+      ((u32x4*)((uint8_t*)a.out + e0 * esz))[i] = ((const u32x4*)(a.bufs[q] + rslot))[i];
+    }
+    for (long i = (v16 << 4) + tid; i < bytes; i += AR_T) {
+      const int q = (int)min((long)R - 1, i / subb);
+      ((uint8_t*)a.out + e0 * esz)[i] = (a.bufs[q] + rslot)[i];
+    }
+  }
+  if (tid == 0) *counter = ep;
+}
+
 }  // namespace la
 
 // C ABI ---------------------------------------------------------------------------
+extern "C" long la_ar2_buffer_bytes() { return la::AR2_DATA + 4 * la::AR2_SLOT; }
+extern "C" long la_ar2_max_elems() { return (long)la::AR2_MAXB * la::AR_CHUNK; }
+extern "C" long la_ar2_err_offset() { return la::AR2_ERR; }
+
+extern "C" int la_allreduce_twoshot(const void* in, void* out, long n, int bf16, int rank, int world,
+                                    const void* const* bufs, long spin_limit, void* stream) {
+  using namespace la;
+  if (world < 1 || world > AR_MAXR || rank < 0 || rank >= world || n < 1) return -1;
+  if (n > (long)AR2_MAXB * AR_CHUNK) return -2;
+  ARArgs a{};
+  a.in = in;
+  a.out = out;
+  a.n = n;
+  a.bf16 = bf16;
+  a.rank = rank;
+  a.world = world;
+  a.spin_limit = spin_limit;
+  for (int r = 0; r < world; ++r) {
+    if (!bufs[r]) return -1;
+    a.bufs[r] = (uint8_t*)bufs[r];
+  }
+  const int nb = (int)((n + AR_CHUNK - 1) / AR_CHUNK);
+  hipLaunchKernelGGL(allreduce_twoshot_kernel, dim3(nb), dim3(AR_T), 0, (hipStream_t)stream, a);
+  return (int)hipGetLastError();
+}
 extern "C" long la_ar_buffer_bytes() { return la::AR_DATA + 2 * la::AR_SLOT; }
 extern "C" long la_ar_max_elems() { return la::AR_MAXB * la::AR_CHUNK; }
 extern "C" long la_ar_err_offset() { return la::AR_ERR; }

@@ -1,6 +1,6 @@
-"""One-shot all-reduce over IPC-mapped peer buffers (ops/csrc/allreduce.hip) for the tensor-parallel
-decode messages; RCCL stays the path for anything larger (prefill chunks) or when peer mapping is
-unavailable.  SURVEY §2.9 (planned TP collective shapes) and §2.11 (custom one-shot all-reduce
+"""One-shot and two-shot all-reduce over IPC-mapped peer buffers (ops/csrc/allreduce.hip) for the
+tensor-parallel messages up to 4 M elements (decode rows of any batch, small prefill chunks); RCCL
+stays the path for anything larger or when peer mapping is unavailable.  SURVEY §2.9 (planned TP collective shapes) and §2.11 (custom one-shot all-reduce
 over peer-mapped IPC buffers, hipIpcGetMemHandle).  The reference has no collective of its own:
 its only tensor parallelism is vLLM's NCCL (backend/python/vllm/backend.py:102-103).
 
@@ -54,71 +54,85 @@ class CustomAllReduce:
     # (err flag set, result wrong) instead of a hung GPU
     SPIN_LIMIT = 1 << 20
 
-    def __init__(self, group, rank: int, world: int, device: torch.device):
+    def __init__(self, group, rank: int, world: int, device: torch.device, twoshot: Optional[bool] = None):
         from .. import ops
         import torch.distributed as dist
         if world < 2 or world > 8:
             raise ValueError("custom all-reduce needs 2..8 ranks")
         self.rank, self.world, self.device = rank, world, torch.device(device)
         self.L = ops.lib()
-        self.L.la_ar_buffer_bytes.restype = ctypes.c_long
-        self.L.la_ar_max_elems.restype = ctypes.c_long
-        self.L.la_ar_err_offset.restype = ctypes.c_long
-        self.L.la_allreduce_oneshot.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_long, ctypes.c_int,
-                                                ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_long,
-                                                ctypes.c_void_p]
-        self.L.la_allreduce_oneshot.restype = ctypes.c_int
-        self.max_elems = int(self.L.la_ar_max_elems())
-        self.nbytes = int(self.L.la_ar_buffer_bytes())
+        for f in ("la_ar_buffer_bytes", "la_ar_max_elems", "la_ar_err_offset", "la_ar2_buffer_bytes",
+                  "la_ar2_max_elems", "la_ar2_err_offset"):
+            getattr(self.L, f).restype = ctypes.c_long
+        for f in ("la_allreduce_oneshot", "la_allreduce_twoshot"):
+            getattr(self.L, f).argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_long, ctypes.c_int,
+                                           ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_long,
+                                           ctypes.c_void_p]
+            getattr(self.L, f).restype = ctypes.c_int
+        if twoshot is None:
+            twoshot = os.environ.get("LOCALAI_AMD_AR_TWOSHOT", "1") != "0"
+        self.max_elems = int(self.L.la_ar_max_elems())          # one-shot: latency-bound decode rows
+        self.max_elems2 = int(self.L.la_ar2_max_elems()) if twoshot else 0  # two-shot: wide batches
+        # one region per protocol: (bytes, error-word offset)
+        sizes = [int(self.L.la_ar_buffer_bytes())] + ([int(self.L.la_ar2_buffer_bytes())] if twoshot else [])
+        self.err_offs = [int(self.L.la_ar_err_offset())] + ([int(self.L.la_ar2_err_offset())] if twoshot else [])
+        self.nbytes = sizes[0]
         self.hip = _hip()
+        self.owns: List[int] = []
         self.own = None
         self._opened: List[int] = []
         err = ""
         with torch.cuda.device(self.device):
             # every rank reaches every collective below whatever fails locally, and all of them
             # agree at the end: a group where one rank cannot map a peer must stay on RCCL
-            hb = b""
+            hbs: List[bytes] = []
             try:
-                ptr = ctypes.c_void_p()
-                self._check(self.hip.hipMalloc(ctypes.byref(ptr), self.nbytes), "hipMalloc")
-                self.own = ptr.value
-                self._check(self.hip.hipMemset(ctypes.c_void_p(self.own), 0, self.nbytes), "hipMemset")
+                for nb in sizes:
+                    ptr = ctypes.c_void_p()
+                    self._check(self.hip.hipMalloc(ctypes.byref(ptr), nb), "hipMalloc")
+                    self.owns.append(ptr.value)
+                    self._check(self.hip.hipMemset(ctypes.c_void_p(ptr.value), 0, nb), "hipMemset")
                 torch.cuda.synchronize(self.device)
-                hnd = _HipIpcHandle()
-                self._check(self.hip.hipIpcGetMemHandle(ctypes.byref(hnd), ctypes.c_void_p(self.own)),
-                            "hipIpcGetMemHandle")
-                hb = ctypes.string_at(ctypes.addressof(hnd), HIP_IPC_HANDLE_SIZE)  # .reserved stops at a NUL
+                for o in self.owns:
+                    hnd = _HipIpcHandle()
+                    self._check(self.hip.hipIpcGetMemHandle(ctypes.byref(hnd), ctypes.c_void_p(o)),
+                                "hipIpcGetMemHandle")
+                    hbs.append(ctypes.string_at(ctypes.addressof(hnd), HIP_IPC_HANDLE_SIZE))  # .reserved stops at a NUL
             except Exception as e:  # noqa: BLE001
                 err = str(e)
-            handles: List[Optional[bytes]] = [None] * world
-            dist.all_gather_object(handles, hb, group=group)
-            self.ptrs: List[int] = []
-            for r, h_bytes in enumerate(handles):
-                if r == rank:
-                    self.ptrs.append(self.own or 0)
-                    continue
-                if err or not h_bytes or len(h_bytes) != HIP_IPC_HANDLE_SIZE:
-                    err = err or f"rank {r} exported no handle"
-                    self.ptrs.append(0)
-                    continue
-                try:
-                    h = _HipIpcHandle()
-                    ctypes.memmove(ctypes.addressof(h), h_bytes, HIP_IPC_HANDLE_SIZE)
-                    p = ctypes.c_void_p()
-                    self._check(self.hip.hipIpcOpenMemHandle(ctypes.byref(p), h, _hipIpcMemLazyEnablePeerAccess),
-                                f"hipIpcOpenMemHandle(rank {r})")
-                    self.ptrs.append(p.value)
-                    self._opened.append(p.value)
-                except Exception as e:  # noqa: BLE001
-                    err = str(e)
-                    self.ptrs.append(0)
+            self.own = self.owns[0] if self.owns else None
+            handles: List[Optional[list]] = [None] * world
+            dist.all_gather_object(handles, hbs, group=group)
+            self.ptr_sets: List[List[int]] = [[] for _ in sizes]
+            for r, h_list in enumerate(handles):
+                for k in range(len(sizes)):
+                    if r == rank:
+                        self.ptr_sets[k].append(self.owns[k] if k < len(self.owns) else 0)
+                        continue
+                    h_bytes = h_list[k] if h_list and k < len(h_list) else None
+                    if err or not h_bytes or len(h_bytes) != HIP_IPC_HANDLE_SIZE:
+                        err = err or f"rank {r} exported no handle"
+                        self.ptr_sets[k].append(0)
+                        continue
+                    try:
+                        h = _HipIpcHandle()
+                        ctypes.memmove(ctypes.addressof(h), h_bytes, HIP_IPC_HANDLE_SIZE)
+                        p = ctypes.c_void_p()
+                        self._check(self.hip.hipIpcOpenMemHandle(ctypes.byref(p), h, _hipIpcMemLazyEnablePeerAccess),
+                                    f"hipIpcOpenMemHandle(rank {r})")
+                        self.ptr_sets[k].append(p.value)
+                        self._opened.append(p.value)
+                    except Exception as e:  # noqa: BLE001
+                        err = str(e)
+                        self.ptr_sets[k].append(0)
             oks: List[Optional[str]] = [None] * world
             dist.all_gather_object(oks, err, group=group)
             bad = [f"rank {r}: {m}" for r, m in enumerate(oks) if m]
             if bad:
                 self.close()
                 raise RuntimeError("; ".join(bad))
-        self._bufs = (ctypes.c_void_p * world)(*self.ptrs)
+        self.ptrs = self.ptr_sets[0]
+        self._bufs = [(ctypes.c_void_p * world)(*ps) for ps in self.ptr_sets]
 
     @staticmethod
     def _check(rc: int, what: str):
@@ -127,35 +141,44 @@ class CustomAllReduce:
 
     def supports(self, t: torch.Tensor) -> bool:
         return (t.is_cuda and t.dtype in (torch.float32, torch.bfloat16) and t.is_contiguous()
-                and 0 < t.numel() <= self.max_elems)
+                and 0 < t.numel() <= max(self.max_elems, self.max_elems2))
 
     def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
-        """In place; the caller checks supports(t).  Runs on the current stream."""
-        rc = self.L.la_allreduce_oneshot(t.data_ptr(), t.data_ptr(), t.numel(), int(t.dtype == torch.bfloat16),
-                                         self.rank, self.world, self._bufs, self.SPIN_LIMIT,
-                                         torch.cuda.current_stream(self.device).cuda_stream)
+        """In place; the caller checks supports(t).  Runs on the current stream: one-shot up to
+        max_elems (one flag round trip, every rank reads all copies), two-shot beyond (reduce-
+        scatter + all-gather: ~2n bytes read per rank instead of world x n)."""
+        two = t.numel() > self.max_elems
+        fn = self.L.la_allreduce_twoshot if two else self.L.la_allreduce_oneshot
+        rc = fn(t.data_ptr(), t.data_ptr(), t.numel(), int(t.dtype == torch.bfloat16), self.rank, self.world,
+                self._bufs[1 if two else 0], self.SPIN_LIMIT, torch.cuda.current_stream(self.device).cuda_stream)
         if rc != 0:
-            raise RuntimeError(f"la_allreduce_oneshot failed with code {rc}")
+            raise RuntimeError(f"la_allreduce_{'twoshot' if two else 'oneshot'} failed with code {rc}")
         return t
 
     def timed_out(self) -> bool:
         """True if a wait ever hit the spin limit (a peer never arrived): results since are suspect."""
-        v = ctypes.c_int(0)
         torch.cuda.synchronize(self.device)
-        self._check(self.hip.hipMemcpy(ctypes.byref(v), ctypes.c_void_p(self.own + int(self.L.la_ar_err_offset())),
-                                       4, 2), "hipMemcpy")  # hipMemcpyDeviceToHost
-        return v.value != 0
+        for own, off in zip(self.owns, self.err_offs):
+            v = ctypes.c_int(0)
+            self._check(self.hip.hipMemcpy(ctypes.byref(v), ctypes.c_void_p(own + off), 4, 2),
+                        "hipMemcpy")  # hipMemcpyDeviceToHost
+            if v.value:
+                return True
+        return False
 
     def close(self):
-        if getattr(self, "own", None) is None:
+        if not getattr(self, "owns", None):
+            self.own = None
             return
         try:
             torch.cuda.synchronize(self.device)
             for p in self._opened:
                 self.hip.hipIpcCloseMemHandle(ctypes.c_void_p(p))
             self._opened = []
-            self.hip.hipFree(ctypes.c_void_p(self.own))
+            for o in self.owns:
+                self.hip.hipFree(ctypes.c_void_p(o))
         finally:
+            self.owns = []
             self.own = None
 
 

@@ -35,7 +35,11 @@ def main():
     dist.init_process_group("gloo")
     car = CustomAllReduce(dist.group.WORLD, rank, world, dev)
     cases = [(4096, torch.float32), (3 * 4096, torch.float32), (4096, torch.bfloat16), (1000, torch.float32),
-             (64 * 4096, torch.float32), (car.max_elems, torch.bfloat16), (4096 + 8, torch.bfloat16)]
+             (64 * 4096, torch.float32), (car.max_elems, torch.bfloat16), (4096 + 8, torch.bfloat16),
+             # two-shot (reduce-scatter + all-gather) past the one-shot's size: a decode batch of 256
+             # rows of 4096 (fp32 and bf16), a ragged size, the largest size
+             (256 * 4096, torch.float32), (256 * 4096, torch.bfloat16), (car.max_elems + 1000 + 3, torch.float32),
+             (car.max_elems2, torch.bfloat16)]
     for call, (n, dt) in enumerate(cases):
         t = inputs(rank, n, dt, dev, call)
         car.all_reduce(t)
@@ -43,8 +47,9 @@ def main():
         ref = expected(world, n, dt, dev, call)
         err = (t.float() - ref.float()).abs().max().item()
         assert err == 0.0, (rank, n, dt, err)
-    # graph capture: three calls of mixed sizes, replayed twice with fresh inputs
-    bufs = [torch.empty(n, dtype=dt, device=dev) for n, dt in cases[:3]]
+    # graph capture: calls of mixed sizes (one-shot and two-shot), replayed twice with fresh inputs
+    gcases = cases[:3] + [cases[7]]
+    bufs = [torch.empty(n, dtype=dt, device=dev) for n, dt in gcases]
     srcs = [torch.empty_like(b) for b in bufs]
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
@@ -56,12 +61,12 @@ def main():
                 car.all_reduce(b)
     torch.cuda.current_stream().wait_stream(s)
     for rep in range(2):
-        for i, (n, dt) in enumerate(cases[:3]):
+        for i, (n, dt) in enumerate(gcases):
             srcs[i].copy_(inputs(rank, n, dt, dev, 100 + 10 * rep + i))
         dist.barrier()
         g.replay()
         torch.cuda.synchronize()
-        for i, (n, dt) in enumerate(cases[:3]):
+        for i, (n, dt) in enumerate(gcases):
             ref = expected(world, n, dt, dev, 100 + 10 * rep + i)
             assert (bufs[i].float() - ref.float()).abs().max().item() == 0.0, (rank, "graph", rep, i)
     assert not car.timed_out()
@@ -74,6 +79,14 @@ def main():
         car.all_reduce(t)
     torch.cuda.synchronize()
     us = (time.perf_counter() - t0) / 200 * 1e6
+    t = inputs(rank, 256 * 4096, torch.float32, dev, 8)   # a 256-row decode batch: two-shot
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(50):
+        car.all_reduce(t)
+    torch.cuda.synchronize()
+    us2 = (time.perf_counter() - t0) / 50 * 1e6
     dist.barrier()
     car.close()
     # a late peer: rank 1 arrives ~1.5 s after rank 0, whose spin limit is tiny -> rank 0's wait
@@ -101,7 +114,8 @@ def main():
     assert (t2.float().cpu() - ref).abs().max().item() < 1e-5, rank
     dist.barrier()
     if rank == 0:
-        print(f"AR_OK world={world} one-row all-reduce {us:.1f} us/call")
+        print(f"AR_OK world={world} one-row all-reduce {us:.1f} us/call, 256-row (4 MiB fp32, two-shot) "
+              f"{us2:.1f} us/call")
     dist.destroy_process_group()
 
 
