@@ -1,7 +1,9 @@
 """CLIP ViT image encoder + LLaVA projector, loaded from a llama.cpp `mmproj` GGUF (the reference
 reaches this through grpc-server.cpp -> llava/clip.cpp).
 
-Preprocessing (PIL decode -> resize -> center crop / pad -> normalise) runs on the host; the ViT
+Preprocessing: PIL decodes on the host; on the GPU the resize (PIL-exact BICUBIC), centre crop /
+letterbox, normalisation and tiling run in two HIP launches per resized image (ops/csrc/image.hip,
+K26); on the CPU the same steps run through PIL.  The ViT
 runs on the device in bf16: patch embedding as one GEMM over unfolded patches (im2col), fused
 QKV, SDPA attention, LayerNorm / quick-GELU, the two-layer GELU projector into the LLM's
 embedding space.  LLaVA-1.5 (one 336^2 tile -> 576 embeddings) and LLaVA-1.6 "anyres"
@@ -14,6 +16,7 @@ from __future__ import annotations
 import base64
 import io
 import math
+import os
 from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -121,8 +124,38 @@ class ClipVision:
         return best
 
     def preprocess(self, data) -> Tuple[torch.Tensor, Optional[Tuple[int, int, int, int]]]:
-        """-> (tiles [n, 3, S, S], anyres layout (grid_w, grid_h, orig_w, orig_h) or None)."""
+        """-> (tiles [n, 3, S, S], anyres layout (grid_w, grid_h, orig_w, orig_h) or None).  On the
+        GPU the resize / crop / letterbox / normalise / tiling run in the image kernels
+        (ops.image_tiles, PIL-exact bicubic); LOCALAI_AMD_CLIP_HOST_PREPROC=1 keeps the PIL path."""
         img = decode_image(data)
+        if self.device.type == "cuda" and os.environ.get("LOCALAI_AMD_CLIP_HOST_PREPROC", "0") != "1":
+            return self._preprocess_device(img)
+        return self._preprocess_host(img)
+
+    def _placements(self, w: int, h: int):
+        """The PIL path's geometry as kernel placements: (n_tiles, placements, layout)."""
+        S = self.image_size
+        if not self.pinpoints or self.merge == "flat":
+            sc = S / min(w, h)
+            rw, rh = max(S, round(w * sc)), max(S, round(h * sc))
+            return 1, [dict(ow=rw, oh=rh, cw=S, ch=S, ox=-((rw - S) // 2), oy=-((rh - S) // 2), t0=0)], None
+        bw, bh = self._best_resolution(w, h)
+        sc = min(bw / w, bh / h)
+        nw, nh = max(1, int(w * sc)), max(1, int(h * sc))
+        fill = tuple(int(255 * m) for m in self.mean)
+        pls = [dict(ow=S, oh=S, cw=S, ch=S, t0=0),  # base image first
+               dict(ow=nw, oh=nh, cw=bw, ch=bh, ox=(bw - nw) // 2, oy=(bh - nh) // 2, t0=1, fill=fill)]
+        return 1 + (bw // S) * (bh // S), pls, (bw // S, bh // S, w, h)
+
+    def _preprocess_device(self, img):
+        from .. import ops
+        w, h = img.size
+        n, pls, layout = self._placements(w, h)
+        u8 = torch.from_numpy(np.ascontiguousarray(np.asarray(img, dtype=np.uint8))).to(self.device)
+        out = torch.empty(n, 3, self.image_size, self.image_size, dtype=torch.float32, device=self.device)
+        return ops.image_tiles(u8, pls, out, self.mean, self.std), layout
+
+    def _preprocess_host(self, img) -> Tuple[torch.Tensor, Optional[Tuple[int, int, int, int]]]:
         if not self.pinpoints or self.merge == "flat":
             return self._norm(self._resize_square(img)).unsqueeze(0), None
         from PIL import Image

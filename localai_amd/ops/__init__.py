@@ -11,6 +11,7 @@ bad call fails in Python instead of faulting the device.
 from __future__ import annotations
 
 import ctypes
+import functools
 import math
 import os
 import threading
@@ -77,6 +78,8 @@ def lib():
             "la_pen_push": [P, I, P, I, P, P, P, P],
             "la_qgemm_glu": [I, P, P, P, I, P, P, P, I, I, I, P, I, I, P, I, I, I, P],
             "la_decode_advance": [P, P, P, P, P, P, I, I, I, P, I, P, P, P],
+            "la_img_resample_h": [P, I, I, P, I, P, P, I, P],
+            "la_img_resample_v_tiles": [P, I, I, P, P, I, I, I, I, I, I, I, P, P, P, P, P],
         }
         for name, args in sig.items():
             fn = getattr(L, name)
@@ -1705,6 +1708,82 @@ def groupnorm_supported(x: torch.Tensor, groups: int) -> bool:
     return (x.is_contiguous(memory_format=torch.channels_last) and groups <= 64 and 256 % (2 * groups) == 0
             and C % groups == 0
             and (C // groups) % 2 == 0 and C <= 2048)
+
+
+# ---------------------------------------------------------------------------------------
+# Image preprocessing (K26): PIL-exact bicubic resample + placement + normalise + tiles
+# ---------------------------------------------------------------------------------------
+
+def _bicubic(x: float) -> float:
+    a = -0.5
+    x = abs(x)
+    if x < 1.0:
+        return ((a + 2.0) * x - (a + 3.0)) * x * x + 1
+    if x < 2.0:
+        return (((x - 5) * x + 8) * x - 4) * a
+    return 0.0
+
+
+@functools.lru_cache(maxsize=64)
+def pil_bicubic_coeffs(in_size: int, out_size: int) -> Tuple[np.ndarray, np.ndarray, int]:
+    """PIL's precompute_coeffs + normalize_coeffs_8bpc for BICUBIC (Resample.c): per output
+    index the first source index and count, and int32 weights in 22-bit fixed point."""
+    scale = in_size / out_size
+    filterscale = max(scale, 1.0)
+    support = 2.0 * filterscale
+    ksize = int(math.ceil(support)) * 2 + 1
+    bounds = np.zeros((out_size, 2), dtype=np.int32)
+    kk = np.zeros((out_size, ksize), dtype=np.int32)
+    ss = 1.0 / filterscale
+    for xx in range(out_size):
+        center = (xx + 0.5) * scale
+        xmin = max(int(center - support + 0.5), 0)
+        xmax = min(int(center + support + 0.5), in_size) - xmin
+        w = [_bicubic((x + xmin - center + 0.5) * ss) for x in range(xmax)]
+        ww = sum(w)
+        for x in range(xmax):
+            c = w[x] / ww if ww != 0.0 else w[x]
+            kk[xx, x] = int(-0.5 + c * (1 << 22)) if c < 0 else int(0.5 + c * (1 << 22))
+        bounds[xx] = (xmin, xmax)
+    return bounds, kk, ksize
+
+
+_IMG_TABLES: dict = {}
+
+
+def _img_tables(in_size: int, out_size: int, device):
+    key = (in_size, out_size, str(device))
+    t = _IMG_TABLES.get(key)
+    if t is None:
+        b, k, ks = pil_bicubic_coeffs(in_size, out_size)
+        t = _IMG_TABLES[key] = (torch.from_numpy(b).to(device), torch.from_numpy(k).to(device), ks)
+    return t
+
+
+def image_tiles(img: torch.Tensor, placements: Sequence[dict], out: torch.Tensor, mean, std) -> torch.Tensor:
+    """img: uint8 [H, W, 3] on the GPU.  Each placement resizes the image to (ow, oh) with PIL's
+    BICUBIC (bit-exact), puts it at (ox, oy) on a (cw, ch) canvas filled with `fill`, and writes the
+    canvas' S x S tiles, normalised, into out[t0 + i] (out: fp32 [n, 3, S, S])."""
+    H, W, _ = img.shape
+    S = out.shape[-1]
+    assert img.dtype == torch.uint8 and img.is_contiguous() and out.is_contiguous() and out.dtype == torch.float32
+    m = torch.tensor(list(mean), dtype=torch.float32, device=img.device)
+    sd = torch.tensor(list(std), dtype=torch.float32, device=img.device)
+    for pl in placements:
+        ow, oh, cw, ch = int(pl["ow"]), int(pl["oh"]), int(pl["cw"]), int(pl["ch"])
+        if cw % S or ch % S or pl["t0"] + (cw // S) * (ch // S) > out.shape[0]:
+            raise ValueError("image_tiles: canvas does not tile the output")
+        bh, kh, ksh = _img_tables(W, ow, img.device)
+        bv, kv, ksv = _img_tables(H, oh, img.device)
+        tmp = torch.empty(H, ow, 3, dtype=torch.uint8, device=img.device)
+        _check(lib().la_img_resample_h(img.data_ptr(), H, W, tmp.data_ptr(), ow, bh.data_ptr(), kh.data_ptr(), ksh,
+                                       _stream()), "la_img_resample_h")
+        fill = torch.tensor(list(pl.get("fill", (0, 0, 0))), dtype=torch.int32, device=img.device)
+        _check(lib().la_img_resample_v_tiles(tmp.data_ptr(), oh, ow, bv.data_ptr(), kv.data_ptr(), ksv, ch, cw,
+                                             int(pl.get("oy", 0)), int(pl.get("ox", 0)), S, int(pl["t0"]),
+                                             m.data_ptr(), sd.data_ptr(), fill.data_ptr(), out.data_ptr(), _stream()),
+               "la_img_resample_v_tiles")
+    return out
 
 
 def groupnorm_nhwc(x: torch.Tensor, groups: int, weight: Optional[torch.Tensor], bias: Optional[torch.Tensor],

@@ -145,6 +145,7 @@ __global__ __launch_bounds__(AR_T) void allreduce_oneshot_kernel(ARArgs a) {
 // kernel (every read of this rank's epoch-e slots) has finished.  Every element is reduced once,
 // by its owner, in rank order (fp32), so all ranks hold identical bits.
 constexpr int AR2_MAXB = 4096;
+constexpr int AR2_GRID = 128;  // persistent workgroups (see allreduce_twoshot_kernel)
 constexpr long AR2_F1 = 0, AR2_F2 = (long)AR2_MAXB * AR_MAXR * 4, AR2_CNT = 2 * AR2_F2,
                AR2_ERR = AR2_CNT + AR2_MAXB * 4;
 constexpr long AR2_DATA = 524288;                 // header rounded up (512 KiB)
@@ -178,8 +179,9 @@ LA_DEV void ar_wait(uint8_t* own, int world, int rank, long flags_off, long err_
   __syncthreads();
 }
 
-__global__ __launch_bounds__(AR_T) void allreduce_twoshot_kernel(ARArgs a) {
-  const int b = blockIdx.x, tid = threadIdx.x, R = a.world;
+// One chunk (1024 elements) of the two-shot protocol, run by one workgroup.
+LA_DEV void ar2_chunk(const ARArgs& a, int b) {
+  const int tid = threadIdx.x, R = a.world;
   const long e0 = (long)b * AR_CHUNK;
   const long e1 = min(a.n, e0 + AR_CHUNK);
   uint8_t* own = a.bufs[a.rank];
@@ -255,6 +257,15 @@ __global__ __launch_bounds__(AR_T) void allreduce_twoshot_kernel(ARArgs a) {
     }
   }
   if (tid == 0) *counter = ep;
+  __syncthreads();  // the next chunk of this workgroup reuses the same LDS-free, register-only path
+}
+
+// Persistent grid of at most AR2_GRID workgroups, each walking chunks g, g + G, ... in order: the
+// waits of chunk c only ever target the peers' workgroup that walks the same chunk sequence, and
+// a grid this small is co-resident with the peers' grids (even with every rank on one GPU), so no
+// wait can depend on a workgroup that is not running.
+__global__ __launch_bounds__(AR_T) void allreduce_twoshot_kernel(ARArgs a, int nb) {
+  for (int c = blockIdx.x; c < nb; c += gridDim.x) ar2_chunk(a, c);
 }
 
 }  // namespace la
@@ -282,7 +293,8 @@ extern "C" int la_allreduce_twoshot(const void* in, void* out, long n, int bf16,
     a.bufs[r] = (uint8_t*)bufs[r];
   }
   const int nb = (int)((n + AR_CHUNK - 1) / AR_CHUNK);
-  hipLaunchKernelGGL(allreduce_twoshot_kernel, dim3(nb), dim3(AR_T), 0, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(allreduce_twoshot_kernel, dim3(nb < AR2_GRID ? nb : AR2_GRID), dim3(AR_T), 0,
+                     (hipStream_t)stream, a, nb);
   return (int)hipGetLastError();
 }
 extern "C" long la_ar_buffer_bytes() { return la::AR_DATA + 2 * la::AR_SLOT; }

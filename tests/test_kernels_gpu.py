@@ -740,3 +740,37 @@ def test_moe_router_fused(E, k, renorm, scale, ep):
         for e, wv in zip(i_ref[t].tolist(), w_ref[t].tolist()):
             if e != L:  # remote experts' weights are not compared (their rows are skipped)
                 assert abs(got[e] - wv) < 1e-4 * max(1.0, scale)
+
+
+@pytest.mark.parametrize("pinpoints", [None, [112, 56, 56, 112, 112, 112]])
+def test_clip_image_preprocess_kernel_matches_pil(tmp_path, pinpoints):
+    """K26 on the device (ops/csrc/image.hip): PIL-exact BICUBIC resize (same coefficient tables,
+    22-bit fixed point, uint8 horizontal pass), centre crop or anyres letterbox with the mean-colour
+    fill, normalisation and tiling equal the PIL host path for images of several sizes."""
+    import io
+
+    import numpy as np
+    from PIL import Image
+
+    from localai_amd.models import synth
+    from localai_amd.models.clip import ClipVision
+    mm = synth.write_mmproj(str(tmp_path / "mm.gguf"), out_dim=64, dim=64, n_layer=1, heads=4, ffn=128,
+                            image_size=56, patch=14, pinpoints=pinpoints)
+    cv = ClipVision(mm, torch.device("cuda:0"))
+    rng = np.random.default_rng(0)
+    for (w, h) in [(64, 48), (300, 120), (57, 203), (56, 56), (500, 333)]:
+        a = (rng.random((h, w, 3)) * 255).astype(np.uint8)
+        buf = io.BytesIO()
+        Image.fromarray(a).save(buf, format="PNG")
+        dev, lay_d = cv.preprocess(buf.getvalue())
+        host, lay_h = cv._preprocess_host(Image.fromarray(a))
+        assert lay_d == lay_h and tuple(dev.shape) == tuple(host.shape), (w, h)
+        assert float((dev.cpu() - host).abs().max()) < 1e-5, (w, h)
+    emb_d = cv.embed_image(buf.getvalue())
+    import os
+    os.environ["LOCALAI_AMD_CLIP_HOST_PREPROC"] = "1"
+    try:
+        emb_h = cv.embed_image(buf.getvalue())
+    finally:
+        del os.environ["LOCALAI_AMD_CLIP_HOST_PREPROC"]
+    assert torch.equal(emb_d, emb_h)
