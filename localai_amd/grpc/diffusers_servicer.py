@@ -1,5 +1,6 @@
 """`diffusers` / `stablediffusion` backend servicer (backend.proto LoadModel + GenerateImage) over
-the native Stable Diffusion pipeline (models/sd.py).
+the native Stable Diffusion 1.x / 2.x / XL pipeline (models/sd.py) and FLUX.1 (models/flux.py,
+`pipeline_type: FluxPipeline` or a FluxPipeline model_index.json).
 
 Mirrors `backend/python/diffusers/backend.py`: LoadModel keeps `CFGScale` (7 when unset),
 `CLIPSkip` and `SchedulerType`; GenerateImage uses `step` (1 when unset), width / height,
@@ -36,9 +37,11 @@ class DiffusersServicer:
         return pb.StatusResponse(state=self.state)
 
     async def LoadModel(self, request, context=None):
+        from ..models.flux import FluxPipeline, is_flux_pipeline
         from ..models.sd import StableDiffusion, is_sd_pipeline
         path = request.ModelFile or request.Model
-        if not is_sd_pipeline(path):
+        flux = is_flux_pipeline(path) or str(request.PipelineType or "").startswith("Flux")
+        if not (is_sd_pipeline(path) or (flux and os.path.isdir(path))):
             return pb.Result(success=False, message=f"not a diffusers pipeline directory: {path}")
         dev = self.device
         if not dev:
@@ -50,9 +53,13 @@ class DiffusersServicer:
         if cn and not os.path.isfile(os.path.join(cn, "config.json")):
             return pb.Result(success=False, message=f"ControlNet model not found: {request.ControlNet}")
         try:
-            p = await asyncio.get_running_loop().run_in_executor(
-                None, lambda: StableDiffusion(path, dev, request.SchedulerType, int(request.CLIPSkip or 0),
-                                              controlnet=cn))
+            if flux:  # backend.py:247-251: FluxPipeline; GenerateImage adds max_sequence_length=256
+                p = await asyncio.get_running_loop().run_in_executor(
+                    None, lambda: FluxPipeline(path, dev, max_sequence_length=256))
+            else:
+                p = await asyncio.get_running_loop().run_in_executor(
+                    None, lambda: StableDiffusion(path, dev, request.SchedulerType, int(request.CLIPSkip or 0),
+                                                  controlnet=cn))
         except Exception as e:  # noqa: BLE001 - reported to the caller like the reference
             return pb.Result(success=False, message=f"Unexpected {e!r}")
         self.pipe, self.state = p, pb.StatusResponse.READY
@@ -77,16 +84,17 @@ class DiffusersServicer:
         h = int(kw.get("height") or default_px)
         image = request.src or None   # backend.py: options["image"] = Image.open(request.src) -> img2img
         control = None
-        if image is not None and p.controlnet is not None:
+        if image is not None and getattr(p, "controlnet", None) is not None:
             control, image = image, None  # backend.py:403: with a ControlNet, src is the control image
         if image is not None:
             # the reference passes width / height only when asked; img2img keeps the source's size otherwise
             w = int(kw["width"]) if kw.get("width") else 0
             h = int(kw["height"]) if kw.get("height") else 0
         with self._lock:
+            extra = {"image": image, "control_image": control} if image is not None or control is not None else {}
             img = p(request.positive_prompt, kw.get("negative_prompt", ""), w, h,
                     steps=int(kw.get("num_inference_steps", 50)), guidance_scale=self.cfg_scale,
-                    seed=request.seed if request.seed > 0 else None, image=image, control_image=control)
+                    seed=request.seed if request.seed > 0 else None, **extra)
             p.save(img, request.dst)
 
     async def GenerateImage(self, request, context=None):

@@ -462,7 +462,9 @@ class VaeDecoder(nn.Module):
         g = int(c.get("norm_num_groups", 32))
         lat = int(c.get("latent_channels", 4))
         self.scaling = float(c.get("scaling_factor", 0.18215))
-        self.post_quant_conv = nn.Conv2d(lat, lat, 1)
+        self.shift = float(c.get("shift_factor") or 0.0)   # FLUX / SD3 VAEs: z / scaling + shift
+        # FLUX / SD3 VAEs have no post-quant convolution (use_post_quant_conv: false)
+        self.post_quant_conv = nn.Conv2d(lat, lat, 1) if c.get("use_post_quant_conv", True) else nn.Identity()
         d = nn.Module()
         d.conv_in = nn.Conv2d(lat, ch[-1], 3, padding=1)
         d.mid_block = nn.Module()
@@ -483,7 +485,7 @@ class VaeDecoder(nn.Module):
 
     def forward(self, z):
         d = self.decoder
-        h = d.conv_in(self.post_quant_conv(z / self.scaling))
+        h = d.conv_in(self.post_quant_conv(z / self.scaling + self.shift))
         h = d.mid_block.resnets[1](d.mid_block.attentions[0](d.mid_block.resnets[0](h)))
         for b in d.up_blocks:
             for r in b.resnets:
@@ -521,7 +523,8 @@ class VaeEncoder(nn.Module):
         e.conv_norm_out = nn.GroupNorm(g, ch[-1], eps=1e-6)
         e.conv_out = nn.Conv2d(ch[-1], 2 * lat, 3, padding=1)
         self.encoder = e
-        self.quant_conv = nn.Conv2d(2 * lat, 2 * lat, 1)
+        self.quant_conv = nn.Conv2d(2 * lat, 2 * lat, 1) if c.get("use_quant_conv", True) else nn.Identity()
+        self.shift = float(c.get("shift_factor") or 0.0)
 
     def forward(self, img: torch.Tensor, gen: Optional[torch.Generator] = None) -> torch.Tensor:
         """img [B, 3, H, W] in [-1, 1] -> scaled latents (a sample of the latent distribution)."""
@@ -537,7 +540,7 @@ class VaeEncoder(nn.Module):
         mean, logvar = m.chunk(2, dim=1)
         std = torch.exp(0.5 * logvar.clamp(-30.0, 20.0))
         eps = torch.randn(mean.shape, generator=gen).to(mean.device)
-        return (mean + std * eps) * self.scaling
+        return (mean + std * eps - self.shift) * self.scaling
 
 
 def _vae_enc_names(sd: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:

@@ -955,3 +955,97 @@ def write_controlnet(out_dir: str, pipe_dir: str, seed: int = 0, zero: bool = Tr
     save_file({k: v.contiguous() for k, v in m.state_dict().items()},
               os.path.join(out_dir, "diffusion_pytorch_model.safetensors"))
     return out_dir
+
+
+FLUX_DEV_TRANSFORMER = dict(in_channels=64, num_layers=19, num_single_layers=38, attention_head_dim=128,
+                            num_attention_heads=24, joint_attention_dim=4096, pooled_projection_dim=768,
+                            guidance_embeds=True, axes_dims_rope=[16, 56, 56], patch_size=1)
+FLUX_VAE = dict(SD15_VAE, latent_channels=16, scaling_factor=0.3611, shift_factor=0.1159,
+                use_post_quant_conv=False, use_quant_conv=False)
+FLUX_SCHEDULER = {"_class_name": "FlowMatchEulerDiscreteScheduler", "base_image_seq_len": 256, "base_shift": 0.5,
+                  "max_image_seq_len": 4096, "max_shift": 1.15, "num_train_timesteps": 1000, "shift": 3.0,
+                  "use_dynamic_shifting": True}
+
+
+def _t5_byte_tokenizer(out_dir: str) -> int:
+    """A byte-level tokenizer.json for a toy T5 (pad 0, eos 1 appended, unk 2) + its config."""
+    from tokenizers import Tokenizer, decoders, models, pre_tokenizers, processors
+    bs = list(range(ord("!"), ord("~") + 1)) + list(range(0xA1, 0xAD)) + list(range(0xAE, 0x100))
+    cs, n = bs[:], 0
+    for b in range(256):
+        if b not in bs:
+            bs.append(b)
+            cs.append(256 + n)
+            n += 1
+    vocab = {"<pad>": 0, "</s>": 1, "<unk>": 2}
+    for c in cs:
+        vocab[chr(c)] = len(vocab)
+    tk = Tokenizer(models.BPE(vocab=vocab, merges=[], unk_token="<unk>"))
+    tk.pre_tokenizer = pre_tokenizers.ByteLevel(add_prefix_space=False)
+    tk.decoder = decoders.ByteLevel()
+    tk.post_processor = processors.TemplateProcessing(single="$A </s>", special_tokens=[("</s>", 1)])
+    os.makedirs(out_dir, exist_ok=True)
+    tk.save(os.path.join(out_dir, "tokenizer.json"))
+    with open(os.path.join(out_dir, "tokenizer_config.json"), "w") as f:
+        json.dump({"pad_token": "<pad>", "eos_token": "</s>", "unk_token": "<unk>",
+                   "tokenizer_class": "PreTrainedTokenizerFast"}, f)
+    return len(vocab)
+
+
+def write_flux_pipeline(out_dir: str, size: str = "tiny", seed: int = 0, guidance: bool = True) -> str:
+    """Random-init FLUX.1 pipeline directory in the diffusers layout (model_index.json,
+    transformer/, text_encoder/ (CLIPTextModel), text_encoder_2/ (T5EncoderModel), tokenizer/,
+    tokenizer_2/, vae/ (16-channel KL-VAE), scheduler/).  size="dev": FLUX.1-dev shapes (12 B
+    transformer); "tiny": a toy with the same structure."""
+    import torch
+    import transformers as tf
+    from safetensors.torch import save_file
+
+    from .flux import FluxTransformer
+    from .sd import VaeDecoder, VaeEncoder
+    torch.manual_seed(seed)
+    for sub in ("transformer", "vae", "text_encoder", "text_encoder_2", "tokenizer", "tokenizer_2", "scheduler"):
+        os.makedirs(os.path.join(out_dir, sub), exist_ok=True)
+    vocab = _clip_byte_vocab()
+    sp = dict(vocab_size=len(vocab), bos_token_id=vocab["<|startoftext|>"], eos_token_id=vocab["<|endoftext|>"],
+              pad_token_id=vocab["<|endoftext|>"])
+    n_t5 = _t5_byte_tokenizer(os.path.join(out_dir, "tokenizer_2"))
+    if size == "dev":
+        trc, vc = dict(FLUX_DEV_TRANSFORMER), dict(FLUX_VAE)
+        tc = dict(SD15_TEXT, **sp)
+        t5c = dict(vocab_size=32128, d_model=4096, d_kv=64, d_ff=10240, num_layers=24, num_heads=64,
+                   feed_forward_proj="gated-gelu")
+    else:
+        tc = dict(SD15_TEXT, hidden_size=32, num_hidden_layers=2, num_attention_heads=2, intermediate_size=64, **sp)
+        t5c = dict(vocab_size=n_t5, d_model=48, d_kv=8, d_ff=96, num_layers=2, num_heads=4,
+                   feed_forward_proj="gated-gelu")
+        trc = dict(FLUX_DEV_TRANSFORMER, num_layers=1, num_single_layers=2, attention_head_dim=16,
+                   num_attention_heads=2, joint_attention_dim=48, pooled_projection_dim=32, axes_dims_rope=[4, 6, 6])
+        vc = dict(FLUX_VAE, block_out_channels=[16, 32], layers_per_block=1, norm_num_groups=8)
+    trc["guidance_embeds"] = guidance
+    dt = torch.bfloat16 if size == "dev" else torch.float32
+    m = FluxTransformer(trc)
+    with open(os.path.join(out_dir, "transformer", "config.json"), "w") as f:
+        json.dump(dict(trc, _class_name="FluxTransformer2DModel"), f)
+    save_file({k: v.to(dt).contiguous() for k, v in m.state_dict().items()},
+              os.path.join(out_dir, "transformer", "diffusion_pytorch_model.safetensors"))
+    del m
+    sd = VaeDecoder(vc).state_dict()
+    sd.update(VaeEncoder(vc).state_dict())
+    with open(os.path.join(out_dir, "vae", "config.json"), "w") as f:
+        json.dump(dict(vc, _class_name="AutoencoderKL"), f)
+    save_file({k: v.to(dt).contiguous() for k, v in sd.items()},
+              os.path.join(out_dir, "vae", "diffusion_pytorch_model.safetensors"))
+    tf.CLIPTextModel(tf.CLIPTextConfig(**tc)).save_pretrained(os.path.join(out_dir, "text_encoder"),
+                                                              safe_serialization=True)
+    t5 = tf.T5EncoderModel(tf.T5Config(**t5c))
+    t5.to(dt).save_pretrained(os.path.join(out_dir, "text_encoder_2"), safe_serialization=True)
+    with open(os.path.join(out_dir, "tokenizer", "vocab.json"), "w") as f:
+        json.dump(vocab, f)
+    with open(os.path.join(out_dir, "tokenizer", "merges.txt"), "w") as f:
+        f.write("#version: 0.2\n")
+    with open(os.path.join(out_dir, "scheduler", "scheduler_config.json"), "w") as f:
+        json.dump(FLUX_SCHEDULER, f)
+    with open(os.path.join(out_dir, "model_index.json"), "w") as f:
+        json.dump({"_class_name": "FluxPipeline"}, f)
+    return out_dir
