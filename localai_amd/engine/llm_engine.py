@@ -669,10 +669,15 @@ class LLMEngine:
         """Sampler features the captured decode graph cannot run: mirostat v1, grammars, more logit
         biases than its table holds, or a penalty window longer than PEN_CAP tokens.  Penalties
         over shorter windows run in the graph (penalty ring), so they keep multi-step decode."""
+        return bool(r.params.grammar) or self._needs_host_sampler(r)
+
+    def _needs_host_sampler(self, r: Request) -> bool:
+        """Sampler features the in-graph sampler cannot run (grammars aside): those force the whole
+        batch onto the host sampler; a grammar alone only needs its own rows fixed up."""
         p = r.params
         pen = p.repeat_penalty != 1.0 or p.frequency_penalty != 0.0 or p.presence_penalty != 0.0
         window = p.repeat_last_n if p.repeat_last_n >= 0 else self.ctx
-        return ((pen and window > self.PEN_CAP) or p.mirostat == 1 or bool(p.grammar)
+        return ((pen and window > self.PEN_CAP) or p.mirostat == 1
                 or len(p.logit_bias) + len(self.tokenizer.eog) > self.cfg.bias_capacity)
 
     def _lookahead(self) -> int:
@@ -796,8 +801,29 @@ class LLMEngine:
             g = self._graphs[Bp] = self._capture(Bp)
         graph, st, logits = g
         device_sampling = not any(self._needs_host_sampling(r) for r in reqs)
+        if not device_sampling and not any(self._needs_host_sampler(r) for r in reqs):
+            # grammar rows only: one step with the in-graph sampler for EVERY row (penalties, bias,
+            # mirostat 2 included), then the grammar rows' samples are checked on the host and
+            # the rejected ones resampled from this step's logits restricted to grammar-valid
+            # tokens (_apply_grammar); unconstrained rows take the native emitter as in a run
+            self._upload_step_inputs(st, reqs, Bp, tok, pos, slots, lens, bt, True)
+            graph.replay()
+            toks = st["hist"][0, :B].cpu().numpy().copy()
+            toks = self._apply_grammar(reqs, logits[:B], st["prm_np"], toks)
+            if any(r.params.mirostat == 2 for r in reqs):
+                muh = st["mu"][:B].cpu().numpy()
+                for j, r in enumerate(reqs):
+                    r.mu = float(muh[j])
+            plain = [j for j, r in enumerate(reqs) if r.grammar is None]
+            if plain:
+                self._emit_run([reqs[j] for j in plain], toks[plain][None, :].astype(np.int32), 1)
+            now = time.perf_counter()
+            for j, r in enumerate(reqs):
+                if r.grammar is not None:
+                    self._on_token(r, int(toks[j]), now)
+            return
         self._upload_step_inputs(st, reqs, Bp, tok, pos, slots, lens, bt, device_sampling)
-        if not device_sampling:  # penalties / mirostat v1 / grammar: one step, host-driven sampling
+        if not device_sampling:  # long penalty windows / mirostat v1 / bias overflow: host sampling
             graph.replay()
             self._sample_and_emit(ids, logits[:B])
             return

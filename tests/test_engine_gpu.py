@@ -248,3 +248,38 @@ def test_draft_model_speculation_on_gpu(tiny_model_path):
     assert got == base
     m = eng.metrics
     assert m["spec_steps"] > 0 and m["spec_accepted"] == m["spec_drafted"] > 0
+
+
+def test_grammar_rows_fixed_up_beside_device_sampling(tiny_model_path):
+    """A batch with grammar-constrained rows keeps the in-graph sampler for every row (plain,
+    penalised, constrained) and only re-samples the constrained rows the grammar rejects: the
+    streams equal the host-driven eager engine's, and every constrained output obeys its grammar."""
+    import re
+
+    def run(eng):
+        outs = {}
+        specs = [("plain one", dict(max_tokens=14, temperature=0.0, ignore_eos=True)),
+                 ("letters only", dict(max_tokens=14, temperature=0.0, ignore_eos=True, grammar="root ::= [a-z ]+")),
+                 ("penalised", dict(max_tokens=14, temperature=0.0, ignore_eos=True, repeat_penalty=1.5,
+                                    repeat_last_n=8)),
+                 ("digits", dict(max_tokens=10, temperature=0.0, ignore_eos=True, grammar='root ::= [0-9]+ "x"')),
+                 ("plain two", dict(max_tokens=14, temperature=0.0, ignore_eos=True))]
+
+        def mk(i):
+            buf = bytearray()
+
+            def cb(ev):
+                buf.extend(ev.text)
+                if ev.finished:
+                    outs[i] = (bytes(buf), ev.completion_tokens, ev.finish_reason)
+            return cb
+        for i, (p, sp) in enumerate(specs):
+            eng.add_request(p, SamplingParams(**sp), mk(i))
+        while len(outs) < len(specs):
+            eng.step()
+        return [outs[i] for i in range(len(specs))]
+    eager = run(LLMEngine(EngineConfig(model_path=tiny_model_path, device="cuda:0", context_size=256, max_num_seqs=8,
+                                       max_batched_tokens=512, use_graphs=False)))
+    graph = run(_eng(tiny_model_path, 8))
+    assert graph == eager
+    assert re.fullmatch(rb"[a-z ]+", graph[1][0]) and re.fullmatch(rb"[0-9]*x?", graph[3][0])
