@@ -1,6 +1,7 @@
 """`diffusers` / `stablediffusion` backend servicer (backend.proto LoadModel + GenerateImage) over
-the native Stable Diffusion 1.x / 2.x / XL pipeline (models/sd.py) and FLUX.1 (models/flux.py,
-`pipeline_type: FluxPipeline` or a FluxPipeline model_index.json).
+the native Stable Diffusion 1.x / 2.x / XL pipeline (models/sd.py), FLUX.1 (models/flux.py,
+`pipeline_type: FluxPipeline` or a FluxPipeline model_index.json) and Stable Diffusion 3
+(models/sd3.py, `pipeline_type: StableDiffusion3Pipeline`).
 
 Mirrors `backend/python/diffusers/backend.py`: LoadModel keeps `CFGScale` (7 when unset),
 `CLIPSkip` and `SchedulerType`; GenerateImage uses `step` (1 when unset), width / height,
@@ -39,9 +40,11 @@ class DiffusersServicer:
     async def LoadModel(self, request, context=None):
         from ..models.flux import FluxPipeline, is_flux_pipeline
         from ..models.sd import StableDiffusion, is_sd_pipeline
+        from ..models.sd3 import SD3Pipeline, is_sd3_pipeline
         path = request.ModelFile or request.Model
         flux = is_flux_pipeline(path) or str(request.PipelineType or "").startswith("Flux")
-        if not (is_sd_pipeline(path) or (flux and os.path.isdir(path))):
+        sd3 = is_sd3_pipeline(path) or str(request.PipelineType or "") == "StableDiffusion3Pipeline"
+        if not (is_sd_pipeline(path) or ((flux or sd3) and os.path.isdir(path))):
             return pb.Result(success=False, message=f"not a diffusers pipeline directory: {path}")
         dev = self.device
         if not dev:
@@ -56,6 +59,9 @@ class DiffusersServicer:
             if flux:  # backend.py:247-251: FluxPipeline; GenerateImage adds max_sequence_length=256
                 p = await asyncio.get_running_loop().run_in_executor(
                     None, lambda: FluxPipeline(path, dev, max_sequence_length=256))
+            elif sd3:  # backend.py:235-246: StableDiffusion3Pipeline
+                p = await asyncio.get_running_loop().run_in_executor(
+                    None, lambda: SD3Pipeline(path, dev, clip_skip=int(request.CLIPSkip or 0)))
             else:
                 p = await asyncio.get_running_loop().run_in_executor(
                     None, lambda: StableDiffusion(path, dev, request.SchedulerType, int(request.CLIPSkip or 0),

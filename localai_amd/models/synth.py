@@ -1049,3 +1049,61 @@ def write_flux_pipeline(out_dir: str, size: str = "tiny", seed: int = 0, guidanc
     with open(os.path.join(out_dir, "model_index.json"), "w") as f:
         json.dump({"_class_name": "FluxPipeline"}, f)
     return out_dir
+
+
+SD3_TRANSFORMER = dict(sample_size=128, patch_size=2, in_channels=16, num_layers=24, attention_head_dim=64,
+                       num_attention_heads=24, joint_attention_dim=4096, caption_projection_dim=1536,
+                       pooled_projection_dim=2048, out_channels=16, pos_embed_max_size=192)
+SD3_VAE = dict(FLUX_VAE, scaling_factor=1.5305, shift_factor=0.0609)
+
+
+def write_sd3_pipeline(out_dir: str, seed: int = 0, t5: bool = True) -> str:
+    """Random-init toy StableDiffusion3Pipeline directory (diffusers layout: transformer/, vae/,
+    text_encoder/ + text_encoder_2/ (CLIPTextModelWithProjection), text_encoder_3/ (T5, optional),
+    tokenizer/, tokenizer_2/, tokenizer_3/, scheduler/ (FlowMatch, shift 3))."""
+    import torch
+    import transformers as tf
+    from safetensors.torch import save_file
+
+    from .sd import VaeDecoder, VaeEncoder
+    from .sd3 import SD3Transformer
+    torch.manual_seed(seed)
+    subs = ["transformer", "vae", "text_encoder", "text_encoder_2", "tokenizer", "tokenizer_2", "scheduler"]
+    for sub in subs:
+        os.makedirs(os.path.join(out_dir, sub), exist_ok=True)
+    vocab = _clip_byte_vocab()
+    sp = dict(vocab_size=len(vocab), bos_token_id=vocab["<|startoftext|>"], eos_token_id=vocab["<|endoftext|>"],
+              pad_token_id=vocab["<|endoftext|>"])
+    for sub, hid, nl in (("text_encoder", 32, 2), ("text_encoder_2", 48, 3)):
+        c = dict(SD15_TEXT, hidden_size=hid, num_hidden_layers=nl, num_attention_heads=2, intermediate_size=2 * hid,
+                 projection_dim=16, hidden_act="gelu", **sp)
+        tf.CLIPTextModelWithProjection(tf.CLIPTextConfig(**c)).save_pretrained(os.path.join(out_dir, sub),
+                                                                              safe_serialization=True)
+    for tk in ("tokenizer", "tokenizer_2"):
+        with open(os.path.join(out_dir, tk, "vocab.json"), "w") as f:
+            json.dump(vocab, f)
+        with open(os.path.join(out_dir, tk, "merges.txt"), "w") as f:
+            f.write("#version: 0.2\n")
+    if t5:
+        n_t5 = _t5_byte_tokenizer(os.path.join(out_dir, "tokenizer_3"))
+        tf.T5EncoderModel(tf.T5Config(vocab_size=n_t5, d_model=96, d_kv=8, d_ff=128, num_layers=2, num_heads=4,
+                                      feed_forward_proj="gated-gelu")).save_pretrained(
+            os.path.join(out_dir, "text_encoder_3"), safe_serialization=True)
+    trc = dict(SD3_TRANSFORMER, sample_size=16, num_layers=2, attention_head_dim=16, num_attention_heads=2,
+               joint_attention_dim=96, caption_projection_dim=32, pooled_projection_dim=32, pos_embed_max_size=24)
+    m = SD3Transformer(trc)
+    with open(os.path.join(out_dir, "transformer", "config.json"), "w") as f:
+        json.dump(dict(trc, _class_name="SD3Transformer2DModel"), f)
+    save_file({k: v.contiguous() for k, v in m.state_dict().items()},
+              os.path.join(out_dir, "transformer", "diffusion_pytorch_model.safetensors"))
+    vc = dict(SD3_VAE, block_out_channels=[16, 32], layers_per_block=1, norm_num_groups=8)
+    sd = VaeDecoder(vc).state_dict()
+    sd.update(VaeEncoder(vc).state_dict())
+    with open(os.path.join(out_dir, "vae", "config.json"), "w") as f:
+        json.dump(dict(vc, _class_name="AutoencoderKL"), f)
+    save_file({k: v.contiguous() for k, v in sd.items()}, os.path.join(out_dir, "vae", "diffusion_pytorch_model.safetensors"))
+    with open(os.path.join(out_dir, "scheduler", "scheduler_config.json"), "w") as f:
+        json.dump({"_class_name": "FlowMatchEulerDiscreteScheduler", "num_train_timesteps": 1000, "shift": 3.0}, f)
+    with open(os.path.join(out_dir, "model_index.json"), "w") as f:
+        json.dump({"_class_name": "StableDiffusion3Pipeline"}, f)
+    return out_dir
