@@ -89,8 +89,13 @@ class T5Encoder:
         self.W, self.hp, self.p = W, hp, prefix
 
     def _rms(self, x, name):
+        # T5LayerNorm: fp32 variance; the normalised states go back to a half-precision weight's dtype
+        w = self.W[self.p + name]
         v = x.float().pow(2).mean(-1, keepdim=True)
-        return self.W[self.p + name] * (x * torch.rsqrt(v + self.hp["layer_norm_epsilon"]))
+        h = x * torch.rsqrt(v + self.hp["layer_norm_epsilon"])
+        if w.dtype in (torch.float16, torch.bfloat16):
+            h = h.to(w.dtype)
+        return w * h
 
     def __call__(self, ids: torch.Tensor, mask: Optional[torch.Tensor] = None) -> torch.Tensor:
         """ids [B, T] -> hidden [B, T, d_model]; mask [B, T] (1 = token)."""

@@ -23,17 +23,27 @@ SHAPES = {
     "down4": ([(4096, GGMLType.Q4_K)], 14336),
     "down6": ([(4096, GGMLType.Q6_K)], 14336),
 }
+# Llama-3-70B (d 8192, 64 q / 8 kv heads, ffn 28672)
+SHAPES_70B = {
+    "qkv": ([(9216, GGMLType.Q4_K), (1024, GGMLType.Q6_K)], 8192),
+    "o": ([(8192, GGMLType.Q4_K)], 8192),
+    "gate_up": ([(28672, GGMLType.Q4_K), (28672, GGMLType.Q4_K)], 8192),
+    "down4": ([(8192, GGMLType.Q4_K)], 28672),
+    "down6": ([(8192, GGMLType.Q6_K)], 28672),
+}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--m", type=int, default=1)
     ap.add_argument("--mib", type=int, default=600, help="weight bytes cycled through per graph")
+    ap.add_argument("--preset", default="8b", choices=["8b", "70b"])
     a = ap.parse_args()
     M = a.m
+    shapes = SHAPES_70B if a.preset == "70b" else SHAPES
     print("| shape | bytes/launch (MB) | default S | S:µs (TB/s) |")
     print("|---|---:|---:|---|")
-    for name, (parts, K) in SHAPES.items():
+    for name, (parts, K) in shapes.items():
         one = sum(n * K * (0.5625 if t == GGMLType.Q4_K else 0.8203) for n, t in parts)
         copies = max(2, int(a.mib * 2 ** 20 // one))
         sets = [[rand_qweight(n, K, t, seed=100 * c + i) for i, (n, t) in enumerate(parts)] for c in range(copies)]

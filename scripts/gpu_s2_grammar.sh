@@ -3,7 +3,7 @@
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp LOCALAI_AMD_CACHE=/tmp/la_cache
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_engine_gpu.py::test_grammar_rows_fixed_up_beside_device_sampling tests/test_flux.py tests/test_sd.py::test_controlnet_on_gpu_graph -m gpu -v --timeout 280 --timeout-method thread -p no:cacheprovider > gpurun_out/s2_gr.log 2>&1
+timeout -k 10 600 python -u -m pytest tests/test_engine_gpu.py::test_grammar_rows_fixed_up_beside_device_sampling tests/test_flux.py tests/test_sd3.py tests/test_sd.py::test_controlnet_on_gpu_graph -m gpu -v --timeout 280 --timeout-method thread -p no:cacheprovider > gpurun_out/s2_gr.log 2>&1
 rc=$?
 grep -E "PASSED|FAILED|passed|failed" gpurun_out/s2_gr.log | tail -6
 [ $rc -eq 0 ] || exit $rc
