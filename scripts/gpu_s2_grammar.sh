@@ -13,4 +13,6 @@ grep "decode" gpurun_out/s2_mixed2.log
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 500 python scripts/fc_bench.py --concurrency 32 > gpurun_out/s2_fc32.log 2>&1; rc=$?; tail -1 gpurun_out/s2_fc32.log | cut -c1-400
 [ $rc -eq 0 ] || exit $rc
-timeout -k 10 120 python scripts/lmhead_bmm_check.py > gpurun_out/s2_lmhead.log 2>&1; rc=$?; grep LMHEAD gpurun_out/s2_lmhead.log; exit $rc
+timeout -k 10 120 python scripts/lmhead_bmm_check.py > gpurun_out/s2_lmhead.log 2>&1; rc=$?; grep LMHEAD gpurun_out/s2_lmhead.log
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python scripts/gemv_sweep.py --preset 70b > gpurun_out/s2_gemv70b.md 2>&1; rc=$?; grep -v amdgpu.ids gpurun_out/s2_gemv70b.md; exit $rc

@@ -119,3 +119,35 @@ def test_model_manager_two_cpu_replicas(tiny_model_path, tmp_path):
             assert o == alone, (p, o, alone)
         await mm.stop_all()
     asyncio.run(run())
+
+
+def test_model_manager_process_replicas_over_grpc(tiny_model_path, tmp_path):
+    """engine_mode=process: each replica is its own worker process (one per GPU on a node) behind a
+    persistent gRPC channel; the replica handle spreads concurrent streams over both."""
+    from localai_amd.config.app_config import ApplicationConfig
+    from localai_amd.config.backend_config import BackendConfig
+    from localai_amd.gateway.model_manager import ModelManager
+    shutil.copy(tiny_model_path, tmp_path / "tiny.gguf")
+    ac = ApplicationConfig(models_path=str(tmp_path))
+    ac.engine_mode = "process"
+    mm = ModelManager(ac, str(tmp_path))
+    cfg = BackendConfig({"name": "tiny", "backend": "localai-amd", "context_size": 256, "replicas": 2,
+                         "parameters": {"model": "tiny.gguf"}})
+
+    async def collect(h, prompt):
+        out = b""
+        async for rep in h.PredictStream(pb.PredictOptions(Prompt=prompt, Tokens=5, Temperature=0.0, IgnoreEOS=True)):
+            out += rep.message
+        return out
+
+    async def run():
+        lm = await mm.load(cfg)
+        try:
+            rb = lm.handle
+            assert isinstance(rb, ReplicaBackend) and len(rb.replicas) == 2 and lm.process is not None
+            outs = await asyncio.gather(*(collect(rb, f"process replica {i}") for i in range(4)))
+            assert all(outs) and all(rb.served)
+            assert await mm._check_alive(lm)
+        finally:
+            await mm.stop_all()
+    asyncio.run(run())
