@@ -196,7 +196,9 @@ class ModelManager:
             log.warning("backend for %s is unhealthy; respawning", lm.id)
             self.models.pop(lm.id, None)
             try:
-                if lm.servicer is not None and getattr(lm.servicer, "engine", None) is not None:
+                if isinstance(lm.servicer, _ReplicaServicers):
+                    lm.servicer.shutdown()  # every replica engine, not just the first
+                elif lm.servicer is not None and getattr(lm.servicer, "engine", None) is not None:
                     lm.servicer.engine.shutdown()
                 if lm.process is not None:
                     lm.process.kill()
