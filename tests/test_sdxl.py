@@ -114,3 +114,15 @@ def test_sdxl_on_gpu_graph_matches_eager(xl_dir):
     # replays and eager agree up to bf16 rounding (library GEMMs may reduce in a different order)
     assert p_close(a, b) and p_close(b, c) and p_close(b, d)
     assert pipe._graphs
+
+
+def test_sdxl_img2img(xl_dir, tmp_path):
+    """SDXL with a source image (diffusers StableDiffusionXLImg2ImgPipeline semantics: the VAE
+    encoder's latents noised to `strength`); strength 0 returns the source through the VAE."""
+    from PIL import Image
+    src = tmp_path / "src.png"
+    Image.fromarray((torch.rand(64, 64, 3) * 255).to(torch.uint8).numpy()).save(src)
+    pipe = StableDiffusion(xl_dir, device="cpu")
+    a = pipe("a red fox", steps=4, seed=2, width=64, height=64, image=str(src), strength=0.5)
+    b = pipe("a red fox", steps=4, seed=2, width=64, height=64, image=str(src), strength=0.9)
+    assert a.shape == (64, 64, 3) and not torch.equal(a, b)
