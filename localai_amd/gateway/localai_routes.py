@@ -13,8 +13,8 @@ from .. import __version__
 from ..config.backend_config import BackendConfig
 from ..grpc import backend_pb as pb
 from .metrics import CONTENT_TYPE
-from .model_manager import (BARK_BACKENDS, ENGINE_BACKENDS, HF_BACKENDS, MAMBA_BACKEND, MUSICGEN_BACKENDS, RWKV_BACKEND,
-                            SD_BACKENDS, STORE_BACKEND, VITS_BACKENDS)
+from .model_manager import (BARK_BACKENDS, ENGINE_BACKENDS, HF_BACKENDS, MAMBA_BACKEND, MUSICGEN_BACKENDS,
+                            PARLER_BACKENDS, RWKV_BACKEND, SD_BACKENDS, STORE_BACKEND, VITS_BACKENDS)
 from . import schema as sc
 from .openai_routes import APIError, merge_request_with_config, model_from_context, read_request, typed_body
 
@@ -50,7 +50,7 @@ def build_router(state) -> APIRouter:
 
     async def system():
         backends = sorted(set(b for b in ENGINE_BACKENDS if b) | HF_BACKENDS | SD_BACKENDS | VITS_BACKENDS |
-                          MUSICGEN_BACKENDS | BARK_BACKENDS | {MAMBA_BACKEND, RWKV_BACKEND}) + \
+                          MUSICGEN_BACKENDS | BARK_BACKENDS | PARLER_BACKENDS | {MAMBA_BACKEND, RWKV_BACKEND}) + \
             [STORE_BACKEND] + list(state.cfg.external_grpc_backends)
         from ..utils.sysinfo import system_info
         return {"backends": backends, "loaded_models": [{"id": m.id} for m in state.manager.list_loaded()],

@@ -44,6 +44,7 @@ SD_BACKENDS = {"diffusers", "stablediffusion", "tinydream"}  # Stable Diffusion 
 VITS_BACKENDS = {"piper", "vits", "mms-tts"}    # VITS text-to-speech voices (models/tts.py)
 MUSICGEN_BACKENDS = {"transformers-musicgen", "musicgen"}  # text-to-music (models/musicgen.py)
 BARK_BACKENDS = {"bark"}                         # text-to-speech/audio (models/bark.py)
+PARLER_BACKENDS = {"parler-tts", "parler_tts"}   # description-conditioned TTS (models/parler.py)
 
 
 def free_port() -> int:
@@ -251,10 +252,11 @@ class ModelManager:
             if not res.success:
                 raise RuntimeError(f"could not load model: {res.message}")
             return LoadedModel(mid, backend, EmbeddedBackend(sv), servicer=sv)
-        if backend in VITS_BACKENDS | MUSICGEN_BACKENDS | BARK_BACKENDS:
+        if backend in VITS_BACKENDS | MUSICGEN_BACKENDS | BARK_BACKENDS | PARLER_BACKENDS:
             from ..grpc import audio_servicer as au
             cls = (au.VitsServicer if backend in VITS_BACKENDS else
-                   au.MusicgenServicer if backend in MUSICGEN_BACKENDS else au.BarkServicer)
+                   au.MusicgenServicer if backend in MUSICGEN_BACKENDS else
+                   au.ParlerServicer if backend in PARLER_BACKENDS else au.BarkServicer)
             sv = cls(device=self._pick_device(cfg))
             res = await sv.LoadModel(grpc_model_options(cfg, self.app, self.models_path), None)
             if not res.success:

@@ -4,10 +4,11 @@ SoundGeneration) over the native audio models.
   piper / vits / mms-tts     VITS voices (models/tts.py)        -- backend/go/tts/piper.go:30-49
   transformers-musicgen      MusicGen (models/musicgen.py)      -- backend/python/transformers-musicgen/backend.py:66,121
   bark                       Bark (models/bark.py)              -- backend/python/bark/backend.py:44
+  parler-tts                 Parler-TTS (models/parler.py)      -- backend/python/parler-tts/backend.py:71-90
 
 TTS writes a 16-bit PCM wav to `request.dst` and answers `Result(success=True)`, as the
 reference backends do.  `voice` selects a speaker id of a multi-speaker VITS voice (a number) or
-a Bark history prompt name; `language` is accepted and ignored (the voice fixes the language).
+a Bark history prompt name, or a Parler-TTS speaker description; `language` is accepted and ignored (the voice fixes the language).
 """
 from __future__ import annotations
 
@@ -147,6 +148,29 @@ class BarkServicer(_AudioBase):
             raise RuntimeError("no model loaded")
         with self._lock:
             audio = m.generate(request.text, voice=request.voice)
+        write_wav(request.dst, audio, m.sampling_rate)
+
+    async def TTS(self, request, context=None):
+        return await self._run(self._tts, request)
+
+
+class ParlerServicer(_AudioBase):
+    """parler-tts: TTS where `voice` is the natural-language speaker description."""
+    kind = "parler-tts"
+
+    def _load(self, path):
+        from ..models.parler import ParlerTTS, is_parler_dir
+        if not is_parler_dir(path):
+            raise ValueError("not a Parler-TTS checkpoint directory (config.json model_type 'parler_tts')")
+        return ParlerTTS(path, self._dev())
+
+    def _tts(self, request):
+        from ..models.tts import write_wav
+        m = self.model
+        if m is None:
+            raise RuntimeError("no model loaded")
+        with self._lock:
+            audio = m.generate(request.text, description=request.voice)
         write_wav(request.dst, audio, m.sampling_rate)
 
     async def TTS(self, request, context=None):

@@ -396,6 +396,10 @@ def _gemv_splits(ws, K: int, M: int) -> int:
         # 1.06 B/weight (vs 0.56 for Q4_K): each split already streams twice the bytes, and half
         # the splits measured fastest (Llama-3-8B Q8_0, M=1: o 9.7 -> 7.8 us, q|k|v 12.7 -> 9.8 us)
         S = max(1, S // 2)
+    if M == 1 and K >= 24576:
+        # 70B-class down projections (K = 28672): 7 splits measured 9 % faster than 4 for Q6_K and
+        # 4 % for Q4_K (profiles/r3_session2_measurements.md, scripts/gemv_sweep.py --preset 70b)
+        S = max(S, 7)
     while nsb % S:
         S -= 1
     mt = 1 if M == 1 else (2 if M == 2 else 4)
