@@ -14,6 +14,7 @@ Decode steps replay per-batch-size HIP graphs (torch.cuda.CUDAGraph == hipGraph 
 """
 from __future__ import annotations
 
+import collections
 import dataclasses
 import hashlib
 import logging
@@ -151,6 +152,10 @@ class LLMEngine:
         self.gvocab = core.GrammarVocab(self.tokenizer.pieces, sorted(self.tokenizer.eog))
         self._eog_list = sorted(self.tokenizer.eog)
         self._grammars: Dict[str, object] = {}
+        # allowed-token masks of grammar parse states, resident on the device (_grammar_mask_slot)
+        self._gmask_cache: "collections.OrderedDict" = collections.OrderedDict()
+        self._gmask_pool: Optional[torch.Tensor] = None
+        self._gmask_free: List[int] = []
         self._mm_embs: Dict[int, list] = {}  # inbox "mm" item -> its images' embeddings (batched encode)
         self.clip = None
         if cfg.mmproj:
@@ -1123,24 +1128,80 @@ class LLMEngine:
             self._on_token(r, int(toks[j]), now)
 
     GRAMMAR_TOPN = 1024
+    GRAMMAR_MASK_BUDGET = 4000   # trie edges a cacheable whole-vocabulary mask walk may feed
+    GRAMMAR_MASK_SLOTS = 512     # device-resident masks (512 x 128 K vocabulary = 64 MB)
+
+    def _grammar_mask_slot(self, r, V: int, dev):
+        """Slot of r's current parse state in the device mask pool; -1 when nothing may follow
+        (the grammar is complete); None when the state is too permissive for a cheap trie walk
+        (inside a JSON string most of the vocabulary is allowed: the top-N filter handles it).
+        Masks are keyed by (grammar text, parse-state hash), so the states a JSON schema's
+        grammar revisits on every request and every row are walked once."""
+        key = (r.params.grammar, r.grammar.key())
+        c = self._gmask_cache
+        if key in c:
+            c.move_to_end(key)
+            return c[key]
+        m = r.grammar.mask_limited(self.GRAMMAR_MASK_BUDGET)
+        if m is None:
+            slot = None
+        elif not m.any():
+            slot = -1
+        else:
+            pool = self._gmask_pool
+            if pool is None or pool.shape[1] != V or pool.device != torch.device(dev):
+                pool = self._gmask_pool = torch.zeros(self.GRAMMAR_MASK_SLOTS, V, dtype=torch.bool, device=dev)
+                self._gmask_free = list(range(self.GRAMMAR_MASK_SLOTS))
+                c.clear()
+            if not self._gmask_free:  # evict the least recently used state that owns a slot
+                victim = next(k for k, v in c.items() if v is not None and v >= 0)
+                self._gmask_free.append(c.pop(victim))
+            slot = self._gmask_free.pop()
+            n = min(len(m), V)
+            pool[slot, :n].copy_(torch.from_numpy(m[:n].astype(bool)))
+        c[key] = slot
+        while len(c) > 4 * self.GRAMMAR_MASK_SLOTS:
+            _, v = c.popitem(last=False)
+            if v is not None and v >= 0:
+                self._gmask_free.append(v)
+        return slot
 
     def _apply_grammar(self, reqs, logits, prm, toks):
         """Constrained decoding: keep the device sample if the grammar accepts it (the common
-        case); otherwise take the device top-N candidates, keep the ones the grammar accepts
-        (whole-vocabulary scan if none is), and re-run the sampler chain on those -- i.e. the
-        sampler's distribution restricted to grammar-valid tokens (llama.cpp resample path)."""
+        case); otherwise re-run the sampler chain on the logits restricted to grammar-valid
+        tokens (llama.cpp resample path).  Rows whose parse state has a cached device mask are
+        re-sampled together on the device in one masked pass; permissive states take the device
+        top-N candidates the grammar accepts (whole-vocabulary scan if none is)."""
         toks = np.array(toks, copy=True)
         need = [j for j, r in enumerate(reqs)
                 if r.grammar is not None and not r.done and not r.grammar.check(int(toks[j]))]
         if not need:
             return toks
-        # one batched top-N and one device->host copy for every row the grammar rejected
-        sub = logits[torch.tensor(need, device=logits.device)].float()
+        dev = logits.device
+        masked, slots, filt = [], [], []
+        for j in need:
+            s = self._grammar_mask_slot(reqs[j], logits.shape[1], dev)
+            if s is None:
+                filt.append(j)
+            elif s < 0:
+                toks[j] = -1  # nothing can follow: the grammar is complete
+            else:
+                masked.append(j)
+                slots.append(s)
+        if masked:
+            sub = logits[torch.tensor(masked, device=dev)].float()
+            allow = self._gmask_pool[torch.tensor(slots, device=dev)]
+            sub.masked_fill_(~allow, float("-inf"))
+            toks[masked] = ops.sample(sub, prm[np.array(masked)]).cpu().numpy()
+        if not filt:
+            return toks
+        # one batched top-N and one device->host copy for the permissive-state rows
+        sub = logits[torch.tensor(filt, device=dev)].float()
         n = min(self.GRAMMAR_TOPN, sub.shape[1])
         vals, idx = torch.topk(sub, n, dim=-1)
         vals_h, idx_h = vals.cpu(), idx.cpu().numpy().astype(np.int32)
         rows_h = None
-        for k, j in enumerate(need):
+        for k, j in enumerate(filt):
             gs = reqs[j].grammar
             ok = gs.filter(idx_h[k]).astype(bool)
             if ok.any():
@@ -1149,7 +1210,7 @@ class LLMEngine:
             else:
                 mask = gs.mask().astype(bool)  # whole vocabulary (byte-trie walk in the native core)
                 if not mask.any():
-                    toks[j] = -1  # nothing can follow: the grammar is complete
+                    toks[j] = -1
                     continue
                 if rows_h is None:
                     rows_h = sub.cpu()

@@ -543,10 +543,62 @@ class GrammarState {
     return out;
   }
 
-  void trie_walk(int node, const std::vector<Stack>& stacks, const Utf8& u, uint8_t* o) const {
+  // whole-vocabulary mask with a bound on the trie edges fed: None when the walk would exceed
+  // `budget` (a permissive state, e.g. inside a JSON string, where most of the vocabulary is
+  // allowed and the full walk costs tens of ms); restrictive states finish far below it
+  py::object mask_limited(long budget) const {
+    const size_t V = v_->size();
+    py::array_t<uint8_t> out(V);
+    auto* o = out.mutable_data();
+    bool ok;
+    {
+      py::gil_scoped_release rel;
+      std::fill(o, o + V, 0);
+      const bool end_ok = can_end();
+      for (int32_t t : v_->eog_list())
+        if (t >= 0 && (size_t)t < V) o[t] = end_ok ? 1 : 0;
+      long left = budget;
+      ok = trie_walk(0, stacks_, u_, o, &left);
+    }
+    if (!ok) return py::none();
+    return std::move(out);
+  }
+
+  // identity of the parse state for mask caching: FNV-1a over the sorted per-stack hashes (stack
+  // order depends on history, the set does not) and the partial UTF-8 code point
+  uint64_t key() const {
+    std::vector<uint64_t> hs;
+    hs.reserve(stacks_.size());
+    for (const Stack& st : stacks_) {
+      uint64_t h = 1469598103934665603ull;
+      for (const El* e : st) {
+        h ^= (uint64_t)(uintptr_t)e;
+        h *= 1099511628211ull;
+      }
+      h ^= st.size();
+      h *= 1099511628211ull;
+      hs.push_back(h);
+    }
+    std::sort(hs.begin(), hs.end());
+    uint64_t h = 1469598103934665603ull;
+    auto mix = [&h](uint64_t x) {
+      for (int i = 0; i < 8; ++i) {
+        h ^= (x >> (8 * i)) & 0xFF;
+        h *= 1099511628211ull;
+      }
+    };
+    for (uint64_t x : hs) mix(x);
+    mix(u_.value);
+    mix(((uint64_t)u_.remain << 32) | u_.min);
+    mix(done_ ? 1 : 0);
+    return h;
+  }
+
+  bool trie_walk(int node, const std::vector<Stack>& stacks, const Utf8& u, uint8_t* o, long* left = nullptr) const {
     const auto& trie = v_->trie();
     std::vector<Stack> st, tmp;
     for (const auto& kv : trie[node].kids) {
+      if (left && --*left < 0) return false;
       st = stacks;
       Utf8 uu = u;
       const std::string one(1, (char)kv.first);
@@ -554,8 +606,9 @@ class GrammarState {
       const TrieNode& child = trie[kv.second];
       if (!child.toks.empty() && partial_ok(st, uu))
         for (int32_t t : child.toks) o[t] = 1;
-      if (!child.kids.empty()) trie_walk(kv.second, st, uu, o);
+      if (!child.kids.empty() && !trie_walk(kv.second, st, uu, o, left)) return false;
     }
+    return true;
   }
 
   bool accept(int tok) {
@@ -611,6 +664,8 @@ void register_grammar(py::module& m) {
       .def("filter", &GrammarState::filter)
       .def("mask", &GrammarState::mask)
       .def("mask_linear", &GrammarState::mask_linear)
+      .def("mask_limited", &GrammarState::mask_limited, py::arg("budget"))
+      .def("key", &GrammarState::key)
       .def("accept", &GrammarState::accept)
       .def("accept_bytes", &GrammarState::accept_bytes)
       .def("can_end", &GrammarState::can_end)

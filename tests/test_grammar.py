@@ -113,3 +113,22 @@ def test_trie_mask_equals_linear_scan():
         if len(ok) == 0:
             break
         assert st.accept(int(rng.choice(list(ok))))
+
+
+def test_mask_limited_and_state_key():
+    """mask_limited() equals mask() when the trie walk fits its edge budget and gives up (None)
+    on permissive states; key() names the parse state independently of the path that reached it
+    (the engine caches device masks under it)."""
+    pieces = [b"", b"1", b"2", b"12", b",", b"1,", b"a", b"ab", b"abc", b"b", b"c", b" "]
+    st = _state('root ::= ([0-9]+ ",")*', pieces)
+    assert (np.asarray(st.mask_limited(10_000)) == np.asarray(st.mask())).all()
+    assert st.mask_limited(1) is None
+    g, v = core.Grammar('root ::= ([0-9]+ ",")*'), core.GrammarVocab(pieces, [0])
+    a, b = core.GrammarState(g, v), core.GrammarState(g, v)   # keys are per Grammar object (the engine caches them)
+    assert a.key() == b.key()
+    assert a.accept_bytes(b"12,") and b.accept_bytes(b"7,")
+    assert a.key() == b.key()                     # same state after different digits
+    assert b.accept_bytes(b"3")
+    assert a.key() != b.key()                     # inside a number vs after a comma
+    free = _state('root ::= [a-c ]*', pieces)
+    assert free.mask_limited(3) is None and free.mask_limited(1000) is not None
