@@ -156,6 +156,7 @@ class LLMEngine:
         self._gmask_cache: "collections.OrderedDict" = collections.OrderedDict()
         self._gmask_pool: Optional[torch.Tensor] = None
         self._gmask_free: List[int] = []
+        self._gmask_over: Dict[tuple, int] = {}   # states whose budgeted walk gave up once
         self._mm_embs: Dict[int, list] = {}  # inbox "mm" item -> its images' embeddings (batched encode)
         self.clip = None
         if cfg.mmproj:
@@ -811,9 +812,22 @@ class LLMEngine:
             # mirostat 2 included), then the grammar rows' samples are checked on the host and
             # the rejected ones resampled from this step's logits restricted to grammar-valid
             # tokens (_apply_grammar); unconstrained rows take the native emitter as in a run
-            self._upload_step_inputs(st, reqs, Bp, tok, pos, slots, lens, bt, True)
+            # rows whose parse state has a cached device mask are masked inside the graph, so
+            # their sample is valid as drawn; the rest are checked and fixed up after the step
+            V = logits.shape[1]
+            gslot = np.full(B, -1, dtype=np.int32)
+            done_rows = []
+            for j, r in enumerate(reqs):
+                if r.grammar is not None and not r.done:
+                    sl = self._grammar_mask_slot(r, V, self.device)
+                    if sl is not None and sl >= 0:
+                        gslot[j] = sl
+                    elif sl is not None:
+                        done_rows.append(j)
+            self._upload_step_inputs(st, reqs, Bp, tok, pos, slots, lens, bt, True, gslot)
             graph.replay()
             toks = st["hist"][0, :B].cpu().numpy().copy()
+            toks[done_rows] = -1
             toks = self._apply_grammar(reqs, logits[:B], st["prm_np"], toks)
             if any(r.params.mirostat == 2 for r in reqs):
                 muh = st["mu"][:B].cpu().numpy()
@@ -876,9 +890,13 @@ class LLMEngine:
                 why, flush = self._REASONS[rs]
                 self._finish(r, why, flush=flush)
 
-    def _upload_step_inputs(self, st, reqs, Bp, tok, pos, slots, lens, bt, device_sampling: bool):
+    def _upload_step_inputs(self, st, reqs, Bp, tok, pos, slots, lens, bt, device_sampling: bool,
+                            gslot: Optional[np.ndarray] = None):
         B = len(reqs)
         h = st["host"]  # one pinned staging block -> one H2D copy per run
+        h["gslot"].fill_(-1)
+        if gslot is not None:
+            h["gslot"][:len(gslot)] = torch.from_numpy(gslot)
         h["tokens"][:] = torch.from_numpy(tok)
         h["pos"][:] = torch.from_numpy(pos)
         h["slots"][:] = torch.from_numpy(slots)
@@ -953,7 +971,7 @@ class LLMEngine:
         layout = [("tokens", Bp), ("pos", Bp), ("slots", Bp), ("lens", Bp), ("bt", Bp * MB), ("step", 1),
                   ("prm", prm_words), ("bias_rows", cap), ("bias_cols", cap), ("bias_vals", cap), ("bias_n", 1),
                   ("mu", Bp), ("phist", Bp * PL), ("pcnt", Bp), ("phl", Bp), ("pcap", Bp), ("pen", Bp * 3),
-                  ("pnl", Bp)]
+                  ("pnl", Bp), ("gslot", Bp)]
         total = sum(n for _, n in layout)
         host_block = torch.zeros(total, dtype=torch.int32).pin_memory()
         dev_block = torch.zeros(total, dtype=torch.int32, device=dev)
@@ -974,7 +992,9 @@ class LLMEngine:
             o += n
         st["slots"].fill_(-1)
         st["lens"].fill_(1)
+        st["gslot"].fill_(-1)
         st["host"], st["host_block"], st["dev_block"] = host, host_block, dev_block
+
         st["prm_np"] = np.zeros(Bp, dtype=ops.SAMPLE_ROW_DTYPE)
         st["bias_np"] = (np.zeros(cap, np.int32), np.zeros(cap, np.int32), np.zeros(cap, np.float32))
         st["next"] = torch.zeros(Bp, dtype=torch.int32, device=dev)
@@ -991,6 +1011,8 @@ class LLMEngine:
             # repeat / frequency / presence penalties over each row's last-n window, kept on the
             # device across the run's steps (rows without penalties return at once)
             ops.penalties(lg, st["phist"], st["phl"], st["pen"], self.tokenizer.nl_id, st["pnl"])
+            # grammar rows whose parse state has a cached mask sample only grammar-valid tokens
+            ops.grammar_mask(lg, st["gslot"], self._gmask_pool_for(lg.shape[1], dev))
             ops.sample(lg, st["prm_np"], mu=st["mu"], params_dev=st["prm"], out=st["next"])
             ops.penalty_push(st["next"], st["phist"], st["pcnt"], st["phl"], st["pcap"])
             ops.decode_advance(st["next"], st["tokens"], st["pos"], st["lens"], st["slots"], st["bt"], bs,
@@ -1128,13 +1150,26 @@ class LLMEngine:
             self._on_token(r, int(toks[j]), now)
 
     GRAMMAR_TOPN = 1024
-    GRAMMAR_MASK_BUDGET = 4000   # trie edges a cacheable whole-vocabulary mask walk may feed
+    GRAMMAR_MASK_BUDGET = 1500   # trie edges a first-sight whole-vocabulary mask walk may feed (~0.5 ms)
     GRAMMAR_MASK_SLOTS = 512     # device-resident masks (512 x 128 K vocabulary = 64 MB)
+
+    def _gmask_pool_for(self, V: int, dev) -> torch.Tensor:
+        """The device mask pool ([slots, V] bool); allocated once before the first graph capture
+        (the captured grammar_mask kernel holds its address) and never reallocated on the GPU."""
+        pool = self._gmask_pool
+        if pool is None or pool.shape[1] != V or pool.device != torch.device(dev):
+            if pool is not None and pool.is_cuda and self._graphs:
+                raise RuntimeError("grammar mask pool shape changed after graph capture")
+            pool = self._gmask_pool = torch.zeros(self.GRAMMAR_MASK_SLOTS, V, dtype=torch.bool, device=dev)
+            self._gmask_free = list(range(self.GRAMMAR_MASK_SLOTS))
+            self._gmask_cache.clear()
+        return pool
 
     def _grammar_mask_slot(self, r, V: int, dev):
         """Slot of r's current parse state in the device mask pool; -1 when nothing may follow
         (the grammar is complete); None when the state is too permissive for a cheap trie walk
-        (inside a JSON string most of the vocabulary is allowed: the top-N filter handles it).
+        on first sight (the top-N filter handles it; if the state recurs its full mask is
+        walked once and cached).
         Masks are keyed by (grammar text, parse-state hash), so the states a JSON schema's
         grammar revisits on every request and every row are walked once."""
         key = (r.params.grammar, r.grammar.key())
@@ -1142,17 +1177,23 @@ class LLMEngine:
         if key in c:
             c.move_to_end(key)
             return c[key]
-        m = r.grammar.mask_limited(self.GRAMMAR_MASK_BUDGET)
-        if m is None:
-            slot = None
-        elif not m.any():
+        over = self._gmask_over
+        if key in over:
+            # a permissive state seen again (e.g. `[a-z ]+`, or inside a string of a JSON
+            # schema): walk the whole trie once and keep its mask
+            del over[key]
+            m = r.grammar.mask()
+        else:
+            m = r.grammar.mask_limited(self.GRAMMAR_MASK_BUDGET)
+            if m is None:
+                if len(over) > 4096:
+                    over.clear()
+                over[key] = 1
+                return None
+        if not m.any():
             slot = -1
         else:
-            pool = self._gmask_pool
-            if pool is None or pool.shape[1] != V or pool.device != torch.device(dev):
-                pool = self._gmask_pool = torch.zeros(self.GRAMMAR_MASK_SLOTS, V, dtype=torch.bool, device=dev)
-                self._gmask_free = list(range(self.GRAMMAR_MASK_SLOTS))
-                c.clear()
+            pool = self._gmask_pool_for(V, dev)
             if not self._gmask_free:  # evict the least recently used state that owns a slot
                 victim = next(k for k, v in c.items() if v is not None and v >= 0)
                 self._gmask_free.append(c.pop(victim))

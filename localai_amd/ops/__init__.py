@@ -65,6 +65,7 @@ def lib():
             "la_attn_prefill": [P, P, P, P, I, P, P, P, I, I, I, I, I, F, P, F, I, P],
             "la_sample": [P, LNG, I, I, P, P, P, P, P],
             "la_penalties": [P, LNG, I, P, I, P, P, I, P, P],
+            "la_grammar_mask": [P, LNG, I, I, P, P, LNG, P],
             "la_sample_row_bytes": [],
             "la_logit_bias": [P, LNG, P, P, P, P, I, P],
             "la_moe_route": [P, I, I, I, P, P, P],
@@ -1619,6 +1620,24 @@ def moe_linear(x: torch.Tensor, mw: MoEWeights, order: torch.Tensor, off: torch.
                              off.data_ptr(), topk, x.data_ptr(), x.shape[1], maxM, S,
                              _ptr(wts) if down else None, out.data_ptr(), mw.N, slab, T, _stream()), "la_moe_gemm")
     return Partial(out)
+
+
+def grammar_mask(logits: torch.Tensor, slot: torch.Tensor, pool: torch.Tensor) -> None:
+    """In-place: logits[b, v] = -inf where pool[slot[b], v] == 0, for rows with slot[b] >= 0
+    (grammar-constrained rows whose parse state has a cached allowed-token mask).  pool is
+    [slots, >= V] uint8 / bool; slot [B] int32."""
+    B, V = logits.shape
+    assert pool.shape[1] >= V and slot.shape[0] >= B and slot.dtype == torch.int32
+    if not logits.is_cuda:
+        for b in range(B):
+            s = int(slot[b])
+            if s >= 0:
+                logits[b].masked_fill_(~pool[s, :V].bool(), float("-inf"))
+        return
+    if logits.dtype != torch.float32 or logits.stride(1) != 1 or pool.stride(1) != 1:
+        raise ValueError("grammar_mask: f32 logits and a row-major pool required")
+    _check(lib().la_grammar_mask(logits.data_ptr(), logits.stride(0), B, V, slot.data_ptr(), pool.data_ptr(),
+                                 pool.stride(0), _stream()), "la_grammar_mask")
 
 
 def penalties(logits: torch.Tensor, hist: torch.Tensor, hist_len: torch.Tensor, pen: torch.Tensor,

@@ -446,6 +446,22 @@ __global__ __launch_bounds__(SMP_T) void sample_kernel(const float* __restrict__
   }
 }
 
+// grammar-constrained rows: tokens outside the row's allowed-token mask (slot of the engine's
+// device mask pool, one byte per token; slot < 0 = unconstrained row) get -inf before the
+// sampler, so the in-graph sample is already grammar-valid.  grid (chunks, rows); unconstrained
+// rows exit at once.
+__global__ __launch_bounds__(256) void grammar_mask_kernel(float* __restrict__ logits, long ld, int V,
+                                                           const int* __restrict__ slot,
+                                                           const unsigned char* __restrict__ pool, long pool_ld) {
+  const int row = blockIdx.y;
+  const int s = slot[row];
+  if (s < 0) return;
+  const unsigned char* m = pool + (long)s * pool_ld;
+  float* l = logits + (long)row * ld;
+  for (int v = blockIdx.x * 256 + threadIdx.x; v < V; v += gridDim.x * 256)
+    if (!m[v]) l[v] = -INFINITY;
+}
+
 // penalties over the last-n window (llama_sampler_penalties): every distinct token t in the
 // window gets  l = l>0 ? l/rp : l*rp ;  l -= count*freq + (count>0)*presence
 __global__ __launch_bounds__(256) void penalties_kernel(float* __restrict__ logits, long ld,
@@ -506,6 +522,13 @@ extern "C" int la_sample(const float* logits, long ld, int B, int V, const void*
                          float* out_p, void* stream) {
   hipLaunchKernelGGL(la::sample_kernel, dim3(B), dim3(la::SMP_T), 0, (hipStream_t)stream, logits, ld, V,
                      (const la::SampleRow*)params, mu, out_tok, out_p);
+  return (int)hipGetLastError();
+}
+
+extern "C" int la_grammar_mask(float* logits, long ld, int B, int V, const int* slot, const unsigned char* pool,
+                               long pool_ld, void* stream) {
+  hipLaunchKernelGGL(la::grammar_mask_kernel, dim3(32, B), dim3(256), 0, (hipStream_t)stream, logits, ld, V, slot,
+                     pool, pool_ld);
   return (int)hipGetLastError();
 }
 

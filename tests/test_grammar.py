@@ -132,3 +132,14 @@ def test_mask_limited_and_state_key():
     assert a.key() != b.key()                     # inside a number vs after a comma
     free = _state('root ::= [a-c ]*', pieces)
     assert free.mask_limited(3) is None and free.mask_limited(1000) is not None
+
+
+def test_grammar_mask_op_cpu_fallback():
+    import torch
+
+    from localai_amd import ops
+    lg = torch.zeros(3, 5)
+    pool = torch.tensor([[1, 0, 1, 0, 0], [0, 0, 0, 0, 1]], dtype=torch.bool)
+    ops.grammar_mask(lg, torch.tensor([1, -1, 0], dtype=torch.int32), pool)
+    inf = float("-inf")
+    assert lg.tolist() == [[inf, inf, inf, inf, 0.0], [0.0] * 5, [0.0, inf, 0.0, inf, inf]]

@@ -774,3 +774,23 @@ def test_clip_image_preprocess_kernel_matches_pil(tmp_path, pinpoints):
     finally:
         del os.environ["LOCALAI_AMD_CLIP_HOST_PREPROC"]
     assert torch.equal(emb_d, emb_h)
+
+
+@pytest.mark.gpu
+def test_grammar_mask_kernel_matches_torch():
+    """grammar_mask (sampling.hip): rows with a slot get -inf outside that slot's allowed-token
+    mask; rows with slot -1 are untouched."""
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device="cpu").manual_seed(3)
+    B, V, S = 6, 128256, 4
+    lg = torch.randn(B, V, generator=g).to(dev)
+    pool = (torch.rand(S, V, generator=g) < 0.1).to(dev)
+    slot = torch.tensor([2, -1, 0, 3, -1, 2], dtype=torch.int32, device=dev)
+    ref = lg.clone()
+    for b in range(B):
+        if int(slot[b]) >= 0:
+            ref[b].masked_fill_(~pool[int(slot[b])], float("-inf"))
+    out = lg.clone()
+    ops.grammar_mask(out, slot, pool)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
