@@ -75,6 +75,10 @@ class EngineConfig:
     draft_model: str = ""             # speculative decoding: draft LM GGUF (engine/speculative.DraftModel)
     quantization: str = ""            # HF checkpoints: load-time quantisation (bnb_4bit / bnb_8bit / ...)
     draft_max_seqs: int = 16          # draft-model KV cache capacity in sequences of context_size
+    # constrained rows inside multi-step graph runs (learned parse-state transitions); off by
+    # default: on random-init benchmarks rows park after ~1 token (profiles/r3_session2_measurements.md)
+    grammar_run_ahead: bool = dataclasses.field(
+        default_factory=lambda: os.environ.get("LOCALAI_AMD_GRAMMAR_RUN_AHEAD", "0") == "1")
 
 
 @dataclass
@@ -157,6 +161,13 @@ class LLMEngine:
         self._gmask_pool: Optional[torch.Tensor] = None
         self._gmask_free: List[int] = []
         self._gmask_over: Dict[tuple, int] = {}   # states whose budgeted walk gave up once
+        self._gnext: Optional[torch.Tensor] = None
+        self._gtrans: Dict[tuple, Optional[int]] = {}   # (slot, token) -> next slot (host mirror)
+        self._gtrans_in: Dict[int, set] = {}
+        self._gpend: List[tuple] = []                    # learned, not yet written to the device
+        self._gdev: set = set()                          # (slot, token) keys the device table holds
+        self._gepoch = 0                                 # bumped whenever a mask slot is reused
+        self._ghit: Dict[str, float] = {}                # per grammar: EMA of learned-transition hits
         self._mm_embs: Dict[int, list] = {}  # inbox "mm" item -> its images' embeddings (batched encode)
         self.clip = None
         if cfg.mmproj:
@@ -195,7 +206,8 @@ class LLMEngine:
         self._pcache = PromptCacheFiles()
         self._graph_pool = None
         self.metrics = {"prompt_tokens": 0, "gen_tokens": 0, "steps": 0, "prefill_s": 0.0, "decode_s": 0.0,
-                        "requests": 0, "spec_steps": 0, "spec_drafted": 0, "spec_accepted": 0}
+                        "requests": 0, "spec_steps": 0, "spec_drafted": 0, "spec_accepted": 0,
+                        "grammar_runs": 0, "grammar_run_rows": 0, "grammar_run_tokens": 0}
         self.last_request_stats: dict = {}
         self.busy = False
 
@@ -698,8 +710,8 @@ class LLMEngine:
             K = max(K, self.cfg.decode_steps_wide)
         rem_tok, rem_ctx = 1, K
         for r in self.requests.values():
-            if r.n_gen == 0 or self._needs_host_sampling(r):
-                return 1  # prefill in flight, or a host-side sampler feature
+            if r.n_gen == 0 or self._needs_host_sampler(r) or (r.grammar is not None and not self._grammar_ready(r)):
+                return 1  # prefill in flight, a host-side sampler feature, or a grammar state without a mask
             n = r.n_prompt + r.n_gen
             rem_ctx = min(rem_ctx, self.ctx - n)
             mt = r.params.max_tokens
@@ -816,15 +828,22 @@ class LLMEngine:
             # their sample is valid as drawn; the rest are checked and fixed up after the step
             V = logits.shape[1]
             gslot = np.full(B, -1, dtype=np.int32)
-            done_rows = []
+            done_rows, grows = [], []
             for j, r in enumerate(reqs):
                 if r.grammar is not None and not r.done:
+                    grows.append(j)
                     sl = self._grammar_mask_slot(r, V, self.device)
                     if sl is not None and sl >= 0:
                         gslot[j] = sl
                     elif sl is not None:
                         done_rows.append(j)
+            if K > 1 and (done_rows or any(gslot[j] < 0 for j in grows)):
+                K = 1  # a constrained row without a device mask cannot run ahead
+            self._gtrans_flush()
             self._upload_step_inputs(st, reqs, Bp, tok, pos, slots, lens, bt, True, gslot)
+            if K > 1:
+                self._grammar_run(graph, st, reqs, grows, gslot, K, V)
+                return
             graph.replay()
             toks = st["hist"][0, :B].cpu().numpy().copy()
             toks[done_rows] = -1
@@ -837,9 +856,20 @@ class LLMEngine:
             if plain:
                 self._emit_run([reqs[j] for j in plain], toks[plain][None, :].astype(np.int32), 1)
             now = time.perf_counter()
+            epoch = self._gepoch
+            learn = self.cfg.grammar_run_ahead
             for j, r in enumerate(reqs):
                 if r.grammar is not None:
-                    self._on_token(r, int(toks[j]), now)
+                    t = int(toks[j])
+                    self._on_token(r, t, now)
+                    s0 = int(gslot[j])
+                    if learn and s0 >= 0 and t >= 0 and not r.done:
+                        # learn the transition and score whether a multi-step run would have
+                        # known it (the hit rate gates running constrained rows ahead)
+                        s2 = self._grammar_mask_slot(r, V, self.device)
+                        self._grammar_hit(r, (s0, t) in self._gdev)
+                        if (s0, t) not in self._gtrans and epoch == self._gepoch:
+                            self._gtrans_learn(s0, t, s2)
             return
         self._upload_step_inputs(st, reqs, Bp, tok, pos, slots, lens, bt, device_sampling)
         if not device_sampling:  # long penalty windows / mirostat v1 / bias overflow: host sampling
@@ -856,6 +886,48 @@ class LLMEngine:
         self._emit_run(reqs, hist, K)
 
     _REASONS = {1: ("stop", True), 2: ("stop", False), 3: ("length", True), 4: ("abort", True)}
+
+    def _grammar_run(self, graph, st, reqs, grows, gslot, K: int, V: int):
+        """K device steps with grammar rows masked in the graph: each row's mask slot follows the
+        learned transition table (grammar_advance).  On the host, a constrained row keeps its
+        tokens up to the first transition the table did not know yet -- that token was sampled
+        under a valid mask, later ones were not -- and the transition is learned for the next
+        runs; the row's dropped positions are recomputed next run (as with rejected drafts)."""
+        B = len(reqs)
+        for _ in range(K):
+            graph.replay()
+        hist = st["hist"][:K, :B].cpu().numpy()
+        if any(r.params.mirostat == 2 for r in reqs):
+            muh = st["mu"][:B].cpu().numpy()
+            for j, r in enumerate(reqs):
+                if r.grammar is None:
+                    r.mu = float(muh[j])
+        gset = set(grows)
+        plain = [j for j in range(B) if j not in gset]
+        if plain:
+            self._emit_run([reqs[j] for j in plain], np.ascontiguousarray(hist[:, plain]), K)
+        now = time.perf_counter()
+        epoch = self._gepoch
+        self.metrics["grammar_runs"] += 1
+        self.metrics["grammar_run_rows"] += len(grows)
+        for j in grows:
+            r, s = reqs[j], int(gslot[j])
+            for i in range(K):
+                t = int(hist[i, j])
+                self._on_token(r, t, now)
+                self.metrics["grammar_run_tokens"] += 1
+                if r.done:
+                    break
+                s2 = self._grammar_mask_slot(r, V, self.device)
+                hit = (s, t) in self._gdev
+                self._grammar_hit(r, hit)
+                if not hit:
+                    if (s, t) not in self._gtrans and epoch == self._gepoch:
+                        self._gtrans_learn(s, t, s2)   # (not after a slot reuse: s may name another state)
+                    break               # the device parked this row after token t
+                if self._gtrans[(s, t)] != s2:
+                    break
+                s = s2
 
     def _emit_run(self, reqs: List[Request], hist: np.ndarray, K: int):
         """Hand a [K, B] block of device-sampled tokens to the native emitter (detokenise, stop
@@ -1014,6 +1086,7 @@ class LLMEngine:
             # grammar rows whose parse state has a cached mask sample only grammar-valid tokens
             ops.grammar_mask(lg, st["gslot"], self._gmask_pool_for(lg.shape[1], dev))
             ops.sample(lg, st["prm_np"], mu=st["mu"], params_dev=st["prm"], out=st["next"])
+            ops.grammar_advance(st["next"], st["gslot"], self._gnext)
             ops.penalty_push(st["next"], st["phist"], st["pcnt"], st["phl"], st["pcap"])
             ops.decode_advance(st["next"], st["tokens"], st["pos"], st["lens"], st["slots"], st["bt"], bs,
                                st["hist"], st["step"], st["prm"])
@@ -1161,9 +1234,63 @@ class LLMEngine:
             if pool is not None and pool.is_cuda and self._graphs:
                 raise RuntimeError("grammar mask pool shape changed after graph capture")
             pool = self._gmask_pool = torch.zeros(self.GRAMMAR_MASK_SLOTS, V, dtype=torch.bool, device=dev)
+            # learned parse-state transitions for multi-step runs: next[slot, token] (-2 unknown)
+            self._gnext = torch.full((self.GRAMMAR_MASK_SLOTS, V), -2, dtype=torch.int16, device=dev)
             self._gmask_free = list(range(self.GRAMMAR_MASK_SLOTS))
             self._gmask_cache.clear()
+            self._gtrans.clear()
+            self._gtrans_in.clear()
+            self._gpend.clear()
+            self._gdev.clear()
         return pool
+
+    def _gslot_release(self, slot: int):
+        """A pool slot is being reused: forget every learned transition into or out of it."""
+        self._gmask_free.append(slot)
+        self._gepoch += 1
+        self._gnext[slot].fill_(-2)
+        for st_t in self._gtrans_in.pop(slot, ()):
+            self._gtrans.pop(st_t, None)
+            if st_t in self._gdev:
+                self._gdev.discard(st_t)
+                self._gnext[st_t[0], st_t[1]] = -2
+        self._gpend = [e for e in self._gpend if e[0] != slot and e[2] != slot]
+        for k in [k for k in self._gtrans if k[0] == slot]:
+            v = self._gtrans.pop(k)
+            self._gdev.discard(k)
+            if v is not None and v >= 0:
+                self._gtrans_in.get(v, set()).discard(k)
+
+    def _gtrans_learn(self, s: int, t: int, s2):
+        """Record the transition (slot s, token t) -> s2 (a slot, -1 complete, None unmasked);
+        only slot targets are written to the device table (the others keep the row on the host)."""
+        self._gtrans[(s, t)] = s2
+        if s2 is not None and s2 >= 0:
+            self._gtrans_in.setdefault(s2, set()).add((s, t))
+            self._gpend.append((s, t, s2))
+
+    def _gtrans_flush(self):
+        if self._gpend:
+            self._gdev.update((a, b) for a, b, _ in self._gpend)
+            a = torch.tensor(self._gpend, dtype=torch.int64)
+            self._gnext[a[:, 0].to(self._gnext.device), a[:, 1].to(self._gnext.device)] = \
+                a[:, 2].to(torch.int16).to(self._gnext.device)
+            self._gpend.clear()
+
+    GRAMMAR_RUN_HIT = 0.8   # learned-transition hit rate above which constrained rows run ahead
+
+    def _grammar_hit(self, r, hit: bool):
+        g = r.params.grammar
+        self._ghit[g] = 0.95 * self._ghit.get(g, 0.0) + (0.05 if hit else 0.0)
+
+    def _grammar_ready(self, r) -> bool:
+        """r can run ahead inside a multi-step graph run: its parse state has a device mask and
+        the transitions its grammar produces are mostly learned already (otherwise each row would
+        park after about one token and waste the rest of the run)."""
+        if not self.cfg.grammar_run_ahead or self._ghit.get(r.params.grammar, 0.0) < self.GRAMMAR_RUN_HIT:
+            return False
+        s = self._gmask_cache.get((r.params.grammar, r.grammar.key()))
+        return s is not None and s >= 0
 
     def _grammar_mask_slot(self, r, V: int, dev):
         """Slot of r's current parse state in the device mask pool; -1 when nothing may follow
@@ -1196,7 +1323,7 @@ class LLMEngine:
             pool = self._gmask_pool_for(V, dev)
             if not self._gmask_free:  # evict the least recently used state that owns a slot
                 victim = next(k for k, v in c.items() if v is not None and v >= 0)
-                self._gmask_free.append(c.pop(victim))
+                self._gslot_release(c.pop(victim))
             slot = self._gmask_free.pop()
             n = min(len(m), V)
             pool[slot, :n].copy_(torch.from_numpy(m[:n].astype(bool)))
@@ -1204,7 +1331,7 @@ class LLMEngine:
         while len(c) > 4 * self.GRAMMAR_MASK_SLOTS:
             _, v = c.popitem(last=False)
             if v is not None and v >= 0:
-                self._gmask_free.append(v)
+                self._gslot_release(v)
         return slot
 
     def _apply_grammar(self, reqs, logits, prm, toks):

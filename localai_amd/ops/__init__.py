@@ -66,6 +66,7 @@ def lib():
             "la_sample": [P, LNG, I, I, P, P, P, P, P],
             "la_penalties": [P, LNG, I, P, I, P, P, I, P, P],
             "la_grammar_mask": [P, LNG, I, I, P, P, LNG, P],
+            "la_grammar_advance": [P, P, P, I, I, P],
             "la_sample_row_bytes": [],
             "la_logit_bias": [P, LNG, P, P, P, P, I, P],
             "la_moe_route": [P, I, I, I, P, P, P],
@@ -1638,6 +1639,24 @@ def grammar_mask(logits: torch.Tensor, slot: torch.Tensor, pool: torch.Tensor) -
         raise ValueError("grammar_mask: f32 logits and a row-major pool required")
     _check(lib().la_grammar_mask(logits.data_ptr(), logits.stride(0), B, V, slot.data_ptr(), pool.data_ptr(),
                                  pool.stride(0), _stream()), "la_grammar_mask")
+
+
+def grammar_advance(tok: torch.Tensor, slot: torch.Tensor, nxt: torch.Tensor) -> None:
+    """In-place: for rows with slot >= 0, slot = nxt[slot, tok] if that transition is known
+    (>= 0) else -3 (parked: the host drops the row's later tokens of this run).  tok / slot
+    int32 [B]; nxt int16 [slots, V]."""
+    B = slot.shape[0]
+    V = nxt.shape[1]
+    assert nxt.dtype == torch.int16 and slot.dtype == torch.int32 and tok.shape[0] >= B
+    if not slot.is_cuda:
+        for b in range(B):
+            s, t = int(slot[b]), int(tok[b])
+            if s >= 0:
+                ns = int(nxt[s, t]) if 0 <= t < V else -2
+                slot[b] = ns if ns >= 0 else -3
+        return
+    _check(lib().la_grammar_advance(tok.data_ptr(), slot.data_ptr(), nxt.data_ptr(), V, B, _stream()),
+           "la_grammar_advance")
 
 
 def penalties(logits: torch.Tensor, hist: torch.Tensor, hist_len: torch.Tensor, pen: torch.Tensor,

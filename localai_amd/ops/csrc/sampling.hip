@@ -462,6 +462,21 @@ __global__ __launch_bounds__(256) void grammar_mask_kernel(float* __restrict__ l
     if (!m[v]) l[v] = -INFINITY;
 }
 
+// grammar rows across a multi-step run: after each in-graph sample, a row's mask slot follows the
+// transition table the host has learned (next[slot][token], -2 = not learned yet).  An unknown
+// transition parks the row at -3 (no mask; the host keeps its tokens up to that point and drops
+// the rest of the run for that row).  Rows at -1 (unconstrained) and -3 are left alone.
+__global__ __launch_bounds__(256) void grammar_advance_kernel(const int* __restrict__ tok, int* __restrict__ slot,
+                                                              const short* __restrict__ next, int V, int B) {
+  const int b = blockIdx.x * 256 + threadIdx.x;
+  if (b >= B) return;
+  const int s = slot[b];
+  if (s < 0) return;
+  const int t = tok[b];
+  const int ns = (t >= 0 && t < V) ? (int)next[(long)s * V + t] : -2;
+  slot[b] = ns >= 0 ? ns : -3;
+}
+
 // penalties over the last-n window (llama_sampler_penalties): every distinct token t in the
 // window gets  l = l>0 ? l/rp : l*rp ;  l -= count*freq + (count>0)*presence
 __global__ __launch_bounds__(256) void penalties_kernel(float* __restrict__ logits, long ld,
@@ -529,6 +544,12 @@ extern "C" int la_grammar_mask(float* logits, long ld, int B, int V, const int* 
                                long pool_ld, void* stream) {
   hipLaunchKernelGGL(la::grammar_mask_kernel, dim3(32, B), dim3(256), 0, (hipStream_t)stream, logits, ld, V, slot,
                      pool, pool_ld);
+  return (int)hipGetLastError();
+}
+
+extern "C" int la_grammar_advance(const int* tok, int* slot, const short* next, int V, int B, void* stream) {
+  hipLaunchKernelGGL(la::grammar_advance_kernel, dim3((B + 255) / 256), dim3(256), 0, (hipStream_t)stream, tok, slot,
+                     next, V, B);
   return (int)hipGetLastError();
 }
 

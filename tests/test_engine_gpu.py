@@ -283,3 +283,30 @@ def test_grammar_rows_fixed_up_beside_device_sampling(tiny_model_path):
     graph = run(_eng(tiny_model_path, 8))
     assert graph == eager
     assert re.fullmatch(rb"[a-z ]+", graph[1][0]) and re.fullmatch(rb"[0-9]*x?", graph[3][0])
+
+
+@pytest.mark.gpu
+def test_grammar_rows_run_ahead_in_multistep_graphs(tiny_model_path):
+    """Constrained rows whose parse states have device masks run inside K-step graph runs (masks
+    follow the learned transition table); greedy outputs equal the eager host-driven engine's
+    and obey the grammar, and later waves keep several tokens per run for constrained rows."""
+    import re
+    g = 'root ::= "{" ("\\"a\\"" | "\\"bb\\"") ":" [0-9] [0-9]? "," [a-c]+ "}"'
+    prompts = [f"grammar wave prompt {i}" for i in range(6)]
+
+    def run(eng, waves):
+        res = []
+        for _ in range(waves):
+            res.append(_run(eng, prompts, max_tokens=20, temperature=0.0, grammar=g))
+        return res
+    eager = run(LLMEngine(EngineConfig(model_path=tiny_model_path, device="cuda:0", context_size=256, max_num_seqs=8,
+                                       max_batched_tokens=512, use_graphs=False)), 1)[0]
+    eng = LLMEngine(EngineConfig(model_path=tiny_model_path, device="cuda:0", context_size=256, max_num_seqs=8,
+                                 max_batched_tokens=512, decode_steps=8, grammar_run_ahead=True))
+    waves = run(eng, 4)
+    for w in waves:
+        assert [o[0] for o in w] == [o[0] for o in eager]
+    for o in waves[-1]:
+        assert re.fullmatch(rb'\{("a"|"bb"):[0-9][0-9]?,[a-c]*\}?', o[0]), o
+    m = eng.metrics
+    assert m["grammar_runs"] > 0 and m["grammar_run_tokens"] > 1.5 * m["grammar_run_rows"], m
