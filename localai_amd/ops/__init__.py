@@ -698,7 +698,7 @@ def _cold_caches(device):
 
 # Quantised tile GEMM (gemm_q.hip): the M > SKINNY_MAX_M path.  Tile ids: (BM, BN).
 GQ_TILES = {0: (256, 256), 1: (256, 128), 2: (128, 256), 3: (128, 128), 4: (256, 64), 5: (64, 256), 6: (256, 256),
-            7: (128, 256), 8: (256, 128), 12: (128, 128), 14: (64, 256), 15: (128, 256),
+            7: (128, 256), 8: (256, 128), 12: (128, 128), 14: (64, 256),
             # software-pipelined schedules of 0, 1, 3, 6, 7
             10: (256, 256), 11: (256, 128), 13: (128, 128), 16: (256, 256), 17: (128, 256)}
 # LOCALAI_AMD_TILE_GEMM=0 restores the round-2 path (hipBLASLt on bf16 weight copies + qgemm_mid)
@@ -770,7 +770,7 @@ def _autotune_mid(x, ws, key, Ntot):
     N = max(w.N for w in ws)
     cands = []
     if all(w.tile_ok for w in ws):
-        tiles = (6, 1, 7, 8, 12, 15) if M > 128 else (7, 12, 14, 3, 15)
+        tiles = (6, 1, 7, 8, 12) if M > 128 else (7, 12, 14, 3)
         for t in tiles:
             g = _tile_grid(M, N, t)
             base = max(1, round(256 / g))
@@ -970,7 +970,7 @@ def glu_linear(x: torch.Tensor, ws: Sequence[QWeight], F: int, mode: int,
         out = torch.empty(M, F, dtype=torch.bfloat16, device=x.device)
         t_ref = _time_cold(lambda: act(linear_multi(x, ws), F, mode))
         best, best_t = None, t_ref
-        for t in ((6, 7, 8, 15) if M > 128 else (7, 12, 14, 15)):
+        for t in ((6, 7, 8) if M > 128 else (7, 12, 14)):
             tt = _time_cold(lambda t=t: _run_glu(x, pair, F, mode, t, out))
             if tt < best_t:
                 best, best_t = t, tt

@@ -741,7 +741,6 @@ static int gq_dispatch_glu(int tile, const QW& wa, const GqGlu& glu, const bf16*
     case 8: gq_launch_glu<FMT, 256, 128, 2, 4, 2>(wa, glu, X, ldx, M, outb, ldo, st); break;
     case 12: gq_launch_glu<FMT, 128, 128, 2, 4, 3>(wa, glu, X, ldx, M, outb, ldo, st); break;
     case 14: gq_launch_glu<FMT, 64, 256, 1, 8, 3>(wa, glu, X, ldx, M, outb, ldo, st); break;
-    case 15: gq_launch_glu<FMT, 128, 256, 1, 4, NS2>(wa, glu, X, ldx, M, outb, ldo, st); break;
     default: return -1;
   }
   return 0;
@@ -753,9 +752,6 @@ static int gq_dispatch_glu(int tile, const QW& wa, const GqGlu& glu, const bf16*
 //   6: 256 x 256 (8 waves 1x8: one dequantised B fragment feeds 16 MFMAs, A reads double)
 //   7: 128 x 256 (8 waves 1x8)   8: 256 x 128 (8 waves 2x4, 2 ring slots)   12: 128 x 128 (8 waves 2x4)
 //   14: 64 x 256 (8 waves 1x8)
-//   15: 128 x 256 (4 waves 1x4: each wave 128 x 64, half the X LDS reads of tile 7 per CU -- at
-//       M = 256 tile 7's eight waves re-read the whole 128-row X tile every K-step, 128 KiB per
-//       CU, about the LDS bandwidth of the step's MFMA time)
 template <int FMT, int ABL = 0>
 static int gq_dispatch(int tile, const QW& w, const bf16* X, int ldx, int M, int splits, float* out, bf16* outb,
                        int ldo, long slab, hipStream_t st) {
@@ -779,7 +775,6 @@ static int gq_dispatch(int tile, const QW& w, const bf16* X, int ldx, int M, int
     case 8: gq_launch<FMT, 256, 128, 2, 4, 2, ABL>(w, X, ldx, M, splits, out, outb, ldo, slab, st); break;
     case 12: gq_launch<FMT, 128, 128, 2, 4, 3, ABL>(w, X, ldx, M, splits, out, outb, ldo, slab, st); break;
     case 14: gq_launch<FMT, 64, 256, 1, 8, 3, ABL>(w, X, ldx, M, splits, out, outb, ldo, slab, st); break;
-    case 15: gq_launch<FMT, 128, 256, 1, 4, NS2, ABL>(w, X, ldx, M, splits, out, outb, ldo, slab, st); break;
     // software-pipelined schedule (PIPE = 1) of tiles 0, 1, 3, 6
     case 10: gq_launch<FMT, 256, 256, 2, 4, NS0, ABL, 1>(w, X, ldx, M, splits, out, outb, ldo, slab, st); break;
     case 11: gq_launch<FMT, 256, 128, 2, 4, NS1, ABL, 1>(w, X, ldx, M, splits, out, outb, ldo, slab, st); break;
