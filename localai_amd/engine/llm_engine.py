@@ -168,6 +168,8 @@ class LLMEngine:
         self._gdev: set = set()                          # (slot, token) keys the device table holds
         self._gepoch = 0                                 # bumped whenever a mask slot is reused
         self._ghit: Dict[str, float] = {}                # per grammar: EMA of learned-transition hits
+        self._gexpanded: set = set()                     # slots whose outgoing transitions are all learned
+        self._gmask_np: Dict[int, np.ndarray] = {}       # host copies of the pool's masks (run-ahead)
         self._mm_embs: Dict[int, list] = {}  # inbox "mm" item -> its images' embeddings (batched encode)
         self.clip = None
         if cfg.mmproj:
@@ -829,16 +831,19 @@ class LLMEngine:
             V = logits.shape[1]
             gslot = np.full(B, -1, dtype=np.int32)
             done_rows, grows = [], []
+            epoch0 = self._gepoch
             for j, r in enumerate(reqs):
                 if r.grammar is not None and not r.done:
                     grows.append(j)
                     sl = self._grammar_mask_slot(r, V, self.device)
                     if sl is not None and sl >= 0:
                         gslot[j] = sl
+                        if self.cfg.grammar_run_ahead:
+                            self._gexpand(r.params.grammar, r.grammar, sl, V)
                     elif sl is not None:
                         done_rows.append(j)
-            if K > 1 and (done_rows or any(gslot[j] < 0 for j in grows)):
-                K = 1  # a constrained row without a device mask cannot run ahead
+            if K > 1 and (done_rows or any(gslot[j] < 0 for j in grows) or epoch0 != self._gepoch):
+                K = 1  # a constrained row without a device mask (or a slot reused meanwhile) cannot run ahead
             self._gtrans_flush()
             self._upload_step_inputs(st, reqs, Bp, tok, pos, slots, lens, bt, True, gslot)
             if K > 1:
@@ -1242,6 +1247,8 @@ class LLMEngine:
             self._gtrans_in.clear()
             self._gpend.clear()
             self._gdev.clear()
+            self._gexpanded.clear()
+            self._gmask_np.clear()
         return pool
 
     def _gslot_release(self, slot: int):
@@ -1249,6 +1256,8 @@ class LLMEngine:
         self._gmask_free.append(slot)
         self._gepoch += 1
         self._gnext[slot].fill_(-2)
+        self._gexpanded.discard(slot)
+        self._gmask_np.pop(slot, None)
         for st_t in self._gtrans_in.pop(slot, ()):
             self._gtrans.pop(st_t, None)
             if st_t in self._gdev:
@@ -1283,6 +1292,44 @@ class LLMEngine:
         g = r.params.grammar
         self._ghit[g] = 0.95 * self._ghit.get(g, 0.0) + (0.05 if hit else 0.0)
 
+    GRAMMAR_EXPAND_MAX = 20000   # allowed tokens up to which a state's transitions are precomputed
+
+    def _gexpand(self, gtext: str, gs, s: int, V: int):
+        """Learn every transition out of slot s at once: the key of the state after each allowed
+        token (one native pass), one mask per distinct successor.  A state like `[a-z ]+`
+        (self-loop) or an enum position of a JSON schema is then fully known to the device
+        table, so constrained rows do not park there.  Permissive states (most of the
+        vocabulary allowed) are left to the per-token learning."""
+        if s in self._gexpanded:
+            return
+        self._gexpanded.add(s)
+        m = self._gmask_np.get(s)
+        if m is None:
+            return
+        toks = np.nonzero(m)[0].astype(np.int32)
+        if len(toks) == 0 or len(toks) > self.GRAMMAR_EXPAND_MAX:
+            return
+        keys = gs.next_keys(toks)
+        epoch = self._gepoch
+        groups: Dict[int, list] = {}
+        for t, k in zip(toks.tolist(), keys.tolist()):
+            if k:
+                groups.setdefault(k, []).append(t)
+        for k, ts in groups.items():
+            if (gtext, k) in self._gmask_cache:
+                s2 = self._gmask_cache[(gtext, k)]
+            else:
+                g2 = gs.clone()
+                if not g2.accept(ts[0]):
+                    continue
+                s2 = self._state_slot(gtext, g2, V, self.device, key=k)
+            if epoch != self._gepoch:   # a slot was reused meanwhile: s may name another state
+                self._gexpanded.discard(s)
+                return
+            for t in ts:
+                if (s, t) not in self._gtrans:
+                    self._gtrans_learn(s, t, s2)
+
     def _grammar_ready(self, r) -> bool:
         """r can run ahead inside a multi-step graph run: its parse state has a device mask and
         the transitions its grammar produces are mostly learned already (otherwise each row would
@@ -1299,7 +1346,11 @@ class LLMEngine:
         walked once and cached).
         Masks are keyed by (grammar text, parse-state hash), so the states a JSON schema's
         grammar revisits on every request and every row are walked once."""
-        key = (r.params.grammar, r.grammar.key())
+        return self._state_slot(r.params.grammar, r.grammar, V, dev)
+
+    def _state_slot(self, gtext: str, gs, V: int, dev, key: Optional[int] = None):
+        """_grammar_mask_slot for a parse state object `gs` of grammar `gtext`."""
+        key = (gtext, gs.key() if key is None else key)
         c = self._gmask_cache
         if key in c:
             c.move_to_end(key)
@@ -1309,9 +1360,9 @@ class LLMEngine:
             # a permissive state seen again (e.g. `[a-z ]+`, or inside a string of a JSON
             # schema): walk the whole trie once and keep its mask
             del over[key]
-            m = r.grammar.mask()
+            m = gs.mask()
         else:
-            m = r.grammar.mask_limited(self.GRAMMAR_MASK_BUDGET)
+            m = gs.mask_limited(self.GRAMMAR_MASK_BUDGET)
             if m is None:
                 if len(over) > 4096:
                     over.clear()
@@ -1327,6 +1378,8 @@ class LLMEngine:
             slot = self._gmask_free.pop()
             n = min(len(m), V)
             pool[slot, :n].copy_(torch.from_numpy(m[:n].astype(bool)))
+            if self.cfg.grammar_run_ahead:
+                self._gmask_np[slot] = m
         c[key] = slot
         while len(c) > 4 * self.GRAMMAR_MASK_SLOTS:
             _, v = c.popitem(last=False)

@@ -566,10 +566,35 @@ class GrammarState {
 
   // identity of the parse state for mask caching: FNV-1a over the sorted per-stack hashes (stack
   // order depends on history, the set does not) and the partial UTF-8 code point
-  uint64_t key() const {
+  uint64_t key() const { return key_of(stacks_, u_, done_); }
+
+  // the key of the state after each candidate token (0: the token is rejected, or ends the
+  // grammar), without changing this state -- one level of the parse-state transition graph
+  py::array_t<uint64_t> next_keys(py::array_t<int32_t, py::array::c_style | py::array::forcecast> cand) const {
+    const auto n = cand.size();
+    py::array_t<uint64_t> out(n);
+    auto* o = out.mutable_data();
+    const int32_t* c = cand.data();
+    py::gil_scoped_release rel;
+    std::vector<Stack> st, tmp;
+    for (py::ssize_t i = 0; i < n; ++i) {
+      o[i] = 0;
+      if (v_->is_eog(c[i])) continue;
+      const std::string& b = v_->piece(c[i]);
+      if (b.empty()) continue;
+      st = stacks_;
+      Utf8 u = u_;
+      if (!feed_bytes(g_->rules, st, u, b, tmp)) continue;
+      o[i] = key_of(st, u, false);
+      if (o[i] == 0) o[i] = 1;
+    }
+    return out;
+  }
+
+  static uint64_t key_of(const std::vector<Stack>& stacks, const Utf8& u, bool done) {
     std::vector<uint64_t> hs;
-    hs.reserve(stacks_.size());
-    for (const Stack& st : stacks_) {
+    hs.reserve(stacks.size());
+    for (const Stack& st : stacks) {
       uint64_t h = 1469598103934665603ull;
       for (const El* e : st) {
         h ^= (uint64_t)(uintptr_t)e;
@@ -588,9 +613,11 @@ class GrammarState {
       }
     };
     for (uint64_t x : hs) mix(x);
-    mix(u_.value);
-    mix(((uint64_t)u_.remain << 32) | u_.min);
-    mix(done_ ? 1 : 0);
+    // the decoder keeps the last code point in `value` after it completes: only a pending
+    // partial code point is part of the state
+    mix(u.remain ? u.value : 0);
+    mix(u.remain ? (((uint64_t)u.remain << 32) | u.min) : 0);
+    mix(done ? 1 : 0);
     return h;
   }
 
@@ -666,6 +693,8 @@ void register_grammar(py::module& m) {
       .def("mask_linear", &GrammarState::mask_linear)
       .def("mask_limited", &GrammarState::mask_limited, py::arg("budget"))
       .def("key", &GrammarState::key)
+      .def("next_keys", &GrammarState::next_keys)
+      .def("clone", [](const GrammarState& s) { return GrammarState(s); })
       .def("accept", &GrammarState::accept)
       .def("accept_bytes", &GrammarState::accept_bytes)
       .def("can_end", &GrammarState::can_end)

@@ -143,3 +143,19 @@ def test_grammar_mask_op_cpu_fallback():
     ops.grammar_mask(lg, torch.tensor([1, -1, 0], dtype=torch.int32), pool)
     inf = float("-inf")
     assert lg.tolist() == [[inf, inf, inf, inf, 0.0], [0.0] * 5, [0.0, inf, 0.0, inf, inf]]
+
+
+def test_next_keys_and_clone():
+    """next_keys() gives the key each candidate token leads to without changing the state (0 when
+    rejected); equal parse states reached by different tokens share a key; clone() is an
+    independent copy."""
+    pieces = [b"", b"1", b"2", b"12", b",", b"1,", b"a"]
+    g, v = core.Grammar('root ::= ([0-9]+ ",")*'), core.GrammarVocab(pieces, [0])
+    st = core.GrammarState(g, v)
+    k0 = st.key()
+    keys = st.next_keys(np.arange(len(pieces), dtype=np.int32)).tolist()
+    assert keys[0] == 0 and keys[4] == 0 and keys[6] == 0          # eog / "," / "a" rejected here
+    assert keys[1] == keys[2] == keys[3] != k0                      # inside a number
+    assert keys[5] == k0                                            # "1," loops back to the start
+    c = st.clone()
+    assert c.accept(1) and c.key() == keys[1] and st.key() == k0
