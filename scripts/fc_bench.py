@@ -87,6 +87,9 @@ def main():
                 args.get("days") in ("1", "3", "7") and args.get("location") in ("paris", "tokyo", "lima", "oslo")
         except (ValueError, TypeError):
             ok = False
+    m = eng.metrics
+    print(f"grammar runs {m['grammar_runs']} rows {m['grammar_run_rows']} tokens {m['grammar_run_tokens']} "
+          f"hit-rate {[round(v, 3) for v in eng._ghit.values()]}", file=sys.stderr, flush=True)
     print(json.dumps({"metric": "function-calling output tokens/s (forced tool, GBNF-constrained)",
                       "value": round(best[0], 1), "concurrency": a.concurrency, "max_tokens": a.max_tokens,
                       "tokens": best[1], "wall_s": round(best[2], 3), "finish_reason": doc["choices"][0]["finish_reason"],

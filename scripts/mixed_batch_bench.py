@@ -55,3 +55,7 @@ wave("warm", "")
 for special in ("", "penalty", "grammar", ""):
     r = wave(f"w{time.time():.0f}", special)
     print(f"{special or 'plain':8s} decode {r:9.1f} tok/s", flush=True)
+    if special == "grammar":
+        m = eng.metrics
+        print(f"  grammar runs {m['grammar_runs']} rows {m['grammar_run_rows']} tokens {m['grammar_run_tokens']} "
+              f"hit-rate {dict((k[:20], round(v, 3)) for k, v in eng._ghit.items())}", flush=True)
