@@ -10,7 +10,9 @@ list naming which of negative_prompt / width / height / num_inference_steps reac
 "none" for none of them -- the rest take the pipeline defaults: sample_size * 8 pixels, 50 steps).
 `src` makes the call img2img (strength 0.8, the diffusers default) -- or, when LoadModel named a
 `ControlNet` (a ControlNetModel directory, relative to the pipeline's parent directory), the
-control image of a ControlNet-conditioned txt2img (backend.py:292-296, 403-405); `SchedulerType` takes every
+control image of a ControlNet-conditioned txt2img (backend.py:292-296, 403-405); `LoraAdapter` (relative to
+the model file's directory) is merged into the UNet / text encoders at load (models/sd_lora.py,
+backend.py:300-314; `LoraScale` when set, else 1); `SchedulerType` takes every
 scheduler name of the reference's mapping (models/schedulers.py).  One image at a time (the
 reference runs one gRPC worker per backend).
 """
@@ -55,6 +57,14 @@ class DiffusersServicer:
             cn = os.path.join(os.path.dirname(os.path.normpath(path)), cn)  # next to the pipeline directory
         if cn and not os.path.isfile(os.path.join(cn, "config.json")):
             return pb.Result(success=False, message=f"ControlNet model not found: {request.ControlNet}")
+        lora = str(request.LoraAdapter or "")
+        if lora and not os.path.isabs(lora):
+            # backend.py:300-305: relative to the model file's directory
+            lora = os.path.join(os.path.dirname(request.ModelFile or path.rstrip("/")), lora)
+        if lora and not os.path.exists(lora):
+            return pb.Result(success=False, message=f"LoRA adapter not found: {request.LoraAdapter}")
+        if lora and (flux or sd3):
+            return pb.Result(success=False, message="LoRA adapters are supported for SD 1.x / 2.x / XL pipelines")
         try:
             if flux:  # backend.py:247-251: FluxPipeline; GenerateImage adds max_sequence_length=256
                 p = await asyncio.get_running_loop().run_in_executor(
@@ -65,7 +75,8 @@ class DiffusersServicer:
             else:
                 p = await asyncio.get_running_loop().run_in_executor(
                     None, lambda: StableDiffusion(path, dev, request.SchedulerType, int(request.CLIPSkip or 0),
-                                                  controlnet=cn))
+                                                  controlnet=cn, lora=lora,
+                                                  lora_scale=float(request.LoraScale) if request.LoraScale else 1.0))
         except Exception as e:  # noqa: BLE001 - reported to the caller like the reference
             return pb.Result(success=False, message=f"Unexpected {e!r}")
         self.pipe, self.state = p, pb.StatusResponse.READY

@@ -628,7 +628,8 @@ class Scheduler:
 # ------------------------------------------------------------------ pipeline
 class StableDiffusion:
     def __init__(self, path: str, device: str = "cpu", scheduler: str = "", clip_skip: int = 0,
-                 channels_last: Optional[bool] = None, controlnet: str = "", controlnet_scale: float = 1.0):
+                 channels_last: Optional[bool] = None, controlnet: str = "", controlnet_scale: float = 1.0,
+                 lora: str = "", lora_scale: float = 1.0):
         self.device = torch.device(device)
         # NHWC activations for the MIOpen convolutions (LOCALAI_AMD_SD_NHWC=0 keeps NCHW)
         if channels_last is None:
@@ -663,6 +664,9 @@ class StableDiffusion:
         if controlnet:
             self.controlnet = ControlNet(_cfg(os.path.join(controlnet, "config.json")))
             self.controlnet.load_state_dict(_load_weights(controlnet), strict=True)
+        if lora:  # LoraAdapter: merged in fp32 before the cast (models/sd_lora.py)
+            from .sd_lora import merge_sd_lora
+            merge_sd_lora(lora, self.unet, self.text, self.text2, lora_scale)
         for m in (self.text, self.text2, self.unet, self.vae, self.controlnet):
             if m is not None:
                 m.to(self.device, self.dtype).eval().requires_grad_(False)
