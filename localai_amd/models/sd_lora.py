@@ -20,8 +20,10 @@ are called):
   attention processors <module.path>.processor.to_q_lora.down.weight / .up.weight (a
                        `load_attn_procs` directory: pytorch_lora_weights.safetensors)
 
-kohya files trained against the original LDM / SGM module names (input_blocks.*) are refused with
-the count of keys that matched nothing, instead of being half applied.
+kohya files trained against the original LDM / SGM module names (`lora_unet_input_blocks_4_1_...`,
+most SD-1.5 / SDXL LoRAs) are mapped onto the diffusers modules from the UNet's own block layout
+(`ldm_unet_path`); any key that still matches nothing makes the load fail with the count of such
+keys, instead of the adapter being half applied.
 """
 from __future__ import annotations
 
@@ -89,6 +91,61 @@ def _params(mod: Optional[nn.Module]) -> Tuple[Dict[str, nn.Parameter], Dict[str
     return ps, under
 
 
+_RES_TAIL = {"in_layers_0": "norm1", "in_layers_2": "conv1", "emb_layers_1": "time_emb_proj",
+             "out_layers_0": "norm2", "out_layers_3": "conv2", "skip_connection": "conv_shortcut"}
+_TOP = {"time_embed_0": "time_embedding.linear_1", "time_embed_2": "time_embedding.linear_2",
+        "label_emb_0_0": "add_embedding.linear_1", "label_emb_0_2": "add_embedding.linear_2",
+        "out_0": "conv_norm_out", "out_2": "conv_out", "input_blocks_0_0": "conv_in"}
+
+
+def ldm_unet_path(key: str, unet: nn.Module) -> Optional[str]:
+    """A kohya key body in the original LDM / SGM UNet naming (input_blocks_N_S_..., middle_block_S_...,
+    output_blocks_N_S_...) -> the underscored diffusers path of the same module, from the UNet's
+    own block layout (layers per block, which blocks carry attentions / up-samplers), as diffusers'
+    single-file conversion lays the blocks out."""
+    if key in _TOP:
+        return _TOP[key].replace(".", "_")
+    lpb = len(unet.down_blocks[0].resnets)
+
+    def res(prefix, tail):
+        for k, v in _RES_TAIL.items():
+            if tail == k or tail.startswith(k + "_"):
+                return prefix + "_" + v + tail[len(k):]
+        return None
+
+    m = re.match(r"input_blocks_(\d+)_(\d+)_(.+)$", key)
+    if m:
+        n, sub, tail = int(m.group(1)), int(m.group(2)), m.group(3)
+        i, j = (n - 1) // (lpb + 1), (n - 1) % (lpb + 1)
+        if n == 0 or i >= len(unet.down_blocks):
+            return None
+        if j == lpb:
+            return f"down_blocks_{i}_downsamplers_0_conv" if tail == "op" else None
+        if sub == 0:
+            return res(f"down_blocks_{i}_resnets_{j}", tail)
+        return f"down_blocks_{i}_attentions_{j}_{tail}" if sub == 1 else None
+    m = re.match(r"middle_block_(\d+)_(.+)$", key)
+    if m:
+        sub, tail = int(m.group(1)), m.group(2)
+        if sub == 1:
+            return f"mid_block_attentions_0_{tail}"
+        return res(f"mid_block_resnets_{sub // 2}", tail) if sub in (0, 2) else None
+    m = re.match(r"output_blocks_(\d+)_(\d+)_(.+)$", key)
+    if m:
+        n, sub, tail = int(m.group(1)), int(m.group(2)), m.group(3)
+        i, j = n // (lpb + 1), n % (lpb + 1)
+        if i >= len(unet.up_blocks):
+            return None
+        blk = unet.up_blocks[i]
+        if sub == 0:
+            return res(f"up_blocks_{i}_resnets_{j}", tail)
+        if sub == 1 and hasattr(blk, "attentions"):
+            return f"up_blocks_{i}_attentions_{j}_{tail}"
+        if tail == "conv" and hasattr(blk, "upsamplers"):
+            return f"up_blocks_{i}_upsamplers_0_conv"
+    return None
+
+
 def merge_sd_lora(path: str, unet: nn.Module, text: Optional[nn.Module] = None,
                   text2: Optional[nn.Module] = None, scale: float = 1.0) -> int:
     """Merge the LoRA at `path` into the modules (fp32 in place); returns the number of weights
@@ -104,6 +161,9 @@ def merge_sd_lora(path: str, unet: nn.Module, text: Optional[nn.Module] = None,
                 continue
             ps, under = targets[target]
             name = under.get(mod[1:]) if mod.startswith("_") else mod
+            if name is None and mod.startswith("_") and target == "unet":
+                alt = ldm_unet_path(mod[1:], unet)
+                name = under.get(alt) if alt else None
             if name not in ps and target != "unet":
                 # text encoders: checkpoints with and without the `text_model.` prefix
                 alt = ("text_model." + name) if name and not name.startswith("text_model.") else None
@@ -120,5 +180,5 @@ def merge_sd_lora(path: str, unet: nn.Module, text: Optional[nn.Module] = None,
             n += 1
     if missing:
         raise ValueError(f"LoRA {os.path.basename(path)}: {len(missing)} of {len(groups)} entries match no "
-                         f"pipeline weight (first: {missing[0]}); LDM/SGM-named kohya files are not supported")
+                         f"pipeline weight (first: {missing[0]})")
     return n

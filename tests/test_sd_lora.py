@@ -80,11 +80,53 @@ def test_attn_processor_layout_and_unknown_keys(pipe_dir, tmp_path):
               str(d / "pytorch_lora_weights.safetensors"))
     assert merge_sd_lora(str(d), base.unet) == 1
     torch.testing.assert_close(dict(base.unet.named_parameters())[name + ".to_v.weight"], w + up @ down)
-    bad = str(tmp_path / "ldm.safetensors")
-    save_file({"lora_unet_input_blocks_1_1_proj_in.lora_down.weight": down,
-               "lora_unet_input_blocks_1_1_proj_in.lora_up.weight": up}, bad)
+    bad = str(tmp_path / "bad.safetensors")
+    save_file({"lora_unet_input_blocks_9_1_proj_in.lora_down.weight": down,
+               "lora_unet_input_blocks_9_1_proj_in.lora_up.weight": up}, bad)
     with pytest.raises(ValueError, match="match no pipeline weight"):
         merge_sd_lora(bad, base.unet)
+
+
+# the tiny UNet: layers_per_block 1; down blocks (CrossAttn + downsampler, plain); up blocks
+# (plain + upsampler, CrossAttn) -- the LDM input / middle / output block numbering of that layout
+LDM_NAMES = {
+    "input_blocks_1_1_transformer_blocks_0_attn1_to_q": "down_blocks.0.attentions.0.transformer_blocks.0.attn1.to_q",
+    "input_blocks_1_0_in_layers_2": "down_blocks.0.resnets.0.conv1",
+    "input_blocks_2_0_op": "down_blocks.0.downsamplers.0.conv",
+    "input_blocks_3_0_emb_layers_1": "down_blocks.1.resnets.0.time_emb_proj",
+    "middle_block_1_proj_in": "mid_block.attentions.0.proj_in",
+    "middle_block_2_out_layers_3": "mid_block.resnets.1.conv2",
+    "output_blocks_0_0_skip_connection": "up_blocks.0.resnets.0.conv_shortcut",
+    "output_blocks_1_1_conv": "up_blocks.0.upsamplers.0.conv",
+    "output_blocks_3_1_transformer_blocks_0_attn2_to_out_0":
+        "up_blocks.1.attentions.1.transformer_blocks.0.attn2.to_out.0",
+    "time_embed_2": "time_embedding.linear_2",
+    "out_2": "conv_out",
+}
+
+
+def test_ldm_named_kohya_lora(pipe_dir, tmp_path):
+    """kohya files in the original LDM / SGM UNet naming land on the same modules as their
+    diffusers-named twins."""
+    from localai_amd.models.sd_lora import ldm_unet_path
+    base = StableDiffusion(pipe_dir, "cpu")
+    params = dict(base.unet.named_parameters())
+    g = torch.Generator().manual_seed(7)
+    ldm, diff = {}, {}
+    for k, name in LDM_NAMES.items():
+        assert ldm_unet_path(k, base.unet) == name.replace(".", "_"), k
+        w = params[name + ".weight"]
+        down = torch.randn((2,) + tuple(w.shape[1:]), generator=g) * 0.1
+        up = torch.randn((w.shape[0], 2) + tuple(1 for _ in w.shape[2:]), generator=g) * 0.1
+        for sd, key in ((ldm, "lora_unet_" + k), (diff, "lora_unet_" + name.replace(".", "_"))):
+            sd[key + ".lora_down.weight"], sd[key + ".lora_up.weight"] = down, up
+    fa, fb = str(tmp_path / "ldm.safetensors"), str(tmp_path / "diffusers.safetensors")
+    save_file(ldm, fa)
+    save_file(diff, fb)
+    a = StableDiffusion(pipe_dir, "cpu", lora=fa)
+    b = StableDiffusion(pipe_dir, "cpu", lora=fb)
+    for (n1, p1), (n2, p2) in zip(a.unet.named_parameters(), b.unet.named_parameters()):
+        assert n1 == n2 and torch.equal(p1, p2), n1
 
 
 def test_backend_lora_adapter_relative_to_model_dir(pipe_dir, tmp_path):
