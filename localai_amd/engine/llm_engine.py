@@ -161,6 +161,8 @@ class LLMEngine:
         self._gmask_pool: Optional[torch.Tensor] = None
         self._gmask_free: List[int] = []
         self._gmask_over: Dict[tuple, int] = {}   # states whose budgeted walk gave up once
+        self._gmask_pending: Dict[tuple, object] = {}   # full walks running on the helper thread
+        self._gmask_bg = None
         self._gnext: Optional[torch.Tensor] = None
         self._gtrans: Dict[tuple, Optional[int]] = {}   # (slot, token) -> next slot (host mirror)
         self._gtrans_in: Dict[int, set] = {}
@@ -356,6 +358,9 @@ class LLMEngine:
         if self._thread is not None:
             self._thread.join(timeout=10)
             self._thread = None
+        if self._gmask_bg is not None:
+            self._gmask_bg.shutdown(wait=False, cancel_futures=True)
+            self._gmask_bg = None
 
     def _loop(self):
         if self.device.type == "cuda":
@@ -1356,10 +1361,24 @@ class LLMEngine:
             c.move_to_end(key)
             return c[key]
         over = self._gmask_over
-        if key in over:
+        pend = self._gmask_pending
+        if key in pend:
+            if not pend[key].done():
+                return None             # the background walk is still running: top-N filter meanwhile
+            m = pend.pop(key).result()
+        elif key in over:
             # a permissive state seen again (e.g. `[a-z ]+`, or inside a string of a JSON
-            # schema): walk the whole trie once and keep its mask
+            # schema): walk the whole trie once and keep its mask.  A full walk can take tens of
+            # ms, so a single-rank engine runs it on a helper thread (the native walk releases
+            # the GIL) and keeps serving the state through the top-N filter until it is ready;
+            # tensor-parallel ranks walk inline so every rank takes the same decisions
             del over[key]
+            if self.tp.world == 1:
+                if self._gmask_bg is None:
+                    import concurrent.futures
+                    self._gmask_bg = concurrent.futures.ThreadPoolExecutor(1, thread_name_prefix="gmask")
+                pend[key] = self._gmask_bg.submit(gs.clone().mask)
+                return None
             m = gs.mask()
         else:
             m = gs.mask_limited(self.GRAMMAR_MASK_BUDGET)

@@ -159,3 +159,32 @@ def test_next_keys_and_clone():
     assert keys[5] == k0                                            # "1," loops back to the start
     c = st.clone()
     assert c.accept(1) and c.key() == keys[1] and st.key() == k0
+
+
+def test_engine_permissive_state_mask_walked_in_background(tiny_model_path):
+    """A permissive grammar state (most of the vocabulary allowed) is served by the top-N filter on
+    first sight, its full mask is walked on the helper thread when the state recurs, and the cached
+    mask is used once ready -- the constrained output obeys the grammar throughout."""
+    import re
+    import time
+
+    import torch
+
+    from localai_amd.engine.llm_engine import EngineConfig, LLMEngine
+    from localai_amd.engine.sampling_params import SamplingParams
+    eng = LLMEngine(EngineConfig(model_path=tiny_model_path, device="cpu", context_size=512, max_num_seqs=4,
+                                 use_graphs=False))
+    eng.GRAMMAR_MASK_BUDGET = 1           # every state is "permissive" for this test
+    g = 'root ::= [a-z ]+'
+    r = eng.generate("letters", SamplingParams(max_tokens=16, temperature=0.0, ignore_eos=True, grammar=g))
+    assert re.fullmatch(r"[a-z ]+", r["text"]), r
+    assert eng._gmask_bg is not None                                  # the recurring state went to the helper
+    for f in list(eng._gmask_pending.values()):
+        f.result(timeout=60)
+    V = eng.hp.n_vocab
+    r2 = eng.generate("letters", SamplingParams(max_tokens=8, temperature=0.0, ignore_eos=True, grammar=g))
+    assert re.fullmatch(r"[a-z ]+", r2["text"])
+    assert any(v is not None and v >= 0 for v in eng._gmask_cache.values())   # the walked mask is in the pool
+    assert eng._gmask_pool is not None and eng._gmask_pool.shape[1] == V
+    eng.shutdown()
+    assert eng._gmask_bg is None
