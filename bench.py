@@ -18,6 +18,11 @@ sum over replicas / max wall time over replicas.
                 server, or uvicorn with --server uvicorn) from out-of-process aiohttp SSE
                 clients (localai_amd/utils/loadgen.py) -> gateway -> engine (default)
 --mode engine : requests are fed to the engine directly (no HTTP), for kernel work
+
+--dp-mode gateway (http): the deployment shape of a LocalAI user with `data_parallel_size: N` --
+ONE gateway process (rank 0) takes concurrency x N streams and spreads them over the N engines
+(rank 0's in-process, ranks 1..N-1 over gRPC: parallel/replicas.py least-in-flight + prefix
+affinity); tokens/s is what that single gateway delivers.
 """
 import argparse
 import json
@@ -54,6 +59,10 @@ def parse():
     ap.add_argument("--clients", type=int, default=int(os.environ.get("BENCH_CLIENTS", 4)),
                     help="load-generator processes (separate from the server process)")
     ap.add_argument("--cache-dir", default=os.environ.get("LOCALAI_AMD_CACHE", "/tmp/localai_amd_cache"))
+    ap.add_argument("--dp-mode", default=os.environ.get("BENCH_DP_MODE", "ranks"), choices=["ranks", "gateway"],
+                    help="ranks: every rank serves its own gateway + load (summed); gateway: rank 0's ONE "
+                         "gateway serves all N GPUs (data_parallel_size: N behind parallel/replicas.py), the "
+                         "other ranks' engines answer it over backend.proto gRPC")
     ap.add_argument("--n-draft", type=int, default=0,
                     help="engine mode: n-gram speculative draft length (model-config n_draft); 0 = off")
     return ap.parse_args()
@@ -103,11 +112,15 @@ def main():
         sys.exit(spawn_ranks(args))
     loadgen = None
     tp_env = max(1, args.tp)
-    if args.mode == "http" and int(os.environ.get("RANK", "0")) % tp_env == 0:
+    gw = args.dp_mode == "gateway" and args.gpus > 1
+    if gw and (args.mode != "http" or tp_env > 1):
+        raise SystemExit("--dp-mode gateway needs --mode http and --tp 1")
+    if args.mode == "http" and int(os.environ.get("RANK", "0")) % tp_env == 0 and \
+            (not gw or int(os.environ.get("RANK", "0")) == 0):
         # client processes are started before this process touches the GPU (no fork/exec
         # from a GPU-initialised process)
         from localai_amd.utils.loadgen import LoadGen
-        loadgen = LoadGen(args.clients)
+        loadgen = LoadGen(args.clients * (args.gpus if gw else 1))
     import torch
     import torch.distributed as dist
 
@@ -201,6 +214,8 @@ def main():
             loadgen.close()
         return
 
+    if gw:
+        return gateway_dp(args, eng, loadgen, rank, world, leaders, t_gen, t_load, t_capture)
     msgs = user_messages(eng.tokenizer, args.concurrency, args.prompt_len, seed=replica)
     if args.mode == "http":
         runner = HttpRunner(eng, args, loadgen)
@@ -279,6 +294,78 @@ def main():
         dist.destroy_process_group()
 
 
+def gateway_dp(args, eng, loadgen, rank, world, ctl, t_gen, t_load, t_capture):
+    """--dp-mode gateway: rank 0 serves ONE gateway over all N engines; ranks 1..N-1 expose their
+    engine over backend.proto gRPC until rank 0 is done."""
+    import asyncio
+    import socket
+
+    import torch.distributed as dist
+    from localai_amd.grpc import backend_pb as pb
+    from localai_amd.grpc.rpc import GRPCBackend, serve
+    from localai_amd.grpc.servicer import EngineServicer
+
+    eng.start()
+    addr = ""
+    loop = server = None
+    if rank > 0:
+        sv = EngineServicer(device=str(eng.device))
+        sv.engine, sv.model_name, sv.state = eng, "llama3-8b-instruct", pb.StatusResponse.READY
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+        addr = f"127.0.0.1:{port}"
+        loop = asyncio.new_event_loop()
+        threading.Thread(target=loop.run_forever, daemon=True).start()
+        server = asyncio.run_coroutine_threadsafe(serve(sv, addr), loop).result(60)
+    addrs = [None] * world
+    dist.all_gather_object(addrs, addr, group=ctl)
+    if rank > 0:
+        dist.barrier(group=ctl)          # rank 0 ran every wave
+        asyncio.run_coroutine_threadsafe(server.stop(1), loop).result(30)
+        loop.call_soon_threadsafe(loop.stop)
+        eng.shutdown()
+        dist.barrier()
+        dist.destroy_process_group()
+        return
+    remote = [GRPCBackend(a) for a in addrs[1:]]
+    runner = HttpRunner(eng, args, loadgen, replicas=remote)
+    n = args.concurrency * world
+    msgs = user_messages(eng.tokenizer, n, args.prompt_len, seed=0)
+
+    def wave(w):
+        return runner.wave([f"(wave {w}) " + m for m in msgs])
+
+    for w in range(args.warmup):
+        wave(-1 - w)
+    t0 = time.perf_counter()
+    ttfts, tokens = [], 0
+    for s_ in range(args.steps):
+        tt, nt = wave(s_)
+        ttfts += tt
+        tokens += nt
+    elapsed = time.perf_counter() - t0
+    served = runner.replica_stats()
+    runner.close()
+    dist.barrier(group=ctl)
+    out = {
+        "metric": METRIC, "value": round(tokens / elapsed, 2), "unit": "tokens/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1000, 2),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
+        "p50_ttft_ms": round(percentile(ttfts, 50) * 1000, 2), "p90_ttft_ms": round(percentile(ttfts, 90) * 1000, 2),
+        "config": {"model": MODEL_NAMES.get(args.preset, args.preset), "global_batch": n,
+                   "seq_len": args.prompt_len + args.max_tokens, "prompt_tokens": args.prompt_len,
+                   "max_tokens": args.max_tokens, "parallelism": f"dp{world}-gateway",
+                   "endpoint": "/v1/chat/completions (stream)", "mode": "http",
+                   "sampling": "greedy, mirostat 0, ignore_eos", "replica_requests": served},
+        "setup_s": {"model_gen": round(t_gen, 1), "load": round(t_load, 1), "graph_capture": round(t_capture, 1)},
+    }
+    print(json.dumps(out), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 MODEL_NAMES = {"llama3-8b": "Llama-3-8B-Instruct GGUF Q4_K_M (random-init)",
                "llama3-70b": "Llama-3-70B-Instruct GGUF Q4_K_M (random-init)",
                "mixtral-8x7b": "Mixtral-8x7B GGUF Q4_K_M (random-init)"}
@@ -327,7 +414,7 @@ class HttpRunner:
     """Real gateway over HTTP: the FastAPI app on the native server (or uvicorn), driven by
     out-of-process aiohttp SSE clients."""
 
-    def __init__(self, eng, args, loadgen):
+    def __init__(self, eng, args, loadgen, replicas=None):
         import socket
         from localai_amd.gateway.app import create_app_for_engine
         self.args = args
@@ -337,7 +424,7 @@ class HttpRunner:
         s.close()
         self.eng = eng
         eng.start()  # engine loop thread: the servicer only enqueues requests
-        self.app, self.model_name = create_app_for_engine(eng, name="llama3-8b-instruct")
+        self.app, self.model_name = create_app_for_engine(eng, name="llama3-8b-instruct", replicas=replicas)
         if args.server == "native":
             from localai_amd.gateway.native_server import NativeHTTPServer
             self.server = NativeHTTPServer(self.app, "127.0.0.1", 0)
@@ -359,6 +446,11 @@ class HttpRunner:
     def wave(self, contents):
         return self.lg.wave(self.url, self.model_name, contents, self.args.max_tokens,
                             extra={"temperature": 0, "ignore_eos": True, "mirostat": 0})
+
+    def replica_stats(self):
+        """Requests each replica served (gateway DP mode), from the ReplicaBackend."""
+        h = getattr(self.app.state, "bench_handle", None)
+        return list(h.served) if h is not None and hasattr(h, "served") else None
 
     def close(self):
         self.lg.close()

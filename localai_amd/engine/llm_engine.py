@@ -192,7 +192,8 @@ class LLMEngine:
         self.kv = self.model.new_kv_cache(num_blocks, bs)
         self.drafter = None
         if cfg.draft_model:
-            self.drafter = DraftModel(cfg.draft_model, self.device, cfg.draft_max_seqs, self.ctx, self.hp.n_vocab)
+            self.drafter = DraftModel(cfg.draft_model, self.device, cfg.draft_max_seqs, self.ctx, self.hp.n_vocab,
+                                      max_batched_tokens=cfg.max_batched_tokens)
         self.sched = core.Scheduler(num_blocks, bs, cfg.max_num_seqs, cfg.max_batched_tokens, self.ctx,
                                     cfg.prefix_cache, 1 if (cfg.use_graphs and self.device.type == "cuda") else 0)
         self.max_blocks = (self.ctx + bs - 1) // bs
@@ -461,12 +462,11 @@ class LLMEngine:
             if tr is not None:
                 tr.complete("decode", t0, t1, batch=len(d_ids), device_steps=K)
             did = True
-        if did and self.tp.car is not None:
-            try:
-                self.tp.check_custom_ar(self.ctrl)
-            except Exception:
-                self._graphs.clear()   # the captured decode graphs call the custom kernel
-                raise
+        if did and self.tp.car is not None and self.leader:
+            # the custom all-reduce's error word, read after the step's token readback (no extra
+            # sync, no collective): a timeout on any rank sets every rank's word, and the leader
+            # hands the verdict to the group with the next step's control broadcast
+            self._ar_err = int(self.tp.car.error_flag())
         if tr is not None:
             tr.counter("sequences", time.perf_counter(), running=self.sched.num_running,
                        waiting=self.sched.num_waiting)
@@ -489,8 +489,12 @@ class LLMEngine:
             # any (most decode steps have none).  group_src: the leader is rank 0 of its replica's
             # group, not necessarily global rank 0 (data-parallel x tensor-parallel layouts)
             import torch.distributed as dist
-            n = torch.tensor([len(items)], dtype=torch.int64)
+            # [new work items, custom all-reduce error verdict of the last step]: ONE host
+            # collective per step
+            n = torch.tensor([len(items), getattr(self, "_ar_err", 0)], dtype=torch.int64)
             dist.broadcast(n, group_src=0, group=self.ctrl)
+            ar_err = int(n[1].item())
+            n = n[:1]
             if int(n.item()):
                 box = [[self._to_wire(it) for it in items] if self.leader else None]
                 dist.broadcast_object_list(box, group_src=0, group=self.ctrl)
@@ -512,6 +516,13 @@ class LLMEngine:
         for item in items:
             self._apply(item)
         self._mm_embs.clear()
+        if self.tp.world > 1 and ar_err and self.tp.car is not None:
+            from ..models.decoder import CustomAllReduceTimeout
+            self._ar_err = 0
+            self._graphs.clear()   # the captured decode graphs call the custom kernel
+            self.tp.drop_custom_ar()
+            raise CustomAllReduceTimeout("tensor-parallel custom all-reduce timed out on a late peer rank: the last "
+                                         "step's results are invalid; the group continues on RCCL")
 
     @staticmethod
     def _to_wire(item):

@@ -49,11 +49,13 @@ class DraftModel:
     The draft model keeps its own paged KV cache.  Per request it remembers which tokens its cache
     holds (`_cached`); a draft call first feeds every sequence the tokens it has not seen (the
     accepted tokens of the last verify, or the whole prompt the first time) in ONE chunked-prefill
-    forward over all sequences, then k-1 batched single-token decode forwards.  Cache entries past
-    the accepted prefix are simply overwritten by the next call (longest-common-prefix rule)."""
+    forward over all sequences (split into chunks of at most `max_batched_tokens` tokens, like the
+    main engine's chunked prefill: a first draft feeds the whole prompt), then k-1 batched
+    single-token decode forwards.  Cache entries past the accepted prefix are simply overwritten
+    by the next call (longest-common-prefix rule)."""
 
     def __init__(self, path: str, device, max_seqs: int, context_size: int, vocab_size: int,
-                 block_size: int = 32):
+                 block_size: int = 32, max_batched_tokens: int = 2048):
         import torch
 
         from ..models.decoder import DecoderModel
@@ -66,6 +68,7 @@ class DraftModel:
             raise ValueError(f"draft model vocabulary {self.model.hp.n_vocab} != main model {vocab_size}")
         self.bs = block_size
         self.ctx = context_size
+        self.max_tokens = max(1, int(max_batched_tokens))  # catch-up tokens per forward
         self.max_blocks = (context_size + block_size - 1) // block_size
         nblk = max(1, max_seqs) * self.max_blocks + 1
         self.kv = self.model.new_kv_cache(nblk, block_size)
@@ -113,8 +116,9 @@ class DraftModel:
         out: List[List[int]] = [[] for _ in seqs]
         if not live:
             return out
-        # 1) catch-up: tokens the draft cache has not seen, one chunked-prefill forward
-        toks, pos, slots, cu, ctxl = [], [], [], [0], []
+        # 1) catch-up: tokens the draft cache has not seen, as chunked-prefill forwards of at most
+        #    max_tokens tokens (a sequence's range may span several chunks, in position order)
+        segs = []
         for i in live:
             rid, seq = rids[i], list(seqs[i])
             old = self._cached.get(rid, [])
@@ -122,25 +126,41 @@ class DraftModel:
             m = min(len(old), len(seq) - 1)  # always re-feed at least the last token
             while lcp < m and old[lcp] == seq[lcp]:
                 lcp += 1
-            pages = self._ensure_pages(rid, len(seq) + ks[i], keep=set(rids))
-            for p in range(lcp, len(seq)):
-                toks.append(seq[p])
-                pos.append(p)
-                slots.append(self._slot(pages, p))
-            cu.append(len(toks))
-            ctxl.append(len(seq))
+            self._ensure_pages(rid, len(seq) + ks[i], keep=set(rids))
+            segs.append((i, lcp, len(seq)))
             self._cached[rid] = seq
-        qlens = [cu[j + 1] - cu[j] for j in range(len(live))]
-        rl = [rids[i] for i in live]
-        last = self._i32([c - 1 for c in cu[1:]])
-        fb = ForwardBatch(tokens=self._i32(toks), pos=self._i32(pos), slots=self._i32(slots), decode=False,
-                          block_tables=self._table(rl), cu_q=self._i32(cu), ctx_lens=self._i32(ctxl),
-                          tiles=ops.prefill_tiles(qlens, self.device) if self.device.type == "cuda" else None,
-                          logits_idx=last)
-        cur = self.model.forward(fb, self.kv).argmax(-1)
-        nxt = [int(t) for t in cur.tolist()]
-        for j, i in enumerate(live):
-            out[i].append(nxt[j])
+        chunks, cur, n = [], [], 0
+        for i, a, b in segs:
+            while a < b:
+                take = min(b - a, self.max_tokens - n)
+                cur.append((i, a, a + take))
+                n += take
+                a += take
+                if n >= self.max_tokens:
+                    chunks.append(cur)
+                    cur, n = [], 0
+        if cur:
+            chunks.append(cur)
+        for ch in chunks:
+            toks, pos, slots, cu, ctxl = [], [], [], [0], []
+            for i, a, b in ch:
+                seq, pages = seqs[i], self._pages[rids[i]]
+                for p in range(a, b):
+                    toks.append(seq[p])
+                    pos.append(p)
+                    slots.append(self._slot(pages, p))
+                cu.append(len(toks))
+                ctxl.append(b)
+            qlens = [cu[j + 1] - cu[j] for j in range(len(ch))]
+            fb = ForwardBatch(tokens=self._i32(toks), pos=self._i32(pos), slots=self._i32(slots), decode=False,
+                              block_tables=self._table([rids[i] for i, _, _ in ch]), cu_q=self._i32(cu),
+                              ctx_lens=self._i32(ctxl),
+                              tiles=ops.prefill_tiles(qlens, self.device) if self.device.type == "cuda" else None,
+                              logits_idx=self._i32([c - 1 for c in cu[1:]]))
+            nxt = self.model.forward(fb, self.kv).argmax(-1).tolist()
+            for j, (i, a, b) in enumerate(ch):
+                if b == len(seqs[i]):     # the piece holding the sequence's last token
+                    out[i].append(int(nxt[j]))
         # 2) k-1 batched single-token decode forwards over the sequences still drafting
         kmax = max(ks[i] for i in live)
         for step in range(1, kmax):

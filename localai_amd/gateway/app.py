@@ -151,7 +151,8 @@ LLAMA3_CHAT = "<|begin_of_text|>{{.Input }}\n<|start_header_id|>assistant<|end_h
 
 
 def create_app_for_engine(engine, name: str = "llama3-8b-instruct", models_path: Optional[str] = None,
-                          app_config: Optional[ApplicationConfig] = None) -> Tuple[FastAPI, str]:
+                          app_config: Optional[ApplicationConfig] = None,
+                          replicas: Optional[list] = None) -> Tuple[FastAPI, str]:
     """Serve an already-constructed LLMEngine under `name` (bench / embedding use).
 
     The model config is the one the reference's guesser produces for a Llama-3 GGUF
@@ -169,7 +170,13 @@ def create_app_for_engine(engine, name: str = "llama3-8b-instruct", models_path:
     sv.engine = engine
     sv.model_name = name
     sv.state = pb.StatusResponse.READY
-    state.manager.register(name, "localai-amd", EmbeddedBackend(sv), servicer=sv)
+    handle = EmbeddedBackend(sv)
+    if replicas:
+        # data-parallel replicas behind the one handle (this engine first, then the remote ones)
+        from ..parallel.replicas import ReplicaBackend
+        handle = ReplicaBackend([handle] + list(replicas), ["embedded"] + [r.addr for r in replicas])
+    state.manager.register(name, "localai-amd" if not replicas else f"localai-amd-dp{1 + len(replicas)}", handle,
+                           servicer=sv)
     bc = BackendConfig({
         "name": name, "backend": "localai-amd", "context_size": engine.cfg.context_size, "mirostat": 0,
         "parameters": {"model": os.path.basename(engine.cfg.model_path), "temperature": 0.8, "top_k": 40,
@@ -179,4 +186,6 @@ def create_app_for_engine(engine, name: str = "llama3-8b-instruct", models_path:
     })
     bc.set_defaults()
     state.configs.add(bc)
-    return create_app(state), name
+    app = create_app(state)
+    app.state.bench_handle = handle
+    return app, name

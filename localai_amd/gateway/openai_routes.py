@@ -545,6 +545,14 @@ async def _native_stream(request, state, cfg, req, pred_input: str, cid: str, cr
     from .native_server import NativeHandledResponse
     po = predict_options(cfg, pred_input, req.get("messages"), state.models_path)
     po.CorrelationId = req.get("_correlation_id", "")
+    pick = getattr(lm.handle, "pick_native", None)
+    rep = None
+    if pick is not None:
+        # data-parallel replicas: the balancer picks; a remote pick takes the generic RPC path
+        rep, sv = pick(po)
+        if sv is None:
+            return None
+        eng = sv.engine
     prompt = sv._prompt(po)
     params = sv._params(po)
     obj = "chat.completion.chunk" if kind == "chat" else "text_completion"
@@ -588,6 +596,8 @@ async def _native_stream(request, state, cfg, req, pred_input: str, cid: str, cr
             metrics.ttft.labels(mid_).observe(tt)
             if ev.completion_tokens > 1:
                 metrics.itl.labels(mid_).observe((time.perf_counter() - t0 - tt) / (ev.completion_tokens - 1))
+        if rep is not None:
+            lm.handle._done(rep)
         loop.call_soon_threadsafe(state.manager.mark_busy, mid_, False)
 
     eng.add_request(prompt, params, on_final, sink=sink)

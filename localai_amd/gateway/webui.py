@@ -34,6 +34,8 @@ button{cursor:pointer}button:hover{background:#2b3242}
 .u{color:#8ab4ff}.a{color:#e6e6e6}.muted{color:#8a93a5;font-size:.9em}
 .row{display:flex;gap:.6em;margin:.8em 0}.row>*{flex:1}.row>button,.row>select{flex:0 0 auto}
 pre.code{background:#0b0d12;border:1px solid #2a2f3a;border-radius:6px;padding:.6em;overflow-x:auto}
+.card{border:1px solid #2a2f3a;border-radius:8px;padding:.6em 1em;margin:.6em 0}.tag{background:#1f2430;border-radius:4px;padding:0 .4em;margin-right:.3em;font-size:.85em}
+.progress{background:#1f2430;border-radius:4px;height:10px;width:60%;display:inline-block}.progress .bar{background:#ff7a45;height:10px;border-radius:4px}
 .grid{display:grid;grid-template-columns:repeat(auto-fill,minmax(220px,1fr));gap:.8em}.grid img{width:100%;border-radius:6px}
 label{color:#8a93a5;font-size:.9em;align-self:center}
 """
@@ -109,26 +111,47 @@ inp.addEventListener('keydown', e => { if(e.key === 'Enter' && !e.shiftKey){ e.p
 """
 
 _BROWSE_JS = _AUTH_JS + """
-async function install(btn){
-  // gallery ids and names come from third-party indexes: they travel as data-* attribute values
-  // (HTML-escaped by the server, read back as plain strings), never as JS source
-  const id = btn.dataset.id;
-  const r = await fetch('/models/apply', {method:'POST', headers:hdrs(), body: JSON.stringify({id})});
-  const j = await r.json(); const cell = btn.closest('tr').querySelector('td.st');
-  if(!j.uuid){cell.textContent = 'error'; return;}
-  for(;;){
-    const s = await (await fetch('/models/jobs/' + j.uuid, {headers:hdrs()})).json();
-    cell.textContent = s.processed ? (s.error ? 'error: ' + s.error : 'installed') : (s.message || '') + ' ' + (s.progress ? s.progress.toFixed(0) + '%' : '');
-    if(s.processed) break; await new Promise(r => setTimeout(r, 1000));
-  }
+// The gallery actions talk to the reference's htmx routes (core/http/routes/ui.go:169-300):
+// POST /browse/search/models -> card list fragment, POST /browse/install|delete/model/:id ->
+// progress fragment, GET /browse/job/progress/:uid every 600 ms until the response carries
+// HX-Trigger: done, then GET /browse/job/:uid for the final fragment.  htmx itself is not
+// shipped (air-gapped servers): this file does the three swaps it would do.
+async function post(url, form){
+  const h = hdrs(); delete h['Content-Type'];
+  return fetch(url, {method:'POST', headers:h, body: form || null});
 }
-async function remove(btn){
-  const name = btn.dataset.name;
-  await fetch('/models/delete/' + encodeURIComponent(name), {method:'POST', headers:hdrs()});
-  location.reload();
+async function search(){
+  const fd = new FormData(); fd.append('search', document.getElementById('q').value);
+  const r = await post('/browse/search/models', fd);
+  document.getElementById('cards').innerHTML = await r.text(); wire();
 }
-function filter(){const q = document.getElementById('q').value.toLowerCase();
-  for(const tr of document.querySelectorAll('tbody tr')) tr.style.display = tr.dataset.k.includes(q) ? '' : 'none';}
+async function act(btn, kind){
+  // gallery ids come from third-party indexes: read back from a data-* attribute (server-escaped)
+  const id = btn.dataset.id, box = btn.closest('.actions');
+  if(kind === 'delete' && !confirm('Are you sure you wish to delete the model?')) return;
+  const r = await post('/browse/' + kind + '/model/' + encodeURIComponent(id));
+  box.innerHTML = await r.text(); poll(box);
+}
+function poll(box){
+  const job = box.querySelector('[data-job]'); if(!job) return wire();
+  const uid = job.dataset.job, bar = job.querySelector('.pbar');
+  const tick = async () => {
+    const r = await fetch('/browse/job/progress/' + uid, {headers:hdrs()});
+    bar.innerHTML = await r.text();
+    if(r.headers.get('HX-Trigger') === 'done'){
+      box.innerHTML = await (await fetch('/browse/job/' + uid, {headers:hdrs()})).text(); wire(); return;
+    }
+    if(bar.querySelector('.err')) { wire(); return; }
+    setTimeout(tick, 600);
+  };
+  tick();
+}
+function wire(){
+  for(const b of document.querySelectorAll('button[data-act]')) b.onclick = () => act(b, b.dataset.act);
+  for(const box of document.querySelectorAll('.actions')) if(box.querySelector('[data-job]') && !box.dataset.polling){
+    box.dataset.polling = '1'; poll(box); }
+}
+window.addEventListener('load', wire);
 """
 
 _TTS_JS = _AUTH_JS + """
@@ -218,6 +241,67 @@ async function toggle(){
 """
 
 
+def _drop_bad(s: str) -> str:
+    """DOM-id-safe gallery id (ui.go's dropBadChars: '@' -> '__')."""
+    return s.replace("@", "__")
+
+
+def _progress_bar(pct) -> str:
+    p = max(0.0, min(100.0, float(pct or 0)))
+    return (f"<div class=progress role=progressbar aria-valuemin=0 aria-valuemax=100 aria-valuenow={p:.0f}>"
+            f"<div class=bar style='width:{p:.0f}%'></div></div><span class=muted>{p:.0f}%</span>")
+
+
+def _start_progress(uid: str, text: str) -> str:
+    u = html.escape(uid)
+    return (f"<div data-job=\"{u}\" hx-trigger=done hx-get=\"/browse/job/{u}\" hx-swap=outerHTML>"
+            f"<h4 role=status>{html.escape(text)}</h4><div class=pbar hx-get=\"/browse/job/progress/{u}\" "
+            f"hx-trigger='every 600ms' hx-swap=innerHTML>{_progress_bar(0)}</div></div>")
+
+
+def _action_button(kind: str, gid: str) -> str:
+    label = {"install": "Install", "delete": "Delete", "reinstall": "Reinstall"}[kind]
+    route = "delete" if kind == "delete" else "install"
+    return (f"<button data-act={route} data-id=\"{html.escape(gid)}\" hx-post=\"/browse/{route}/model/"
+            f"{html.escape(urllib.parse.quote(gid, safe='@'))}\">{label}</button>")
+
+
+def _model_cards(models, installed, processing: dict, statuses) -> str:
+    """The gallery card list (elements.ListModels): name, description, repository, license, tags,
+    links, and an action box holding the install / delete button or a running job's progress."""
+    out = []
+    for m in models:
+        gname = (m.get("gallery") or {}).get("name", "")
+        name = m.get("name", "")
+        gid = f"{gname}@{name}"
+        meta = [f"repository: {html.escape(gname)}"]
+        if m.get("license"):
+            meta.append(f"license: {html.escape(str(m['license']))}")
+        tags = " ".join(f"<span class=tag>{html.escape(str(t))}</span>" for t in (m.get("tags") or []))
+        links = " ".join(f"<a href=\"{html.escape(str(u))}\" target=_blank rel=noopener>link #{i + 1}</a>"
+                         for i, u in enumerate(m.get("urls") or []))
+        uid = processing.get(gid)
+        if uid:
+            st = statuses(uid) or {}
+            box = _start_progress(uid, "Deletion" if st.get("deletion") else "Installation")
+        elif name in installed:
+            box = _action_button("reinstall", gid) + " " + _action_button("delete", gid)
+        else:
+            box = _action_button("install", gid)
+        out.append(f"<div class=card><h4>{html.escape(name)}</h4><p class=muted>"
+                   f"{html.escape((m.get('description') or '')[:300])}</p><p class=muted>{' · '.join(meta)}</p>"
+                   f"<p>{tags}</p><p>{links}</p><div class=actions id=\"action-div-{html.escape(_drop_bad(gid))}\">"
+                   f"{box}</div></div>")
+    return "".join(out) or "<p class=muted>no models match</p>"
+
+
+def _search(models, term: str):
+    """GalleryModels.Search (core/gallery/request.go:39-51): case-sensitive substring of the name,
+    the description, the gallery name or the comma-joined tags."""
+    return [m for m in models if term in m.get("name", "") or term in (m.get("description") or "")
+            or term in (m.get("gallery") or {}).get("name", "") or term in ",".join(m.get("tags") or [])]
+
+
 def build_router(state) -> APIRouter:
     r = APIRouter()
 
@@ -247,33 +331,93 @@ def build_router(state) -> APIRouter:
                 f"<a href='/metrics'>metrics</a> · <a href='/system'>system</a> · <a href='/swagger'>API docs</a></p>")
         return _page("LocalAI", body, _HOME_JS)
 
-    async def browse():
+    # gallery id -> job uid of the install / delete running from the UI (ui.go processingModels)
+    processing: dict = {}
+
+    async def _available():
         import asyncio
 
         from .. import gallery as gal
+        return [m.to_json() for m in await asyncio.to_thread(gal.available_models, state.cfg.galleries,
+                                                              state.models_path)]
+
+    def _status(uid):
+        g = getattr(state, "gallery", None)
+        return g.get(uid) if g is not None else None
+
+    async def browse():
         try:
-            avail = [m.to_json() | {"id": m.id()} for m in await asyncio.to_thread(
-                gal.available_models, state.cfg.galleries, state.models_path)]
-            err = ""
+            avail, err = await _available(), ""
         except Exception as e:  # gallery unreachable (air-gapped): show installed only
             avail, err = [], str(e)
-        installed = set(models())
-        rows = []
-        for m in avail:
-            gid = m.get("id") or f"{m.get('gallery', {}).get('name', '')}@{m.get('name', '')}"
-            name = m.get("name", gid)
-            key = (name + " " + " ".join(m.get("tags") or []) + " " + (m.get("description") or "")).lower()
-            act = (f"<button data-name=\"{html.escape(name)}\" onclick='remove(this)'>delete</button>"
-                   if name in installed else
-                   f"<button data-id=\"{html.escape(gid)}\" onclick='install(this)'>install</button>")
-            rows.append(f"<tr data-k=\"{html.escape(key)}\"><td>{html.escape(name)}</td>"
-                        f"<td class=muted>{html.escape((m.get('description') or '')[:140])}</td>"
-                        f"<td>{act}</td><td class=st></td></tr>")
-        body = ("<h2>Model gallery</h2><div class=row><input id=q placeholder='search' oninput='filter()'></div>"
+        cards = _model_cards(avail, set(models()), processing, _status)
+        body = ("<h2>Model gallery</h2><div class=row><input id=q name=search placeholder='search' "
+                "hx-post=/browse/search/models hx-trigger='keyup changed delay:500ms' hx-target=#cards "
+                "oninput='search()'></div>"
                 + (f"<p class=muted>gallery unavailable: {html.escape(err)}</p>" if err else "")
-                + "<table><thead><tr><th>model</th><th>description</th><th></th><th>status</th></tr></thead>"
-                + f"<tbody>{''.join(rows)}</tbody></table>")
+                + f"<p class=muted>{len(avail)} models available</p><div id=cards>{cards}</div>")
         return _page("Models", body, _BROWSE_JS)
+
+    async def browse_search(request: Request):
+        from ..utils.multipart import read_form
+        try:
+            form = await read_form(request) if await request.body() else {}
+        except ValueError:
+            form = {}
+        term = str(form.get("search", ""))
+        try:
+            avail = await _available()
+        except Exception as e:
+            return HTMLResponse(f"<p class=muted>gallery unavailable: {html.escape(str(e))}</p>")
+        return HTMLResponse(_model_cards(_search(avail, term), set(models()), processing, _status))
+
+    def _svc():
+        g = getattr(state, "gallery", None)
+        if g is None:
+            raise RuntimeError("gallery service not running")
+        return g
+
+    async def browse_install(gid: str):
+        from .. import gallery as gal
+        op = gal.GalleryOp(id=gal.new_op_id(), gallery_model_name=gid, galleries=list(state.cfg.galleries))
+        processing[gid] = op.id
+        _svc().submit(op)
+        return HTMLResponse(_start_progress(op.id, "Installation"))
+
+    async def browse_delete(gid: str):
+        from .. import gallery as gal
+        name = gid.split("@", 1)[1] if "@" in gid else gid  # local models need no repository id
+        op = gal.GalleryOp(id=gal.new_op_id(), gallery_model_name=name, delete=True)
+        processing[name] = op.id
+        processing[gid] = op.id
+        _svc().submit(op)
+        state.configs.remove(name)
+        return HTMLResponse(_start_progress(op.id, "Deletion"))
+
+    def _forget(uid: str):
+        for k in [k for k, v in processing.items() if v == uid]:
+            del processing[k]
+
+    async def browse_job_progress(uid: str):
+        st = _status(uid)
+        if st is None:
+            return HTMLResponse(_progress_bar(0))
+        if st.get("error"):
+            _forget(uid)
+            name = st.get("gallery_model_name", "")
+            return HTMLResponse(f"<div class=err><h4 role=status>Error {html.escape(str(st['error']))}</h4>"
+                                f"{_action_button('install', name)}</div>")
+        if st.get("processed") and float(st.get("progress") or 0) >= 100:
+            return HTMLResponse(_progress_bar(100), headers={"HX-Trigger": "done"})
+        return HTMLResponse(_progress_bar(st.get("progress", 0)))
+
+    async def browse_job(uid: str):
+        st = _status(uid) or {}
+        gid = next((k for k, v in processing.items() if v == uid and "@" in k), "") or st.get("gallery_model_name", "")
+        _forget(uid)
+        if st.get("deletion"):
+            return HTMLResponse(f"<h4 role=status>Deletion completed</h4>{_action_button('reinstall', gid)}")
+        return HTMLResponse(f"<h4 role=status>Installation completed</h4>{_action_button('delete', gid)}")
 
     async def chat(model: str = ""):
         ms = models()
@@ -344,6 +488,11 @@ def build_router(state) -> APIRouter:
     r.add_api_route("/", home, methods=["GET"])
     if not state.cfg.disable_webui:
         r.add_api_route("/browse", browse, methods=["GET"])
+        r.add_api_route("/browse/search/models", browse_search, methods=["POST"])
+        r.add_api_route("/browse/install/model/{gid:path}", browse_install, methods=["POST"])
+        r.add_api_route("/browse/delete/model/{gid:path}", browse_delete, methods=["POST"])
+        r.add_api_route("/browse/job/progress/{uid}", browse_job_progress, methods=["GET"])
+        r.add_api_route("/browse/job/{uid}", browse_job, methods=["GET"])
         r.add_api_route("/chat/", chat, methods=["GET"])
         r.add_api_route("/chat/{model}", chat_model, methods=["GET"])
         r.add_api_route("/tts/", tts, methods=["GET"])

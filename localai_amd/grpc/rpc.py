@@ -59,7 +59,19 @@ class GRPCBackend:
 
     def __init__(self, addr: str):
         self.addr = addr
-        self.channel = grpc.aio.insecure_channel(addr, options=_OPTS)
+        self.channel = None
+        self._calls = {}
+        self._loop = None
+        try:
+            asyncio.get_running_loop()
+            self._connect()
+        except RuntimeError:
+            pass  # built outside an event loop: connect on first use, on the loop that uses it
+
+    def _connect(self):
+        # a grpc.aio channel belongs to the event loop it was created on
+        self._loop = asyncio.get_running_loop()
+        self.channel = grpc.aio.insecure_channel(self.addr, options=_OPTS)
         self._calls = {}
         for rpc, req, resp, stream in pb.RPCS:
             mk = self.channel.unary_stream if stream else self.channel.unary_unary
@@ -67,20 +79,22 @@ class GRPCBackend:
                                   response_deserializer=pb.M[resp].FromString)
 
     def __getattr__(self, rpc):
-        calls = self.__dict__.get("_calls", {})
-        if rpc in calls:
-            return calls[rpc]
+        if any(r == rpc for r, _, _, _ in pb.RPCS):
+            if self.__dict__.get("channel") is None:
+                self._connect()
+            return self.__dict__["_calls"][rpc]
         raise AttributeError(rpc)
 
     async def health(self, timeout: float = 5.0) -> bool:
         try:
-            r = await self._calls["Health"](pb.HealthMessage(), timeout=timeout)
+            r = await self.Health(pb.HealthMessage(), timeout=timeout)
             return r.message == b"OK"
         except Exception:
             return False
 
     async def close(self):
-        await self.channel.close()
+        if self.channel is not None:
+            await self.channel.close()
 
 
 class EmbeddedBackend:

@@ -41,6 +41,9 @@ FUSED_ROUTER_OFF = os.environ.get("LOCALAI_AMD_FUSED_ROUTER_OFF", "0") == "1"
 _ACT = {"swiglu": ops.ACT_SWIGLU, "gelu": ops.ACT_GELU, "geglu": ops.ACT_GEGLU}
 
 
+TP_AR_BF16 = os.environ.get("LOCALAI_AMD_TP_AR_BF16", "1") == "1"
+
+
 class CustomAllReduceTimeout(RuntimeError):
     pass
 
@@ -60,6 +63,11 @@ class TPInfo:
             import torch.distributed as dist
             dist.all_reduce(t, group=self.group)  # RCCL: prefill chunks, CPU (gloo)
         return t
+
+    def drop_custom_ar(self) -> None:
+        car, self.car = self.car, None
+        if car is not None:
+            car.close()
 
     def check_custom_ar(self, ctrl) -> None:
         """Called once per engine step, at a host sync point that exists anyway: if ANY rank's
@@ -439,6 +447,12 @@ class DecoderModel:
     def _row_parallel_out(self, p: ops.Partial, bias) -> ops.Partial:
         if self.tp.world == 1:
             return ops.Partial(p.t, bias)
+        if TP_AR_BF16 and p.t.is_cuda:
+            # decode rows travel in bf16 (16 KiB per 8192-wide row): half the bytes
+            # of the fp32 sum over xGMI; the consumer (add_norm) reads a bf16 matrix directly
+            dense = ops.reduce(p, dtype=torch.bfloat16)
+            self.tp.all_reduce(dense)
+            return ops.Partial(dense, bias)
         dense = ops.reduce(p)
         self.tp.all_reduce(dense)
         return ops.Partial(dense.unsqueeze(0), bias)

@@ -79,6 +79,10 @@ def lib():
             "la_qgemm_tile2": [I, P, P, P, I, I, P, P, P, I, I, P, I, I, I, P, I, LNG, I, I, P],
             "la_pen_push": [P, I, P, I, P, P, P, P],
             "la_qgemm_glu": [I, P, P, P, I, P, P, P, I, I, I, P, I, I, P, I, I, I, P],
+            "la_qgemm32": [I, P, P, P, I, I, P, I, I, I, P, I, LNG, I, I, P],
+            "la_qgemm32_2": [I, P, P, P, I, I, P, P, P, I, I, P, I, I, I, P, I, LNG, I, I, P],
+            "la_qgemm32_glu": [I, P, P, P, I, P, P, P, I, I, I, P, I, I, P, I, I, I, P],
+            "la_qgemm32_probe": [I, I, P, P, I, I, P, I, I, P, P],
             "la_decode_advance": [P, P, P, P, P, P, I, I, I, P, I, P, P, P],
             "la_img_resample_h": [P, I, I, P, I, P, P, I, P],
             "la_img_resample_v_tiles": [P, I, I, P, P, I, I, I, I, I, I, I, P, P, P, P, P],
@@ -644,18 +648,37 @@ def fuse_bf16(ws: Sequence[QWeight]) -> Optional[torch.Tensor]:
 _SCRATCH: dict = {}
 
 
+def _scratch(device, need: int) -> torch.Tensor:
+    """bf16 dequant scratch of >= need elements for the calling thread.
+
+    One buffer per (device, thread): two engines serving from different threads on one GPU
+    (in-process whisper / CLIP / a second LLM) enqueue their dequant + GEMM pairs interleaved,
+    so a shared buffer would hand one engine's GEMM the other's weights.  Inside a stream
+    capture the buffer is allocated fresh from the graph's private pool instead: a replayed
+    graph must never write into memory that a later (larger) scratch reallocation returned to
+    the caching allocator."""
+    if torch.cuda.is_current_stream_capturing():
+        return torch.empty(need, dtype=torch.bfloat16, device=device)
+    key = (device, threading.get_ident())
+    buf = _SCRATCH.get(key)
+    if buf is None or buf.numel() < need:
+        _SCRATCH.pop(key, None)
+        buf = _SCRATCH[key] = torch.empty(need, dtype=torch.bfloat16, device=device)
+    return buf
+
+
 def _run_scratch_blas(x, ws, Ntot):
-    """Large-M (prefill chunk) GEMM: dequantise the weights into ONE per-device bf16 scratch
+    """Large-M (prefill chunk) GEMM: dequantise the weights into a per-thread bf16 scratch
     buffer (reused by every call, sized by the largest fused weight seen), then a library GEMM
     on it -- the reference's own large-batch path (ggml convert.cu dequant + hipBLAS GemmEx,
     SURVEY K7), without a persistent bf16 copy of the model.  The dequant streams the quantised
-    bytes once and writes 2 B/weight: ~6 % of a 8192-row chunk's GEMM time."""
+    bytes once and writes 2 B/weight: ~6 % of a 8192-row chunk's GEMM time.  A lone bf16 weight
+    is multiplied in place (no copy)."""
     K = x.shape[1]
+    if len(ws) == 1 and ws[0].fmt == FMT_BF16:
+        return torch.matmul(x, ws[0].planes[0].view(torch.bfloat16).view(ws[0].N, K).t())
     need = Ntot * K
-    buf = _SCRATCH.get(x.device)
-    if buf is None or buf.numel() < need:
-        buf = _SCRATCH[x.device] = torch.empty(need, dtype=torch.bfloat16, device=x.device)
-    wt = buf[:need].view(Ntot, K)
+    wt = _scratch(x.device, need)[:need].view(Ntot, K)
     row = 0
     for w in ws:
         if w.fmt == FMT_BF16:
@@ -738,6 +761,50 @@ def _run_tile(x, ws, S, out, Ntot, tile):
         col += w.N
 
 
+# 32x32x16 quantised GEMM (gemm_q32.hip): variant id -> (BM, BN).  Variants 2 / 6 (256 x 256
+# tiles) are built for Q4_K only and not for two-weight launches.
+Q32_TILES = {0: (256, 128), 1: (128, 256), 2: (256, 256), 3: (128, 128), 4: (256, 128), 5: (128, 256),
+             6: (256, 256), 7: (128, 128), 8: (128, 256), 9: (128, 256)}
+Q32_FMTS = (FMT_Q4_K, FMT_Q6_K, FMT_Q8_0)
+Q32 = os.environ.get("LOCALAI_AMD_Q32", "1") == "1"
+
+
+def q32_ok(ws: Sequence[QWeight], var: int) -> bool:
+    """Can the 32x32x16 kernel run these weights (one launch per weight, or one for a Q4_K/Q6_K
+    pair) in this variant."""
+    if not Q32 or not all(w.fmt in Q32_FMTS and w.K % 256 == 0 and w.planes[0] is not None for w in ws):
+        return False
+    if var in (2, 6):
+        return all(w.fmt == FMT_Q4_K for w in ws) and len(ws) == 1
+    return True
+
+
+def _run_q32(x, ws, S, out, Ntot, var):
+    """out: fp32 slabs [S, M, Ntot], or a bf16 [M, Ntot] matrix (S == 1).  A Q4_K/Q6_K pair (q|k +
+    v) runs as ONE launch (la_qgemm32_2)."""
+    M, K = x.shape
+    bf = out.dtype == torch.bfloat16
+    esz = 2 if bf else 4
+    if len(ws) == 2 and (ws[0].fmt, ws[1].fmt) in _TILE2_PAIRS:
+        a0, a1, ag = ws[0].tile_planes()
+        b0, b1, bg = ws[1].tile_planes()
+        _check(lib().la_qgemm32_2(ws[0].fmt, a0, a1, ag, ws[0].N, ws[1].fmt, b0, b1, bg, ws[1].N, K, x.data_ptr(), K,
+                                  M, S, out.data_ptr(), Ntot, 0 if bf else M * Ntot, int(bf), var, _stream()),
+               "la_qgemm32_2")
+        return
+    col = 0
+    for w in ws:
+        p0, p1, g = w.tile_planes()
+        _check(lib().la_qgemm32(w.fmt, p0, p1, g, w.N, w.K, x.data_ptr(), K, M, S, out.data_ptr() + col * esz, Ntot,
+                                0 if bf else M * Ntot, int(bf), var, _stream()), "la_qgemm32")
+        col += w.N
+
+
+def _q32_grid(M: int, N: int, var: int) -> int:
+    bm, bn = Q32_TILES[var]
+    return -(-M // bm) * -(-N // bn)
+
+
 def _tile_grid(M: int, N: int, tile: int) -> int:
     bm, bn = GQ_TILES[tile]
     return -(-M // bm) * -(-N // bn)
@@ -778,6 +845,13 @@ def _autotune_mid(x, ws, key, Ntot):
             for S in sorted({1, max(1, base // 2), base, base * 2}):
                 if S <= min(8, K // 256) and _tile_split_ok(K, S):
                     cands.append(("tile", S, t))
+        for v in ((9, 8, 4, 6, 0) if M > 128 else (9, 8, 7, 3)):
+            if not q32_ok(ws, v):
+                continue
+            base = max(1, round(256 / _q32_grid(M, N, v)))
+            for S in sorted({1, max(1, base // 2), base, base * 2}):
+                if S <= min(8, K // 256) and _tile_split_ok(K, S):
+                    cands.append(("q32", S, v))
     if not cands or os.environ.get("LOCALAI_AMD_BLAS_CANDIDATE") == "1" or not TILE_GEMM:
         cands.append(("blas", 0, 0))
     if not TILE_GEMM:
@@ -793,6 +867,8 @@ def _autotune_mid(x, ws, key, Ntot):
             fn = lambda: _run_blas(x, ws, Ntot)  # noqa: E731
         elif kind == "tile":
             fn = lambda S=S, t=t: _run_tile(x, ws, S, outs[S], Ntot, t)  # noqa: E731
+        elif kind == "q32":
+            fn = lambda S=S, t=t: _run_q32(x, ws, S, outs[S], Ntot, t)  # noqa: E731
         else:
             fn = lambda S=S, t=t: _run_mid(x, ws, S, outs[S], Ntot, t)  # noqa: E731
         fn()
@@ -845,6 +921,9 @@ def linear_multi(x: torch.Tensor, ws: Sequence[QWeight], bias: Optional[torch.Te
         S, kind = 1, "ws"
     elif force == "mid":
         S, kind = min(pick_mid_splits(w.N, w.K, M) for w in ws), "mid"
+    elif force is not None and force.startswith("q32:"):
+        _, v, s_ = force.split(":")
+        tile, S, kind = int(v), int(s_), "q32"
     elif force is not None and force.startswith("tile"):
         # "tile" (heuristic) or "tile:<id>:<S>"
         parts = force.split(":")
@@ -860,14 +939,14 @@ def linear_multi(x: torch.Tensor, ws: Sequence[QWeight], bias: Optional[torch.Te
         if choice is None and tile_ok:
             t, s_ = pick_tile(M, [w.N for w in ws], K)
             choice = ("tile", s_, t)
-        if choice is not None and choice[0] in ("mid", "ws", "dq", "tile"):
+        if choice is not None and choice[0] in ("mid", "ws", "dq", "tile", "q32"):
             kind, S, tile = choice
     elif force is None and not use_skinny and tile_ok and PREFILL_GEMM == "tile":
         tile, S = pick_tile(M, [w.N for w in ws], K)   # prefill: heuristic, never tuned inline
         kind = "tile"
-    if kind == "tile" and S == 1 and out_slabs is None:
+    if kind in ("tile", "q32") and S == 1 and out_slabs is None:
         y = torch.empty(M, Ntot, dtype=torch.bfloat16, device=x.device)
-        _run_tile(x, ws, 1, y, Ntot, tile)
+        (_run_tile if kind == "tile" else _run_q32)(x, ws, 1, y, Ntot, tile)
         return Partial(y, bias)
     if S:
         out = out_slabs
@@ -875,6 +954,8 @@ def linear_multi(x: torch.Tensor, ws: Sequence[QWeight], bias: Optional[torch.Te
             out = torch.empty(S, M, Ntot, dtype=torch.float32, device=x.device)
         if kind == "tile":
             _run_tile(x, ws, S, out, Ntot, tile)
+        elif kind == "q32":
+            _run_q32(x, ws, S, out, Ntot, tile)
         elif kind == "ws":
             _run_ws(x, ws, S, out, Ntot)
         elif kind == "dq":
@@ -927,10 +1008,15 @@ def _glu_pair(ws: Sequence[QWeight], F: int):
 
 
 def _run_glu(x: torch.Tensor, pair, F: int, mode: int, tile: int, out: torch.Tensor) -> None:
+    """tile < 100: gemm_q.hip tile id; 100 + v: gemm_q32.hip variant v."""
     M, K = x.shape
     wa, oa, wb, ob = pair
     a0, a1, ag = wa.tile_planes()
     b0, b1, bg = wb.tile_planes()
+    if tile >= 100:
+        _check(lib().la_qgemm32_glu(wa.fmt, a0, a1, ag, oa, b0, b1, bg, ob, F, K, x.data_ptr(), K, M, out.data_ptr(),
+                                    F, mode, tile - 100, _stream()), "la_qgemm32_glu")
+        return
     _check(lib().la_qgemm_glu(wa.fmt, a0, a1, ag, oa, b0, b1, bg, ob, F, K, x.data_ptr(), K, M, out.data_ptr(), F,
                               mode, tile, _stream()), "la_qgemm_glu")
 
@@ -970,7 +1056,10 @@ def glu_linear(x: torch.Tensor, ws: Sequence[QWeight], F: int, mode: int,
         out = torch.empty(M, F, dtype=torch.bfloat16, device=x.device)
         t_ref = _time_cold(lambda: act(linear_multi(x, ws), F, mode))
         best, best_t = None, t_ref
-        for t in ((6, 7, 8) if M > 128 else (7, 12, 14)):
+        cands = [6, 7, 8] if M > 128 else [7, 12, 14]
+        if q32_ok([pair[0]], 9) and pair[0].fmt == pair[2].fmt:
+            cands += [109, 108, 104] if M > 128 else [109, 108, 107]
+        for t in cands:
             tt = _time_cold(lambda t=t: _run_glu(x, pair, F, mode, t, out))
             if tt < best_t:
                 best, best_t = t, tt

@@ -85,7 +85,9 @@ __global__ __launch_bounds__(AR_T) void allreduce_oneshot_kernel(ARArgs a) {
     while (ar_load_flag(f) < ep) {
       __builtin_amdgcn_s_sleep(2);
       if (++spins > a.spin_limit) {
-        __hip_atomic_store((int*)(own + AR_ERR), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        // every rank's error word: the group drops the custom path together whichever rank timed out
+        for (int r = 0; r < a.world; ++r)
+          __hip_atomic_store((int*)(a.bufs[r] + AR_ERR), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
       }
     }
@@ -161,15 +163,16 @@ LA_DEV void ar_signal(uint8_t* const* bufs, int world, int rank, long flags_off,
   }
 }
 
-LA_DEV void ar_wait(uint8_t* own, int world, int rank, long flags_off, long err_off, int b, int ep, int tid,
-                    long spin_limit) {
+LA_DEV void ar_wait(uint8_t* own, uint8_t* const* bufs, int world, int rank, long flags_off, long err_off, int b,
+                    int ep, int tid, long spin_limit) {
   if (tid < world && tid != rank) {
     const int* f = (const int*)(own + flags_off) + b * AR_MAXR + tid;
     long spins = 0;
     while (ar_load_flag(f) < ep) {
       __builtin_amdgcn_s_sleep(2);
       if (++spins > spin_limit) {
-        __hip_atomic_store((int*)(own + err_off), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        for (int r = 0; r < world; ++r)  // every rank's error word (see the one-shot wait)
+          __hip_atomic_store((int*)(bufs[r] + err_off), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
       }
     }
@@ -202,7 +205,7 @@ LA_DEV void ar2_chunk(const ARArgs& a, int b) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   ar_signal(a.bufs, R, a.rank, AR2_F1, b, ep, tid);
-  ar_wait(own, R, a.rank, AR2_F1, AR2_ERR, b, ep, tid, a.spin_limit);
+  ar_wait(own, a.bufs, R, a.rank, AR2_F1, AR2_ERR, b, ep, tid, a.spin_limit);
   // 2. reduce-scatter: this rank's sub-range of the block (multiples of 8 elements)
   const long sub = ((AR_CHUNK / R) + 7) & ~7L;
   const long s0 = min(e1, e0 + (long)a.rank * sub), s1 = min(e1, s0 + sub);
@@ -242,7 +245,7 @@ LA_DEV void ar2_chunk(const ARArgs& a, int b) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   ar_signal(a.bufs, R, a.rank, AR2_F2, b, ep, tid);
-  ar_wait(own, R, a.rank, AR2_F2, AR2_ERR, b, ep, tid, a.spin_limit);
+  ar_wait(own, a.bufs, R, a.rank, AR2_F2, AR2_ERR, b, ep, tid, a.spin_limit);
   // 3. all-gather: every rank's reduced sub-range, from its result slot, into out
   {
     const long bytes = (e1 - e0) * esz, v16 = bytes >> 4;
@@ -261,9 +264,11 @@ LA_DEV void ar2_chunk(const ARArgs& a, int b) {
 }
 
 // Persistent grid of at most AR2_GRID workgroups, each walking chunks g, g + G, ... in order: the
-// waits of chunk c only ever target the peers' workgroup that walks the same chunk sequence, and
-// a grid this small is co-resident with the peers' grids (even with every rank on one GPU), so no
-// wait can depend on a workgroup that is not running.
+// waits of chunk c only ever target the peers' workgroup that walks the same chunk sequence.  The
+// protocol needs every rank's grid resident at once: on separate GPUs a 128-workgroup grid always
+// is; when R ranks SHARE one device (tests, rehearsals) the caller caps the grid at AR2_GRID / R
+// (max_grid) so the R grids -- beside a GEMM on another stream -- still fit the CUs' wave slots,
+// and every wait is bounded by spin_limit (error word set, RCCL from then on) if they do not.
 __global__ __launch_bounds__(AR_T) void allreduce_twoshot_kernel(ARArgs a, int nb) {
   for (int c = blockIdx.x; c < nb; c += gridDim.x) ar2_chunk(a, c);
 }
@@ -276,7 +281,7 @@ extern "C" long la_ar2_max_elems() { return (long)la::AR2_MAXB * la::AR_CHUNK; }
 extern "C" long la_ar2_err_offset() { return la::AR2_ERR; }
 
 extern "C" int la_allreduce_twoshot(const void* in, void* out, long n, int bf16, int rank, int world,
-                                    const void* const* bufs, long spin_limit, void* stream) {
+                                    const void* const* bufs, long spin_limit, void* stream, int max_grid) {
   using namespace la;
   if (world < 1 || world > AR_MAXR || rank < 0 || rank >= world || n < 1) return -1;
   if (n > (long)AR2_MAXB * AR_CHUNK) return -2;
@@ -293,8 +298,9 @@ extern "C" int la_allreduce_twoshot(const void* in, void* out, long n, int bf16,
     a.bufs[r] = (uint8_t*)bufs[r];
   }
   const int nb = (int)((n + AR_CHUNK - 1) / AR_CHUNK);
-  hipLaunchKernelGGL(allreduce_twoshot_kernel, dim3(nb < AR2_GRID ? nb : AR2_GRID), dim3(AR_T), 0,
-                     (hipStream_t)stream, a, nb);
+  const int cap = (max_grid > 0 && max_grid < AR2_GRID) ? max_grid : AR2_GRID;
+  hipLaunchKernelGGL(allreduce_twoshot_kernel, dim3(nb < cap ? nb : cap), dim3(AR_T), 0, (hipStream_t)stream, a,
+                     nb);
   return (int)hipGetLastError();
 }
 extern "C" long la_ar_buffer_bytes() { return la::AR_DATA + 2 * la::AR_SLOT; }

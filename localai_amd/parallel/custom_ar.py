@@ -67,7 +67,7 @@ class CustomAllReduce:
         for f in ("la_allreduce_oneshot", "la_allreduce_twoshot"):
             getattr(self.L, f).argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_long, ctypes.c_int,
                                            ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_long,
-                                           ctypes.c_void_p]
+                                           ctypes.c_void_p] + ([ctypes.c_int] if "twoshot" in f else [])
             getattr(self.L, f).restype = ctypes.c_int
         if twoshot is None:
             twoshot = os.environ.get("LOCALAI_AMD_AR_TWOSHOT", "1") != "0"
@@ -103,6 +103,12 @@ class CustomAllReduce:
             self.own = self.owns[0] if self.owns else None
             handles: List[Optional[list]] = [None] * world
             dist.all_gather_object(handles, hbs, group=group)
+            # ranks sharing this GPU (tests, rehearsals): the two-shot grid is capped so all of
+            # their persistent grids fit on the device at once (allreduce.hip two-shot comment)
+            keys: List[Optional[str]] = [None] * world
+            dist.all_gather_object(keys, self._device_key(), group=group)
+            self.share = max(1, sum(1 for k in keys if k == keys[rank]))
+            self.max_grid2 = max(16, 128 // self.share)
             self.ptr_sets: List[List[int]] = [[] for _ in sizes]
             for r, h_list in enumerate(handles):
                 for k in range(len(sizes)):
@@ -134,6 +140,16 @@ class CustomAllReduce:
         self.ptrs = self.ptr_sets[0]
         self._bufs = [(ctypes.c_void_p * world)(*ps) for ps in self.ptr_sets]
 
+    def _device_key(self) -> str:
+        try:
+            p = torch.cuda.get_device_properties(self.device)
+            u = getattr(p, "uuid", None)
+            if u is not None:
+                return str(u)
+            return f"{os.uname().nodename}:{p.name}:{self.device.index}"
+        except Exception:  # noqa: BLE001
+            return f"{os.uname().nodename}:{self.device}"
+
     @staticmethod
     def _check(rc: int, what: str):
         if rc != 0:
@@ -148,9 +164,9 @@ class CustomAllReduce:
         max_elems (one flag round trip, every rank reads all copies), two-shot beyond (reduce-
         scatter + all-gather: ~2n bytes read per rank instead of world x n)."""
         two = t.numel() > self.max_elems
-        fn = self.L.la_allreduce_twoshot if two else self.L.la_allreduce_oneshot
-        rc = fn(t.data_ptr(), t.data_ptr(), t.numel(), int(t.dtype == torch.bfloat16), self.rank, self.world,
+        args = (t.data_ptr(), t.data_ptr(), t.numel(), int(t.dtype == torch.bfloat16), self.rank, self.world,
                 self._bufs[1 if two else 0], self.SPIN_LIMIT, torch.cuda.current_stream(self.device).cuda_stream)
+        rc = self.L.la_allreduce_twoshot(*args, self.max_grid2) if two else self.L.la_allreduce_oneshot(*args)
         if rc != 0:
             raise RuntimeError(f"la_allreduce_{'twoshot' if two else 'oneshot'} failed with code {rc}")
         return t
@@ -158,6 +174,12 @@ class CustomAllReduce:
     def timed_out(self) -> bool:
         """True if a wait ever hit the spin limit (a peer never arrived): results since are suspect."""
         torch.cuda.synchronize(self.device)
+        return self.error_flag()
+
+    def error_flag(self) -> bool:
+        """This rank's error words, without a device-wide synchronize: read at a point where the
+        stream is already drained (the engine's token readback).  A timed-out wait on ANY rank
+        writes every rank's word (allreduce.hip), so one rank's read speaks for the group."""
         for own, off in zip(self.owns, self.err_offs):
             v = ctypes.c_int(0)
             self._check(self.hip.hipMemcpy(ctypes.byref(v), ctypes.c_void_p(own + off), 4, 2),

@@ -20,6 +20,7 @@ Each replica is any handle with the backend.proto call surface (`grpc.rpc.GRPCBa
 worker processes, `EmbeddedBackend` for in-process engines)."""
 from __future__ import annotations
 
+import contextvars
 import hashlib
 import itertools
 import threading
@@ -27,6 +28,8 @@ from typing import List, Optional, Sequence
 
 from ..grpc import backend_pb as pb
 
+# replica chosen by pick_native() for this task's next streaming call (a remote one)
+_PINNED: contextvars.ContextVar = contextvars.ContextVar("localai_amd_replica_pin", default=None)
 STREAM_RPCS = {r for r, _, _, s in pb.RPCS if s}
 STICKY_RPCS = {"StoresSet", "StoresDelete", "StoresGet", "StoresFind"}
 BROADCAST_RPCS = {"LoadModel", "Free"}
@@ -89,13 +92,39 @@ class ReplicaBackend:
         with self._lock:
             self.inflight[i] = max(0, self.inflight[i] - 1)
 
+    def pick_native(self, request):
+        """Replica choice for the gateway's native SSE fast path (openai_routes._native_stream),
+        which hands tokens to an in-process engine without the RPC surface.  Returns (i, servicer)
+        for an in-process replica -- counted in flight until `_done(i)` -- or (i, None) for a
+        remote one, which is then pinned for this task's next streaming RPC so the generic path
+        sends the request exactly where the balancer chose."""
+        i = self.pick(request)
+        sv = vars(self.replicas[i]).get("servicer")
+        if sv is not None and getattr(sv, "engine", None) is not None:
+            return i, sv
+        with self._lock:
+            self.inflight[i] -= 1
+            self.served[i] -= 1
+        _PINNED.set(i)
+        return i, None
+
+    def _pick_stream(self, request) -> int:
+        i = _PINNED.get()
+        if i is None:
+            return self.pick(request)
+        _PINNED.set(None)
+        with self._lock:
+            self.inflight[i] += 1
+            self.served[i] += 1
+        return i
+
     # ------------------------------------------------------------------ call surface
     def __getattr__(self, rpc):
         if rpc.startswith("_") or rpc not in {r for r, _, _, _ in pb.RPCS}:
             raise AttributeError(rpc)
         if rpc in STREAM_RPCS:
             def call_stream(request, timeout=None):
-                i = self.pick(request)
+                i = self._pick_stream(request)
                 return self._stream(i, rpc, request, timeout)
             return call_stream
         if rpc in BROADCAST_RPCS:

@@ -102,6 +102,10 @@ def main():
         time.sleep(1.5)
     tpi.all_reduce(t)
     torch.cuda.synchronize()
+    dist.barrier()
+    # the timed-out wait wrote EVERY rank's error word (allreduce.hip): no collective needed to
+    # learn about it, so the engine reads only its own word after the step's token readback
+    assert car2.error_flag(), (rank, "error word not set by the peer's timeout")
     raised = False
     try:
         tpi.check_custom_ar(dist.group.WORLD)

@@ -49,3 +49,16 @@ def test_bench_dp_times_tp_http(tmp_path):
     assert out["n_gpus"] == 4
     assert out["config"]["parallelism"] == "dp2xtp2"
     assert out["value"] * out["ms_per_step"] / 1000 == pytest.approx(64, rel=1e-3)
+
+
+def test_bench_gateway_data_parallel(tmp_path):
+    """--dp-mode gateway: ONE gateway (rank 0) fronts both engines (rank 1's over backend.proto
+    gRPC); it drives concurrency x N streams and reports how many each replica served."""
+    out = _bench(tmp_path, "--gpus", "2", "--mode", "http", "--dp-mode", "gateway")
+    assert out["n_gpus"] == 2
+    assert out["config"]["parallelism"] == "dp2-gateway"
+    assert out["config"]["global_batch"] == 8
+    assert out["value"] * out["ms_per_step"] / 1000 == pytest.approx(64, rel=1e-3)
+    served = out["config"]["replica_requests"]
+    # warmup + timed wave of 8 requests each, spread over both replicas
+    assert sum(served) == 16 and min(served) > 0

@@ -11,11 +11,16 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 @pytest.mark.gpu
-def test_custom_allreduce_two_ranks_one_gpu():
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_custom_allreduce_ranks_share_one_gpu(world):
+    """2, 4 and 8 ranks (the 8-GPU node's TP=8 epoch protocol and 7-peer read pattern) sharing the
+    test box's GPU: one-shot and two-shot sums, graph replay, and a late peer's timeout reaching
+    every rank's error word."""
     env = dict(os.environ, LOCALAI_AMD_AR_SAME_GPU="1")
-    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-                        "--master-addr", "127.0.0.1", "--master-port", "29533", os.path.join(ROOT, "scripts", "ar_check.py")],
-                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+                        "--master-addr", "127.0.0.1", "--master-port", str(29533 + world),
+                        os.path.join(ROOT, "scripts", "ar_check.py")],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "AR_OK" in r.stdout, r.stdout[-2000:]
 

@@ -267,6 +267,70 @@ def test_browse_page_escapes_gallery_names(engine, tmp_path_factory):
     with TestClient(app) as c:
         page = c.get("/browse", headers={"accept": "text/html"}).text
     assert "fetch(&#x27;/evil&#x27;)" in page, page[page.find("<main>"):][:600]  # escaped attribute text only
-    assert "install(this)" in page and "install('" not in page
-    assert "onclick=\"install" not in page
+    assert "data-act=install" in page and "install('" not in page
+    assert "onclick=" not in page[page.find("<main>"):page.find("<script>")]
+
+
+def test_browse_gallery_actions_install_and_delete(engine, tmp_path_factory):
+    """The web UI's htmx gallery routes (core/http/routes/ui.go:169-300): search, install from a
+    file:// gallery, progress polling until HX-Trigger: done, the completion fragment, then delete."""
+    import yaml
+    from fastapi.testclient import TestClient
+    from localai_amd.gateway.app import create_app_for_engine
+    models = tmp_path_factory.mktemp("uimodels")
+    gal_dir = models / "gallery"
+    gal_dir.mkdir()
+    (gal_dir / "weights.bin").write_bytes(b"\x00" * 32)
+    cfg = gal_dir / "tiny-ui.yaml"
+    cfg.write_text(yaml.safe_dump({
+        "name": "tiny-ui", "config_file": yaml.safe_dump({"backend": "llama-cpp", "parameters": {"model": "weights.bin"}}),
+        "files": [{"filename": "weights.bin", "uri": f"file://{gal_dir}/weights.bin"}]}))
+    (gal_dir / "index.yaml").write_text(yaml.safe_dump([
+        {"name": "tiny-ui", "url": f"file://{cfg}", "description": "a tiny test model", "tags": ["llm", "test"]},
+        {"name": "other", "url": f"file://{cfg}", "description": "not matched", "tags": ["tts"]}]))
+    ac = _app_config(tmp_path_factory, galleries=[{"name": "local", "url": f"file://{gal_dir / 'index.yaml'}"}])
+    ac.models_path = str(models)
+    app, _ = create_app_for_engine(engine, name="tiny", app_config=ac, models_path=str(models))
+    with TestClient(app) as c:
+        # search: substring of name / description / gallery name / comma-joined tags
+        frag = c.post("/browse/search/models", data={"search": "llm,test"}).text
+        assert "tiny-ui" in frag and "other" not in frag
+        frag = c.post("/browse/search/models", data={"search": "local"}).text
+        assert "tiny-ui" in frag and "other" in frag
+        # install through the UI route, poll the progress fragment until the done trigger
+        frag = c.post("/browse/install/model/local@tiny-ui").text
+        uid = frag.split('data-job="', 1)[1].split('"', 1)[0]
+        assert f"/browse/job/progress/{uid}" in frag and f"/browse/job/{uid}" in frag
+        t0 = time.time()
+        while True:
+            r = c.get(f"/browse/job/progress/{uid}")
+            assert "Error" not in r.text, r.text
+            if r.headers.get("HX-Trigger") == "done":
+                break
+            assert time.time() - t0 < 30, r.text
+            time.sleep(0.05)
+        assert 'aria-valuenow=100' in r.text
+        done = c.get(f"/browse/job/{uid}").text
+        assert "Installation completed" in done and "/browse/delete/model/local@tiny-ui" in done
+        assert (models / "weights.bin").exists() and (models / "tiny-ui.yaml").exists()
+        # the card list now offers delete (installed) instead of install
+        frag = c.post("/browse/search/models", data={"search": "tiny-ui"}).text
+        assert "data-act=delete" in frag
+        # delete through the UI route
+        frag = c.post("/browse/delete/model/local@tiny-ui").text
+        uid = frag.split('data-job="', 1)[1].split('"', 1)[0]
+        t0 = time.time()
+        while c.get(f"/browse/job/progress/{uid}").headers.get("HX-Trigger") != "done":
+            assert time.time() - t0 < 30
+            time.sleep(0.05)
+        assert "Deletion completed" in c.get(f"/browse/job/{uid}").text
+        assert not (models / "tiny-ui.yaml").exists()
+        # an unknown model reports the error fragment (with an install button to retry)
+        frag = c.post("/browse/install/model/local@nope").text
+        uid = frag.split('data-job="', 1)[1].split('"', 1)[0]
+        t0 = time.time()
+        while "Error" not in (txt := c.get(f"/browse/job/progress/{uid}").text):
+            assert time.time() - t0 < 30
+            time.sleep(0.05)
+        assert "data-act=install" in txt
 

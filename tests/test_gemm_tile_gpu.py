@@ -116,7 +116,7 @@ def test_linear_dispatch_llama3_shapes(M):
         assert rel < 1e-2 and cos > 0.9999, (name, rel, cos)
         assert ops._GEMM_CHOICE, "autotune recorded no choice"
         for key, ch in ops._GEMM_CHOICE.items():
-            assert ch[0] == "tile", (key, ch)
+            assert ch[0] in ("tile", "q32"), (key, ch)
 
 
 @pytest.mark.parametrize("tile", [7, 8, 12])
@@ -176,3 +176,88 @@ def test_glu_linear_dispatch():
     xc = x.float().cpu()
     ref = torch.nn.functional.silu(xc @ ws[0].ref.t()) * (xc @ ws[1].ref.t())
     _check(h.float().cpu(), ref, 3e-2)
+
+
+# ---------------------------------------------------------------- gemm_q32.hip (32x32x16 MFMA)
+Q32_VARS = sorted(ops.Q32_TILES)
+
+
+@pytest.mark.parametrize("t", [GGMLType.Q4_K, GGMLType.Q6_K, GGMLType.Q8_0])
+@pytest.mark.parametrize("var", Q32_VARS)
+def test_q32_formats(t, var):
+    """Every variant (tile shape, 4 or 8 waves, schedule) and format vs fp32: N off every tile
+    width, M off every tile height, split-K over odd K-step boundaries, bf16 output."""
+    N, K, M = 200, 1536, 150
+    w = _qw(N, K, t, seed=100 + var)
+    if not ops.q32_ok([w], var):
+        pytest.skip("variant not built for this format")
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    ref = x.float().cpu() @ w.ref.t()
+    for S in (1, 5):
+        out = torch.full((S, M, N), float("nan"), dtype=torch.float32, device=DEV)
+        ops._run_q32(x, [w], S, out, N, var)
+        torch.cuda.synchronize()
+        _check(out.sum(0).cpu(), ref)
+    ob = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=DEV)
+    ops._run_q32(x, [w], 1, ob, N, var)
+    torch.cuda.synchronize()
+    _check(ob.float().cpu(), ref)
+
+
+def test_q32_asymmetric_identity():
+    """A = I with an asymmetric W: the output is W^T exactly as dequantised (swapped fragment
+    maps or a transposed C write would show)."""
+    N, K = 96, 256
+    w = _qw(N, K, GGMLType.Q8_0, seed=3)
+    x = torch.zeros(K, K, dtype=torch.bfloat16, device=DEV)
+    x[torch.arange(K), torch.arange(K)] = 1
+    for var in (0, 8):
+        out = torch.full((1, K, N), float("nan"), dtype=torch.float32, device=DEV)
+        ops._run_q32(x, [w], 1, out, N, var)
+        torch.cuda.synchronize()
+        ref = w.ref.t().to(torch.bfloat16).float()
+        assert (out[0].cpu() - ref).abs().max().item() < 1e-6
+
+
+@pytest.mark.parametrize("var", [0, 1, 3, 4, 8, 9])
+def test_q32_two_segments_one_launch(var):
+    """Q4_K q|k beside a Q6_K v (and the reverse) in one la_qgemm32_2 launch."""
+    K, M = 1536, 200
+    for fa, fb in ((GGMLType.Q4_K, GGMLType.Q6_K), (GGMLType.Q6_K, GGMLType.Q4_K)):
+        ws = [_qw(320, K, fa, seed=11), _qw(96, K, fb, seed=12)]
+        x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+        Ntot = 416
+        for S in (1, 3):
+            out = torch.full((S, M, Ntot), float("nan"), dtype=torch.float32, device=DEV)
+            ops._run_q32(x, ws, S, out, Ntot, var)
+            torch.cuda.synchronize()
+            ref = torch.cat([x.float().cpu() @ w.ref.t() for w in ws], -1)
+            _check(out.sum(0).cpu(), ref)
+
+
+@pytest.mark.parametrize("t", [GGMLType.Q4_K, GGMLType.Q6_K, GGMLType.Q8_0])
+@pytest.mark.parametrize("var", [0, 2, 4, 8, 9])
+def test_q32_glu(t, var):
+    """gate|up with SwiGLU / GeGLU in the q32 epilogue vs fp32 (two weights, and the halves of
+    one fused [2F, K] weight)."""
+    F, K, M = 200, 768, 150
+    g, u = _qw(F, K, t, seed=70 + var), _qw(F, K, t, seed=71 + var)
+    if not ops.q32_ok([g], var):
+        pytest.skip("variant not built for this format")
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    xc = x.float().cpu()
+    for mode in (ops.ACT_SWIGLU, ops.ACT_GEGLU):
+        gr, ur = xc @ g.ref.t(), xc @ u.ref.t()
+        act = (torch.nn.functional.silu(gr) if mode == ops.ACT_SWIGLU
+               else torch.nn.functional.gelu(gr, approximate="tanh"))
+        out = torch.full((M, F), float("nan"), dtype=torch.bfloat16, device=DEV)
+        ops._run_glu(x, (g, 0, u, 0), F, mode, 100 + var, out)
+        torch.cuda.synchronize()
+        _check(out.float().cpu(), act * ur, 3e-2)
+    F2 = 208
+    w = _qw(2 * F2, K, t, seed=80 + var)
+    out = torch.full((M, F2), float("nan"), dtype=torch.bfloat16, device=DEV)
+    ops._run_glu(x, (w, 0, w, F2), F2, ops.ACT_SWIGLU, 100 + var, out)
+    torch.cuda.synchronize()
+    full = xc @ w.ref.t()
+    _check(out.float().cpu(), torch.nn.functional.silu(full[:, :F2]) * full[:, F2:], 3e-2)

@@ -59,6 +59,31 @@ def test_least_busy_dispatch_and_release():
     asyncio.run(run())
 
 
+def test_pick_native_local_and_pinned_remote():
+    """The gateway's native SSE path (openai_routes._native_stream): an in-process replica is
+    returned with its servicer; a remote pick is pinned so the next streaming RPC of the same
+    task lands on it, counted once."""
+    from localai_amd.grpc.rpc import EmbeddedBackend
+
+    class _Sv:
+        engine = object()
+
+    local, remote = EmbeddedBackend(_Sv()), _Fake("r")
+    rb = ReplicaBackend([local, remote], affinity_chars=10_000)
+
+    async def run():
+        i, sv = rb.pick_native(pb.PredictOptions(Prompt="a"))
+        assert i == 0 and isinstance(sv, _Sv) and rb.inflight == [1, 0]
+        j, sv2 = rb.pick_native(pb.PredictOptions(Prompt="b"))  # least busy: the remote
+        assert j == 1 and sv2 is None and rb.inflight == [1, 0] and rb.served == [1, 0]
+        # the local replica is now idle: an unpinned pick would choose it, the pin must win
+        rb._done(0)
+        async for rep in rb.PredictStream(pb.PredictOptions(Prompt="b")):
+            assert rep.message == b"r"
+        assert rb.served == [1, 1] and rb.inflight == [0, 0] and remote.calls == [("PredictStream", "b")]
+    asyncio.run(run())
+
+
 def test_prefix_affinity_and_sticky_stores():
     a, b, c = _Fake("a"), _Fake("b"), _Fake("c")
     rb = ReplicaBackend([a, b, c], affinity_chars=64)

@@ -142,3 +142,39 @@ def test_draft_model_vocab_mismatch_is_a_load_error(tiny_model_path, tmp_path):
     synth.write_model(other, "tiny-llama", exact=True, n_vocab=PRESETS["tiny-llama"].n_vocab - 64)
     with pytest.raises(ValueError, match="vocabulary"):
         _engine(tiny_model_path, draft_model=other)
+
+
+def test_draft_model_catch_up_is_chunked(tiny_model_path):
+    """A long prompt's first draft feeds the whole prompt to the draft model: the catch-up must run
+    in forwards of at most max_batched_tokens tokens (like the main engine's chunked prefill), with
+    several requests drafting at once, and the text stays the main model's greedy text."""
+    import threading
+    prompts = [("long prompt number %d " % i) + "word " * 60 for i in range(3)]
+    sp = SamplingParams(max_tokens=8, temperature=0.0, ignore_eos=True)
+    ref = [_engine(tiny_model_path).generate(p, sp)["text"] for p in prompts]
+    eng = _engine(tiny_model_path, draft_model=tiny_model_path, max_batched_tokens=32)
+    sizes = []
+    fwd = eng.drafter.model.forward
+
+    def spy(fb, *a, **kw):
+        sizes.append(int(fb.tokens.shape[0]))
+        return fwd(fb, *a, **kw)
+
+    eng.drafter.model.forward = spy
+    eng.start()
+    try:
+        outs = [None] * len(prompts)
+
+        def run(j):
+            outs[j] = eng.generate(prompts[j], sp)["text"]
+
+        ths = [threading.Thread(target=run, args=(j,)) for j in range(len(prompts))]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join(120)
+    finally:
+        eng.shutdown()
+    assert outs == ref
+    assert sizes and max(sizes) <= 32, sizes
+    assert sum(1 for s in sizes if s == 32) >= 2  # the prompts really were split

@@ -136,3 +136,80 @@ def test_tp2_chunked_row_parallel(tiny_model_path, monkeypatch):
     monkeypatch.setenv("LOCALAI_AMD_TP_OVERLAP_ROWS", "2")
     monkeypatch.setenv("LOCALAI_AMD_TP_OVERLAP_CHUNKS", "3")
     _run_tp2(tiny_model_path)
+
+
+def _logits_worker(rank, world, port, path, q):
+    """One rank of a TP group: prefill a fixed sequence through the sharded model, then two decode
+    steps; rank 0 reports every row of logits."""
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        q.put((rank, _sequence_logits(path, rank, world)))
+    finally:
+        dist.destroy_process_group()
+
+
+def _sequence_logits(path, rank=0, world=1):
+    import torch
+    import torch.distributed as dist
+    from localai_amd.engine.llm_engine import EngineConfig, LLMEngine
+    from localai_amd.models.decoder import ForwardBatch, TPInfo
+    kw = {}
+    if world > 1:
+        kw = dict(tp=TPInfo(rank=rank, world=world, group=dist.group.WORLD), ctrl_group=dist.new_group(backend="gloo"))
+    eng = LLMEngine(EngineConfig(model_path=path, device="cpu", context_size=128, max_num_seqs=2, use_graphs=False,
+                                 block_size=16), **kw)
+    i32 = lambda a: torch.tensor(a, dtype=torch.int32)  # noqa: E731
+    toks = [17, 923, 41, 5000, 7, 7, 311, 28000, 95, 1024, 3, 64]
+    T = len(toks)
+    bt = i32([list(range(8))])
+    fb = ForwardBatch(tokens=i32(toks), pos=i32(list(range(T))), slots=i32(list(range(T))), decode=False,
+                      block_tables=bt, cu_q=i32([0, T]), ctx_lens=i32([T]))
+    rows = [eng.model.forward(fb, eng.kv).float()]
+    nxt = int(rows[-1][-1].argmax())
+    for step in range(2):
+        p = T + step
+        fb = ForwardBatch(tokens=i32([nxt]), pos=i32([p]), slots=i32([p]), decode=True, block_tables=bt,
+                          seq_lens=i32([p + 1]), max_len=p + 1)
+        rows.append(eng.model.forward(fb, eng.kv).float())
+        nxt = int(rows[-1][-1].argmax())
+    return torch.cat(rows).tolist()
+
+
+def test_tp8_per_token_logits_70b_shaped(tmp_path_factory):
+    """TP=8 on a Llama-3-70B-shaped tiny model (8 kv heads: ONE kv head per rank, 8:1 GQA): every
+    row of logits -- a 12-token prefill and two decode steps -- against the unsharded model
+    (rel <= 1e-2, cosine >= 0.9999), not just the first token."""
+    import torch
+    from localai_amd.models import synth
+    p = tmp_path_factory.mktemp("tp8") / "tiny-70b-shape.gguf"
+    synth.write_model(str(p), "tiny-llama", exact=True, n_embd=512, n_head=16, n_head_kv=8, n_ff=1024)
+    ref = torch.tensor(_sequence_logits(str(p)))
+    world = 8
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_logits_worker, args=(r, world, port, str(p), q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    out, t0 = {}, time.time()
+    while len(out) < world:
+        try:
+            r = q.get(timeout=2)
+            out[r[0]] = r[1]
+        except queue.Empty:
+            assert all(pr.is_alive() or pr.exitcode == 0 for pr in procs), "a TP rank crashed"
+            assert time.time() - t0 < 300
+    for pr in procs:
+        pr.join(60)
+        assert pr.exitcode == 0
+    for r in range(world):
+        got = torch.tensor(out[r])
+        assert got.shape == ref.shape
+        for i in range(ref.shape[0]):
+            rel = float((got[i] - ref[i]).norm() / ref[i].norm())
+            cos = float(torch.nn.functional.cosine_similarity(got[i], ref[i], dim=0))
+            assert rel <= 1e-2 and cos >= 0.9999, (r, i, rel, cos)
