@@ -72,6 +72,10 @@ class EngineConfig:
     blas_tune: bool = True            # tune the hipBLASLt/rocBLAS solution per decode GEMM shape at warm-up
     lora_adapters: tuple = ()         # ((adapter GGUF path, scale), ...) merged into the weights at load
     record_tokens: bool = False       # final Event carries the generated token ids (numerics tests)
+    # ... and the raw model logits row (fp32, on the device) each token was sampled from: the
+    # decode graph copies every step's logits into a [K, B, V] buffer (one extra copy kernel in
+    # the graph; numerics tests only)
+    record_logits: bool = False
     draft_model: str = ""             # speculative decoding: draft LM GGUF (engine/speculative.DraftModel)
     quantization: str = ""            # HF checkpoints: load-time quantisation (bnb_4bit / bnb_8bit / ...)
     draft_max_seqs: int = 16          # draft-model KV cache capacity in sequences of context_size
@@ -91,6 +95,7 @@ class Event:
     completion_tokens: int = 0
     error: str = ""
     token_ids: Optional[List[int]] = None   # final event, with EngineConfig.record_tokens
+    logits: Optional[List[torch.Tensor]] = None  # final event, with EngineConfig.record_logits
 
 
 @dataclass
@@ -115,6 +120,7 @@ class Request:
     spec_accepted: int = 0
     spec_off: bool = False
     out_ids: Optional[List[int]] = None  # generated ids (EngineConfig.record_tokens)
+    out_logits: Optional[list] = None    # their logits rows (EngineConfig.record_logits)
 
 
 def _noop_callback(ev):  # follower ranks: the leader talks to the client
@@ -279,6 +285,7 @@ class LLMEngine:
         r = Request(rid, toks, params, callback, n_prompt=len(toks), mu=2.0 * params.mirostat_tau)
         if self.cfg.record_tokens:
             r.out_ids = []
+            r.out_logits = [] if self.cfg.record_logits else None
         r.stream = core.TextStream(self.vocab, stops)
         if params.grammar:
             r.grammar = core.GrammarState(self._grammar(params.grammar), self.gvocab)
@@ -325,6 +332,10 @@ class LLMEngine:
             if ev.finished:
                 res.update(finish_reason=ev.finish_reason, prompt_tokens=ev.prompt_tokens,
                            completion_tokens=ev.completion_tokens, error=ev.error)
+                if ev.token_ids is not None:
+                    res["token_ids"] = ev.token_ids
+                if ev.logits is not None:
+                    res["logits"] = ev.logits
                 done.set()
 
         self.add_request(prompt, params, cb)
@@ -628,6 +639,7 @@ class LLMEngine:
         r = Request(rid, toks, params, callback, n_prompt=len(toks), mu=2.0 * params.mirostat_tau)
         if self.cfg.record_tokens:
             r.out_ids = []
+            r.out_logits = [] if self.cfg.record_logits else None
         r.stream = core.TextStream(self.vocab, list(params.stop))
         if params.grammar:
             r.grammar = core.GrammarState(self._grammar(params.grammar), self.gvocab)
@@ -727,14 +739,34 @@ class LLMEngine:
         if len(self.requests) >= self.cfg.wide_batch and s.num_waiting == 0:
             K = max(K, self.cfg.decode_steps_wide)
         rem_tok, rem_ctx = 1, K
+        riders = 0
         for r in self.requests.values():
-            if r.n_gen == 0 or self._needs_host_sampler(r) or (r.grammar is not None and not self._grammar_ready(r)):
-                return 1  # prefill in flight, a host-side sampler feature, or a grammar state without a mask
+            if r.n_gen == 0 or self._needs_host_sampler(r):
+                return 1  # prefill in flight, or a host-side sampler feature
+            if r.grammar is not None and not self._grammar_ready(r):
+                if not self._grammar_slot_cached(r):
+                    return 1  # a parse state without a device mask: the host walks it first
+                riders += 1
             n = r.n_prompt + r.n_gen
             rem_ctx = min(rem_ctx, self.ctx - n)
             mt = r.params.max_tokens
             rem_tok = max(rem_tok, (mt - r.n_gen) if mt > 0 else K)
+        if riders:
+            # constrained rows whose transitions are not learned yet ride along a mostly-plain
+            # batch: the plain rows keep a multi-step run, each constrained row takes at least its
+            # first (masked) token per run and parks at its first unknown transition (_grammar_run);
+            # a batch that is mostly constrained stays at one step per round trip
+            if riders > self.GRAMMAR_MIXED_FRAC * len(self.requests):
+                return 1
+            K = min(K, self.GRAMMAR_MIXED_K)
         return max(1, min(K, rem_ctx, rem_tok))
+
+    GRAMMAR_MIXED_K = 8        # device steps per run while unlearned constrained rows ride along
+    GRAMMAR_MIXED_FRAC = 0.125  # ... when they are at most this fraction of the batch
+
+    def _grammar_slot_cached(self, r) -> bool:
+        s = self._gmask_cache.get((r.params.grammar, r.grammar.key()))
+        return s is not None and s >= 0
 
     SPEC_MAX_BATCH = 8   # speculation pays while decode streams weights (small batches)
     SPEC_MAX_DRAFT = 16
@@ -904,7 +936,7 @@ class LLMEngine:
             muh = st["mu"][:B].cpu().numpy()
             for j, r in enumerate(reqs):
                 r.mu = float(muh[j])
-        self._emit_run(reqs, hist, K)
+        self._emit_run(reqs, hist, K, st.get("rec"))
 
     _REASONS = {1: ("stop", True), 2: ("stop", False), 3: ("length", True), 4: ("abort", True)}
 
@@ -950,7 +982,7 @@ class LLMEngine:
                     break
                 s = s2
 
-    def _emit_run(self, reqs: List[Request], hist: np.ndarray, K: int):
+    def _emit_run(self, reqs: List[Request], hist: np.ndarray, K: int, rec: Optional[torch.Tensor] = None):
         """Hand a [K, B] block of device-sampled tokens to the native emitter (detokenise, stop
         strings, EOS / length limits, SSE writes), then update Python-side request state once
         per row."""
@@ -974,6 +1006,8 @@ class LLMEngine:
             self.metrics["gen_tokens"] += n
             if r.out_ids is not None:
                 r.out_ids.extend(int(t) for t in hist[:n, j])
+                if r.out_logits is not None and rec is not None:
+                    r.out_logits.extend(rec[k, j].clone() for k in range(n))
             if texts[j]:
                 r.callback(Event(text=texts[j], token=-1))
             rs = int(reason[j])
@@ -1097,9 +1131,13 @@ class LLMEngine:
         ws = ops.decode_workspace(Bp, self.model.Hq, self.model.Hkv, self.model.Dh, self.ctx, dev,
                                   self.cfg.block_size)
         bs = self.cfg.block_size
+        if self.cfg.record_logits:
+            st["rec"] = torch.zeros(K, Bp, self.model.hp.n_vocab, dtype=torch.float32, device=dev)
 
         def body():
             lg = self.model.forward(fb, self.kv, attn_workspace=ws)
+            if "rec" in st:
+                st["rec"].index_copy_(0, st["step"][:1].long(), lg.float().unsqueeze(0))
             ops.logit_bias(lg, st["bias_rows"], st["bias_cols"], st["bias_vals"], st["bias_n"])
             # repeat / frequency / presence penalties over each row's last-n window, kept on the
             # device across the run's steps (rows without penalties return at once)
@@ -1179,6 +1217,7 @@ class LLMEngine:
 
     # ------------------------------------------------------------------ sampling + output
     def _sample_and_emit(self, seq_ids: List[int], logits: torch.Tensor):
+        raw = logits  # before bias / penalties (EngineConfig.record_logits)
         n = len(seq_ids)
         reqs = [self.requests[i] for i in seq_ids]
         prm = np.zeros(n, dtype=ops.SAMPLE_ROW_DTYPE)
@@ -1241,6 +1280,8 @@ class LLMEngine:
                 r.mu = float(muh[j])
         now = time.perf_counter()
         for j, r in enumerate(reqs):
+            if r.out_logits is not None and not r.done:
+                r.out_logits.append(raw[j].float().clone())
             self._on_token(r, int(toks[j]), now)
 
     GRAMMAR_TOPN = 1024
@@ -1587,7 +1628,8 @@ class LLMEngine:
                       self.last_request_stats["tokens_per_second"])
         try:
             r.callback(Event(text=tail, finished=True, finish_reason=reason, prompt_tokens=r.n_prompt,
-                             completion_tokens=r.n_gen, error=error, token_ids=r.out_ids))
+                             completion_tokens=r.n_gen, error=error, token_ids=r.out_ids,
+                             logits=r.out_logits))
         except Exception:
             log.exception("callback failed")
 

@@ -93,6 +93,10 @@ PRESETS: Dict[str, Preset] = {
                             qtype="Q8_0", name="tiny-llama-q8"),
     "tiny-mixtral": Preset(n_layer=2, n_embd=256, n_head=4, n_head_kv=2, n_ff=512, n_vocab=32256, ctx=512,
                            n_expert=4, n_expert_used=2, qtype="Q4_K", name="tiny-mixtral"),
+    # Mixtral's 32000-entry SentencePiece-style vocabulary on the tiny MoE shapes
+    "tiny-mixtral-spm": Preset(n_layer=2, n_embd=256, n_head=4, n_head_kv=2, n_ff=512, n_vocab=32000, ctx=512,
+                               n_expert=4, n_expert_used=2, qtype="Q4_K", tokenizer="mistral",
+                               name="tiny-mixtral-spm"),
     "tiny-phi2": Preset(arch="phi2", n_layer=2, n_embd=256, n_head=4, n_head_kv=4, n_ff=512, n_vocab=32256,
                         ctx=512, rope_theta=10000.0, rope_dim=32, qtype="Q8_0", tokenizer="phi2", name="tiny-phi2"),
     # Qwen2: q/k/v biases, NEOX rotary, ChatML; Phi-3: fused attn_qkv and gate|up ffn_up, head dim 96;

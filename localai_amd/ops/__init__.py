@@ -39,7 +39,10 @@ def lib():
             return _LIB
         from . import _build
         path = _build.LIB
-        if not path.exists() or os.environ.get("LOCALAI_AMD_REBUILD"):
+        alt = os.environ.get("LOCALAI_AMD_KLIB")  # an A/B build of the same sources (_build.build_variant)
+        if alt:
+            path = _build.HERE / alt
+        elif not path.exists() or os.environ.get("LOCALAI_AMD_REBUILD"):
             _build.build()
         L = ctypes.CDLL(str(path))
         P, I, F, LNG = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_long

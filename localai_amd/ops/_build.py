@@ -47,14 +47,24 @@ def _hipcc() -> str:
 
 
 def build(force: bool = False, verbose: bool = False, jobs: int = 8) -> Path:
-    stamp = HERE / "_la_kernels.stamp"
-    dig = _digest()
+    return _build_lib(LIB, [], force, verbose, jobs)
+
+
+def build_variant(name: str, defines, verbose: bool = False, jobs: int = 8) -> Path:
+    """An A/B build of the same sources with extra -D flags into ops/<name> (selected at run time
+    by LOCALAI_AMD_KLIB=<name>), e.g. build_variant("_la_kernels_wnt.so", ["LA_W_AUX=2"])."""
+    return _build_lib(HERE / name, list(defines), False, verbose, jobs)
+
+
+def _build_lib(LIB: Path, defines, force: bool, verbose: bool, jobs: int) -> Path:
+    stamp = LIB.with_suffix(".stamp")
+    dig = _digest() + ("".join(defines) if defines else "")
     if not force and LIB.exists() and stamp.exists() and stamp.read_text().strip() == dig:
         return LIB
-    objdir = HERE / "build"
+    objdir = HERE / ("build" if not defines else "build_" + LIB.stem)
     objdir.mkdir(exist_ok=True)
     flags = ["-O3", f"--offload-arch={ARCH}", "-fPIC", "-std=c++17", "-Wno-unused-result",
-             "-I", str(CSRC)]
+             "-I", str(CSRC)] + [f"-D{d}" for d in defines]
 
     def compile_one(src: Path) -> Path:
         obj = objdir / (src.stem + ".o")

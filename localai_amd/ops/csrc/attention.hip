@@ -14,6 +14,8 @@
 // * attn_prefill: causal flash attention on MFMA (v_mfma_f32_16x16x32_bf16) for chunks of new
 //   tokens appended to a (possibly prefix-cached) context; K/V tiles of 32 keys come from the
 //   paged cache, so prefix reuse and chunked prefill need no special casing.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace la {
@@ -110,7 +112,11 @@ LA_DEV void rope_src_load(const DecRope& R, int b, int col, float (&v)[N]) {
   }
 }
 
-template <int DH, int GT, int NW>
+// K/V are streamed once per decode step: non-temporal loads (the default) read them 12-14 %
+// faster at batch 256 (5.05 -> 5.70 TB/s at 256 keys, 5.21 -> 5.98 at 384;
+// profiles/r4_attn_decode_nt.md).  VAR bit 0 = ordinary cached loads (A/B only); bit 1 = keys
+// two tiles ahead (measured no faster; kept for the A/B).
+template <int DH, int GT, int NW, int VAR = 0>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) void attn_decode_kernel(
     const bf16* __restrict__ q, const bf16* __restrict__ kc, const bf16* __restrict__ vc,
     const int* __restrict__ block_tables, int max_blocks, const int* __restrict__ seq_lens, int Hkv, int G,
@@ -196,7 +202,12 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
   __syncthreads();
 
   const long head_off = (long)kvh * BS * DH;  // inside a page: [Hkv][BS][Dh] / [Hkv][Dh][BS]
-  auto load_tile = [&](int kb, DecTile<DH>& T) {
+  constexpr bool NTL = !(VAR & 1);
+  auto ld16 = [](const bf16* p) -> bf16x8 {
+    if constexpr (NTL) return __builtin_nontemporal_load((const bf16x8*)p);
+    else return *(const bf16x8*)p;
+  };
+  auto load_k = [&](int kb, bf16x8 (&K)[2][(DH + 31) / 32]) {
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       // K row r of MFMA t: key kb + 8(r>>2) + 4t + (r&3) (clamped to a real key)
@@ -206,17 +217,23 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
 #pragma unroll
       for (int c = 0; c < KC; ++c) {
         const int d = min(32 * c + 8 * g, DH - 8);
-        T.k[t][c] = *(const bf16x8*)(krow + d);
+        K[t][c] = ld16(krow + d);
       }
     }
+  };
+  auto load_v = [&](int kb, bf16x8 (&V)[DH / 16]) {
     // V^T: keys kb + 8g .. +7 at d (an 8-aligned run inside one page, clamped to a real key)
     const int kv = min(kb + 8 * g, kend - 1) & ~7;
     const long pv = (long)sh.bt[(kv - t0) / BS] * Hkv * BS * DH + head_off;
 #pragma unroll
     for (int nd = 0; nd < ND; ++nd) {
       const int d = 16 * nd + r;
-      T.v[nd] = *(const bf16x8*)(vc + pv + ((long)((kv % BS) >> 3) * DH + d) * 8);
+      V[nd] = ld16(vc + pv + ((long)((kv % BS) >> 3) * DH + d) * 8);
     }
+  };
+  auto load_tile = [&](int kb, DecTile<DH>& T) {
+    load_k(kb, T.k);
+    load_v(kb, T.v);
   };
 
   f32x4 o[ND];
@@ -227,13 +244,25 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
   // register double buffer up to Dh 128; a Dh-256 tile (Gemma) is 128 VGPRs on its own, so it
   // is loaded at the top of each iteration instead (no prefetch, no spills)
   constexpr bool DB = DH <= 128;
+  // K2: keys two tiles ahead (V stays one ahead: a whole second tile does not fit in 256 VGPRs)
+  constexpr bool K2 = (VAR & 2) != 0;
   int kb = t0 + 32 * wave;
   if (kb < kend) {
     DecTile<DH> cur, nxt;
-    if constexpr (DB) load_tile(kb, cur);
+    bf16x8 k2[2][(DH + 31) / 32];
+    if constexpr (DB) {
+      load_tile(kb, cur);
+      if constexpr (K2)
+        if (kb + 32 * NW < kend) load_k(kb + 32 * NW, nxt.k);
+    }
     for (; kb < kend; kb += 32 * NW) {
       if constexpr (DB) {
-        if (kb + 32 * NW < kend) load_tile(kb + 32 * NW, nxt);
+        if constexpr (K2) {
+          if (kb + 2 * 32 * NW < kend) load_k(kb + 2 * 32 * NW, k2);
+          if (kb + 32 * NW < kend) load_v(kb + 32 * NW, nxt.v);
+        } else {
+          if (kb + 32 * NW < kend) load_tile(kb + 32 * NW, nxt);
+        }
       } else {
         load_tile(kb, cur);
       }
@@ -285,7 +314,15 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
       }
 #pragma unroll
       for (int nd = 0; nd < ND; ++nd) o[nd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, cur.v[nd], o[nd], 0, 0, 0);
-      if constexpr (DB) cur = nxt;
+      if constexpr (DB) {
+        cur = nxt;
+        if constexpr (K2) {
+#pragma unroll
+          for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int c = 0; c < (DH + 31) / 32; ++c) nxt.k[t][c] = k2[t][c];
+        }
+      }
     }
   }
   // wave totals: lsum over the 4 lane groups (same head r)
@@ -582,10 +619,25 @@ extern "C" int la_attn_decode(const void* q, const void* kc, const void* vc, con
   const float sl2 = scale * 1.4426950408889634f;
   const float cap_l2 = softcap > 0.f ? softcap * 1.4426950408889634f : 0.f;
   const float cap_mul = softcap > 0.f ? scale / softcap : 0.f;
-#define DEC_NW(D, GT, NW)                                                                                         \
-  hipLaunchKernelGGL((la::attn_decode_kernel<D, GT, NW>), grid, dim3(NW * 64), 0, st, (const bf16*)q,           \
+  static const int var = [] {
+    const char* e = getenv("LOCALAI_AMD_ATTN_VAR");
+    return e ? atoi(e) & 3 : 0;
+  }();
+#define DEC_LAUNCH(D, GT, NW, V)                                                                                  \
+  hipLaunchKernelGGL((la::attn_decode_kernel<D, GT, NW, V>), grid, dim3(NW * 64), 0, st, (const bf16*)q,        \
                      (const bf16*)kc, (const bf16*)vc, block_tables, max_blocks, seq_lens, Hkv, G, BS, sl2, PS,  \
                      (bf16*)out, po, pml, P, tk, R, cap_l2, cap_mul, window)
+#define DEC_NW(D, GT, NW)                                                  \
+  do {                                                                     \
+    if constexpr (D == 128 && GT == 4 && NW == 1) {                        \
+      if (var == 1) DEC_LAUNCH(D, GT, NW, 1);                              \
+      else if (var == 2) DEC_LAUNCH(D, GT, NW, 2);                         \
+      else if (var == 3) DEC_LAUNCH(D, GT, NW, 3);                         \
+      else DEC_LAUNCH(D, GT, NW, 0);                                       \
+    } else {                                                               \
+      DEC_LAUNCH(D, GT, NW, 0);                                            \
+    }                                                                      \
+  } while (0)
 #define DEC(D, GT)          \
   do {                      \
     if (nw == 1)            \
@@ -611,6 +663,7 @@ extern "C" int la_attn_decode(const void* q, const void* kc, const void* vc, con
 #undef DEC_G
 #undef DEC
 #undef DEC_NW
+#undef DEC_LAUNCH
   return (int)hipGetLastError();
 }
 

@@ -14,6 +14,12 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
+// cache policy of the quantised-weight LDS-DMA loads in the GEMM kernels (0 = default, 2 = nt);
+// an A/B build flag (-DLA_W_AUX=2)
+#ifndef LA_W_AUX
+#define LA_W_AUX 0
+#endif
+
 namespace la {
 
 constexpr int WAVE = 64;

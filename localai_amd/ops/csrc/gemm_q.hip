@@ -31,6 +31,9 @@ constexpr int GQ_BK = 64;
 LA_DEV void gq_glds16(const void* g, void* l) {
   __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)l, 16, 0, 0);
 }
+LA_DEV void gq_glds16w(const void* g, void* l) {  // quantised weight bytes (streamed once per step)
+  __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)l, 16, 0, LA_W_AUX);
+}
 
 template <int N>
 LA_DEV void gq_vmwait() {
@@ -80,7 +83,7 @@ template <int BN> struct GqScales {
   LA_DEV static void issue(const CM& cm, int KS, int q, int ks, uint8_t* dst, int lane) {
     const int c = 128 * q + 16 * (lane >> 3);  // this lane's 16-column block
     const int b = cm.n(c) >> 4;
-    gq_glds16(cm.template plane<2>(c) + ((size_t)b * KS + ks) * 128 + 16 * (lane & 7), dst + q * 1024);
+    gq_glds16w(cm.template plane<2>(c) + ((size_t)b * KS + ks) * 128 + 16 * (lane & 7), dst + q * 1024);
   }
 };
 
@@ -90,7 +93,7 @@ template <int P, class CM>
 LA_DEV void gq_issue32(const CM& cm, int row_bytes, int p, int kofs, uint8_t* dst, int lane) {
   const int c = 32 * p + (lane >> 1);
   const int lh = (lane & 1) ^ ((c >> 3) & 1);
-  gq_glds16(cm.template plane<P>(c) + (size_t)cm.n(c) * row_bytes + kofs + 16 * lh, dst + p * 1024);
+  gq_glds16w(cm.template plane<P>(c) + (size_t)cm.n(c) * row_bytes + kofs + 16 * lh, dst + p * 1024);
 }
 LA_DEV u32x2 gq_read32(const uint8_t* area, int col, int g) {
   return *(const u32x2*)(area + col * 32 + 16 * ((g >> 1) ^ ((col >> 3) & 1)) + 8 * (g & 1));
@@ -204,7 +207,7 @@ template <int BN> struct GqW<FMT_Q8_0, BN> {
     if (p < PC) {
       const int c = 16 * p + (lane >> 2);
       const int lc = (lane & 3) ^ ((c >> 2) & 3);
-      gq_glds16(cm.template plane<0>(c) + (size_t)cm.n(c) * K + 64 * ks + 16 * lc, wl + p * 1024);
+      gq_glds16w(cm.template plane<0>(c) + (size_t)cm.n(c) * K + 64 * ks + 16 * lc, wl + p * 1024);
     } else {
       GqScales<BN>::issue(cm, K >> 6, p - PC, ks, wl + CODES, lane);
     }
@@ -242,7 +245,7 @@ template <int BN> struct GqW<FMT_BF16, BN> {
   LA_DEV static void issue(const CM& cm, int K, int p, int ks, uint8_t* wl, int lane) {
     const int c = 8 * p + (lane >> 3);
     const int lc = (lane & 7) ^ ((c >> 1) & 7);
-    gq_glds16(cm.template plane<0>(c) + ((size_t)cm.n(c) * K + 64 * ks + 8 * lc) * 2, wl + p * 1024);
+    gq_glds16w(cm.template plane<0>(c) + ((size_t)cm.n(c) * K + 64 * ks + 8 * lc) * 2, wl + p * 1024);
   }
   struct Frag {
     bf16x8 v[2];

@@ -32,6 +32,9 @@ typedef float f32x16_t __attribute__((ext_vector_type(16)));
 LA_DEV void q32_glds16(const void* g, void* l) {
   __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)l, 16, 0, 0);
 }
+LA_DEV void q32_glds16w(const void* g, void* l) {  // quantised weight bytes
+  __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)l, 16, 0, LA_W_AUX);
+}
 LA_DEV void q32_glds4(const void* g, void* l) {
   __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)l, 4, 0, 0);
 }
@@ -77,7 +80,7 @@ template <> struct Q32F<FMT_Q4_K> {
   LA_DEV static void issue(const Q32Cols& cm, int ks, int p, uint8_t* dst, int lane) {
     const int c = 32 * p + (lane >> 1);
     const int lh = (lane & 1) ^ ((c >> 3) & 1);
-    q32_glds16(cm.p0 + (size_t)cm.n(c) * (cm.K >> 1) + 32 * ks + 16 * lh, dst + p * 1024);
+    q32_glds16w(cm.p0 + (size_t)cm.n(c) * (cm.K >> 1) + 32 * ks + 16 * lh, dst + p * 1024);
   }
   static constexpr int PIECES(int WN) { return WN * RAW / 1024; }
   struct St {
@@ -135,7 +138,7 @@ template <> struct Q32F<FMT_Q6_K> {
     const int n = cm.n(c);
     const uint8_t* src = half == 0 ? cm.p0 + (size_t)n * (cm.K >> 1) + 128 * sb + 64 * hh + 32 * part + 16 * lh
                                    : cm.p1 + (size_t)n * (cm.K >> 2) + 64 * sb + 32 * hh + 16 * lh;
-    q32_glds16(src, dst + p * 1024);
+    q32_glds16w(src, dst + p * 1024);
   }
   struct St {
     u32x4 ql, qh;
@@ -190,7 +193,7 @@ template <> struct Q32F<FMT_Q8_0> {
   LA_DEV static void issue(const Q32Cols& cm, int ks, int p, uint8_t* dst, int lane) {
     const int c = 16 * p + (lane >> 2);
     const int lc = (lane & 3) ^ ((c >> 2) & 3);
-    q32_glds16(cm.p0 + (size_t)cm.n(c) * cm.K + 64 * ks + 16 * lc, dst + p * 1024);
+    q32_glds16w(cm.p0 + (size_t)cm.n(c) * cm.K + 64 * ks + 16 * lc, dst + p * 1024);
   }
   struct St {
     u32x4 q0, q1;

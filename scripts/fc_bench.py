@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--max-tokens", type=int, default=64)
     ap.add_argument("--preset", default="llama3-8b")
     ap.add_argument("--waves", type=int, default=2)
+    ap.add_argument("--checks", type=int, default=8, help="non-streaming requests whose tool call is validated")
     a = ap.parse_args()
     from localai_amd.utils.loadgen import LoadGen
     lg = LoadGen(2)  # client processes first: nothing forks after the GPU is initialised
@@ -71,29 +72,51 @@ def main():
         el = time.perf_counter() - t0
         if best is None or tok / el > best[0]:
             best = (tok / el, tok, el)
-    body = json.dumps({"model": name, "max_tokens": a.max_tokens, "messages": [{"role": "user", "content": msgs[0]}],
-                       **extra}).encode()
-    req = urllib.request.Request(url, data=body, headers={"Content-Type": "application/json"})
-    with urllib.request.urlopen(req, timeout=600) as r:
-        doc = json.loads(r.read())
-    msg = doc["choices"][0]["message"]
-    calls = msg.get("tool_calls") or []
-    ok = False
-    if calls:
-        fn = calls[0]["function"]
-        try:
-            args = json.loads(fn["arguments"])
-            ok = fn["name"] == "get_weather" and args.get("unit") in ("celsius", "fahrenheit") and \
-                args.get("days") in ("1", "3", "7") and args.get("location") in ("paris", "tokyo", "lima", "oslo")
-        except (ValueError, TypeError):
-            ok = False
+    # same concurrency and token budget without the grammar, on the same engine (same box)
+    plain = None
+    for w in range(a.waves):
+        t0 = time.perf_counter()
+        _, tok = lg.wave(url, name, [f"[p{w}] " + m for m in msgs], a.max_tokens,
+                         extra={"temperature": 0, "ignore_eos": True})
+        el = time.perf_counter() - t0
+        if plain is None or tok / el > plain:
+            plain = tok / el
+    def check(content):
+        body = json.dumps({"model": name, "max_tokens": a.max_tokens, "messages": [{"role": "user", "content": content}],
+                           **extra}).encode()
+        req = urllib.request.Request(url, data=body, headers={"Content-Type": "application/json"})
+        with urllib.request.urlopen(req, timeout=600) as r:
+            doc = json.loads(r.read())
+        msg = doc["choices"][0]["message"]
+        calls = msg.get("tool_calls") or []
+        ok = False
+        if calls:
+            fn = calls[0]["function"]
+            try:
+                args = json.loads(fn["arguments"])
+                ok = fn["name"] == "get_weather" and args.get("unit") in ("celsius", "fahrenheit") and \
+                    args.get("days") in ("1", "3", "7") and args.get("location") in ("paris", "tokyo", "lima", "oslo")
+            except (ValueError, TypeError):
+                ok = False
+        if not ok:
+            print(f"INVALID tool call for {content!r}: finish={doc['choices'][0]['finish_reason']} "
+                  f"usage={doc.get('usage')} message={json.dumps(msg)[:600]}", file=sys.stderr, flush=True)
+        return ok, doc, msg, calls
+    n_ok = 0
+    for i in range(a.checks):
+        ok, d_, m_, c_ = check(msgs[i % len(msgs)])
+        n_ok += int(ok)
+        if i == 0:
+            ok0, doc, msg, calls = ok, d_, m_, c_
+    ok = ok0
     m = eng.metrics
     print(f"grammar runs {m['grammar_runs']} rows {m['grammar_run_rows']} tokens {m['grammar_run_tokens']} "
           f"hit-rate {[round(v, 3) for v in eng._ghit.values()]}", file=sys.stderr, flush=True)
     print(json.dumps({"metric": "function-calling output tokens/s (forced tool, GBNF-constrained)",
-                      "value": round(best[0], 1), "concurrency": a.concurrency, "max_tokens": a.max_tokens,
+                      "value": round(best[0], 1), "plain_value": round(plain, 1), "preset": a.preset,
+                      "concurrency": a.concurrency, "max_tokens": a.max_tokens,
                       "tokens": best[1], "wall_s": round(best[2], 3), "finish_reason": doc["choices"][0]["finish_reason"],
-                      "tool_call_valid": ok, "sample_call": calls[0]["function"] if calls else msg.get("content")}),
+                      "tool_call_valid": ok, "valid_calls": f"{n_ok}/{a.checks}", "sample_call": calls[0]["function"] if calls else msg.get("content")}),
           flush=True)
     lg.close()
     srv.shutdown()

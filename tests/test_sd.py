@@ -184,6 +184,19 @@ def test_groupnorm_nhwc_kernel_matches_fp32(shape, groups, silu):
 
 
 @pytest.mark.gpu
+def test_unet_on_gpu_matches_fp32_forward(pipe_dir):
+    """Every UNet evaluation of a GPU run (bf16, NHWC, our GroupNorm kernels, graph capture and
+    replays) against the same UNet weights in fp32 PyTorch on the CPU, on the same inputs."""
+    from conftest import compare_to_fp32, record_calls
+    gpu = StableDiffusion(pipe_dir, "cuda:0")
+    calls = record_calls(gpu, "_unet")
+    gpu("a cat", "blurry", 32, 32, steps=3, seed=11)
+    assert gpu._graphs
+    cpu = StableDiffusion(pipe_dir, "cpu")
+    compare_to_fp32(calls, cpu._unet)
+
+
+@pytest.mark.gpu
 def test_unet_graph_replay_matches_eager(pipe_dir):
     p = StableDiffusion(pipe_dir, "cuda:0")
     assert p.use_graphs and p.channels_last

@@ -102,3 +102,15 @@ def test_sd3_on_gpu_graph_matches_eager(sd3_dir):
     p.use_graphs = False
     c = p("graph capture", "", 64, 64, steps=3, seed=4)
     assert float((a.float() - b.float()).abs().max()) <= 3 and float((b.float() - c.float()).abs().max()) <= 3
+
+
+@pytest.mark.gpu
+def test_transformer_on_gpu_matches_fp32_forward(sd3_dir):
+    """Every transformer evaluation of a GPU run (bf16, graph capture and replays) against the
+    same weights in fp32 PyTorch on the CPU, on the same inputs."""
+    from conftest import compare_to_fp32, record_calls
+    p = SD3Pipeline(sd3_dir, "cuda:0")
+    calls = record_calls(p, "_step")
+    p("numerics", "", 64, 64, steps=2, seed=4)
+    cpu = SD3Pipeline(sd3_dir, "cpu")
+    compare_to_fp32(calls, cpu.tr)
