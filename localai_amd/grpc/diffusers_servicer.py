@@ -44,6 +44,17 @@ class DiffusersServicer:
         from ..models.sd import StableDiffusion, is_sd_pipeline
         from ..models.sd3 import SD3Pipeline, is_sd3_pipeline
         path = request.ModelFile or request.Model
+        from ..models import sd_single_file as ssf
+        if ssf.is_single_file(path):
+            # backend.py:184-191: a local file is a from_single_file checkpoint (SD 1.x / 2.x / XL)
+            clip = str(request.CLIPModel or "")
+            if clip and not os.path.isabs(clip):
+                clip = os.path.join(os.path.dirname(os.path.abspath(path)), clip)
+            try:
+                path = await asyncio.get_running_loop().run_in_executor(
+                    None, lambda: ssf.convert(path, tokenizer_dir=clip if os.path.isdir(clip) else None))
+            except Exception as e:  # noqa: BLE001
+                return pb.Result(success=False, message=f"single-file checkpoint: {e}")
         flux = is_flux_pipeline(path) or str(request.PipelineType or "").startswith("Flux")
         sd3 = is_sd3_pipeline(path) or str(request.PipelineType or "") == "StableDiffusion3Pipeline"
         if not (is_sd_pipeline(path) or ((flux or sd3) and os.path.isdir(path))):

@@ -689,7 +689,23 @@ class StableDiffusion:
         self.tok = CLIPTokenizer.from_pretrained(os.path.join(path, "tokenizer"))
         self.tok2 = CLIPTokenizer.from_pretrained(os.path.join(path, "tokenizer_2")) if self.xl else None
         self.max_len = self.text.text_model.embeddings.position_embedding.weight.shape[0]
-        self.latent_ch = self.unet.conv_in.in_channels
+        # latent channels come from the VAE; a depth2img UNet takes one more (the depth map)
+        self.latent_ch = int(vcfg.get("latent_channels", self.unet.conv_in.in_channels))
+        self.extra_ch = self.unet.conv_in.in_channels - self.latent_ch
+        # StableDiffusionDepth2ImgPipeline (backend.py:196-198): a DPT depth estimator and its
+        # image processor beside the UNet; the estimated depth of the source image, resized to the
+        # latent grid and scaled to [-1, 1], is concatenated to every UNet input
+        self.depth = self.depth_fe = None
+        de = os.path.join(path, "depth_estimator")
+        if os.path.isdir(de):
+            import transformers as tf
+            self.depth = tf.DPTForDepthEstimation.from_pretrained(de).to(self.device, self.dtype).eval()
+            fe = os.path.join(path, "feature_extractor")
+            self.depth_fe = (tf.DPTImageProcessor.from_pretrained(fe) if os.path.isdir(fe) else
+                             tf.DPTImageProcessor(size={"height": 384, "width": 384}, keep_aspect_ratio=False))
+        if self.extra_ch != (1 if self.depth is not None else 0):
+            raise ValueError(f"UNet takes {self.unet.conv_in.in_channels} input channels for {self.latent_ch} latent "
+                             "channels: only depth2img (one extra channel, with a depth_estimator) is supported")
         # one hipGraph per (batch, latent size) replays the whole UNet step (~1300 launches)
         self.use_graphs = self.device.type == "cuda" and os.environ.get("LOCALAI_AMD_SD_GRAPH", "1") != "0"
         # bounded LRU: every captured graph owns its activation pool, so a stream of distinct image
@@ -778,6 +794,8 @@ class StableDiffusion:
         xin = torch.cat([x, x]) if cfg else x
         tt = torch.full((xin.shape[0],), float(t), device=self.device)
         xin = xin.to(self.dtype)
+        if self._depth_map is not None:
+            xin = torch.cat([xin, self._depth_map.expand(xin.shape[0], -1, -1, -1)], dim=1)
         if self.channels_last:
             xin = xin.contiguous(memory_format=torch.channels_last)
         out = self._unet(xin, tt, ctx, add, cond).float()
@@ -785,6 +803,21 @@ class StableDiffusion:
             u, c = out.chunk(2)
             out = u + guidance_scale * (c - u)
         return out
+
+    _depth_map = None
+
+    @torch.inference_mode()
+    def _estimate_depth(self, image, w: int, h: int) -> torch.Tensor:
+        """diffusers StableDiffusionDepth2ImgPipeline.prepare_depth_map: DPT depth of the source,
+        bicubic to the latent grid, min/max-scaled to [-1, 1] -> [1, 1, h, w]."""
+        from PIL import Image
+        im = image if isinstance(image, Image.Image) else Image.open(image)
+        px = self.depth_fe(images=im.convert("RGB"), return_tensors="pt").pixel_values.to(self.device, self.dtype)
+        d = self.depth(pixel_values=px).predicted_depth.float()
+        d = F.interpolate(d.unsqueeze(1), size=(h, w), mode="bicubic", align_corners=False)
+        lo, hi = d.amin(dim=[1, 2, 3], keepdim=True), d.amax(dim=[1, 2, 3], keepdim=True)
+        d = 2.0 * (d - lo) / (hi - lo).clamp_min(1e-12) - 1.0
+        return d.to(self.dtype)
 
     def _init_latents(self, image, w: int, h: int, g: torch.Generator) -> torch.Tensor:
         """img2img source -> scaled latents of the requested size."""
@@ -838,6 +871,10 @@ class StableDiffusion:
         if control_image is not None:
             cond = self._control_image(control_image, w * self.vae_scale, h * self.vae_scale, len(prompts))
         steps = max(1, steps)
+        if self.depth is not None:
+            if image is None:
+                raise ValueError("a depth2img pipeline needs a source image (src)")
+            self._depth_map = self._estimate_depth(image, w, h)
         x0 = self._init_latents(image, w, h, g) if image is not None else None
         # img2img: skip the first (1 - strength) of the schedule (diffusers get_timesteps)
         skip = max(steps - min(int(steps * strength), steps), 0) if x0 is not None else 0
@@ -869,6 +906,7 @@ class StableDiffusion:
             for i, t in enumerate(ts):
                 out = self._eps(x, t, ctx, cfg, guidance_scale, add, cond)
                 x = self.sched.step(out, t, ts[i + 1] if i + 1 < len(ts) else None, x)
+        self._depth_map = None
         img = self.vae(x.to(self.dtype)).float()
         img = ((img[0] / 2 + 0.5).clamp(0, 1) * 255).round().to(torch.uint8)
         return img.permute(1, 2, 0).cpu()

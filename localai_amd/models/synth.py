@@ -851,12 +851,15 @@ def _clip_byte_vocab():
     return {t: i for i, t in enumerate(toks)}
 
 
-def write_sd_pipeline(out_dir: str, size: str = "tiny", seed: int = 0, v_prediction: bool = False) -> str:
+def write_sd_pipeline(out_dir: str, size: str = "tiny", seed: int = 0, v_prediction: bool = False,
+                      depth: bool = False) -> str:
     """Random-init Stable Diffusion pipeline directory in the diffusers layout (model_index.json,
     unet/, vae/, text_encoder/ (transformers CLIPTextModel), tokenizer/, scheduler/; SDXL adds
     text_encoder_2/ (CLIPTextModelWithProjection) and tokenizer_2/).
     size="sd15": the SD-1.5 architecture (860M-parameter UNet); "sdxl": SDXL base 1.0;
-    "tiny": a two-level toy; "tiny-xl": a two-level SDXL-shaped toy."""
+    "tiny": a two-level toy; "tiny-xl": a two-level SDXL-shaped toy.
+    depth=True: a StableDiffusionDepth2ImgPipeline (5-channel UNet input, a transformers DPT
+    depth_estimator/ and its feature_extractor/)."""
     import torch
     import transformers as tf
     from safetensors.torch import save_file
@@ -893,6 +896,8 @@ def write_sd_pipeline(out_dir: str, size: str = "tiny", seed: int = 0, v_predict
                   pad_token_id=vocab["<|endoftext|>"])
     if v_prediction:
         uc["use_linear_projection"] = True
+    if depth:
+        uc["in_channels"] = 5
     torch.manual_seed(seed)
     subs = ["unet", "vae", "text_encoder", "tokenizer", "scheduler"] + (["text_encoder_2", "tokenizer_2"] if xl else [])
     for sub in subs:
@@ -925,10 +930,33 @@ def write_sd_pipeline(out_dir: str, size: str = "tiny", seed: int = 0, v_predict
                    "beta_schedule": "scaled_linear", "num_train_timesteps": 1000, "steps_offset": 1,
                    "set_alpha_to_one": False, "clip_sample": False,
                    "prediction_type": "v_prediction" if v_prediction else "epsilon"}, f)
+    if depth:
+        tiny = size.startswith("tiny")
+        dc = tf.DPTConfig(hidden_size=32, num_hidden_layers=4, num_attention_heads=2, intermediate_size=64,
+                          image_size=64, patch_size=16, backbone_out_indices=[0, 1, 2, 3],
+                          neck_hidden_sizes=[8, 16, 32, 32], fusion_hidden_size=16) if tiny else tf.DPTConfig()
+        tf.DPTForDepthEstimation(dc).save_pretrained(os.path.join(out_dir, "depth_estimator"), safe_serialization=True)
+        px = 64 if tiny else 384
+        tf.DPTImageProcessor(size={"height": px, "width": px}, keep_aspect_ratio=False).save_pretrained(
+            os.path.join(out_dir, "feature_extractor"))
     with open(os.path.join(out_dir, "model_index.json"), "w") as f:
         json.dump({"_class_name": "StableDiffusionXLPipeline", "force_zeros_for_empty_prompt": True} if xl
-                  else {"_class_name": "StableDiffusionPipeline"}, f)
+                  else {"_class_name": "StableDiffusionDepth2ImgPipeline" if depth else "StableDiffusionPipeline"}, f)
     return out_dir
+
+
+def write_sd_single_file(path: str, size: str = "tiny", seed: int = 0, fam: str = "", hints: bool = True) -> str:
+    """A random-init Stable Diffusion checkpoint as ONE file in the original LDM / SGM layout
+    (what `from_single_file` reads: the AIO DreamShaper_8_pruned.safetensors shape at
+    size="sd15"); fam: sd1 / sd2 / sdxl (default from size).  The exact configs ride along in
+    the safetensors metadata unless hints=False (then the loader infers them)."""
+    import tempfile
+
+    from .sd_single_file import to_single_file
+    fam = fam or ("sdxl" if size in ("sdxl", "tiny-xl") else "sd1")
+    with tempfile.TemporaryDirectory() as td:
+        d = write_sd_pipeline(os.path.join(td, "p"), size=size, seed=seed, v_prediction=(fam == "sd2"))
+        return to_single_file(d, path, fam, with_hints=hints)
 
 
 def write_controlnet(out_dir: str, pipe_dir: str, seed: int = 0, zero: bool = True) -> str:

@@ -1290,17 +1290,33 @@ def decode_waves(B: int, Hkv: int) -> int:
     return 1 if DEC_NW1_MIN <= B * Hkv <= max(DEC_NW1_MAX, DEC_NW1_MIN) else 4
 
 
+# B * Hkv up to this: short sequences are split over the grid's partitions too (32-key
+# granularity) instead of running as one partition -- a handful of workgroups cannot hide the
+# KV load latency at batch 1 (attn_decode's one_part rule, nw bit 8)
+DEC_SPLIT_SHORT = int(os.environ.get("LOCALAI_AMD_DEC_SPLIT_SHORT", "0"))
+
+
+def _dec_split_short(B: int, Hkv: int) -> bool:
+    return B * Hkv <= DEC_SPLIT_SHORT
+
+
 def decode_partitions(B: int, Hkv: int, max_len: int, block_size: int = 32) -> Tuple[int, int]:
     """Split-KV partitioning for attn_decode: (P, PS).  Enough partitions to put ~16 waves on
-    every CU; each workgroup (decode_waves waves) covers PS keys (multiple of 128, at most 2048
-    pages so the partition's block-table slice fits the kernel's LDS stage)."""
+    every CU; each workgroup (decode_waves waves) covers PS keys (multiple of 128 -- of 32 for
+    the few-sequence split -- at most 2048 pages so the partition's block-table slice fits the
+    kernel's LDS stage)."""
     max_len = max(1, max_len)
     nw = decode_waves(B, Hkv)
-    P = max(1, min(-(-DEC_TARGET_WAVES // (B * Hkv * nw)), -(-max_len // 128), 64))
+    gran = max(32, block_size) if _dec_split_short(B, Hkv) else 128
+    P = max(1, min(-(-DEC_TARGET_WAVES // (B * Hkv * nw)), -(-max_len // gran), 64))
     P = max(P, -(-max_len // (2048 * block_size)))
-    PS = -(-(-(-max_len // P)) // 128) * 128
+    PS = -(-(-(-max_len // P)) // gran) * gran
     P = -(-max_len // PS)
     return P, PS
+
+
+def _dec_nw(B: int, Hkv: int) -> int:
+    return decode_waves(B, Hkv) | (256 if _dec_split_short(B, Hkv) else 0)
 
 
 def decode_workspace(B: int, Hq: int, Hkv: int, Dh: int, max_len: int, device, block_size: int = 32):
@@ -1334,7 +1350,7 @@ def attn_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, b
     _check(lib().la_attn_decode(q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr(),
                                 block_tables.shape[1], seq_lens.data_ptr(), B, Hq, Hkv, Dh, BS, float(scale), P, PS,
                                 out.data_ptr(), po.data_ptr(), pml.data_ptr(), tk.data_ptr(), None, 0, 0, None, None,
-                                None, None, float(softcap), int(window), decode_waves(B, Hkv), _stream()),
+                                None, None, float(softcap), int(window), _dec_nw(B, Hkv), _stream()),
            "la_attn_decode")
     return out
 
@@ -1379,7 +1395,7 @@ def attn_decode_rope(qkv: Partial, pos: torch.Tensor, slots: torch.Tensor, cos_s
                                 block_tables.shape[1], seq_lens.data_ptr(), T, Hq, Hkv, Dh, BS, float(scale), P, PS,
                                 out.data_ptr(), po.data_ptr(), pml.data_ptr(), tk.data_ptr(), a[0], a[1], a[2], a[3],
                                 pos.data_ptr(), slots.data_ptr(), cos_sin.data_ptr(), float(softcap), int(window),
-                                decode_waves(T, Hkv), _stream()),
+                                _dec_nw(T, Hkv), _stream()),
            "la_attn_decode(rope)")
     return out
 

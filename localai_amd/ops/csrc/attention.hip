@@ -122,7 +122,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
     const int* __restrict__ block_tables, int max_blocks, const int* __restrict__ seq_lens, int Hkv, int G,
     int BS, float scale_log2, int PS_grid, bf16* __restrict__ out, float* __restrict__ part_o,
     float* __restrict__ part_ml, int P, int* __restrict__ tickets, DecRope R, float cap_l2, float cap_mul,
-    int window) {
+    int window, int one_part) {
   constexpr int KC = (DH + 31) / 32;  // 32-wide k chunks of the QK^T product
   constexpr int ND = DH / 16;         // 16-wide d tiles of the PV product
   constexpr int NT = NW * 64;
@@ -135,7 +135,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
   // a short sequence takes ONE partition of DEC_ONE_PART keys instead, so it skips the split-KV
   // merge round trip (partials + ticket + last-arriver reduction) -- worth more than the
   // parallelism at a few hundred keys.  Decided per sequence, uniformly for its workgroups.
-  const int PS = (L <= DEC_ONE_PART && PS_grid < DEC_ONE_PART) ? DEC_ONE_PART : PS_grid;
+  const int PS = (L <= one_part && PS_grid < one_part) ? one_part : PS_grid;
   const int t0 = p * PS;
   if (t0 >= L) return;  // empty partition: the combiner only waits for ceil(L / PS) of them
   const int wlo = window > 0 ? L - window : 0;  // first key inside the sliding window
@@ -602,7 +602,11 @@ extern "C" int la_attn_decode(const void* q, const void* kc, const void* vc, con
                               void* out, void* part_o, void* part_ml, void* tickets, const void* rope_p,
                               long rope_slab, int rope_S, const void* rope_bias, const int* pos, const int* slots,
                               const float* cos_sin, float softcap, int window, int nw, void* stream) {
-  if (Hq % Hkv || Hq / Hkv > 16 || (BS % 16) || (128 % BS && BS % 128) || (PS % 128) || P < 1 ||
+  // nw bit 8: split even short sequences over the grid's partitions (few sequences: the
+  // parallelism is worth the merge); otherwise a sequence of <= DEC_ONE_PART keys is one partition
+  const int one_part = (nw & 256) ? 0 : la::DEC_ONE_PART;
+  nw &= 255;
+  if (Hq % Hkv || Hq / Hkv > 16 || (BS % 16) || (128 % BS && BS % 128) || (PS % 32) || (PS % BS) || P < 1 ||
       (nw != 1 && nw != 4) ||
       PS / BS > la::DEC_MAXBT || P > 64 || (P > 1 && !tickets))
     return -1;
@@ -626,7 +630,7 @@ extern "C" int la_attn_decode(const void* q, const void* kc, const void* vc, con
 #define DEC_LAUNCH(D, GT, NW, V)                                                                                  \
   hipLaunchKernelGGL((la::attn_decode_kernel<D, GT, NW, V>), grid, dim3(NW * 64), 0, st, (const bf16*)q,        \
                      (const bf16*)kc, (const bf16*)vc, block_tables, max_blocks, seq_lens, Hkv, G, BS, sl2, PS,  \
-                     (bf16*)out, po, pml, P, tk, R, cap_l2, cap_mul, window)
+                     (bf16*)out, po, pml, P, tk, R, cap_l2, cap_mul, window, one_part)
 #define DEC_NW(D, GT, NW)                                                  \
   do {                                                                     \
     if constexpr (D == 128 && GT == 4 && NW == 1) {                        \

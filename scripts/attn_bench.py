@@ -11,7 +11,7 @@ from localai_amd import ops
 
 dev = torch.device("cuda:0")
 Hq, Hkv, Dh, BS = 32, 8, 128, 32
-cases = [(1, 256), (1, 2000), (64, 512), (128, 384), (256, 256), (256, 384), (512, 300)]
+cases = [(1, 128), (1, 256), (1, 512), (2, 300), (1, 2000), (64, 512), (128, 384), (256, 256), (256, 384), (512, 300)]
 runs = [(B, L, nw1) for B, L in cases for nw1 in ((False, True) if B * Hkv >= 512 else (False,))]
 for B, L, nw1 in runs:
     ops.DEC_NW1_MIN = 1 if nw1 else 1 << 30

@@ -339,3 +339,44 @@ def test_controlnet_on_gpu_graph(pipe_dir, tmp_path):
     p.use_graphs = False
     c = p("a cat", "", 32, 32, steps=3, seed=3, control_image=str(ctrl))
     assert (b.float() - c.float()).abs().max() <= 3
+
+
+def test_depth2img_pipeline(tmp_path):
+    """StableDiffusionDepth2ImgPipeline (backend.py:196-198): the DPT depth of the source image,
+    on the latent grid and scaled to [-1, 1], is the UNet's fifth input channel; the depth map
+    changes the result; no source image is an error; the backend path works."""
+    import asyncio
+
+    from PIL import Image
+
+    from localai_amd.grpc import backend_pb as pb
+    from localai_amd.grpc.diffusers_servicer import DiffusersServicer
+    d = synth.write_sd_pipeline(str(tmp_path / "depth"), depth=True)
+    p = StableDiffusion(d, "cpu")
+    assert p.depth is not None and p.extra_ch == 1 and p.latent_ch == 4
+    src = tmp_path / "src.png"
+    Image.fromarray((torch.rand(32, 32, 3) * 255).to(torch.uint8).numpy()).save(src)
+    dm = p._estimate_depth(str(src), 4, 4)
+    assert dm.shape == (1, 1, 4, 4) and float(dm.min()) == -1.0 and float(dm.max()) == 1.0
+    a = p("a room", "", 32, 32, steps=3, seed=1, image=str(src), strength=0.9)
+    b = p("a room", "", 32, 32, steps=3, seed=1, image=str(src), strength=0.9)
+    assert a.shape == (32, 32, 3) and torch.equal(a, b)
+    # the depth channel matters: zeroing the estimator's output changes the image
+    est = p._estimate_depth
+    p._estimate_depth = lambda *a_: torch.zeros_like(est(*a_))
+    c = p("a room", "", 32, 32, steps=3, seed=1, image=str(src), strength=0.9)
+    assert not torch.equal(a, c)
+    p._estimate_depth = est
+    with pytest.raises(ValueError, match="source image"):
+        p("a room", "", 32, 32, steps=2, seed=1)
+    sv = DiffusersServicer(device="cpu")
+
+    async def go():
+        r = await sv.LoadModel(pb.ModelOptions(ModelFile=d, PipelineType="StableDiffusionDepth2ImgPipeline"), None)
+        assert r.success, r.message
+        dst = str(tmp_path / "o.png")
+        r = await sv.GenerateImage(pb.GenerateImageRequest(positive_prompt="a room", src=str(src), step=2, seed=3,
+                                                           dst=dst), None)
+        assert r.success, r.message
+        assert Image.open(dst).size == (32, 32)
+    asyncio.run(go())
