@@ -121,6 +121,7 @@ class Request:
     spec_off: bool = False
     out_ids: Optional[List[int]] = None  # generated ids (EngineConfig.record_tokens)
     out_logits: Optional[list] = None    # their logits rows (EngineConfig.record_logits)
+    prompt_text: Optional[str] = None    # the prompt as given (GetMetrics' prompt_json_for_slot)
 
 
 def _noop_callback(ev):  # follower ranks: the leader talks to the client
@@ -187,11 +188,14 @@ class LLMEngine:
                 raise ValueError(f"mmproj projects to {self.clip.out_dim}, the LLM embeds {self.hp.n_embd}")
         self.ctx = cfg.context_size
         bs = cfg.block_size
-        if self.device.type == "cuda" and not ops.TILE_GEMM:
+        if self.device.type == "cuda":
             # legacy path (LOCALAI_AMD_TILE_GEMM=0): prefill / big decode batches run hipBLASLt on
             # bf16 copies, materialised before any graph capture.  The default path multiplies the
-            # quantised weights directly (gemm_q.hip) and keeps no copy.
-            self._materialize_bf16()
+            # quantised weights directly (gemm_q.hip) and keeps no copy -- except for formats the
+            # tile GEMM does not read (Q5_K, Q3_K, Q2_K, IQ*, F16, K % 256 != 0): those get a
+            # persistent bf16 copy up front, so a decode batch of 65-256 rows never re-dequantises
+            # them into scratch inside its graph (2 B/weight written + read back every step)
+            self._materialize_bf16(only_non_tile=ops.TILE_GEMM)
         num_blocks = self._num_kv_blocks()
         if faults.hit("kv_alloc"):
             raise faults.InjectedFault("hipMalloc failed for the KV cache (injected fault): out of memory")
@@ -223,18 +227,26 @@ class LLMEngine:
         self.busy = False
 
     # ------------------------------------------------------------------ setup
-    def _materialize_bf16(self):
+    def _materialize_bf16(self, only_non_tile: bool = False):
         m = self.model
+
+        def want(ws) -> bool:
+            return not only_non_tile or not all(w.tile_ok for w in ws)
         for L in m.layers:
-            for w in L.qkv + L.gate_up + [L.wo] + ([L.down] if L.down is not None else []):
-                w.materialize_bf16()
-            ops.fuse_bf16(L.qkv)       # one library GEMM for a mixed-format q|k + v
-            ops.fuse_bf16(L.gate_up)
-            if L.experts:
-                for gu, d in L.experts:
-                    for w in gu + [d]:
+            for grp in (L.qkv, L.gate_up, [L.wo]) + (([L.down],) if L.down is not None else ()):
+                if want(grp):
+                    for w in grp:
                         w.materialize_bf16()
-        m.output.materialize_bf16()
+                    if len(grp) > 1:
+                        ops.fuse_bf16(grp)   # one library GEMM for a mixed-format q|k + v
+            if L.experts and not only_non_tile:   # (the grouped MoE kernels read their own planes)
+                for gu, d in L.experts:
+                    for grp in (gu, [d]):
+                        if want(grp):
+                            for w in grp:
+                                w.materialize_bf16()
+        if want([m.output]):
+            m.output.materialize_bf16()
         torch.cuda.synchronize(self.device)
 
     def _num_kv_blocks(self) -> int:
@@ -283,6 +295,7 @@ class LLMEngine:
         params.resolved_seed()
         stops = list(params.stop)
         r = Request(rid, toks, params, callback, n_prompt=len(toks), mu=2.0 * params.mirostat_tau)
+        r.prompt_text = prompt if isinstance(prompt, str) else None
         if self.cfg.record_tokens:
             r.out_ids = []
             r.out_logits = [] if self.cfg.record_logits else None
@@ -433,7 +446,8 @@ class LLMEngine:
             return None
         gen_s = (now - best.first_token_t) if best.first_token_t else 0.0
         return {"id": best.id, "prompt_tokens": best.n_prompt or len(best.prompt), "completion_tokens": best.n_gen,
-                "tokens_per_second": (best.n_gen / gen_s) if gen_s > 0 else 0.0, "prompt": list(best.prompt)}
+                "tokens_per_second": (best.n_gen / gen_s) if gen_s > 0 else 0.0,
+                "prompt": best.prompt_text if best.prompt_text is not None else self.tokenizer.decode(best.prompt)}
 
     def has_work(self) -> bool:
         return bool(self.requests) or not self._inbox.empty()
@@ -761,7 +775,7 @@ class LLMEngine:
             K = min(K, self.GRAMMAR_MIXED_K)
         return max(1, min(K, rem_ctx, rem_tok))
 
-    GRAMMAR_MIXED_K = 8        # device steps per run while unlearned constrained rows ride along
+    GRAMMAR_MIXED_K = 4        # device steps per run while unlearned constrained rows ride along
     GRAMMAR_MIXED_FRAC = 0.125  # ... when they are at most this fraction of the batch
 
     def _grammar_slot_cached(self, r) -> bool:
@@ -886,7 +900,9 @@ class LLMEngine:
                     sl = self._grammar_mask_slot(r, V, self.device)
                     if sl is not None and sl >= 0:
                         gslot[j] = sl
-                        if self.cfg.grammar_run_ahead:
+                        if self.cfg.grammar_run_ahead or K > 1:
+                            # run-ahead, or a rider in a mostly-plain multi-step run: learn the
+                            # state's transitions at once so the row does not park after one token
                             self._gexpand(r.params.grammar, r.grammar, sl, V)
                     elif sl is not None:
                         done_rows.append(j)
@@ -1449,8 +1465,7 @@ class LLMEngine:
             slot = self._gmask_free.pop()
             n = min(len(m), V)
             pool[slot, :n].copy_(torch.from_numpy(m[:n].astype(bool)))
-            if self.cfg.grammar_run_ahead:
-                self._gmask_np[slot] = m
+            self._gmask_np[slot] = m   # host copy: transitions out of the state can be expanded
         c[key] = slot
         while len(c) > 4 * self.GRAMMAR_MASK_SLOTS:
             _, v = c.popitem(last=False)

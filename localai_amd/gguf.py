@@ -410,6 +410,43 @@ def quantize_q4_k(x: np.ndarray) -> np.ndarray:
     return out.reshape(-1)
 
 
+def quantize_q5_k(x: np.ndarray) -> np.ndarray:
+    """Asymmetric min/max quantiser producing valid ggml Q5_K blocks (d, dmin, the Q4_K 6-bit
+    scale/min packing, qh[32] high bits -- bit 2c of byte l for sub-block 2c, bit 2c+1 for 2c+1 --
+    and qs[128] low nibbles)."""
+    x = np.asarray(x, dtype=np.float32).reshape(-1, 8, 32)
+    nb = x.shape[0]
+    mn = np.minimum(x.min(axis=2), 0.0)
+    scale = (x.max(axis=2) - mn) / 31.0
+    mins = -mn
+    d = np.where(scale.max(axis=1) > 0, scale.max(axis=1) / 63.0, 0.0).astype(np.float32)
+    dmin = np.where(mins.max(axis=1) > 0, mins.max(axis=1) / 63.0, 0.0).astype(np.float32)
+    d16 = _f16(d).astype(np.float32)
+    dm16 = _f16(dmin).astype(np.float32)
+    inv_d = np.where(d16 > 0, 1.0 / np.where(d16 > 0, d16, 1), 0.0)
+    inv_m = np.where(dm16 > 0, 1.0 / np.where(dm16 > 0, dm16, 1), 0.0)
+    ls = np.clip(np.rint(scale * inv_d[:, None]), 0, 63).astype(np.uint8)
+    lm = np.clip(np.rint(mins * inv_m[:, None]), 0, 63).astype(np.uint8)
+    eff_d = d16[:, None] * ls.astype(np.float32)
+    eff_m = dm16[:, None] * lm.astype(np.float32)
+    inv_eff = np.where(eff_d > 0, 1.0 / np.where(eff_d > 0, eff_d, 1), 0.0)
+    L = np.clip(np.rint((x + eff_m[:, :, None]) * inv_eff[:, :, None]), 0, 31).astype(np.uint8).reshape(nb, 256)
+    out = np.zeros((nb, 176), dtype=np.uint8)
+    out[:, 0:2] = d16.astype(np.float16).view(np.uint8).reshape(-1, 2)
+    out[:, 2:4] = dm16.astype(np.float16).view(np.uint8).reshape(-1, 2)
+    out[:, 4:16] = _pack_q4k_scales(ls, lm)
+    qh = np.zeros((nb, 32), dtype=np.uint8)
+    qs = np.zeros((nb, 128), dtype=np.uint8)
+    for c in range(4):
+        lo = L[:, 64 * c: 64 * c + 32]
+        hi = L[:, 64 * c + 32: 64 * c + 64]
+        qs[:, 32 * c: 32 * c + 32] = (lo & 0xF) | ((hi & 0xF) << 4)
+        qh |= ((lo >> 4) << (2 * c)) | ((hi >> 4) << (2 * c + 1))
+    out[:, 16:48] = qh
+    out[:, 48:] = qs
+    return out.reshape(-1)
+
+
 def quantize_q6_k(x: np.ndarray) -> np.ndarray:
     x = np.asarray(x, dtype=np.float32).reshape(-1, 16, 16)
     nb = x.shape[0]
@@ -455,6 +492,8 @@ def quantize(x: np.ndarray, t: int) -> np.ndarray:
         return quantize_q4_k(x)
     if t == GGMLType.Q6_K:
         return quantize_q6_k(x)
+    if t == GGMLType.Q5_K:
+        return quantize_q5_k(x)
     raise NotImplementedError(f"quantize to {GGMLType(t).name}")
 
 
@@ -619,6 +658,19 @@ def random_q4_k_blocks(rng: np.random.Generator, n_blocks: int, std: float) -> n
     out[:, 2:4] = _f16(d * 8.0).view(np.uint8).reshape(-1, 2)
     out[:, 4:16] = _pack_q4k_scales(sc, mn)
     out[:, 16:] = rng.integers(0, 256, size=(n_blocks, 128), dtype=np.uint8)
+    return out.reshape(-1)
+
+
+def random_q5_k_blocks(rng: np.random.Generator, n_blocks: int, std: float) -> np.ndarray:
+    """Random valid Q5_K blocks (5-bit codes uniform in 0..31), ~zero mean, the requested std."""
+    out = np.empty((n_blocks, 176), dtype=np.uint8)
+    sc = rng.integers(32, 64, size=(n_blocks, 8), dtype=np.uint8)
+    mn = np.clip(np.rint(sc.astype(np.float32) * 15.5 / 16.0), 0, 63).astype(np.uint8)
+    d = np.full(n_blocks, std / (47.5 * 9.23), dtype=np.float32)
+    out[:, 0:2] = _f16(d).view(np.uint8).reshape(-1, 2)
+    out[:, 2:4] = _f16(d * 16.0).view(np.uint8).reshape(-1, 2)
+    out[:, 4:16] = _pack_q4k_scales(sc, mn)
+    out[:, 16:] = rng.integers(0, 256, size=(n_blocks, 160), dtype=np.uint8)
     return out.reshape(-1)
 
 

@@ -358,6 +358,7 @@ class EngineServicer:
             r.tokens_per_second = float(s["tokens_per_second"])
             r.tokens_generated = int(s["completion_tokens"])
             r.prompt_tokens_processed = int(s["prompt_tokens"])
+            # the slot's prompt as a JSON string (grpc-server.cpp:2441: slot->prompt.dump())
             r.prompt_json_for_slot = json.dumps(s["prompt"])
         return r
 

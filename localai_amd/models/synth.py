@@ -22,8 +22,8 @@ from typing import Dict, List, Optional, Sequence
 
 import numpy as np
 
-from ..gguf import (GGMLType, GGUFValueType, GGUFWriter, quantize, random_q4_k_blocks, random_q6_k_blocks,
-                    random_q8_0_blocks)
+from ..gguf import (GGMLType, GGUFValueType, GGUFWriter, quantize, random_q4_k_blocks, random_q5_k_blocks,
+                    random_q6_k_blocks, random_q8_0_blocks)
 
 ASSETS = Path(__file__).resolve().parent.parent / "assets"
 
@@ -50,7 +50,7 @@ class Preset:
     n_expert_used: int = 0
     rope_dim: Optional[int] = None
     head_dim: Optional[int] = None   # default n_embd // n_head (Gemma: 256 with q_dim != n_embd)
-    qtype: str = "Q4_K_M"            # Q4_K_M | Q4_K | Q8_0 | F16 | F32
+    qtype: str = "Q4_K_M"            # Q4_K_M | Q5_K_M | Q4_K | Q8_0 | F16 | F32
     tokenizer: str = "llama3"        # llama3 | mistral | phi2 | chatml
     tied: bool = False               # no output.weight: the lm_head is token_embd (Gemma, small Qwen2)
     attn_softcap: float = 0.0        # Gemma-2 keys
@@ -74,6 +74,7 @@ class Preset:
 PRESETS: Dict[str, Preset] = {
     "llama3-8b": Preset(name="Meta-Llama-3-8B-Instruct (random-init)"),
     "llama3-8b-q8_0": Preset(qtype="Q8_0", name="Meta-Llama-3-8B-Instruct Q8_0 (random-init)"),
+    "llama3-8b-q5_k_m": Preset(qtype="Q5_K_M", name="Meta-Llama-3-8B-Instruct Q5_K_M (random-init)"),
     # the Llama-3-8B layer shapes (4096 wide, GQA 32/8, 14336 FFN, Q4_K_M mixed Q4_K/Q6_K, 128256 vocab)
     # on 2 layers: the headline decode path at a size the fp32 oracle can check (tests/test_engine_gpu.py)
     "llama3-8b-2l": Preset(n_layer=2, ctx=1024, name="Llama-3-8B shapes, 2 layers (random-init)"),
@@ -89,6 +90,8 @@ PRESETS: Dict[str, Preset] = {
     # small shapes for tests (CPU reference runs) -- K dims multiples of 256 so every kernel path is used
     "tiny-llama": Preset(n_layer=2, n_embd=256, n_head=4, n_head_kv=2, n_ff=512, n_vocab=32256, ctx=512,
                          qtype="Q4_K", name="tiny-llama"),
+    "tiny-llama-q5km": Preset(n_layer=2, n_embd=256, n_head=4, n_head_kv=2, n_ff=512, n_vocab=32256, ctx=512,
+                              qtype="Q5_K_M", name="tiny-llama-q5km"),
     "tiny-llama-q8": Preset(n_layer=2, n_embd=256, n_head=4, n_head_kv=2, n_ff=512, n_vocab=32256, ctx=512,
                             qtype="Q8_0", name="tiny-llama-q8"),
     "tiny-mixtral": Preset(n_layer=2, n_embd=256, n_head=4, n_head_kv=2, n_ff=512, n_vocab=32256, ctx=512,
@@ -234,14 +237,15 @@ def _tensor_types(p: Preset, name: str, layer: int) -> int:
         return GGMLType.Q8_0
     if q == "Q4_K":
         return GGMLType.Q6_K if name == "output.weight" else GGMLType.Q4_K
-    # Q4_K_M
+    # Q4_K_M / Q5_K_M (llama.cpp's mixes: Q6_K output, and Q6_K attn_v / ffn_down on the
+    # use_more_bits layers)
     if name == "output.weight":
         return GGMLType.Q6_K
     if name.endswith("attn_v.weight") and _more_bits(layer, p.n_layer):
         return GGMLType.Q6_K
     if (name.endswith("ffn_down.weight") or name.endswith("ffn_down_exps.weight")) and _more_bits(layer, p.n_layer):
         return GGMLType.Q6_K
-    return GGMLType.Q4_K
+    return GGMLType.Q5_K if q == "Q5_K_M" else GGMLType.Q4_K
 
 
 def tensor_list(p: Preset):
@@ -332,7 +336,7 @@ def write_model(path: str, preset: str | Preset, seed: int = 0, exact: bool = Fa
     a = p.arch
     hd = p.hd
     w.add_string("general.name", p.name)
-    w.add_uint32("general.file_type", 15 if p.qtype == "Q4_K_M" else 7)
+    w.add_uint32("general.file_type", {"Q4_K_M": 15, "Q5_K_M": 17}.get(p.qtype, 7))
     w.add_uint32(f"{a}.context_length", p.ctx)
     w.add_uint32(f"{a}.embedding_length", p.n_embd)
     w.add_uint32(f"{a}.block_count", p.n_layer)
@@ -415,6 +419,8 @@ def write_model(path: str, preset: str | Preset, seed: int = 0, exact: bool = Fa
                 return random_q4_k_blocks(rng, n // 256, sd)
             if t == GGMLType.Q6_K:
                 return random_q6_k_blocks(rng, n // 256, sd)
+            if t == GGMLType.Q5_K:
+                return random_q5_k_blocks(rng, n // 256, sd)
             if t == GGMLType.Q8_0:
                 return random_q8_0_blocks(rng, n // 32, sd)
             raise NotImplementedError(t)

@@ -20,6 +20,11 @@ typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 #define LA_W_AUX 0
 #endif
 
+// s_setprio(1) around the GEMM kernels' MFMA clusters (an A/B build flag, -DLA_SETPRIO=1)
+#ifndef LA_SETPRIO
+#define LA_SETPRIO 0
+#endif
+
 namespace la {
 
 constexpr int WAVE = 64;

@@ -371,6 +371,7 @@ LA_DEV void gq_tile(uint8_t* __restrict__ lds, const QW& w, int tile, const bf16
           b[nt] = WS::template deq<1>(f[nt]);
         }
       }
+      if constexpr (LA_SETPRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
 #pragma unroll
@@ -382,6 +383,7 @@ LA_DEV void gq_tile(uint8_t* __restrict__ lds, const QW& w, int tile, const bf16
           }
         }
       }
+      if constexpr (LA_SETPRIO) __builtin_amdgcn_s_setprio(0);
     }
   };
 
@@ -449,6 +451,7 @@ LA_DEV void gq_tile(uint8_t* __restrict__ lds, const QW& w, int tile, const bf16
             else b[nt] = WS::template deq<1>(f[nt]);
           }
         }
+        if constexpr (LA_SETPRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int j = 0; j < MG; ++j)
 #pragma unroll
@@ -456,6 +459,7 @@ LA_DEV void gq_tile(uint8_t* __restrict__ lds, const QW& w, int tile, const bf16
             if constexpr (ABL & 1) acc[grp * MG + j][nt][0] += (float)a[j][nt & 7] * (float)b[nt][j & 7];
             else acc[grp * MG + j][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[j], b[nt], acc[grp * MG + j][nt], 0, 0, 0);
           }
+        if constexpr (LA_SETPRIO) __builtin_amdgcn_s_setprio(0);
 #pragma unroll
         for (int j = 0; j < MG; ++j) a[j] = an[j];
       }

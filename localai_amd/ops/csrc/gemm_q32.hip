@@ -357,6 +357,7 @@ LA_DEV void q32_tile(uint8_t* __restrict__ lds, const QW& w, int tile, const bf1
     for (int cb = 0; cb < CB; ++cb) F::load(rw, sw, cb * 32 + r32, h, ks0 + t, dst[cb]);
   };
   auto mm = [&](const bf16x8 (&a)[MB], const bf16x8 (&b)[CB]) {
+    if constexpr (LA_SETPRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
@@ -364,6 +365,7 @@ LA_DEV void q32_tile(uint8_t* __restrict__ lds, const QW& w, int tile, const bf1
         if constexpr (ABL & 1) asm volatile("; probe: no MFMA" ::"v"(a[mb]), "v"(b[cb]));
         else acc[mb][cb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mb], b[cb], acc[mb][cb], 0, 0, 0);
       }
+    if constexpr (LA_SETPRIO) __builtin_amdgcn_s_setprio(0);
   };
   auto deqs = [&](bf16x8 (&b)[CB], const typename F::St (&st)[CB], auto S_) {
     constexpr int S = decltype(S_)::value;

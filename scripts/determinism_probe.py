@@ -18,7 +18,10 @@ from localai_amd.models.sd import StableDiffusion  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--size", default="tiny-xl")
+    ap.add_argument("--deterministic", action="store_true", help="torch.backends.cudnn.deterministic (MIOpen)")
     a = ap.parse_args()
+    if a.deterministic:
+        torch.backends.cudnn.deterministic = True
     d = synth.write_sd_pipeline(os.path.join(tempfile.mkdtemp(), "p"), size=a.size)
     p = StableDiffusion(d, "cuda:0")
     p.use_graphs = False
@@ -46,6 +49,18 @@ def main():
         torch.cuda.synchronize()
         outs.append((y.clone(), list(rec)))
     (y0, r0), (y1, r1) = outs
+    import time
+    for h in hooks:
+        h.remove()
+    with torch.inference_mode():
+        for _ in range(3):
+            orig(*ins)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(20):
+            orig(*ins)
+        torch.cuda.synchronize()
+    print(f"UNet eager forward {(time.perf_counter() - t0) / 20 * 1e3:.2f} ms (deterministic={a.deterministic})")
     print(f"UNet output equal: {torch.equal(y0, y1)}  max diff {float((y0.float() - y1.float()).abs().max()):.3e}")
     for (n0, t0), (n1, t1) in zip(r0, r1):
         if t0 is None or t1 is None:

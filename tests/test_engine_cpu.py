@@ -391,10 +391,17 @@ def test_get_metrics_reports_the_active_slot(eng):
     assert m.slot_id == rid
     assert 0 < m.tokens_generated <= 6
     assert m.prompt_tokens_processed == len(ids)
-    assert _json.loads(m.prompt_json_for_slot) == list(ids)
+    # the prompt as a JSON string (grpc-server.cpp:2441 slot->prompt.dump()); ids are detokenised
+    assert _json.loads(m.prompt_json_for_slot) == eng.tokenizer.decode(ids)
     while eng.has_work():
         eng.step()
     assert asyncio.run(sv.GetMetrics(pb.MetricsRequest())).slot_id == 0
+    eng.add_request("metrics text probe", SamplingParams(max_tokens=4, temperature=0.0, ignore_eos=True),
+                    lambda ev: None)
+    eng.step()
+    assert _json.loads(asyncio.run(sv.GetMetrics(pb.MetricsRequest())).prompt_json_for_slot) == "metrics text probe"
+    while eng.has_work():
+        eng.step()
 
 
 def test_penalties_keep_device_sampling_within_the_ring(tiny_model_path):
