@@ -76,6 +76,12 @@ class EngineConfig:
     # decode graph copies every step's logits into a [K, B, V] buffer (one extra copy kernel in
     # the graph; numerics tests only)
     record_logits: bool = False
+    # burst admission: an idle engine that receives work waits until arrivals pause for
+    # admission_quiet_ms (at most admission_window_ms) before its first prefill, so a burst of
+    # concurrent requests is prefilled in full chunks instead of the first arrival alone while the
+    # gateway thread is still parsing the rest (it holds the GIL meanwhile); 0 disables
+    admission_window_ms: float = 30.0
+    admission_quiet_ms: float = 2.0
     draft_model: str = ""             # speculative decoding: draft LM GGUF (engine/speculative.DraftModel)
     quantization: str = ""            # HF checkpoints: load-time quantisation (bnb_4bit / bnb_8bit / ...)
     draft_max_seqs: int = 16          # draft-model KV cache capacity in sequences of context_size
@@ -220,6 +226,7 @@ class LLMEngine:
         self.tracer = get_tracer()
         self._pcache = PromptCacheFiles()
         self._graph_pool = None
+        self.k1_reasons = collections.Counter()
         self.metrics = {"prompt_tokens": 0, "gen_tokens": 0, "steps": 0, "prefill_s": 0.0, "decode_s": 0.0,
                         "requests": 0, "spec_steps": 0, "spec_drafted": 0, "spec_accepted": 0,
                         "grammar_runs": 0, "grammar_run_rows": 0, "grammar_run_tokens": 0}
@@ -361,6 +368,12 @@ class LLMEngine:
         return res
 
     def start(self):
+        # the serving thread shares the GIL with the gateway's event loop: a shorter switch
+        # interval (default 5 ms) keeps its launch loop moving while a request burst is parsed
+        sw = float(os.environ.get("LOCALAI_AMD_GIL_SWITCH_MS", "1"))
+        if sw > 0:
+            import sys
+            sys.setswitchinterval(min(sys.getswitchinterval(), sw / 1e3))
         if self._thread is None:
             self._stop = False
             self._thread = threading.Thread(target=self._loop, name="llm-engine", daemon=True)
@@ -408,6 +421,20 @@ class LLMEngine:
             if not worked:
                 self._wake.wait(0.05)
                 self._wake.clear()
+                if self.cfg.admission_window_ms > 0 and not self.requests and not self._inbox.empty():
+                    self._admit_burst()
+
+    def _admit_burst(self):
+        """Idle -> busy: let a burst of arrivals land before scheduling (see EngineConfig)."""
+        t_end = time.perf_counter() + self.cfg.admission_window_ms / 1e3
+        quiet = self.cfg.admission_quiet_ms / 1e3
+        n = self._inbox.qsize()
+        while time.perf_counter() < t_end:
+            time.sleep(quiet)
+            m = self._inbox.qsize()
+            if m == n:
+                return
+            n = m
 
     @staticmethod
     def _is_fatal(e: Exception) -> bool:
@@ -742,13 +769,17 @@ class LLMEngine:
         return ((pen and window > self.PEN_CAP) or p.mirostat == 1
                 or len(p.logit_bias) + len(self.tokenizer.eog) > self.cfg.bias_capacity)
 
+    k1_reasons: "collections.Counter"   # why a decode step ran one device step (diagnostics)
+
     def _lookahead(self) -> int:
         """Decode steps to run on the device before coming back to the host."""
         K = self.cfg.decode_steps
         if K <= 1 or not (self.cfg.use_graphs and self.device.type == "cuda"):
             return 1
         s = self.sched
+        why = self.k1_reasons
         if s.num_waiting > 0 and s.num_running < self.cfg.max_num_seqs:
+            why["admit"] += 1
             return 1  # admit new prompts promptly
         if len(self.requests) >= self.cfg.wide_batch and s.num_waiting == 0:
             K = max(K, self.cfg.decode_steps_wide)
@@ -756,9 +787,11 @@ class LLMEngine:
         riders = 0
         for r in self.requests.values():
             if r.n_gen == 0 or self._needs_host_sampler(r):
+                why["prefill" if r.n_gen == 0 else "host_sampler"] += 1
                 return 1  # prefill in flight, or a host-side sampler feature
             if r.grammar is not None and not self._grammar_ready(r):
                 if not self._grammar_slot_cached(r):
+                    why["grammar_no_mask"] += 1
                     return 1  # a parse state without a device mask: the host walks it first
                 riders += 1
             n = r.n_prompt + r.n_gen
@@ -771,6 +804,7 @@ class LLMEngine:
             # first (masked) token per run and parks at its first unknown transition (_grammar_run);
             # a batch that is mostly constrained stays at one step per round trip
             if riders > self.GRAMMAR_MIXED_FRAC * len(self.requests):
+                why["grammar_majority"] += 1
                 return 1
             K = min(K, self.GRAMMAR_MIXED_K)
         return max(1, min(K, rem_ctx, rem_tok))
@@ -907,6 +941,7 @@ class LLMEngine:
                     elif sl is not None:
                         done_rows.append(j)
             if K > 1 and (done_rows or any(gslot[j] < 0 for j in grows) or epoch0 != self._gepoch):
+                self.k1_reasons["grammar_demoted"] += 1
                 K = 1  # a constrained row without a device mask (or a slot reused meanwhile) cannot run ahead
             self._gtrans_flush()
             self._upload_step_inputs(st, reqs, Bp, tok, pos, slots, lens, bt, True, gslot)

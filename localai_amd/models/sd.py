@@ -629,8 +629,16 @@ class Scheduler:
 class StableDiffusion:
     def __init__(self, path: str, device: str = "cpu", scheduler: str = "", clip_skip: int = 0,
                  channels_last: Optional[bool] = None, controlnet: str = "", controlnet_scale: float = 1.0,
-                 lora: str = "", lora_scale: float = 1.0):
+                 lora: str = "", lora_scale: float = 1.0, deterministic: Optional[bool] = None):
         self.device = torch.device(device)
+        # MIOpen's default convolution solvers are not bitwise reproducible run to run (a 1-ulp
+        # difference in a bf16 conv output, scripts/determinism_probe.py); deterministic=True (or
+        # LOCALAI_AMD_SD_DETERMINISTIC=1) restricts the convolutions -- eager and captured -- to
+        # deterministic solvers: identical images for identical requests, ~1.8x the UNet time on
+        # the toy shapes measured
+        if deterministic is None:
+            deterministic = os.environ.get("LOCALAI_AMD_SD_DETERMINISTIC", "0") == "1"
+        self.deterministic = bool(deterministic)
         # NHWC activations for the MIOpen convolutions (LOCALAI_AMD_SD_NHWC=0 keeps NCHW)
         if channels_last is None:
             channels_last = os.environ.get("LOCALAI_AMD_SD_NHWC", "1") != "0"
@@ -842,10 +850,16 @@ class StableDiffusion:
         a = a.expand(batch, -1, -1, -1).to(self.device, self.dtype)
         return a.contiguous(memory_format=torch.channels_last) if self.channels_last else a.contiguous()
 
+    def __call__(self, *args, **kw) -> torch.Tensor:
+        if not self.deterministic:
+            return self._call(*args, **kw)
+        with torch.backends.cudnn.flags(enabled=True, benchmark=False, deterministic=True):
+            return self._call(*args, **kw)
+
     @torch.inference_mode()
-    def __call__(self, prompt: str, negative_prompt: str = "", width: int = 512, height: int = 512,
-                 steps: int = 1, guidance_scale: float = 7.0, seed: Optional[int] = None,
-                 image=None, strength: float = 0.8, control_image=None) -> torch.Tensor:
+    def _call(self, prompt: str, negative_prompt: str = "", width: int = 512, height: int = 512,
+              steps: int = 1, guidance_scale: float = 7.0, seed: Optional[int] = None,
+              image=None, strength: float = 0.8, control_image=None) -> torch.Tensor:
         """-> uint8 image [H, W, 3] on the CPU.  `image` (a path or PIL image) turns the call into
         img2img: its latents are noised to `strength` of the schedule and denoised from there.
         `control_image` conditions every step through the ControlNet (pipelines loaded with one)."""

@@ -58,4 +58,6 @@ for special in ("", "penalty", "grammar", ""):
     if special == "grammar":
         m = eng.metrics
         print(f"  grammar runs {m['grammar_runs']} rows {m['grammar_run_rows']} tokens {m['grammar_run_tokens']} "
-              f"hit-rate {dict((k[:20], round(v, 3)) for k, v in eng._ghit.items())}", flush=True)
+              f"hit-rate {dict((k[:20], round(v, 3)) for k, v in eng._ghit.items())} "
+              f"single-step reasons {dict(eng.k1_reasons)}", flush=True)
+    eng.k1_reasons.clear()

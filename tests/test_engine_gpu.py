@@ -356,14 +356,19 @@ def test_grammar_row_rides_multistep_plain_batch(tiny_model_path):
     assert mixed[0][1] == 24 and re.fullmatch(r"[a-z ]+", txt), txt
 
 
-def test_q5_k_m_decode_batch_uses_persistent_bf16_copies(tmp_path):
-    """Formats the tile GEMM does not read (Q5_K here) get a persistent bf16 copy before any
-    graph capture, so a 65-256-row decode batch runs the library GEMM on it instead of
-    re-dequantising into scratch inside its graph; multi-step == single-step at batch 100."""
+def test_non_tile_weights_decode_batch_uses_persistent_bf16_copies(tmp_path):
+    """Weights the tile GEMM cannot read (here K = 320 / 640, not multiples of 256) get a
+    persistent bf16 copy before any graph capture, so a 65-256-row decode batch runs the library
+    GEMM on it instead of re-dequantising into scratch inside its graph; multi-step ==
+    single-step at batch 100.  (Q5_K and other non-native formats are already bf16 on the GPU.)"""
+    import dataclasses
+
     from localai_amd import ops
     from localai_amd.models import synth
-    p = str(tmp_path / "q5.gguf")
-    synth.write_model(p, "tiny-llama-q5km")
+    synth.PRESETS["tiny-k320"] = dataclasses.replace(synth.PRESETS["tiny-llama"], n_embd=320, n_ff=640,
+                                                     qtype="Q8_0", name="tiny-k320")
+    p = str(tmp_path / "k320.gguf")
+    synth.write_model(p, "tiny-k320")
 
     def eng(K):
         return LLMEngine(EngineConfig(model_path=p, device="cuda:0", context_size=256, max_num_seqs=128,
@@ -372,10 +377,11 @@ def test_q5_k_m_decode_batch_uses_persistent_bf16_copies(tmp_path):
     non_tile = [w for L in e1.model.layers for grp in (L.qkv, L.gate_up, [L.wo], [L.down]) for w in grp
                 if not w.tile_ok]
     assert non_tile and all(w.bf16 is not None for w in non_tile)
-    prompts = [f"q5 batch {i}" for i in range(100)]
+    prompts = [f"k320 batch {i}" for i in range(100)]
     a = _run(e1, prompts, max_tokens=6, temperature=0.0, ignore_eos=True)
     ops._SCRATCH.clear()
     e8 = eng(8)
     b = _run(e8, prompts, max_tokens=6, temperature=0.0, ignore_eos=True)
     assert a == b and all(x[1] == 6 for x in a)
     assert any(bp > 64 for bp in e8._graphs)
+    assert not ops._SCRATCH, "a decode graph dequantised into the shared scratch"

@@ -111,11 +111,16 @@ def test_sdxl_on_gpu_graph_matches_eager(xl_dir):
     pipe.use_graphs = False
     d = pipe("graph capture", steps=3, seed=5, width=64, height=64)
     assert a.shape == (64, 64, 3)
-    # two all-replay runs are bitwise equal; replays vs eager agree up to bf16 rounding (the
-    # eager first call and the captured graph may pick different library GEMM solutions)
-    assert torch.equal(b, c)
-    assert p_close(a, b) and p_close(b, d)
+    # MIOpen's default conv solvers are not bitwise reproducible (scripts/determinism_probe.py:
+    # 1 bf16 ulp in a conv output): replays and eager agree up to rounding
+    assert p_close(a, b) and p_close(b, c) and p_close(b, d)
     assert pipe._graphs
+    # deterministic=True: two all-replay runs are bitwise equal
+    det = StableDiffusion(xl_dir, device="cuda:0", deterministic=True)
+    det("graph capture", steps=3, seed=5, width=64, height=64)
+    b2 = det("graph capture", steps=3, seed=5, width=64, height=64)
+    c2 = det("graph capture", steps=3, seed=5, width=64, height=64)
+    assert torch.equal(b2, c2) and p_close(b2, b)
 
 
 @pytest.mark.gpu
