@@ -227,6 +227,7 @@ class LLMEngine:
         self._pcache = PromptCacheFiles()
         self._graph_pool = None
         self.k1_reasons = collections.Counter()
+        self.k_hist = collections.Counter()   # (device steps, constrained rows in the batch) per decode run
         self.metrics = {"prompt_tokens": 0, "gen_tokens": 0, "steps": 0, "prefill_s": 0.0, "decode_s": 0.0,
                         "requests": 0, "spec_steps": 0, "spec_drafted": 0, "spec_accepted": 0,
                         "grammar_runs": 0, "grammar_run_rows": 0, "grammar_run_tokens": 0}
@@ -508,6 +509,7 @@ class LLMEngine:
                 if spec_k:
                     self._run_spec(plan, spec_k)
                 else:
+                    self.k_hist[(K, sum(1 for i in d_ids if self.requests[int(i)].grammar is not None))] += 1
                     self._run_decode(plan, K)
             t1 = time.perf_counter()
             self.metrics["decode_s"] += t1 - t0
@@ -1082,58 +1084,75 @@ class LLMEngine:
         nb = bt.shape[1]
         h["bt"][:, :nb] = torch.from_numpy(bt)
         h["step"][0] = 0
-        n_bias = 0
+        # the per-request sampling inputs (params, logit bias, penalty windows) depend only on the
+        # batch's requests: an unchanged batch (the common multi-run case) refreshes just the
+        # per-row counters instead of rebuilding ~256 rows in Python between two graph runs
+        key = (device_sampling, tuple(r.id for r in reqs))
+        same = st.get("in_key") == key
+        st["in_key"] = key
+        n_bias = st.get("in_nbias", 0) if same else 0
         if device_sampling:
             prm = st["prm_np"]
-            prm[:] = 0  # padding rows: greedy
-            for j, r in enumerate(reqs):
-                p = r.params
-                prm[j] = (p.temperature, p.top_p, p.min_p, p.typical_p, p.tfs_z, p.mirostat_tau, p.mirostat_eta,
-                          p.top_k, 2 if p.mirostat == 2 else 0, 0, p.seed & 0xFFFFFFFFFFFFFFFF, r.n_gen)
+            if same:
+                prm["counter"][:B] = [r.n_gen for r in reqs]
+            else:
+                prm[:] = 0  # padding rows: greedy
+                for j, r in enumerate(reqs):
+                    p = r.params
+                    prm[j] = (p.temperature, p.top_p, p.min_p, p.typical_p, p.tfs_z, p.mirostat_tau, p.mirostat_eta,
+                              p.top_k, 2 if p.mirostat == 2 else 0, 0, p.seed & 0xFFFFFFFFFFFFFFFF, r.n_gen)
             h["prm"][:] = torch.from_numpy(prm.view(np.uint8))
-            rows, cols, vals = st["bias_np"]
-            for j, r in enumerate(reqs):
-                for t, b in r.params.logit_bias.items():
-                    if 0 <= t < self.hp.n_vocab:
-                        rows[n_bias], cols[n_bias], vals[n_bias] = j, t, b
-                        n_bias += 1
-                if r.params.ignore_eos:
-                    for t in self.tokenizer.eog:
-                        rows[n_bias], cols[n_bias], vals[n_bias] = j, t, -math.inf
-                        n_bias += 1
-            h["bias_rows"][:] = torch.from_numpy(rows)
-            h["bias_cols"][:] = torch.from_numpy(cols)
-            h["bias_vals"][:] = torch.from_numpy(vals)
-            mu = np.zeros(Bp, dtype=np.float32)
-            for j, r in enumerate(reqs):
-                mu[j] = r.mu
-            h["mu"][:] = torch.from_numpy(mu)
-        # penalty windows: neutral unless a device-sampled row asks for penalties
-        pen = np.zeros((Bp, 3), dtype=np.float32)
-        pen[:, 0] = 1.0
-        pcap = np.zeros(Bp, dtype=np.int32)
-        pcnt = np.zeros(Bp, dtype=np.int32)
-        pnl = np.ones(Bp, dtype=np.int32)
-        if device_sampling:
-            for j, r in enumerate(reqs):
-                p = r.params
-                if p.repeat_penalty == 1.0 and p.frequency_penalty == 0.0 and p.presence_penalty == 0.0:
-                    continue
-                ln = p.repeat_last_n if p.repeat_last_n >= 0 else self.ctx
-                if ln <= 0:
-                    continue
-                toks = self.sched.tokens(r.id)[-ln:]
-                pen[j] = (p.repeat_penalty, p.frequency_penalty, p.presence_penalty)
-                pcap[j] = ln
-                pcnt[j] = len(toks)
-                pnl[j] = 1 if p.penalize_nl else 0
-                if toks:
-                    h["phist"][j, :len(toks)] = torch.tensor(toks, dtype=torch.int32)
-        h["pen"][:] = torch.from_numpy(pen)
-        h["pcap"][:] = torch.from_numpy(pcap)
-        h["pcnt"][:] = torch.from_numpy(pcnt)
-        h["phl"][:] = torch.from_numpy(np.minimum(pcnt, pcap))
-        h["pnl"][:] = torch.from_numpy(pnl)
+            if not same:
+                rows, cols, vals = st["bias_np"]
+                for j, r in enumerate(reqs):
+                    for t, b in r.params.logit_bias.items():
+                        if 0 <= t < self.hp.n_vocab:
+                            rows[n_bias], cols[n_bias], vals[n_bias] = j, t, b
+                            n_bias += 1
+                    if r.params.ignore_eos:
+                        for t in self.tokenizer.eog:
+                            rows[n_bias], cols[n_bias], vals[n_bias] = j, t, -math.inf
+                            n_bias += 1
+                h["bias_rows"][:] = torch.from_numpy(rows)
+                h["bias_cols"][:] = torch.from_numpy(cols)
+                h["bias_vals"][:] = torch.from_numpy(vals)
+                st["in_nbias"] = n_bias
+                st["in_miro"] = any(r.params.mirostat for r in reqs)
+                st["in_pen"] = any(r.params.repeat_penalty != 1.0 or r.params.frequency_penalty != 0.0
+                                   or r.params.presence_penalty != 0.0 for r in reqs)
+            if st["in_miro"] or not same:
+                mu = np.zeros(Bp, dtype=np.float32)
+                for j, r in enumerate(reqs):
+                    mu[j] = r.mu
+                h["mu"][:] = torch.from_numpy(mu)
+        if not (same and not (device_sampling and st.get("in_pen"))):
+            # penalty windows: neutral unless a device-sampled row asks for penalties (rebuilt
+            # every run while any row uses them: the windows slide)
+            pen = np.zeros((Bp, 3), dtype=np.float32)
+            pen[:, 0] = 1.0
+            pcap = np.zeros(Bp, dtype=np.int32)
+            pcnt = np.zeros(Bp, dtype=np.int32)
+            pnl = np.ones(Bp, dtype=np.int32)
+            if device_sampling:
+                for j, r in enumerate(reqs):
+                    p = r.params
+                    if p.repeat_penalty == 1.0 and p.frequency_penalty == 0.0 and p.presence_penalty == 0.0:
+                        continue
+                    ln = p.repeat_last_n if p.repeat_last_n >= 0 else self.ctx
+                    if ln <= 0:
+                        continue
+                    toks = self.sched.tokens(r.id)[-ln:]
+                    pen[j] = (p.repeat_penalty, p.frequency_penalty, p.presence_penalty)
+                    pcap[j] = ln
+                    pcnt[j] = len(toks)
+                    pnl[j] = 1 if p.penalize_nl else 0
+                    if toks:
+                        h["phist"][j, :len(toks)] = torch.tensor(toks, dtype=torch.int32)
+            h["pen"][:] = torch.from_numpy(pen)
+            h["pcap"][:] = torch.from_numpy(pcap)
+            h["pcnt"][:] = torch.from_numpy(pcnt)
+            h["phl"][:] = torch.from_numpy(np.minimum(pcnt, pcap))
+            h["pnl"][:] = torch.from_numpy(pnl)
         h["bias_n"][0] = n_bias
         st["dev_block"].copy_(st["host_block"], non_blocking=True)
 

@@ -516,6 +516,15 @@ class DecoderModel:
             k = hp.n_expert_used
             ids, wts = ops.moe_router(xn, L.router, k, hp.moe_renorm, hp.expert_weights_scale,
                                       base if self.ep else 0, El if self.ep else 0)
+            if ops.moe_gemv_ok(L.moe_gu, T) and ops.moe_gemv_ok(L.moe_down, T):
+                # 1-2 token decode: the routed experts as int8-dot GEMVs, SwiGLU fused into the
+                # down projection's prologue (no route / grouping launch, no activation launch)
+                fid = ids.reshape(-1)
+                gu = ops.moe_gemv(xn, L.moe_gu, fid, k, T, El)
+                d = ops.moe_gemv(None, L.moe_down, fid, k, T, El, act_src=gu, act_mode=ops.ACT_SWIGLU, wts=wts)
+                if L.shexp_down is not None:
+                    d = ops.Partial((ops.reduce(d) + self._shared_expert(L, xn)).unsqueeze(0))
+                return self._row_parallel_out(d, None)
             order, off = ops.moe_route(ids, El + 1 if self.ep else El)
             gu = ops.moe_linear(xn, L.moe_gu, order, off, k, T)
             h = ops.act(gu, L.F or self.F, ops.ACT_SWIGLU)

@@ -53,6 +53,7 @@ def lib():
             "la_dq_swizzle": [I, P, P, P, I, I, P, P, P],
             "la_qgemm_dq": [I, P, P, I, I, P, I, I, I, P, I, LNG, I, I, P],
             "la_qgemv_dp4": [I, P, P, P, I, P, I, I, I, P, I, LNG, P, LNG, I, P, I, P],
+            "la_moe_gemv": [I, I, P, I, I, I, P, I, I, P, I, I, P, LNG, I, I, P, P, I, LNG, P],
             "la_gemv_variant": [I],
             "la_qgemv_dp4_rope": [I, P, P, P, I, P, I, P, P, P, I, I, I, P, P, P, I, P],
             "la_add_norm": [P, P, LNG, I, P, I, P, P, P, I, I, F, I, P, P],
@@ -1728,6 +1729,45 @@ def moe_linear(x: torch.Tensor, mw: MoEWeights, order: torch.Tensor, off: torch.
     _check(lib().la_moe_gemm(mw.fmt, 1 if down else 0, mw.desc.data_ptr(), mw.N, mw.K, mw.E, order.data_ptr(),
                              off.data_ptr(), topk, x.data_ptr(), x.shape[1], maxM, S,
                              _ptr(wts) if down else None, out.data_ptr(), mw.N, slab, T, _stream()), "la_moe_gemm")
+    return Partial(out)
+
+
+MOE_GEMV = os.environ.get("LOCALAI_AMD_MOE_GEMV", "1") == "1"
+MOE_GEMV_MAX_T = 2
+
+
+def moe_gemv_ok(mw: MoEWeights, T: int) -> bool:
+    """Decode of 1-2 tokens: the routed experts on the int8-dot GEMV path (gemv_dp4.hip
+    moe_gemv_kernel) instead of the MFMA grouped GEMM, which pads each expert's 1-2 rows to 16."""
+    return (MOE_GEMV and T <= MOE_GEMV_MAX_T and mw.desc is not None and mw.K % 256 == 0
+            and mw.fmt in (FMT_Q4_K, FMT_Q6_K, FMT_Q8_0) and all(w.gemv_ok for w in mw.experts[:1]))
+
+
+def moe_gemv(x: Optional[torch.Tensor], mw: MoEWeights, ids: torch.Tensor, topk: int, T: int, E_local: int,
+             act_src: Optional[Partial] = None, act_mode: int = ACT_SWIGLU,
+             wts: Optional[torch.Tensor] = None) -> Partial:
+    """gate|up (act_src None): x [T, K] -> Partial [S, T*topk, N] (row = routed pair); down
+    (act_src = the gate|up Partial): x = wts[p] * act(gate|up row p) -> Partial [S*topk, T, N],
+    the same slab contract as moe_linear.  ids: [T*topk] int32 local expert ids (>= E_local:
+    another rank's expert, rows read as zero)."""
+    P = T * topk
+    S = _gemv_splits([mw.experts[0]], mw.K, 1)
+    dev = ids.device
+    if act_src is None:
+        out = torch.empty(S, P, mw.N, dtype=torch.float32, device=dev)
+        slab = P * mw.N
+        _check(lib().la_moe_gemv(mw.fmt, 0, mw.desc.data_ptr(), mw.N, mw.K, E_local, ids.data_ptr(), T, topk,
+                                 x.data_ptr(), x.shape[1], S, None, 0, 0, 0, None, out.data_ptr(), mw.N, slab,
+                                 _stream()), "la_moe_gemv")
+    else:
+        a = act_src.src_args()
+        if act_src.t.dim() != 3 or a[3]:
+            raise ValueError("moe_gemv: the activation source must be fp32 slabs without bias")
+        out = torch.empty(S * topk, T, mw.N, dtype=torch.float32, device=dev)
+        slab = T * mw.N
+        _check(lib().la_moe_gemv(mw.fmt, 1, mw.desc.data_ptr(), mw.N, mw.K, E_local, ids.data_ptr(), T, topk,
+                                 None, 0, S, a[0], a[1], a[2], act_mode, wts.data_ptr(), out.data_ptr(), mw.N, slab,
+                                 _stream()), "la_moe_gemv")
     return Partial(out)
 
 

@@ -70,6 +70,7 @@ struct GVAct {
   int S;
   const float* bias;   // optional per-column bias of the gate|up output (length W)
   int mode, F;
+  float scale = 1.f;   // x multiplied by this (an MoE routing weight: down(w x) = w down(x))
 };
 
 LA_DEV float4 gv_sum_slabs(const GVAct& a, long idx, int col) {
@@ -126,7 +127,7 @@ LA_DEV void quantize_x(const bf16* X, int ldx, const GVAct& act, int M, int k0, 
       if (act.p) {
         float v[4];
         gv_act_x(act, m, k0 + sb * 256 + 4 * l, v);
-        v0 = v[0]; v1 = v[1]; v2 = v[2]; v3 = v[3];
+        v0 = v[0] * act.scale; v1 = v[1] * act.scale; v2 = v[2] * act.scale; v3 = v[3] * act.scale;
       } else {
         const u32x2 raw = *(const u32x2*)(xr + sb * 256 + 4 * l);
         v0 = bf16_bits_to_f(raw.x & 0xFFFFu); v1 = bf16_bits_to_f(raw.x >> 16);
@@ -776,6 +777,51 @@ __global__ __launch_bounds__(GV_THREADS) void qgemv_dp4_kernel(GVArgs a, const b
   }
 }
 
+// MoE decode (1-2 tokens): the routed experts' projections as GEMVs on the int8-dot path.  One
+// workgroup = (32-row block, K split, routed pair p = token t x slot); the expert is read from
+// the device routing (ids[p], local ids, >= E_local: another rank's expert -> zero rows), its
+// planes from the device QW descriptors, so the launch is graph-capturable with no host routing.
+//   gate|up (down = 0): x = X[t]           -> out [S][P][N]        (row p)
+//   down    (down = 1): x = wts[p] * act(gate|up slab row p) -> out [S*topk][T][N] (slab
+//                       split*topk + slot, row t): summing the slabs is the weighted combine.
+template <int FMT, int VAR>
+__global__ __launch_bounds__(GV_THREADS) void moe_gemv_kernel(const QW* __restrict__ qws, const int* __restrict__ ids,
+                                                              int E_local, int topk, const bf16* __restrict__ X,
+                                                              int ldx, GVAct act, const float* __restrict__ wts,
+                                                              int down, int kper, float* __restrict__ out, int ldo,
+                                                              long slab) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t gv_lds[];
+  int8_t* xq = (int8_t*)gv_lds;
+  int* bs = (int*)(gv_lds + kper);
+  float* dx = (float*)(gv_lds + kper + (kper >> 4) * 4);
+  constexpr int RS = gv_rs<VAR>();
+  constexpr int NT = VAR & 1, EARLY = (VAR >> 1) & 1, PD = (VAR & 16) ? 4 : 0;
+  const int p = blockIdx.z, t = p / topk, slot = p - t * topk;
+  const int row0 = blockIdx.x * (32 * RS);
+  float* o = down ? out + ((size_t)blockIdx.y * topk + slot) * slab + (size_t)t * ldo
+                  : out + (size_t)blockIdx.y * slab + (size_t)p * ldo;
+  const int e = ids[p];
+  if (e < 0 || e >= E_local) {  // not computed here: its rows read as zero
+    const int N = qws[0].N;
+    for (int i = threadIdx.x; i < 32 * RS; i += GV_THREADS)
+      if (row0 + i < N) o[row0 + i] = 0.f;
+    return;
+  }
+  const QW w = qws[e];
+  GVAct a = act;
+  const bf16* xp = X;
+  if (down) {
+    a.p = act.p + (size_t)p * ((act.mode == 0 || act.mode == 3) ? 2L * act.F : (long)act.F);
+    a.scale = wts[p];
+  } else {
+    xp = X + (size_t)t * ldx;
+  }
+  const GVRope rp{};
+  if constexpr (FMT == FMT_Q8_0) gv_q8<1, NT, EARLY, RS, PD>(w, row0, xp, ldx, a, 1, kper, o, 0, 0, xq, bs, dx, rp);
+  else if constexpr (FMT == FMT_Q4_K) gv_q4k<1, NT, EARLY, RS, PD>(w, row0, xp, ldx, a, 1, kper, o, 0, 0, xq, bs, dx, rp);
+  else gv_q6k<1, NT, EARLY, RS, PD>(w, row0, xp, ldx, a, 1, kper, o, 0, 0, xq, bs, dx, rp);
+}
+
 static inline size_t gv_lds_bytes(int MT, int kper) {
   return (size_t)MT * kper + (size_t)MT * (kper >> 4) * 4 + (size_t)MT * (kper >> 5) * 4;
 }
@@ -899,6 +945,37 @@ extern "C" int la_qgemv_dp4_rope(int nseg, const int* fmts, const void* const* p
   // out / slab are unused by the rope epilogue; pass a non-null dummy that passes the checks
   return qgemv_dp4_impl(nseg, fmts, planes, Ns, K, X, K, M, 1, q_out, W, (long)M * W, nullptr, 0, 0, nullptr, 0,
                         stream, rp);
+}
+
+// MoE decode GEMV (see moe_gemv_kernel): fmt / N / K shared by the E_local experts of `qws`
+// (device QW descriptors); ids [P = T*topk] local expert ids; down: act_p = the gate|up fp32
+// slabs [act_S][P][2F] (SwiGLU, act_mode 0 / GeGLU 3) or [..][P][F], wts [P] routing weights.
+extern "C" int la_moe_gemv(int fmt, int down, const void* qws, int N, int K, int E_local, const int* ids, int T,
+                           int topk, const void* X, int ldx, int splits, const void* act_p, long act_slab, int act_S,
+                           int act_mode, const float* wts, void* out, int ldo, long slab, void* stream) {
+  using namespace la;
+  if (T < 1 || topk < 1 || N < 1 || (K & 255) || splits < 1 || ((K >> 8) % splits) || E_local < 1 || !qws || !ids)
+    return -1;
+  if (fmt != FMT_Q4_K && fmt != FMT_Q6_K && fmt != FMT_Q8_0) return -2;
+  if (down ? (!act_p || !wts || act_S < 1 || act_S > 16 || (act_mode != 0 && act_mode != 3 && act_mode != 1 &&
+                                                             act_mode != 2))
+           : (!X || ldx < K))
+    return -1;
+  const int kper = K / splits;
+  const size_t lds = gv_lds_bytes(1, kper);
+  if (lds > 64 * 1024) return -3;
+  GVAct act{(const float*)act_p, act_slab, act_S, nullptr, act_mode, K};
+  constexpr int V = 5;  // non-temporal weights, x staged first, one 8-row slot per wave
+  const int rows = 32 * gv_rs<V>();
+  dim3 grid((N + rows - 1) / rows, splits, T * topk);
+  hipStream_t st = (hipStream_t)stream;
+#define MG(F) hipLaunchKernelGGL((moe_gemv_kernel<F, V>), grid, dim3(GV_THREADS), lds, st, (const QW*)qws, ids, \
+                                 E_local, topk, (const bf16*)X, ldx, act, wts, down, kper, (float*)out, ldo, slab)
+  if (fmt == FMT_Q4_K) MG(FMT_Q4_K);
+  else if (fmt == FMT_Q6_K) MG(FMT_Q6_K);
+  else MG(FMT_Q8_0);
+#undef MG
+  return (int)hipGetLastError();
 }
 
 // Tuning hook: select the kernel variant (bit 0 non-temporal loads, bit 1 early weight prefetch).

@@ -52,12 +52,18 @@ def wave(tag, special):
 
 
 wave("warm", "")
+eng.k1_reasons.clear()
+eng.k_hist.clear()
 for special in ("", "penalty", "grammar", ""):
+    eng.k1_reasons.clear()
+    eng.k_hist.clear()
     r = wave(f"w{time.time():.0f}", special)
     print(f"{special or 'plain':8s} decode {r:9.1f} tok/s", flush=True)
     if special == "grammar":
         m = eng.metrics
         print(f"  grammar runs {m['grammar_runs']} rows {m['grammar_run_rows']} tokens {m['grammar_run_tokens']} "
               f"hit-rate {dict((k[:20], round(v, 3)) for k, v in eng._ghit.items())} "
-              f"single-step reasons {dict(eng.k1_reasons)}", flush=True)
+              f"single-step reasons {dict(eng.k1_reasons)} runs by (K, constrained rows) {dict(eng.k_hist)}",
+              flush=True)
     eng.k1_reasons.clear()
+    eng.k_hist.clear()

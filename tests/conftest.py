@@ -44,7 +44,11 @@ def record_calls(obj, name):
 
     def wrapped(*args):
         out = fn(*args)
-        calls.append((tuple(a.detach().clone() if hasattr(a, "detach") else a for a in args), out.detach().clone()))
+        def keep(a):
+            if isinstance(a, (tuple, list)):
+                return type(a)(keep(v) for v in a)
+            return a.detach().clone() if hasattr(a, "detach") else a
+        calls.append((tuple(keep(a) for a in args), out.detach().clone()))
         return out
     setattr(obj, name, wrapped)
     return calls
@@ -55,9 +59,14 @@ def compare_to_fp32(calls, fp32_fn, min_cos=0.999, max_rel=3e-2):
     same inputs: cosine similarity and relative L2 error of the outputs.  Returns the worst pair."""
     import torch
     worst_cos, worst_rel = 1.0, 0.0
+    def to32(a):
+        if isinstance(a, (tuple, list)):
+            return type(a)(to32(v) for v in a)
+        if hasattr(a, "is_floating_point"):
+            return a.float().cpu() if a.is_floating_point() else a.cpu()
+        return a
     for args, out in calls:
-        a32 = tuple(a.float().cpu() if hasattr(a, "is_floating_point") and a.is_floating_point()
-                    else (a.cpu() if hasattr(a, "cpu") else a) for a in args)
+        a32 = tuple(to32(a) for a in args)
         with torch.inference_mode():
             ref = fp32_fn(*a32).float().flatten()
         got = out.float().cpu().flatten()

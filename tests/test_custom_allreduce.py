@@ -21,7 +21,12 @@ def test_custom_allreduce_ranks_share_one_gpu(world):
                         "--master-addr", "127.0.0.1", "--master-port", str(29533 + world),
                         os.path.join(ROOT, "scripts", "ar_check.py")],
                        cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    if r.returncode != 0:
+        # the failing rank's traceback, not just torchrun's summary
+        lines = [ln for ln in r.stderr.splitlines() if "Gloo" not in ln]
+        tb = [i for i, ln in enumerate(lines) if "Traceback" in ln]
+        head = "\n".join(lines[tb[0]:tb[0] + 40]) if tb else ""
+        raise AssertionError(head + "\n---\n" + r.stdout[-2000:] + r.stderr[-1500:])
     assert "AR_OK" in r.stdout, r.stdout[-2000:]
 
 

@@ -794,3 +794,35 @@ def test_grammar_mask_kernel_matches_torch():
     ops.grammar_mask(out, slot, pool)
     torch.cuda.synchronize()
     assert torch.equal(out, ref)
+
+
+@pytest.mark.parametrize("T", [1, 2])
+@pytest.mark.parametrize("fmts", [(GGMLType.Q4_K, GGMLType.Q6_K), (GGMLType.Q8_0, GGMLType.Q8_0)])
+def test_moe_gemv_decode(T, fmts):
+    """1-2 token MoE decode on the int8-dot GEMV (moe_gemv_kernel): device routing ids, SwiGLU +
+    routing weight fused into the down prologue; vs the fp32 reference of the same weights.  A
+    pair routed to another rank's expert (id >= E_local) contributes zero."""
+    E, topk, D, F = 8, 2, 512, 768
+    gu = [_qw(2 * F, D, fmts[0], seed=10 + e) for e in range(E)]
+    dn = [_qw(D, F, fmts[1], seed=30 + e) for e in range(E)]
+    mg, md = ops.MoEWeights(gu), ops.MoEWeights(dn)
+    assert ops.moe_gemv_ok(mg, T) and ops.moe_gemv_ok(md, T)
+    x = torch.randn(T, D, device=DEV).to(torch.bfloat16)
+    ids = torch.stack([torch.randperm(E)[:topk] for _ in range(T)]).to(torch.int32).view(-1)
+    if T == 2:
+        ids[3] = E  # another rank's expert
+    ids = ids.to(DEV)
+    wts = torch.rand(T * topk, device=DEV)
+    g = ops.moe_gemv(x, mg, ids, topk, T, E)
+    z = ops.moe_gemv(None, md, ids, topk, T, E, act_src=g, act_mode=ops.ACT_SWIGLU, wts=wts).dense().cpu()
+    xc, idc, wc = x.float().cpu(), ids.cpu().long(), wts.cpu()
+    ref = torch.zeros(T, D)
+    for p in range(T * topk):
+        e = int(idc[p])
+        if e >= E:
+            continue
+        h = xc[p // topk] @ gu[e].ref.t()
+        a = torch.nn.functional.silu(h[:F]) * h[F:]
+        ref[p // topk] += float(wc[p]) * (a @ dn[e].ref.t())
+    err = float((z - ref).abs().max() / ref.abs().max())
+    assert err < 3e-2, err
