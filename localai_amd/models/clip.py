@@ -93,6 +93,18 @@ class ClipVision:
         self.newline = t("model.image_newline", False)
         self.grid = self.image_size // self.patch
         self.n_patches = self.grid * self.grid
+        # GPU: the tower's projections through ops.linear (bf16 weights: the tile GEMM at small
+        # M, the library GEMM on the weight in place at large M), residual + LayerNorm fused in
+        # add_norm, activations in the act kernel (SURVEY K19 / K20 / K21 on the native ops)
+        self.native = device.type == "cuda" and os.environ.get("LOCALAI_AMD_CLIP_NATIVE", "1") == "1"
+        if self.native:
+            from .. import ops
+            qw = ops.QWeight.from_float
+            self.q_patch = qw(self.patch_w)
+            for ly in self.layers:
+                for k in ("qkv_w", "o_w", "f1_w", "f2_w"):
+                    ly["q_" + k] = qw(ly[k])
+            self.q_mm0, self.q_mm2 = qw(self.mm0[0]), qw(self.mm2[0])
 
     # ------------------------------------------------------------------ preprocessing
     def _norm(self, img) -> torch.Tensor:
@@ -176,6 +188,8 @@ class ClipVision:
     @torch.inference_mode()
     def encode_tiles(self, pix: torch.Tensor) -> torch.Tensor:
         """pixels [n, 3, S, S] -> projected patch embeddings [n, n_patches, out_dim] (f32)."""
+        if self.native:
+            return self._encode_native(pix)
         n = pix.shape[0]
         D, P, H = self.dim, self.patch, self.heads
         x = pix.to(self.device, torch.float32)
@@ -210,6 +224,55 @@ class ClipVision:
         y = F.gelu(y)
         y = (y.to(self.dtype) @ self.mm2[0].t()).float() + self.mm2[1]
         return y
+
+    def _encode_native(self, pix: torch.Tensor) -> torch.Tensor:
+        """encode_tiles on the native ops: im2col + GEMM patch embedding, fused residual +
+        LayerNorm (add_norm mode 1), GELU / quick-GELU in the act kernel (llama.cpp's clip uses
+        the tanh GELU too), attention through SDPA (non-causal, L <= 730)."""
+        from .. import ops
+        n = pix.shape[0]
+        D, P, H = self.dim, self.patch, self.heads
+        x = pix.to(self.device, torch.float32)
+        cols = F.unfold(x, kernel_size=P, stride=P).transpose(1, 2)           # [n, np, 3*P*P]
+        npch = cols.shape[1]
+        pe = ops.reduce(ops.linear(cols.reshape(n * npch, -1).to(self.dtype).contiguous(), self.q_patch,
+                                   bias=self.patch_b)).view(n, npch, D)
+        if self.cls is not None:
+            pe = torch.cat([self.cls.view(1, 1, D).expand(n, 1, D), pe], 1)
+        L = pe.shape[1]
+        h = (pe + self.pos[:L]).reshape(n * L, D).contiguous()                 # fp32 residual stream
+        eps = self.eps
+        if self.pre_ln[0] is not None:
+            nrm = torch.empty_like(h)
+            ops.add_norm(h, None, self.pre_ln[0], self.pre_ln[1], eps, mode=1, want_out=False, out_f32=nrm)
+            h = nrm
+        act = ops.ACT_GELU if self.use_gelu else ops.ACT_GELU_QUICK
+        a = ops.add_norm(h, None, self.layers[0]["ln1"][0], self.layers[0]["ln1"][1], eps, mode=1)
+        for i, ly in enumerate(self.layers):
+            qkv = ops.reduce(ops.linear(a, ly["q_qkv_w"], bias=ly["qkv_b"]), dtype=self.dtype)
+            q, k, v = qkv.view(n, L, 3, H, D // H).permute(2, 0, 3, 1, 4)
+            o = F.scaled_dot_product_attention(q, k, v)                        # non-causal
+            o = o.transpose(1, 2).reshape(n * L, D).contiguous()
+            a2 = ops.add_norm(h, ops.linear(o, ly["q_o_w"], bias=ly["o_b"]), ly["ln2"][0], ly["ln2"][1], eps, mode=1)
+            f1 = ops.linear(a2, ly["q_f1_w"], bias=ly["f1_b"])
+            g = ops.act(f1, f1.N, act)
+            f2 = ops.linear(g, ly["q_f2_w"], bias=ly["f2_b"])
+            if i + 1 < len(self.layers):
+                nx = self.layers[i + 1]["ln1"]
+                a = ops.add_norm(h, f2, nx[0], nx[1], eps, mode=1)
+            elif self.post_ln[0] is not None:
+                nrm = torch.empty_like(h)
+                ops.add_norm(h, f2, self.post_ln[0], self.post_ln[1], eps, mode=1, want_out=False, out_f32=nrm)
+                h = nrm
+            else:
+                ops.add_norm(h, f2, self.layers[-1]["ln2"][0], self.layers[-1]["ln2"][1], eps, mode=1, want_out=False)
+        h = h.view(n, L, D)
+        if self.cls is not None:
+            h = h[:, 1:]                                                       # drop CLS
+        hb = h.reshape(-1, D).to(self.dtype).contiguous()
+        y = ops.act(ops.linear(hb, self.q_mm0, bias=self.mm0[1]), self.mm0[0].shape[0], ops.ACT_GELU)
+        y = ops.reduce(ops.linear(y, self.q_mm2, bias=self.mm2[1]))
+        return y.view(n, -1, self.out_dim)
 
     def embed_image(self, data) -> torch.Tensor:
         """One image -> [n_tokens, out_dim] f32 rows to splice into the prompt."""

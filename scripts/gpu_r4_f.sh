@@ -7,7 +7,7 @@ HB=$!
 trap 'kill $HB 2>/dev/null' EXIT
 step() { local log=$1 t=$2; shift 2; timeout -k 10 $t "$@" > gpurun_out/$log 2>&1; local rc=$?; tail -2 gpurun_out/$log | cut -c1-400; [ $rc -eq 0 ] || { grep -E "FAILED|Error" gpurun_out/$log | head -20; tail -40 gpurun_out/$log; exit $rc; }; }
 PT="python -u -m pytest -x -v --timeout 300 --timeout-method thread"
-step t_moe.log 300 $PT tests/test_kernels_gpu.py -k "moe"
+step t_moe.log 300 $PT tests/test_kernels_gpu.py -k "moe or clip"
 step t_fix.log 600 $PT tests/test_engine_gpu.py -k "penalties or rides or stride or mixtral"
 step t_xl.log 300 $PT tests/test_sdxl.py -k "fp32_forward or graph_matches"
 step t_ar8.log 400 $PT tests/test_custom_allreduce.py

@@ -826,3 +826,25 @@ def test_moe_gemv_decode(T, fmts):
         ref[p // topk] += float(wc[p]) * (a @ dn[e].ref.t())
     err = float((z - ref).abs().max() / ref.abs().max())
     assert err < 3e-2, err
+
+
+@pytest.mark.parametrize("cls_token", [True, False])
+def test_clip_tower_native_ops_match_fp32(tmp_path, cls_token):
+    """The vision tower on the native ops (ops.linear projections, fused residual + LayerNorm in
+    add_norm, act-kernel GELU) vs the fp32 PyTorch tower on the CPU, same mmproj and pixels:
+    every projected patch embedding row close in cosine and relative L2."""
+    from localai_amd.models import synth
+    from localai_amd.models.clip import ClipVision
+    kw = dict(out_dim=256, dim=128, n_layer=2, heads=4, ffn=256, image_size=56, patch=14)
+    if not cls_token:
+        kw["siglip"] = True
+    mm = synth.write_mmproj(str(tmp_path / "mm.gguf"), **kw)
+    gpu, cpu = ClipVision(mm, DEV), ClipVision(mm, torch.device("cpu"), dtype=torch.float32)
+    assert gpu.native and not cpu.native
+    pix = torch.randn(3, 3, 56, 56)
+    a = gpu.encode_tiles(pix.to(DEV)).float().cpu()
+    b = cpu.encode_tiles(pix)
+    assert a.shape == b.shape
+    cos = torch.nn.functional.cosine_similarity(a.reshape(-1, a.shape[-1]), b.reshape(-1, b.shape[-1]), dim=1)
+    rel = float((a - b).norm() / b.norm())
+    assert float(cos.min()) > 0.995 and rel < 5e-2, (float(cos.min()), rel)
