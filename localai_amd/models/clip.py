@@ -244,7 +244,7 @@ class ClipVision:
         eps = self.eps
         if self.pre_ln[0] is not None:
             nrm = torch.empty_like(h)
-            ops.add_norm(h, None, self.pre_ln[0], self.pre_ln[1], eps, mode=1, want_out=False, out_f32=nrm)
+            ops.add_norm(h, None, self.pre_ln[0], self.pre_ln[1], eps, mode=1, out_f32=nrm)  # (out_f32 needs the bf16 output too)
             h = nrm
         act = ops.ACT_GELU if self.use_gelu else ops.ACT_GELU_QUICK
         a = ops.add_norm(h, None, self.layers[0]["ln1"][0], self.layers[0]["ln1"][1], eps, mode=1)
@@ -262,7 +262,7 @@ class ClipVision:
                 a = ops.add_norm(h, f2, nx[0], nx[1], eps, mode=1)
             elif self.post_ln[0] is not None:
                 nrm = torch.empty_like(h)
-                ops.add_norm(h, f2, self.post_ln[0], self.post_ln[1], eps, mode=1, want_out=False, out_f32=nrm)
+                ops.add_norm(h, f2, self.post_ln[0], self.post_ln[1], eps, mode=1, out_f32=nrm)  # (out_f32 needs the bf16 output too)
                 h = nrm
             else:
                 ops.add_norm(h, f2, self.layers[-1]["ln2"][0], self.layers[-1]["ln2"][1], eps, mode=1, want_out=False)

@@ -13,3 +13,7 @@ step t_xl.log 300 $PT tests/test_sdxl.py -k "fp32_forward or graph_matches"
 step t_ar8.log 400 $PT tests/test_custom_allreduce.py
 step mx1.log 600 python -u bench.py --mode engine --preset mixtral-8x7b --steps 2 --warmup 1 --concurrency 1 --max-tokens 128
 LOCALAI_AMD_MOE_GEMV=0 step mx1_old.log 600 python -u bench.py --mode engine --preset mixtral-8x7b --steps 2 --warmup 1 --concurrency 1 --max-tokens 128
+step fc8.log 500 python -u scripts/fc_bench.py --preset llama3-8b --concurrency 32
+LOCALAI_AMD_GRAMMAR_RUN_AHEAD=1 step fc8_ra.log 500 python -u scripts/fc_bench.py --preset llama3-8b --concurrency 32
+step mixed_b.log 600 python -u scripts/mixed_batch_bench.py
+grep -h "reasons\|decode" gpurun_out/mixed_b.log
