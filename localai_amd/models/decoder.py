@@ -49,6 +49,16 @@ class CustomAllReduceTimeout(RuntimeError):
 
 
 @dataclass
+class PendingAR:
+    """A row-parallel output whose all-reduce is deferred to its consumer, the layer-boundary
+    add_norm: CustomAllReduce.add_norm then runs slab sum + all-reduce + bias + residual + norm as
+    ONE launch (decode steps of a GPU TP group).  Deliberately not an ops.Partial: any other
+    consumer fails loudly instead of reading a rank-local partial sum."""
+    part: "ops.Partial"
+    bias: Optional[torch.Tensor]
+
+
+@dataclass
 class TPInfo:
     rank: int = 0
     world: int = 1
@@ -192,6 +202,8 @@ def _raw2d(t, rows: Optional[slice] = None, cols: Optional[slice] = None):
 
 
 class DecoderModel:
+    _defer_ar = False  # set per forward: decode all-reduces fused into the next add_norm (PendingAR)
+
     def __init__(self, reader: GGUFReader, device: torch.device, tp: Optional[TPInfo] = None,
                  max_pos: Optional[int] = None, rope_overrides: Optional[dict] = None, lora=None):
         self.hp = hp = HParams.from_gguf(reader)
@@ -447,6 +459,8 @@ class DecoderModel:
     def _row_parallel_out(self, p: ops.Partial, bias) -> ops.Partial:
         if self.tp.world == 1:
             return ops.Partial(p.t, bias)
+        if self._defer_ar and p.t.is_cuda and p.bias is None:
+            return PendingAR(p, bias)
         if TP_AR_BF16 and p.t.is_cuda:
             # decode rows travel in bf16 (16 KiB per 8192-wide row): half the bytes
             # of the fp32 sum over xGMI; the consumer (add_norm) reads a bf16 matrix directly
@@ -585,8 +599,17 @@ class DecoderModel:
             return sh
         return sh * torch.sigmoid(xn.float() @ L.shexp_gate).unsqueeze(1)
 
-    def _post_attn(self, i: int, L: Layer, xn: torch.Tensor, res: torch.Tensor, o: ops.Partial) -> torch.Tensor:
-        """Residual + norm around the MLP of layer i; returns the next layer's normed input."""
+    def _add_norm(self, res, o, w, b, eps, nm):
+        """ops.add_norm, or -- for a deferred TP all-reduce -- the fused all-reduce + add + norm."""
+        if isinstance(o, PendingAR):
+            return self.tp.car.add_norm(o.part, o.bias, res, w, b, eps, nm)
+        return ops.add_norm(res, o, w, b, eps, nm)
+
+    def _post_attn(self, i: int, L: Layer, xn: torch.Tensor, res: torch.Tensor, o: ops.Partial,
+                   defer_to: Optional[torch.Tensor] = None):
+        """Residual + norm around the MLP of layer i; returns the next layer's normed input -- or,
+        with defer_to (batch-1/2 decode, next consumer = the fused q|k|v GEMV), an ops.NormIn that
+        the next GEMV applies in its prologue, the updated residual landing in defer_to."""
         hp = self.hp
         eps, nm = hp.norm_eps, self.norm_mode
         nxt = self.layers[i + 1] if i + 1 < len(self.layers) else None
@@ -598,11 +621,14 @@ class DecoderModel:
             return ops.add_norm(res, f, nw, nb, eps, nm)
         if L.post_attn_norm is not None:
             o = self._post_norm(o, L.post_attn_norm)
-        xn = ops.add_norm(res, o, L.ffn_norm, L.ffn_norm_b, eps, nm)
+        xn = self._add_norm(res, o, L.ffn_norm, L.ffn_norm_b, eps, nm)
         f = self._mlp(L, xn)
         if L.post_ffw_norm is not None:
             f = self._post_norm(f, L.post_ffw_norm)
-        return ops.add_norm(res, f, nw, nb, eps, nm)
+        if (defer_to is not None and nxt is not None and nm == 0 and isinstance(f, ops.Partial)
+                and ops.norm_in_ok(res, f, nw, nb)):
+            return ops.NormIn(res, f, nw, eps, defer_to)
+        return self._add_norm(res, f, nw, nb, eps, nm)
 
     def _post_norm(self, p: ops.Partial, w: torch.Tensor) -> ops.Partial:
         """RMSNorm(p) * w as an fp32 partial (Gemma-2's post-attention / post-FFW norms)."""
@@ -622,18 +648,35 @@ class DecoderModel:
         if fb.inject_idx is not None:
             res.index_copy_(0, fb.inject_idx, fb.inject_rows.to(res.dtype))
         L0 = self.layers[0]
-        xn = ops.add_norm(res, None, L0.attn_norm, L0.attn_norm_b, eps, nm)
-        fuse_qkv = fb.decode and FUSED_QKV_ROPE and ops.qkv_rope_ok(xn, self.layers[0].qkv, self.layers[0].qkv_bias,
+        fuse_qkv = fb.decode and FUSED_QKV_ROPE and ops.qkv_rope_ok(res, self.layers[0].qkv, self.layers[0].qkv_bias,
                                                                     hp.rope_mode, self.rot, self.Dh, kv.block_size)
+        # batch-1/2 decode: every layer boundary's residual-add + RMSNorm runs inside the next
+        # q|k|v GEMV's prologue (ops.NormIn); the residual ping-pongs between two buffers because
+        # that GEMV's workgroups read one while its first workgroup writes the other
+        fuse_norm = (fuse_qkv and nm == 0 and not hp.parallel_residual
+                     and ops.norm_in_ok(res, None, L0.attn_norm, L0.attn_norm_b))
+        res2 = torch.empty_like(res) if fuse_norm else None
+        # GPU TP decode: each layer boundary's all-reduce runs fused with its add_norm
+        car = self.tp.car
+        self._defer_ar = bool(fb.decode and self.tp.world > 1 and car is not None and res.is_cuda
+                              and not hp.parallel_residual and hasattr(car, "supports_add_norm")
+                              and car.supports_add_norm(T, res.shape[1])
+                              and all(L.post_attn_norm is None and L.post_ffw_norm is None for L in self.layers))
+        if fuse_norm:
+            xn = ops.NormIn(res, None, L0.attn_norm, eps, None)
+        else:
+            xn = ops.add_norm(res, None, L0.attn_norm, L0.attn_norm_b, eps, nm)
         for i, L in enumerate(self.layers):
             if fuse_qkv:
                 # batch-1/2 decode: q|k|v GEMV with RoPE + the paged K/V append in its epilogue
                 q = ops.qkv_rope_dp4(xn, L.qkv, fb.pos, fb.slots, self.cos_sin, self.Hq, self.Hkv, self.Dh,
                                      kv.k[i], kv.v[i], kv.block_size)
+                if isinstance(xn, ops.NormIn) and xn.res_out is not None:
+                    res, res2 = xn.res_out, xn.res  # the updated residual now lives in the other buffer
                 a = ops.attn_decode(q, kv.k[i], kv.v[i], fb.block_tables, fb.seq_lens, self.scale, fb.max_len,
                                     workspace=attn_workspace, softcap=hp.attn_softcap, window=L.window)
                 o = self._row_parallel_out(ops.linear(a.view(T, self.Hq * self.Dh), L.wo), L.wo_bias)
-                xn = self._post_attn(i, L, xn, res, o)
+                xn = self._post_attn(i, L, xn, res, o, defer_to=res2)
                 continue
             qkv = self._mla_qkv(L, xn) if L.mla is not None else ops.linear_multi(xn, L.qkv, bias=L.qkv_bias)
             if fb.decode:

@@ -56,6 +56,9 @@ def lib():
             "la_moe_gemv": [I, I, P, I, I, I, P, I, I, P, I, I, P, LNG, I, I, P, P, I, LNG, P],
             "la_gemv_variant": [I],
             "la_qgemv_dp4_rope": [I, P, P, P, I, P, I, P, P, P, I, I, I, P, P, P, I, P],
+            "la_qgemv_dp4_norm": [I, P, P, P, I, I, I, P, I, LNG, P, P, LNG, I, P, P, F, P, P],
+            "la_qgemv_dp4_rope_norm": [I, P, P, P, I, I, P, P, P, I, I, I, P, P, P, I, P, P, LNG, I, P, P, F,
+                                       P, P],
             "la_add_norm": [P, P, LNG, I, P, I, P, P, P, I, I, F, I, P, P],
             "la_rope_kv": [P, LNG, I, P, P, P, P, I, I, I, I, I, I, P, P, P, I, P],
             "la_mamba_conv_step": [P, P, LNG, P, P, P, I, I, I, P],
@@ -448,6 +451,53 @@ def gemv_dp4(x: Optional[torch.Tensor], ws: Sequence[QWeight], S: int, out: torc
         col += sum(w.N for w in seg)
 
 
+GEMV_NORM = os.environ.get("LOCALAI_AMD_GEMV_NORM", "1") == "1"
+
+
+@dataclass
+class NormIn:
+    """A deferred layer-boundary residual-add + RMSNorm, handed to the consuming decode GEMV
+    instead of a materialised bf16 x: x = rmsnorm(res + add) * weight is formed in the GEMV
+    prologue (gemv_dp4.hip GV_NORM) and the updated residual lands in res_out (written once, by
+    one workgroup; None when there is no add).  Removes the add_norm launch at every layer
+    boundary of a batch-1/2 decode step (SURVEY §2.8 K2 + K14 folded into K5)."""
+    res: torch.Tensor               # fp32 [M, D]
+    add: Optional[Partial]          # fp32 split-K slabs [S, M, D] or None
+    weight: torch.Tensor            # fp32 [D]
+    eps: float
+    res_out: Optional[torch.Tensor]  # fp32 [M, D], not res; None iff add is None
+
+    @property
+    def shape(self):
+        return self.res.shape
+
+    @property
+    def is_cuda(self) -> bool:
+        return self.res.is_cuda
+
+    def args(self):
+        a = self.add.src_args() if self.add is not None else (None, 0, 0, None)
+        return (self.res.data_ptr(), a[0], a[1], a[2], a[3], self.weight.data_ptr(), float(self.eps),
+                _ptr(self.res_out))
+
+    def materialize(self) -> torch.Tensor:
+        """The same x through add_norm (residual updated in res, then copied to res_out)."""
+        xn = add_norm(self.res, self.add, self.weight, None, self.eps, 0)
+        if self.res_out is not None:
+            self.res_out.copy_(self.res)
+        return xn
+
+
+def norm_in_ok(res: torch.Tensor, add: Optional[Partial], weight: torch.Tensor, bias) -> bool:
+    """A NormIn can feed the fused GEMV prologue: GPU, fp32 residual of <= GEMV_MAX_M rows and
+    width <= 8192, fp32 weight, no norm bias (RMSNorm), the add as fp32 split-K slabs."""
+    M, D = res.shape
+    return (GEMV_NORM and GEMV_DP4 and res.is_cuda and res.dtype == torch.float32 and M <= GEMV_MAX_M
+            and D <= 8192 and D % 256 == 0 and bias is None and weight.dtype == torch.float32
+            and (add is None or (add.t.dim() == 3 and add.t.dtype == torch.float32 and add.S <= 16
+                                 and add.N == D)))
+
+
 def qkv_rope_ok(x: torch.Tensor, ws: Sequence[QWeight], bias, mode: int, rot: int, Dh: int, block_size: int) -> bool:
     """The fused decode q|k|v GEMV + RoPE + KV append (gemv_dp4.hip GVRope) applies: GPU, batch
     <= GEMV_MAX_M, Q4_K/Q6_K weights, no bias, NORM rotary over the whole head."""
@@ -464,6 +514,20 @@ def qkv_rope_dp4(x: torch.Tensor, ws: Sequence[QWeight], pos: torch.Tensor, slot
     cache at `slots` -- one GEMV launch (split-K 1) with the rotation and the append in its
     epilogue, instead of a GEMV + rope_kv."""
     M, K = x.shape
+    if isinstance(x, NormIn):
+        if q_out is None:
+            q_out = torch.empty(M, Hq, Dh, dtype=torch.bfloat16, device=x.res.device)
+        if sum(w.N for w in ws) != (Hq + 2 * Hkv) * Dh:
+            raise ValueError("qkv_rope_dp4: weights do not form q|k|v")
+        n = len(ws)
+        fmts = (ctypes.c_int * n)(*[w.fmt for w in ws])
+        planes = (ctypes.c_void_p * (4 * n))(*[p for w in ws for p in w.ptrs()])
+        Ns = (ctypes.c_int * n)(*[w.N for w in ws])
+        _check(lib().la_qgemv_dp4_rope_norm(n, fmts, planes, Ns, K, M, pos.data_ptr(), slots.data_ptr(),
+                                            cos_sin.data_ptr(), Hq, Hkv, Dh, q_out.data_ptr(), k_cache.data_ptr(),
+                                            v_cache.data_ptr(), block_size, *x.args(), _stream()),
+               "la_qgemv_dp4_rope_norm")
+        return q_out
     if x.dtype != torch.bfloat16 or not x.is_contiguous():
         raise ValueError("qkv_rope_dp4: x must be contiguous bf16")
     if sum(w.N for w in ws) != (Hq + 2 * Hkv) * Dh:

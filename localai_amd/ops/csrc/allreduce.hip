@@ -133,7 +133,171 @@ __global__ __launch_bounds__(AR_T) void allreduce_oneshot_kernel(ARArgs a) {
   if (tid == 0) *counter = ep;
 }
 
-// ----------------------------------------------------------------------------- two-shot
+// ----------------------------------------------------------------------------- fused AR + add + norm
+// The decode layer boundary of a tensor-parallel group in ONE launch: split-K slab sum of the local
+// row-parallel partial (bf16 into the one-shot data slot), the one-shot exchange, the rank-ordered
+// sum, + bias, + residual (fp32, updated in place), and RMSNorm / LayerNorm into the next layer's
+// bf16 input -- where the unfused path runs reduce -> all-reduce -> add_norm (three launches,
+// SURVEY §2.11).  One workgroup per row; row t owns the channels [t*nch, (t+1)*nch) (nch = D/1024
+// rounded up) of the one-shot region, element e of the row in channel e/1024 at its own parity
+// slot, so rows are independent channels and calls interleave freely with one-shot calls.
+constexpr int ARN_IT = 4;  // 8-element groups per thread: D <= 256 x 8 x 4 = 8192
+
+struct ARNArgs {
+  const void* p;        // local partial: S fp32 slabs [S][M][D] (S >= 1) or one bf16 matrix (S == 0)
+  long slab;
+  int S;
+  int D, rank, world;
+  uint8_t* bufs[AR_MAXR];
+  long spin_limit;
+  float* residual;      // [M][D] fp32, += sum (+ bias)
+  const float* bias;    // [D] or null: added once, after the sum
+  const float* w;       // norm weight [D]
+  const float* nb;      // LayerNorm bias [D] or null
+  bf16* out;            // [M][D]
+  float eps;
+  int mode;             // 0 RMSNorm, 1 LayerNorm
+};
+
+__global__ __launch_bounds__(AR_T) void allreduce_add_norm_kernel(ARNArgs a) {
+  __shared__ float red[AR_T / 64];
+  const int t = blockIdx.x, tid = threadIdx.x, D = a.D;
+  const int nch = (D + (int)AR_CHUNK - 1) / (int)AR_CHUNK, b0 = t * nch;
+  uint8_t* own = a.bufs[a.rank];
+  const int* counters = (const int*)(own + AR_COUNTER);
+  // this thread's element groups: e = 8 (tid + AR_T k)
+  float v[ARN_IT][8];
+  long off[ARN_IT];  // byte offset of the group inside a slot region (channel base + within)
+  int par[ARN_IT];
+  // 1. local row (slab sum in fp32, rounded to bf16 as the wire format) -> own data slots
+#pragma unroll
+  for (int k = 0; k < ARN_IT; ++k) {
+    const int e = 8 * (tid + AR_T * k);
+    off[k] = 0;
+    par[k] = 0;
+    if (e >= D) continue;
+    const int ch = e / (int)AR_CHUNK;
+    par[k] = (counters[b0 + ch] + 1) & 1;
+    off[k] = (long)(b0 + ch) * AR_CHUNK * 4 + (long)(e - ch * (int)AR_CHUNK) * 2;
+    bf16x8 o;
+    if (a.S == 0) {
+      o = *(const bf16x8*)((const bf16*)a.p + (long)t * D + e);
+    } else {
+      const float* src = (const float*)a.p + (long)t * D + e;
+      float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int s0 = 0; s0 < a.S; s0 += 4) {
+        f32x4 lo[4], hi[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {  // clamped, all in flight before the adds
+          const float* q = src + (long)min(s0 + i, a.S - 1) * a.slab;
+          lo[i] = *(const f32x4*)q;
+          hi[i] = *(const f32x4*)(q + 4);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float m = (s0 + i < a.S) ? 1.f : 0.f;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            acc[j] = fmaf(m, lo[i][j], acc[j]);
+            acc[j + 4] = fmaf(m, hi[i][j], acc[j + 4]);
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (bf16)acc[j];
+    }
+    *(bf16x8*)(own + AR_DATA + (long)par[k] * AR_SLOT + off[k]) = o;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  // 2./3. per channel c (thread c * 8 + q): signal peer q, then wait for peer q's epoch
+  const int c = tid >> 3, q = tid & 7;
+  const bool fl = c < nch && q < a.world && q != a.rank;
+  const int ep_c = (c < nch) ? counters[b0 + c] + 1 : 0;
+  if (fl) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int* pf = (int*)(a.bufs[q] + AR_FLAGS) + (b0 + c) * AR_MAXR + a.rank;
+    __hip_atomic_store(pf, ep_c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  if (fl) {
+    const int* f = (const int*)(own + AR_FLAGS) + (b0 + c) * AR_MAXR + q;
+    long spins = 0;
+    while (ar_load_flag(f) < ep_c) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > a.spin_limit) {
+        for (int r = 0; r < a.world; ++r)
+          __hip_atomic_store((int*)(a.bufs[r] + AR_ERR), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  // 4. rank-ordered sum (identical bits everywhere) + bias + residual; row statistics
+  float* rrow = a.residual + (long)t * D;
+  float s1 = 0.f;
+#pragma unroll
+  for (int k = 0; k < ARN_IT; ++k) {
+    const int e = 8 * (tid + AR_T * k);
+    if (e >= D) continue;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int r = 0; r < a.world; ++r) {
+      const bf16x8 x = *(const bf16x8*)(a.bufs[r] + AR_DATA + (long)par[k] * AR_SLOT + off[k]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += (float)x[j];
+    }
+    const f32x4 r0 = *(const f32x4*)(rrow + e), r1 = *(const f32x4*)(rrow + e + 4);
+    f32x4 b0v = {0.f, 0.f, 0.f, 0.f}, b1v = {0.f, 0.f, 0.f, 0.f};
+    if (a.bias) {
+      b0v = *(const f32x4*)(a.bias + e);
+      b1v = *(const f32x4*)(a.bias + e + 4);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v[k][j] = r0[j] + (acc[j] + b0v[j]);
+      v[k][j + 4] = r1[j] + (acc[j + 4] + b1v[j]);
+    }
+    *(f32x4*)(rrow + e) = f32x4{v[k][0], v[k][1], v[k][2], v[k][3]};
+    *(f32x4*)(rrow + e + 4) = f32x4{v[k][4], v[k][5], v[k][6], v[k][7]};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s1 += a.mode == 0 ? v[k][j] * v[k][j] : v[k][j];
+  }
+  float mean = 0.f, rstd;
+  if (a.mode == 0) {
+    rstd = rsqrtf(block_sum<AR_T>(s1, red) / (float)D + a.eps);
+  } else {
+    mean = block_sum<AR_T>(s1, red) / (float)D;
+    float s2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < ARN_IT; ++k) {
+      const int e = 8 * (tid + AR_T * k);
+      if (e >= D) continue;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s2 += (v[k][j] - mean) * (v[k][j] - mean);
+    }
+    rstd = rsqrtf(block_sum<AR_T>(s2, red) / (float)D + a.eps);
+  }
+  // 5. the next layer's normed input
+#pragma unroll
+  for (int k = 0; k < ARN_IT; ++k) {
+    const int e = 8 * (tid + AR_T * k);
+    if (e >= D) continue;
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float y = (v[k][j] - mean) * rstd * a.w[e + j];
+      if (a.nb) y += a.nb[e + j];
+      o[j] = (bf16)y;
+    }
+    *(bf16x8*)(a.out + (long)t * D + e) = o;
+  }
+  // 6. this row's channels advance one epoch
+  if (tid < nch) ((int*)(own + AR_COUNTER))[b0 + tid] = counters[b0 + tid] + 1;
+}
+
+// ----------------------------------------------------------------------------- two-shot// ----------------------------------------------------------------------------- two-shot
 // Reduce-scatter + all-gather over the same kind of peer-mapped region, for messages past the
 // one-shot's 256 K elements (decode rows of a wide TP batch: 256 x 4096 fp32 = 4 MiB; prefill
 // chunks up to 4 M elements).  One-shot makes every rank read all R copies of the message (R x n
@@ -303,6 +467,41 @@ extern "C" int la_allreduce_twoshot(const void* in, void* out, long n, int bf16,
                      nb);
   return (int)hipGetLastError();
 }
+// Fused decode layer boundary (allreduce_add_norm_kernel): M rows of D (D % 8 == 0, D <= 8192,
+// M * ceil(D / 1024) <= 256 channels) on the one-shot region `bufs`.
+extern "C" int la_allreduce_add_norm(const void* p, long slab, int S, int M, int D, int rank, int world,
+                                     const void* const* bufs, long spin_limit, void* residual, const void* bias,
+                                     const void* w, const void* nb, void* out, float eps, int mode, void* stream) {
+  using namespace la;
+  if (world < 1 || world > AR_MAXR || rank < 0 || rank >= world || M < 1 || D < 8 || (D & 7) ||
+      D > AR_T * 8 * ARN_IT || S < 0 || S > 64 || (S > 0 && slab < (long)M * D) || !p || !residual || !w || !out ||
+      (mode != 0 && mode != 1))
+    return -1;
+  const int nch = (D + (int)AR_CHUNK - 1) / (int)AR_CHUNK;
+  if ((long)M * nch > AR_MAXB) return -2;
+  ARNArgs a{};
+  a.p = p;
+  a.slab = slab;
+  a.S = S;
+  a.D = D;
+  a.rank = rank;
+  a.world = world;
+  a.spin_limit = spin_limit;
+  for (int r = 0; r < world; ++r) {
+    if (!bufs[r]) return -1;
+    a.bufs[r] = (uint8_t*)bufs[r];
+  }
+  a.residual = (float*)residual;
+  a.bias = (const float*)bias;
+  a.w = (const float*)w;
+  a.nb = (const float*)nb;
+  a.out = (bf16*)out;
+  a.eps = eps;
+  a.mode = mode;
+  hipLaunchKernelGGL(allreduce_add_norm_kernel, dim3(M), dim3(AR_T), 0, (hipStream_t)stream, a);
+  return (int)hipGetLastError();
+}
+
 extern "C" long la_ar_buffer_bytes() { return la::AR_DATA + 2 * la::AR_SLOT; }
 extern "C" long la_ar_max_elems() { return la::AR_MAXB * la::AR_CHUNK; }
 extern "C" long la_ar_err_offset() { return la::AR_ERR; }

@@ -64,6 +64,15 @@ LA_DEV u32x4 ldg16(const uint8_t* p) {
 //   mode 0: x = silu(g) * u with g = row[k], u = row[F + k] (SwiGLU, row width 2F)
 //   mode 1: x = gelu_tanh(row[k]);  mode 2: x = quick_gelu(row[k])      (row width F)
 //   mode 3: x = gelu_tanh(g) * u (GeGLU, row width 2F)
+//   mode 4 (GV_NORM): x = rmsnorm(res + sum(slabs) + bias) * nw over the whole row (width F = K):
+//     the residual-add + RMSNorm of the layer boundary (K2 + K14) folded into the consuming GEMV,
+//     so a batch-1/2 decode step has no add_norm launch between the down projection and the next
+//     q|k|v GEMV.  Every workgroup recomputes the row statistics (one 16-32 KiB row from L2, its
+//     loads in flight together with the first weight super-blocks); workgroup (0, 0) writes the
+//     updated residual to res_out (a different buffer: the other workgroups still read res).
+constexpr int GV_NORM = 4;
+constexpr int GV_NORM_IT = 8;  // float4 per thread per row: K <= 8192
+
 struct GVAct {
   const float* p;      // [S][M][W] fp32 slabs, W = 2F (mode 0) or F; null = plain bf16 x
   long slab;           // elements between slabs
@@ -71,13 +80,27 @@ struct GVAct {
   const float* bias;   // optional per-column bias of the gate|up output (length W)
   int mode, F;
   float scale = 1.f;   // x multiplied by this (an MoE routing weight: down(w x) = w down(x))
+  const float* res = nullptr;  // GV_NORM: fp32 residual [M][F]
+  float* res_out = nullptr;    // GV_NORM: residual + add, [M][F] (null: not written)
+  const float* nw = nullptr;   // GV_NORM: norm weight [F]
+  float eps = 0.f;
 };
 
+// x prologues that read fp32 sources (act / norm) issue the first weight loads before them
+LA_DEV bool gv_late(const GVAct& a) { return a.p != nullptr; }
+
+// every slab load issued before the first add (clamped index, masked add: no per-slab wait)
 LA_DEV float4 gv_sum_slabs(const GVAct& a, long idx, int col) {
-  float4 v = *(const float4*)(a.p + idx);
-  for (int s = 1; s < a.S; ++s) {
-    const float4 w = *(const float4*)(a.p + (long)s * a.slab + idx);
-    v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
+  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int s0 = 0; s0 < a.S; s0 += 4) {
+    float4 b[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) b[i] = *(const float4*)(a.p + (long)min(s0 + i, a.S - 1) * a.slab + idx);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float m = (s0 + i < a.S) ? 1.f : 0.f;
+      v.x = fmaf(m, b[i].x, v.x); v.y = fmaf(m, b[i].y, v.y); v.z = fmaf(m, b[i].z, v.z); v.w = fmaf(m, b[i].w, v.w);
+    }
   }
   if (a.bias) {
     const float4 b = *(const float4*)(a.bias + col);
@@ -111,9 +134,88 @@ LA_DEV void gv_act_x(const GVAct& a, int m, int k, float v[4]) {
 // Quantise x[m, k0 : k0+kper] into the LDS image (ggml q8_1 granularity: one scale per 32).
 // Wave w handles super-blocks w, w+4, ...; lane l owns elements 4l..4l+3 of the super-block,
 // so 8 lanes share a 32-block and 4 lanes a 16-run.
+// One 32-block of x (4 elements per lane, 8 lanes per block) into the int8 image.
+LA_DEV void gv_quant4(float v0, float v1, float v2, float v3, int l, int8_t* q, int* b, float* d) {
+  const float amax = group_max<8>(fmaxf(fmaxf(fabsf(v0), fabsf(v1)), fmaxf(fabsf(v2), fabsf(v3))));
+  const float inv = amax > 0.f ? 127.f / amax : 0.f;
+  const int q0 = __float2int_rn(v0 * inv), q1 = __float2int_rn(v1 * inv);
+  const int q2 = __float2int_rn(v2 * inv), q3 = __float2int_rn(v3 * inv);
+  *(uint32_t*)(q + 4 * l) = (uint32_t)(q0 & 0xFF) | ((uint32_t)(q1 & 0xFF) << 8) | ((uint32_t)(q2 & 0xFF) << 16) |
+                            ((uint32_t)(q3 & 0xFF) << 24);
+  int s = q0 + q1 + q2 + q3;
+  s += __shfl_xor(s, 1, 64);
+  s += __shfl_xor(s, 2, 64);
+  if ((l & 3) == 0) b[l >> 2] = s;
+  if ((l & 7) == 0) d[l >> 3] = amax / 127.f;
+}
+
+// GV_NORM prologue.  Thread (wave w, lane l) holds float4 chunks c = tid + 256 i of the row, which
+// is exactly super-block sb = w + 4 i, elements 4l..4l+3 -- the quantiser's own mapping -- so the
+// normed values go from registers to the int8 image with no LDS round trip; only the row's sum of
+// squares crosses the waves.
 template <int MT>
+LA_DEV void norm_quantize_x(const GVAct& a, int M, int k0, int kper, int8_t* xq, int* bs, float* dx) {
+  __shared__ float red[MT][GV_THREADS / 64];
+  const int tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
+  const int K = a.F, nv = K >> 2;
+  const bool wr = a.res_out && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0;
+  float v[MT][GV_NORM_IT][4];
+  float4 wgt[GV_NORM_IT];
+#pragma unroll
+  for (int i = 0; i < GV_NORM_IT; ++i) {
+    const int c = min(tid + GV_THREADS * i, nv - 1);
+    wgt[i] = *(const float4*)(a.nw + 4 * c);
+  }
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < GV_NORM_IT; ++i) {
+      const int c = tid + GV_THREADS * i;
+      v[m][i][0] = v[m][i][1] = v[m][i][2] = v[m][i][3] = 0.f;
+      if (m < M && c < nv) {
+        float4 r = *(const float4*)(a.res + (long)m * K + 4 * c);
+        if (a.p) {
+          const float4 s = gv_sum_slabs(a, (long)m * K + 4 * c, 4 * c);
+          r.x += s.x; r.y += s.y; r.z += s.z; r.w += s.w;
+        } else if (a.bias) {
+          const float4 b = *(const float4*)(a.bias + 4 * c);
+          r.x += b.x; r.y += b.y; r.z += b.z; r.w += b.w;
+        }
+        if (wr) *(float4*)(a.res_out + (long)m * K + 4 * c) = r;
+        v[m][i][0] = r.x; v[m][i][1] = r.y; v[m][i][2] = r.z; v[m][i][3] = r.w;
+        ss += r.x * r.x + r.y * r.y + r.z * r.z + r.w * r.w;
+      }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) ss += __shfl_xor(ss, o, 64);
+    if (l == 0) red[m][wv] = ss;
+  }
+  __syncthreads();
+  const int sb_lo = k0 >> 8, sb_hi = (k0 + kper) >> 8;
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    if (m >= M) break;
+    const float rstd = rsqrtf((red[m][0] + red[m][1] + red[m][2] + red[m][3]) / (float)K + a.eps);
+#pragma unroll
+    for (int i = 0; i < GV_NORM_IT; ++i) {
+      const int sb = wv + 4 * i;  // uniform per wave
+      if (sb < sb_lo || sb >= sb_hi) continue;
+      const int ls = sb - sb_lo;
+      gv_quant4(v[m][i][0] * rstd * wgt[i].x, v[m][i][1] * rstd * wgt[i].y, v[m][i][2] * rstd * wgt[i].z,
+                v[m][i][3] * rstd * wgt[i].w, l, xq + m * kper + ls * 256, bs + m * (kper >> 4) + ls * 16,
+                dx + m * (kper >> 5) + ls * 8);
+    }
+  }
+}
+
+template <int MT, int NM = 0>
 LA_DEV void quantize_x(const bf16* X, int ldx, const GVAct& act, int M, int k0, int kper, int8_t* xq, int* bs,
                        float* dx) {
+  if constexpr (NM && MT <= 2) {  // its own kernel instantiation (VAR bit 5): the row lives in VGPRs
+    norm_quantize_x<MT>(act, M, k0, kper, xq, bs, dx);
+    return;
+  }
   const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int nsb = kper >> 8;
   for (int m = 0; m < MT; ++m) {
@@ -262,7 +364,7 @@ LA_DEV void gv_store(const float (&acc)[MT][RS], const int (&n)[RS], int N, int 
   }
 }
 
-template <int MT, int NT, int EARLY, int RS, int PD = 0>
+template <int MT, int NT, int EARLY, int RS, int PD = 0, int NM = 0>
 LA_DEV void gv_q4k(const QW& w, int row0, const bf16* X, int ldx, const GVAct& act, int M, int kper, float* o,
                    int ldo, int col0,
                    int8_t* xq, int* bs, float* dx, const GVRope& rp) {
@@ -285,14 +387,13 @@ LA_DEV void gv_q4k(const QW& w, int row0, const bf16* X, int ldx, const GVAct& a
     sp[s] = w.p2 + nc * srow + (size_t)sb0 * 16 + 4 * j;
     dp[s] = w.p3 + nc * drow + (size_t)sb0 * 4;
   }
-  const bool staged = !EARLY && x_staged_ok<MT>(act, kper);
+  const bool staged = !EARLY && !NM && x_staged_ok<MT>(act, kper);
+  const bool late = EARLY || NM || gv_late(act);  // fused prologues: first weight round trip goes out first
   u32x2 xr[GV_XI];
   if (staged) x_issue<MT>(X, ldx, M, k0, kper, xr);
-  if constexpr (!EARLY) {
-    if (!staged) {
-      quantize_x<MT>(X, ldx, act, M, k0, kper, xq, bs, dx);
-      __syncthreads();
-    }
+  if (!staged && !late) {
+    quantize_x<MT, NM>(X, ldx, act, M, k0, kper, xq, bs, dx);
+    __syncthreads();
   }
   u32x4 qa[RS];
   uint32_t sa[RS], da[RS];
@@ -306,8 +407,8 @@ LA_DEV void gv_q4k(const QW& w, int row0, const bf16* X, int ldx, const GVAct& a
     x_commit<MT>(M, kper, xr, xq, bs, dx);
     __syncthreads();
   }
-  if constexpr (EARLY) {
-    quantize_x<MT>(X, ldx, act, M, k0, kper, xq, bs, dx);
+  if (late) {
+    quantize_x<MT, NM>(X, ldx, act, M, k0, kper, xq, bs, dx);
     __syncthreads();
   }
 
@@ -449,7 +550,7 @@ LA_DEV void gv_q4k(const QW& w, int row0, const bf16* X, int ldx, const GVAct& a
   gv_store<MT, RS>(acc, n, w.N, M, t, o, ldo, col0, rp);
 }
 
-template <int MT, int NT, int EARLY, int RS, int PD = 0>
+template <int MT, int NT, int EARLY, int RS, int PD = 0, int NM = 0>
 LA_DEV void gv_q6k(const QW& w, int row0, const bf16* X, int ldx, const GVAct& act, int M, int kper, float* o,
                    int ldo, int col0,
                    int8_t* xq, int* bs, float* dx, const GVRope& rp) {
@@ -477,14 +578,13 @@ LA_DEV void gv_q6k(const QW& w, int row0, const bf16* X, int ldx, const GVAct& a
     cp[s] = w.p2 + nc * crow + (size_t)sb0 * 16 + 8 * hh;
     dp[s] = w.p3 + nc * drow + (size_t)sb0 * 2;
   }
-  const bool staged = !EARLY && x_staged_ok<MT>(act, kper);
+  const bool staged = !EARLY && !NM && x_staged_ok<MT>(act, kper);
+  const bool late = EARLY || NM || gv_late(act);  // fused prologues: first weight round trip goes out first
   u32x2 xr[GV_XI];
   if (staged) x_issue<MT>(X, ldx, M, k0, kper, xr);
-  if constexpr (!EARLY) {
-    if (!staged) {
-      quantize_x<MT>(X, ldx, act, M, k0, kper, xq, bs, dx);
-      __syncthreads();
-    }
+  if (!staged && !late) {
+    quantize_x<MT, NM>(X, ldx, act, M, k0, kper, xq, bs, dx);
+    __syncthreads();
   }
   u32x4 la_[RS], ha[RS];
   u32x2 ca[RS];
@@ -500,8 +600,8 @@ LA_DEV void gv_q6k(const QW& w, int row0, const bf16* X, int ldx, const GVAct& a
     x_commit<MT>(M, kper, xr, xq, bs, dx);
     __syncthreads();
   }
-  if constexpr (EARLY) {
-    quantize_x<MT>(X, ldx, act, M, k0, kper, xq, bs, dx);
+  if (late) {
+    quantize_x<MT, NM>(X, ldx, act, M, k0, kper, xq, bs, dx);
     __syncthreads();
   }
 
@@ -649,7 +749,7 @@ LA_DEV void gv_q6k(const QW& w, int row0, const bf16* X, int ldx, const GVAct& a
 // (two 16-B loads), 8 v_dot4 against the int8 activation block, one scale product per block --
 // symmetric codes, so no 16-run sums.  Reference: ggml_vec_dot_q8_0_q8_0 [external, llama.cpp @
 // d5cb868 ggml/src/ggml-quants.c].
-template <int MT, int NT, int EARLY, int RS, int PD = 0>
+template <int MT, int NT, int EARLY, int RS, int PD = 0, int NM = 0>
 LA_DEV void gv_q8(const QW& w, int row0, const bf16* X, int ldx, const GVAct& act, int M, int kper, float* o,
                   int ldo, int col0, int8_t* xq, int* bs, float* dx, const GVRope& rp) {
   const int k0 = blockIdx.y * kper, nsb = kper >> 8, sb0 = k0 >> 8;
@@ -666,14 +766,13 @@ LA_DEV void gv_q8(const QW& w, int row0, const bf16* X, int ldx, const GVAct& ac
     qp[s] = w.p0 + nc * qrow + (size_t)sb0 * 256 + 32 * t;
     dp[s] = w.p1 + nc * drow + ((size_t)sb0 * 8 + t) * 2;
   }
-  const bool staged = !EARLY && x_staged_ok<MT>(act, kper);
+  const bool staged = !EARLY && !NM && x_staged_ok<MT>(act, kper);
+  const bool late = EARLY || NM || gv_late(act);  // fused prologues: first weight round trip goes out first
   u32x2 xr[GV_XI];
   if (staged) x_issue<MT>(X, ldx, M, k0, kper, xr);
-  if constexpr (!EARLY) {
-    if (!staged) {
-      quantize_x<MT>(X, ldx, act, M, k0, kper, xq, bs, dx);
-      __syncthreads();
-    }
+  if (!staged && !late) {
+    quantize_x<MT, NM>(X, ldx, act, M, k0, kper, xq, bs, dx);
+    __syncthreads();
   }
   // PD-deep register ring over 256-weight chunks (PD 0: a 2-deep double buffer)
   constexpr int D = PD > 0 ? PD : 2;
@@ -692,8 +791,8 @@ LA_DEV void gv_q8(const QW& w, int row0, const bf16* X, int ldx, const GVAct& ac
     x_commit<MT>(M, kper, xr, xq, bs, dx);
     __syncthreads();
   }
-  if constexpr (EARLY) {
-    quantize_x<MT>(X, ldx, act, M, k0, kper, xq, bs, dx);
+  if (late) {
+    quantize_x<MT, NM>(X, ldx, act, M, k0, kper, xq, bs, dx);
     __syncthreads();
   }
   float acc[MT][RS];
@@ -764,16 +863,16 @@ __global__ __launch_bounds__(GV_THREADS) void qgemv_dp4_kernel(GVArgs a, const b
   constexpr int RS = gv_rs<VAR>();
   const int row0 = (blk - (seg ? a.blk_end[seg - 1] : 0)) * (32 * RS);
   float* o = out + (size_t)blockIdx.y * slab;
-  constexpr int NT = VAR & 1, EARLY = (VAR >> 1) & 1, PD = (VAR & 16) ? 4 : 0;
+  constexpr int NT = VAR & 1, EARLY = (VAR >> 1) & 1, PD = (VAR & 16) ? 4 : 0, NM = (VAR >> 5) & 1;
   const bool fa = FA == FB || a.fmt[seg] == FA;
   if constexpr (FA == FMT_Q8_0) {  // Q8_0 launches are homogeneous (host-checked)
-    gv_q8<MT, NT, EARLY, RS, PD>(a.w[seg], row0, X, ldx, act, M, kper, o, ldo, a.col0[seg], xq, bs, dx, rp);
+    gv_q8<MT, NT, EARLY, RS, PD, NM>(a.w[seg], row0, X, ldx, act, M, kper, o, ldo, a.col0[seg], xq, bs, dx, rp);
   } else if (fa) {
-    if constexpr (FA == FMT_Q4_K) gv_q4k<MT, NT, EARLY, RS, PD>(a.w[seg], row0, X, ldx, act, M, kper, o, ldo, a.col0[seg], xq, bs, dx, rp);
-    else gv_q6k<MT, NT, EARLY, RS, PD>(a.w[seg], row0, X, ldx, act, M, kper, o, ldo, a.col0[seg], xq, bs, dx, rp);
+    if constexpr (FA == FMT_Q4_K) gv_q4k<MT, NT, EARLY, RS, PD, NM>(a.w[seg], row0, X, ldx, act, M, kper, o, ldo, a.col0[seg], xq, bs, dx, rp);
+    else gv_q6k<MT, NT, EARLY, RS, PD, NM>(a.w[seg], row0, X, ldx, act, M, kper, o, ldo, a.col0[seg], xq, bs, dx, rp);
   } else if constexpr (FA != FB) {
-    if constexpr (FB == FMT_Q4_K) gv_q4k<MT, NT, EARLY, RS, PD>(a.w[seg], row0, X, ldx, act, M, kper, o, ldo, a.col0[seg], xq, bs, dx, rp);
-    else gv_q6k<MT, NT, EARLY, RS, PD>(a.w[seg], row0, X, ldx, act, M, kper, o, ldo, a.col0[seg], xq, bs, dx, rp);
+    if constexpr (FB == FMT_Q4_K) gv_q4k<MT, NT, EARLY, RS, PD, NM>(a.w[seg], row0, X, ldx, act, M, kper, o, ldo, a.col0[seg], xq, bs, dx, rp);
+    else gv_q6k<MT, NT, EARLY, RS, PD, NM>(a.w[seg], row0, X, ldx, act, M, kper, o, ldo, a.col0[seg], xq, bs, dx, rp);
   }
 }
 
@@ -839,10 +938,14 @@ static int launch_gv(const GVArgs& a, int nblk, int K, const bf16* X, int ldx, c
   // 4-deep weight ring (VAR bit 4) of the default variant
   int var = (rp.q_out && g_gv_variant == 5) ? 21 : g_gv_variant;
   if ((var & 16) && ((kper >> 8) % 4)) var &= ~16;  // the ring walks whole groups of 4 super-blocks
+  if (act.mode == GV_NORM) {
+    if (MT > 2 || (var != 5 && var != 21)) return -4;
+    var |= 32;  // the fused-norm prologue's own instantiation
+  }
   switch (var) {
 #define GV_CASE(V) \
     case V: hipLaunchKernelGGL((qgemv_dp4_kernel<MT, FA, FB, V>), grid, dim3(GV_THREADS), lds, st, a, X, ldx, act, M, kper, out, ldo, slab, rp); break;
-    GV_CASE(0) GV_CASE(1) GV_CASE(2) GV_CASE(3) GV_CASE(5) GV_CASE(9) GV_CASE(21)
+    GV_CASE(0) GV_CASE(1) GV_CASE(2) GV_CASE(3) GV_CASE(5) GV_CASE(9) GV_CASE(21) GV_CASE(37) GV_CASE(53)
 #undef GV_CASE
     default: return -4;
   }
@@ -868,13 +971,19 @@ static int launch_gv_m(const GVArgs& a, int nblk, int K, const bf16* X, int ldx,
 static int qgemv_dp4_impl(int nseg, const int* fmts, const void* const* planes, const int* Ns, int K,
                           const void* X, int ldx, int M, int splits, void* out, int ldo, long slab,
                           const void* act_p, long act_slab, int act_S, const void* act_bias, int act_mode,
-                          void* stream, const la::GVRope& rp) {
+                          void* stream, const la::GVRope& rp, const la::GVAct* norm = nullptr) {
   using namespace la;
   if (nseg < 1 || nseg > GV_SEGS || M < 1 || M > 4 || (K & 255) || splits < 1 || ((K >> 8) % splits) ||
       slab < (long)M * ldo)
     return -1;
   GVAct act{(const float*)act_p, act_slab, act_S, (const float*)act_bias, act_mode, K};
-  if (act_p) {
+  if (norm) {
+    // fused residual-add + RMSNorm prologue: M <= 2, K <= 8192 (row in VGPRs), slabs optional
+    act = *norm;
+    if (M > 2 || K > GV_THREADS * GV_NORM_IT * 4 || !act.res || !act.nw || act.mode != GV_NORM || act.F != K ||
+        (act.p && (act.S < 1 || act.S > 16 || act.slab < (long)M * K)) || act.res_out == act.res)
+      return -1;
+  } else if (act_p) {
     if (act_S < 1 || act_S > 16 || act_mode < 0 || act_mode > 3 ||
         act_slab < (long)M * ((act_mode == 0 || act_mode == 3) ? 2L * K : (long)K))
       return -1;
@@ -945,6 +1054,45 @@ extern "C" int la_qgemv_dp4_rope(int nseg, const int* fmts, const void* const* p
   // out / slab are unused by the rope epilogue; pass a non-null dummy that passes the checks
   return qgemv_dp4_impl(nseg, fmts, planes, Ns, K, X, K, M, 1, q_out, W, (long)M * W, nullptr, 0, 0, nullptr, 0,
                         stream, rp);
+}
+
+// The same two launches with the layer-boundary residual-add + RMSNorm as their x prologue
+// (GV_NORM): x = rmsnorm(res + sum(add slabs) + add_bias) * nw, res_out = res + ... (written
+// once, by workgroup (0, 0); must not alias res).  add_p may be null (no add: the first layer).
+static la::GVAct gv_norm_args(int K, const void* res, const void* add_p, long add_slab, int add_S,
+                              const void* add_bias, const void* nw, float eps, void* res_out) {
+  la::GVAct a{(const float*)add_p, add_slab, add_S, (const float*)add_bias, la::GV_NORM, K};
+  a.res = (const float*)res;
+  a.res_out = (float*)res_out;
+  a.nw = (const float*)nw;
+  a.eps = eps;
+  return a;
+}
+
+extern "C" int la_qgemv_dp4_norm(int nseg, const int* fmts, const void* const* planes, const int* Ns, int K, int M,
+                                 int splits, void* out, int ldo, long slab, const void* res, const void* add_p,
+                                 long add_slab, int add_S, const void* add_bias, const void* nw, float eps,
+                                 void* res_out, void* stream) {
+  la::GVRope rp{};
+  const la::GVAct na = gv_norm_args(K, res, add_p, add_slab, add_S, add_bias, nw, eps, res_out);
+  return qgemv_dp4_impl(nseg, fmts, planes, Ns, K, nullptr, K, M, splits, out, ldo, slab, nullptr, 0, 0, nullptr, 0,
+                        stream, rp, &na);
+}
+
+extern "C" int la_qgemv_dp4_rope_norm(int nseg, const int* fmts, const void* const* planes, const int* Ns, int K,
+                                      int M, const int* pos, const int* slots, const float* cos_sin, int Hq, int Hkv,
+                                      int Dh, void* q_out, void* kc, void* vc, int BS, const void* res,
+                                      const void* add_p, long add_slab, int add_S, const void* add_bias,
+                                      const void* nw, float eps, void* res_out, void* stream) {
+  if (!q_out || !kc || !vc || !pos || !slots || !cos_sin || (Dh & 1) || Dh < 2 || BS < 8 || (BS & 7)) return -1;
+  if ((K >> 8) % 4) return -1;
+  int W = 0;
+  for (int i = 0; i < nseg; ++i) W += Ns[i];
+  if (W != (Hq + 2 * Hkv) * Dh) return -1;
+  la::GVRope rp{pos, slots, cos_sin, (__bf16*)q_out, (__bf16*)kc, (__bf16*)vc, Hq, Hkv, Dh, BS};
+  const la::GVAct na = gv_norm_args(K, res, add_p, add_slab, add_S, add_bias, nw, eps, res_out);
+  return qgemv_dp4_impl(nseg, fmts, planes, Ns, K, nullptr, K, M, 1, q_out, W, (long)M * W, nullptr, 0, 0, nullptr, 0,
+                        stream, rp, &na);
 }
 
 // MoE decode GEMV (see moe_gemv_kernel): fmt / N / K shared by the E_local experts of `qws`

@@ -21,6 +21,9 @@ import torch
 
 log = logging.getLogger("localai_amd.custom_ar")
 
+# decode layer boundaries as one fused all-reduce + residual + norm launch (CustomAllReduce.add_norm)
+FUSED_ADD_NORM = os.environ.get("LOCALAI_AMD_AR_ADD_NORM", "1") == "1"
+
 HIP_IPC_HANDLE_SIZE = 64
 _hipIpcMemLazyEnablePeerAccess = 0x1
 
@@ -69,6 +72,12 @@ class CustomAllReduce:
                                            ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_long,
                                            ctypes.c_void_p] + ([ctypes.c_int] if "twoshot" in f else [])
             getattr(self.L, f).restype = ctypes.c_int
+        self.L.la_allreduce_add_norm.argtypes = [ctypes.c_void_p, ctypes.c_long, ctypes.c_int, ctypes.c_int,
+                                                 ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                                 ctypes.c_long, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                 ctypes.c_void_p, ctypes.c_void_p, ctypes.c_float, ctypes.c_int,
+                                                 ctypes.c_void_p]
+        self.L.la_allreduce_add_norm.restype = ctypes.c_int
         if twoshot is None:
             twoshot = os.environ.get("LOCALAI_AMD_AR_TWOSHOT", "1") != "0"
         self.max_elems = int(self.L.la_ar_max_elems())          # one-shot: latency-bound decode rows
@@ -170,6 +179,38 @@ class CustomAllReduce:
         if rc != 0:
             raise RuntimeError(f"la_allreduce_{'twoshot' if two else 'oneshot'} failed with code {rc}")
         return t
+
+    ADD_NORM_CHANNELS = 256   # one-shot channels (1024 elements each) a fused call may span
+
+    def supports_add_norm(self, M: int, D: int) -> bool:
+        """The fused all-reduce + residual + norm kernel takes M rows of D: D % 8 == 0, D <= 8192,
+        every row on its own one-shot channels (M * ceil(D / 1024) <= 256)."""
+        return (FUSED_ADD_NORM and 1 <= M and 8 <= D <= 8192 and D % 8 == 0
+                and M * -(-D // 1024) <= self.ADD_NORM_CHANNELS)
+
+    def add_norm(self, part, bias, residual: torch.Tensor, weight: torch.Tensor, nbias, eps: float,
+                 mode: int) -> torch.Tensor:
+        """residual += all_reduce(part) (+ bias); return norm(residual) * weight (+ nbias) as bf16 --
+        the decode layer boundary of a TP group in one launch (allreduce.hip
+        allreduce_add_norm_kernel).  `part` is this rank's un-reduced ops.Partial (fp32 slabs or one
+        bf16 matrix); every rank gets identical bits (rank-ordered fp32 sum of the bf16 wire rows)."""
+        M, D = residual.shape
+        t = part.t
+        if t.dim() == 3:
+            S, slab = t.shape[0], t.shape[1] * t.shape[2]
+            assert t.dtype == torch.float32 and t.is_contiguous()
+        else:
+            S, slab = 0, 0
+            assert t.dtype == torch.bfloat16 and t.is_contiguous()
+        out = torch.empty(M, D, dtype=torch.bfloat16, device=residual.device)
+        fp = lambda x: None if x is None else x.data_ptr()  # noqa: E731
+        rc = self.L.la_allreduce_add_norm(t.data_ptr(), slab, S, M, D, self.rank, self.world, self._bufs[0],
+                                          self.SPIN_LIMIT, residual.data_ptr(), fp(bias), weight.data_ptr(),
+                                          fp(nbias), out.data_ptr(), float(eps), int(mode),
+                                          torch.cuda.current_stream(self.device).cuda_stream)
+        if rc != 0:
+            raise RuntimeError(f"la_allreduce_add_norm failed with code {rc}")
+        return out
 
     def timed_out(self) -> bool:
         """True if a wait ever hit the spin limit (a peer never arrived): results since are suspect."""

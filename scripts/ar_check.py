@@ -70,6 +70,48 @@ def main():
             ref = expected(world, n, dt, dev, 100 + 10 * rep + i)
             assert (bufs[i].float() - ref.float()).abs().max().item() == 0.0, (rank, "graph", rep, i)
     assert not car.timed_out()
+    # fused all-reduce + bias + residual + norm (CustomAllReduce.add_norm), interleaved with plain
+    # one-shot calls on the same channels: residual exact, normed row within bf16 rounding
+    def an_case(call, M, D, S, mode, with_bias):
+        g0 = torch.Generator().manual_seed(5000 + call)            # shared by all ranks
+        res = torch.randn(M, D, generator=g0)
+        w = torch.rand(D, generator=g0) + 0.5
+        nb = torch.randn(D, generator=g0) * 0.1 if mode == 1 else None
+        bias = torch.randn(D, generator=g0) * 0.1 if with_bias else None
+        tot = torch.zeros(M, D)
+        for r in range(world):
+            gr = torch.Generator().manual_seed(6000 + 10 * call + r)
+            loc = torch.randn(max(S, 1), M, D, generator=gr)
+            acc = loc[0].clone()
+            for k in range(1, S):
+                acc = acc + loc[k]                                 # the kernel's slab order
+            wire = acc.to(torch.bfloat16)
+            tot += wire.float()
+            if r == rank:
+                part = ops.Partial(loc.to(dev) if S else wire.to(dev))
+        ref_res = res + (tot + (bias if bias is not None else 0.0))
+        if mode == 0:
+            ref = ref_res * torch.rsqrt(ref_res.pow(2).mean(-1, keepdim=True) + 1e-5) * w
+        else:
+            mu = ref_res.mean(-1, keepdim=True)
+            ref = (ref_res - mu) * torch.rsqrt((ref_res - mu).pow(2).mean(-1, keepdim=True) + 1e-5) * w + nb
+        rd = res.to(dev)
+        out = car.add_norm(part, None if bias is None else bias.to(dev), rd, w.to(dev),
+                           None if nb is None else nb.to(dev), 1e-5, mode)
+        torch.cuda.synchronize()
+        assert torch.allclose(rd.cpu(), ref_res, rtol=0, atol=1e-5), (rank, "add_norm residual", call)
+        err = (out.float().cpu() - ref).abs().max().item()
+        assert err < 2e-2 * max(1.0, ref.abs().max().item()), (rank, "add_norm out", call, err)
+    from localai_amd import ops
+    an_case(0, 1, 4096, 3, 0, True)
+    t = inputs(rank, 3 * 4096, torch.float32, dev, 40)          # one-shot on overlapping channels
+    car.all_reduce(t)
+    an_case(1, 3, 256, 0, 1, False)
+    an_case(2, 2, 8192, 9, 0, False)
+    an_case(3, 64, 4096, 1, 0, True)
+    torch.cuda.synchronize()
+    assert (t.float() - expected(world, 3 * 4096, torch.float32, dev, 40).float()).abs().max().item() == 0.0
+    assert not car.timed_out()
     # latency of one decode row (same-GPU numbers say nothing about xGMI; recorded for reference)
     t = inputs(rank, 4096, torch.float32, dev, 7)
     dist.barrier()

@@ -132,6 +132,63 @@ def test_headline_path_against_fp32_oracle(tmp_path):
     assert exact >= 0.75 * n and worst < 0.05, (exact, n, worst)
 
 
+def _b1_oracle_error(p, n_req, fused_flag, monkeypatch):
+    """(min cosine, max rel-L2, fused?) of every sampled logits row of a batch-n_req decode vs the
+    fp32 oracle, with the fused-norm q|k|v GEMV on or off."""
+    from localai_amd import ops
+    monkeypatch.setattr(ops, "GEMV_NORM", fused_flag)
+    fused = []
+    orig = ops.qkv_rope_dp4
+
+    def spy(x, *a, **k):
+        fused.append(isinstance(x, ops.NormIn))
+        return orig(x, *a, **k)
+    monkeypatch.setattr(ops, "qkv_rope_dp4", spy)
+    eng = LLMEngine(EngineConfig(model_path=p, device="cuda:0", context_size=256, max_num_seqs=4,
+                                 max_batched_tokens=1024, decode_steps=8, record_tokens=True, record_logits=True))
+    prompts = [f"fused norm check {i} " + "word " * (3 * i) for i in range(n_req)]
+    got, rows_of = {}, {}
+
+    def mk(i):
+        def cb(ev):
+            if ev.finished:
+                got[i], rows_of[i] = ev.token_ids, ev.logits
+        return cb
+    for i, pr in enumerate(prompts):
+        eng.add_request(pr, SamplingParams(max_tokens=10, temperature=0.0, ignore_eos=True), mk(i))
+    while len(got) < n_req:
+        eng.step()
+    min_cos, max_rel = 1.0, 0.0
+    for i in range(n_req):
+        ids = eng.tokenize(prompts[i])
+        ref = eng.model.reference_logits(ids + got[i][:-1]).float()
+        for j in range(len(got[i])):
+            row = ref[len(ids) - 1 + j]
+            mine = rows_of[i][j].to(row.device)
+            min_cos = min(min_cos, float(torch.nn.functional.cosine_similarity(mine, row, dim=0)))
+            max_rel = max(max_rel, float((mine - row).norm() / row.norm()))
+    monkeypatch.setattr(ops, "qkv_rope_dp4", orig)
+    return min_cos, max_rel, bool(fused) and all(fused)
+
+
+@pytest.mark.parametrize("n_req", [1, 2])
+def test_batch1_fused_norm_decode_against_fp32_oracle(tmp_path, monkeypatch, n_req):
+    """Batch-1/2 decode on Llama-3-8B layer shapes: every layer boundary's residual-add + RMSNorm
+    runs inside the fused q|k|v GEMV (ops.NormIn, no add_norm launch).  Every sampled logits row
+    against the fp32 oracle: cosine >= 0.999, and relative L2 no worse than the unfused batch-1
+    path's (both carry the int8 activation rounding of the dp4 GEMV, ~2 % rel-L2)."""
+    from localai_amd.models import synth
+    p = str(tmp_path / "l3-2l.gguf")
+    synth.write_model(p, "llama3-8b-2l")
+    c0, r0, f0 = _b1_oracle_error(p, n_req, False, monkeypatch)
+    c1, r1, f1 = _b1_oracle_error(p, n_req, True, monkeypatch)
+    print(f"batch {n_req} vs fp32 oracle: unfused min cos {c0:.5f} max rel {r0:.4f}; "
+          f"fused min cos {c1:.5f} max rel {r1:.4f}")
+    assert f1 and not f0, "the fused-norm q|k|v GEMV did not run (or ran with the flag off)"
+    assert c1 >= 0.999 and c0 >= 0.999, (c0, c1)
+    assert r1 <= max(2.5e-2, 1.15 * r0), (r0, r1)
+
+
 def test_mixtral_moe_wide_batch_graph_decode(tmp_path):
     """Decode batches past 64 tokens run the row-chunked grouped expert GEMM inside the captured
     graph (no per-expert host loop): 100 concurrent requests, multi-step == single-step, and a

@@ -129,3 +129,29 @@ def test_gemv_splits_fit_lds(K, M):
     assert nsb % S == 0
     kper = K // S
     assert mt * (kper + kper // 16 * 4 + kper // 32 * 4) <= 64 * 1024
+
+
+def test_norm_in_prologue_mapping_and_materialize():
+    """GV_NORM prologue (gemv_dp4.hip norm_quantize_x): thread tid's float4 chunk c = tid + 256 i is
+    super-block w + 4 i, elements 4l..4l+3 -- the quantiser's own lane mapping -- for every split
+    range; and NormIn.materialize() (the non-fused fallback) gives add_norm's x with the updated
+    residual in res_out and res itself updated in place."""
+    K = 4096
+    for tid in range(256):
+        wv, l = tid >> 6, tid & 63
+        for i in range(8):
+            c = tid + 256 * i
+            sb, within = divmod(4 * c, 256)
+            assert (sb, within) == (wv + 4 * i, 4 * l)
+    g = torch.Generator().manual_seed(0)
+    res = torch.randn(2, K, generator=g)
+    add = ops.Partial(torch.randn(3, 2, K, generator=g))
+    w = torch.rand(K, generator=g) + 0.5
+    out = torch.empty_like(res)
+    nin = ops.NormIn(res.clone(), add, w, 1e-5, out)
+    x = nin.materialize()
+    r = res + add.t.sum(0)
+    ref = r * torch.rsqrt(r.pow(2).mean(-1, keepdim=True) + 1e-5) * w
+    assert torch.allclose(out, r, atol=1e-5) and torch.allclose(nin.res, r, atol=1e-5)
+    assert torch.allclose(x.float(), ref, rtol=1e-2, atol=1e-2)
+    assert not ops.norm_in_ok(res, add, w, None)  # CPU tensors: never the fused path

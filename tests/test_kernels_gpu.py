@@ -631,6 +631,51 @@ def test_qkv_rope_dp4_fused(M):
     assert kc.abs().sum().item() > 0 and vc.abs().sum().item() > 0
 
 
+@pytest.mark.parametrize("M,S", [(1, 0), (1, 3), (2, 8), (2, 11)])
+def test_qkv_rope_dp4_fused_norm(M, S):
+    """The layer-boundary residual-add + RMSNorm folded into the fused q|k|v GEMV's prologue
+    (ops.NormIn, gemv_dp4.hip GV_NORM) vs add_norm + the same GEMV: q, the appended K/V, and the
+    updated residual (written to the other buffer; S = 0: no add, nothing written)."""
+    Hq, Hkv, Dh, BS, K, nblk = 8, 2, 128, 32, 4096, 4
+    qk = _qw((Hq + Hkv) * Dh, K, GGMLType.Q4_K, seed=33)
+    v = _qw(Hkv * Dh, K, GGMLType.Q6_K, seed=34)
+    g = torch.Generator().manual_seed(5)
+    res = (torch.randn(M, K, generator=g) * 2).to(DEV)
+    add = ops.Partial((torch.randn(S, M, K, generator=g) * 0.5).to(DEV)) if S else None
+    w = (1 + 0.1 * torch.randn(K, generator=g)).to(DEV)
+    cs = ops.rope_cos_sin(512, Dh, 500000.0, DEV)
+    pos = torch.tensor([37, 200][:M], dtype=torch.int32, device=DEV)
+    slots = torch.tensor([45, 77][:M], dtype=torch.int32, device=DEV)
+    kc, vc = torch.zeros(nblk, Hkv, BS, Dh, dtype=torch.bfloat16, device=DEV), ops.v_pages(nblk, Hkv, BS, Dh, device=DEV)
+    res_out = torch.full_like(res, float("nan")) if S else None
+    nin = ops.NormIn(res.clone(), add, w, 1e-5, res_out)
+    assert ops.norm_in_ok(nin.res, add, w, None)
+    q = ops.qkv_rope_dp4(nin, [qk, v], pos, slots, cs, Hq, Hkv, Dh, kc, vc, BS)
+    r2 = res.clone()
+    xn = ops.add_norm(r2, add, w, None, 1e-5, 0)
+    kr, vr = torch.zeros_like(kc), torch.zeros_like(vc)
+    qr = ops.qkv_rope_dp4(xn, [qk, v], pos, slots, cs, Hq, Hkv, Dh, kr, vr, BS)
+    torch.cuda.synchronize()
+    assert torch.equal(nin.res, res), "the input residual must not be written"
+    if S:
+        assert torch.allclose(res_out, r2, rtol=1e-6, atol=1e-5)
+    # x differs only by the bf16 rounding of xn on the unfused path (int8 image of the same values)
+    tol = 2e-2 * max(1.0, qr.float().abs().max().item())
+    assert (q.float() - qr.float()).abs().max().item() < tol
+    assert (kc.float() - kr.float()).abs().max().item() < tol
+    assert (vc.float() - vr.float()).abs().max().item() < tol
+    # and against the fp32 reference of the whole op
+    x32 = r2.cpu()
+    x32 = x32 * torch.rsqrt(x32.pow(2).mean(-1, keepdim=True) + 1e-5) * w.cpu()
+    ref = torch.cat([x32 @ qk.ref.t(), x32 @ v.ref.t()], -1)[:, :Hq * Dh].view(M, Hq, Dh)
+    c, s_ = cs.cpu()[pos.long().cpu()][..., 0], cs.cpu()[pos.long().cpu()][..., 1]
+    r0, r1 = ref[..., 0::2].clone(), ref[..., 1::2].clone()
+    ref[..., 0::2] = r0 * c[:, None] - r1 * s_[:, None]
+    ref[..., 1::2] = r0 * s_[:, None] + r1 * c[:, None]
+    rel = (q.float().cpu() - ref).norm() / ref.norm()
+    assert rel < 2e-2, rel
+
+
 @pytest.mark.parametrize("T", [1, 5])
 def test_moe_grouped_gemm_expert_parallel(T):
     """Expert-parallel grouping: this rank holds experts 0..El-1; picks of other ranks' experts are
