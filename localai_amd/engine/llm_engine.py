@@ -184,6 +184,7 @@ class LLMEngine:
         self._gepoch = 0                                 # bumped whenever a mask slot is reused
         self._ghit: Dict[str, float] = {}                # per grammar: EMA of learned-transition hits
         self._gexpanded: set = set()                     # slots whose outgoing transitions are all learned
+        self._gexp_pend: dict = {}                       # slot -> background expansion in flight
         self._gmask_np: Dict[int, np.ndarray] = {}       # host copies of the pool's masks (run-ahead)
         self._mm_embs: Dict[int, list] = {}  # inbox "mm" item -> its images' embeddings (batched encode)
         self.clip = None
@@ -791,7 +792,7 @@ class LLMEngine:
             if r.n_gen == 0 or self._needs_host_sampler(r):
                 why["prefill" if r.n_gen == 0 else "host_sampler"] += 1
                 return 1  # prefill in flight, or a host-side sampler feature
-            if r.grammar is not None and not self._grammar_ready(r):
+            if r.grammar is not None and not self._grammar_ready(r) and not self._gready(r):
                 if not self._grammar_slot_cached(r):
                     why["grammar_no_mask"] += 1
                     return 1  # a parse state without a device mask: the host walks it first
@@ -927,6 +928,8 @@ class LLMEngine:
             # rows whose parse state has a cached device mask are masked inside the graph, so
             # their sample is valid as drawn; the rest are checked and fixed up after the step
             V = logits.shape[1]
+            if self._gexp_pend:
+                self._gexpand_poll(V)
             gslot = np.full(B, -1, dtype=np.int32)
             done_rows, grows = [], []
             epoch0 = self._gepoch
@@ -936,10 +939,10 @@ class LLMEngine:
                     sl = self._grammar_mask_slot(r, V, self.device)
                     if sl is not None and sl >= 0:
                         gslot[j] = sl
-                        if self.cfg.grammar_run_ahead or K > 1:
-                            # run-ahead, or a rider in a mostly-plain multi-step run: learn the
-                            # state's transitions at once so the row does not park after one token
-                            self._gexpand(r.params.grammar, r.grammar, sl, V)
+                        # learn the state's transitions at once (inline, or on the helper
+                        # thread for permissive states): a row in a fully learned state rides
+                        # multi-step runs without parking (_gready), at any batch mix
+                        self._gexpand(r.params.grammar, r.grammar, sl, V)
                     elif sl is not None:
                         done_rows.append(j)
             if K > 1 and (done_rows or any(gslot[j] < 0 for j in grows) or epoch0 != self._gepoch):
@@ -1375,6 +1378,7 @@ class LLMEngine:
             self._gpend.clear()
             self._gdev.clear()
             self._gexpanded.clear()
+            self._gexp_pend.clear()
             self._gmask_np.clear()
         return pool
 
@@ -1384,6 +1388,7 @@ class LLMEngine:
         self._gepoch += 1
         self._gnext[slot].fill_(-2)
         self._gexpanded.discard(slot)
+        self._gexp_pend.pop(slot, None)
         self._gmask_np.pop(slot, None)
         for st_t in self._gtrans_in.pop(slot, ()):
             self._gtrans.pop(st_t, None)
@@ -1419,43 +1424,77 @@ class LLMEngine:
         g = r.params.grammar
         self._ghit[g] = 0.95 * self._ghit.get(g, 0.0) + (0.05 if hit else 0.0)
 
-    GRAMMAR_EXPAND_MAX = 20000   # allowed tokens up to which a state's transitions are precomputed
+    GRAMMAR_EXPAND_MAX = 20000   # allowed tokens up to which a state's transitions are learned inline
+    # permissive states (`[a-z ]+`, the inside of a JSON string: 10^4-10^5 allowed tokens) are
+    # expanded too, their successor keys computed on the helper thread (the native pass releases
+    # the GIL) and applied in bulk when ready; until then the row learns per token as before
+    GRAMMAR_EXPAND_BG = os.environ.get("LOCALAI_AMD_GRAMMAR_EXPAND_BG", "1") == "1"
 
     def _gexpand(self, gtext: str, gs, s: int, V: int):
         """Learn every transition out of slot s at once: the key of the state after each allowed
         token (one native pass), one mask per distinct successor.  A state like `[a-z ]+`
         (self-loop) or an enum position of a JSON schema is then fully known to the device
-        table, so constrained rows do not park there.  Permissive states (most of the
-        vocabulary allowed) are left to the per-token learning."""
-        if s in self._gexpanded:
+        table, so constrained rows do not park there (_gready: such a row is no rider)."""
+        if s in self._gexpanded or s in self._gexp_pend:
             return
-        self._gexpanded.add(s)
         m = self._gmask_np.get(s)
         if m is None:
+            self._gexpanded.add(s)
             return
         toks = np.nonzero(m)[0].astype(np.int32)
-        if len(toks) == 0 or len(toks) > self.GRAMMAR_EXPAND_MAX:
+        if len(toks) == 0:
+            self._gexpanded.add(s)
             return
-        keys = gs.next_keys(toks)
-        epoch = self._gepoch
-        groups: Dict[int, list] = {}
-        for t, k in zip(toks.tolist(), keys.tolist()):
-            if k:
-                groups.setdefault(k, []).append(t)
-        for k, ts in groups.items():
+        if len(toks) > self.GRAMMAR_EXPAND_MAX:
+            if self.GRAMMAR_EXPAND_BG and self.tp.world == 1:
+                if self._gmask_bg is None:
+                    import concurrent.futures
+                    self._gmask_bg = concurrent.futures.ThreadPoolExecutor(1, thread_name_prefix="gmask")
+                g = gs.clone()
+                self._gexp_pend[s] = (self._gmask_bg.submit(g.next_keys, toks), toks, gtext, g, self._gepoch)
+            else:
+                self._gexpanded.add(s)   # tensor-parallel ranks: per-token learning (same on every rank)
+            return
+        self._gexpand_apply(s, toks, gs.next_keys(toks), gtext, gs, self._gepoch, V)
+
+    def _gexpand_poll(self, V: int):
+        """Apply the background expansions that finished (called once per constrained step)."""
+        for s in [s for s, e in self._gexp_pend.items() if e[0].done()]:
+            fut, toks, gtext, gs, epoch = self._gexp_pend.pop(s)
+            if epoch == self._gepoch:
+                self._gexpand_apply(s, toks, fut.result(), gtext, gs, epoch, V)
+
+    def _gexpand_apply(self, s: int, toks: np.ndarray, keys: np.ndarray, gtext: str, gs, epoch: int, V: int):
+        """Every transition out of slot s, grouped by successor key: one successor slot per key,
+        then the (s, t) -> s2 entries in bulk (host tables + one device index_put per key)."""
+        uk, inv = np.unique(keys, return_inverse=True)
+        for i, k in enumerate(uk.tolist()):
+            if not k:
+                continue
+            ts = toks[inv == i]
             if (gtext, k) in self._gmask_cache:
                 s2 = self._gmask_cache[(gtext, k)]
             else:
                 g2 = gs.clone()
-                if not g2.accept(ts[0]):
+                if not g2.accept(int(ts[0])):
                     continue
                 s2 = self._state_slot(gtext, g2, V, self.device, key=k)
             if epoch != self._gepoch:   # a slot was reused meanwhile: s may name another state
-                self._gexpanded.discard(s)
                 return
-            for t in ts:
-                if (s, t) not in self._gtrans:
-                    self._gtrans_learn(s, t, s2)
+            pairs = [(s, t) for t in ts.tolist()]
+            self._gtrans.update(dict.fromkeys(pairs, s2))
+            if s2 is not None and s2 >= 0:
+                self._gtrans_in.setdefault(s2, set()).update(pairs)
+                self._gdev.update(pairs)
+                self._gnext[s, torch.from_numpy(ts.astype(np.int64)).to(self._gnext.device)] = s2
+        self._gexpanded.add(s)
+
+    def _gready(self, r) -> bool:
+        """r's parse state has a device mask whose every transition is learned: it cannot park in
+        this state, so it rides a multi-step run without shortening it (it may still park at a
+        successor state it has not seen before)."""
+        s = self._gmask_cache.get((r.params.grammar, r.grammar.key()))
+        return s is not None and s >= 0 and s in self._gexpanded
 
     def _grammar_ready(self, r) -> bool:
         """r can run ahead inside a multi-step graph run: its parse state has a device mask and

@@ -45,7 +45,20 @@ class DiffusersServicer:
         from ..models.sd3 import SD3Pipeline, is_sd3_pipeline
         path = request.ModelFile or request.Model
         from ..models import sd_single_file as ssf
-        if ssf.is_single_file(path):
+        flux_file = None
+        if str(request.PipelineType or "") == "FluxTransformer2DModel":
+            # backend.py:255-269: the transformer from the single file, everything else from
+            # BFL_REPO (here a local diffusers FLUX directory: there is no hub to fetch from)
+            base = os.environ.get("BFL_REPO", "")
+            if not os.path.isabs(base) and base:
+                base = os.path.join(os.path.dirname(os.path.abspath(path)), base)
+            if not ssf.is_single_file(path):
+                return pb.Result(success=False, message=f"FluxTransformer2DModel needs a single-file transformer: {path}")
+            if not (base and is_flux_pipeline(base)):
+                return pb.Result(success=False, message="FluxTransformer2DModel: set BFL_REPO to a local diffusers "
+                                                        f"FLUX pipeline directory (got {base!r})")
+            flux_file, path = path, base
+        elif ssf.is_single_file(path):
             # backend.py:184-191: a local file is a from_single_file checkpoint (SD 1.x / 2.x / XL)
             clip = str(request.CLIPModel or "")
             if clip and not os.path.isabs(clip):
@@ -79,7 +92,7 @@ class DiffusersServicer:
         try:
             if flux:  # backend.py:247-251: FluxPipeline; GenerateImage adds max_sequence_length=256
                 p = await asyncio.get_running_loop().run_in_executor(
-                    None, lambda: FluxPipeline(path, dev, max_sequence_length=256))
+                    None, lambda: FluxPipeline(path, dev, max_sequence_length=256, transformer_file=flux_file))
             elif sd3:  # backend.py:235-246: StableDiffusion3Pipeline
                 p = await asyncio.get_running_loop().run_in_executor(
                     None, lambda: SD3Pipeline(path, dev, clip_skip=int(request.CLIPSkip or 0)))

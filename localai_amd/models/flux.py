@@ -250,7 +250,11 @@ def is_flux_pipeline(path: str) -> bool:
 
 
 class FluxPipeline:
-    def __init__(self, path: str, device: str = "cpu", max_sequence_length: int = 256):
+    def __init__(self, path: str, device: str = "cpu", max_sequence_length: int = 256,
+                 transformer_file: Optional[str] = None):
+        """path: a diffusers FLUX directory; transformer_file: a single-file transformer (BFL
+        layout, models/flux_single_file.py) replacing path/transformer (pipeline_type
+        FluxTransformer2DModel, reference backend.py:255-269)."""
         from transformers import CLIPTokenizer, PreTrainedTokenizerFast
 
         from .musicgen import T5Encoder
@@ -263,9 +267,14 @@ class FluxPipeline:
                                          "layer_norm_epsilon")}
         w2 = {k: v.to(self.device, self.dtype) for k, v in _load_weights(os.path.join(path, "text_encoder_2")).items()}
         self.t5 = T5Encoder(w2, self.t5_hp, prefix="")
-        tc = _cfg(os.path.join(path, "transformer", "config.json"))
+        if transformer_file:
+            from .flux_single_file import load_transformer_file
+            tc, tw = load_transformer_file(transformer_file, path)
+        else:
+            tc = _cfg(os.path.join(path, "transformer", "config.json"))
+            tw = _load_weights(os.path.join(path, "transformer"))
         self.tr = FluxTransformer(tc)
-        self.tr.load_state_dict(_load_weights(os.path.join(path, "transformer")), strict=True)
+        self.tr.load_state_dict(tw, strict=True)
         vc = _cfg(os.path.join(path, "vae", "config.json"))
         self.vae = VaeDecoder(vc)
         self.vae.load_state_dict(_vae_names(_load_weights(os.path.join(path, "vae"))), strict=True)

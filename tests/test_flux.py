@@ -98,6 +98,60 @@ def test_flux_through_diffusers_backend(flux_dir, tmp_path):
     asyncio.run(go())
 
 
+def test_bfl_single_file_mapping_is_exact_inverse(flux_dir):
+    """BFL layout <-> diffusers names: fused q|k|v (double blocks), fused q|k|v|mlp (single
+    blocks), final adaLN halves swapped; every tensor mapped, the round trip bit-exact, and the
+    config inferred from the shapes equals the pipeline's transformer config."""
+    from localai_amd.models import flux_single_file as fsf
+    from localai_amd.models.sd import _cfg, _load_weights
+    sd = _load_weights(os.path.join(flux_dir, "transformer"))
+    bfl = fsf.diffusers_to_bfl(sd)
+    assert fsf.is_bfl(bfl) and "double_blocks.0.img_attn.qkv.weight" in bfl and "single_blocks.1.linear1.bias" in bfl
+    assert "final_layer.adaLN_modulation.1.weight" in bfl and "guidance_in.in_layer.weight" in bfl
+    d = sd["x_embedder.weight"].shape[0]
+    assert bfl["single_blocks.0.linear1.weight"].shape[0] == 3 * d + sd["single_transformer_blocks.0.proj_mlp.weight"].shape[0]
+    w = bfl["final_layer.adaLN_modulation.1.weight"]
+    assert torch.equal(w[: w.shape[0] // 2], sd["norm_out.linear.weight"][w.shape[0] // 2:])  # (shift, scale)
+    back = fsf.bfl_to_diffusers({"model.diffusion_model." + k: v for k, v in bfl.items()})
+    assert set(back) == set(sd) and all(torch.equal(back[k], sd[k]) for k in sd)
+    tc = _cfg(os.path.join(flux_dir, "transformer", "config.json"))
+    got = fsf.infer_config(bfl, {"axes_dims_rope": tc["axes_dims_rope"]})
+    for k in ("in_channels", "num_layers", "num_single_layers", "attention_head_dim", "num_attention_heads",
+              "joint_attention_dim", "pooled_projection_dim", "guidance_embeds", "axes_dims_rope"):
+        assert got[k] == tc[k], (k, got[k], tc[k])
+    with pytest.raises(KeyError, match="unmapped|unknown"):
+        fsf.bfl_to_diffusers(dict(bfl, **{"double_blocks.0.img_attn.extra.weight": w}))
+
+
+def test_flux_transformer_single_file_through_backend(flux_dir, tmp_path, monkeypatch):
+    """pipeline_type FluxTransformer2DModel (backend.py:255-269): the transformer from a BFL
+    single file (here: the pipeline's weights with proj_out doubled, so the file is provably the
+    one served), the rest of the pipeline from BFL_REPO; without BFL_REPO the load is refused."""
+    from localai_amd.grpc.diffusers_servicer import DiffusersServicer
+    from localai_amd.models import flux_single_file as fsf
+    from localai_amd.models.sd import _cfg, _load_weights
+    sd = _load_weights(os.path.join(flux_dir, "transformer"))
+    sd["proj_out.weight"] = sd["proj_out.weight"] * 2
+    tc = _cfg(os.path.join(flux_dir, "transformer", "config.json"))
+    f = fsf.write_bfl_file(sd, str(tmp_path / "flux1-tiny.safetensors"), axes=tc["axes_dims_rope"])
+    p = FluxPipeline(flux_dir, "cpu", transformer_file=f)
+    assert torch.equal(p.tr.state_dict()["proj_out.weight"], sd["proj_out.weight"])
+    sv = DiffusersServicer(device="cpu")
+
+    async def go():
+        monkeypatch.delenv("BFL_REPO", raising=False)
+        r = await sv.LoadModel(pb.ModelOptions(ModelFile=f, PipelineType="FluxTransformer2DModel"), None)
+        assert not r.success and "BFL_REPO" in r.message
+        monkeypatch.setenv("BFL_REPO", flux_dir)
+        r = await sv.LoadModel(pb.ModelOptions(ModelFile=f, PipelineType="FluxTransformer2DModel"), None)
+        assert r.success, r.message
+        dst = str(tmp_path / "fluxsf.png")
+        r = await sv.GenerateImage(pb.GenerateImageRequest(positive_prompt="a castle", width=64, height=64, step=2,
+                                                           seed=9, dst=dst), None)
+        assert r.success, r.message
+    asyncio.run(go())
+
+
 @pytest.mark.gpu
 def test_flux_on_gpu_graph_matches_eager(flux_dir):
     p = FluxPipeline(flux_dir, "cuda:0")
