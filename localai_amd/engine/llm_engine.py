@@ -229,6 +229,7 @@ class LLMEngine:
         self._graph_pool = None
         self.k1_reasons = collections.Counter()
         self.k_hist = collections.Counter()   # (device steps, constrained rows in the batch) per decode run
+        self.k_log = collections.deque(maxlen=1024)  # (K, constrained rows, batch, waiting) per run, in order
         self.metrics = {"prompt_tokens": 0, "gen_tokens": 0, "steps": 0, "prefill_s": 0.0, "decode_s": 0.0,
                         "requests": 0, "spec_steps": 0, "spec_drafted": 0, "spec_accepted": 0,
                         "grammar_runs": 0, "grammar_run_rows": 0, "grammar_run_tokens": 0}
@@ -510,7 +511,9 @@ class LLMEngine:
                 if spec_k:
                     self._run_spec(plan, spec_k)
                 else:
-                    self.k_hist[(K, sum(1 for i in d_ids if self.requests[int(i)].grammar is not None))] += 1
+                    nc = sum(1 for i in d_ids if self.requests[int(i)].grammar is not None)
+                    self.k_hist[(K, nc)] += 1
+                    self.k_log.append((K, nc, len(d_ids), self.sched.num_waiting))
                     self._run_decode(plan, K)
             t1 = time.perf_counter()
             self.metrics["decode_s"] += t1 - t0
@@ -787,29 +790,36 @@ class LLMEngine:
         if len(self.requests) >= self.cfg.wide_batch and s.num_waiting == 0:
             K = max(K, self.cfg.decode_steps_wide)
         rem_tok, rem_ctx = 1, K
-        riders = 0
+        riders = cons = unsure = 0
         for r in self.requests.values():
             if r.n_gen == 0 or self._needs_host_sampler(r):
                 why["prefill" if r.n_gen == 0 else "host_sampler"] += 1
                 return 1  # prefill in flight, or a host-side sampler feature
-            if r.grammar is not None and not self._grammar_ready(r) and not self._gready(r):
+            if r.grammar is not None and not self._grammar_ready(r):
                 if not self._grammar_slot_cached(r):
                     why["grammar_no_mask"] += 1
                     return 1  # a parse state without a device mask: the host walks it first
-                riders += 1
+                cons += 1
+                if not self._gready(r):
+                    riders += 1
+                elif self._ghit.get(r.params.grammar, 0.0) < self.GRAMMAR_RUN_HIT:
+                    unsure += 1  # learned state, but its grammar often parks rows at new successors
             n = r.n_prompt + r.n_gen
             rem_ctx = min(rem_ctx, self.ctx - n)
             mt = r.params.max_tokens
             rem_tok = max(rem_tok, (mt - r.n_gen) if mt > 0 else K)
-        if riders:
-            # constrained rows whose transitions are not learned yet ride along a mostly-plain
-            # batch: the plain rows keep a multi-step run, each constrained row takes at least its
-            # first (masked) token per run and parks at its first unknown transition (_grammar_run);
-            # a batch that is mostly constrained stays at one step per round trip
-            if riders > self.GRAMMAR_MIXED_FRAC * len(self.requests):
+        if cons:
+            # constrained rows ride along a mostly-plain batch: the plain rows keep a multi-step
+            # run, each constrained row takes at least its first (masked) token per run and parks
+            # at its first unknown transition (_grammar_run).  Rows in a fully learned state
+            # (_gready) do not shorten the run; unlearned ones cap it at GRAMMAR_MIXED_K.  A batch
+            # that is mostly constrained stays at one step per round trip (rows park after a few
+            # tokens: a long run would mostly compute discarded positions) unless run-ahead is on
+            if cons > self.GRAMMAR_MIXED_FRAC * len(self.requests) and (riders or unsure):
                 why["grammar_majority"] += 1
                 return 1
-            K = min(K, self.GRAMMAR_MIXED_K)
+            if riders:
+                K = min(K, self.GRAMMAR_MIXED_K)
         return max(1, min(K, rem_ctx, rem_tok))
 
     GRAMMAR_MIXED_K = 4        # device steps per run while unlearned constrained rows ride along
@@ -1021,12 +1031,14 @@ class LLMEngine:
         self.metrics["grammar_run_rows"] += len(grows)
         for j in grows:
             r, s = reqs[j], int(gslot[j])
+            kept = []
             for i in range(K):
                 t = int(hist[i, j])
-                self._on_token(r, t, now)
+                self._on_token(r, t, now, append=False)
                 self.metrics["grammar_run_tokens"] += 1
                 if r.done:
                     break
+                kept.append(t)
                 s2 = self._grammar_mask_slot(r, V, self.device)
                 hit = (s, t) in self._gdev
                 self._grammar_hit(r, hit)
@@ -1037,6 +1049,12 @@ class LLMEngine:
                 if self._gtrans[(s, t)] != s2:
                     break
                 s = s2
+            if kept and not r.done:
+                # the device already wrote the KV of every kept token but the last (fed by the
+                # next step): hand them over as a run, like the plain rows' _emit_run -- appending
+                # them one by one marked them all uncomputed, and the row spent every other run
+                # re-prefilling its own positions instead of decoding
+                self.sched.append_run(r.id, kept)
 
     def _emit_run(self, reqs: List[Request], hist: np.ndarray, K: int, rec: Optional[torch.Tensor] = None):
         """Hand a [K, B] block of device-sampled tokens to the native emitter (detokenise, stop

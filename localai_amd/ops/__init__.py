@@ -451,7 +451,10 @@ def gemv_dp4(x: Optional[torch.Tensor], ws: Sequence[QWeight], S: int, out: torc
         col += sum(w.N for w in seg)
 
 
-GEMV_NORM = os.environ.get("LOCALAI_AMD_GEMV_NORM", "1") == "1"
+# off by default: measured neutral on Llama-3-8B C=1 (profiles/r4_c1_fused_norm.md) -- the 33
+# add_norm launches go away, but every q|k|v workgroup re-reads the residual plus the down
+# projection's 8 split-K slabs (144 KiB from L2 per workgroup) and the GEMV grows by the same ~4 us
+GEMV_NORM = os.environ.get("LOCALAI_AMD_GEMV_NORM", "0") == "1"
 
 
 @dataclass

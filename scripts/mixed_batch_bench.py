@@ -57,6 +57,7 @@ eng.k_hist.clear()
 for special in ("", "penalty", "grammar", ""):
     eng.k1_reasons.clear()
     eng.k_hist.clear()
+    eng.k_log.clear()
     r = wave(f"w{time.time():.0f}", special)
     print(f"{special or 'plain':8s} decode {r:9.1f} tok/s", flush=True)
     if special == "grammar":
@@ -65,5 +66,6 @@ for special in ("", "penalty", "grammar", ""):
               f"hit-rate {dict((k[:20], round(v, 3)) for k, v in eng._ghit.items())} "
               f"single-step reasons {dict(eng.k1_reasons)} runs by (K, constrained rows) {dict(eng.k_hist)}",
               flush=True)
+        print("  run sequence (K, constrained, batch, waiting):", list(eng.k_log), flush=True)
     eng.k1_reasons.clear()
     eng.k_hist.clear()
