@@ -55,21 +55,30 @@ __global__ void __launch_bounds__(GN_THREADS) gn_stats_kernel(const unsigned* __
       }
     }
   }
-  __shared__ float acc[GN_MAXG * 2];
-  for (int i = t; i < 2 * G; i += GN_THREADS) acc[i] = 0.0f;
-  __syncthreads();
+  // per-group totals in a FIXED order (no LDS float atomics: their arrival order made the sums,
+  // and so every SD / SDXL image, differ in the last bits run to run): every thread parks its
+  // per-pair partials in LDS, then lane (g, k) walks group g's pairs and row slots in order
+  __shared__ float ps[GN_THREADS * GN_MAXP * 2];
 #pragma unroll
   for (int i = 0; i < GN_MAXP; ++i) {
-    const int p = pb + i * GN_THREADS;
-    if (tr < RS && p < P) {
-      const int g = (2 * p) / cg;
-      atomicAdd(&acc[2 * g], sum[i]);
-      atomicAdd(&acc[2 * g + 1], sq[i]);
-    }
+    const bool own = tr < RS && pb + i * GN_THREADS < P;
+    ps[(t * GN_MAXP + i) * 2] = own ? sum[i] : 0.0f;
+    ps[(t * GN_MAXP + i) * 2 + 1] = own ? sq[i] : 0.0f;
   }
   __syncthreads();
   float* out = part + ((long)b * S + s) * G * 2;
-  for (int i = t; i < 2 * G; i += GN_THREADS) out[i] = acc[i];
+  if (t < 2 * G) {
+    const int g = t >> 1, k = t & 1, hp = cg >> 1;
+    float a = 0.0f;
+    for (int p = g * hp; p < (g + 1) * hp; ++p) {
+      if (P <= GN_THREADS) {
+        for (int r = 0; r < RS; ++r) a += ps[((r * P + p) * GN_MAXP) * 2 + k];
+      } else {
+        a += ps[((p % GN_THREADS) * GN_MAXP + p / GN_THREADS) * 2 + k];
+      }
+    }
+    out[t] = a;
+  }
 }
 
 __global__ void __launch_bounds__(GN_THREADS) gn_apply_kernel(const unsigned* __restrict__ x, unsigned* __restrict__ y,

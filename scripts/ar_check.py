@@ -34,6 +34,11 @@ def main():
     torch.cuda.set_device(dev)
     dist.init_process_group("gloo")
     car = CustomAllReduce(dist.group.WORLD, rank, world, dev)
+    if os.environ.get("LOCALAI_AMD_AR_SAME_GPU") == "1":
+        # every rank on ONE device: 8 processes x 4 HIP queues oversubscribe the hardware queues,
+        # so a peer's kernel may wait for a time slice while this one spins -- allow ~16 s
+        # instead of ~1 s before a wait counts as a dead peer (separate GPUs never need it)
+        car.SPIN_LIMIT = 1 << 24
     cases = [(4096, torch.float32), (3 * 4096, torch.float32), (4096, torch.bfloat16), (1000, torch.float32),
              (64 * 4096, torch.float32), (car.max_elems, torch.bfloat16), (4096 + 8, torch.bfloat16),
              # two-shot (reduce-scatter + all-gather) past the one-shot's size: a decode batch of 256
@@ -46,7 +51,7 @@ def main():
         torch.cuda.synchronize()
         ref = expected(world, n, dt, dev, call)
         err = (t.float() - ref.float()).abs().max().item()
-        assert err == 0.0, (rank, n, dt, err)
+        assert err == 0.0, (rank, n, dt, err, "timed out" if car.error_flag() else "no timeout")
     # graph capture: calls of mixed sizes (one-shot and two-shot), replayed twice with fresh inputs
     gcases = cases[:3] + [cases[7]]
     bufs = [torch.empty(n, dtype=dt, device=dev) for n, dt in gcases]
@@ -68,7 +73,9 @@ def main():
         torch.cuda.synchronize()
         for i, (n, dt) in enumerate(gcases):
             ref = expected(world, n, dt, dev, 100 + 10 * rep + i)
-            assert (bufs[i].float() - ref.float()).abs().max().item() == 0.0, (rank, "graph", rep, i)
+            assert (bufs[i].float() - ref.float()).abs().max().item() == 0.0, (rank, "graph", rep, i,
+                                                                               "timed out" if car.error_flag() else
+                                                                               "no timeout")
     assert not car.timed_out()
     # fused all-reduce + bias + residual + norm (CustomAllReduce.add_norm), interleaved with plain
     # one-shot calls on the same channels: residual exact, normed row within bf16 rounding

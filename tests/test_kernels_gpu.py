@@ -632,7 +632,7 @@ def test_qkv_rope_dp4_fused(M):
 
 
 @pytest.mark.parametrize("M,S", [(1, 0), (1, 3), (2, 8), (2, 11)])
-def test_qkv_rope_dp4_fused_norm(M, S):
+def test_qkv_rope_dp4_fused_norm(M, S, monkeypatch):
     """The layer-boundary residual-add + RMSNorm folded into the fused q|k|v GEMV's prologue
     (ops.NormIn, gemv_dp4.hip GV_NORM) vs add_norm + the same GEMV: q, the appended K/V, and the
     updated residual (written to the other buffer; S = 0: no add, nothing written)."""
@@ -649,6 +649,7 @@ def test_qkv_rope_dp4_fused_norm(M, S):
     kc, vc = torch.zeros(nblk, Hkv, BS, Dh, dtype=torch.bfloat16, device=DEV), ops.v_pages(nblk, Hkv, BS, Dh, device=DEV)
     res_out = torch.full_like(res, float("nan")) if S else None
     nin = ops.NormIn(res.clone(), add, w, 1e-5, res_out)
+    monkeypatch.setattr(ops, "GEMV_NORM", True)  # off by default (measured neutral), tested here
     assert ops.norm_in_ok(nin.res, add, w, None)
     q = ops.qkv_rope_dp4(nin, [qk, v], pos, slots, cs, Hq, Hkv, Dh, kc, vc, BS)
     r2 = res.clone()

@@ -181,6 +181,9 @@ def test_groupnorm_nhwc_kernel_matches_fp32(shape, groups, silu):
     got = ops.groupnorm_nhwc(x, groups, None, None, 1e-5, silu)  # affine-free
     ref = F.group_norm(x.float(), groups, None, None, 1e-5)
     torch.testing.assert_close(got.float(), F.silu(ref) if silu else ref, atol=3e-2, rtol=2e-2)
+    # fixed-order statistics (no float atomics): repeated launches are bit-identical
+    for _ in range(3):
+        assert torch.equal(ops.groupnorm_nhwc(x, groups, None, None, 1e-5, silu), got)
 
 
 @pytest.mark.gpu
@@ -332,7 +335,9 @@ def test_controlnet_on_gpu_graph(pipe_dir, tmp_path):
     cdir = synth.write_controlnet(str(tmp_path / "cn"), pipe_dir, zero=False, seed=5)
     ctrl = tmp_path / "ctrl.png"
     Image.fromarray((torch.rand(32, 32, 3) * 255).to(torch.uint8).numpy()).save(ctrl)
-    p = StableDiffusion(pipe_dir, "cuda:0", controlnet=cdir)
+    # deterministic convolution solvers: replays and eager differ only by what the graph changes
+    # (MIOpen's default solvers alone moved a pixel by 4 between two otherwise identical runs)
+    p = StableDiffusion(pipe_dir, "cuda:0", controlnet=cdir, deterministic=True)
     a = p("a cat", "", 32, 32, steps=3, seed=3, control_image=str(ctrl))
     b = p("a cat", "", 32, 32, steps=3, seed=3, control_image=str(ctrl))
     assert p._graphs and (a.float() - b.float()).abs().max() <= 3
