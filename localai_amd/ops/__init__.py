@@ -55,6 +55,7 @@ def lib():
             "la_qgemv_dp4": [I, P, P, P, I, P, I, I, I, P, I, LNG, P, LNG, I, P, I, P],
             "la_moe_gemv": [I, I, P, I, I, I, P, I, I, P, I, I, P, LNG, I, I, P, P, I, LNG, P],
             "la_gemv_variant": [I],
+            "la_moe_tune": [I, I],
             "la_qgemv_dp4_rope": [I, P, P, P, I, P, I, P, P, P, I, I, I, P, P, P, I, P],
             "la_qgemv_dp4_norm": [I, P, P, P, I, I, I, P, I, LNG, P, P, LNG, I, P, P, F, P, P],
             "la_qgemv_dp4_rope_norm": [I, P, P, P, I, I, P, P, P, I, I, I, P, P, P, I, P, P, LNG, I, P, P, F,
@@ -103,6 +104,10 @@ def lib():
         gv = os.environ.get("LOCALAI_AMD_GEMV_VARIANT")
         if gv is not None:
             _check(L.la_gemv_variant(int(gv)), "la_gemv_variant")
+        mt = os.environ.get("LOCALAI_AMD_MOE_TUNE")  # "row_tile,waves" of the wide-batch MoE GEMM (A/B)
+        if mt:
+            a, b = (int(v) for v in mt.split(","))
+            _check(L.la_moe_tune(a, b), "la_moe_tune")
         _LIB = L
         return L
 

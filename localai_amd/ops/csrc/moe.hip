@@ -11,6 +11,8 @@
 //                  DOWN   : out[split*topk + slot][token][n] * w[pair]  (X row = pair)
 //                DOWN writes the routing-weighted expert outputs as extra split-K slabs, so the
 //                next kernel's slab-sum prologue (add_norm) performs the top-k combine for free.
+#include <cmath>
+
 #include "qweight.h"
 
 namespace la {
@@ -111,8 +113,11 @@ __global__ __launch_bounds__(256) void moe_router_kernel(const bf16* __restrict_
   }
 }
 
-template <int FMT, int MT, bool DOWN>
-__global__ __launch_bounds__(MOE_THREADS, 2) void moe_gemm_kernel(
+// NW waves per workgroup, 16 output columns each: the X tile staged in LDS per super-block serves
+// 16 * NW columns, so NW = 8 halves the L2 -> LDS activation traffic of a wide batch (where every
+// column block of an expert re-stages the same gathered rows) and doubles the waves per CU.
+template <int FMT, int MT, bool DOWN, int NW = MOE_WAVES>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void moe_gemm_kernel(
     const QW* __restrict__ qws, const int* __restrict__ order, const int* __restrict__ off, int topk,
     const bf16* __restrict__ X, int ldx, int k_per_split, const float* __restrict__ wts, float* __restrict__ out,
     int ldo, long slab, int T, int nchunk) {
@@ -133,18 +138,19 @@ __global__ __launch_bounds__(MOE_THREADS, 2) void moe_gemm_kernel(
   const int split = blockIdx.y;
   const int kbeg = split * k_per_split;
   const int nsb = min(k_per_split, K - kbeg) >> 8;
-  const int n = blockIdx.x * (16 * MOE_WAVES) + wave * 16 + r;
+  constexpr int NT = 64 * NW;
+  const int n = blockIdx.x * (16 * NW) + wave * 16 + r;
   const int nl = min(n, N - 1);
   if (tid < MP) prow[tid] = tid < M ? order[o0 + tid] : 0;
   __syncthreads();
 
   constexpr int XCH = MP * 32;
-  constexpr int XPT = (XCH + MOE_THREADS - 1) / MOE_THREADS;
+  constexpr int XPT = (XCH + NT - 1) / NT;
   bf16x8 xr[XPT];
   auto x_issue = [&](int sb) {
 #pragma unroll
     for (int i = 0; i < XPT; ++i) {
-      const int c = tid + i * MOE_THREADS;
+      const int c = tid + i * NT;
       const int row = min(c >> 5, MP - 1), col = (c & 31) * 8;
       const int p = prow[row];
       const int xrow = DOWN ? p : p / topk;
@@ -156,7 +162,7 @@ __global__ __launch_bounds__(MOE_THREADS, 2) void moe_gemm_kernel(
   auto x_store = [&]() {
 #pragma unroll
     for (int i = 0; i < XPT; ++i) {
-      const int c = tid + i * MOE_THREADS;
+      const int c = tid + i * NT;
       if (c < XCH) *(bf16x8*)(xs + (c >> 5) * MOE_LDS_STRIDE + (c & 31) * 8) = xr[i];
     }
   };
@@ -219,22 +225,41 @@ __global__ __launch_bounds__(MOE_THREADS, 2) void moe_gemm_kernel(
   }
 }
 
+static int g_moe_mt = 0;  // 0: auto; else the row tile (MT x 16 rows) for batches past 64 rows
+static int g_moe_nw = 8;  // waves (16 columns each) per workgroup for batches past 64 rows
+
 template <int FMT, bool DOWN>
 static void launch_moe(const QW* qws, int N, int K, int E, const int* order, const int* off, int topk,
                        const bf16* X, int ldx, int maxM, int splits, const float* wts, float* out, int ldo, long slab,
                        int T, hipStream_t st) {
   const int per = (K >> 8) / splits;
-  const int gx = (N + 16 * MOE_WAVES - 1) / (16 * MOE_WAVES);
-#define MOE_L(MT)                                                                                                \
-  {                                                                                                              \
-    const int nch = (maxM + 16 * (MT)-1) / (16 * (MT));                                                          \
-    hipLaunchKernelGGL((moe_gemm_kernel<FMT, MT, DOWN>), dim3(gx, splits, E * nch), dim3(MOE_THREADS), 0, st, qws, \
-                       order, off, topk, X, ldx, per * 256, wts, out, ldo, slab, T, nch);                        \
+#define MOE_L(MT, NW)                                                                                             \
+  {                                                                                                               \
+    const int gx = (N + 16 * (NW)-1) / (16 * (NW));                                                               \
+    const int nch = (maxM + 16 * (MT)-1) / (16 * (MT));                                                           \
+    hipLaunchKernelGGL((moe_gemm_kernel<FMT, MT, DOWN, NW>), dim3(gx, splits, E * nch), dim3(64 * (NW)), 0, st,   \
+                       qws, order, off, topk, X, ldx, per * 256, wts, out, ldo, slab, T, nch);                    \
   }
-  if (maxM <= 16) MOE_L(1)
-  else if (maxM <= 32) MOE_L(2)
-  else if (maxM <= 64) MOE_L(4)
-  else MOE_L(8)
+  if (maxM <= 16) MOE_L(1, 4)
+  else if (maxM <= 32) MOE_L(2, 4)
+  else if (maxM <= 64) MOE_L(4, 4)
+  else {
+    // wide batch: the row tile sized for an expert's EXPECTED rows (mean + 3 sigma of a balanced
+    // top-k router, T * topk / E), not the worst case T -- a 128-row tile for ~64 rows per
+    // expert ran half its MFMAs on zero rows and staged twice the LDS; experts above the tile
+    // take a second chunk (their weights stream twice)
+    int mt = g_moe_mt;
+    if (mt <= 0) {
+      const double mean = (double)T * topk / E;
+      mt = (int)((mean + 3.0 * sqrt(mean) + 15.0) / 16.0);
+      mt = mt < 4 ? 4 : (mt > 8 ? 8 : mt);
+    }
+    if (g_moe_nw == 8) {
+      if (mt <= 4) MOE_L(4, 8) else if (mt <= 5) MOE_L(5, 8) else if (mt <= 6) MOE_L(6, 8) else MOE_L(8, 8)
+    } else {
+      if (mt <= 4) MOE_L(4, 4) else if (mt <= 5) MOE_L(5, 4) else if (mt <= 6) MOE_L(6, 4) else MOE_L(8, 4)
+    }
+  }
 #undef MOE_L
 }
 
@@ -281,3 +306,11 @@ extern "C" int la_moe_gemm(int fmt, int down, const void* qws, int N, int K, int
 }
 
 extern "C" int la_qw_size() { return (int)sizeof(la::QW); }
+
+// Tuning hook (A/B): wide-batch row tile (0 auto, 4..8) and waves per workgroup (4 or 8).
+extern "C" int la_moe_tune(int mt, int nw) {
+  if (mt < 0 || mt > 8 || (nw != 4 && nw != 8)) return -1;
+  la::g_moe_mt = mt;
+  la::g_moe_nw = nw;
+  return 0;
+}

@@ -527,15 +527,21 @@ def test_decode_advance_kernel():
     assert int(g[5].item()) == 1 and list(g[4][0].cpu()) == [7, 8, 9, 10, 11]
 
 
-@pytest.mark.parametrize("T", [1, 5, 33, 100, 300])
-def test_moe_grouped_gemm(T):
-    """Grouped expert GEMM at decode and wide / prefill batch sizes (T > 64: row-chunked grid)."""
+@pytest.mark.parametrize("T,skew", [(1, False), (5, False), (33, False), (100, False), (256, False), (300, False),
+                                    (300, True), (256, True)])
+def test_moe_grouped_gemm(T, skew):
+    """Grouped expert GEMM at decode and wide / prefill batch sizes (T > 64: row-chunked grid, the
+    row tile sized for a balanced router's expected rows); skew: every token picks experts 0 and
+    1, so two experts take T rows each (several row chunks) and the others none."""
     E, topk, D, F = 8, 2, 512, 768
     gu = [_qw(2 * F, D, GGMLType.Q4_K, seed=10 + e) for e in range(E)]
     dn = [_qw(D, F, GGMLType.Q6_K, seed=30 + e) for e in range(E)]
     mg, md = ops.MoEWeights(gu), ops.MoEWeights(dn)
     x = torch.randn(T, D, device=DEV).to(torch.bfloat16)
-    ids = torch.stack([torch.randperm(E)[:topk] for _ in range(T)]).to(torch.int32).to(DEV)
+    if skew:
+        ids = torch.tensor([[0, 1]] * T, dtype=torch.int32, device=DEV)
+    else:
+        ids = torch.stack([torch.randperm(E)[:topk] for _ in range(T)]).to(torch.int32).to(DEV)
     wts = torch.rand(T, topk, device=DEV)
     order, off = ops.moe_route(ids, E)
     o = order.cpu().tolist()
