@@ -244,16 +244,12 @@ static void launch_moe(const QW* qws, int N, int K, int E, const int* order, con
   else if (maxM <= 32) MOE_L(2, 4)
   else if (maxM <= 64) MOE_L(4, 4)
   else {
-    // wide batch: the row tile sized for an expert's EXPECTED rows (mean + 3 sigma of a balanced
-    // top-k router, T * topk / E), not the worst case T -- a 128-row tile for ~64 rows per
-    // expert ran half its MFMAs on zero rows and staged twice the LDS; experts above the tile
-    // take a second chunk (their weights stream twice)
-    int mt = g_moe_mt;
-    if (mt <= 0) {
-      const double mean = (double)T * topk / E;
-      mt = (int)((mean + 3.0 * sqrt(mean) + 15.0) / 16.0);
-      mt = mt < 4 ? 4 : (mt > 8 ? 8 : mt);
-    }
+    // wide batch: 64-row tiles in 8-wave workgroups, whatever the batch.  Mixtral-8x7B, engine
+    // C=256 (decode + the prefill chunks, one box): 64-row / 8 waves 3951 tok/s; 128-row / 4 waves
+    // (round 3) 3461; 128 / 8: 3475; 96 / 8: 3346-3592; 80 / 8: 3119 (scripts/gpu_r4_m.sh).  The
+    // 64-row tile keeps two workgroups (16 waves) per CU -- occupancy outweighs streaming the
+    // weights of an expert with more rows once per extra chunk (they come back from L2 / MALL)
+    const int mt = g_moe_mt > 0 ? g_moe_mt : 4;
     if (g_moe_nw == 8) {
       if (mt <= 4) MOE_L(4, 8) else if (mt <= 5) MOE_L(5, 8) else if (mt <= 6) MOE_L(6, 8) else MOE_L(8, 8)
     } else {
