@@ -116,8 +116,8 @@ __global__ __launch_bounds__(256) void moe_router_kernel(const bf16* __restrict_
 // NW waves per workgroup, 16 output columns each: the X tile staged in LDS per super-block serves
 // 16 * NW columns, so NW = 8 halves the L2 -> LDS activation traffic of a wide batch (where every
 // column block of an expert re-stages the same gathered rows) and doubles the waves per CU.
-template <int FMT, int MT, bool DOWN, int NW = MOE_WAVES>
-__global__ __launch_bounds__(64 * NW, 8 / NW) void moe_gemm_kernel(
+template <int FMT, int MT, bool DOWN, int NW = MOE_WAVES, bool W3 = false>
+__global__ __launch_bounds__(64 * NW, W3 ? 2 : 8 / NW) void moe_gemm_kernel(
     const QW* __restrict__ qws, const int* __restrict__ order, const int* __restrict__ off, int topk,
     const bf16* __restrict__ X, int ldx, int k_per_split, const float* __restrict__ wts, float* __restrict__ out,
     int ldo, long slab, int T, int nchunk) {
@@ -174,6 +174,10 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void moe_gemm_kernel(
   WFrag<FMT> fa, fb;
   x_issue(0);
   fa.load(w, nl, sb0, g);
+  WFrag<FMT> fc;
+  if constexpr (W3) {
+    if (nsb > 1) fb.load(w, nl, sb0 + 1, g);
+  }
   auto compute = [&](WFrag<FMT>& f) {
     f.prep(g);
 #define MOE_STEP(S)                                                                          \
@@ -188,6 +192,26 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void moe_gemm_kernel(
     MOE_STEP(0) MOE_STEP(1) MOE_STEP(2) MOE_STEP(3) MOE_STEP(4) MOE_STEP(5) MOE_STEP(6) MOE_STEP(7)
 #undef MOE_STEP
   };
+  if constexpr (W3) {
+    // three-slot weight ring: super-block s + 2 is requested while s computes, so each HBM weight
+    // round trip has two compute phases to land instead of one (the gathered activation rows come
+    // from L2 and keep the one-ahead register stage)
+    auto step = [&](int s, WFrag<FMT>& cur, WFrag<FMT>& nxt2) {
+      __syncthreads();
+      x_store();
+      __syncthreads();
+      if (s + 1 < nsb) x_issue(s + 1);
+      if (s + 2 < nsb) nxt2.load(w, nl, sb0 + s + 2, g);
+      compute(cur);
+    };
+    for (int sb = 0; sb < nsb; sb += 3) {
+      step(sb, fa, fc);
+      if (sb + 1 >= nsb) break;
+      step(sb + 1, fb, fa);
+      if (sb + 2 >= nsb) break;
+      step(sb + 2, fc, fb);
+    }
+  } else {
   for (int sb = 0; sb < nsb; sb += 2) {
     __syncthreads();
     x_store();
@@ -206,6 +230,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void moe_gemm_kernel(
       fa.load(w, nl, sb0 + sb + 2, g);
     }
     compute(fb);
+  }
   }
   if (n >= N) return;
 #pragma unroll
@@ -227,19 +252,21 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void moe_gemm_kernel(
 
 static int g_moe_mt = 0;  // 0: auto; else the row tile (MT x 16 rows) for batches past 64 rows
 static int g_moe_nw = 8;  // waves (16 columns each) per workgroup for batches past 64 rows
+static int g_moe_w3 = 0;  // three-slot weight ring (A/B)
 
 template <int FMT, bool DOWN>
 static void launch_moe(const QW* qws, int N, int K, int E, const int* order, const int* off, int topk,
                        const bf16* X, int ldx, int maxM, int splits, const float* wts, float* out, int ldo, long slab,
                        int T, hipStream_t st) {
   const int per = (K >> 8) / splits;
-#define MOE_L(MT, NW)                                                                                             \
+#define MOE_LW(MT, NW, W3)                                                                                        \
   {                                                                                                               \
     const int gx = (N + 16 * (NW)-1) / (16 * (NW));                                                               \
     const int nch = (maxM + 16 * (MT)-1) / (16 * (MT));                                                           \
-    hipLaunchKernelGGL((moe_gemm_kernel<FMT, MT, DOWN, NW>), dim3(gx, splits, E * nch), dim3(64 * (NW)), 0, st,   \
-                       qws, order, off, topk, X, ldx, per * 256, wts, out, ldo, slab, T, nch);                    \
+    hipLaunchKernelGGL((moe_gemm_kernel<FMT, MT, DOWN, NW, W3>), dim3(gx, splits, E * nch), dim3(64 * (NW)), 0,  \
+                       st, qws, order, off, topk, X, ldx, per * 256, wts, out, ldo, slab, T, nch);                \
   }
+#define MOE_L(MT, NW) MOE_LW(MT, NW, false)
   if (maxM <= 16) MOE_L(1, 4)
   else if (maxM <= 32) MOE_L(2, 4)
   else if (maxM <= 64) MOE_L(4, 4)
@@ -250,13 +277,15 @@ static void launch_moe(const QW* qws, int N, int K, int E, const int* order, con
     // 64-row tile keeps two workgroups (16 waves) per CU -- occupancy outweighs streaming the
     // weights of an expert with more rows once per extra chunk (they come back from L2 / MALL)
     const int mt = g_moe_mt > 0 ? g_moe_mt : 4;
-    if (g_moe_nw == 8) {
+    if (g_moe_w3 && mt == 4 && g_moe_nw == 8) MOE_LW(4, 8, true)
+    else if (g_moe_nw == 8) {
       if (mt <= 4) MOE_L(4, 8) else if (mt <= 5) MOE_L(5, 8) else if (mt <= 6) MOE_L(6, 8) else MOE_L(8, 8)
     } else {
       if (mt <= 4) MOE_L(4, 4) else if (mt <= 5) MOE_L(5, 4) else if (mt <= 6) MOE_L(6, 4) else MOE_L(8, 4)
     }
   }
 #undef MOE_L
+#undef MOE_LW
 }
 
 }  // namespace la
@@ -305,8 +334,9 @@ extern "C" int la_qw_size() { return (int)sizeof(la::QW); }
 
 // Tuning hook (A/B): wide-batch row tile (0 auto, 4..8) and waves per workgroup (4 or 8).
 extern "C" int la_moe_tune(int mt, int nw) {
-  if (mt < 0 || mt > 8 || (nw != 4 && nw != 8)) return -1;
+  if (mt < 0 || mt > 8 || (nw != 4 && nw != 8 && nw != 9)) return -1;  // nw 9: 8 waves + weight ring
   la::g_moe_mt = mt;
-  la::g_moe_nw = nw;
+  la::g_moe_nw = nw == 9 ? 8 : nw;
+  la::g_moe_w3 = nw == 9;
   return 0;
 }
