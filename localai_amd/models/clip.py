@@ -295,9 +295,32 @@ class ClipVision:
         return out
 
     def _assemble(self, e: torch.Tensor, layout) -> torch.Tensor:
-        """Encoded tiles of one image -> its prompt rows (anyres: base tile, unpadded grid, newlines)."""
+        """Encoded tiles of one image -> its prompt rows (anyres: base tile, unpadded grid, newlines).
+        On the GPU: one gather (ops.gather_rows) through an index vector cached per layout."""
         if layout is None:
             return e[0]
+        if e.is_cuda:
+            from .. import ops
+            n_t, n_p, C = e.shape
+            key = (tuple(layout), n_t, n_p, self.newline is not None)
+            idx = self._asm_idx.get(key) if hasattr(self, "_asm_idx") else None
+            if idx is None:
+                # the torch assembly below run on row numbers gives the source row of every output row
+                rows = torch.arange(n_t * n_p, dtype=torch.float64).view(n_t, n_p, 1)
+                saved, self.newline = self.newline, (torch.full((1,), -1.0, dtype=torch.float64)
+                                                     if self.newline is not None else None)
+                try:
+                    idx = self._assemble_torch(rows, layout).view(-1).round().long().to(e.device)
+                finally:
+                    self.newline = saved
+                if not hasattr(self, "_asm_idx"):
+                    self._asm_idx = {}
+                self._asm_idx[key] = idx
+            fill = self.newline.to(e.dtype) if self.newline is not None else None
+            return ops.gather_rows(e.reshape(n_t * n_p, C), idx, fill)
+        return self._assemble_torch(e, layout)
+
+    def _assemble_torch(self, e: torch.Tensor, layout) -> torch.Tensor:
         gw, gh, ow, oh = layout
         g = self.grid
         base, rest = e[0], e[1:]                                               # [np, C]

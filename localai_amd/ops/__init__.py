@@ -56,6 +56,7 @@ def lib():
             "la_moe_gemv": [I, I, P, I, I, I, P, I, I, P, I, I, P, LNG, I, I, P, P, I, LNG, P],
             "la_gemv_variant": [I],
             "la_moe_tune": [I, I],
+            "la_gather_rows": [P, P, LNG, P, P, LNG, P],
             "la_qgemv_dp4_rope": [I, P, P, P, I, P, I, P, P, P, I, I, I, P, P, P, I, P],
             "la_qgemv_dp4_norm": [I, P, P, P, I, I, I, P, I, LNG, P, P, LNG, I, P, P, F, P, P],
             "la_qgemv_dp4_rope_norm": [I, P, P, P, I, I, P, P, P, I, I, I, P, P, P, I, P, P, LNG, I, P, P, F,
@@ -1339,6 +1340,24 @@ def embed(tokens: torch.Tensor, w: QWeight, scale: float = 1.0, out: Optional[to
     assert tokens.dtype == torch.int32
     _check(lib().la_embed(w.fmt, *w.ptrs(), w.N, w.K, tokens.data_ptr(), T, out.data_ptr(), float(scale),
                           _stream()), "la_embed")
+    return out
+
+
+def gather_rows(src: torch.Tensor, idx: torch.Tensor, fill: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """out[t] = src[idx[t]] if idx[t] >= 0 else fill: one launch (elementwise.hip gather_rows_kernel).
+    src [R, C] contiguous, idx int64 [T] on the same device, fill [C] (needed when idx has -1s)."""
+    T, C = idx.shape[0], src.shape[1]
+    if not src.is_cuda:
+        out = src[idx.clamp(min=0)]
+        if fill is not None:
+            out[idx < 0] = fill.to(out.dtype)
+        return out
+    assert src.is_contiguous() and idx.dtype == torch.int64 and idx.device == src.device
+    out = torch.empty(T, C, dtype=src.dtype, device=src.device)
+    if fill is not None:
+        fill = fill.to(src.dtype).contiguous()
+    _check(lib().la_gather_rows(src.data_ptr(), idx.data_ptr(), T, _ptr(fill), out.data_ptr(),
+                                C * src.element_size(), _stream()), "la_gather_rows")
     return out
 
 

@@ -396,10 +396,38 @@ __global__ __launch_bounds__(256) void dequant_kernel(QW w, bf16* __restrict__ o
   *(bf16x8*)(out + (long)n * w.K + k) = o;
 }
 
+// ------------------------------------------------------------------------------------
+// Row gather with a fill row: out[t] = idx[t] >= 0 ? src[idx[t]] : fill  (any 2-byte or 4-byte
+// element type, rows of C elements, 16-byte vectors when C allows).  The LLaVA-1.6 anyres image
+// assembly (base tile, grid tiles permuted to row-major, spatial unpadding, an
+// image_newline row after every feature row) is one precomputed index vector and this one launch,
+// where the torch path ran a permute copy, a slice, an expand + cat and a final cat.
+__global__ __launch_bounds__(256) void gather_rows_kernel(const uint8_t* __restrict__ src, const long* __restrict__ idx,
+                                                          const uint8_t* __restrict__ fill, uint8_t* __restrict__ out,
+                                                          long row_bytes) {
+  const long t = blockIdx.x;
+  const long i = idx[t];
+  const uint8_t* s = i >= 0 ? src + i * row_bytes : fill;
+  uint8_t* d = out + t * row_bytes;
+  if ((row_bytes & 15) == 0) {
+    for (long b = (long)threadIdx.x * 16; b < row_bytes; b += 256 * 16) *(u32x4*)(d + b) = *(const u32x4*)(s + b);
+  } else {
+    for (long b = threadIdx.x; b < row_bytes; b += 256) d[b] = s[b];
+  }
+}
+
 }  // namespace la
 
 // C ABI ------------------------------------------------------------------------------
 using la::Src;
+
+extern "C" int la_gather_rows(const void* src, const long* idx, long T, const void* fill, void* out, long row_bytes,
+                               void* stream) {
+  if (T < 1 || row_bytes < 1 || !src || !idx || !out) return -1;
+  hipLaunchKernelGGL(la::gather_rows_kernel, dim3(T), dim3(256), 0, (hipStream_t)stream, (const uint8_t*)src, idx,
+                     (const uint8_t*)(fill ? fill : src), (uint8_t*)out, row_bytes);
+  return (int)hipGetLastError();
+}
 
 extern "C" int la_add_norm(void* residual, const void* add_p, long add_slab, int add_S, const void* add_bias,
                            int has_add, const void* w, const void* b, void* out, int T, int D, float eps,

@@ -155,3 +155,26 @@ def test_norm_in_prologue_mapping_and_materialize():
     assert torch.allclose(out, r, atol=1e-5) and torch.allclose(nin.res, r, atol=1e-5)
     assert torch.allclose(x.float(), ref, rtol=1e-2, atol=1e-2)
     assert not ops.norm_in_ok(res, add, w, None)  # CPU tensors: never the fused path
+
+
+def test_anyres_assembly_index_matches_torch_path():
+    """LLaVA-1.6 anyres assembly as ONE gather (ops.gather_rows through an index vector derived
+    by running the torch assembly on row numbers, clip.py ClipVision._assemble) equals the torch
+    permute / unpad / newline / cat path, for wide and tall images and without a newline row."""
+    from localai_amd.models.clip import ClipVision
+
+    class M:
+        grid = 4
+
+    for layout in [(2, 2, 300, 200), (2, 1, 200, 500), (3, 2, 640, 480)]:
+        gw, gh = layout[0], layout[1]
+        for nl in (torch.randn(8), None):
+            m = M()
+            m.newline = nl
+            e = torch.randn(1 + gw * gh, 16, 8)
+            ref = ClipVision._assemble_torch(m, e, layout)
+            rows = torch.arange(e.shape[0] * 16, dtype=torch.float64).view(e.shape[0], 16, 1)
+            m.newline = torch.full((1,), -1.0, dtype=torch.float64) if nl is not None else None
+            idx = ClipVision._assemble_torch(m, rows, layout).view(-1).round().long()
+            got = ops.gather_rows(e.reshape(-1, 8), idx, nl)
+            assert torch.equal(ref, got), (layout, nl is None)

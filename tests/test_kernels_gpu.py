@@ -900,3 +900,16 @@ def test_clip_tower_native_ops_match_fp32(tmp_path, cls_token):
     cos = torch.nn.functional.cosine_similarity(a.reshape(-1, a.shape[-1]), b.reshape(-1, b.shape[-1]), dim=1)
     rel = float((a - b).norm() / b.norm())
     assert float(cos.min()) > 0.995 and rel < 5e-2, (float(cos.min()), rel)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("C", [4096, 1000, 7])
+def test_gather_rows_kernel(dtype, C):
+    """gather_rows_kernel (16-byte and byte-wise rows) vs torch indexing, fill rows for -1."""
+    src = torch.randn(50, C, device=DEV).to(dtype)
+    fill = torch.randn(C, device=DEV).to(dtype)
+    idx = torch.tensor([3, -1, 49, 0, 0, -1, 17], dtype=torch.long, device=DEV)
+    got = ops.gather_rows(src, idx, fill)
+    ref = src[idx.clamp(min=0)].clone()
+    ref[idx < 0] = fill
+    assert torch.equal(got, ref)
