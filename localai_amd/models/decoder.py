@@ -37,6 +37,10 @@ TP_OVERLAP_ROWS = int(os.environ.get("LOCALAI_AMD_TP_OVERLAP_ROWS", "1024"))
 TP_OVERLAP_CHUNKS = int(os.environ.get("LOCALAI_AMD_TP_OVERLAP_CHUNKS", "4"))
 # MoE decode batches route with the fused router kernel (moe.hip); =1 falls back to the torch ops
 FUSED_ROUTER_OFF = os.environ.get("LOCALAI_AMD_FUSED_ROUTER_OFF", "0") == "1"
+# prefill chunks of at least this many tokens run each expert as a dense GEMM over its gathered
+# rows (~T * topk / E rows: the library / tile prefill path, weights dequantised once per expert)
+# instead of the decode-shaped grouped kernel, which streams an expert's weights once per 64 rows
+MOE_DENSE_MIN_T = int(os.environ.get("LOCALAI_AMD_MOE_DENSE_MIN_T", "1024"))
 
 _ACT = {"swiglu": ops.ACT_SWIGLU, "gelu": ops.ACT_GELU, "geglu": ops.ACT_GEGLU}
 
@@ -523,6 +527,9 @@ class DecoderModel:
         hp = self.hp
         T = xn.shape[0]
         El, base = self.E_local, self.ep_base
+        if (L.moe_gu is not None and xn.is_cuda and not FUSED_ROUTER_OFF and L.experts is not None
+                and T >= MOE_DENSE_MIN_T and not torch.cuda.is_current_stream_capturing()):
+            return self._moe_dense_prefill(L, xn)
         if L.moe_gu is not None and xn.is_cuda and not FUSED_ROUTER_OFF:
             # any batch: one fused router launch (softmax, top-k, renorm, EP remap) feeds the
             # grouped expert GEMMs (row-chunked past 64 rows per expert); no host round trip
@@ -585,6 +592,39 @@ class DecoderModel:
                 h = ops.act(gu, L.F or self.F, ops.ACT_SWIGLU)
                 d = ops.reduce(ops.linear(h, down))
                 out.index_add_(0, rows, d * flat_w[sel].unsqueeze(1))
+        if L.shexp_down is not None:
+            out += self._shared_expert(L, xn)
+        self.tp.all_reduce(out)
+        return ops.Partial(out.unsqueeze(0))
+
+    def _moe_dense_prefill(self, L: Layer, xn: torch.Tensor) -> ops.Partial:
+        """Prefill-sized MoE: device routing (fused router + grouping), ONE host read of the
+        per-expert row offsets, then per expert a dense gate|up GEMM over its gathered rows, the
+        SwiGLU, the down GEMM, and a routing-weighted index_add back to the tokens (two
+        contributions per row for top-2 -- order-independent in fp32)."""
+        hp = self.hp
+        T = xn.shape[0]
+        k = hp.n_expert_used
+        El, base = self.E_local, self.ep_base
+        ids, wts = ops.moe_router(xn, L.router, k, hp.moe_renorm, hp.expert_weights_scale,
+                                  base if self.ep else 0, El if self.ep else 0)
+        order, off = ops.moe_route(ids, El + 1 if self.ep else El)
+        off_h = off.cpu().tolist()
+        order_l = order.long()
+        tok = order_l // k
+        xs = xn.index_select(0, tok)                         # [T*k, D], grouped by expert
+        wsel = wts.reshape(-1).float().index_select(0, order_l)
+        out = torch.zeros(T, hp.n_embd, dtype=torch.float32, device=xn.device)
+        with ops.blas_tuning_paused():  # per-expert row counts vary every chunk: never tune them
+            for e in range(El):
+                r0, r1 = off_h[e], off_h[e + 1]
+                if r1 <= r0:
+                    continue
+                gate_up, down = L.experts[e]
+                gu = ops.linear_multi(xs[r0:r1], gate_up)
+                h = ops.act(gu, L.F or self.F, ops.ACT_SWIGLU)
+                d = ops.reduce(ops.linear(h, down))
+                out.index_add_(0, tok[r0:r1], d * wsel[r0:r1].unsqueeze(1))
         if L.shexp_down is not None:
             out += self._shared_expert(L, xn)
         self.tp.all_reduce(out)

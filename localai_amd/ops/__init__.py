@@ -96,10 +96,21 @@ def lib():
             "la_img_resample_h": [P, I, I, P, I, P, P, I, P],
             "la_img_resample_v_tiles": [P, I, I, P, P, I, I, I, I, I, I, I, P, P, P, P, P],
         }
+        missing = []
         for name, args in sig.items():
-            fn = getattr(L, name)
+            try:
+                fn = getattr(L, name)
+            except AttributeError:
+                # a library older than these bindings (an A/B build, a stale .so): everything else
+                # still binds; calling the missing entry point fails loudly (ctypes AttributeError)
+                missing.append(name)
+                continue
             fn.argtypes = args
             fn.restype = I
+        if missing:
+            import warnings
+            warnings.warn(f"{path.name} lacks {', '.join(missing)}: rebuild it (python -c 'from localai_amd.ops "
+                          f"import _build; _build.build()')")
         L.la_gemm_scales_bytes.argtypes = [I, I]
         L.la_gemm_scales_bytes.restype = LNG
         gv = os.environ.get("LOCALAI_AMD_GEMV_VARIANT")

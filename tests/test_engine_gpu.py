@@ -84,6 +84,44 @@ def test_mixtral_moe_graph_decode(tmp_path):
     assert first == int(top.indices[0]) or float(top.values[0] - ref[first]) < 0.05
 
 
+def test_mixtral_dense_prefill_matches_grouped_and_oracle(tmp_path, monkeypatch):
+    """Prefill-sized MoE through per-expert dense GEMMs (decoder._moe_dense_prefill, forced here
+    from 1 token) vs the grouped kernel path and vs the fp32 oracle: the first sampled logits row
+    of every prompt (prefill) and the decode rows after it."""
+    from localai_amd.models import decoder, synth
+    p = str(tmp_path / "tiny-mixtral.gguf")
+    synth.write_model(p, "tiny-mixtral", exact=True)
+    prompts = ["mixture of experts " * 6, "dense prefill " * 9]
+
+    def rows(min_t):
+        monkeypatch.setattr(decoder, "MOE_DENSE_MIN_T", min_t)
+        eng = LLMEngine(EngineConfig(model_path=p, device="cuda:0", context_size=256, max_num_seqs=4,
+                                     max_batched_tokens=512, decode_steps=4, record_tokens=True, record_logits=True))
+        got = {}
+
+        def mk(i):
+            def cb(ev):
+                if ev.finished:
+                    got[i] = (ev.token_ids, ev.logits)
+            return cb
+        for i, pr in enumerate(prompts):
+            eng.add_request(pr, SamplingParams(max_tokens=4, temperature=0.0, ignore_eos=True), mk(i))
+        while len(got) < len(prompts):
+            eng.step()
+        return eng, got
+    eng_d, dense = rows(1)
+    _, grouped = rows(1 << 30)
+    for i, pr in enumerate(prompts):
+        ids = eng_d.tokenize(pr)
+        ref = eng_d.model.reference_logits(ids + dense[i][0][:-1]).float()
+        for j, row in enumerate(dense[i][1]):
+            o = ref[len(ids) - 1 + j]
+            cos = float(torch.nn.functional.cosine_similarity(row.to(o.device), o, dim=0))
+            assert cos >= 0.999, (i, j, cos)
+        a, b = dense[i][1][0].float().cpu(), grouped[i][1][0].float().cpu()
+        assert float(torch.nn.functional.cosine_similarity(a, b, dim=0)) >= 0.999
+
+
 def test_headline_path_against_fp32_oracle(tmp_path):
     """The C=256 headline decode path -- Llama-3-8B layer shapes with Q4_K_M mixed formats,
     decode batches up to 200 through the autotuned tile GEMMs, wide-batch 16-step graphs, paged
