@@ -163,7 +163,7 @@ class BertEmbedder:
     def is_ranker(self) -> bool:
         return self.cls_out_w is not None
 
-    @torch.inference_mode()
+    @torch.no_grad()
     def _hidden(self, ids: List[int], types: Optional[List[int]] = None) -> torch.Tensor:
         ids = ids[: self.max_pos]
         n = len(ids)
@@ -193,7 +193,7 @@ class BertEmbedder:
         v = x[0] if self.pooling in (2, 4) else x.mean(0)
         return F.normalize(v, dim=0)
 
-    @torch.inference_mode()
+    @torch.no_grad()
     def score(self, query: str, doc: str) -> float:
         """Cross-encoder relevance logit of (query, doc): CLS -> tanh(dense) -> 1 logit."""
         if not self.is_ranker:

@@ -185,7 +185,7 @@ class ClipVision:
         return torch.stack(tiles), (bw // S, bh // S, w, h)
 
     # ------------------------------------------------------------------ encoder
-    @torch.inference_mode()
+    @torch.no_grad()
     def encode_tiles(self, pix: torch.Tensor) -> torch.Tensor:
         """pixels [n, 3, S, S] -> projected patch embeddings [n, n_patches, out_dim] (f32)."""
         if self.native:

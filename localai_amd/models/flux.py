@@ -333,7 +333,10 @@ class FluxPipeline:
         graph.replay()
         return so.clone()
 
-    @torch.inference_mode()
+    # no_grad, not inference_mode, around every pipeline that captures hipGraphs: a capture under
+    # inference_mode creates the CUDA generator's graph-state tensors as inference tensors, and
+    # every later capture outside it (the LLM engine's decode graphs) then fails
+    @torch.no_grad()
     def __call__(self, prompt: str, negative_prompt: str = "", width: int = 1024, height: int = 1024,
                  steps: int = 28, guidance_scale: float = 3.5, seed: Optional[int] = None, image=None,
                  control_image=None) -> torch.Tensor:

@@ -147,7 +147,7 @@ class MambaLM:
         z = lambda *s: torch.zeros(*s, dtype=torch.float32, device=self.device)  # noqa: E731
         return [(z(B, self.I, self.K), z(B, self.I, self.N)) for _ in range(self.n_layer)]
 
-    @torch.inference_mode()
+    @torch.no_grad()
     def prefill(self, ids: List[int], state) -> torch.Tensor:
         """Scan the prompt (batch 1) from `state` (updated in place); -> logits [L, V] fp32."""
         L, I, K, N, R = len(ids), self.I, self.K, self.N, self.R
@@ -174,7 +174,7 @@ class MambaLM:
             h = h + self._lin(y, ly["out_proj"], ly["out_b"])
         return self._lin(self._rms(h, self.norm_f), self.lm_head)
 
-    @torch.inference_mode()
+    @torch.no_grad()
     def step(self, tokens: torch.Tensor, state) -> torch.Tensor:
         """One recurrent step for B sequences: tokens [B] -> logits [B, V]; state updated in place."""
         I, N, R = self.I, self.N, self.R

@@ -124,7 +124,7 @@ class RwkvLM:
     def _lin(self, x, wt):
         return (x.to(self.mm) @ wt.t()).float()
 
-    @torch.inference_mode()
+    @torch.no_grad()
     def step(self, tokens: torch.Tensor, state) -> torch.Tensor:
         """One token for B sequences -> logits [B, V]; state updated in place."""
         D = self.D
@@ -155,7 +155,7 @@ class RwkvLM:
         x = F.layer_norm(x, (D,), self.ln_out[0], self.ln_out[1], self.eps)
         return self._lin(x, self.head)
 
-    @torch.inference_mode()
+    @torch.no_grad()
     def prefill(self, ids: List[int], state) -> torch.Tensor:
         """Feed the prompt token by token (batch 1); -> logits [L, V]."""
         out = [self.step(torch.tensor([t], device=self.device), state)[0] for t in ids]

@@ -814,7 +814,7 @@ class StableDiffusion:
 
     _depth_map = None
 
-    @torch.inference_mode()
+    @torch.no_grad()
     def _estimate_depth(self, image, w: int, h: int) -> torch.Tensor:
         """diffusers StableDiffusionDepth2ImgPipeline.prepare_depth_map: DPT depth of the source,
         bicubic to the latent grid, min/max-scaled to [-1, 1] -> [1, 1, h, w]."""
@@ -856,7 +856,7 @@ class StableDiffusion:
         with torch.backends.cudnn.flags(enabled=True, benchmark=False, deterministic=True):
             return self._call(*args, **kw)
 
-    @torch.inference_mode()
+    @torch.no_grad()
     def _call(self, prompt: str, negative_prompt: str = "", width: int = 512, height: int = 512,
               steps: int = 1, guidance_scale: float = 7.0, seed: Optional[int] = None,
               image=None, strength: float = 0.8, control_image=None) -> torch.Tensor:

@@ -273,7 +273,7 @@ class SD3Pipeline:
         graph.replay()
         return so.clone()
 
-    @torch.inference_mode()
+    @torch.no_grad()
     def __call__(self, prompt: str, negative_prompt: str = "", width: int = 1024, height: int = 1024,
                  steps: int = 28, guidance_scale: float = 7.0, seed: Optional[int] = None, image=None,
                  control_image=None) -> torch.Tensor:

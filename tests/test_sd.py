@@ -385,3 +385,21 @@ def test_depth2img_pipeline(tmp_path):
         assert r.success, r.message
         assert Image.open(dst).size == (32, 32)
     asyncio.run(go())
+
+
+@pytest.mark.gpu
+def test_llm_graph_capture_after_diffusion_graphs(pipe_dir, tiny_model_path):
+    """A diffusion pipeline's hipGraph captures must leave the CUDA generator usable for later
+    captures outside them (an inference_mode capture turned its graph-state tensors into inference
+    tensors and every later LLM decode-graph capture in the process failed)."""
+    import torch
+    from localai_amd.engine.llm_engine import EngineConfig, LLMEngine
+    from localai_amd.engine.sampling_params import SamplingParams
+    p = StableDiffusion(pipe_dir, "cuda:0")
+    p("a cat", "", 32, 32, steps=2, seed=1)
+    assert p._graphs
+    eng = LLMEngine(EngineConfig(model_path=tiny_model_path, device="cuda:0", context_size=128, max_num_seqs=2,
+                                 max_batched_tokens=128, decode_steps=4))
+    res = eng.generate("after the unet", SamplingParams(max_tokens=6, temperature=0.0, ignore_eos=True))
+    assert res["completion_tokens"] == 6 and eng._graphs
+    torch.randn(4, device="cuda:0")  # the default generator is not left mid-capture
