@@ -16,7 +16,10 @@ def test_custom_allreduce_ranks_share_one_gpu(world):
     """2, 4 and 8 ranks (the 8-GPU node's TP=8 epoch protocol and 7-peer read pattern) sharing the
     test box's GPU: one-shot and two-shot sums, graph replay, and a late peer's timeout reaching
     every rank's error word."""
-    env = dict(os.environ, LOCALAI_AMD_AR_SAME_GPU="1")
+    # one hardware queue per rank: 8 processes x HIP's default 4 queues oversubscribe the GPU's
+    # hardware queues, so a peer's kernel could wait for a queue time slice while the others spin
+    # (a timeout on a shared device; separate GPUs never have it)
+    env = dict(os.environ, LOCALAI_AMD_AR_SAME_GPU="1", GPU_MAX_HW_QUEUES="1")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
                         "--master-addr", "127.0.0.1", "--master-port", str(29533 + world),
                         os.path.join(ROOT, "scripts", "ar_check.py")],
