@@ -117,7 +117,7 @@ __global__ __launch_bounds__(256) void moe_router_kernel(const bf16* __restrict_
 // 16 * NW columns, so NW = 8 halves the L2 -> LDS activation traffic of a wide batch (where every
 // column block of an expert re-stages the same gathered rows) and doubles the waves per CU.
 template <int FMT, int MT, bool DOWN, int NW = MOE_WAVES, bool W3 = false>
-__global__ __launch_bounds__(64 * NW, W3 ? 2 : 8 / NW) void moe_gemm_kernel(
+__global__ __launch_bounds__(64 * NW, W3 ? 2 : (NW > 8 ? 1 : 8 / NW)) void moe_gemm_kernel(
     const QW* __restrict__ qws, const int* __restrict__ order, const int* __restrict__ off, int topk,
     const bf16* __restrict__ X, int ldx, int k_per_split, const float* __restrict__ wts, float* __restrict__ out,
     int ldo, long slab, int T, int nchunk) {
@@ -278,7 +278,8 @@ static void launch_moe(const QW* qws, int N, int K, int E, const int* order, con
     // weights of an expert with more rows once per extra chunk (they come back from L2 / MALL)
     const int mt = g_moe_mt > 0 ? g_moe_mt : 4;
     if (g_moe_w3 && mt == 4 && g_moe_nw == 8) MOE_LW(4, 8, true)
-    else if (g_moe_nw == 8) {
+    else if (g_moe_nw == 16 && mt == 4) MOE_L(4, 16)
+    else if (g_moe_nw >= 8) {
       if (mt <= 4) MOE_L(4, 8) else if (mt <= 5) MOE_L(5, 8) else if (mt <= 6) MOE_L(6, 8) else MOE_L(8, 8)
     } else {
       if (mt <= 4) MOE_L(4, 4) else if (mt <= 5) MOE_L(5, 4) else if (mt <= 6) MOE_L(6, 4) else MOE_L(8, 4)
@@ -334,7 +335,7 @@ extern "C" int la_qw_size() { return (int)sizeof(la::QW); }
 
 // Tuning hook (A/B): wide-batch row tile (0 auto, 4..8) and waves per workgroup (4 or 8).
 extern "C" int la_moe_tune(int mt, int nw) {
-  if (mt < 0 || mt > 8 || (nw != 4 && nw != 8 && nw != 9)) return -1;  // nw 9: 8 waves + weight ring
+  if (mt < 0 || mt > 8 || (nw != 4 && nw != 8 && nw != 9 && nw != 16)) return -1;  // nw 9: 8 waves + weight ring
   la::g_moe_mt = mt;
   la::g_moe_nw = nw == 9 ? 8 : nw;
   la::g_moe_w3 = nw == 9;
