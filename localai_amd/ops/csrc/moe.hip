@@ -253,6 +253,7 @@ __global__ __launch_bounds__(64 * NW, W3 ? 2 : (NW > 8 ? 1 : 8 / NW)) void moe_g
 static int g_moe_mt = 0;  // 0: auto; else the row tile (MT x 16 rows) for batches past 64 rows
 static int g_moe_nw = 8;  // waves (16 columns each) per workgroup for batches past 64 rows
 static int g_moe_w3 = 0;  // three-slot weight ring (A/B)
+static int g_moe_mid8 = 0;  // 8-wave workgroups for 33..64-row batches too (A/B)
 
 template <int FMT, bool DOWN>
 static void launch_moe(const QW* qws, int N, int K, int E, const int* order, const int* off, int topk,
@@ -269,7 +270,9 @@ static void launch_moe(const QW* qws, int N, int K, int E, const int* order, con
 #define MOE_L(MT, NW) MOE_LW(MT, NW, false)
   if (maxM <= 16) MOE_L(1, 4)
   else if (maxM <= 32) MOE_L(2, 4)
-  else if (maxM <= 64) MOE_L(4, 4)
+  else if (maxM <= 64) {
+    if (g_moe_mid8) MOE_L(4, 8) else MOE_L(4, 4)
+  }
   else {
     // wide batch: 64-row tiles in 8-wave workgroups, whatever the batch.  Mixtral-8x7B, engine
     // C=256 (decode + the prefill chunks, one box): 64-row / 8 waves 3951 tok/s; 128-row / 4 waves
@@ -335,7 +338,10 @@ extern "C" int la_qw_size() { return (int)sizeof(la::QW); }
 
 // Tuning hook (A/B): wide-batch row tile (0 auto, 4..8) and waves per workgroup (4 or 8).
 extern "C" int la_moe_tune(int mt, int nw) {
-  if (mt < 0 || mt > 8 || (nw != 4 && nw != 8 && nw != 9 && nw != 16)) return -1;  // nw 9: 8 waves + weight ring
+  // nw 9: 8 waves + weight ring; nw 10: 8 waves also for 33..64-row batches
+  if (mt < 0 || mt > 8 || (nw != 4 && nw != 8 && nw != 9 && nw != 10 && nw != 16)) return -1;
+  la::g_moe_mid8 = nw == 10;
+  if (nw == 10) nw = 8;
   la::g_moe_mt = mt;
   la::g_moe_nw = nw == 9 ? 8 : nw;
   la::g_moe_w3 = nw == 9;
