@@ -253,7 +253,8 @@ __global__ __launch_bounds__(64 * NW, W3 ? 2 : (NW > 8 ? 1 : 8 / NW)) void moe_g
 static int g_moe_mt = 0;  // 0: auto; else the row tile (MT x 16 rows) for batches past 64 rows
 static int g_moe_nw = 8;  // waves (16 columns each) per workgroup for batches past 64 rows
 static int g_moe_w3 = 0;  // three-slot weight ring (A/B)
-static int g_moe_mid8 = 0;  // 8-wave workgroups for 33..64-row batches too (A/B)
+static int g_moe_mid8 = 1;   // 8-wave workgroups for 33..64-row batches too
+static int g_moe_small8 = 0; // ... and for 17..32-row batches (A/B)
 
 template <int FMT, bool DOWN>
 static void launch_moe(const QW* qws, int N, int K, int E, const int* order, const int* off, int topk,
@@ -269,8 +270,11 @@ static void launch_moe(const QW* qws, int N, int K, int E, const int* order, con
   }
 #define MOE_L(MT, NW) MOE_LW(MT, NW, false)
   if (maxM <= 16) MOE_L(1, 4)
-  else if (maxM <= 32) MOE_L(2, 4)
-  else if (maxM <= 64) {
+  else if (maxM <= 32) {
+    if (g_moe_small8) MOE_L(2, 8) else MOE_L(2, 4)
+  } else if (maxM <= 64) {
+    // 8-wave workgroups here too: Mixtral-8x7B engine C=64 3309 / 3311 tok/s vs 3047 / 3043
+    // with 4 waves (scripts/gpu_r4_t.sh)
     if (g_moe_mid8) MOE_L(4, 8) else MOE_L(4, 4)
   }
   else {
@@ -338,10 +342,12 @@ extern "C" int la_qw_size() { return (int)sizeof(la::QW); }
 
 // Tuning hook (A/B): wide-batch row tile (0 auto, 4..8) and waves per workgroup (4 or 8).
 extern "C" int la_moe_tune(int mt, int nw) {
-  // nw 9: 8 waves + weight ring; nw 10: 8 waves also for 33..64-row batches
-  if (mt < 0 || mt > 8 || (nw != 4 && nw != 8 && nw != 9 && nw != 10 && nw != 16)) return -1;
-  la::g_moe_mid8 = nw == 10;
-  if (nw == 10) nw = 8;
+  // nw 9: 8 waves + weight ring; nw 10: 4 waves for 33..64-row batches (round-3 shape);
+  // nw 11: 8 waves also for 17..32-row batches
+  if (mt < 0 || mt > 8 || (nw != 4 && nw != 8 && nw != 9 && nw != 10 && nw != 11 && nw != 16)) return -1;
+  la::g_moe_mid8 = nw != 10;
+  la::g_moe_small8 = nw == 11;
+  if (nw == 10 || nw == 11) nw = 8;
   la::g_moe_mt = mt;
   la::g_moe_nw = nw == 9 ? 8 : nw;
   la::g_moe_w3 = nw == 9;
