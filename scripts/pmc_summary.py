@@ -22,7 +22,7 @@ names = sorted({n for v in acc.values() for n in v})
 print("| kernel | " + " | ".join(names) + " |")
 print("|---|" + "---:|" * len(names))
 for k, v in acc.items():
-    if "qgemm" not in k and "attn" not in k:
+    if not any(t in k for t in (sys.argv[2].split(",") if len(sys.argv) > 2 else ("qgemm", "attn"))):
         continue
     cells = []
     for n in names:
