@@ -822,8 +822,11 @@ class LLMEngine:
                 K = min(K, self.GRAMMAR_MIXED_K)
         return max(1, min(K, rem_ctx, rem_tok))
 
-    GRAMMAR_MIXED_K = 4        # device steps per run while unlearned constrained rows ride along
-    GRAMMAR_MIXED_FRAC = 0.125  # ... when they are at most this fraction of the batch
+    # device steps per run while unlearned constrained rows ride along ...
+    GRAMMAR_MIXED_K = int(os.environ.get("LOCALAI_AMD_GRAMMAR_MIXED_K", "4"))
+    # ... when they are at most this fraction of the batch (above it: one step per round trip
+    # unless every constrained row is in a fully learned, predictable state)
+    GRAMMAR_MIXED_FRAC = float(os.environ.get("LOCALAI_AMD_GRAMMAR_MIXED_FRAC", "0.125"))
 
     def _grammar_slot_cached(self, r) -> bool:
         s = self._gmask_cache.get((r.params.grammar, r.grammar.key()))
