@@ -929,14 +929,14 @@ static int g_gv_variant = 5;  // non-temporal weight loads, x staged first, one 
 
 template <int MT, int FA, int FB>
 static int launch_gv(const GVArgs& a, int nblk, int K, const bf16* X, int ldx, const GVAct& act, int M, int splits,
-                     float* out, int ldo, long slab, hipStream_t st, const GVRope& rp) {
+                     float* out, int ldo, long slab, hipStream_t st, const GVRope& rp, int cvar) {
   const int kper = K / splits;
   const size_t lds = gv_lds_bytes(MT, kper);
   if (lds > 64 * 1024) return -3;
   dim3 grid(nblk, splits);
   // the fused-RoPE launch runs split-K 1: each workgroup walks the whole row, so it takes the
   // 4-deep weight ring (VAR bit 4) of the default variant
-  int var = (rp.q_out && g_gv_variant == 5) ? 21 : g_gv_variant;
+  int var = (rp.q_out && cvar == 5) ? 21 : cvar;
   if ((var & 16) && ((kper >> 8) % 4)) var &= ~16;  // the ring walks whole groups of 4 super-blocks
   if (act.mode == GV_NORM) {
     if (MT > 2 || (var != 5 && var != 21)) return -4;
@@ -954,10 +954,10 @@ static int launch_gv(const GVArgs& a, int nblk, int K, const bf16* X, int ldx, c
 
 template <int FA, int FB>
 static int launch_gv_m(const GVArgs& a, int nblk, int K, const bf16* X, int ldx, const GVAct& act, int M, int splits,
-                       float* out, int ldo, long slab, hipStream_t st, const GVRope& rp) {
-  if (M == 1) return launch_gv<1, FA, FB>(a, nblk, K, X, ldx, act, M, splits, out, ldo, slab, st, rp);
-  if (M == 2) return launch_gv<2, FA, FB>(a, nblk, K, X, ldx, act, M, splits, out, ldo, slab, st, rp);
-  return launch_gv<4, FA, FB>(a, nblk, K, X, ldx, act, M, splits, out, ldo, slab, st, rp);
+                       float* out, int ldo, long slab, hipStream_t st, const GVRope& rp, int cvar) {
+  if (M == 1) return launch_gv<1, FA, FB>(a, nblk, K, X, ldx, act, M, splits, out, ldo, slab, st, rp, cvar);
+  if (M == 2) return launch_gv<2, FA, FB>(a, nblk, K, X, ldx, act, M, splits, out, ldo, slab, st, rp, cvar);
+  return launch_gv<4, FA, FB>(a, nblk, K, X, ldx, act, M, splits, out, ldo, slab, st, rp, cvar);
 }
 
 }  // namespace la
@@ -992,7 +992,13 @@ static int qgemv_dp4_impl(int nseg, const int* fmts, const void* const* planes, 
   }
   GVArgs a{};
   int nblk = 0, col = 0;
-  const int rows = 32 * ((g_gv_variant & 4) ? 1 : ((g_gv_variant & 8) ? 4 : 2));  // rows per workgroup
+  // per-call variant: the default (5) except the widest batch-1 plain GEMVs (gate|up, N >= 16384),
+  // where four 8-row slots per wave measured faster (28672 x 4096 Q4_K: 18.2 vs 18.9 us,
+  // scripts/gpu_r4_gv.sh); every other shape keeps 5
+  int Nsum = 0;
+  for (int i = 0; i < nseg; ++i) Nsum += Ns[i];
+  const int cvar = (g_gv_variant == 5 && M == 1 && Nsum >= 16384 && !rp.q_out && !norm && !act_p) ? 9 : g_gv_variant;
+  const int rows = 32 * ((cvar & 4) ? 1 : ((cvar & 8) ? 4 : 2));  // rows per workgroup
   for (int i = 0; i < nseg; ++i) {
     const int f = fmts[i], N = Ns[i];
     const void* const* p = planes + 4 * i;
@@ -1021,11 +1027,11 @@ static int qgemv_dp4_impl(int nseg, const int* fmts, const void* const* planes, 
   float* o = (float*)out;
   int rc;
   if ((fa == FMT_Q8_0) != (fb == FMT_Q8_0)) return -2;  // Q8_0 weights launch on their own
-  if (fa == FMT_Q8_0) rc = launch_gv_m<FMT_Q8_0, FMT_Q8_0>(a, nblk, K, x, ldx, act, M, splits, o, ldo, slab, st, rp);
-  else if (fa == FMT_Q4_K && fb == FMT_Q4_K) rc = launch_gv_m<FMT_Q4_K, FMT_Q4_K>(a, nblk, K, x, ldx, act, M, splits, o, ldo, slab, st, rp);
-  else if (fa == FMT_Q6_K && fb == FMT_Q6_K) rc = launch_gv_m<FMT_Q6_K, FMT_Q6_K>(a, nblk, K, x, ldx, act, M, splits, o, ldo, slab, st, rp);
-  else if (fa == FMT_Q4_K) rc = launch_gv_m<FMT_Q4_K, FMT_Q6_K>(a, nblk, K, x, ldx, act, M, splits, o, ldo, slab, st, rp);
-  else rc = launch_gv_m<FMT_Q6_K, FMT_Q4_K>(a, nblk, K, x, ldx, act, M, splits, o, ldo, slab, st, rp);
+  if (fa == FMT_Q8_0) rc = launch_gv_m<FMT_Q8_0, FMT_Q8_0>(a, nblk, K, x, ldx, act, M, splits, o, ldo, slab, st, rp, cvar);
+  else if (fa == FMT_Q4_K && fb == FMT_Q4_K) rc = launch_gv_m<FMT_Q4_K, FMT_Q4_K>(a, nblk, K, x, ldx, act, M, splits, o, ldo, slab, st, rp, cvar);
+  else if (fa == FMT_Q6_K && fb == FMT_Q6_K) rc = launch_gv_m<FMT_Q6_K, FMT_Q6_K>(a, nblk, K, x, ldx, act, M, splits, o, ldo, slab, st, rp, cvar);
+  else if (fa == FMT_Q4_K) rc = launch_gv_m<FMT_Q4_K, FMT_Q6_K>(a, nblk, K, x, ldx, act, M, splits, o, ldo, slab, st, rp, cvar);
+  else rc = launch_gv_m<FMT_Q6_K, FMT_Q4_K>(a, nblk, K, x, ldx, act, M, splits, o, ldo, slab, st, rp, cvar);
   if (rc) return rc;
   return (int)hipGetLastError();
 }

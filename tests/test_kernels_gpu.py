@@ -913,3 +913,18 @@ def test_gather_rows_kernel(dtype, C):
     ref = src[idx.clamp(min=0)].clone()
     ref[idx < 0] = fill
     assert torch.equal(got, ref)
+
+
+def test_gemv_dp4_wide_batch1_variant():
+    """Batch-1 GEMVs with N >= 16384 launch with four 8-row slots per wave (per-call variant 9):
+    numerics vs fp32, repeated launches bit-identical, M=2 (variant 5) agreeing per row."""
+    N, K = 16400, 1024
+    w = _qw(N, K, GGMLType.Q4_K, seed=41)
+    x = torch.randn(2, K, device=DEV).to(torch.bfloat16)
+    ref = x.float().cpu() @ w.ref.t()
+    tol = 2e-2 * max(1.0, ref.abs().max().item())
+    y1 = ops.linear(x[:1], w, force="dp4").dense()
+    assert (y1.cpu() - ref[:1]).abs().max().item() < tol
+    assert torch.equal(y1, ops.linear(x[:1], w, force="dp4").dense())
+    y2 = ops.linear(x, w, force="dp4").dense().cpu()
+    assert (y2 - ref).abs().max().item() < tol
