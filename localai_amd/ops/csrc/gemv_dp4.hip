@@ -997,7 +997,10 @@ static int qgemv_dp4_impl(int nseg, const int* fmts, const void* const* planes, 
   // scripts/gpu_r4_gv.sh); every other shape keeps 5
   int Nsum = 0;
   for (int i = 0; i < nseg; ++i) Nsum += Ns[i];
-  const int cvar = (g_gv_variant == 5 && M == 1 && Nsum >= 16384 && !rp.q_out && !norm && !act_p) ? 9 : g_gv_variant;
+  // (at M = 2 variant 1 timed faster per GEMV -- gate|up 20.9 vs 22.0 us -- but engine C=2 did
+  // not confirm it: 733-734 tok/s; M = 2 keeps 5)
+  const bool plain = g_gv_variant == 5 && !rp.q_out && !norm && !act_p;
+  const int cvar = (plain && M == 1 && Nsum >= 16384) ? 9 : g_gv_variant;
   const int rows = 32 * ((cvar & 4) ? 1 : ((cvar & 8) ? 4 : 2));  // rows per workgroup
   for (int i = 0; i < nseg; ++i) {
     const int f = fmts[i], N = Ns[i];
