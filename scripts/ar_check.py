@@ -27,13 +27,28 @@ def expected(world, n, dtype, dev, call):
     return acc.to(dtype)
 
 
+def make_car(rank, world, dev):
+    """The IPC setup can fail transiently when 8 processes share one GPU (hipIpcGetMemHandle on a
+    fresh dmabuf export returned invalid-value on 2 of 8 ranks once); every rank learns about any
+    rank's failure in the constructor's final all-gather and raises together, so all of them retry
+    in lockstep.  (Serving never retries: maybe_create() falls back to RCCL.)"""
+    for attempt in range(3):
+        try:
+            return CustomAllReduce(dist.group.WORLD, rank, world, dev)
+        except RuntimeError as e:
+            if attempt == 2:
+                raise
+            print(f"rank {rank}: custom all-reduce setup failed ({e}); retrying", flush=True)
+            time.sleep(1.0)
+
+
 def main():
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     local = 0 if os.environ.get("LOCALAI_AMD_AR_SAME_GPU") == "1" else int(os.environ.get("LOCAL_RANK", rank))
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
     dist.init_process_group("gloo")
-    car = CustomAllReduce(dist.group.WORLD, rank, world, dev)
+    car = make_car(rank, world, dev)
     if os.environ.get("LOCALAI_AMD_AR_SAME_GPU") == "1":
         # every rank on ONE device: 8 processes x 4 HIP queues oversubscribe the hardware queues,
         # so a peer's kernel may wait for a time slice while this one spins -- allow ~16 s
@@ -142,7 +157,7 @@ def main():
     # times out; the per-step agreement (TPInfo.check_custom_ar) must fail loudly on EVERY rank
     # and drop the custom path, never hand out the stale sum silently
     from localai_amd.models.decoder import CustomAllReduceTimeout, TPInfo
-    car2 = CustomAllReduce(dist.group.WORLD, rank, world, dev)
+    car2 = make_car(rank, world, dev)
     car2.SPIN_LIMIT = 1 << 8
     tpi = TPInfo(rank=rank, world=world, group=dist.group.WORLD, car=car2)
     t = inputs(rank, 4096, torch.float32, dev, 9)
