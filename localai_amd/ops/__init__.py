@@ -92,6 +92,9 @@ def lib():
             "la_qgemm32_2": [I, P, P, P, I, I, P, P, P, I, I, P, I, I, I, P, I, LNG, I, I, P],
             "la_qgemm32_glu": [I, P, P, P, I, P, P, P, I, I, I, P, I, I, P, I, I, I, P],
             "la_qgemm32_probe": [I, I, P, P, I, I, P, I, I, P, P],
+            "la_gemm_pp": [I, P, P, P, I, I, P, I, I, I, P, I, LNG, I, P],
+            "la_gemm_pp2": [I, P, P, P, I, I, P, P, P, I, I, P, I, I, I, P, I, LNG, I, P],
+            "la_gemm_pp_glu": [I, P, P, P, I, P, P, P, I, I, I, P, I, I, P, I, I, P],
             "la_decode_advance": [P, P, P, P, P, P, I, I, I, P, I, P, P, P],
             "la_img_resample_h": [P, I, I, P, I, P, P, I, P],
             "la_img_resample_v_tiles": [P, I, I, P, P, I, I, I, I, I, I, I, P, P, P, P, P],
@@ -886,6 +889,71 @@ def _run_q32(x, ws, S, out, Ntot, var):
         _check(lib().la_qgemm32(w.fmt, p0, p1, g, w.N, w.K, x.data_ptr(), K, M, S, out.data_ptr() + col * esz, Ntot,
                                 0 if bf else M * Ntot, int(bf), var, _stream()), "la_qgemm32")
         col += w.N
+
+
+# Prefill GEMM (gemm_pp.hip): 256 x 256 ping-pong MFMA tiles with the GGUF dequantisation in the
+# kernel (Q4_K, Q6_K, bf16 weights); no bf16 weight copy, no library GEMM.
+PP_FMTS = (FMT_Q4_K, FMT_Q6_K, FMT_BF16)
+
+
+def pp_ok(ws: Sequence[QWeight], K: int, S: int = 1) -> bool:
+    """Can gemm_pp.hip run these weights (one launch per weight, or one for a two-weight pair)."""
+    kt = K // 64
+    if K % 128 or kt % S or (kt // S) % 2:
+        return False
+    if not all(w.fmt in PP_FMTS and w.K == K and w.planes[0] is not None for w in ws):
+        return False
+    return len(ws) <= 2 or all(w.fmt == ws[0].fmt for w in ws)
+
+
+def pp_splits(M: int, Ntot: int, K: int) -> int:
+    """Split-K so the grid covers the 256 CUs at least once (prefill chunks of 1-2k rows on the
+    4096-wide projections); each split keeps an even number of 64-deep K-tiles."""
+    tiles = -(-M // 256) * -(-Ntot // 256)
+    kt = K // 64
+    S = 1
+    while tiles * S < 224 and kt % (2 * S) == 0 and (kt // (2 * S)) % 2 == 0 and kt // (2 * S) >= 16:
+        S *= 2
+    return S
+
+
+def _pp_planes(w: QWeight):
+    if w.fmt == FMT_BF16:
+        return _ptr(w.planes[0]), None, None
+    return w.tile_planes()
+
+
+def _run_pp(x, ws, S, out, Ntot):
+    """out: fp32 slabs [S, M, Ntot], or a bf16 [M, Ntot] matrix (S == 1).  Two weights of one
+    output run as ONE launch."""
+    M, K = x.shape
+    bf = out.dtype == torch.bfloat16
+    esz = 2 if bf else 4
+    slab = 0 if bf else M * Ntot
+    if len(ws) == 2 and (ws[0].fmt, ws[1].fmt) in _PP2_PAIRS:
+        a0, a1, ag = _pp_planes(ws[0])
+        b0, b1, bg = _pp_planes(ws[1])
+        _check(lib().la_gemm_pp2(ws[0].fmt, a0, a1, ag, ws[0].N, ws[1].fmt, b0, b1, bg, ws[1].N, K, x.data_ptr(), K,
+                                 M, S, out.data_ptr(), Ntot, slab, int(bf), _stream()), "la_gemm_pp2")
+        return
+    col = 0
+    for w in ws:
+        p0, p1, g = _pp_planes(w)
+        _check(lib().la_gemm_pp(w.fmt, p0, p1, g, w.N, K, x.data_ptr(), K, M, S, out.data_ptr() + col * esz, Ntot,
+                                slab, int(bf), _stream()), "la_gemm_pp")
+        col += w.N
+
+
+_PP2_PAIRS = {(FMT_Q4_K, FMT_Q6_K), (FMT_Q6_K, FMT_Q4_K), (FMT_Q4_K, FMT_Q4_K)}
+
+
+def _run_pp_glu(x, pair, F: int, mode: int, out) -> None:
+    M, K = x.shape
+    wa, oa, wb, ob = pair
+    a0, a1, ag = _pp_planes(wa)
+    b0, b1, bg = _pp_planes(wb)
+    _check(lib().la_gemm_pp_glu(wa.fmt, a0, a1, ag, oa, b0, b1, bg, ob, F, K, x.data_ptr(), K, M, out.data_ptr(), F,
+                                mode, _stream()), "la_gemm_pp_glu")
 
 
 def _q32_grid(M: int, N: int, var: int) -> int:
