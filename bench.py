@@ -239,6 +239,7 @@ def main():
     sync()
     t0 = time.perf_counter()
     ttfts, tokens = [], 0
+    ev0 = getattr(runner, "events", None)
     for s_ in range(args.steps):
         tt, nt = wave(s_)
         ttfts += tt
@@ -247,6 +248,16 @@ def main():
     lbarrier()
     sync()
     elapsed = time.perf_counter() - t0
+    # the token count is the server's usage report; check it against the stream itself: ignore_eos
+    # fixes every request at max_tokens, and each generated token with non-empty text arrives as
+    # its own SSE event (counted by the clients on the wire)
+    stream_check = None
+    if ev0 is not None:
+        expect = args.steps * len(msgs) * args.max_tokens
+        events = runner.events - ev0
+        stream_check = {"expected_tokens": expect, "reported_tokens": tokens, "streamed_events": events}
+        if tokens != expect or events < 0.9 * tokens:
+            print(f"bench: stream check FAILED {stream_check}", file=sys.stderr, flush=True)
 
     all_ttft, tot_tokens, max_el = ttfts, tokens, elapsed
     if leaders is not None and n_rep > 1:
@@ -288,6 +299,8 @@ def main():
                        **({"n_draft": args.n_draft} if args.n_draft else {})},
             "setup_s": {"model_gen": round(t_gen, 1), "load": round(t_load, 1), "graph_capture": round(t_capture, 1)},
         }
+        if stream_check is not None:
+            out["stream_check"] = stream_check
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
@@ -341,6 +354,7 @@ def gateway_dp(args, eng, loadgen, rank, world, ctl, t_gen, t_load, t_capture):
         wave(-1 - w)
     t0 = time.perf_counter()
     ttfts, tokens = [], 0
+    ev0 = getattr(runner, "events", None)
     for s_ in range(args.steps):
         tt, nt = wave(s_)
         ttfts += tt
@@ -444,8 +458,10 @@ class HttpRunner:
         self.url = f"http://127.0.0.1:{self.port}/v1/chat/completions"
 
     def wave(self, contents):
-        return self.lg.wave(self.url, self.model_name, contents, self.args.max_tokens,
-                            extra={"temperature": 0, "ignore_eos": True, "mirostat": 0})
+        r = self.lg.wave(self.url, self.model_name, contents, self.args.max_tokens,
+                         extra={"temperature": 0, "ignore_eos": True, "mirostat": 0})
+        self.events = getattr(self, "events", 0) + getattr(self.lg, "last_events", 0)
+        return r
 
     def replica_stats(self):
         """Requests each replica served (gateway DP mode), from the ReplicaBackend."""

@@ -68,6 +68,61 @@ class AuthMiddleware:
         return await self.app(scope, receive, send)
 
 
+class CSRFMiddleware:
+    """Double-submit CSRF protection behind --csrf / LOCALAI_CSRF (reference:
+    core/http/app.go:146-148, fiber's csrf.New() defaults).  A safe request (GET, HEAD, OPTIONS,
+    TRACE) is issued a token in the `csrf_` cookie (SameSite=Lax, 1 h); a state-changing request
+    must echo that token in the X-Csrf-Token header, and the token must be one this server
+    issued and has not expired -- otherwise 403 Forbidden before any handler runs."""
+
+    SAFE = frozenset({"GET", "HEAD", "OPTIONS", "TRACE"})
+    COOKIE, HEADER, TTL = "csrf_", "x-csrf-token", 3600.0
+
+    def __init__(self, app):
+        self.app = app
+        self.tokens: dict = {}   # token -> expiry (monotonic seconds)
+
+    def _valid(self, tok: str, now: float) -> bool:
+        exp = self.tokens.get(tok)
+        if exp is None:
+            return False
+        if exp < now:
+            self.tokens.pop(tok, None)
+            return False
+        return True
+
+    def _issue(self, now: float) -> str:
+        import secrets
+        if len(self.tokens) > 4096:   # drop expired entries before growing further
+            for k in [k for k, e in self.tokens.items() if e < now]:
+                del self.tokens[k]
+        tok = secrets.token_urlsafe(24)
+        self.tokens[tok] = now + self.TTL
+        return tok
+
+    async def __call__(self, scope, receive, send):
+        if scope["type"] != "http":
+            return await self.app(scope, receive, send)
+        request = Request(scope)
+        now = time.monotonic()
+        cookie = request.cookies.get(self.COOKIE, "")
+        if request.method.upper() not in self.SAFE:
+            header = request.headers.get(self.HEADER, "")
+            if not header or not cookie or not hmac.compare_digest(header, cookie) or not self._valid(cookie, now):
+                return await Response("Forbidden", status_code=403)(scope, receive, send)
+            return await self.app(scope, receive, send)
+        tok = cookie if cookie and self._valid(cookie, now) else self._issue(now)
+        self.tokens[tok] = now + self.TTL   # a token in use is refreshed
+        set_cookie = f"{self.COOKIE}={tok}; Path=/; Max-Age={int(self.TTL)}; SameSite=Lax".encode()
+
+        async def send_wrap(msg):
+            if msg["type"] == "http.response.start":
+                msg = dict(msg)
+                msg["headers"] = list(msg.get("headers", [])) + [(b"set-cookie", set_cookie)]
+            await send(msg)
+        return await self.app(scope, receive, send_wrap)
+
+
 class MetricsMiddleware:
     """api_call{method,path} histogram (time to response start, like fiber's middleware)."""
 
@@ -128,6 +183,9 @@ def create_app(state: AppState) -> FastAPI:
     if not cfg.disable_metrics:
         app.add_middleware(MetricsMiddleware, state=state)
     app.add_middleware(AuthMiddleware, state=state)
+    if cfg.csrf:
+        log.debug("CSRF middleware enabled: state-changing requests need the X-Csrf-Token header")
+        app.add_middleware(CSRFMiddleware)
     if cfg.cors:
         from starlette.middleware.cors import CORSMiddleware
         origins = [o for o in cfg.cors_allow_origins.split(",") if o] or ["*"]

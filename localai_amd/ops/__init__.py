@@ -817,8 +817,10 @@ GQ_TILES = {0: (256, 256), 1: (256, 128), 2: (128, 256), 3: (128, 128), 4: (256,
             10: (256, 256), 11: (256, 128), 13: (128, 128), 16: (256, 256), 17: (128, 256)}
 # LOCALAI_AMD_TILE_GEMM=0 restores the round-2 path (hipBLASLt on bf16 weight copies + qgemm_mid)
 TILE_GEMM = os.environ.get("LOCALAI_AMD_TILE_GEMM", "1") == "1"
-# M > MID_MAX_M (prefill chunks): "blas" = dequantise into a scratch buffer + library GEMM (faster
-# than the tile kernel at M = 8192 today: profiles/r3_gemm_tile.md), "tile" = the tile kernel
+# M > MID_MAX_M (prefill chunks): "blas" = dequantise into a scratch buffer + library GEMM, "pp" =
+# gemm_pp.hip (in-kernel dequant, no bf16 copy), "tile" = gemm_q.hip.  gate|up always takes the
+# fused gemm_pp GLU (PP_GLU); the other projections stay on "blas", still 1.0-1.4x faster there at
+# M = 2048 / 8192 (profiles/r5_prefill_gemm.md)
 PREFILL_GEMM = os.environ.get("LOCALAI_AMD_PREFILL_GEMM", "blas")
 
 
@@ -899,7 +901,7 @@ PP_FMTS = (FMT_Q4_K, FMT_Q6_K, FMT_BF16)
 def pp_ok(ws: Sequence[QWeight], K: int, S: int = 1) -> bool:
     """Can gemm_pp.hip run these weights (one launch per weight, or one for a two-weight pair)."""
     kt = K // 64
-    if K % 128 or kt % S or (kt // S) % 2:
+    if K % 256 or kt % S or (kt // S) % 4:
         return False
     if not all(w.fmt in PP_FMTS and w.K == K and w.planes[0] is not None for w in ws):
         return False
@@ -912,7 +914,7 @@ def pp_splits(M: int, Ntot: int, K: int) -> int:
     tiles = -(-M // 256) * -(-Ntot // 256)
     kt = K // 64
     S = 1
-    while tiles * S < 224 and kt % (2 * S) == 0 and (kt // (2 * S)) % 2 == 0 and kt // (2 * S) >= 16:
+    while tiles * S < 224 and kt % (2 * S) == 0 and (kt // (2 * S)) % 4 == 0 and kt // (2 * S) >= 16:
         S *= 2
     return S
 
@@ -1100,9 +1102,18 @@ def linear_multi(x: torch.Tensor, ws: Sequence[QWeight], bias: Optional[torch.Te
     elif force is None and not use_skinny and tile_ok and PREFILL_GEMM == "tile":
         tile, S = pick_tile(M, [w.N for w in ws], K)   # prefill: heuristic, never tuned inline
         kind = "tile"
-    if kind in ("tile", "q32") and S == 1 and out_slabs is None:
+    elif (force == "pp" or (force is None and not use_skinny and M > MID_MAX_M and PREFILL_GEMM == "pp")) \
+            and pp_ok(ws, K) and (len(ws) == 1 or (len(ws) == 2 and (ws[0].fmt, ws[1].fmt) in _PP2_PAIRS)
+                                 or all(w.fmt == ws[0].fmt for w in ws)):
+        S, kind = pp_splits(M, Ntot, K), "pp"
+        while S > 1 and not pp_ok(ws, K, S):
+            S //= 2
+    if kind in ("tile", "q32", "pp") and S == 1 and out_slabs is None:
         y = torch.empty(M, Ntot, dtype=torch.bfloat16, device=x.device)
-        (_run_tile if kind == "tile" else _run_q32)(x, ws, 1, y, Ntot, tile)
+        if kind == "pp":
+            _run_pp(x, ws, 1, y, Ntot)
+        else:
+            (_run_tile if kind == "tile" else _run_q32)(x, ws, 1, y, Ntot, tile)
         return Partial(y, bias)
     if S:
         out = out_slabs
@@ -1110,6 +1121,8 @@ def linear_multi(x: torch.Tensor, ws: Sequence[QWeight], bias: Optional[torch.Te
             out = torch.empty(S, M, Ntot, dtype=torch.float32, device=x.device)
         if kind == "tile":
             _run_tile(x, ws, S, out, Ntot, tile)
+        elif kind == "pp":
+            _run_pp(x, ws, S, out, Ntot)
         elif kind == "q32":
             _run_q32(x, ws, S, out, Ntot, tile)
         elif kind == "ws":
@@ -1149,6 +1162,8 @@ def linear_multi(x: torch.Tensor, ws: Sequence[QWeight], bias: Optional[torch.Te
 
 
 GLU_FUSE = os.environ.get("LOCALAI_AMD_GLU_FUSE", "1") == "1"
+PP_GLU = os.environ.get("LOCALAI_AMD_PP_GLU", "1") == "1"   # prefill gate|up on gemm_pp.hip
+PP_GLU_MIN_M = 1024   # below ~4 row tiles the 256 x 256 grid leaves CUs idle
 _GLU_CHOICE: Dict[tuple, Optional[int]] = {}
 
 
@@ -1200,7 +1215,17 @@ def glu_linear(x: torch.Tensor, ws: Sequence[QWeight], F: int, mode: int,
     if not (GLU_FUSE and TILE_GEMM and x.is_cuda and bias is None and mode in GLU_ACTS):
         return None
     M, K = x.shape
-    if M <= SKINNY_MAX_M or M > MID_MAX_M:
+    if M > MID_MAX_M:
+        # prefill chunks: gemm_pp.hip's fused GLU (gate and up of one index share a 256-wide tile,
+        # the activation runs in the epilogue) beats dequant + hipBLASLt + the activation kernel
+        # at every prefill size measured (profiles/r5_prefill_gemm.md)
+        pair = _glu_pair(ws, F) if PP_GLU and M >= PP_GLU_MIN_M else None
+        if pair is None or pair[0].fmt != pair[2].fmt or not pp_ok([pair[0], pair[2]], K):
+            return None
+        out = torch.empty(M, F, dtype=torch.bfloat16, device=x.device)
+        _run_pp_glu(x, pair, F, mode, out)
+        return out
+    if M <= SKINNY_MAX_M:
         return None
     pair = _glu_pair(ws, F)
     if pair is None:

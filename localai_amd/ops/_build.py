@@ -26,6 +26,11 @@ def _torch_lib() -> str:
     return str(Path(spec.origin).parent / "lib")
 
 
+# per-file hipcc flags: the prefill GEMM's dequant runs beside MFMAs, where the packed
+# v_pk_fma_f32 the SLP vectoriser forms issues slower than two scalar FMAs (profiles/r5_prefill_gemm.md)
+FILE_FLAGS = {"gemm_pp.hip": ["-fno-slp-vectorize"]}
+
+
 def _sources():
     return sorted(CSRC.glob("*.hip"))
 
@@ -36,6 +41,7 @@ def _digest() -> str:
         h.update(p.name.encode())
         h.update(p.read_bytes())
     h.update(ARCH.encode())
+    h.update(repr(sorted(FILE_FLAGS.items())).encode())
     return h.hexdigest()[:16]
 
 
@@ -68,7 +74,7 @@ def _build_lib(LIB: Path, defines, force: bool, verbose: bool, jobs: int) -> Pat
 
     def compile_one(src: Path) -> Path:
         obj = objdir / (src.stem + ".o")
-        cmd = [_hipcc(), *flags, "-c", str(src), "-o", str(obj)]
+        cmd = [_hipcc(), *flags, *FILE_FLAGS.get(src.name, []), "-c", str(src), "-o", str(obj)]
         if verbose:
             print(" ".join(cmd), flush=True)
         r = subprocess.run(cmd, capture_output=True, text=True)

@@ -4,7 +4,12 @@ measuring client never shares a GIL with the server under test.
     python -m localai_amd.utils.loadgen        (reads one JSON job per stdin line)
 
 job  = {"url", "model", "contents": [...], "max_tokens", "extra": {...}}
-reply= {"ttft": [s...], "tokens": n, "errors": k}   (one JSON line per job)
+reply= {"ttft": [s...], "tokens": n, "events": e, "errors": k}   (one JSON line per job)
+
+`tokens` is the server's final usage.completion_tokens; `events` is counted on the wire: the SSE
+events that carried non-empty generated text (the server emits one per token, skipping tokens
+whose text is empty, e.g. half of a UTF-8 sequence), so the caller can check the reported count
+against what was actually streamed.
 """
 from __future__ import annotations
 
@@ -30,6 +35,7 @@ async def _wave(job) -> dict:
             t0 = time.perf_counter()
             ttft = None
             ntok = 0
+            nev = 0
             try:
                 async with sess.post(job["url"], json=body) as resp:
                     resp.raise_for_status()
@@ -39,8 +45,10 @@ async def _wave(job) -> dict:
                         data = raw[5:].strip()
                         if data == b"[DONE]":
                             break
-                        if ttft is None and b'"content":""' not in data and b'"content"' in data:
-                            ttft = time.perf_counter() - t0
+                        if b'"content":""' not in data and (b'"content":"' in data or b'"text":"' in data):
+                            nev += 1
+                            if ttft is None:
+                                ttft = time.perf_counter() - t0
                         u = data.rfind(b'"completion_tokens":')
                         if u >= 0:
                             e = u + 20
@@ -49,9 +57,10 @@ async def _wave(job) -> dict:
                             ntok = int(data[u + 20:e])
             except Exception:
                 errors += 1
-            return (ttft if ttft is not None else time.perf_counter() - t0), ntok
+            return (ttft if ttft is not None else time.perf_counter() - t0), ntok, nev
         res = await asyncio.gather(*[one(c) for c in job["contents"]])
-    return {"ttft": [r[0] for r in res], "tokens": sum(r[1] for r in res), "errors": errors}
+    return {"ttft": [r[0] for r in res], "tokens": sum(r[1] for r in res), "events": sum(r[2] for r in res),
+            "errors": errors}
 
 
 def _main():
@@ -87,14 +96,16 @@ class LoadGen:
             p.stdin.write(json.dumps({"url": url, "model": model, "contents": part, "max_tokens": max_tokens,
                                       "extra": extra or {}}) + "\n")
             p.stdin.flush()
-        ttft, tokens, errors = [], 0, 0
+        ttft, tokens, events, errors = [], 0, 0, 0
         for p, part in zip(self.procs, parts):
             r = json.loads(p.stdout.readline())
             ttft += r["ttft"]
             tokens += r["tokens"]
+            events += r["events"]
             errors += r["errors"]
         if errors:
             raise RuntimeError(f"{errors} streaming requests failed")
+        self.last_events = events
         return ttft, tokens
 
     def close(self):

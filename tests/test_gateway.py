@@ -334,3 +334,31 @@ def test_browse_gallery_actions_install_and_delete(engine, tmp_path_factory):
             time.sleep(0.05)
         assert "data-act=install" in txt
 
+
+
+def test_csrf_middleware(engine, tmp_path_factory):
+    """--csrf (reference core/http/app.go:146-148): a state-changing POST without the token is
+    refused with 403 before any handler runs; GET hands out the csrf_ cookie, and echoing it in
+    X-Csrf-Token lets the same POST through.  A forged or stale token is refused."""
+    from fastapi.testclient import TestClient
+    from localai_amd.gateway.app import create_app_for_engine
+    ac = _app_config(tmp_path_factory)
+    ac.csrf = True
+    app, name = create_app_for_engine(engine, name="tiny", app_config=ac)
+    body = {"model": name, "input": "hi"}
+    with TestClient(app) as c:
+        assert c.post("/v1/tokenize", json=body).status_code == 403
+        r = c.get("/v1/models")
+        assert r.status_code == 200
+        tok = r.cookies.get("csrf_")
+        assert tok
+        assert c.post("/v1/tokenize", json=body, headers={"X-Csrf-Token": "forged"}).status_code == 403
+        ok = c.post("/v1/tokenize", json=body, headers={"X-Csrf-Token": tok})
+        assert ok.status_code == 200, ok.text
+        c.cookies.clear()
+        c.cookies.set("csrf_", "never-issued")
+        assert c.post("/v1/tokenize", json=body, headers={"X-Csrf-Token": "never-issued"}).status_code == 403
+    ac2 = _app_config(tmp_path_factory)
+    app2, _ = create_app_for_engine(engine, name="tiny", app_config=ac2)
+    with TestClient(app2) as c:   # off by default
+        assert c.post("/v1/tokenize", json=body).status_code == 200
