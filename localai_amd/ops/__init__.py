@@ -818,9 +818,8 @@ GQ_TILES = {0: (256, 256), 1: (256, 128), 2: (128, 256), 3: (128, 128), 4: (256,
 # LOCALAI_AMD_TILE_GEMM=0 restores the round-2 path (hipBLASLt on bf16 weight copies + qgemm_mid)
 TILE_GEMM = os.environ.get("LOCALAI_AMD_TILE_GEMM", "1") == "1"
 # M > MID_MAX_M (prefill chunks): "blas" = dequantise into a scratch buffer + library GEMM, "pp" =
-# gemm_pp.hip (in-kernel dequant, no bf16 copy), "tile" = gemm_q.hip.  gate|up always takes the
-# fused gemm_pp GLU (PP_GLU); the other projections stay on "blas", still 1.0-1.4x faster there at
-# M = 2048 / 8192 (profiles/r5_prefill_gemm.md)
+# gemm_pp.hip (in-kernel dequant, no bf16 copy), "tile" = gemm_q.hip.  "blas" stays the default:
+# it is still 1.0-1.4x faster than gemm_pp at M = 2048 / 8192 (profiles/r5_prefill_gemm.md)
 PREFILL_GEMM = os.environ.get("LOCALAI_AMD_PREFILL_GEMM", "blas")
 
 
@@ -1162,7 +1161,7 @@ def linear_multi(x: torch.Tensor, ws: Sequence[QWeight], bias: Optional[torch.Te
 
 
 GLU_FUSE = os.environ.get("LOCALAI_AMD_GLU_FUSE", "1") == "1"
-PP_GLU = os.environ.get("LOCALAI_AMD_PP_GLU", "1") == "1"   # prefill gate|up on gemm_pp.hip
+PP_GLU = os.environ.get("LOCALAI_AMD_PP_GLU", "0") == "1"   # prefill gate|up on gemm_pp.hip
 PP_GLU_MIN_M = 1024   # below ~4 row tiles the 256 x 256 grid leaves CUs idle
 _GLU_CHOICE: Dict[tuple, Optional[int]] = {}
 
@@ -1217,8 +1216,9 @@ def glu_linear(x: torch.Tensor, ws: Sequence[QWeight], F: int, mode: int,
     M, K = x.shape
     if M > MID_MAX_M:
         # prefill chunks: gemm_pp.hip's fused GLU (gate and up of one index share a 256-wide tile,
-        # the activation runs in the epilogue) beats dequant + hipBLASLt + the activation kernel
-        # at every prefill size measured (profiles/r5_prefill_gemm.md)
+        # the activation runs in the epilogue).  Opt-in (LOCALAI_AMD_PP_GLU=1): it is still ~1.3x
+        # slower than dequant + hipBLASLt + the activation kernel at M = 8192, and the engine
+        # A/B lost 30 ms of p50 TTFT with it (profiles/r5_prefill_gemm.md)
         pair = _glu_pair(ws, F) if PP_GLU and M >= PP_GLU_MIN_M else None
         if pair is None or pair[0].fmt != pair[2].fmt or not pp_ok([pair[0], pair[2]], K):
             return None
