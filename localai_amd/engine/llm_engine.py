@@ -238,33 +238,66 @@ class LLMEngine:
 
     # ------------------------------------------------------------------ setup
     def _materialize_bf16(self, only_non_tile: bool = False):
+        """bf16 copies for the weights the quantised GEMMs cannot read (only_non_tile), or for all
+        of them (legacy LOCALAI_AMD_TILE_GEMM=0 path).  The copies for non-tile formats are a speed
+        option (no re-dequantisation of Q5_K / Q3_K / IQ* ... per call), so they are made only when
+        they fit: after them the KV cache must still get every block the config asks for within
+        gpu_memory_utilization (a 70B Q5_K_M would otherwise gain ~140 GB of copies and stop
+        loading).  LOCALAI_AMD_BF16_COPIES=always|never overrides; the bytes spent are logged."""
         m = self.model
 
         def want(ws) -> bool:
             return not only_non_tile or not all(w.tile_ok for w in ws)
+        groups = []
         for L in m.layers:
             for grp in (L.qkv, L.gate_up, [L.wo]) + (([L.down],) if L.down is not None else ()):
                 if want(grp):
-                    for w in grp:
-                        w.materialize_bf16()
-                    if len(grp) > 1:
-                        ops.fuse_bf16(grp)   # one library GEMM for a mixed-format q|k + v
+                    groups.append(grp)
             if L.experts and not only_non_tile:   # (the grouped MoE kernels read their own planes)
                 for gu, d in L.experts:
                     for grp in (gu, [d]):
                         if want(grp):
-                            for w in grp:
-                                w.materialize_bf16()
+                            groups.append(grp)
         if want([m.output]):
-            m.output.materialize_bf16()
-        torch.cuda.synchronize(self.device)
+            groups.append([m.output])
+        need = sum(w.N * w.K * 2 for grp in groups for w in grp if w.bf16 is None and w.fmt != ops.FMT_BF16)
+        if not need:
+            return
+        policy = os.environ.get("LOCALAI_AMD_BF16_COPIES", "auto")
+        if policy == "never" and only_non_tile:
+            log.info("bf16 copies disabled: %.2f GB of weights stay quantised (dequantised per call)", need / 2**30)
+            return
+        if policy == "auto" and only_non_tile and self.device.type == "cuda":
+            free, total = torch.cuda.mem_get_info(self.device)
+            budget = int(free - (1.0 - self.cfg.gpu_memory_utilization) * total) - (4 << 30)
+            kv = self._kv_blocks_wanted() * self._kv_block_bytes()
+            if need > budget - kv:
+                log.warning("not materialising %.2f GB of bf16 weight copies (%.2f GB left after the %.2f GB KV "
+                            "cache): those weights are dequantised per call", need / 2**30,
+                            max(0, budget - kv) / 2**30, kv / 2**30)
+                return
+        for grp in groups:
+            for w in grp:
+                w.materialize_bf16()
+            if len(grp) > 1:
+                ops.fuse_bf16(grp)   # one library GEMM for a mixed-format q|k + v
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        log.info("materialised %.2f GB of bf16 weight copies", need / 2**30)
+
+    def _kv_block_bytes(self) -> int:
+        return 2 * self.hp.n_layer * self.model.Hkv * self.cfg.block_size * self.model.Dh * 2
+
+    def _kv_blocks_wanted(self) -> int:
+        cfg = self.cfg
+        bs = cfg.block_size
+        want_tokens = cfg.max_kv_tokens or cfg.max_num_seqs * self.ctx
+        return (want_tokens + bs - 1) // bs + cfg.max_num_seqs + 4
 
     def _num_kv_blocks(self) -> int:
         cfg = self.cfg
-        bs = cfg.block_size
-        bpb = 2 * self.hp.n_layer * self.model.Hkv * bs * self.model.Dh * 2
-        want_tokens = cfg.max_kv_tokens or cfg.max_num_seqs * self.ctx
-        want = (want_tokens + bs - 1) // bs + cfg.max_num_seqs + 4
+        bpb = self._kv_block_bytes()
+        want = self._kv_blocks_wanted()
         if self.device.type == "cuda":
             free, total = torch.cuda.mem_get_info(self.device)
             budget = int(free - (1.0 - cfg.gpu_memory_utilization) * total) - (4 << 30)

@@ -46,6 +46,8 @@ _ACT = {"swiglu": ops.ACT_SWIGLU, "gelu": ops.ACT_GELU, "geglu": ops.ACT_GEGLU}
 
 
 TP_AR_BF16 = os.environ.get("LOCALAI_AMD_TP_AR_BF16", "1") == "1"
+TP_AR_BF16_MAX_ROWS = 512           # decode batches only; prefill chunks reduce in fp32
+ALLREDUCE_ADD_NORM_MAX_SLABS = 64   # allreduce.hip la_allreduce_add_norm rejects more split-K slabs
 
 
 class CustomAllReduceTimeout(RuntimeError):
@@ -463,11 +465,17 @@ class DecoderModel:
     def _row_parallel_out(self, p: ops.Partial, bias) -> ops.Partial:
         if self.tp.world == 1:
             return ops.Partial(p.t, bias)
-        if self._defer_ar and p.t.is_cuda and p.bias is None:
+        if self._defer_ar and p.t.is_cuda and p.bias is None and p.S <= ALLREDUCE_ADD_NORM_MAX_SLABS:
+            # (the fused AR + add + norm kernel takes at most 64 split-K slabs; a MoE down
+            # projection's S * top-k slabs take the reduce + all-reduce path below)
             return PendingAR(p, bias)
-        if TP_AR_BF16 and p.t.is_cuda:
+        car = self.tp.car
+        if (TP_AR_BF16 and p.t.is_cuda and p.M <= TP_AR_BF16_MAX_ROWS and car is not None
+                and p.M * p.N <= max(car.max_elems, car.max_elems2)):
             # decode rows travel in bf16 (16 KiB per 8192-wide row): half the bytes
-            # of the fp32 sum over xGMI; the consumer (add_norm) reads a bf16 matrix directly
+            # of the fp32 sum over xGMI; the consumer (add_norm) reads a bf16 matrix directly.
+            # Only where the custom one-/two-shot all-reduce (fp32 accumulate) takes it: an RCCL
+            # ring would round at every step, and prefill-size sums keep fp32 at every chunk size
             dense = ops.reduce(p, dtype=torch.bfloat16)
             self.tp.all_reduce(dense)
             return ops.Partial(dense, bias)

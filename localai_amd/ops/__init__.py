@@ -48,10 +48,6 @@ def lib():
         P, I, F, LNG = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_long
         sig = {
             "la_qgemm_skinny": [I, P, P, P, P, I, I, P, I, I, I, P, I, LNG, P],
-            "la_qgemm_mid": [I, P, P, P, P, I, I, P, I, I, I, P, I, LNG, I, P],
-            "la_qgemm_ws": [I, P, P, P, P, I, I, P, I, I, I, P, I, LNG, P],
-            "la_dq_swizzle": [I, P, P, P, I, I, P, P, P],
-            "la_qgemm_dq": [I, P, P, I, I, P, I, I, I, P, I, LNG, I, I, P],
             "la_qgemv_dp4": [I, P, P, P, I, P, I, I, I, P, I, LNG, P, LNG, I, P, I, P],
             "la_moe_gemv": [I, I, P, I, I, I, P, I, I, P, I, I, P, LNG, I, I, P, P, I, LNG, P],
             "la_gemv_variant": [I],
@@ -161,7 +157,6 @@ class QWeight:
     planes: Tuple[Optional[torch.Tensor], ...]   # p0..p3 device planes (GPU path)
     ref: Optional[torch.Tensor] = None            # fp32 [N, K] (CPU path / oracle)
     bf16: Optional[torch.Tensor] = None           # optional HBM-resident bf16 copy (prefill GEMMs)
-    dq: Optional[Tuple[torch.Tensor, torch.Tensor]] = None  # fragment-ordered Q4_K copy (gemm_dq.hip)
     gsc: Optional[torch.Tensor] = None            # blocked per-(column, K-step) scale plane (gemm_q.hip)
 
     @property
@@ -239,26 +234,6 @@ class QWeight:
                 self.bf16 = out
         return self.bf16
 
-    @property
-    def dq_ok(self) -> bool:
-        """Can feed the in-register-dequant batch GEMM (gemm_dq.hip): Q4_K with its unpacked
-        scale planes."""
-        return self.fmt == FMT_Q4_K and self.planes[2] is not None and self.K % 256 == 0
-
-    def dq_planes(self) -> Tuple[torch.Tensor, torch.Tensor]:
-        """Fragment-ordered copy for gemm_dq.hip, built once on the device: codes [NB][K/64][64][16 B]
-        and per-(column, K-step) scale records [NB/4][K/64][4][32][8 B] (0.625 B per weight), NB =
-        32-column blocks with N padded to the kernel's 256-column tile."""
-        if self.dq is None:
-            nb, ks = (self.N + 255) // 256 * 8, self.K // 64
-            qsw = torch.empty(nb * ks * 1024, dtype=torch.uint8, device=self.device)
-            ssw = torch.empty(nb // 4 * ks * 1024, dtype=torch.uint8, device=self.device)
-            _check(lib().la_dq_swizzle(self.fmt, _ptr(self.planes[0]), _ptr(self.planes[2]), _ptr(self.planes[3]),
-                                       self.N, self.K, qsw.data_ptr(), ssw.data_ptr(), _stream()), "la_dq_swizzle")
-            self.dq = (qsw, ssw)
-        return self.dq
-
-    @property
     def tile_ok(self) -> bool:
         """Can feed the quantised tile GEMM (gemm_q.hip)."""
         return self.K % 256 == 0 and self.fmt in (FMT_Q4_K, FMT_Q6_K, FMT_Q8_0, FMT_BF16) and self.planes[0] is not None
@@ -572,76 +547,11 @@ def qkv_rope_dp4(x: torch.Tensor, ws: Sequence[QWeight], pos: torch.Tensor, slot
 SKINNY_MAX_M = 64
 GEMV_MAX_M = 2           # M <= GEMV_MAX_M: int8-dot decode GEMV (gemv_dp4.hip, supports M <= 4) on Q4_K/Q6_K
 GEMV_DP4 = os.environ.get("LOCALAI_AMD_GEMV", "dp4") == "dp4"
-MID_MAX_M = 256          # 64 < M <= MID_MAX_M: quantised mid-M MFMA GEMM (gemm_mid.hip) or hipBLASLt
-MID_FMTS = (FMT_Q4_K, FMT_Q6_K, FMT_Q8_0)
+MID_MAX_M = 256          # 64 < M <= MID_MAX_M: quantised MFMA tile GEMMs (gemm_q.hip / gemm_q32.hip), autotuned
 GEMM_AUTOTUNE = True
-# gemm_dq.hip joins the autotune candidates only on request: it needs a second (fragment-ordered)
-# copy of every Q4_K weight it times, and measured on par with qgemm_mid / hipBLASLt at decode
-# batch 256 (profiles/decode_gemv_study.md §5)
-GEMM_DQ = os.environ.get("LOCALAI_AMD_DQ", "0") == "1"
-# (M, K, ((fmt, N), ...)) -> ("mid", S) | ("blas", 0); filled by _autotune_mid at warm-up (eager
-# runs before each decode-graph capture), consulted during capture / replay.
+# (M, K, ((fmt, N), ...)) -> (kind, S, variant); filled by _autotune_mid at warm-up (eager runs
+# before each decode-graph capture), consulted during capture / replay.
 _GEMM_CHOICE: dict = {}
-
-
-def _mid_split_ok(K: int, S: int) -> bool:
-    ks = K // 64
-    return S >= 1 and -(-ks // S) * (S - 1) < ks
-
-
-def pick_mid_splits(N: int, K: int, M: int) -> int:
-    """Default split-K for the mid-M GEMM when no tuned choice exists: ~2 workgroups per CU,
-    every split >= 8 K-steps of 64, fp32 slab round trip kept below the weight bytes."""
-    tiles = ((N + 127) // 128) * ((M + 127) // 128)
-    ksteps = K // 64
-    s = max(1, min(ksteps // 8, round(512 / tiles)))
-    while s > 1 and s * M * N * 4 * 2 > N * K:
-        s -= 1
-    while s > 1 and not _mid_split_ok(K, s):
-        s -= 1
-    return s
-
-
-def _run_mid(x, ws, S, out, Ntot, tile=0):
-    M, K = x.shape
-    col = 0
-    for w in ws:
-        _check(lib().la_qgemm_mid(w.fmt, *w.ptrs(), w.N, w.K, x.data_ptr(), K, M, S, out.data_ptr() + col * 4,
-                                  Ntot, M * Ntot, tile, _stream()), "la_qgemm_mid")
-        col += w.N
-
-
-def _ws_ok(ws, K: int, S: int) -> bool:
-    """Warp-specialised LDS-DMA GEMM (gemm_ws.hip): Q4_K weights, equal K splits."""
-    return all(w.fmt == FMT_Q4_K for w in ws) and (K // 64) % S == 0
-
-
-def _run_ws(x, ws, S, out, Ntot):
-    M, K = x.shape
-    col = 0
-    for w in ws:
-        _check(lib().la_qgemm_ws(w.fmt, *w.ptrs(), w.N, w.K, x.data_ptr(), K, M, S, out.data_ptr() + col * 4,
-                                 Ntot, M * Ntot, _stream()), "la_qgemm_ws")
-        col += w.N
-
-
-def _dq_ok(ws, K: int, S: int) -> bool:
-    """In-register-dequant GEMM (gemm_dq.hip): Q4_K weights, equal K splits."""
-    return all(w.dq_ok for w in ws) and (K // 64) % S == 0
-
-
-def _run_dq(x, ws, S, out, Ntot, wnt=2):
-    """out: fp32 slabs [S, M, Ntot], or a bf16 [M, Ntot] matrix (S == 1)."""
-    M, K = x.shape
-    bf = out.dtype == torch.bfloat16
-    col = 0
-    for w in ws:
-        qsw, ssw = w.dq_planes()
-        esz = 2 if bf else 4
-        _check(lib().la_qgemm_dq(w.fmt, qsw.data_ptr(), ssw.data_ptr(), w.N, w.K, x.data_ptr(), K, M, S,
-                                 out.data_ptr() + col * esz, Ntot, 0 if bf else M * Ntot, int(bf), wnt, _stream()),
-               "la_qgemm_dq")
-        col += w.N
 
 
 def blas_tuning_start(path: Optional[str] = None) -> bool:
@@ -737,6 +647,7 @@ def fuse_bf16(ws: Sequence[QWeight]) -> Optional[torch.Tensor]:
 
 
 _SCRATCH: dict = {}
+_SCRATCH_LOCK = threading.Lock()
 
 
 def _scratch(device, need: int) -> torch.Tensor:
@@ -744,18 +655,30 @@ def _scratch(device, need: int) -> torch.Tensor:
 
     One buffer per (device, thread): two engines serving from different threads on one GPU
     (in-process whisper / CLIP / a second LLM) enqueue their dequant + GEMM pairs interleaved,
-    so a shared buffer would hand one engine's GEMM the other's weights.  Inside a stream
-    capture the buffer is allocated fresh from the graph's private pool instead: a replayed
-    graph must never write into memory that a later (larger) scratch reallocation returned to
-    the caching allocator."""
+    so a shared buffer would hand one engine's GEMM the other's weights.  Entries of threads that
+    have exited are dropped on the next call, so an executor pool's turnover does not keep one
+    large buffer per dead thread (VRAM outside the KV budget).  Inside a stream capture the buffer
+    is allocated fresh from the graph's private pool instead: a replayed graph must never write
+    into memory that a later (larger) scratch reallocation returned to the caching allocator."""
     if torch.cuda.is_current_stream_capturing():
         return torch.empty(need, dtype=torch.bfloat16, device=device)
     key = (device, threading.get_ident())
-    buf = _SCRATCH.get(key)
-    if buf is None or buf.numel() < need:
-        _SCRATCH.pop(key, None)
-        buf = _SCRATCH[key] = torch.empty(need, dtype=torch.bfloat16, device=device)
+    with _SCRATCH_LOCK:
+        buf = _SCRATCH.get(key)
+        if buf is None or buf.numel() < need:
+            live = {t.ident for t in threading.enumerate()}
+            for k in [k for k in _SCRATCH if k[1] not in live]:
+                del _SCRATCH[k]
+            _SCRATCH.pop(key, None)
+            buf = _SCRATCH[key] = torch.empty(need, dtype=torch.bfloat16, device=device)
     return buf
+
+
+def release_scratch(device=None) -> None:
+    """Drop the calling thread's dequant scratch (a non-engine caller after a large GEMM)."""
+    with _SCRATCH_LOCK:
+        for k in [k for k in _SCRATCH if k[1] == threading.get_ident() and (device is None or k[0] == device)]:
+            del _SCRATCH[k]
 
 
 def _run_scratch_blas(x, ws, Ntot):
@@ -815,7 +738,7 @@ GQ_TILES = {0: (256, 256), 1: (256, 128), 2: (128, 256), 3: (128, 128), 4: (256,
             7: (128, 256), 8: (256, 128), 12: (128, 128), 14: (64, 256),
             # software-pipelined schedules of 0, 1, 3, 6, 7
             10: (256, 256), 11: (256, 128), 13: (128, 128), 16: (256, 256), 17: (128, 256)}
-# LOCALAI_AMD_TILE_GEMM=0 restores the round-2 path (hipBLASLt on bf16 weight copies + qgemm_mid)
+# LOCALAI_AMD_TILE_GEMM=0 restores the round-2 path (hipBLASLt on bf16 weight copies)
 TILE_GEMM = os.environ.get("LOCALAI_AMD_TILE_GEMM", "1") == "1"
 # M > MID_MAX_M (prefill chunks): "blas" = dequantise into a scratch buffer + library GEMM, "pp" =
 # gemm_pp.hip (in-kernel dequant, no bf16 copy), "tile" = gemm_q.hip.  "blas" stays the default:
@@ -1012,22 +935,17 @@ def _autotune_mid(x, ws, key, Ntot):
     if not cands or os.environ.get("LOCALAI_AMD_BLAS_CANDIDATE") == "1" or not TILE_GEMM:
         cands.append(("blas", 0, 0))
     if not TILE_GEMM:
-        cands = [("blas", 0, 0)] + [("mid", S, t) for t in ((22, 21) if M <= 128 else (42, 41, 22, 21))
-                                    for S in (1, 2, 4, 8) if _mid_split_ok(K, S)]
-    outs = {S: torch.empty(S, M, Ntot, dtype=torch.float32, device=x.device) for _, S, _ in cands
-            if S > 1 or (S == 1 and not TILE_GEMM)}
-    if TILE_GEMM:
-        outs[1] = torch.empty(M, Ntot, dtype=torch.bfloat16, device=x.device)   # S = 1: one bf16 matrix
+        cands = [("blas", 0, 0)]
+    outs = {S: torch.empty(S, M, Ntot, dtype=torch.float32, device=x.device) for _, S, _ in cands if S > 1}
+    outs[1] = torch.empty(M, Ntot, dtype=torch.bfloat16, device=x.device)   # S = 1: one bf16 matrix
     best, best_t = cands[0], float("inf")
     for kind, S, t in cands:
         if kind == "blas":
             fn = lambda: _run_blas(x, ws, Ntot)  # noqa: E731
         elif kind == "tile":
             fn = lambda S=S, t=t: _run_tile(x, ws, S, outs[S], Ntot, t)  # noqa: E731
-        elif kind == "q32":
-            fn = lambda S=S, t=t: _run_q32(x, ws, S, outs[S], Ntot, t)  # noqa: E731
         else:
-            fn = lambda S=S, t=t: _run_mid(x, ws, S, outs[S], Ntot, t)  # noqa: E731
+            fn = lambda S=S, t=t: _run_q32(x, ws, S, outs[S], Ntot, t)  # noqa: E731
         fn()
         ts = []
         for _ in range(3):
@@ -1071,14 +989,9 @@ def linear_multi(x: torch.Tensor, ws: Sequence[QWeight], bias: Optional[torch.Te
         raise ValueError("linear: x must be contiguous bf16")
     skinny_ok = all(w.K % 256 == 0 for w in ws)
     use_skinny = (M <= SKINNY_MAX_M and skinny_ok) if force is None else force == "skinny"
-    mid_ok = skinny_ok and all(w.fmt in MID_FMTS for w in ws)
     tile_ok = TILE_GEMM and all(w.tile_ok for w in ws)
     S, tile, kind = 0, 0, None
-    if force == "ws":
-        S, kind = 1, "ws"
-    elif force == "mid":
-        S, kind = min(pick_mid_splits(w.N, w.K, M) for w in ws), "mid"
-    elif force is not None and force.startswith("q32:"):
+    if force is not None and force.startswith("q32:"):
         _, v, s_ = force.split(":")
         tile, S, kind = int(v), int(s_), "q32"
     elif force is not None and force.startswith("tile"):
@@ -1086,7 +999,7 @@ def linear_multi(x: torch.Tensor, ws: Sequence[QWeight], bias: Optional[torch.Te
         parts = force.split(":")
         tile, S = (int(parts[1]), int(parts[2])) if len(parts) == 3 else pick_tile(M, [w.N for w in ws], K)
         kind = "tile"
-    elif force is None and not use_skinny and M <= MID_MAX_M and (tile_ok or mid_ok):
+    elif force is None and not use_skinny and M <= MID_MAX_M and tile_ok:
         # one tuned choice per 32-row bucket: prefill chunk / decode batch sizes vary per step
         # and must not re-run the (cache-flushing) autotune inside the serving loop
         key = ((M + 31) // 32 * 32, K, tuple((w.fmt, w.N) for w in ws))
@@ -1096,7 +1009,7 @@ def linear_multi(x: torch.Tensor, ws: Sequence[QWeight], bias: Optional[torch.Te
         if choice is None and tile_ok:
             t, s_ = pick_tile(M, [w.N for w in ws], K)
             choice = ("tile", s_, t)
-        if choice is not None and choice[0] in ("mid", "ws", "dq", "tile", "q32"):
+        if choice is not None and choice[0] in ("tile", "q32"):
             kind, S, tile = choice
     elif force is None and not use_skinny and tile_ok and PREFILL_GEMM == "tile":
         tile, S = pick_tile(M, [w.N for w in ws], K)   # prefill: heuristic, never tuned inline
@@ -1122,14 +1035,8 @@ def linear_multi(x: torch.Tensor, ws: Sequence[QWeight], bias: Optional[torch.Te
             _run_tile(x, ws, S, out, Ntot, tile)
         elif kind == "pp":
             _run_pp(x, ws, S, out, Ntot)
-        elif kind == "q32":
-            _run_q32(x, ws, S, out, Ntot, tile)
-        elif kind == "ws":
-            _run_ws(x, ws, S, out, Ntot)
-        elif kind == "dq":
-            _run_dq(x, ws, S, out, Ntot)
         else:
-            _run_mid(x, ws, S, out, Ntot, tile)
+            _run_q32(x, ws, S, out, Ntot, tile)
         return Partial(out, bias)
     use_gemv = (force == "dp4") or (force is None and use_skinny and GEMV_DP4 and M <= GEMV_MAX_M
                                     and all(w.gemv_ok for w in ws))

@@ -125,53 +125,15 @@ def test_gemv_dp4_outlier_rows():
 @pytest.mark.parametrize("t", [GGMLType.Q4_K, GGMLType.Q6_K, GGMLType.Q8_0])
 @pytest.mark.parametrize("M", [65, 128, 200, 256, 300])
 def test_mid_gemm(t, M):
-    """Mid-M quantised MFMA GEMM (LDS-dequantised weight tiles) vs the fp32 reference; N not a
-    multiple of the 128-wide tile, M spanning several 128-row tiles."""
+    """Mid-M quantised MFMA GEMM (the gemm_q.hip tile kernel, heuristic tile / split-K) vs the fp32
+    reference; N not a multiple of the 128-wide tile, M spanning several 128-row tiles."""
     N, K = 200, 1536
     w = _qw(N, K, t, seed=7)
     x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
-    y = ops.linear(x, w, force="mid").dense()
+    y = ops.linear(x, w, force="tile").dense()
     ref = x.float().cpu() @ w.ref.t()
     err = (y.cpu() - ref).abs().max().item()
     assert err < 2e-2 * max(1.0, ref.abs().max().item()), err
-
-
-def test_mid_gemm_splits():
-    N, K, M = 130, 2048, 150
-    w = _qw(N, K, GGMLType.Q4_K, seed=8)
-    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
-    ref = x.float().cpu() @ w.ref.t()
-    for tile in (0, 42, 41, 22, 21):  # auto, 256x128, 256x64, 128x128, 128x64
-        for S in (1, 3, 4, 8):
-            out = torch.full((S, M, N), float("nan"), dtype=torch.float32, device=DEV)
-            rc = ops.lib().la_qgemm_mid(w.fmt, *w.ptrs(), N, K, x.data_ptr(), K, M, S, out.data_ptr(), N, M * N,
-                                        tile, ops._stream())
-            assert rc == 0
-            assert (out.sum(0).cpu() - ref).abs().max().item() < 3e-2, (tile, S)
-
-
-@pytest.mark.parametrize("M", [1, 100, 256, 300])
-@pytest.mark.parametrize("K", [1024, 3584])
-def test_ws_gemm(M, K):
-    """Warp-specialised LDS-DMA Q4_K GEMM vs the fp32 reference: N off the 128 tile, several
-    M tiles, every equal split of the K-steps (repeated launches bit-identical)."""
-    N = 200
-    w = _qw(N, K, GGMLType.Q4_K, seed=9)
-    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
-    ref = x.float().cpu() @ w.ref.t()
-    for S in (1, 2, 4, 7):
-        if (K // 64) % S:
-            continue
-        out = torch.full((S, M, N), float("nan"), dtype=torch.float32, device=DEV)
-        rc = ops.lib().la_qgemm_ws(w.fmt, *w.ptrs(), N, K, x.data_ptr(), K, M, S, out.data_ptr(), N, M * N,
-                                   ops._stream())
-        assert rc == 0
-        y = out.sum(0).cpu()
-        assert (y - ref).abs().max().item() < 3e-2 * max(1.0, ref.abs().max().item()), S
-        out2 = torch.empty_like(out)
-        ops.lib().la_qgemm_ws(w.fmt, *w.ptrs(), N, K, x.data_ptr(), K, M, S, out2.data_ptr(), N, M * N,
-                              ops._stream())
-        assert torch.equal(out, out2)
 
 
 @pytest.mark.parametrize("M", [3, 100])
@@ -574,44 +536,6 @@ def test_moe_route_skewed_large():
         ref = torch.sort(ids.view(-1).long(), stable=True).indices
         assert torch.equal(order.cpu().long(), ref)
         assert off.cpu().tolist() == [0] + torch.bincount(ids.view(-1).long(), minlength=E).cumsum(0).tolist()
-
-
-@pytest.mark.parametrize("M", [1, 100, 256, 300])
-@pytest.mark.parametrize("K", [1024, 3584])
-def test_dq_gemm(M, K):
-    """In-register-dequant Q4_K batch GEMM (gemm_dq.hip) vs the fp32 reference: N off the 32 and
-    256 tiles, several M tiles, every equal split of the K-steps (fp32
-    slabs) and the bf16 single-matrix output; repeated launches bit-identical."""
-    N = 200
-    w = _qw(N, K, GGMLType.Q4_K, seed=19)
-    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
-    ref = x.float().cpu() @ w.ref.t()
-    tol = 3e-2 * max(1.0, ref.abs().max().item())
-    for wnt in (1,):
-        for S in (1, 2, 4, 7):
-            if (K // 64) % S:
-                continue
-            out = torch.full((S, M, N), float("nan"), dtype=torch.float32, device=DEV)
-            ops._run_dq(x, [w], S, out, N, wnt)
-            y = out.sum(0).cpu()
-            assert (y - ref).abs().max().item() < tol, (wnt, S)
-            out2 = torch.empty_like(out)
-            ops._run_dq(x, [w], S, out2, N, wnt)
-            assert torch.equal(out, out2)
-        ob = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
-        ops._run_dq(x, [w], 1, ob, N, wnt)
-        assert (ob.float().cpu() - ref).abs().max().item() < tol, wnt
-
-
-def test_dq_gemm_two_weights_side_by_side():
-    """q|k-style call: two Q4_K weights written into column ranges of one output."""
-    K, M = 2048, 256
-    ws = [_qw(320, K, GGMLType.Q4_K, seed=21), _qw(96, K, GGMLType.Q4_K, seed=22)]
-    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
-    ref = torch.cat([x.float().cpu() @ w.ref.t() for w in ws], -1)
-    out = torch.empty(2, M, 416, dtype=torch.float32, device=DEV)
-    ops._run_dq(x, ws, 2, out, 416)
-    assert (out.sum(0).cpu() - ref).abs().max().item() < 3e-2 * max(1.0, ref.abs().max().item())
 
 
 @pytest.mark.parametrize("M", [1, 2])
