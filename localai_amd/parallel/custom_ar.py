@@ -26,6 +26,11 @@ FUSED_ADD_NORM = os.environ.get("LOCALAI_AMD_AR_ADD_NORM", "1") == "1"
 
 HIP_IPC_HANDLE_SIZE = 64
 _hipIpcMemLazyEnablePeerAccess = 0x1
+_hipDeviceMallocUncached = 0x3
+# regions are rounded up to this so no allocator ever sub-allocates them from a shared chunk
+# (hipIpcGetMemHandle exports whole allocations only: a sub-allocated pointer fails with
+# hipErrorInvalidValue)
+_REGION_ALIGN = 2 << 20
 
 
 class _HipIpcHandle(ctypes.Structure):
@@ -38,6 +43,9 @@ def _hip():
     lib = os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so")
     h = ctypes.CDLL(lib if os.path.exists(lib) else "libamdhip64.so")
     h.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
+    h.hipExtMallocWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_uint]
+    h.hipMemGetAddressRange.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t),
+                                        ctypes.c_void_p]
     h.hipFree.argtypes = [ctypes.c_void_p]
     h.hipMemset.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t]
     h.hipIpcGetMemHandle.argtypes = [ctypes.POINTER(_HipIpcHandle), ctypes.c_void_p]
@@ -45,7 +53,7 @@ def _hip():
     h.hipIpcCloseMemHandle.argtypes = [ctypes.c_void_p]
     h.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
     for f in ("hipMalloc", "hipFree", "hipMemset", "hipIpcGetMemHandle", "hipIpcOpenMemHandle",
-              "hipIpcCloseMemHandle", "hipMemcpy"):
+              "hipIpcCloseMemHandle", "hipMemcpy", "hipExtMallocWithFlags", "hipMemGetAddressRange"):
         getattr(h, f).restype = ctypes.c_int
     return h
 
@@ -97,18 +105,21 @@ class CustomAllReduce:
             hbs: List[bytes] = []
             try:
                 for nb in sizes:
-                    ptr = ctypes.c_void_p()
-                    self._check(self.hip.hipMalloc(ctypes.byref(ptr), nb), "hipMalloc")
-                    self.owns.append(ptr.value)
-                    self._check(self.hip.hipMemset(ctypes.c_void_p(ptr.value), 0, nb), "hipMemset")
+                    nb = -(-nb // _REGION_ALIGN) * _REGION_ALIGN
+                    ptr = self._alloc(nb)
+                    self.owns.append(ptr)
+                    self._check(self.hip.hipMemset(ctypes.c_void_p(ptr), 0, nb), "hipMemset")
                 torch.cuda.synchronize(self.device)
-                for o in self.owns:
+                for k, o in enumerate(self.owns):
                     hnd = _HipIpcHandle()
-                    self._check(self.hip.hipIpcGetMemHandle(ctypes.byref(hnd), ctypes.c_void_p(o)),
-                                "hipIpcGetMemHandle")
+                    rc = self.hip.hipIpcGetMemHandle(ctypes.byref(hnd), ctypes.c_void_p(o))
+                    if rc != 0:
+                        raise RuntimeError(f"hipIpcGetMemHandle failed with hipError {rc} on region {k} "
+                                           f"({self._describe(o, sizes[k])})")
                     hbs.append(ctypes.string_at(ctypes.addressof(hnd), HIP_IPC_HANDLE_SIZE))  # .reserved stops at a NUL
             except Exception as e:  # noqa: BLE001
                 err = str(e)
+                log.warning("rank %d: custom all-reduce setup: %s", rank, err)
             self.own = self.owns[0] if self.owns else None
             handles: List[Optional[list]] = [None] * world
             dist.all_gather_object(handles, hbs, group=group)
@@ -148,6 +159,27 @@ class CustomAllReduce:
                 raise RuntimeError("; ".join(bad))
         self.ptrs = self.ptr_sets[0]
         self._bufs = [(ctypes.c_void_p * world)(*ps) for ps in self.ptr_sets]
+
+    def _alloc(self, nb: int) -> int:
+        """The region: uncached device memory (MTYPE UC), so the peers' flag stores and data are
+        seen by polling loads without relying on system-scope L2 write-back / invalidate; plain
+        hipMalloc if the driver refuses that flag.  Sized to whole 2 MiB granules: never a
+        sub-allocation, which IPC export would reject."""
+        ptr = ctypes.c_void_p()
+        self.uncached = self.hip.hipExtMallocWithFlags(ctypes.byref(ptr), nb, _hipDeviceMallocUncached) == 0
+        if not self.uncached:
+            self._check(self.hip.hipMalloc(ctypes.byref(ptr), nb), "hipMalloc")
+        return ptr.value
+
+    def _describe(self, ptr: int, nb: int) -> str:
+        """Pointer, size and whether it is the base of its allocation (diagnostics for an IPC
+        export failure)."""
+        base, size = ctypes.c_void_p(), ctypes.c_size_t()
+        rc = self.hip.hipMemGetAddressRange(ctypes.byref(base), ctypes.byref(size), ctypes.c_void_p(ptr))
+        if rc != 0:
+            return f"ptr 0x{ptr:x}, {nb} B, hipMemGetAddressRange error {rc}"
+        return (f"ptr 0x{ptr:x}, {nb} B, allocation base 0x{(base.value or 0):x} size {size.value} B"
+                f"{'' if base.value == ptr else ' (SUB-ALLOCATED)'}, uncached={getattr(self, 'uncached', None)}")
 
     def _device_key(self) -> str:
         try:

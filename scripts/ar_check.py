@@ -28,18 +28,9 @@ def expected(world, n, dtype, dev, call):
 
 
 def make_car(rank, world, dev):
-    """The IPC setup can fail transiently when 8 processes share one GPU (hipIpcGetMemHandle on a
-    fresh dmabuf export returned invalid-value on 2 of 8 ranks once); every rank learns about any
-    rank's failure in the constructor's final all-gather and raises together, so all of them retry
-    in lockstep.  (Serving never retries: maybe_create() falls back to RCCL.)"""
-    for attempt in range(3):
-        try:
-            return CustomAllReduce(dist.group.WORLD, rank, world, dev)
-        except RuntimeError as e:
-            if attempt == 2:
-                raise
-            print(f"rank {rank}: custom all-reduce setup failed ({e}); retrying", flush=True)
-            time.sleep(1.0)
+    """One setup attempt: the regions are uncached whole-granule allocations (custom_ar._alloc),
+    and any rank's failure raises on every rank with the region, pointer and allocation base."""
+    return CustomAllReduce(dist.group.WORLD, rank, world, dev)
 
 
 def main():
