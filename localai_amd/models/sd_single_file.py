@@ -347,6 +347,10 @@ def convert(path: str, out_dir: Optional[str] = None, tokenizer_dir: Optional[st
     if os.path.isfile(mark) and open(mark).read() == stamp:
         return out_dir
     sd, hints = load_checkpoint(path)
+    from . import sd3_single_file as sd3f
+    if hints.get("family") == "sd3" or sd3f.is_sd3_file(sd):
+        # backend.py:238-242: StableDiffusion3Pipeline.from_single_file
+        return sd3f.convert(path, sd, hints, out_dir, tokenizer_dir)
     fam = hints.get("family") or family(sd)
     tmp = out_dir + ".partial"
     shutil.rmtree(tmp, ignore_errors=True)
