@@ -228,7 +228,8 @@ class ClipVision:
     def _encode_native(self, pix: torch.Tensor) -> torch.Tensor:
         """encode_tiles on the native ops: im2col + GEMM patch embedding, fused residual +
         LayerNorm (add_norm mode 1), GELU / quick-GELU in the act kernel (llama.cpp's clip uses
-        the tanh GELU too), attention through SDPA (non-causal, L <= 730)."""
+        the tanh GELU too), non-causal attention on the MFMA flash-attention kernel read straight
+        from the fused q|k|v output (ops.attn_dense)."""
         from .. import ops
         n = pix.shape[0]
         D, P, H = self.dim, self.patch, self.heads
@@ -250,9 +251,12 @@ class ClipVision:
         a = ops.add_norm(h, None, self.layers[0]["ln1"][0], self.layers[0]["ln1"][1], eps, mode=1)
         for i, ly in enumerate(self.layers):
             qkv = ops.reduce(ops.linear(a, ly["q_qkv_w"], bias=ly["qkv_b"]), dtype=self.dtype)
-            q, k, v = qkv.view(n, L, 3, H, D // H).permute(2, 0, 3, 1, 4)
-            o = F.scaled_dot_product_attention(q, k, v)                        # non-causal
-            o = o.transpose(1, 2).reshape(n * L, D).contiguous()
+            if self.dtype == torch.bfloat16 and (D // H) in (64, 80, 96, 128):
+                o = ops.attn_dense(qkv.contiguous(), n, L, H)                   # non-causal, MFMA
+            else:
+                q, k, v = qkv.view(n, L, 3, H, D // H).permute(2, 0, 3, 1, 4)
+                o = F.scaled_dot_product_attention(q, k, v)                    # non-causal
+                o = o.transpose(1, 2).reshape(n * L, D).contiguous()
             a2 = ops.add_norm(h, ops.linear(o, ly["q_o_w"], bias=ly["o_b"]), ly["ln2"][0], ly["ln2"][1], eps, mode=1)
             f1 = ops.linear(a2, ly["q_f1_w"], bias=ly["f1_b"])
             g = ops.act(f1, f1.N, act)

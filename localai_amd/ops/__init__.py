@@ -89,6 +89,7 @@ def lib():
             "la_qgemm32_glu": [I, P, P, P, I, P, P, P, I, I, I, P, I, I, P, I, I, I, P],
             "la_qgemm32_probe": [I, I, P, P, I, I, P, I, I, P, P],
             "la_gemm_pp": [I, P, P, P, I, I, P, I, I, I, P, I, LNG, I, P],
+            "la_attn_dense": [P, LNG, P, LNG, P, LNG, P, LNG, P, I, P, I, I, I, F, P],
             "la_gemm_pp2": [I, P, P, P, I, I, P, P, P, I, I, P, I, I, I, P, I, LNG, I, P],
             "la_gemm_pp_glu": [I, P, P, P, I, P, P, P, I, I, I, P, I, I, P, I, I, P],
             "la_decode_advance": [P, P, P, P, P, P, I, I, I, P, I, P, P, P],
@@ -234,6 +235,7 @@ class QWeight:
                 self.bf16 = out
         return self.bf16
 
+    @property
     def tile_ok(self) -> bool:
         """Can feed the quantised tile GEMM (gemm_q.hip)."""
         return self.K % 256 == 0 and self.fmt in (FMT_Q4_K, FMT_Q6_K, FMT_Q8_0, FMT_BF16) and self.planes[0] is not None
@@ -1580,6 +1582,39 @@ def attn_prefill(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, 
                                  tiles.shape[0], cu_q.data_ptr(), ctx_lens.data_ptr(), block_tables.data_ptr(),
                                  block_tables.shape[1], Hq, Hkv, Dh, k_cache.shape[2], float(scale),
                                  out.data_ptr(), float(softcap), int(window), _stream()), "la_attn_prefill")
+    return out
+
+
+_DENSE_META: Dict[tuple, tuple] = {}
+
+
+def attn_dense(qkv: torch.Tensor, n: int, L: int, H: int, scale: Optional[float] = None,
+               out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Non-causal self-attention of n sequences of L tokens, read in place from a fused q|k|v
+    projection output [n * L, 3 * D] (bf16; D = H * Dh): the MFMA flash-attention kernel of
+    la_attn_prefill in its dense mode (vision towers).  Returns [n * L, D] bf16."""
+    T, W = qkv.shape
+    D = W // 3
+    Dh = D // H
+    if scale is None:
+        scale = Dh ** -0.5
+    if not qkv.is_cuda:
+        q, k, v = qkv.float().view(n, L, 3, H, Dh).permute(2, 0, 3, 1, 4)
+        o = torch.softmax(q @ k.transpose(-1, -2) * scale, -1) @ v
+        return o.transpose(1, 2).reshape(T, D).to(qkv.dtype)
+    if qkv.dtype != torch.bfloat16 or not qkv.is_contiguous() or T != n * L or W != 3 * D:
+        raise ValueError("attn_dense: qkv must be a contiguous bf16 [n * L, 3 * D] matrix")
+    key = (n, L, qkv.device)
+    meta = _DENSE_META.get(key)
+    if meta is None:
+        cu = torch.arange(0, (n + 1) * L, L, dtype=torch.int32, device=qkv.device)
+        meta = _DENSE_META[key] = (cu, prefill_tiles([L] * n, qkv.device))
+    cu, tiles = meta
+    if out is None:
+        out = torch.empty(T, D, dtype=torch.bfloat16, device=qkv.device)
+    base = qkv.data_ptr()
+    _check(lib().la_attn_dense(base, W, base + 2 * D, W, base + 4 * D, W, out.data_ptr(), D, tiles.data_ptr(),
+                               tiles.shape[0], cu.data_ptr(), H, H, Dh, float(scale), _stream()), "la_attn_dense")
     return out
 
 

@@ -446,17 +446,21 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
 
 // ----------------------------------------------------------------------------- prefill
 // Workgroup = 64 query rows (4 waves x 16) of one sequence x one query head.
+// DENSE = false: causal, K/V from the paged cache (engine prefill).  DENSE = true: non-causal
+// over K/V rows of the same tokens in plain strided matrices -- a vision tower's bidirectional
+// self-attention (CLIP ViT, SURVEY K12 "non-causal variant"): q/k/v/out row t, head h at
+// ptr + t * ld + h * DH (the fused q|k|v projection output read in place).
 constexpr int PF_T = 256;
 constexpr int PF_KT = 32;  // keys per tile
 
-template <int DH>
+template <int DH, bool DENSE = false>
 __global__ __launch_bounds__(PF_T) void attn_prefill_kernel(
     const bf16* __restrict__ q, const bf16* __restrict__ kc, const bf16* __restrict__ vc,
     const int* __restrict__ tiles,          // [ntiles][2] = (seq, first query row within seq)
     const int* __restrict__ cu_q,           // [nseq+1] token offsets of each seq's queries
     const int* __restrict__ ctx_lens,       // [nseq] total keys (cached + new)
     const int* __restrict__ block_tables, int max_blocks, int Hq, int Hkv, int BS, float scale,
-    bf16* __restrict__ out, float cap, int window) {
+    bf16* __restrict__ out, float cap, int window, long ldq = 0, long ldk = 0, long ldv = 0, long ldo = 0) {
   constexpr int DP = (DH + 31) / 32 * 32;  // padded head dim for the MFMA k loop
   constexpr int KC = DP / 32;               // k-chunks of 32
   constexpr int ND = DP / 16;               // 16-wide output column tiles
@@ -470,9 +474,10 @@ __global__ __launch_bounds__(PF_T) void attn_prefill_kernel(
   const int s = tiles[2 * tile], r0 = tiles[2 * tile + 1];
   const int G = Hq / Hkv, kvh = h / G;
   const int qbeg = cu_q[s], qlen = cu_q[s + 1] - qbeg;
-  const int L = ctx_lens[s];
+  const int L = DENSE ? qlen : ctx_lens[s];
   const int pos0 = L - qlen;  // absolute position of query row 0
-  const int* bt = block_tables + (long)s * max_blocks;
+  const int* bt = DENSE ? nullptr : block_tables + (long)s * max_blocks;
+  if constexpr (!DENSE) ldq = ldo = (long)Hq * DH;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fq = lane >> 4;
@@ -484,7 +489,7 @@ __global__ __launch_bounds__(PF_T) void attn_prefill_kernel(
   for (int kc2 = 0; kc2 < KC; ++kc2) {
     bf16x8 v = {};
     const int d = 32 * kc2 + 8 * fq;
-    if (qrow < qlen && d < DH) v = *(const bf16x8*)(q + ((long)(qbeg + qrow) * Hq + h) * DH + d);
+    if (qrow < qlen && d < DH) v = *(const bf16x8*)(q + (long)(qbeg + qrow) * ldq + (long)h * DH + d);
     qa[kc2] = v;
   }
 
@@ -497,7 +502,7 @@ __global__ __launch_bounds__(PF_T) void attn_prefill_kernel(
 
   const float sl2 = scale * 1.4426950408889634f;
   const int last_row = min(qlen, r0 + 64) - 1;
-  const int kend = min(L, pos0 + last_row + 1);  // exclusive
+  const int kend = DENSE ? L : min(L, pos0 + last_row + 1);  // exclusive
 
   for (int k0 = 0; k0 < kend; k0 += PF_KT) {
     __syncthreads();
@@ -507,12 +512,27 @@ __global__ __launch_bounds__(PF_T) void attn_prefill_kernel(
       const int key = k0 + kr;
       bf16x8 kv = {};
       if (key < kend && d < DH) {
-        const int blk = bt[key / BS], off = key % BS;
-        kv = *(const bf16x8*)(kc + (((long)blk * Hkv + kvh) * BS + off) * DH + d);
+        if constexpr (DENSE) {
+          kv = *(const bf16x8*)(kc + (long)(qbeg + key) * ldk + (long)kvh * DH + d);
+        } else {
+          const int blk = bt[key / BS], off = key % BS;
+          kv = *(const bf16x8*)(kc + (((long)blk * Hkv + kvh) * BS + off) * DH + d);
+        }
       }
       *(bf16x8*)(ks + kr * KS + d) = kv;
     }
-    for (int cidx = tid; cidx < DP * (PF_KT / 8); cidx += PF_T) {
+    if constexpr (DENSE) {
+      // V rows are key-major: 16 B (8 d) per load, transposed into V^T[d][key] by scalar writes
+      for (int cidx = tid; cidx < PF_KT * (DP / 8); cidx += PF_T) {
+        const int kr = cidx / (DP / 8), d = (cidx % (DP / 8)) * 8;
+        const int key = k0 + kr;
+        bf16x8 vv = {};
+        if (key < kend && d < DH) vv = *(const bf16x8*)(vc + (long)(qbeg + key) * ldv + (long)kvh * DH + d);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) vt[(d + j) * VS + kr] = vv[j];
+      }
+    }
+    for (int cidx = tid; !DENSE && cidx < DP * (PF_KT / 8); cidx += PF_T) {
       const int d = cidx % DP, q8 = (cidx / DP) * 8;  // consecutive threads: consecutive d of one key group
       const int key = k0 + q8;
       bf16x8 vv = {};
@@ -554,8 +574,9 @@ __global__ __launch_bounds__(PF_T) void attn_prefill_kernel(
       }
       const int key0 = k0 + fr, key1 = k0 + 16 + fr;
       const int wlo = window > 0 ? qpos - window + 1 : 0;
-      if (key0 > qpos || key0 >= kend || qr >= qlen || key0 < wlo) v0 = -INFINITY;
-      if (key1 > qpos || key1 >= kend || qr >= qlen || key1 < wlo) v1 = -INFINITY;
+      const bool causal = !DENSE;
+      if ((causal && key0 > qpos) || key0 >= kend || qr >= qlen || key0 < wlo) v0 = -INFINITY;
+      if ((causal && key1 > qpos) || key1 >= kend || qr >= qlen || key1 < wlo) v1 = -INFINITY;
       float mx = group_max<16>(fmaxf(v0, v1));
       const float mnew = fmaxf(mrow[i], mx);
       const float msafe = (mnew == -INFINITY) ? 0.f : mnew;
@@ -589,7 +610,7 @@ __global__ __launch_bounds__(PF_T) void attn_prefill_kernel(
 #pragma unroll
     for (int nd = 0; nd < ND; ++nd) {
       const int d = 16 * nd + fr;
-      if (d < DH) out[((long)(qbeg + qr) * Hq + h) * DH + d] = (bf16)(o[nd][i] * inv);
+      if (d < DH) out[(long)(qbeg + qr) * ldo + (long)h * DH + d] = (bf16)(o[nd][i] * inv);
     }
   }
 }
@@ -668,6 +689,28 @@ extern "C" int la_attn_decode(const void* q, const void* kc, const void* vc, con
 #undef DEC
 #undef DEC_NW
 #undef DEC_LAUNCH
+  return (int)hipGetLastError();
+}
+
+// Non-causal attention over strided q / k / v rows of the same tokens (vision towers): sequence s
+// holds tokens cu_q[s] .. cu_q[s+1]; tiles as la_attn_prefill's (seq, first query row).
+extern "C" int la_attn_dense(const void* q, long ldq, const void* k, long ldk, const void* v, long ldv, void* out,
+                             long ldo, const int* tiles, int ntiles, const int* cu_q, int Hq, int Hkv, int Dh,
+                             float scale, void* stream) {
+  if (Hq % Hkv || (ldq & 7) || (ldk & 7) || (ldv & 7) || ntiles < 1) return -1;
+  hipStream_t st = (hipStream_t)stream;
+  dim3 grid(ntiles, Hq);
+#define DENSE_CASE(D)                                                                                              \
+  case D:                                                                                                          \
+    hipLaunchKernelGGL((la::attn_prefill_kernel<D, true>), grid, dim3(la::PF_T), 0, st, (const bf16*)q,          \
+                       (const bf16*)k, (const bf16*)v, tiles, cu_q, nullptr, nullptr, 0, Hq, Hkv, 0, scale,       \
+                       (bf16*)out, 0.f, 0, ldq, ldk, ldv, ldo);                                                   \
+    break;
+  switch (Dh) {
+    DENSE_CASE(64) DENSE_CASE(80) DENSE_CASE(96) DENSE_CASE(128)
+    default: return -2;
+  }
+#undef DENSE_CASE
   return (int)hipGetLastError();
 }
 

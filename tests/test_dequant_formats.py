@@ -91,3 +91,13 @@ def test_dequant_matches_ggml_loops(t):
     got = dequantize(raw.reshape(-1), t, (nblk * bs,))
     want = np.concatenate([np.asarray(ref_block(t, [int(x) for x in raw[i]]), np.float32) for i in range(nblk)])
     np.testing.assert_allclose(got, want, rtol=1e-6, atol=1e-6)
+
+
+def test_qweight_tile_ok_is_a_shape_predicate():
+    """QWeight.tile_ok is a property (a bound method would be truthy for every weight and send a
+    K = 588 CLIP patch embedding into the tile GEMM, which needs K % 256 == 0)."""
+    import torch
+
+    from localai_amd import ops
+    a = ops.QWeight.from_float(torch.randn(64, 588))
+    assert isinstance(type(a).tile_ok, property) and a.tile_ok is False

@@ -805,13 +805,15 @@ def test_moe_gemv_decode(T, fmts):
 
 
 @pytest.mark.parametrize("cls_token", [True, False])
-def test_clip_tower_native_ops_match_fp32(tmp_path, cls_token):
+@pytest.mark.parametrize("heads", [2, 4])
+def test_clip_tower_native_ops_match_fp32(tmp_path, cls_token, heads):
     """The vision tower on the native ops (ops.linear projections, fused residual + LayerNorm in
-    add_norm, act-kernel GELU) vs the fp32 PyTorch tower on the CPU, same mmproj and pixels:
-    every projected patch embedding row close in cosine and relative L2."""
+    add_norm, act-kernel GELU; 64-wide heads: non-causal MFMA attention, ops.attn_dense) vs the
+    fp32 PyTorch tower on the CPU, same mmproj and pixels: every projected patch embedding row
+    close in cosine and relative L2."""
     from localai_amd.models import synth
     from localai_amd.models.clip import ClipVision
-    kw = dict(out_dim=256, dim=128, n_layer=2, heads=4, ffn=256, image_size=56, patch=14)
+    kw = dict(out_dim=256, dim=128, n_layer=2, heads=heads, ffn=256, image_size=56, patch=14)
     if not cls_token:
         kw["siglip"] = True
     mm = synth.write_mmproj(str(tmp_path / "mm.gguf"), **kw)
@@ -852,3 +854,22 @@ def test_gemv_dp4_wide_batch1_variant():
     assert torch.equal(y1, ops.linear(x[:1], w, force="dp4").dense())
     y2 = ops.linear(x, w, force="dp4").dense().cpu()
     assert (y2 - ref).abs().max().item() < tol
+
+
+@pytest.mark.parametrize("n,L,H,Dh", [(3, 577, 16, 64), (2, 50, 12, 64), (1, 130, 4, 128), (2, 33, 5, 80)])
+def test_attn_dense_noncausal(n, L, H, Dh):
+    """Vision-tower self-attention on the MFMA flash kernel (la_attn_dense: non-causal, q|k|v read
+    in place from the fused projection output) vs the fp32 PyTorch softmax attention; ragged L
+    (not a multiple of the 64-row query tile or the 32-key tile)."""
+    D = H * Dh
+    qkv = (torch.randn(n * L, 3 * D, device=DEV) * 0.5).to(torch.bfloat16)
+    out = ops.attn_dense(qkv, n, L, H)
+    torch.cuda.synchronize()
+    q, k, v = qkv.float().cpu().view(n, L, 3, H, Dh).permute(2, 0, 3, 1, 4)
+    ref = (torch.softmax(q @ k.transpose(-1, -2) * Dh ** -0.5, -1) @ v).transpose(1, 2).reshape(n * L, D)
+    got = out.float().cpu()
+    assert torch.isfinite(got).all()
+    err = (got - ref).abs().max().item()
+    assert err < 2e-2 * max(1.0, ref.abs().max().item()), err
+    cos = torch.nn.functional.cosine_similarity(got.flatten(), ref.flatten(), dim=0).item()
+    assert cos > 0.9999, cos
