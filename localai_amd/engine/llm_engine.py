@@ -224,6 +224,9 @@ class LLMEngine:
         self.healthy = True          # False after a fatal device error: the model manager respawns
         self.fatal_error = ""
         self._graphs: Dict[int, tuple] = {}
+        # tensor parallelism, all-greedy batches: graphs whose sampler is the distributed argmax
+        # (TPInfo.argmax_cols) -- no full-vocabulary all-gather, no RCCL call in the graph
+        self._graphs_tpg: Dict[int, tuple] = {}
         self.tracer = get_tracer()
         self._pcache = PromptCacheFiles()
         self._graph_pool = None
@@ -611,6 +614,7 @@ class LLMEngine:
             from ..models.decoder import CustomAllReduceTimeout
             self._ar_err = 0
             self._graphs.clear()   # the captured decode graphs call the custom kernel
+            self._graphs_tpg.clear()
             self.tp.drop_custom_ar()
             raise CustomAllReduceTimeout("tensor-parallel custom all-reduce timed out on a late peer rank: the last "
                                          "step's results are invalid; the group continues on RCCL")
@@ -961,11 +965,25 @@ class LLMEngine:
             self._sample_and_emit(ids, logits[:B])
             return
         reqs = [self.requests[i] for i in ids]
+        device_sampling = not any(self._needs_host_sampling(r) for r in reqs)
+        if device_sampling and self._tp_greedy_ok(reqs):
+            g = self._graphs_tpg.get(Bp)
+            if g is None:
+                g = self._graphs_tpg[Bp] = self._capture(Bp, tp_greedy=True)
+            graph, st, _ = g
+            self._upload_step_inputs(st, reqs, Bp, tok, pos, slots, lens, bt, True)
+            for _ in range(K):
+                graph.replay()
+            hist = st["hist"][:K, :B].cpu().numpy()
+            rec = st.get("rec")
+            if rec is not None:   # record_logits (tests): this rank's columns -> full rows, off the graph
+                rec = self.model.tp.all_gather_cols(rec)
+            self._emit_run(reqs, hist, K, rec)
+            return
         g = self._graphs.get(Bp)
         if g is None:
             g = self._graphs[Bp] = self._capture(Bp)
         graph, st, logits = g
-        device_sampling = not any(self._needs_host_sampling(r) for r in reqs)
         if not device_sampling and not any(self._needs_host_sampler(r) for r in reqs):
             # grammar rows only: one step with the in-graph sampler for EVERY row (penalties, bias,
             # mirostat 2 included), then the grammar rows' samples are checked on the host and
@@ -1161,14 +1179,16 @@ class LLMEngine:
             h["prm"][:] = torch.from_numpy(prm.view(np.uint8))
             if not same:
                 rows, cols, vals = st["bias_np"]
+                lo, hi = 0, self.hp.n_vocab
+                if "tp_cols" in st:   # distributed-argmax graph: this rank's columns only
+                    lo, hi = st["tp_cols"][0], st["tp_cols"][0] + st["tp_cols"][1]
                 for j, r in enumerate(reqs):
-                    for t, b in r.params.logit_bias.items():
-                        if 0 <= t < self.hp.n_vocab:
-                            rows[n_bias], cols[n_bias], vals[n_bias] = j, t, b
-                            n_bias += 1
+                    ent = list(r.params.logit_bias.items())
                     if r.params.ignore_eos:
-                        for t in self.tokenizer.eog:
-                            rows[n_bias], cols[n_bias], vals[n_bias] = j, t, -math.inf
+                        ent += [(t, -math.inf) for t in self.tokenizer.eog]
+                    for t, b in ent:
+                        if lo <= t < hi and n_bias < len(rows):
+                            rows[n_bias], cols[n_bias], vals[n_bias] = j, t - lo, b
                             n_bias += 1
                 h["bias_rows"][:] = torch.from_numpy(rows)
                 h["bias_cols"][:] = torch.from_numpy(cols)
@@ -1213,8 +1233,25 @@ class LLMEngine:
         h["bias_n"][0] = n_bias
         st["dev_block"].copy_(st["host_block"], non_blocking=True)
 
-    def _capture(self, Bp: int):
-        """One hipGraph per padded batch size: forward + logit bias + sampler + advance."""
+    TP_GREEDY = os.environ.get("LOCALAI_AMD_TP_GREEDY", "1") == "1"
+
+    def _tp_greedy_ok(self, reqs) -> bool:
+        """Tensor parallelism and every row plain greedy (temperature <= 0, no penalties, no
+        mirostat, no grammar; logit bias and ignore_eos are fine): the batch can run the
+        distributed-argmax graph.  Every rank decides alike (replicated request state)."""
+        if self.tp.world < 2 or not self.TP_GREEDY:
+            return False
+        for r in reqs:
+            p = r.params
+            if (p.temperature > 0 or p.mirostat or r.grammar is not None or p.repeat_penalty != 1.0
+                    or p.frequency_penalty != 0.0 or p.presence_penalty != 0.0):
+                return False
+        return True
+
+    def _capture(self, Bp: int, tp_greedy: bool = False):
+        """One hipGraph per padded batch size: forward + logit bias + sampler + advance.
+        tp_greedy: this rank's vocabulary columns only, logit bias on them, and the exact
+        distributed argmax (TPInfo.argmax_cols) as the sampler."""
         dev = self.device
         MB = self.max_blocks
         cap = max(1, Bp * self.cfg.bias_capacity)
@@ -1258,8 +1295,22 @@ class LLMEngine:
         ws = ops.decode_workspace(Bp, self.model.Hq, self.model.Hkv, self.model.Dh, self.ctx, dev,
                                   self.cfg.block_size)
         bs = self.cfg.block_size
+        if tp_greedy:
+            vl = self.model.vocab_local
+            st["tp_cols"] = (self.model.tp.rank * vl, vl)   # bias entries are translated to these columns
         if self.cfg.record_logits:
-            st["rec"] = torch.zeros(K, Bp, self.model.hp.n_vocab, dtype=torch.float32, device=dev)
+            st["rec"] = torch.zeros(K, Bp, self.model.vocab_local if tp_greedy else self.model.hp.n_vocab,
+                                    dtype=torch.float32, device=dev)
+
+        def body_tpg():
+            lg = self.model.forward(fb, self.kv, attn_workspace=ws, local_logits=True)
+            if "rec" in st:
+                st["rec"].index_copy_(0, st["step"][:1].long(), lg.float().unsqueeze(0))
+            ops.logit_bias(lg, st["bias_rows"], st["bias_cols"], st["bias_vals"], st["bias_n"])
+            st["next"].copy_(self.model.tp.argmax_cols(lg))
+            ops.decode_advance(st["next"], st["tokens"], st["pos"], st["lens"], st["slots"], st["bt"], bs,
+                               st["hist"], st["step"], st["prm"])
+            return lg
 
         def body():
             lg = self.model.forward(fb, self.kv, attn_workspace=ws)
@@ -1280,6 +1331,8 @@ class LLMEngine:
 
         s = torch.cuda.Stream(device=dev)
         s.wait_stream(torch.cuda.current_stream(dev))
+        if tp_greedy:
+            body = body_tpg  # noqa: F811
         with torch.cuda.stream(s):
             for _ in range(2):  # warm up allocator / kernels outside the graph
                 body()

@@ -85,6 +85,7 @@ def lib():
             "la_pen_push": [P, I, P, I, P, P, P, P],
             "la_qgemm_glu": [I, P, P, P, I, P, P, P, I, I, I, P, I, I, P, I, I, I, P],
             "la_qgemm32": [I, P, P, P, I, I, P, I, I, I, P, I, LNG, I, I, P],
+            "la_moe32": [I, I, P, I, I, I, P, P, I, P, I, I, I, P, P, I, LNG, I, I, P],
             "la_qgemm32_2": [I, P, P, P, I, I, P, P, P, I, I, P, I, I, I, P, I, LNG, I, I, P],
             "la_qgemm32_glu": [I, P, P, P, I, P, P, P, I, I, I, P, I, I, P, I, I, I, P],
             "la_qgemm32_probe": [I, I, P, P, I, I, P, I, I, P, P],
@@ -1774,6 +1775,19 @@ class MoEWeights:
                 qw[e]["p"] = [_ptr(p) or 0 for p in w.planes]
                 qw[e]["N"], qw[e]["K"] = w.N, w.K
             self.desc = torch.from_numpy(qw.view(np.uint8).copy()).to(dev)
+        self._desc32 = None
+
+    def desc32(self) -> torch.Tensor:
+        """Descriptors for the 32x32x16 grouped GEMM (la_moe32): {codes, aux, blocked scale
+        plane, -} per expert; the scale planes are built on first use (0.125 B per weight)."""
+        if self._desc32 is None:
+            qw = np.zeros(self.E, dtype=[("p", "<u8", 4), ("N", "<i4"), ("K", "<i4")])
+            for e, w in enumerate(self.experts):
+                p0, p1, g = w.tile_planes()
+                qw[e]["p"] = [p0 or 0, p1 or 0, g or 0, 0]
+                qw[e]["N"], qw[e]["K"] = w.N, w.K
+            self._desc32 = torch.from_numpy(qw.view(np.uint8).copy()).to(self.desc.device)
+        return self._desc32
 
 
 def moe_router(xn: torch.Tensor, router: torch.Tensor, topk: int, renorm: bool, scale: float = 1.0,
@@ -1866,6 +1880,82 @@ def moe_linear(x: torch.Tensor, mw: MoEWeights, order: torch.Tensor, off: torch.
     _check(lib().la_moe_gemm(mw.fmt, 1 if down else 0, mw.desc.data_ptr(), mw.N, mw.K, mw.E, order.data_ptr(),
                              off.data_ptr(), topk, x.data_ptr(), x.shape[1], maxM, S,
                              _ptr(wts) if down else None, out.data_ptr(), mw.N, slab, T, _stream()), "la_moe_gemm")
+    return Partial(out)
+
+
+# Grouped expert GEMMs on the 32x32x16 tile (gemm_q32.hip moe32_kernel) for batches of at least
+# MOE32_MIN_T tokens: gate|up with the SwiGLU fused (bf16 h in grouped row order), then the
+# routing-weighted down projection.  Variant ids: gemm_q32.hip moe32_var.
+MOE32 = os.environ.get("LOCALAI_AMD_MOE32", "1") == "1"
+# Variant by batch (scripts/moe_bench.py, Mixtral-8x7B shapes, gpurun_out/r5_moe32_bench.log):
+# T = 64: 32-row tiles, 4 workgroups per CU (var 9) 156 + 86 us vs the 16-column kernel's
+# 285 + 9 (act) + 143; T = 128 / 256: 64-row tiles in 8-wave workgroups (var 4) 180 + 91 /
+# 291 + 162 us vs 276 + 15 + 145 / 470 + 16 + 255.
+MOE32_MIN_T = int(os.environ.get("LOCALAI_AMD_MOE32_MIN_T", "33"))
+MOE32_SMALL_T = 96     # below: var 9 (32-row tiles); from here: var 4
+MOE32_VAR_GLU = int(os.environ.get("LOCALAI_AMD_MOE32_VAR_GLU", "-1"))     # -1: by batch
+MOE32_VAR_DOWN = int(os.environ.get("LOCALAI_AMD_MOE32_VAR_DOWN", "-1"))
+MOE32_SPLITS = int(os.environ.get("LOCALAI_AMD_MOE32_SPLITS", "0"))   # 0: picked from the tile count
+MOE32_TILES = {0: (64, 128), 1: (64, 128), 2: (64, 256), 3: (64, 256), 4: (64, 256), 5: (32, 128), 6: (128, 128),
+               7: (64, 128), 8: (64, 128), 9: (32, 128), 10: (32, 256), 11: (64, 256), 12: (32, 256),
+               13: (64, 128), 14: (32, 256)}
+_MOE32_FMTS = (FMT_Q4_K, FMT_Q6_K, FMT_Q8_0)
+
+
+def moe32_ok(gu: "MoEWeights", down: "MoEWeights", T: int) -> bool:
+    """Can the gate|up / down pair of a layer run on la_moe32 for a T-token batch."""
+    return (MOE32 and T >= MOE32_MIN_T and gu.desc is not None and down.desc is not None
+            and gu.fmt in _MOE32_FMTS and down.fmt in _MOE32_FMTS and gu.K % 256 == 0 and down.K % 256 == 0
+            and gu.N % 32 == 0 and down.K == gu.N // 2)
+
+
+def moe_glu32(x: torch.Tensor, mw: "MoEWeights", order: torch.Tensor, off: torch.Tensor, topk: int, T: int,
+              act: int = ACT_SWIGLU, var: Optional[int] = None) -> torch.Tensor:
+    """h = act(x Wg^T) * (x Wu^T) for every routed pair: x [T, K] bf16 -> h [T*topk, F] bf16 in
+    the grouping's row order (row off[e] + m is pair order[off[e] + m]); rows of pairs routed to
+    no local expert stay unwritten (the down projection never reads them)."""
+    F = mw.N // 2
+    if x.dtype != torch.bfloat16 or not x.is_contiguous() or x.shape[1] != mw.K:
+        raise ValueError("moe_glu32: x must be contiguous bf16 [T, K]")
+    h = torch.empty(T * topk, F, dtype=torch.bfloat16, device=x.device)
+    a = {ACT_SWIGLU: 0, ACT_GEGLU: 3}[act]
+    _check(lib().la_moe32(mw.fmt, 1, mw.desc32().data_ptr(), F, mw.K, mw.E, order.data_ptr(), off.data_ptr(), topk,
+                          x.data_ptr(), x.shape[1], T, 1, None, h.data_ptr(), F, 0, a,
+                          _moe32_var(MOE32_VAR_GLU, T) if var is None else var, _stream()), "la_moe32")
+    return h
+
+
+def _moe32_var(env: int, T: int) -> int:
+    return env if env >= 0 else (9 if T < MOE32_SMALL_T else 4)
+
+
+def _moe32_splits(mw: "MoEWeights", T: int, topk: int, var: int) -> int:
+    if MOE32_SPLITS:
+        S = MOE32_SPLITS
+    else:
+        bm, bn = MOE32_TILES[var]
+        live = (-(-T * topk // bm) + mw.E // 2) * -(-mw.N // bn)   # tiles with rows (balanced router)
+        S = 1
+        while S < 8 and live * S * 2 <= 1024 and mw.K // 64 >= 64 * S:
+            S *= 2
+    ks = mw.K // 64
+    while S > 1 and -(-ks // S) * (S - 1) >= ks:
+        S -= 1
+    return S
+
+
+def moe_down32(h: torch.Tensor, mw: "MoEWeights", order: torch.Tensor, off: torch.Tensor, topk: int, T: int,
+               wts: torch.Tensor, zero: bool = False, var: Optional[int] = None) -> Partial:
+    """Down projection of moe_glu32's grouped h rows -> Partial [S*topk, T, N]: slab
+    (split*topk + slot) row t holds wts[pair] * (h_pair Wd^T) of token t's slot-th pick, so the
+    consumer's slab sum is the weighted top-k combine (moe_linear's down contract)."""
+    v = _moe32_var(MOE32_VAR_DOWN, T) if var is None else var
+    S = _moe32_splits(mw, T, topk, v)
+    alloc = torch.zeros if zero else torch.empty
+    out = alloc(S * topk, T, mw.N, dtype=torch.float32, device=h.device)
+    _check(lib().la_moe32(mw.fmt, 2, mw.desc32().data_ptr(), mw.N, mw.K, mw.E, order.data_ptr(), off.data_ptr(), topk,
+                          h.data_ptr(), h.shape[1], T, S, wts.data_ptr(), out.data_ptr(), mw.N, T * mw.N, 0, v,
+                          _stream()), "la_moe32")
     return Partial(out)
 
 

@@ -45,10 +45,15 @@ LA_DEV void q32_vmwait() {
 }
 template <int L>
 LA_DEV void q32_wait_stages(int ahead) {
+  // at most `ahead` stages (L DMAs each) still in flight; vmcnt holds 6 bits
   if (ahead <= 0) q32_vmwait<0>();
   else if (ahead == 1) q32_vmwait<L>();
   else if (ahead == 2) q32_vmwait<2 * L>();
-  else q32_vmwait<3 * L>();
+  else if (ahead == 3 || 4 * L > 63) q32_vmwait<3 * L <= 63 ? 3 * L : 0>();
+  else if (ahead == 4 || 5 * L > 63) q32_vmwait<4 * L>();
+  else if (ahead == 5 || 6 * L > 63) q32_vmwait<5 * L <= 63 ? 5 * L : 0>();
+  else if (ahead == 6 || 7 * L > 63) q32_vmwait<6 * L <= 63 ? 6 * L : 0>();
+  else q32_vmwait<7 * L <= 63 ? 7 * L : 0>();
 }
 
 // One wave's columns: weight planes + row map (local column c -> weight row).
@@ -250,20 +255,29 @@ struct Q32Glu {
   int oa, ob, F, act;
 };
 
+// Grouped (MoE) tiles: MOE 1 gathers X row m from rows[m] / rdiv (a routed pair's token), MOE 2
+// scatters output row m to slab (split * rdiv + slot) row t of pair p = rows[m] (t = p / rdiv,
+// slot = p % rdiv), scaled by the routing weight wts[p].
+struct Q32Moe {
+  const int* rows;
+  int rdiv;
+  const float* wts;
+};
+
 LA_DEV float q32_gelu_tanh(float x) { return 0.5f * x * (1.f + tanhf(0.7978845608f * (x + 0.044715f * x * x * x))); }
 
 // One (M tile, N tile, K split).  GLU: columns [0, BN/2) of the tile are gate rows, [BN/2, BN)
 // the matching up rows; no split.
-template <int FMT, int BM, int WN, int NS, bool GLU, int PIPE = 0, int NW_ = 4, int ABL = 0>
+template <int FMT, int BM, int WN, int NS, bool GLU, int PIPE = 0, int NW_ = 4, int ABL = 0, int MOE = 0>
 LA_DEV void q32_tile(uint8_t* __restrict__ lds, const QW& w, int tile, const bf16* __restrict__ X, int ldx, int M,
                      int per_split, int m_tiles, int n_tiles, float* __restrict__ out, bf16* __restrict__ outb,
-                     int ldo, long slab, const Q32Glu& glu) {
+                     int ldo, long slab, const Q32Glu& glu, const Q32Moe& moe = Q32Moe{}) {
   using F = Q32F<FMT>;
   using G = Q32Geo<FMT, BM, WN, NW_>;
   constexpr int NW = G::NW, BN = G::BN, MB = BM / 32, CB = WN / 32;
   constexpr int XB = G::XB, SLOT = G::SLOT, PX = G::PX, PR = G::PR, PS = G::PS, L = G::L;
   static_assert(WN % 32 == 0 && BM % 32 == 0 && PR * 1024 == G::RW && PS * 256 == G::SW, "geometry");
-  static_assert(NS >= 2 && NS <= 4 && NS * SLOT <= 163840, "ring");
+  static_assert(NS >= 2 && NS <= 8 && NS * SLOT <= 163840, "ring");
 
   const int mt_i = tile % m_tiles;
   const int rest = tile / m_tiles;
@@ -294,7 +308,8 @@ LA_DEV void q32_tile(uint8_t* __restrict__ lds, const QW& w, int tile, const bf1
   for (int j = 0; j < PX; ++j) {
     const int r = 8 * (wave * PX + j) + (lane >> 3);
     const int c = (lane & 7) ^ ((r >> 1) & 7);  // logical chunk stored at this physical chunk
-    xoff[j] = (uint32_t)min(m0 + r, M - 1) * ldx + F::kofs(c);
+    const int mr = min(m0 + r, M - 1);
+    xoff[j] = (uint32_t)(MOE == 1 ? moe.rows[mr] / moe.rdiv : mr) * ldx + F::kofs(c);
   }
   // scale records of this wave's columns: piece p = columns 32p .. 32p+31, lane -> (column, dword)
   const uint8_t* srec[PS];
@@ -538,7 +553,19 @@ LA_DEV void q32_tile(uint8_t* __restrict__ lds, const QW& w, int tile, const bf1
         const int r = idx / CH, c4 = idx % CH;
         const f32x4 v = *(const f32x4*)(img + r * WN + 4 * c4);
         const int m = m0 + pass * ER + r, n = cbase + 4 * c4;
-        if (m < M) {
+        if (MOE == 2 && m < M) {
+          // routed pair -> (slot slab, token row), weighted: the consumer's slab sum is the combine
+          const int p = moe.rows[m], t = p / moe.rdiv, slot = p - t * moe.rdiv;
+          const float sc = moe.wts[p];
+          float* dst = out + ((size_t)split * moe.rdiv + slot) * slab + (size_t)t * ldo + n;
+          if (n + 3 < w.N) {
+            *(f32x4*)dst = f32x4{v[0] * sc, v[1] * sc, v[2] * sc, v[3] * sc};
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              if (n + e < w.N) dst[e] = v[e] * sc;
+          }
+        } else if (m < M) {
           if (n + 3 < w.N) {
             if (f32out) {
               *(f32x4*)(o + (size_t)m * ldo + n) = v;
@@ -706,6 +733,99 @@ static int q32_launch_glu(int var, const QW& wa, const Q32Glu& glu, const bf16* 
   });
 }
 
+// ---------------------------------------------------------------- grouped MoE GEMM
+// The routed rows of every expert through the same per-wave-columns MFMA tile (replaces the
+// 16-column-per-wave moe_gemm_kernel of moe.hip for wide batches: there each wave dequantised
+// its own 16 columns for 16-row MFMAs, 12.8 VALU per MFMA; here one dequantised 32-column
+// fragment feeds BM/32 32x32x16 MFMAs).  Tile id -> (row chunk fastest, column tile, split,
+// expert); chunks past an expert's row count exit at once, so any routing is one fixed launch
+// (graph-capturable).  MODE 1: gate|up of the expert (gate rows [0, F), up rows [F, 2F) of one
+// weight) with the GLU fused, bf16 h rows in grouped order (row off[e] + m); MODE 2: down
+// projection of the grouped h rows, routing-weighted fp32 output scattered to slab
+// (split * topk + slot) row token.  qws[e] = {codes, aux, blocked scale plane, -, N, K}.
+template <class C, int OCC_, int NS_ = 0>
+struct MoeCfg : C {
+  static constexpr int OCC = OCC_;  // workgroups per CU the register budget is sized for
+  static constexpr int NS = NS_;    // ring slots (0: q32_ns, <= 4); up to 8 stages of weight bytes in flight
+};
+
+template <int FMT, class C, int MODE>
+__global__ __launch_bounds__(C::NW * 64) __attribute__((amdgpu_waves_per_eu(C::NW / 4 * C::OCC, C::NW / 4 * C::OCC))) void moe32_kernel(
+    const QW* __restrict__ qws, const int* __restrict__ order, const int* __restrict__ off, int topk,
+    const bf16* __restrict__ X, int ldx, int mch, int n_tiles, int splits, int per_split, int real_tiles,
+    const float* __restrict__ wts, float* __restrict__ out, bf16* __restrict__ outb, int ldo, long slab, int F, int act) {
+  constexpr int FIT = 163840 / Q32Geo<FMT, C::BM, C::WN, C::NW>::SLOT;  // Q6_K / Q8_0 slots are larger
+  constexpr int NS = C::NS ? (C::NS < FIT ? C::NS : FIT) : q32_ns<FMT, C::BM, C::WN, C::NW>();
+  __shared__ __attribute__((aligned(1024))) uint8_t lds[NS * Q32Geo<FMT, C::BM, C::WN, C::NW>::SLOT];
+  // expert fastest, then row chunk, column tile, split; XCD-contiguous runs of tiles therefore
+  // hold every expert's tiles of a few column tiles: the XCDs stay balanced however the router
+  // skews the row counts, and the row chunks of one (expert, column tile) share its weight
+  // bytes in one L2
+  const int tile = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+  if (tile >= real_tiles) return;
+  const int E = real_tiles / (mch * n_tiles * splits);
+  const int e = tile % E;
+  int r = tile / E;
+  const int chunk = r % mch;
+  r /= mch;
+  const int nt = r % n_tiles, split = r / n_tiles;
+  const int o0 = off[e], Me = off[e + 1] - o0;
+  if (chunk * C::BM >= Me) return;
+  const int mte = (Me + C::BM - 1) / C::BM;
+  const int t2 = chunk + mte * (nt + n_tiles * split);
+  QW w = qws[e];
+  const Q32Moe mo{order + o0, topk, wts};
+  if constexpr (MODE == 1) {
+    const Q32Glu glu{w, 0, F, F, act};
+    w.N = F;
+    q32_tile<FMT, C::BM, C::WN, NS, true, C::PIPE, C::NW, 0, 1>(lds, w, t2, X, ldx, Me, w.K >> 6, mte, n_tiles,
+                                                               nullptr, outb + (size_t)o0 * ldo, ldo, 0, glu, mo);
+  } else {
+    q32_tile<FMT, C::BM, C::WN, NS, false, C::PIPE, C::NW, 0, 2>(lds, w, t2, X + (size_t)o0 * ldx, ldx, Me, per_split,
+                                                                mte, n_tiles, out, nullptr, ldo, slab, Q32Glu{}, mo);
+  }
+}
+
+// MoE variant ids (ops/__init__.py MOE32_TILES): row tile x (waves x columns per wave), schedule
+template <class Fn>
+static int moe32_var(int var, Fn&& fn) {
+  switch (var) {
+    case 0: fn(MoeCfg<Q32Cfg<64, 32, 4, 0>, 2>{}); break;
+    case 1: fn(MoeCfg<Q32Cfg<64, 32, 4, 1>, 2>{}); break;
+    case 2: fn(MoeCfg<Q32Cfg<64, 64, 4, 0>, 2>{}); break;
+    case 3: fn(MoeCfg<Q32Cfg<64, 64, 4, 1>, 2>{}); break;
+    case 4: fn(MoeCfg<Q32Cfg<64, 32, 8, 0>, 2>{}); break;
+    case 5: fn(MoeCfg<Q32Cfg<32, 32, 4, 0>, 2>{}); break;
+    case 6: fn(MoeCfg<Q32Cfg<128, 32, 4, 1>, 1>{}); break;
+    case 7: fn(MoeCfg<Q32Cfg<64, 32, 4, 0>, 3>{}); break;
+    case 8: fn(MoeCfg<Q32Cfg<64, 32, 4, 1>, 3>{}); break;
+    case 9: fn(MoeCfg<Q32Cfg<32, 32, 4, 0>, 4>{}); break;
+    case 10: fn(MoeCfg<Q32Cfg<32, 64, 4, 0>, 2>{}); break;
+    case 11: fn(MoeCfg<Q32Cfg<64, 64, 4, 0>, 1, 8>{}); break;
+    case 12: fn(MoeCfg<Q32Cfg<32, 64, 4, 0>, 2, 5>{}); break;
+    case 13: fn(MoeCfg<Q32Cfg<64, 32, 4, 0>, 1, 8>{}); break;
+    case 14: fn(MoeCfg<Q32Cfg<32, 64, 4, 0>, 1, 8>{}); break;
+    default: return -1;
+  }
+  return 0;
+}
+
+template <int FMT, int MODE>
+static int moe32_launch(int var, const QW* qws, int N, int K, int E, const int* order, const int* off, int topk,
+                        const bf16* X, int ldx, int maxM, int splits, const float* wts, float* out, bf16* outb,
+                        int ldo, long slab, int act, hipStream_t st) {
+  const int KS = K >> 6, per = (KS + splits - 1) / splits;
+  return moe32_var(var, [&](auto c) {
+    using C = decltype(c);
+    const int mch = (maxM + C::BM - 1) / C::BM;
+    const int n_tiles = MODE == 1 ? (N + C::BN / 2 - 1) / (C::BN / 2) : (N + C::BN - 1) / C::BN;
+    const long real = (long)E * mch * n_tiles * splits;
+    const int grid = (int)((real + 7) / 8 * 8);
+    hipLaunchKernelGGL((moe32_kernel<FMT, C, MODE>), dim3(grid), dim3(C::NW * 64), 0, st, qws, order, off, topk, X,
+                       ldx, mch, n_tiles, splits, per, (int)real, wts, out, outb, ldo, slab, N, act);
+  });
+}
+
 }  // namespace la
 
 // C ABI ---------------------------------------------------------------------------
@@ -806,4 +926,42 @@ extern "C" int la_qgemm32_probe(int var, int abl, const void* p0, const void* gs
     default: return -1;
   }
 #undef Q32_PROBE
+}
+
+// Grouped expert GEMM on the 32x32x16 tile (see moe32_kernel).  qws: device array of E QW
+// descriptors {p0, p1, blocked scale plane, -, N, K}; order / off: the pair grouping of
+// la_moe_route; maxM: most rows any expert can hold (<= T).
+//   mode 1: X [T][ldx] tokens -> out bf16 [P][ldo] (row off[e] + m = act(gate) * up of pair
+//           order[off[e] + m]); N = F (the expert weight holds 2F rows); splits must be 1.
+//   mode 2: X [P][ldx] grouped h rows -> out fp32 [splits * topk][T][ldo] (stride slab), each
+//           row scaled by wts[pair].
+extern "C" int la_moe32(int fmt, int mode, const void* qws, int N, int K, int E, const int* order, const int* off,
+                        int topk, const void* X, int ldx, int maxM, int splits, const float* wts, void* out, int ldo,
+                        long slab, int act, int var, void* stream) {
+  using namespace la;
+  if (maxM < 1 || N < 1 || E < 1 || (K & 255) || splits < 1 || ldo < N || ldx < K || (ldx & 7) || topk < 1) return -1;
+  if (mode == 1 && (splits != 1 || (N & 15) || (act != 0 && act != 3))) return -1;
+  if (mode == 2 && (!wts || slab < (long)maxM * ldo)) return -1;
+  if (mode != 1 && mode != 2) return -1;
+  const int KS = K / 64, per = (KS + splits - 1) / splits;
+  if (per * (splits - 1) >= KS) return -1;
+  if ((long)maxM * topk * ldx >= (1L << 31) || (long)E * ((maxM + 31) / 32) * ((N + 63) / 64) * splits >= (1L << 31)) return -1;
+  hipStream_t st = (hipStream_t)stream;
+  const QW* q = (const QW*)qws;
+  const bf16* x = (const bf16*)X;
+  float* o = mode == 2 ? (float*)out : nullptr;
+  bf16* ob = mode == 1 ? (bf16*)out : nullptr;
+  int rc;
+#define MOE32_F(F_)                                                                                                \
+  rc = mode == 1 ? moe32_launch<F_, 1>(var, q, N, K, E, order, off, topk, x, ldx, maxM, 1, wts, o, ob, ldo, slab, act, st) \
+                 : moe32_launch<F_, 2>(var, q, N, K, E, order, off, topk, x, ldx, maxM, splits, wts, o, ob, ldo, slab, act, st);
+  switch (fmt) {
+    case FMT_Q4_K: MOE32_F(FMT_Q4_K) break;
+    case FMT_Q6_K: MOE32_F(FMT_Q6_K) break;
+    case FMT_Q8_0: MOE32_F(FMT_Q8_0) break;
+    default: return -2;
+  }
+#undef MOE32_F
+  if (rc) return rc;
+  return (int)hipGetLastError();
 }

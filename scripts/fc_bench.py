@@ -4,10 +4,14 @@ every token is sampled under the GBNF grammar generated from its JSON schema), t
 gateway on the native HTTP server, on random-init Llama-3-8B Q4_K_M.  Prints tokens/s and checks
 that a non-streaming request returns a tool call whose arguments parse under the schema.
 
-    python scripts/fc_bench.py --concurrency 32 --max-tokens 64
+    python scripts/fc_bench.py --concurrency 32 [--waves 8 --max-tokens 256]
 
-The schema uses enum-valued fields so that the grammar bounds every argument; with random
-weights an open string or integer field would run to max_tokens.
+Measurement (same engine, same box): WAVES forced-tool waves and WAVES plain waves, interleaved
+(FC, plain, FC, plain, ...) so drift hits both alike; each request asks for MAX_TOKENS (256).  The
+throughput tool's schema ends in an open string field ("notes"), so a random-init model keeps
+sampling under the grammar's string state until max_tokens (the enum fields before it exercise
+the bounded states); plain waves use ignore_eos.  Reported: median tokens/s of each kind and
+their ratio.  The validity checks use the all-enum tool, whose calls close on their own.
 """
 import argparse
 import json
@@ -26,14 +30,22 @@ TOOLS = [{"type": "function", "function": {
         "unit": {"type": "string", "enum": ["celsius", "fahrenheit"]},
         "days": {"type": "string", "enum": ["1", "3", "7"]}}, "required": ["location", "unit", "days"]}}}]
 CHOICE = {"type": "function", "function": {"name": "get_weather"}}
+# throughput tool: bounded fields first, then an open string the model fills until max_tokens
+TOOLS_TP = [{"type": "function", "function": {
+    "name": "log_weather", "description": "record a weather observation",
+    "parameters": {"type": "object", "properties": {
+        "location": {"type": "string", "enum": ["paris", "tokyo", "lima", "oslo"]},
+        "unit": {"type": "string", "enum": ["celsius", "fahrenheit"]},
+        "notes": {"type": "string"}}, "required": ["location", "unit", "notes"]}}}]
+CHOICE_TP = {"type": "function", "function": {"name": "log_weather"}}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--concurrency", type=int, default=32)
-    ap.add_argument("--max-tokens", type=int, default=64)
+    ap.add_argument("--max-tokens", type=int, default=256)
     ap.add_argument("--preset", default="llama3-8b")
-    ap.add_argument("--waves", type=int, default=2)
+    ap.add_argument("--waves", type=int, default=8)
     ap.add_argument("--checks", type=int, default=8, help="non-streaming requests whose tool call is validated")
     a = ap.parse_args()
     from localai_amd.utils.loadgen import LoadGen
@@ -64,23 +76,25 @@ def main():
     url = f"http://127.0.0.1:{srv.port}/v1/chat/completions"
     extra = {"tools": TOOLS, "tool_choice": CHOICE, "temperature": 0}
     msgs = [f"(q{i}) What is the weather like in city number {i} for the next few days?" for i in range(a.concurrency)]
-    lg.wave(url, name, msgs[:2], 8, extra=extra)  # warm the grammar path
-    best = None
+    extra_tp = {"tools": TOOLS_TP, "tool_choice": CHOICE_TP, "temperature": 0}
+    lg.wave(url, name, msgs[:2], 8, extra=extra)  # warm the grammar paths
+    lg.wave(url, name, msgs[:2], 8, extra=extra_tp)
+    import statistics
+    fc_r, pl_r, fc_tok = [], [], []
     for w in range(a.waves):
         t0 = time.perf_counter()
-        _, tok = lg.wave(url, name, [f"[{w}] " + m for m in msgs], a.max_tokens, extra=extra)
-        el = time.perf_counter() - t0
-        if best is None or tok / el > best[0]:
-            best = (tok / el, tok, el)
-    # same concurrency and token budget without the grammar, on the same engine (same box)
-    plain = None
-    for w in range(a.waves):
+        _, tok = lg.wave(url, name, [f"[{w}] " + m for m in msgs], a.max_tokens, extra=extra_tp)
+        fc_r.append(tok / (time.perf_counter() - t0))
+        fc_tok.append(tok)
+        # same concurrency and token budget without the grammar, on the same engine (same box)
         t0 = time.perf_counter()
         _, tok = lg.wave(url, name, [f"[p{w}] " + m for m in msgs], a.max_tokens,
                          extra={"temperature": 0, "ignore_eos": True})
-        el = time.perf_counter() - t0
-        if plain is None or tok / el > plain:
-            plain = tok / el
+        pl_r.append(tok / (time.perf_counter() - t0))
+        print(f"wave {w}: fc {fc_r[-1]:.1f} tok/s ({fc_tok[-1]} tokens)  plain {pl_r[-1]:.1f} tok/s",
+              file=sys.stderr, flush=True)
+    fc_med, pl_med = statistics.median(fc_r), statistics.median(pl_r)
+
     def check(content):
         body = json.dumps({"model": name, "max_tokens": a.max_tokens, "messages": [{"role": "user", "content": content}],
                            **extra}).encode()
@@ -113,10 +127,14 @@ def main():
     print(f"grammar runs {m['grammar_runs']} rows {m['grammar_run_rows']} tokens {m['grammar_run_tokens']} "
           f"hit-rate {[round(v, 3) for v in eng._ghit.values()]}", file=sys.stderr, flush=True)
     print(json.dumps({"metric": "function-calling output tokens/s (forced tool, GBNF-constrained)",
-                      "value": round(best[0], 1), "plain_value": round(plain, 1), "preset": a.preset,
-                      "concurrency": a.concurrency, "max_tokens": a.max_tokens,
-                      "tokens": best[1], "wall_s": round(best[2], 3), "finish_reason": doc["choices"][0]["finish_reason"],
-                      "tool_call_valid": ok, "valid_calls": f"{n_ok}/{a.checks}", "sample_call": calls[0]["function"] if calls else msg.get("content")}),
+                      "value": round(fc_med, 1), "plain_value": round(pl_med, 1),
+                      "fc_over_plain": round(fc_med / pl_med, 3), "waves": a.waves,
+                      "fc_waves": [round(v, 1) for v in fc_r], "plain_waves": [round(v, 1) for v in pl_r],
+                      "fc_tokens_per_wave": fc_tok, "preset": a.preset, "concurrency": a.concurrency,
+                      "max_tokens": a.max_tokens, "finish_reason": doc["choices"][0]["finish_reason"],
+                      "tool_call_valid": ok, "valid_calls": f"{n_ok}/{a.checks}",
+                      "sample_call": calls[0]["function"] if calls else msg.get("content"),
+                      "k1_reasons": dict(eng.k1_reasons)}),
           flush=True)
     lg.close()
     srv.shutdown()

@@ -1,0 +1,59 @@
+"""Mixtral-8x7B-shaped MoE layer on the GPU: the 16-column grouped GEMM (moe.hip, moe_linear +
+act + moe_linear down) vs the 32x32x16 grouped tiles (gemm_q32.hip moe32, moe_glu32 +
+moe_down32), per variant, cold caches (each decode step streams every expert once).
+
+  python scripts/moe_bench.py [--T 64 128 256] [--vars 0 1 2 3 4 5 6] [--down-fmt q4k|q6k]"""
+import argparse
+import sys
+from pathlib import Path
+
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+from localai_amd import ops  # noqa: E402
+from localai_amd.gguf import GGMLType  # noqa: E402
+from scripts.gq_bench import rand_qweight, timeit  # noqa: E402
+
+DEV = torch.device("cuda:0")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--T", type=int, nargs="+", default=[64, 128, 256])
+    ap.add_argument("--vars", type=int, nargs="+", default=sorted(ops.MOE32_TILES))
+    ap.add_argument("--down-fmt", default="q4k")
+    ap.add_argument("--E", type=int, default=8)
+    a = ap.parse_args()
+    E, topk, D, F = a.E, 2, 4096, 14336
+    td = GGMLType.Q6_K if a.down_fmt == "q6k" else GGMLType.Q4_K
+    mg = ops.MoEWeights([rand_qweight(2 * F, D, GGMLType.Q4_K, 1 + e) for e in range(E)])
+    md = ops.MoEWeights([rand_qweight(D, F, td, 100 + e) for e in range(E)])
+    print(f"E={E} D={D} F={F} down={a.down_fmt} gate|up bytes/expert ~{2 * F * D * 0.5625 / 1e6:.0f} MB", flush=True)
+    for T in a.T:
+        g = torch.Generator(device=DEV).manual_seed(T)
+        x = (torch.randn(T, D, device=DEV, generator=g) * 0.5).to(torch.bfloat16)
+        ids = torch.stack([torch.randperm(E, device=DEV, generator=g)[:topk] for _ in range(T)]).to(torch.int32)
+        wts = torch.rand(T * topk, device=DEV, generator=g)
+        order, off = ops.moe_route(ids, E)
+        gu_old = lambda: ops.moe_linear(x, mg, order, off, topk, T)  # noqa: E731
+        gu = gu_old()
+        h_old = ops.act(gu, F, ops.ACT_SWIGLU)
+        t_gu = timeit(gu_old)
+        t_act = timeit(lambda: ops.act(gu, F, ops.ACT_SWIGLU))
+        t_dn = timeit(lambda: ops.moe_linear(h_old, md, order, off, topk, T, down=True, wts=wts))
+        ref = ops.moe_linear(h_old, md, order, off, topk, T, down=True, wts=wts).dense().float()
+        print(f"T={T} old: gate|up {t_gu:.1f} us + act {t_act:.1f} + down {t_dn:.1f} = {t_gu + t_act + t_dn:.1f} us",
+              flush=True)
+        for v in a.vars:
+            h = ops.moe_glu32(x, mg, order, off, topk, T, var=v)
+            d = ops.moe_down32(h, md, order, off, topk, T, wts, var=v).dense().float()
+            rel = ((d - ref).norm() / ref.norm()).item()
+            t1 = timeit(lambda: ops.moe_glu32(x, mg, order, off, topk, T, var=v))
+            t2 = timeit(lambda: ops.moe_down32(h, md, order, off, topk, T, wts, var=v))
+            gbs = E * 2 * F * D * 0.625 / t1 / 1e6
+            print(f"T={T} moe32 var {v}: glu {t1:.1f} us ({gbs:.2f} TB/s codes+scales) + down {t2:.1f} "
+                  f"(S={ops._moe32_splits(md, T, topk, v)}) = {t1 + t2:.1f} us  rel-L2 vs old {rel:.2e}", flush=True)
+
+
+if __name__ == "__main__":
+    main()

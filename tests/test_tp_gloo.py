@@ -213,3 +213,44 @@ def test_tp8_per_token_logits_70b_shaped(tmp_path_factory):
             rel = float((got[i] - ref[i]).norm() / ref[i].norm())
             cos = float(torch.nn.functional.cosine_similarity(got[i], ref[i], dim=0))
             assert rel <= 1e-2 and cos >= 0.9999, (r, i, rel, cos)
+
+
+def _argmax_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from localai_amd.models.decoder import TPInfo
+        g = torch.Generator().manual_seed(7)
+        full = torch.randn(6, 40 * world, generator=g)
+        full[1, :] = -float("inf")
+        full[1, 40 * world - 1] = 0.0           # the max in the last shard
+        full[2, :] = 1.0                        # all tied: the lowest id (rank 0, column 0)
+        full[3, 45] = full[3, 5] = 100.0        # tie across the first two shards: id 5
+        full[4, 40 * (world - 1)] = 50.0        # first column of the last shard
+        tp = TPInfo(rank=rank, world=world, group=dist.group.WORLD)
+        got = tp.argmax_cols(full[:, rank * 40:(rank + 1) * 40].contiguous())
+        q.put((rank, got.tolist(), full.argmax(-1).tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_tp_distributed_argmax(world):
+    """TPInfo.argmax_cols (the sampler of the TP greedy decode graph) equals the argmax of the
+    gathered rows, ties included (lowest id), without gathering them."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_argmax_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    for _, got, ref in res:
+        assert got == ref, (got, ref)
+    assert res[0][2][2] == 0 and res[0][2][3] == 5
