@@ -37,6 +37,14 @@ sys.path.insert(0, ROOT)
 METRIC = "output tokens/sec + p50 TTFT, /v1/chat/completions Llama-3-8B GGUF, 1/2/4/8 GPU"
 
 
+def _metric(preset: str) -> str:
+    """BASELINE.json's headline metric for the headline model; the same measurement named after
+    the model for the other presets (Mixtral, 70B ...)."""
+    if preset == "llama3-8b":
+        return METRIC
+    return METRIC.replace("Llama-3-8B GGUF", MODEL_NAMES.get(preset, preset))
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -277,7 +285,7 @@ def main():
         seq = args.prompt_len + args.max_tokens
         par = f"dp{n_rep}" + (f"xtp{tp}" if tp > 1 else "")
         out = {
-            "metric": METRIC,
+            "metric": _metric(args.preset),
             "value": round(value, 2),
             "unit": "tokens/s",
             "n_gpus": world,
@@ -364,7 +372,7 @@ def gateway_dp(args, eng, loadgen, rank, world, ctl, t_gen, t_load, t_capture):
     runner.close()
     dist.barrier(group=ctl)
     out = {
-        "metric": METRIC, "value": round(tokens / elapsed, 2), "unit": "tokens/s", "n_gpus": world,
+        "metric": _metric(args.preset), "value": round(tokens / elapsed, 2), "unit": "tokens/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1000, 2),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
         "p50_ttft_ms": round(percentile(ttfts, 50) * 1000, 2), "p90_ttft_ms": round(percentile(ttfts, 90) * 1000, 2),

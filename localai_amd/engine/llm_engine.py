@@ -85,10 +85,13 @@ class EngineConfig:
     draft_model: str = ""             # speculative decoding: draft LM GGUF (engine/speculative.DraftModel)
     quantization: str = ""            # HF checkpoints: load-time quantisation (bnb_4bit / bnb_8bit / ...)
     draft_max_seqs: int = 16          # draft-model KV cache capacity in sequences of context_size
-    # constrained rows inside multi-step graph runs (learned parse-state transitions); off by
-    # default: on random-init benchmarks rows park after ~1 token (profiles/r3_session2_measurements.md)
+    # constrained rows inside multi-step graph runs: the device transition table
+    # (grammar_advance_kernel) walks the learned parse-state transitions, permissive states
+    # (JSON strings) are expanded on the helper thread, and rows park only at table misses.  On
+    # by default since the background expansion (FC C=32: 1914 single-step round trips per 6
+    # waves -> 121; gpurun_out/r5_fc_base.log vs r5_fc_ra.log)
     grammar_run_ahead: bool = dataclasses.field(
-        default_factory=lambda: os.environ.get("LOCALAI_AMD_GRAMMAR_RUN_AHEAD", "0") == "1")
+        default_factory=lambda: os.environ.get("LOCALAI_AMD_GRAMMAR_RUN_AHEAD", "1") == "1")
 
 
 @dataclass

@@ -3,8 +3,8 @@ measuring client never shares a GIL with the server under test.
 
     python -m localai_amd.utils.loadgen        (reads one JSON job per stdin line)
 
-job  = {"url", "model", "contents": [...], "max_tokens", "extra": {...}}
-reply= {"ttft": [s...], "tokens": n, "events": e, "errors": k}   (one JSON line per job)
+job  = {"url", "model", "contents": [...], "max_tokens": n | [n per content], "extra": {...}}
+reply= {"ttft": [s...], "tokens": n, "per": [n per content], "events": e, "errors": k}   (one JSON line per job)
 
 `tokens` is the server's final usage.completion_tokens; `events` is counted on the wire: the SSE
 events that carried non-empty generated text (the server emits one per token, skipping tokens
@@ -28,9 +28,11 @@ async def _wave(job) -> dict:
     timeout = aiohttp.ClientTimeout(total=3600)
     errors = 0
     async with aiohttp.ClientSession(connector=conn, timeout=timeout) as sess:
-        async def one(c):
+        mt = job["max_tokens"]
+
+        async def one(i, c):
             nonlocal errors
-            body = {"model": job["model"], "stream": True, "max_tokens": job["max_tokens"],
+            body = {"model": job["model"], "stream": True, "max_tokens": mt[i] if isinstance(mt, list) else mt,
                     "messages": [{"role": "user", "content": c}], **job.get("extra", {})}
             t0 = time.perf_counter()
             ttft = None
@@ -58,9 +60,9 @@ async def _wave(job) -> dict:
             except Exception:
                 errors += 1
             return (ttft if ttft is not None else time.perf_counter() - t0), ntok, nev
-        res = await asyncio.gather(*[one(c) for c in job["contents"]])
-    return {"ttft": [r[0] for r in res], "tokens": sum(r[1] for r in res), "events": sum(r[2] for r in res),
-            "errors": errors}
+        res = await asyncio.gather(*[one(i, c) for i, c in enumerate(job["contents"])])
+    return {"ttft": [r[0] for r in res], "tokens": sum(r[1] for r in res), "per": [r[1] for r in res],
+            "events": sum(r[2] for r in res), "errors": errors}
 
 
 def _main():
@@ -89,23 +91,30 @@ class LoadGen:
                                        stdout=subprocess.PIPE, env=env, text=True, bufsize=1)
                       for _ in range(max(1, n_procs))]
 
-    def wave(self, url: str, model: str, contents: List[str], max_tokens: int, extra=None) -> Tuple[list, int]:
+    def wave(self, url: str, model: str, contents: List[str], max_tokens, extra=None) -> Tuple[list, int]:
+        """One concurrent wave; max_tokens: one budget for all, or a list (one per content).
+        Per-request completion counts (in content order) are left in self.last_per."""
         n = len(self.procs)
         parts = [contents[i::n] for i in range(n)]
-        for p, part in zip(self.procs, parts):
-            p.stdin.write(json.dumps({"url": url, "model": model, "contents": part, "max_tokens": max_tokens,
+        mts = [max_tokens[i::n] if isinstance(max_tokens, list) else max_tokens for i in range(n)]
+        for p, part, mt in zip(self.procs, parts, mts):
+            p.stdin.write(json.dumps({"url": url, "model": model, "contents": part, "max_tokens": mt,
                                       "extra": extra or {}}) + "\n")
             p.stdin.flush()
         ttft, tokens, events, errors = [], 0, 0, 0
-        for p, part in zip(self.procs, parts):
+        per = [0] * len(contents)
+        for k, (p, part) in enumerate(zip(self.procs, parts)):
             r = json.loads(p.stdout.readline())
             ttft += r["ttft"]
             tokens += r["tokens"]
             events += r["events"]
             errors += r["errors"]
+            for j, v in enumerate(r.get("per", [])):
+                per[k + j * n] = v
         if errors:
             raise RuntimeError(f"{errors} streaming requests failed")
         self.last_events = events
+        self.last_per = per
         return ttft, tokens
 
     def close(self):

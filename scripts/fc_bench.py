@@ -6,8 +6,8 @@ that a non-streaming request returns a tool call whose arguments parse under the
 
     python scripts/fc_bench.py --concurrency 32 [--waves 8 --max-tokens 256]
 
-Measurement (same engine, same box): WAVES forced-tool waves and WAVES plain waves, interleaved
-(FC, plain, FC, plain, ...) so drift hits both alike; each request asks for MAX_TOKENS (256).  The
+Measurement (same engine, same box): WAVES forced-tool waves, WAVES plain waves and WAVES plain
+waves with the FC wave's per-request lengths, interleaved so drift hits all alike; each request asks for MAX_TOKENS (256).  The
 throughput tool's schema ends in an open string field ("notes"), so a random-init model keeps
 sampling under the grammar's string state until max_tokens (the enum fields before it exercise
 the bounded states); plain waves use ignore_eos.  Reported: median tokens/s of each kind and
@@ -80,20 +80,26 @@ def main():
     lg.wave(url, name, msgs[:2], 8, extra=extra)  # warm the grammar paths
     lg.wave(url, name, msgs[:2], 8, extra=extra_tp)
     import statistics
-    fc_r, pl_r, fc_tok = [], [], []
+    fc_r, pl_r, pm_r, fc_tok = [], [], [], []
+    plain_extra = {"temperature": 0, "ignore_eos": True}
     for w in range(a.waves):
         t0 = time.perf_counter()
         _, tok = lg.wave(url, name, [f"[{w}] " + m for m in msgs], a.max_tokens, extra=extra_tp)
         fc_r.append(tok / (time.perf_counter() - t0))
         fc_tok.append(tok)
+        per = list(lg.last_per)
         # same concurrency and token budget without the grammar, on the same engine (same box)
         t0 = time.perf_counter()
-        _, tok = lg.wave(url, name, [f"[p{w}] " + m for m in msgs], a.max_tokens,
-                         extra={"temperature": 0, "ignore_eos": True})
+        _, tok = lg.wave(url, name, [f"[p{w}] " + m for m in msgs], a.max_tokens, extra=plain_extra)
         pl_r.append(tok / (time.perf_counter() - t0))
-        print(f"wave {w}: fc {fc_r[-1]:.1f} tok/s ({fc_tok[-1]} tokens)  plain {pl_r[-1]:.1f} tok/s",
-              file=sys.stderr, flush=True)
-    fc_med, pl_med = statistics.median(fc_r), statistics.median(pl_r)
+        # ... and with the FC wave's per-request lengths (a tool call that closes early leaves the
+        # batch thinner at the tail: the matched wave isolates the grammar's own cost)
+        t0 = time.perf_counter()
+        _, tok = lg.wave(url, name, [f"[m{w}] " + m for m in msgs], [max(1, v) for v in per], extra=plain_extra)
+        pm_r.append(tok / (time.perf_counter() - t0))
+        print(f"wave {w}: fc {fc_r[-1]:.1f} tok/s ({fc_tok[-1]} tokens)  plain {pl_r[-1]:.1f} tok/s  "
+              f"plain-matched {pm_r[-1]:.1f} tok/s ({tok} tokens)", file=sys.stderr, flush=True)
+    fc_med, pl_med, pm_med = statistics.median(fc_r), statistics.median(pl_r), statistics.median(pm_r)
 
     def check(content):
         body = json.dumps({"model": name, "max_tokens": a.max_tokens, "messages": [{"role": "user", "content": content}],
@@ -128,7 +134,8 @@ def main():
           f"hit-rate {[round(v, 3) for v in eng._ghit.values()]}", file=sys.stderr, flush=True)
     print(json.dumps({"metric": "function-calling output tokens/s (forced tool, GBNF-constrained)",
                       "value": round(fc_med, 1), "plain_value": round(pl_med, 1),
-                      "fc_over_plain": round(fc_med / pl_med, 3), "waves": a.waves,
+                      "fc_over_plain": round(fc_med / pl_med, 3), "plain_matched_value": round(pm_med, 1),
+                      "fc_over_plain_matched": round(fc_med / pm_med, 3), "waves": a.waves,
                       "fc_waves": [round(v, 1) for v in fc_r], "plain_waves": [round(v, 1) for v in pl_r],
                       "fc_tokens_per_wave": fc_tok, "preset": a.preset, "concurrency": a.concurrency,
                       "max_tokens": a.max_tokens, "finish_reason": doc["choices"][0]["finish_reason"],
