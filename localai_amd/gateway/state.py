@@ -53,10 +53,21 @@ class AppState:
             out.append(n)
         return out
 
+    EXISTS_TTL = 2.0   # seconds a model-path existence answer is reused (one stat per template lookup otherwise)
+
     def exists_in_model_path(self, name: str) -> bool:
         if not name or "/" in name or ".." in name:
             return False
-        return os.path.exists(os.path.join(self.models_path, name))
+        cache = self.__dict__.setdefault("_exists_cache", {})
+        now = time.monotonic()
+        hit = cache.get(name)
+        if hit is not None and now - hit[1] < self.EXISTS_TTL:
+            return hit[0]
+        ok = os.path.exists(os.path.join(self.models_path, name))
+        if len(cache) > 4096:
+            cache.clear()
+        cache[name] = (ok, now)
+        return ok
 
     def list_models(self, flt=None, policy: int = SKIP_IF_CONFIGURED) -> List[str]:
         """services.ListModels (core/services/list_models.go:17-49)."""

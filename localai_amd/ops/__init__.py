@@ -86,6 +86,7 @@ def lib():
             "la_qgemm_glu": [I, P, P, P, I, P, P, P, I, I, I, P, I, I, P, I, I, I, P],
             "la_qgemm32": [I, P, P, P, I, I, P, I, I, I, P, I, LNG, I, I, P],
             "la_moe32": [I, I, P, I, I, I, P, P, I, P, I, I, I, P, P, I, LNG, I, I, P],
+            "la_moe32_probe": [I, P, I, I, I, P, P, I, P, I, I, P, I, P],
             "la_qgemm32_2": [I, P, P, P, I, I, P, P, P, I, I, P, I, I, I, P, I, LNG, I, I, P],
             "la_qgemm32_glu": [I, P, P, P, I, P, P, P, I, I, I, P, I, I, P, I, I, I, P],
             "la_qgemm32_probe": [I, I, P, P, I, I, P, I, I, P, P],

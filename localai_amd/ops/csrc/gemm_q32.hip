@@ -749,7 +749,7 @@ struct MoeCfg : C {
   static constexpr int NS = NS_;    // ring slots (0: q32_ns, <= 4); up to 8 stages of weight bytes in flight
 };
 
-template <int FMT, class C, int MODE>
+template <int FMT, class C, int MODE, int ABL = 0>
 __global__ __launch_bounds__(C::NW * 64) __attribute__((amdgpu_waves_per_eu(C::NW / 4 * C::OCC, C::NW / 4 * C::OCC))) void moe32_kernel(
     const QW* __restrict__ qws, const int* __restrict__ order, const int* __restrict__ off, int topk,
     const bf16* __restrict__ X, int ldx, int mch, int n_tiles, int splits, int per_split, int real_tiles,
@@ -778,10 +778,10 @@ __global__ __launch_bounds__(C::NW * 64) __attribute__((amdgpu_waves_per_eu(C::N
   if constexpr (MODE == 1) {
     const Q32Glu glu{w, 0, F, F, act};
     w.N = F;
-    q32_tile<FMT, C::BM, C::WN, NS, true, C::PIPE, C::NW, 0, 1>(lds, w, t2, X, ldx, Me, w.K >> 6, mte, n_tiles,
+    q32_tile<FMT, C::BM, C::WN, NS, true, C::PIPE, C::NW, ABL, 1>(lds, w, t2, X, ldx, Me, w.K >> 6, mte, n_tiles,
                                                                nullptr, outb + (size_t)o0 * ldo, ldo, 0, glu, mo);
   } else {
-    q32_tile<FMT, C::BM, C::WN, NS, false, C::PIPE, C::NW, 0, 2>(lds, w, t2, X + (size_t)o0 * ldx, ldx, Me, per_split,
+    q32_tile<FMT, C::BM, C::WN, NS, false, C::PIPE, C::NW, ABL, 2>(lds, w, t2, X + (size_t)o0 * ldx, ldx, Me, per_split,
                                                                 mte, n_tiles, out, nullptr, ldo, slab, Q32Glu{}, mo);
   }
 }
@@ -963,5 +963,29 @@ extern "C" int la_moe32(int fmt, int mode, const void* qws, int N, int K, int E,
   }
 #undef MOE32_F
   if (rc) return rc;
+  return (int)hipGetLastError();
+}
+
+// Probe (scripts/moe_bench.py --abl): la_moe32 mode 1, Q4_K, variant 4 geometry, with q32_tile's
+// ablation bits (1 no MFMA, 2 no dequant, 4 no DMA, 8 no A LDS reads, 16 no mid-step barrier).
+extern "C" int la_moe32_probe(int abl, const void* qws, int N, int K, int E, const int* order, const int* off,
+                              int topk, const void* X, int ldx, int maxM, void* out, int ldo, void* stream) {
+  using namespace la;
+  using C = MoeCfg<Q32Cfg<64, 32, 8, 0>, 2>;
+  const int mch = (maxM + C::BM - 1) / C::BM, n_tiles = (N + C::BN / 2 - 1) / (C::BN / 2);
+  const long real = (long)E * mch * n_tiles;
+  const int grid = (int)((real + 7) / 8 * 8);
+  hipStream_t st = (hipStream_t)stream;
+#define MOE32_P(A)                                                                                              \
+  case A:                                                                                                       \
+    hipLaunchKernelGGL((moe32_kernel<FMT_Q4_K, C, 1, A>), dim3(grid), dim3(C::NW * 64), 0, st, (const QW*)qws, order, \
+                       off, topk, (const bf16*)X, ldx, mch, n_tiles, 1, K >> 6, (int)real, nullptr, nullptr, (bf16*)out, \
+                       ldo, 0L, N, 0);                                                                            \
+    break;
+  switch (abl) {
+    MOE32_P(1) MOE32_P(2) MOE32_P(3) MOE32_P(4) MOE32_P(8) MOE32_P(16) MOE32_P(11)
+    default: return -1;
+  }
+#undef MOE32_P
   return (int)hipGetLastError();
 }

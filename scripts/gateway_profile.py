@@ -98,6 +98,8 @@ def main():
     if prof is not None:
         import pstats
         pstats.Stats(prof).sort_stats(os.environ.get("SORT", "tottime")).print_stats(30)
+        if os.environ.get("PROF_OUT"):
+            prof.dump_stats(os.environ["PROF_OUT"])
 
 
 if __name__ == "__main__":

@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--vars", type=int, nargs="+", default=sorted(ops.MOE32_TILES))
     ap.add_argument("--down-fmt", default="q4k")
     ap.add_argument("--E", type=int, default=8)
+    ap.add_argument("--abl", action="store_true", help="ablation probes of the gate|up kernel (variant 4)")
     a = ap.parse_args()
     E, topk, D, F = a.E, 2, 4096, 14336
     td = GGMLType.Q6_K if a.down_fmt == "q6k" else GGMLType.Q4_K
@@ -44,6 +45,20 @@ def main():
         ref = ops.moe_linear(h_old, md, order, off, topk, T, down=True, wts=wts).dense().float()
         print(f"T={T} old: gate|up {t_gu:.1f} us + act {t_act:.1f} + down {t_dn:.1f} = {t_gu + t_act + t_dn:.1f} us",
               flush=True)
+        if a.abl:
+            F_ = mg.N // 2
+            h = torch.empty(T * topk, F_, dtype=torch.bfloat16, device=DEV)
+            base = timeit(lambda: ops.moe_glu32(x, mg, order, off, topk, T, var=4))
+            res = [f"base {base:.1f}"]
+            for ab in (1, 2, 3, 4, 8, 11, 16):
+                def fn(ab=ab):
+                    rc = ops.lib().la_moe32_probe(ab, mg.desc32().data_ptr(), F_, mg.K, mg.E, order.data_ptr(),
+                                                  off.data_ptr(), topk, x.data_ptr(), x.shape[1], T, h.data_ptr(),
+                                                  F_, ops._stream())
+                    assert rc == 0, rc
+                res.append(f"abl{ab} {timeit(fn):.1f}")
+            print(f"T={T} gate|up var 4 ablations (us): " + "  ".join(res), flush=True)
+            continue
         for v in a.vars:
             h = ops.moe_glu32(x, mg, order, off, topk, T, var=v)
             d = ops.moe_down32(h, md, order, off, topk, T, wts, var=v).dense().float()
