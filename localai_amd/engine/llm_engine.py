@@ -275,9 +275,14 @@ class LLMEngine:
             return
         if policy == "auto" and only_non_tile and self.device.type == "cuda":
             free, total = torch.cuda.mem_get_info(self.device)
+            # memory PyTorch's caching allocator holds but no tensor uses is free for these copies
+            free += torch.cuda.memory_reserved(self.device) - torch.cuda.memory_allocated(self.device)
             budget = int(free - (1.0 - self.cfg.gpu_memory_utilization) * total) - (4 << 30)
             kv = self._kv_blocks_wanted() * self._kv_block_bytes()
-            if need > budget - kv:
+            # copies under 1 GiB are always made (a small model beside other tenants of the GPU --
+            # e.g. earlier engines of the same process -- would otherwise lose them to a budget
+            # computed from the device-wide free memory)
+            if need > budget - kv and need > (1 << 30):
                 log.warning("not materialising %.2f GB of bf16 weight copies (%.2f GB left after the %.2f GB KV "
                             "cache): those weights are dequantised per call", need / 2**30,
                             max(0, budget - kv) / 2**30, kv / 2**30)
@@ -306,6 +311,7 @@ class LLMEngine:
         want = self._kv_blocks_wanted()
         if self.device.type == "cuda":
             free, total = torch.cuda.mem_get_info(self.device)
+            free += torch.cuda.memory_reserved(self.device) - torch.cuda.memory_allocated(self.device)
             budget = int(free - (1.0 - cfg.gpu_memory_utilization) * total) - (4 << 30)
             cap = max(64, budget // bpb)
             want = min(want, cap)

@@ -1,7 +1,9 @@
 """`diffusers` / `stablediffusion` backend servicer (backend.proto LoadModel + GenerateImage) over
 the native Stable Diffusion 1.x / 2.x / XL pipeline (models/sd.py), FLUX.1 (models/flux.py,
 `pipeline_type: FluxPipeline` or a FluxPipeline model_index.json) and Stable Diffusion 3
-(models/sd3.py, `pipeline_type: StableDiffusion3Pipeline`).
+(models/sd3.py, `pipeline_type: StableDiffusion3Pipeline`) and text-to-video
+(models/video.py, `pipeline_type: VideoDiffusionPipeline` or a TextToVideoSDPipeline
+model_index.json).
 
 Mirrors `backend/python/diffusers/backend.py`: LoadModel keeps `CFGScale` (7 when unset),
 `CLIPSkip` and `SchedulerType`; GenerateImage uses `step` (1 when unset), width / height,
@@ -70,6 +72,11 @@ class DiffusersServicer:
                 return pb.Result(success=False, message=f"single-file checkpoint: {e}")
         flux = is_flux_pipeline(path) or str(request.PipelineType or "").startswith("Flux")
         sd3 = is_sd3_pipeline(path) or str(request.PipelineType or "") == "StableDiffusion3Pipeline"
+        from ..models.video import TextToVideo, is_video_pipeline
+        # backend.py:223-226: VideoDiffusionPipeline = a text-to-video DiffusionPipeline
+        t2v = is_video_pipeline(path) or str(request.PipelineType or "") == "VideoDiffusionPipeline"
+        if t2v and not is_video_pipeline(path):
+            return pb.Result(success=False, message=f"VideoDiffusionPipeline needs a TextToVideoSDPipeline directory: {path}")
         if not (is_sd_pipeline(path) or ((flux or sd3) and os.path.isdir(path))):
             return pb.Result(success=False, message=f"not a diffusers pipeline directory: {path}")
         dev = self.device
@@ -90,7 +97,9 @@ class DiffusersServicer:
         if lora and (flux or sd3):
             return pb.Result(success=False, message="LoRA adapters are supported for SD 1.x / 2.x / XL pipelines")
         try:
-            if flux:  # backend.py:247-251: FluxPipeline; GenerateImage adds max_sequence_length=256
+            if t2v:
+                p = await asyncio.get_running_loop().run_in_executor(None, lambda: TextToVideo(path, dev))
+            elif flux:  # backend.py:247-251: FluxPipeline; GenerateImage adds max_sequence_length=256
                 p = await asyncio.get_running_loop().run_in_executor(
                     None, lambda: FluxPipeline(path, dev, max_sequence_length=256, transformer_file=flux_file))
             elif sd3:  # backend.py:235-246: StableDiffusion3Pipeline
@@ -114,6 +123,18 @@ class DiffusersServicer:
         p = self.pipe
         if p is None:
             raise RuntimeError("no model loaded")
+        from ..models.video import TextToVideo, export_video
+        if isinstance(p, TextToVideo):
+            # backend.py:445-448: num_frames = FRAMES (64), num_inference_steps = step, guidance
+            # cfg_scale; export_to_video at FPS (7)
+            frames = int(os.environ.get("FRAMES", "64"))
+            fps = int(os.environ.get("FPS", "7"))
+            with self._lock:
+                v = p(request.positive_prompt, request.negative_prompt or "", request.width or 256,
+                      request.height or 256, num_frames=frames, steps=int(request.step or 25),
+                      guidance_scale=self.cfg_scale, seed=request.seed if request.seed > 0 else None)
+                export_video(v, request.dst, fps)
+            return
         default_px = p.unet_sample_size * p.vae_scale
         options = {"negative_prompt": request.negative_prompt, "width": request.width, "height": request.height,
                    "num_inference_steps": request.step if request.step else 1}

@@ -951,6 +951,59 @@ def write_sd_pipeline(out_dir: str, size: str = "tiny", seed: int = 0, v_predict
     return out_dir
 
 
+def write_t2v_pipeline(out_dir: str, seed: int = 0) -> str:
+    """Random-init text-to-video pipeline (diffusers TextToVideoSDPipeline layout: a two-level
+    UNet3DConditionModel toy, the SD VAE, a CLIP text encoder and its byte-level tokenizer, a DDIM
+    scheduler) for models/video.py."""
+    import torch
+    import transformers as tf
+    from safetensors.torch import save_file
+
+    from .sd import VaeDecoder, VaeEncoder
+    from .video import UNet3D
+    uc = {"_class_name": "UNet3DConditionModel", "act_fn": "silu", "attention_head_dim": 8,
+          "block_out_channels": [32, 64], "cross_attention_dim": 32, "layers_per_block": 1, "in_channels": 4,
+          "out_channels": 4, "norm_num_groups": 8, "norm_eps": 1e-5, "sample_size": 8,
+          "down_block_types": ["CrossAttnDownBlock3D", "DownBlock3D"],
+          "up_block_types": ["UpBlock3D", "CrossAttnUpBlock3D"]}
+    vc = dict(SD15_VAE, block_out_channels=[16, 32], layers_per_block=1, norm_num_groups=8)
+    vocab = _clip_byte_vocab()
+    tc = dict(SD15_TEXT, hidden_size=32, num_hidden_layers=2, num_attention_heads=2, intermediate_size=64,
+              vocab_size=len(vocab), bos_token_id=vocab["<|startoftext|>"], eos_token_id=vocab["<|endoftext|>"],
+              pad_token_id=vocab["<|endoftext|>"], hidden_act="gelu")
+    torch.manual_seed(seed)
+    for sub in ("unet", "vae", "text_encoder", "tokenizer", "scheduler"):
+        os.makedirs(os.path.join(out_dir, sub), exist_ok=True)
+    unet = UNet3D(uc)
+    with torch.no_grad():  # temporal layers scaled up so they visibly mix frames in the toy
+        for n_, p_ in unet.named_parameters():
+            if ".temp_" in n_ or n_.startswith("transformer_in."):
+                p_.mul_(4.0)
+    with open(os.path.join(out_dir, "unet", "config.json"), "w") as f:
+        json.dump(uc, f)
+    save_file({k: v.contiguous() for k, v in unet.state_dict().items()},
+              os.path.join(out_dir, "unet", "diffusion_pytorch_model.safetensors"))
+    sd = VaeDecoder(vc).state_dict()
+    sd.update(VaeEncoder(vc).state_dict())
+    with open(os.path.join(out_dir, "vae", "config.json"), "w") as f:
+        json.dump(dict(vc, _class_name="AutoencoderKL"), f)
+    save_file({k: v.contiguous() for k, v in sd.items()}, os.path.join(out_dir, "vae", "diffusion_pytorch_model.safetensors"))
+    tf.CLIPTextModel(tf.CLIPTextConfig(**tc)).save_pretrained(os.path.join(out_dir, "text_encoder"), safe_serialization=True)
+    with open(os.path.join(out_dir, "tokenizer", "vocab.json"), "w") as f:
+        json.dump(vocab, f)
+    with open(os.path.join(out_dir, "tokenizer", "merges.txt"), "w") as f:
+        f.write("#version: 0.2\n")
+    with open(os.path.join(out_dir, "scheduler", "scheduler_config.json"), "w") as f:
+        json.dump({"_class_name": "DDIMScheduler", "beta_start": 0.00085, "beta_end": 0.012,
+                   "beta_schedule": "scaled_linear", "num_train_timesteps": 1000, "steps_offset": 1,
+                   "set_alpha_to_one": False, "clip_sample": False, "prediction_type": "epsilon"}, f)
+    with open(os.path.join(out_dir, "model_index.json"), "w") as f:
+        json.dump({"_class_name": "TextToVideoSDPipeline", "unet": ["diffusers", "UNet3DConditionModel"],
+                   "vae": ["diffusers", "AutoencoderKL"], "text_encoder": ["transformers", "CLIPTextModel"],
+                   "tokenizer": ["transformers", "CLIPTokenizer"], "scheduler": ["diffusers", "DDIMScheduler"]}, f)
+    return out_dir
+
+
 def write_sd_single_file(path: str, size: str = "tiny", seed: int = 0, fam: str = "", hints: bool = True) -> str:
     """A random-init Stable Diffusion checkpoint as ONE file in the original LDM / SGM layout
     (what `from_single_file` reads: the AIO DreamShaper_8_pruned.safetensors shape at
