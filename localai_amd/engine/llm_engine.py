@@ -268,6 +268,12 @@ class LLMEngine:
             groups.append([m.output])
         need = sum(w.N * w.K * 2 for grp in groups for w in grp if w.bf16 is None and w.fmt != ops.FMT_BF16)
         if not need:
+            # only bf16-format weights (or copies made already): their "copy" is a view of the planes
+            for grp in groups:
+                for w in grp:
+                    w.materialize_bf16()
+                if len(grp) > 1:
+                    ops.fuse_bf16(grp)
             return
         policy = os.environ.get("LOCALAI_AMD_BF16_COPIES", "auto")
         if policy == "never" and only_non_tile:

@@ -49,6 +49,7 @@ def lib():
         sig = {
             "la_qgemm_skinny": [I, P, P, P, P, I, I, P, I, I, I, P, I, LNG, P],
             "la_qgemv_dp4": [I, P, P, P, I, P, I, I, I, P, I, LNG, P, LNG, I, P, I, P],
+            "la_qgemv_dp4_red": [I, P, P, P, I, P, I, I, I, P, I, LNG, P, LNG, I, P, I, P, P],
             "la_moe_gemv": [I, I, P, I, I, I, P, I, I, P, I, I, P, LNG, I, I, P, P, I, LNG, P],
             "la_gemv_variant": [I],
             "la_moe_tune": [I, I],
@@ -420,11 +421,28 @@ def _gemv_splits(ws, K: int, M: int) -> int:
     return S
 
 
+# split-K partials of the decode GEMV summed inside the kernel (gemv_dp4.hip gv_reduce): the
+# consumers -- add_norm, the next GEMV's activation / norm prologue -- read ONE slab.  Off: every
+# workgroup's agent-scope release writes back its XCD's L2 before the ticket, and at ~1000
+# workgroups per GEMV that costs more than the slab reads it saves -- engine C=1 260.9 vs 436.4
+# tok/s, C=2 304.5 vs 727.4 (gpurun_out/r5_c*_red.log vs *_nored.log)
+GEMV_REDUCE = os.environ.get("LOCALAI_AMD_GEMV_REDUCE", "0") == "1"
+_GV_TICKETS: dict = {}
+
+
+def _gv_tickets(dev: torch.device) -> torch.Tensor:
+    t = _GV_TICKETS.get(dev)
+    if t is None:
+        t = _GV_TICKETS[dev] = torch.zeros(int(lib().la_gv_max_tickets()), dtype=torch.int32, device=dev)
+    return t
+
+
 def gemv_dp4(x: Optional[torch.Tensor], ws: Sequence[QWeight], S: int, out: torch.Tensor,
-             act_src: Optional[Partial] = None, act_mode: int = 0) -> None:
+             act_src: Optional[Partial] = None, act_mode: int = 0, reduce_splits: bool = False) -> None:
     """out[S, M, sum(N)] = split-K partials of x @ [W0; W1; ...]^T from the int8-dot decode GEMV,
     up to 3 weights (mixed Q4_K / Q6_K, same K) per launch.  With act_src (fp32 gate|up slabs)
-    x = act(act_src) is formed inside the GEMV prologue instead of being read."""
+    x = act(act_src) is formed inside the GEMV prologue instead of being read.  reduce_splits:
+    the S partials are summed in the kernel into out[0] (the result is out[:1])."""
     M = out.shape[1]
     K = ws[0].K
     a = (None, 0, 0, None) if act_src is None else act_src.src_args()
@@ -444,9 +462,12 @@ def gemv_dp4(x: Optional[torch.Tensor], ws: Sequence[QWeight], S: int, out: torc
         fmts = (ctypes.c_int * n)(*[w.fmt for w in seg])
         planes = (ctypes.c_void_p * (4 * n))(*[p for w in seg for p in w.ptrs()])
         Ns = (ctypes.c_int * n)(*[w.N for w in seg])
-        _check(lib().la_qgemv_dp4(n, fmts, planes, Ns, K, None if x is None else x.data_ptr(), K, M, S,
-                                  out.data_ptr() + col * 4, Ntot, M * Ntot, a[0], a[1], a[2], a[3], act_mode,
-                                  _stream()), "la_qgemv_dp4")
+        args = (n, fmts, planes, Ns, K, None if x is None else x.data_ptr(), K, M, S, out.data_ptr() + col * 4,
+                Ntot, M * Ntot, a[0], a[1], a[2], a[3], act_mode)
+        if reduce_splits and S > 1:
+            _check(lib().la_qgemv_dp4_red(*args, _gv_tickets(out.device).data_ptr(), _stream()), "la_qgemv_dp4_red")
+        else:
+            _check(lib().la_qgemv_dp4(*args, _stream()), "la_qgemv_dp4")
         col += sum(w.N for w in seg)
 
 
@@ -1051,8 +1072,9 @@ def linear_multi(x: torch.Tensor, ws: Sequence[QWeight], bias: Optional[torch.Te
         out = out_slabs
         if out is None or out.shape != (S, M, Ntot):
             out = torch.empty(S, M, Ntot, dtype=torch.float32, device=x.device)
-        gemv_dp4(x, ws, S, out)
-        return Partial(out, bias)
+        red = GEMV_REDUCE and S > 1 and out_slabs is None
+        gemv_dp4(x, ws, S, out, reduce_splits=red)
+        return Partial(out[:1] if red else out, bias)
     if use_skinny:
         S = min(pick_splits(w.N, w.K, M) for w in ws)
         nsb = K // 256
@@ -1319,8 +1341,9 @@ def act_linear(src: Partial, F: int, mode: int, w: QWeight) -> Partial:
             and w.K == F and src.N == width):
         S = _gemv_splits([w], w.K, M)
         out = torch.empty(S, M, w.N, dtype=torch.float32, device=src.t.device)
-        gemv_dp4(None, [w], S, out, act_src=src, act_mode=mode)
-        return Partial(out)
+        red = GEMV_REDUCE and S > 1
+        gemv_dp4(None, [w], S, out, act_src=src, act_mode=mode, reduce_splits=red)
+        return Partial(out[:1] if red else out)
     return linear(act(src, F, mode), w)
 
 

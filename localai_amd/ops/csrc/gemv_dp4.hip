@@ -47,7 +47,10 @@ struct GVArgs {
   int blk_end[GV_SEGS];  // exclusive prefix sum of row blocks
   int col0[GV_SEGS];     // first output column of each segment
   int nseg;
+  int* tickets;          // non-null: split-K partials reduced in the kernel (gv_reduce), one per row block
 };
+
+constexpr int GV_MAX_TICKETS = 8192;  // row blocks of one launch with an in-kernel split-K reduction
 
 LA_DEV int dot4(uint32_t a, uint32_t b, int c) { return __builtin_amdgcn_sdot4((int)a, (int)b, c, false); }
 
@@ -846,6 +849,49 @@ LA_DEV void gv_q8(const QW& w, int row0, const bf16* X, int ldx, const GVAct& ac
   gv_store<MT, RS>(acc, n, w.N, M, t, o, ldo, col0, rp);
 }
 
+// In-kernel split-K reduction: the last of the gridDim.y workgroups of a row block to finish
+// (agent-scope release / ticket / acquire, the attention kernel's partition-merge protocol) sums
+// the block's S partial rows into slab 0, so the consumer -- the next GEMV's activation or norm
+// prologue, add_norm -- reads one slab instead of S (each of ~1000 consumer workgroups re-read
+// all S before).  The ticket resets itself for the next launch / graph replay.
+template <int RS>
+LA_DEV void gv_reduce(const GVArgs& a, int seg, int blk, int row0, float* __restrict__ out, int ldo, long slab,
+                      int M) {
+  __shared__ int last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int* tk = a.tickets + blk;
+    const int prev = __hip_atomic_fetch_add(tk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = prev == (int)gridDim.y - 1;
+    if (last) {
+      *tk = 0;
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!last) return;
+  constexpr int NR = 32 * RS;
+  const int N = a.w[seg].N, S = gridDim.y;
+  for (int i = threadIdx.x; i < M * NR; i += GV_THREADS) {
+    const int m = i / NR, n = row0 + i % NR;
+    if (n >= N) continue;
+    const long idx = (long)m * ldo + a.col0[seg] + n;
+    float v[8], acc = 0.f;
+    for (int y0 = 0; y0 < S; y0 += 8) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = out[(long)min(y0 + j, S - 1) * slab + idx];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (y0 + j < S) acc += v[j];
+    }
+    out[idx] = acc;
+  }
+}
+
 // Segments [0, nA) are format FA, [nA, nseg) format FB (a q|k + v fusion is (Q4_K, Q6_K)).
 // VAR bit 0: non-temporal weight loads; bit 1: weights requested before the x prologue.
 template <int MT, int FA, int FB, int VAR>
@@ -874,6 +920,7 @@ __global__ __launch_bounds__(GV_THREADS) void qgemv_dp4_kernel(GVArgs a, const b
     if constexpr (FB == FMT_Q4_K) gv_q4k<MT, NT, EARLY, RS, PD, NM>(a.w[seg], row0, X, ldx, act, M, kper, o, ldo, a.col0[seg], xq, bs, dx, rp);
     else gv_q6k<MT, NT, EARLY, RS, PD, NM>(a.w[seg], row0, X, ldx, act, M, kper, o, ldo, a.col0[seg], xq, bs, dx, rp);
   }
+  if (a.tickets && gridDim.y > 1) gv_reduce<RS>(a, seg, blk, row0, out, ldo, slab, M);
 }
 
 // MoE decode (1-2 tokens): the routed experts' projections as GEMVs on the int8-dot path.  One
@@ -971,7 +1018,8 @@ static int launch_gv_m(const GVArgs& a, int nblk, int K, const bf16* X, int ldx,
 static int qgemv_dp4_impl(int nseg, const int* fmts, const void* const* planes, const int* Ns, int K,
                           const void* X, int ldx, int M, int splits, void* out, int ldo, long slab,
                           const void* act_p, long act_slab, int act_S, const void* act_bias, int act_mode,
-                          void* stream, const la::GVRope& rp, const la::GVAct* norm = nullptr) {
+                          void* stream, const la::GVRope& rp, const la::GVAct* norm = nullptr,
+                          int* tickets = nullptr) {
   using namespace la;
   if (nseg < 1 || nseg > GV_SEGS || M < 1 || M > 4 || (K & 255) || splits < 1 || ((K >> 8) % splits) ||
       slab < (long)M * ldo)
@@ -1019,6 +1067,8 @@ static int qgemv_dp4_impl(int nseg, const int* fmts, const void* const* planes, 
   }
   a.nseg = nseg;
   if (ldo < col) return -1;
+  if (tickets && (nblk > la::GV_MAX_TICKETS || rp.q_out || norm)) return -1;
+  a.tickets = splits > 1 ? tickets : nullptr;
   // formats must form at most two runs: [FA ...][FB ...]
   int fa = a.fmt[0], fb = a.fmt[nseg - 1];
   for (int i = 0; i < nseg; ++i)
@@ -1038,6 +1088,20 @@ static int qgemv_dp4_impl(int nseg, const int* fmts, const void* const* planes, 
   if (rc) return rc;
   return (int)hipGetLastError();
 }
+
+// la_qgemv_dp4 with the split-K partials summed in the kernel into slab 0 (tickets: a zeroed int
+// array of >= GV_MAX_TICKETS entries, private to the stream; it is left zeroed).
+extern "C" int la_qgemv_dp4_red(int nseg, const int* fmts, const void* const* planes, const int* Ns, int K,
+                                const void* X, int ldx, int M, int splits, void* out, int ldo, long slab,
+                                const void* act_p, long act_slab, int act_S, const void* act_bias, int act_mode,
+                                void* tickets, void* stream) {
+  la::GVRope rp{};
+  if (!tickets) return -1;
+  return qgemv_dp4_impl(nseg, fmts, planes, Ns, K, X, ldx, M, splits, out, ldo, slab, act_p, act_slab, act_S,
+                        act_bias, act_mode, stream, rp, nullptr, (int*)tickets);
+}
+
+extern "C" int la_gv_max_tickets() { return la::GV_MAX_TICKETS; }
 
 extern "C" int la_qgemv_dp4(int nseg, const int* fmts, const void* const* planes, const int* Ns, int K,
                             const void* X, int ldx, int M, int splits, void* out, int ldo, long slab,

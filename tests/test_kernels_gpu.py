@@ -873,3 +873,42 @@ def test_attn_dense_noncausal(n, L, H, Dh):
     assert err < 2e-2 * max(1.0, ref.abs().max().item()), err
     cos = torch.nn.functional.cosine_similarity(got.flatten(), ref.flatten(), dim=0).item()
     assert cos > 0.9999, cos
+
+
+@pytest.mark.parametrize("M", [1, 2])
+def test_gemv_in_kernel_split_reduction(M, monkeypatch):
+    """gemv_dp4.hip gv_reduce: the last workgroup of each row block sums the split-K partials
+    into slab 0 -- same result as the consumer summing the slabs (fp32, order may differ), the
+    tickets reset themselves (repeated launches and a graph replay agree), and the fused
+    activation prologue (down GEMV reading gate|up) sees the reduced slab."""
+    K, N = 4096, 4160
+    w = _qw(N, K, GGMLType.Q4_K, seed=71)
+    wd = _qw(2048, 2048, GGMLType.Q6_K, seed=72)
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    monkeypatch.setattr(ops, "GEMV_REDUCE", False)
+    ref = ops.reduce(ops.linear(x, w))
+    monkeypatch.setattr(ops, "GEMV_REDUCE", True)
+    p = ops.linear(x, w)
+    assert p.S == 1
+    got = ops.reduce(p)
+    assert (got - ref).abs().max().item() <= 1e-4 * max(1.0, ref.abs().max().item())
+    for _ in range(3):
+        assert torch.equal(ops.reduce(ops.linear(x, w)), got)
+    gu = ops.Partial(torch.randn(4, M, 4096, device=DEV))
+    monkeypatch.setattr(ops, "GEMV_REDUCE", False)
+    a0 = ops.reduce(ops.act_linear(gu, 2048, ops.ACT_SWIGLU, wd))
+    monkeypatch.setattr(ops, "GEMV_REDUCE", True)
+    a1 = ops.reduce(ops.act_linear(gu, 2048, ops.ACT_SWIGLU, wd))
+    assert (a1 - a0).abs().max().item() <= 1e-4 * max(1.0, a0.abs().max().item())
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        ops.linear(x, w)
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        gp = ops.linear(x, w)
+    for _ in range(2):
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(ops.reduce(gp), got)
