@@ -975,10 +975,6 @@ def write_t2v_pipeline(out_dir: str, seed: int = 0) -> str:
     for sub in ("unet", "vae", "text_encoder", "tokenizer", "scheduler"):
         os.makedirs(os.path.join(out_dir, sub), exist_ok=True)
     unet = UNet3D(uc)
-    with torch.no_grad():  # temporal layers scaled up so they visibly mix frames in the toy
-        for n_, p_ in unet.named_parameters():
-            if ".temp_" in n_ or n_.startswith("transformer_in."):
-                p_.mul_(4.0)
     with open(os.path.join(out_dir, "unet", "config.json"), "w") as f:
         json.dump(uc, f)
     save_file({k: v.contiguous() for k, v in unet.state_dict().items()},

