@@ -1,9 +1,9 @@
 """`diffusers` / `stablediffusion` backend servicer (backend.proto LoadModel + GenerateImage) over
 the native Stable Diffusion 1.x / 2.x / XL pipeline (models/sd.py), FLUX.1 (models/flux.py,
 `pipeline_type: FluxPipeline` or a FluxPipeline model_index.json) and Stable Diffusion 3
-(models/sd3.py, `pipeline_type: StableDiffusion3Pipeline`) and text-to-video
+(models/sd3.py, `pipeline_type: StableDiffusion3Pipeline`), text-to-video
 (models/video.py, `pipeline_type: VideoDiffusionPipeline` or a TextToVideoSDPipeline
-model_index.json).
+model_index.json) and image-to-video (models/svd.py, `pipeline_type: StableVideoDiffusionPipeline`).
 
 Mirrors `backend/python/diffusers/backend.py`: LoadModel keeps `CFGScale` (7 when unset),
 `CLIPSkip` and `SchedulerType`; GenerateImage uses `step` (1 when unset), width / height,
@@ -72,12 +72,17 @@ class DiffusersServicer:
                 return pb.Result(success=False, message=f"single-file checkpoint: {e}")
         flux = is_flux_pipeline(path) or str(request.PipelineType or "").startswith("Flux")
         sd3 = is_sd3_pipeline(path) or str(request.PipelineType or "") == "StableDiffusion3Pipeline"
+        from ..models.svd import StableVideoDiffusion, is_svd_pipeline
         from ..models.video import TextToVideo, is_video_pipeline
         # backend.py:223-226: VideoDiffusionPipeline = a text-to-video DiffusionPipeline
         t2v = is_video_pipeline(path) or str(request.PipelineType or "") == "VideoDiffusionPipeline"
         if t2v and not is_video_pipeline(path):
             return pb.Result(success=False, message=f"VideoDiffusionPipeline needs a TextToVideoSDPipeline directory: {path}")
-        if not (is_sd_pipeline(path) or ((flux or sd3) and os.path.isdir(path))):
+        # backend.py:199-205: StableVideoDiffusionPipeline (img2vid)
+        i2v = is_svd_pipeline(path) or str(request.PipelineType or "") == "StableVideoDiffusionPipeline"
+        if i2v and not is_svd_pipeline(path):
+            return pb.Result(success=False, message=f"StableVideoDiffusionPipeline directory expected: {path}")
+        if not (t2v or i2v or is_sd_pipeline(path) or ((flux or sd3) and os.path.isdir(path))):
             return pb.Result(success=False, message=f"not a diffusers pipeline directory: {path}")
         dev = self.device
         if not dev:
@@ -99,6 +104,8 @@ class DiffusersServicer:
         try:
             if t2v:
                 p = await asyncio.get_running_loop().run_in_executor(None, lambda: TextToVideo(path, dev))
+            elif i2v:
+                p = await asyncio.get_running_loop().run_in_executor(None, lambda: StableVideoDiffusion(path, dev))
             elif flux:  # backend.py:247-251: FluxPipeline; GenerateImage adds max_sequence_length=256
                 p = await asyncio.get_running_loop().run_in_executor(
                     None, lambda: FluxPipeline(path, dev, max_sequence_length=256, transformer_file=flux_file))
@@ -123,7 +130,21 @@ class DiffusersServicer:
         p = self.pipe
         if p is None:
             raise RuntimeError("no model loaded")
+        from ..models.svd import StableVideoDiffusion
         from ..models.video import TextToVideo, export_video
+        if isinstance(p, StableVideoDiffusion):
+            # backend.py:435-443: src resized to 1024 x 576, guidance cfg_scale (the top of the
+            # per-frame ramp), decode_chunk_size CHUNK_SIZE (8), export_to_video at FPS (7)
+            if not request.src:
+                raise ValueError("StableVideoDiffusionPipeline needs a source image (src)")
+            fps = int(os.environ.get("FPS", "7"))
+            with self._lock:
+                v = p(request.src, request.width or 1024, request.height or 576, steps=int(request.step or 25),
+                      max_guidance_scale=self.cfg_scale, fps=fps,
+                      decode_chunk_size=int(os.environ.get("CHUNK_SIZE", "8")),
+                      seed=request.seed if request.seed > 0 else None)
+                export_video(v, request.dst, fps)
+            return
         if isinstance(p, TextToVideo):
             # backend.py:445-448: num_frames = FRAMES (64), num_inference_steps = step, guidance
             # cfg_scale; export_to_video at FPS (7)

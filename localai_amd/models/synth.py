@@ -1000,6 +1000,59 @@ def write_t2v_pipeline(out_dir: str, seed: int = 0) -> str:
     return out_dir
 
 
+def write_svd_pipeline(out_dir: str, seed: int = 0) -> str:
+    """Random-init image-to-video pipeline (diffusers StableVideoDiffusionPipeline layout: a
+    two-level UNetSpatioTemporalConditionModel toy, an AutoencoderKLTemporalDecoder toy, a
+    transformers CLIPVisionModelWithProjection image encoder, an EulerDiscrete scheduler with
+    Karras sigmas / v-prediction) for models/svd.py."""
+    import torch
+    import transformers as tf
+    from safetensors.torch import save_file
+
+    from .sd import VaeEncoder
+    from .svd import TemporalVaeDecoder, UNetSTC
+    uc = {"_class_name": "UNetSpatioTemporalConditionModel", "block_out_channels": [32, 64], "layers_per_block": 1,
+          "num_attention_heads": [2, 4], "cross_attention_dim": 32, "addition_time_embed_dim": 8,
+          "projection_class_embeddings_input_dim": 24, "in_channels": 8, "out_channels": 4, "num_frames": 4,
+          "norm_num_groups": 8, "transformer_layers_per_block": 1,
+          "down_block_types": ["CrossAttnDownBlockSpatioTemporal", "DownBlockSpatioTemporal"],
+          "up_block_types": ["UpBlockSpatioTemporal", "CrossAttnUpBlockSpatioTemporal"]}
+    vc = dict(SD15_VAE, _class_name="AutoencoderKLTemporalDecoder", block_out_channels=[16, 32], layers_per_block=2,
+              norm_num_groups=8)
+    torch.manual_seed(seed)
+    for sub in ("unet", "vae", "image_encoder", "feature_extractor", "scheduler"):
+        os.makedirs(os.path.join(out_dir, sub), exist_ok=True)
+    unet = UNetSTC(uc)
+    with open(os.path.join(out_dir, "unet", "config.json"), "w") as f:
+        json.dump(uc, f)
+    save_file({k: v.contiguous() for k, v in unet.state_dict().items()},
+              os.path.join(out_dir, "unet", "diffusion_pytorch_model.safetensors"))
+    sd = TemporalVaeDecoder(vc).state_dict()
+    sd.update(VaeEncoder(vc).state_dict())
+    sd = {k: v for k, v in sd.items() if not k.startswith("post_quant_conv.")}
+    with open(os.path.join(out_dir, "vae", "config.json"), "w") as f:
+        json.dump(vc, f)
+    save_file({k: v.contiguous() for k, v in sd.items()}, os.path.join(out_dir, "vae", "diffusion_pytorch_model.safetensors"))
+    ic = tf.CLIPVisionConfig(hidden_size=32, num_hidden_layers=2, num_attention_heads=2, intermediate_size=64,
+                             image_size=32, patch_size=16, projection_dim=32)
+    tf.CLIPVisionModelWithProjection(ic).save_pretrained(os.path.join(out_dir, "image_encoder"), safe_serialization=True)
+    with open(os.path.join(out_dir, "feature_extractor", "preprocessor_config.json"), "w") as f:
+        json.dump({"image_processor_type": "CLIPImageProcessor", "crop_size": 32, "size": {"shortest_edge": 32},
+                   "image_mean": [0.48145466, 0.4578275, 0.40821073],
+                   "image_std": [0.26862954, 0.26130258, 0.27577711]}, f)
+    with open(os.path.join(out_dir, "scheduler", "scheduler_config.json"), "w") as f:
+        json.dump({"_class_name": "EulerDiscreteScheduler", "sigma_min": 0.002, "sigma_max": 700.0,
+                   "use_karras_sigmas": True, "prediction_type": "v_prediction", "timestep_type": "continuous",
+                   "timestep_spacing": "leading", "num_train_timesteps": 1000}, f)
+    with open(os.path.join(out_dir, "model_index.json"), "w") as f:
+        json.dump({"_class_name": "StableVideoDiffusionPipeline", "unet": ["diffusers", "UNetSpatioTemporalConditionModel"],
+                   "vae": ["diffusers", "AutoencoderKLTemporalDecoder"],
+                   "image_encoder": ["transformers", "CLIPVisionModelWithProjection"],
+                   "feature_extractor": ["transformers", "CLIPImageProcessor"],
+                   "scheduler": ["diffusers", "EulerDiscreteScheduler"]}, f)
+    return out_dir
+
+
 def write_sd_single_file(path: str, size: str = "tiny", seed: int = 0, fam: str = "", hints: bool = True) -> str:
     """A random-init Stable Diffusion checkpoint as ONE file in the original LDM / SGM layout
     (what `from_single_file` reads: the AIO DreamShaper_8_pruned.safetensors shape at
