@@ -174,6 +174,7 @@ class LLMEngine:
         self._grammars: Dict[str, object] = {}
         # allowed-token masks of grammar parse states, resident on the device (_grammar_mask_slot)
         self._gmask_cache: "collections.OrderedDict" = collections.OrderedDict()
+        self._gslot_key: Dict[int, tuple] = {}   # device mask slot -> its (grammar, state key) cache entry
         self._gmask_pool: Optional[torch.Tensor] = None
         self._gmask_free: List[int] = []
         self._gmask_over: Dict[tuple, int] = {}   # states whose budgeted walk gave up once
@@ -1136,6 +1137,7 @@ class LLMEngine:
         epoch = self._gepoch
         self.metrics["grammar_runs"] += 1
         self.metrics["grammar_run_rows"] += len(grows)
+        gdev, gtrans, cache, skey = self._gdev, self._gtrans, self._gmask_cache, self._gslot_key
         for j in grows:
             r, s = reqs[j], int(gslot[j])
             kept = []
@@ -1146,16 +1148,22 @@ class LLMEngine:
                 if r.done:
                     break
                 kept.append(t)
-                s2 = self._grammar_mask_slot(r, V, self.device)
-                hit = (s, t) in self._gdev
+                hit = (s, t) in gdev
                 self._grammar_hit(r, hit)
                 if not hit:
-                    if (s, t) not in self._gtrans and epoch == self._gepoch:
-                        self._gtrans_learn(s, t, s2)   # (not after a slot reuse: s may name another state)
-                    break               # the device parked this row after token t
-                if self._gtrans[(s, t)] != s2:
+                    # the device parked this row after token t: learn the transition from the real
+                    # state (not after a slot reuse: s may name another state)
+                    s2 = self._grammar_mask_slot(r, V, self.device)
+                    if (s, t) not in gtrans and epoch == self._gepoch:
+                        self._gtrans_learn(s, t, s2)
                     break
-                s = s2
+                # a learned transition within this epoch names the state's slot exactly (the table
+                # was written from the real successor), so the host follows it without hashing the
+                # parse state per token; the slot's mask stays recently used
+                s = gtrans[(s, t)]
+                k = skey.get(s)
+                if k is not None and k in cache:
+                    cache.move_to_end(k)
             if kept and not r.done:
                 # the device already wrote the KV of every kept token but the last (fed by the
                 # next step): hand them over as a run, like the plain rows' _emit_run -- appending
@@ -1533,6 +1541,7 @@ class LLMEngine:
             self._gnext = torch.full((self.GRAMMAR_MASK_SLOTS, V), -2, dtype=torch.int16, device=dev)
             self._gmask_free = list(range(self.GRAMMAR_MASK_SLOTS))
             self._gmask_cache.clear()
+            self._gslot_key.clear()
             self._gtrans.clear()
             self._gtrans_in.clear()
             self._gpend.clear()
@@ -1720,6 +1729,8 @@ class LLMEngine:
             pool[slot, :n].copy_(torch.from_numpy(m[:n].astype(bool)))
             self._gmask_np[slot] = m   # host copy: transitions out of the state can be expanded
         c[key] = slot
+        if slot is not None and slot >= 0:
+            self._gslot_key[slot] = key
         while len(c) > 4 * self.GRAMMAR_MASK_SLOTS:
             _, v = c.popitem(last=False)
             if v is not None and v >= 0:

@@ -400,6 +400,9 @@ def pick_splits(N: int, K: int, M: int) -> int:
     return best
 
 
+GEMV_MAX_SPLITS = int(os.environ.get("LOCALAI_AMD_GEMV_MAX_SPLITS", "0"))   # 0: no cap (A/B knob)
+
+
 def _gemv_splits(ws, K: int, M: int) -> int:
     """Split-K for the dp4 GEMV: ~2 workgroups per CU (pick_splits), then grown until the
     workgroup's int8 activation image (kper bytes + 16-run sums + scales per row) fits 64 KiB."""
@@ -413,6 +416,8 @@ def _gemv_splits(ws, K: int, M: int) -> int:
         # 70B-class down projections (K = 28672): 7 splits measured 9 % faster than 4 for Q6_K and
         # 4 % for Q4_K (profiles/r3_session2_measurements.md, scripts/gemv_sweep.py --preset 70b)
         S = max(S, 7)
+    if GEMV_MAX_SPLITS:
+        S = min(S, GEMV_MAX_SPLITS)
     while nsb % S:
         S -= 1
     mt = 1 if M == 1 else (2 if M == 2 else 4)
