@@ -1920,7 +1920,9 @@ MOE32 = os.environ.get("LOCALAI_AMD_MOE32", "1") == "1"
 # T = 64: 32-row tiles, 4 workgroups per CU (var 9) 156 + 86 us vs the 16-column kernel's
 # 285 + 9 (act) + 143; T = 128 / 256: 64-row tiles in 8-wave workgroups (var 4) 180 + 91 /
 # 291 + 162 us vs 276 + 15 + 145 / 470 + 16 + 255.
-MOE32_MIN_T = int(os.environ.get("LOCALAI_AMD_MOE32_MIN_T", "33"))
+# T = 16 / 24 / 32: var 9 232 / 234 / 237 us vs 266 / 315 / 317; T = 8: 221 vs 212
+# (gpurun_out/r5_moe_small.log)
+MOE32_MIN_T = int(os.environ.get("LOCALAI_AMD_MOE32_MIN_T", "12"))
 MOE32_SMALL_T = 96     # below: var 9 (32-row tiles); from here: var 4
 MOE32_VAR_GLU = int(os.environ.get("LOCALAI_AMD_MOE32_VAR_GLU", "-1"))     # -1: by batch
 MOE32_VAR_DOWN = int(os.environ.get("LOCALAI_AMD_MOE32_VAR_DOWN", "-1"))
