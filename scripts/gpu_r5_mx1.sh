@@ -1,0 +1,12 @@
+#!/bin/bash
+# Mixtral-8x7B C=1 / C=256 engine after the router change (+ router / MoE numerics tests)
+set -o pipefail
+mkdir -p gpurun_out
+export LOCALAI_AMD_CACHE=/tmp/la_cache
+( while sleep 50; do date >> gpurun_out/r5_heartbeat.log; done ) &
+HB=$!
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "moe" > gpurun_out/r5_mx1_tests.log 2>&1 || { kill $HB; exit 1; }
+timeout -k 10 600 python -u bench.py --mode engine --preset mixtral-8x7b --steps 2 --warmup 1 --concurrency 1 --max-tokens 128 > gpurun_out/r5_mx1_c1.log 2>&1
+rc=$?
+kill $HB
+exit $rc
