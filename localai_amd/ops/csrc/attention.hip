@@ -618,6 +618,15 @@ __global__ __launch_bounds__(PF_T) void attn_prefill_kernel(
 }  // namespace la
 
 // C ABI ------------------------------------------------------------------------------------
+static int g_dec_one_part = la::DEC_ONE_PART;  // tuning hook (la_dec_one_part)
+
+// Sequences of up to n keys run as one partition per kv head (no split-KV merge); n % 128 == 0.
+extern "C" int la_dec_one_part(int n) {
+  if (n < 0 || n > 2048 * 16 || n % 128) return -1;
+  g_dec_one_part = n;
+  return 0;
+}
+
 extern "C" int la_attn_decode(const void* q, const void* kc, const void* vc, const int* block_tables, int max_blocks,
                               const int* seq_lens, int B, int Hq, int Hkv, int Dh, int BS, float scale, int P, int PS,
                               void* out, void* part_o, void* part_ml, void* tickets, const void* rope_p,
@@ -625,7 +634,7 @@ extern "C" int la_attn_decode(const void* q, const void* kc, const void* vc, con
                               const float* cos_sin, float softcap, int window, int nw, void* stream) {
   // nw bit 8: split even short sequences over the grid's partitions (few sequences: the
   // parallelism is worth the merge); otherwise a sequence of <= DEC_ONE_PART keys is one partition
-  const int one_part = (nw & 256) ? 0 : la::DEC_ONE_PART;
+  const int one_part = (nw & 256) ? 0 : g_dec_one_part;
   nw &= 255;
   if (Hq % Hkv || Hq / Hkv > 16 || (BS % 16) || (128 % BS && BS % 128) || (PS % 32) || (PS % BS) || P < 1 ||
       (nw != 1 && nw != 4) ||
