@@ -1180,6 +1180,8 @@ def glu_linear(x: torch.Tensor, ws: Sequence[QWeight], F: int, mode: int,
         best, best_t = None, t_ref
         cands = [6, 7, 8] if M > 128 else [7, 12, 14]
         if q32_ok([pair[0]], 9) and pair[0].fmt == pair[2].fmt:
+            # (128-row tiles at M > 128 -- 107 / 105, two row tiles to fill the chip -- were timed
+            # and never won: r5_glu_bench.log)
             cands += [109, 108, 104] if M > 128 else [109, 108, 107]
         for t in cands:
             tt = _time_cold(lambda t=t: _run_glu(x, pair, F, mode, t, out))
