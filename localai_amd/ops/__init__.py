@@ -1961,8 +1961,12 @@ def moe_glu32(x: torch.Tensor, mw: "MoEWeights", order: torch.Tensor, off: torch
     return h
 
 
-def _moe32_var(env: int, T: int) -> int:
-    return env if env >= 0 else (9 if T < MOE32_SMALL_T else 4)
+def _moe32_var(env: int, T: int, fmt: int = FMT_Q4_K, down: bool = False) -> int:
+    if env >= 0:
+        return env
+    # (Q6_K down on var 8 timed 255 vs 281 us in isolation at T = 256 -- r5_moe_q6.log -- but the
+    # engine did not move: Mixtral C=256 8140 vs 8198 tok/s, r5_mx256_*.log)
+    return 9 if T < MOE32_SMALL_T else 4
 
 
 def _moe32_splits(mw: "MoEWeights", T: int, topk: int, var: int) -> int:
@@ -1985,7 +1989,7 @@ def moe_down32(h: torch.Tensor, mw: "MoEWeights", order: torch.Tensor, off: torc
     """Down projection of moe_glu32's grouped h rows -> Partial [S*topk, T, N]: slab
     (split*topk + slot) row t holds wts[pair] * (h_pair Wd^T) of token t's slot-th pick, so the
     consumer's slab sum is the weighted top-k combine (moe_linear's down contract)."""
-    v = _moe32_var(MOE32_VAR_DOWN, T) if var is None else var
+    v = _moe32_var(MOE32_VAR_DOWN, T, mw.fmt, down=True) if var is None else var
     S = _moe32_splits(mw, T, topk, v)
     alloc = torch.zeros if zero else torch.empty
     out = alloc(S * topk, T, mw.N, dtype=torch.float32, device=h.device)
