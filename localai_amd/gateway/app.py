@@ -192,7 +192,8 @@ def create_app(state: AppState) -> FastAPI:
         app.add_middleware(CORSMiddleware, allow_origins=origins, allow_methods=["*"], allow_headers=["*"])
 
     from . import openai_routes, localai_routes, files_routes, gallery_routes, p2p, webui
-    app.include_router(openai_routes.build_router(state))
+    oai = openai_routes.build_router(state)
+    app.include_router(oai)
     app.include_router(files_routes.build_router(state))
     app.include_router(localai_routes.build_router(state))
     app.include_router(webui.build_router(state))
@@ -201,7 +202,44 @@ def create_app(state: AppState) -> FastAPI:
         app.include_router(gallery_routes.build_router(state))
     app.state.localai = state
     app.state.p2p = p2p_node
+    # the streaming chat / completion routes on the native server skip Starlette's middleware
+    # stack, router and FastAPI's endpoint wrapper (~0.25 of ~0.85 ms of gateway CPU per
+    # request, scripts/gateway_profile.py): the same auth and metrics middleware and the same
+    # exception handlers, composed around the endpoint.  Not with CSRF / CORS (stateful or
+    # response-rewriting middleware stays on the one regular stack).
+    if not (cfg.csrf or cfg.cors):
+        fast = {}
+        for path, ep in oai.native_fast.items():
+            h = _FastEndpoint(ep, _api_err, _err)
+            if not cfg.disable_metrics:
+                h = MetricsMiddleware(h, state=state)
+            fast[path] = AuthMiddleware(h, state=state)
+        app.state.native_fast = fast
     return app
+
+
+class _FastEndpoint:
+    """ASGI app for an endpoint taking only the Request (see create_app: native_fast)."""
+
+    def __init__(self, endpoint, api_err, err):
+        self.endpoint, self.api_err, self.err = endpoint, api_err, err
+
+    async def __call__(self, scope, receive, send):
+        from starlette.exceptions import HTTPException
+        request = Request(scope, receive)
+        try:
+            resp = await self.endpoint(request)
+        except APIError as e:
+            resp = await self.api_err(request, e)
+        except HTTPException as e:
+            from fastapi.exception_handlers import http_exception_handler
+            resp = await http_exception_handler(request, e)
+        except Exception as e:  # noqa: BLE001 - same catch-all as the app's handler
+            resp = await self.err(request, e)
+        if not isinstance(resp, Response):
+            from fastapi.encoders import jsonable_encoder
+            resp = JSONResponse(jsonable_encoder(resp))
+        await resp(scope, receive, send)
 
 
 LLAMA3_CHAT_MESSAGE = ("<|start_header_id|>{{ .RoleName }}<|end_header_id|>\n\n{{.Content }}<|eot_id|>")

@@ -41,6 +41,8 @@ class NativeHTTPServer:
     def __init__(self, app, host: str = "0.0.0.0", port: int = 8080):
         from ..native import http
         self.app = app
+        # exact-path POST routes the app serves without its router (gateway/app.py native_fast)
+        self.fast = dict(getattr(getattr(app, "state", None), "native_fast", None) or {})
         self.srv = http().Server(host, int(port))
         self.host = host
         self.port = self.srv.port
@@ -151,8 +153,11 @@ class NativeHTTPServer:
                     st["done"] = True
                     srv.stream_end(conn, data)
 
+        fast = self.fast.get(scope["path"]) if method == "POST" and self.fast else None
+        if fast is not None:
+            scope["app"] = self.app
         try:
-            await self.app(scope, receive, send)
+            await (fast or self.app)(scope, receive, send)
         except Exception:
             log.exception("unhandled error serving %s %s", method, path)
             if not st["streaming"] and not st["done"]:

@@ -317,6 +317,9 @@ def build_router(state) -> APIRouter:
 
     for p in ("/v1/chat/completions", "/chat/completions"):
         r.add_api_route(p, chat, methods=["POST"], openapi_extra=_DOC)
+    # endpoints that read only the Request: the native server may call them without Starlette's
+    # router (app.create_app composes the same middleware and error handlers around them)
+    r.native_fast = {p: chat for p in ("/v1/chat/completions", "/chat/completions")}
 
     # ------------------------------------------------------------------------ completion
     async def completion(request: Request, model_path: str = ""):
@@ -384,6 +387,7 @@ def build_router(state) -> APIRouter:
 
     for p in ("/v1/completions", "/completions"):
         r.add_api_route(p, completion, methods=["POST"], openapi_extra=_DOC)
+    r.native_fast.update({p: completion for p in ("/v1/completions", "/completions")})
     r.add_api_route("/v1/engines/{model}/completions", completion_engine, methods=["POST"])
 
     # ------------------------------------------------------------------------ edits

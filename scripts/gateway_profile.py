@@ -87,11 +87,18 @@ def main():
     msgs = [f"(wave 0) Request {i}: " + " ".join(words[(i + j) % len(words)] for j in range(100))
             for i in range(a.requests)]
     lg.wave(url, name, msgs[:16], 1, extra={"temperature": 0, "ignore_eos": True, "mirostat": 0})
+    import psutil
+
+    def srv_cpu():  # CPU seconds of the server thread (the gateway's event loop)
+        return sum(t.user_time + t.system_time for t in psutil.Process().threads() if t.id == th.native_id)
+    c0 = srv_cpu()
     t0 = time.perf_counter()
     ttft, _ = lg.wave(url, name, msgs, 1, extra={"temperature": 0, "ignore_eos": True, "mirostat": 0})
     el = time.perf_counter() - t0
+    cpu = srv_cpu() - c0
     print(f"{a.requests} requests in {el * 1e3:.1f} ms: {a.requests / el:.0f} req/s, "
-          f"{el / a.requests * 1e3:.3f} ms per request; p50 ttft {sorted(ttft)[len(ttft) // 2] * 1e3:.1f} ms")
+          f"{el / a.requests * 1e3:.3f} ms per request; p50 ttft {sorted(ttft)[len(ttft) // 2] * 1e3:.1f} ms; "
+          f"gateway thread CPU {cpu / a.requests * 1e3:.3f} ms per request")
     lg.close()
     srv.shutdown()
     th.join(10)

@@ -234,6 +234,59 @@ def test_api_key_auth(engine, tmp_path_factory):
         assert c.get("/v1/models", headers={"Authorization": "Bearer nope"}).status_code == 403
 
 
+def test_native_fast_routes_keep_auth_errors_and_metrics(engine, tmp_path_factory):
+    """The native server serves chat / completions POSTs without Starlette's router
+    (app.state.native_fast): the same API-key check, typed-body 400s, metrics and streaming."""
+    import urllib.error
+    from localai_amd.gateway.app import create_app_for_engine
+    from localai_amd.gateway.native_server import NativeHTTPServer
+    engine.start()  # an earlier TestClient's lifespan shutdown may have stopped the shared engine
+    app, name = create_app_for_engine(engine, name="tiny",
+                                      app_config=_app_config(tmp_path_factory, api_keys=["sekrit"]))
+    srv = NativeHTTPServer(app, "127.0.0.1", 0)
+    assert set(srv.fast) == {"/v1/chat/completions", "/chat/completions", "/v1/completions", "/completions"}
+    seen = []
+    inner = srv.fast["/v1/chat/completions"]
+
+    async def spy(scope, receive, send):
+        seen.append(scope["path"])
+        await inner(scope, receive, send)
+    srv.fast["/v1/chat/completions"] = spy
+    th = threading.Thread(target=srv.run, daemon=True)
+    th.start()
+    t0 = time.time()
+    while not srv.started and time.time() - t0 < 30:
+        time.sleep(0.02)
+    base = f"http://127.0.0.1:{srv.port}"
+    key = {"authorization": "Bearer sekrit"}
+    msgs = [{"role": "user", "content": "hi"}]
+    try:
+        with pytest.raises(urllib.error.HTTPError) as e:
+            _post(base + "/v1/chat/completions", {"model": name, "messages": msgs})
+        assert e.value.code == 403
+        with pytest.raises(urllib.error.HTTPError) as e:
+            _post(base + "/v1/chat/completions", {"model": name, "messages": msgs, "temperature": "hot"}, key)
+        assert e.value.code == 400 and "temperature" in json.loads(e.value.read())["error"]["message"]
+        st, raw = _post(base + "/v1/chat/completions", {"model": name, "messages": msgs, "max_tokens": 3,
+                                                        "ignore_eos": True, "stream": True}, key)
+        evs = _sse(raw)
+        assert st == 200 and evs[-1] == "[DONE]" and evs[-2]["usage"]["completion_tokens"] == 3
+        st, raw = _post(base + "/v1/chat/completions", {"model": name, "messages": msgs, "max_tokens": 2,
+                                                        "ignore_eos": True}, key)
+        assert json.loads(raw)["usage"]["completion_tokens"] == 2
+        assert len(seen) == 4
+        req = urllib.request.Request(base + "/metrics", headers=key)
+        with urllib.request.urlopen(req, timeout=30) as r:
+            txt = r.read().decode()
+        assert 'path="/v1/chat/completions"' in txt
+    finally:
+        srv.shutdown()
+        th.join(10)
+    # stateful / response-rewriting middleware keeps the regular stack
+    app2, _ = create_app_for_engine(engine, name="tiny", app_config=_app_config(tmp_path_factory, csrf=True))
+    assert not getattr(app2.state, "native_fast", None)
+
+
 def test_files_and_assistants(client, tmp_path):
     r = client.post("/v1/files", files={"file": ("a.txt", b"hello")}, data={"purpose": "fine-tune"})
     assert r.status_code == 200, r.text
