@@ -230,11 +230,24 @@ def main():
     else:
         runner = EngineRunner(eng, args)
 
+    arrivals = os.environ.get("BENCH_ARRIVALS") == "1"
+
     def wave(w):
         # the wave tag leads the message: no prompt shares more than the chat-template header with a
         # prompt of an earlier wave, so every wave prefills its 256 prompts in full (a trailing tag
         # would let the engine's prefix cache skip ~90 % of the prefill of every repeated wave)
-        return runner.wave([f"(wave {w}) " + m for m in msgs])
+        if arrivals:
+            eng.arrival_log, eng.admit_log = [], []
+            tw = time.perf_counter()
+        r = runner.wave([f"(wave {w}) " + m for m in msgs])
+        if arrivals:  # server-side view of the burst (diagnostics on stderr, outside the JSON line)
+            a_ = eng.arrival_log
+            ad = eng.admit_log[0] if eng.admit_log else (float("nan"), 0)
+            print(f"bench: wave {w} arrivals {len(a_)}: first +{(a_[0] - tw) * 1e3:.1f} ms, spread "
+                  f"{(a_[-1] - a_[0]) * 1e3:.1f} ms (p50 +{(a_[len(a_) // 2] - a_[0]) * 1e3:.1f}); admission closed "
+                  f"+{(ad[0] - a_[0]) * 1e3:.1f} ms with {ad[1]} waiting; p50 ttft "
+                  f"{percentile(r[0], 50) * 1e3:.1f} ms", file=sys.stderr, flush=True)
+        return r
 
     def lbarrier():
         if leaders is not None:

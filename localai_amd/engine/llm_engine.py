@@ -82,6 +82,9 @@ class EngineConfig:
     # gateway thread is still parsing the rest (it holds the GIL meanwhile); 0 disables
     admission_window_ms: float = 30.0
     admission_quiet_ms: float = 2.0
+    # ... and closes early once the waiting prompts fill one prefill chunk (the first chunk is
+    # full, later arrivals join the next while it runs); -1 = max_batched_tokens, 0 = never
+    admission_close_tokens: int = -1
     draft_model: str = ""             # speculative decoding: draft LM GGUF (engine/speculative.DraftModel)
     quantization: str = ""            # HF checkpoints: load-time quantisation (bnb_4bit / bnb_8bit / ...)
     draft_max_seqs: int = 16          # draft-model KV cache capacity in sequences of context_size
@@ -224,6 +227,10 @@ class LLMEngine:
         self._next_id = 1
         self._id_lock = threading.Lock()
         self._wake = threading.Event()
+        # diagnostics (bench.py BENCH_ARRIVALS=1): perf_counter of every add_request and, per idle ->
+        # busy transition, (time the admission window closed, requests waiting then)
+        self.arrival_log: Optional[list] = None
+        self.admit_log: Optional[list] = None
         self._thread: Optional[threading.Thread] = None
         self._stop = False
         self.healthy = True          # False after a fatal device error: the model manager respawns
@@ -379,6 +386,8 @@ class LLMEngine:
         `sink.push(text, n_generated)` (no Python Event per token) and only the final event
         reaches `callback`."""
         rid = req_id if req_id is not None else self.new_id()
+        if self.arrival_log is not None:
+            self.arrival_log.append(time.perf_counter())
         if not self.healthy:  # dead device: refuse instead of queueing work nobody will run
             callback(Event(finished=True, finish_reason="error", error=f"backend unhealthy: {self.fatal_error}"))
             return rid
@@ -521,13 +530,22 @@ class LLMEngine:
         """Idle -> busy: let a burst of arrivals land before scheduling (see EngineConfig)."""
         t_end = time.perf_counter() + self.cfg.admission_window_ms / 1e3
         quiet = self.cfg.admission_quiet_ms / 1e3
+        close = int(os.environ.get("LOCALAI_AMD_ADMIT_TOKENS", self.cfg.admission_close_tokens))
+        if close < 0:
+            close = self.cfg.max_batched_tokens
         n = self._inbox.qsize()
         while time.perf_counter() < t_end:
             time.sleep(quiet)
             m = self._inbox.qsize()
-            if m == n:
-                return
+            if m == n or (close and self._inbox_tokens() >= close):
+                break
             n = m
+        if self.admit_log is not None:
+            self.admit_log.append((time.perf_counter(), n))
+
+    def _inbox_tokens(self) -> int:
+        with self._inbox.mutex:
+            return sum(len(r.prompt) for r in self._inbox.queue if isinstance(r, Request))
 
     @staticmethod
     def _is_fatal(e: Exception) -> bool:

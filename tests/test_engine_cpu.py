@@ -435,3 +435,37 @@ def test_penalty_ring_push_cpu():
         ops.penalty_push(torch.tensor([t, t], dtype=torch.int32), hist, cnt, hl, cap)
     assert hist[0].tolist() == [5, 6, -1, -1] and hl.tolist() == [2, 3]
     assert sorted(hist[1, :3].tolist()) == [5, 6, 9]   # the two oldest (7, 8) dropped out of the window
+
+
+def test_admission_window_closes_once_a_prefill_chunk_waits(tiny_model_path, monkeypatch):
+    """Burst admission: an idle engine waits for arrivals to pause (or the window to end), but
+    stops waiting as soon as the queued prompts fill one prefill chunk (admission_close_tokens,
+    default max_batched_tokens); 0 restores the plain window."""
+    import time
+    monkeypatch.delenv("LOCALAI_AMD_ADMIT_TOKENS", raising=False)
+    e = _engine(tiny_model_path, seqs=16, max_batched_tokens=64, admission_window_ms=400.0,
+                admission_quiet_ms=50.0)
+    e.admit_log = []
+    sp = SamplingParams(max_tokens=1, temperature=0.0)
+    stop = threading.Event()
+
+    def trickle():  # one arrival every 10 ms: the quiet gap never comes
+        while not stop.is_set():
+            e.add_request("hello there general kenobi " * 2, sp, lambda ev: None)
+            time.sleep(0.01)
+    th = threading.Thread(target=trickle)
+    th.start()
+    try:
+        time.sleep(0.02)
+        t0 = time.perf_counter()
+        e._admit_burst()
+        early = time.perf_counter() - t0
+        assert e._inbox_tokens() >= 64 and early < 0.3
+        e.cfg.admission_close_tokens = 0
+        t0 = time.perf_counter()
+        e._admit_burst()
+        assert time.perf_counter() - t0 >= 0.35  # the full window
+    finally:
+        stop.set()
+        th.join()
+    assert len(e.admit_log) == 2
