@@ -1,7 +1,8 @@
 """Text-to-speech / sound-generation backend servicers (backend.proto LoadModel + TTS /
 SoundGeneration) over the native audio models.
 
-  piper / vits / mms-tts     VITS voices (models/tts.py)        -- backend/go/tts/piper.go:30-49
+  piper / vits / mms-tts     VITS voices (models/tts.py; piper .onnx voices: models/piper.py)
+                                                                 -- backend/go/tts/piper.go:30-49
   transformers-musicgen      MusicGen (models/musicgen.py)      -- backend/python/transformers-musicgen/backend.py:66,121
   bark                       Bark (models/bark.py)              -- backend/python/bark/backend.py:44
   parler-tts                 Parler-TTS (models/parler.py)      -- backend/python/parler-tts/backend.py:71-90
@@ -75,9 +76,9 @@ class VitsServicer(_AudioBase):
 
     def _load(self, path):
         from ..models.tts import VitsVoice, is_vits_dir
-        if path.endswith(".onnx"):
-            raise ValueError("ONNX piper voices are not loadable here (no ONNX runtime): use the voice's VITS "
-                             "checkpoint in the Hugging Face layout (config.json + vocab.json + model.safetensors)")
+        if path.endswith(".onnx"):  # a piper voice: <voice>.onnx + <voice>.onnx.json (models/piper.py)
+            from ..models.piper import PiperVoice
+            return PiperVoice(path, self._dev())
         if not is_vits_dir(path):
             raise ValueError("not a VITS checkpoint directory (config.json model_type 'vits')")
         return VitsVoice(path, self._dev())
@@ -88,6 +89,8 @@ class VitsServicer(_AudioBase):
         if v is None:
             raise RuntimeError("no model loaded")
         sid = int(request.voice) if request.voice.strip().isdigit() else None
+        if hasattr(v, "speaker"):  # piper: speaker names from the voice's speaker_id_map
+            sid = v.speaker(request.voice)
         with self._lock:
             audio = v.synthesize(request.text, speaker_id=sid)
         write_wav(request.dst, audio, v.sampling_rate)

@@ -1247,3 +1247,60 @@ def write_sd3_pipeline(out_dir: str, seed: int = 0, t5: bool = True) -> str:
     with open(os.path.join(out_dir, "model_index.json"), "w") as f:
         json.dump({"_class_name": "StableDiffusion3Pipeline"}, f)
     return out_dir
+
+
+PIPER_SYMBOLS = "_^$ abcdefghijklmnopqrstuvwxyz',.?!"
+
+
+def write_piper_voice(path: str, seed: int = 0, sampling_rate: int = 8000):
+    """A piper-layout voice (`<name>.onnx` + `<name>.onnx.json`, phoneme_type "text") exported
+    from a random-init transformers VitsModel with the noise scales at 0 (deterministic), through
+    torch's TorchScript ONNX exporter.  Returns the VitsModel (the test oracle).  The exporter's
+    last pass (attaching onnxscript functions) imports the onnx package, which is not installed;
+    a graph without such functions leaves that pass a no-op, so it is skipped when onnx is absent."""
+    import io
+
+    import torch
+    from transformers import VitsConfig, VitsModel
+    try:
+        import onnx  # noqa: F401
+    except ImportError:
+        import torch.onnx._internal.torchscript_exporter.onnx_proto_utils as opu
+        opu._add_onnxscript_fn = lambda model_bytes, custom_opsets: model_bytes
+    cfg = VitsConfig(vocab_size=len(PIPER_SYMBOLS), hidden_size=16, num_hidden_layers=2, num_attention_heads=2,
+                     window_size=2, ffn_dim=24, flow_size=8, upsample_initial_channel=16, upsample_rates=[4, 2],
+                     upsample_kernel_sizes=[8, 4], resblock_kernel_sizes=[3, 5],
+                     resblock_dilation_sizes=[[1, 3], [1, 3]], duration_predictor_filter_channels=12,
+                     prior_encoder_num_wavenet_layers=2, sampling_rate=sampling_rate)
+    torch.manual_seed(seed)
+    m = VitsModel(cfg).eval()
+    m.noise_scale = 0.0
+    m.noise_scale_duration = 0.0
+
+    class PiperSig(torch.nn.Module):  # piper's graph signature: input, input_lengths, scales
+        def __init__(self, m):
+            super().__init__()
+            self.m = m
+
+        def forward(self, input, input_lengths, scales):
+            w = self.m(input_ids=input).waveform
+            keep = (scales[0] * 0 + 1) * (input_lengths[0] * 0 + 1).to(w.dtype)
+            return (w * keep).unsqueeze(1)
+
+    ids = torch.tensor([[1, 0, 10, 0, 2]])
+    buf = io.BytesIO()
+    with torch.no_grad():
+        torch.onnx.export(PiperSig(m).eval(), (ids, torch.tensor([5]), torch.tensor([0.667, 1.0, 0.8])), buf,
+                          dynamo=False, opset_version=15, input_names=["input", "input_lengths", "scales"],
+                          output_names=["output"], dynamic_axes={"input": {1: "phonemes"}, "output": {2: "time"}})
+    m.eval()  # the exporter restores the wrapper's training flag recursively
+    os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+    with open(path, "wb") as f:
+        f.write(buf.getvalue())
+    conf = {"audio": {"sample_rate": sampling_rate, "quality": "x_low"}, "espeak": {"voice": "en-us"},
+            "inference": {"noise_scale": 0.667, "length_scale": 1, "noise_w": 0.8}, "phoneme_type": "text",
+            "phoneme_map": {}, "phoneme_id_map": {c: [i] for i, c in enumerate(PIPER_SYMBOLS)},
+            "num_symbols": len(PIPER_SYMBOLS), "num_speakers": 1, "speaker_id_map": {}, "piper_version": "1.0.0"}
+    with open(path + ".json", "w", encoding="utf-8") as f:
+        json.dump(conf, f, ensure_ascii=False)
+    return m
