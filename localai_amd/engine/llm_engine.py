@@ -85,6 +85,12 @@ class EngineConfig:
     # ... and closes early once the waiting prompts fill one prefill chunk (the first chunk is
     # full, later arrivals join the next while it runs); -1 = max_batched_tokens, 0 = never
     admission_close_tokens: int = -1
+    # burst prefill first: while prompts of a burst are still being prefilled and every sequence
+    # that could decode holds only its first token (younger than this many ms), steps are
+    # prefill-only, so the burst's chunks run back to back (TTFT) and its rows then decode as one
+    # batch; a running stream (rows past their first token) keeps prefill and decode mixed.
+    # 0 disables
+    prefill_first_ms: float = 400.0
     draft_model: str = ""             # speculative decoding: draft LM GGUF (engine/speculative.DraftModel)
     quantization: str = ""            # HF checkpoints: load-time quantisation (bnb_4bit / bnb_8bit / ...)
     draft_max_seqs: int = 16          # draft-model KV cache capacity in sequences of context_size
@@ -599,7 +605,7 @@ class LLMEngine:
         self.busy = True
         spec_k = self._spec_k()
         K = 1 + spec_k if spec_k else self._lookahead()
-        plan = self.sched.schedule(K)  # spec: reserves KV slots for the draft positions
+        plan = self.sched.schedule(K, self._defer_decode())  # spec: reserves KV slots for the draft positions
         did = False
         tr = self.tracer
         p_ids = plan["p_ids"]
@@ -885,6 +891,25 @@ class LLMEngine:
                 or len(p.logit_bias) + len(self.tokenizer.eog) > self.cfg.bias_capacity)
 
     k1_reasons: "collections.Counter"   # why a decode step ran one device step (diagnostics)
+
+    def _defer_decode(self) -> bool:
+        """EngineConfig.prefill_first_ms: True while a burst is being prefilled (the native
+        scheduler then plans prefill only, when any prefill work is left)."""
+        ms = float(os.environ.get("LOCALAI_AMD_PREFILL_FIRST_MS", self.cfg.prefill_first_ms))
+        if ms <= 0 or self.tp.world > 1:
+            return False
+        oldest = None
+        pending = self.sched.num_waiting > 0
+        for r in self.requests.values():
+            if r.n_gen == 0:
+                pending = True
+            elif r.n_gen > 1 or not r.first_token_t:
+                return False  # a decoding stream: keep it moving
+            elif oldest is None or r.first_token_t < oldest:
+                oldest = r.first_token_t
+        if not pending or oldest is None:
+            return False
+        return (time.perf_counter() - oldest) * 1e3 < ms
 
     def _lookahead(self) -> int:
         """Decode steps to run on the device before coming back to the host."""

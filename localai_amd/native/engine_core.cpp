@@ -293,8 +293,19 @@ class Scheduler {
 
   // lookahead > 1 reserves KV slots for that many decode steps (device-resident multi-step
   // decode: the host comes back only after `lookahead` tokens per sequence).
-  py::dict schedule(int lookahead = 1) {
+  // defer_decode: while prompts are waiting or mid-prefill, this step is prefill only (the
+  // decode-ready sequences keep their state and reserve nothing) -- the engine asks for it
+  // during a request burst, so the burst's prefill chunks run back to back.
+  py::dict schedule(int lookahead = 1, bool defer_decode = false) {
     if (lookahead < 1) lookahead = 1;
+    if (defer_decode) {
+      bool prefill_work = !waiting_.empty() && (int)running_.size() < max_seqs_;
+      for (int64_t id : running_) {
+        const SeqInfo& s = seqs_.at(id);
+        if (!(s.n_computed >= (int)s.toks.size() - 1 && s.n_computed >= s.n_prompt)) prefill_work = true;
+      }
+      defer_decode = prefill_work;
+    }
     std::vector<int64_t> preempted;
     // ---- 1. decode: every running sequence whose prompt is fully computed
     std::vector<int64_t> dec;
@@ -306,6 +317,7 @@ class Scheduler {
       const int64_t id = running_[i];
       SeqInfo& s = seqs_.at(id);
       if (s.n_computed >= (int)s.toks.size() - 1 && s.n_computed >= s.n_prompt) {
+        if (defer_decode) continue;
         // needs one new slot for token toks.back() at position toks.size()-1
         while (!bm_.ensure(id, (int)s.toks.size() + lookahead - 1)) {
           // preempt youngest running sequence (recompute later)
@@ -528,7 +540,7 @@ PYBIND11_MODULE(_la_core, m) {
       .def("add", &Scheduler::add)
       .def("finish", &Scheduler::finish)
       .def("append", &Scheduler::append)
-      .def("schedule", &Scheduler::schedule, py::arg("lookahead") = 1)
+      .def("schedule", &Scheduler::schedule, py::arg("lookahead") = 1, py::arg("defer_decode") = false)
       .def("append_run", &Scheduler::append_run)
       .def("has", &Scheduler::has)
       .def("n_gen", &Scheduler::n_gen)

@@ -469,3 +469,49 @@ def test_admission_window_closes_once_a_prefill_chunk_waits(tiny_model_path, mon
         stop.set()
         th.join()
     assert len(e.admit_log) == 2
+
+
+@pytest.mark.parametrize("first_ms", [400.0, 0.0])
+def test_burst_prefill_first_policy(tiny_model_path, monkeypatch, first_ms):
+    """EngineConfig.prefill_first_ms: while a burst's prompts are still being prefilled (several
+    chunks under a small token budget) and every decodable row holds only its first token, steps
+    are prefill-only; the rows then decode together.  0 restores mixed prefill + decode steps.
+    Greedy outputs are the same either way."""
+    monkeypatch.delenv("LOCALAI_AMD_PREFILL_FIRST_MS", raising=False)
+    e = _engine(tiny_model_path, seqs=8, max_batched_tokens=24, prefill_first_ms=first_ms, prefix_cache=False)
+    kinds = []
+    run_p, run_d = e._run_prefill, e._run_decode
+
+    def rp(plan):
+        kinds.append("p")
+        return run_p(plan)
+
+    def rd(plan, K):
+        kinds.append("d")
+        return run_d(plan, K)
+    e._run_prefill, e._run_decode = rp, rd
+    prompts = [f"prompt number {i} with a few more words in it" for i in range(6)]
+    sp = dict(max_tokens=4, temperature=0.0, ignore_eos=True)
+    outs, done = {}, threading.Event()
+
+    def mk(i):
+        buf = bytearray()
+
+        def cb(ev):
+            buf.extend(ev.text)
+            if ev.finished:
+                outs[i] = buf.decode("utf-8", "replace")
+                if len(outs) == len(prompts):
+                    done.set()
+        return cb
+    for i, p in enumerate(prompts):
+        e.add_request(p, SamplingParams(**sp), mk(i))
+    while not done.is_set():
+        e.step()
+    n_p = kinds.count("p")
+    assert n_p >= 3  # the burst needs several prefill chunks
+    last_p = len(kinds) - 1 - kinds[::-1].index("p")
+    decode_during_prefill = "d" in kinds[:last_p]
+    assert decode_during_prefill == (first_ms == 0.0)
+    ref = {i: e.generate(p, SamplingParams(**sp))["text"] for i, p in enumerate(prompts)}
+    assert sum(outs[i] == ref[i] for i in ref) >= len(ref) - 1  # bf16 batch-order ties may flip one token
