@@ -320,6 +320,8 @@ def main():
                        **({"n_draft": args.n_draft} if args.n_draft else {})},
             "setup_s": {"model_gen": round(t_gen, 1), "load": round(t_load, 1), "graph_capture": round(t_capture, 1)},
         }
+        if dev != "cpu":  # weights + resident copies + KV cache + workspaces of this rank
+            out["device_mem_gb"] = round(torch.cuda.max_memory_allocated(dev) / 2**30, 1)
         if stream_check is not None:
             out["stream_check"] = stream_check
         print(json.dumps(out), flush=True)

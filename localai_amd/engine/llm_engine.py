@@ -324,6 +324,11 @@ class LLMEngine:
     # for the KV cache after the cache the config asks for (Llama-3-8B: 15 GB of 288 GB).
     PREFILL_BF16 = os.environ.get("LOCALAI_AMD_PREFILL_BF16", "auto")
     PREFILL_BF16_FRAC = 0.5
+    # the experts of a sparse MoE too (their prefill runs per-expert library GEMMs over the routed
+    # rows, models/decoder._moe_dense_prefill).  Off by default: Mixtral-8x7B HTTP C=256 measured
+    # 9791 / 9841 / 10068 tok/s with the copies vs 9602 / 10022 without (p50 TTFT 984 / 900 / 990
+    # vs 1008 / 878 ms) -- within box noise, for 84 GB more device memory (r5_mxe_*.log)
+    PREFILL_BF16_EXPERTS = os.environ.get("LOCALAI_AMD_PREFILL_BF16_EXPERTS", "0") == "1"
 
     def _prefill_bf16_copies(self):
         if self.PREFILL_BF16 == "never" or not ops.TILE_GEMM or ops.PREFILL_GEMM != "blas":
@@ -331,8 +336,12 @@ class LLMEngine:
         m = self.model
         groups = []
         for L in m.layers:
-            for grp in (L.qkv, L.gate_up, [L.wo]) + (([L.down],) if L.down is not None else ()):
-                if all(w.tile_ok for w in grp) and any(w.bf16 is None for w in grp):
+            grps = [L.qkv, L.gate_up, [L.wo]] + ([[L.down]] if L.down is not None else [])
+            if L.experts and self.PREFILL_BF16_EXPERTS:
+                for gu, d in L.experts:
+                    grps += [list(gu), [d]]
+            for grp in grps:
+                if grp and all(w is not None and w.tile_ok for w in grp) and any(w.bf16 is None for w in grp):
                     groups.append(grp)
         need = sum(w.N * w.K * 2 for grp in groups for w in grp if w.bf16 is None and w.fmt != ops.FMT_BF16)
         if not need:
