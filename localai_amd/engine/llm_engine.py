@@ -82,15 +82,16 @@ class EngineConfig:
     # gateway thread is still parsing the rest (it holds the GIL meanwhile); 0 disables
     admission_window_ms: float = 30.0
     admission_quiet_ms: float = 2.0
-    # ... and closes early once the waiting prompts fill one prefill chunk (the first chunk is
-    # full, later arrivals join the next while it runs); -1 = max_batched_tokens, 0 = never
+    # ... and closes early once the waiting prompts fill half a prefill chunk (that chunk runs
+    # while the rest of the burst arrives; HTTP C=256 p50 TTFT 293 -> 275 ms vs closing at a full
+    # chunk, r5_k2_*.log); -1 = max_batched_tokens / 2, 0 = never
     admission_close_tokens: int = -1
     # burst prefill first: while prompts of a burst are still being prefilled and every sequence
     # that could decode holds only its first token (younger than this many ms), steps are
     # prefill-only, so the burst's chunks run back to back (TTFT) and its rows then decode as one
     # batch; a running stream (rows past their first token) keeps prefill and decode mixed.
-    # 0 disables
-    prefill_first_ms: float = 400.0
+    # 2 s covers a Mixtral-8x7B C=256 burst (r5_k2_mx_*.log); 0 disables
+    prefill_first_ms: float = 2000.0
     draft_model: str = ""             # speculative decoding: draft LM GGUF (engine/speculative.DraftModel)
     quantization: str = ""            # HF checkpoints: load-time quantisation (bnb_4bit / bnb_8bit / ...)
     draft_max_seqs: int = 16          # draft-model KV cache capacity in sequences of context_size
@@ -485,9 +486,10 @@ class LLMEngine:
         return res
 
     def start(self):
-        # the serving thread shares the GIL with the gateway's event loop: a shorter switch
-        # interval (default 5 ms) keeps its launch loop moving while a request burst is parsed
-        sw = float(os.environ.get("LOCALAI_AMD_GIL_SWITCH_MS", "1"))
+        # the serving thread shares the GIL with the gateway's event loop.  Round 4 shortened the
+        # switch interval to 1 ms; with burst admission + prefill-first the interpreter's default
+        # 5 ms measures better (HTTP C=256 26.11-26.18 k vs 26.03-26.06 k tok/s, r5_kn_*.log)
+        sw = float(os.environ.get("LOCALAI_AMD_GIL_SWITCH_MS", "5"))
         if sw > 0:
             import sys
             sys.setswitchinterval(min(sys.getswitchinterval(), sw / 1e3))
@@ -547,7 +549,7 @@ class LLMEngine:
         quiet = self.cfg.admission_quiet_ms / 1e3
         close = int(os.environ.get("LOCALAI_AMD_ADMIT_TOKENS", self.cfg.admission_close_tokens))
         if close < 0:
-            close = self.cfg.max_batched_tokens
+            close = max(1, self.cfg.max_batched_tokens // 2)
         n = self._inbox.qsize()
         while time.perf_counter() < t_end:
             time.sleep(quiet)

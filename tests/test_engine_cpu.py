@@ -439,8 +439,8 @@ def test_penalty_ring_push_cpu():
 
 def test_admission_window_closes_once_a_prefill_chunk_waits(tiny_model_path, monkeypatch):
     """Burst admission: an idle engine waits for arrivals to pause (or the window to end), but
-    stops waiting as soon as the queued prompts fill one prefill chunk (admission_close_tokens,
-    default max_batched_tokens); 0 restores the plain window."""
+    stops waiting as soon as the queued prompts fill half a prefill chunk (admission_close_tokens,
+    default max_batched_tokens / 2); 0 restores the plain window."""
     import time
     monkeypatch.delenv("LOCALAI_AMD_ADMIT_TOKENS", raising=False)
     e = _engine(tiny_model_path, seqs=16, max_batched_tokens=64, admission_window_ms=400.0,
@@ -460,7 +460,7 @@ def test_admission_window_closes_once_a_prefill_chunk_waits(tiny_model_path, mon
         t0 = time.perf_counter()
         e._admit_burst()
         early = time.perf_counter() - t0
-        assert e._inbox_tokens() >= 64 and early < 0.3
+        assert e._inbox_tokens() >= 32 and early < 0.3   # half of max_batched_tokens
         e.cfg.admission_close_tokens = 0
         t0 = time.perf_counter()
         e._admit_burst()
@@ -471,7 +471,7 @@ def test_admission_window_closes_once_a_prefill_chunk_waits(tiny_model_path, mon
     assert len(e.admit_log) == 2
 
 
-@pytest.mark.parametrize("first_ms", [400.0, 0.0])
+@pytest.mark.parametrize("first_ms", [60000.0, 0.0])   # (a CPU prefill under a loaded test run is slow)
 def test_burst_prefill_first_policy(tiny_model_path, monkeypatch, first_ms):
     """EngineConfig.prefill_first_ms: while a burst's prompts are still being prefilled (several
     chunks under a small token budget) and every decodable row holds only its first token, steps

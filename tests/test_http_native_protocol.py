@@ -109,8 +109,10 @@ def test_half_close_after_request_is_answered(echo):
     s = _connect(srv)
     s.sendall(b"GET /v1/models HTTP/1.1\r\nhost: a\r\n\r\n")
     s.shutdown(socket.SHUT_WR)
-    resp = _read_all(s)
-    assert resp.startswith(b"HTTP/1.1 200") and b"connection: close" in resp
+    resp = _read_all(s)   # returns at the server's close
+    # "connection: close" is announced when the FIN is seen before the response is built; when
+    # the request is answered first, the FIN then ends the idle connection -- both are correct
+    assert resp.startswith(b"HTTP/1.1 200") and resp.endswith(b"\r\n\r\n0")
     assert served and served[-1][1] == b"/v1/models"
 
 
