@@ -20,7 +20,7 @@ def _runtime(name: str) -> str:
     return p if r.returncode == 0 and os.path.isabs(p) and os.path.exists(p) else ""
 
 
-@pytest.mark.timeout(600)
+@pytest.mark.timeout(1200)  # includes the sanitized rebuild after a native source change
 def test_native_core_under_asan_ubsan():
     asan = _runtime("libasan.so")
     if not asan:
@@ -35,7 +35,7 @@ def test_native_core_under_asan_ubsan():
                ASAN_OPTIONS="detect_leaks=0:abort_on_error=1:halt_on_error=1",
                UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
     r = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider", "-m", "not gpu",
-                        *NATIVE_TESTS], cwd=ROOT, env=env, capture_output=True, text=True, timeout=540)
+                        *NATIVE_TESTS], cwd=ROOT, env=env, capture_output=True, text=True, timeout=900)
     out = r.stdout[-4000:] + r.stderr[-4000:]
     assert "AddressSanitizer" not in out and "runtime error" not in out, out
     assert r.returncode == 0, out
