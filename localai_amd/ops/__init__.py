@@ -2010,6 +2010,10 @@ def moe_gemv_ok(mw: MoEWeights, T: int) -> bool:
             and mw.fmt in (FMT_Q4_K, FMT_Q6_K, FMT_Q8_0) and all(w.gemv_ok for w in mw.experts[:1]))
 
 
+# split-K override of the MoE decode GEMVs (gate|up, down); 0: the dense GEMV's heuristic (A/B knob)
+MOE_GEMV_SPLITS = tuple(int(v) for v in os.environ.get("LOCALAI_AMD_MOE_GEMV_SPLITS", "0,0").split(","))
+
+
 def moe_gemv(x: Optional[torch.Tensor], mw: MoEWeights, ids: torch.Tensor, topk: int, T: int, E_local: int,
              act_src: Optional[Partial] = None, act_mode: int = ACT_SWIGLU,
              wts: Optional[torch.Tensor] = None) -> Partial:
@@ -2019,6 +2023,17 @@ def moe_gemv(x: Optional[torch.Tensor], mw: MoEWeights, ids: torch.Tensor, topk:
     another rank's expert, rows read as zero)."""
     P = T * topk
     S = _gemv_splits([mw.experts[0]], mw.K, 1)
+    # one token: its topk routed pairs already multiply the down launch's grid -- half the dense
+    # GEMV's splits (Mixtral C=1 8 -> 4: 295.4 -> 300.3 / 294.5 -> 298.5 tok/s; gate|up 2 -> 1
+    # neutral; at C=2 quartering both measured 1.3 % slower; r5_mxs*_*.log)
+    if T == 1 and act_src is not None:
+        nsb = mw.K // 256
+        S = max(1, S // 2)
+        while nsb % S or (mw.K // S) * (1 + 4 / 16 + 4 / 32) > 65536:
+            S += 1
+    ov = MOE_GEMV_SPLITS[0 if act_src is None else 1]
+    if ov > 0 and (mw.K // 256) % ov == 0 and (mw.K // ov) * (1 + 4 / 16 + 4 / 32) <= 65536:
+        S = ov
     dev = ids.device
     if act_src is None:
         out = torch.empty(S, P, mw.N, dtype=torch.float32, device=dev)
