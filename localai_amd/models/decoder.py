@@ -556,7 +556,7 @@ class DecoderModel:
         d = ops.act_linear(gu, F, mode, L.down)
         return self._row_parallel_out(d, L.down_bias)
 
-    def _moe(self, L: Layer, xn: torch.Tensor) -> ops.Partial:
+    def _moe(self, L: Layer, xn: torch.Tensor, routed=None) -> ops.Partial:
         """Mixtral sparse MoE: softmax router, top-k, renormalised weights (K16/K18), per-expert
         quantised GEMMs on the routed rows (K17), weighted scatter-add."""
         hp = self.hp
@@ -564,14 +564,14 @@ class DecoderModel:
         El, base = self.E_local, self.ep_base
         if (L.moe_gu is not None and xn.is_cuda and not FUSED_ROUTER_OFF and L.experts is not None
                 and T >= MOE_DENSE_MIN_T and not torch.cuda.is_current_stream_capturing()):
-            return self._moe_dense_prefill(L, xn)
+            return self._moe_dense_prefill(L, xn, routed)
         if L.moe_gu is not None and xn.is_cuda and not FUSED_ROUTER_OFF:
             # any batch: one fused router launch (softmax, top-k, renorm, EP remap) feeds the
             # grouped expert GEMMs (row-chunked past 64 rows per expert); no host round trip
             # anywhere, so decode steps at every batch size capture into graphs
             k = hp.n_expert_used
-            ids, wts = ops.moe_router(xn, L.router, k, hp.moe_renorm, hp.expert_weights_scale,
-                                      base if self.ep else 0, El if self.ep else 0)
+            ids, wts = routed if routed is not None else ops.moe_router(
+                xn, L.router, k, hp.moe_renorm, hp.expert_weights_scale, base if self.ep else 0, El if self.ep else 0)
             if ops.moe_gemv_ok(L.moe_gu, T) and ops.moe_gemv_ok(L.moe_down, T):
                 # 1-2 token decode: the routed experts as int8-dot GEMVs, SwiGLU fused into the
                 # down projection's prologue (no route / grouping launch, no activation launch)
@@ -637,7 +637,7 @@ class DecoderModel:
         self.tp.all_reduce(out)
         return ops.Partial(out.unsqueeze(0))
 
-    def _moe_dense_prefill(self, L: Layer, xn: torch.Tensor) -> ops.Partial:
+    def _moe_dense_prefill(self, L: Layer, xn: torch.Tensor, routed=None) -> ops.Partial:
         """Prefill-sized MoE: device routing (fused router + grouping), ONE host read of the
         per-expert row offsets, then per expert a dense gate|up GEMM over its gathered rows, the
         SwiGLU, the down GEMM, and a routing-weighted index_add back to the tokens (two
@@ -646,8 +646,8 @@ class DecoderModel:
         T = xn.shape[0]
         k = hp.n_expert_used
         El, base = self.E_local, self.ep_base
-        ids, wts = ops.moe_router(xn, L.router, k, hp.moe_renorm, hp.expert_weights_scale,
-                                  base if self.ep else 0, El if self.ep else 0)
+        ids, wts = routed if routed is not None else ops.moe_router(
+            xn, L.router, k, hp.moe_renorm, hp.expert_weights_scale, base if self.ep else 0, El if self.ep else 0)
         order, off = ops.moe_route(ids, El + 1 if self.ep else El)
         off_h = off.cpu().tolist()
         order_l = order.long()
@@ -701,8 +701,20 @@ class DecoderModel:
             return ops.add_norm(res, f, nw, nb, eps, nm)
         if L.post_attn_norm is not None:
             o = self._post_norm(o, L.post_attn_norm)
-        xn = self._add_norm(res, o, L.ffn_norm, L.ffn_norm_b, eps, nm)
-        f = self._mlp(L, xn)
+        fused = None
+        if (L.experts is not None and L.moe_gu is not None and res.is_cuda and not FUSED_ROUTER_OFF
+                and not isinstance(o, PendingAR)):
+            # sparse MoE: the router rides on the add_norm launch (ops.add_norm_router)
+            k = hp.n_expert_used
+            fused = ops.add_norm_router(res, o, L.ffn_norm, L.ffn_norm_b, eps, nm, L.router, k, hp.moe_renorm,
+                                        hp.expert_weights_scale, self.ep_base if self.ep else 0,
+                                        self.E_local if self.ep else 0)
+        if fused is not None:
+            xn = fused[0]
+            f = self._moe(L, xn, routed=fused[1:])
+        else:
+            xn = self._add_norm(res, o, L.ffn_norm, L.ffn_norm_b, eps, nm)
+            f = self._mlp(L, xn)
         if L.post_ffw_norm is not None:
             f = self._post_norm(f, L.post_ffw_norm)
         if (defer_to is not None and nxt is not None and nm == 0 and isinstance(f, ops.Partial)

@@ -60,6 +60,7 @@ def lib():
             "la_qgemv_dp4_rope_norm": [I, P, P, P, I, I, P, P, P, I, I, I, P, P, P, I, P, P, LNG, I, P, P, F,
                                        P, P],
             "la_add_norm": [P, P, LNG, I, P, I, P, P, P, I, I, F, I, P, P],
+            "la_add_norm_router": [P, P, LNG, I, P, I, P, P, P, I, I, F, I, P, I, I, I, F, I, I, P, P, P],
             "la_rope_kv": [P, LNG, I, P, P, P, P, I, I, I, I, I, I, P, P, P, I, P],
             "la_mamba_conv_step": [P, P, LNG, P, P, P, I, I, I, P],
             "la_groupnorm_nhwc": [P, P, P, P, P, I, I, I, I, I, I, F, I, P],
@@ -1236,6 +1237,35 @@ def add_norm(residual: torch.Tensor, add: Optional[Partial], weight: torch.Tenso
                              weight.data_ptr(), _ptr(bias), _ptr(out) if want_out else None, T, D,
                              float(eps), mode, _ptr(out_f32), _stream()), "la_add_norm")
     return out if want_out else None
+
+
+NORM_ROUTER = os.environ.get("LOCALAI_AMD_NORM_ROUTER", "1") == "1"
+
+
+def add_norm_router(residual: torch.Tensor, add: Optional["Partial"], weight: torch.Tensor,
+                    bias: Optional[torch.Tensor], eps: float, mode: int, router: torch.Tensor, topk: int,
+                    renorm: bool, scale: float = 1.0, ep_base: int = 0, ep_local: int = 0):
+    """add_norm + moe_router in one launch (elementwise.hip add_norm_router_kernel): returns
+    (xn bf16 [T, D], ids [T, topk] int32, wts [T*topk] fp32) -- the router reads the bf16-rounded
+    normed row, like moe_router on add_norm's output -- or None when the fused kernel does not
+    apply (CPU, E > 64, D > 8192); the caller then runs the two ops."""
+    T, D = residual.shape
+    E = router.shape[0]
+    if (not NORM_ROUTER or not residual.is_cuda or E > 64 or topk > min(16, E) or D % 4 or D > 8192
+            or router.dtype != torch.float32 or not router.is_contiguous() or router.shape[1] != D):
+        return None
+    if add is not None and (add.M != T or add.N != D):
+        raise ValueError(f"add_norm_router: add {tuple(add.t.shape)} vs residual {T}x{D}")
+    assert residual.dtype == torch.float32 and residual.is_contiguous()
+    out = torch.empty(T, D, dtype=torch.bfloat16, device=residual.device)
+    ids = torch.empty(T, topk, dtype=torch.int32, device=residual.device)
+    wts = torch.empty(T * topk, dtype=torch.float32, device=residual.device)
+    a = add.src_args() if add is not None else (None, 0, 0, None)
+    _check(lib().la_add_norm_router(residual.data_ptr(), a[0], a[1], a[2], a[3], int(add is not None),
+                                    weight.data_ptr(), _ptr(bias), out.data_ptr(), T, D, float(eps), mode,
+                                    router.data_ptr(), E, topk, int(renorm), float(scale), ep_base,
+                                    ep_local or E, ids.data_ptr(), wts.data_ptr(), _stream()), "la_add_norm_router")
+    return out, ids, wts
 
 
 def rope_cos_sin(max_pos: int, rot_dim: int, theta: float, device, freq_scale: float = 1.0,

@@ -140,6 +140,150 @@ __global__ __launch_bounds__(NT) void add_norm_kernel(float* __restrict__ residu
 }
 
 // ------------------------------------------------------------------------------------
+// add_norm + the MoE router of the same row (replaces add_norm + moe_router_kernel before a
+// sparse-MoE FFN: one launch less per layer, the normed row never re-read).  The router reads the
+// bf16-ROUNDED normed values, as the unfused router reads the bf16 activation; its logits are
+// reduced across the block 8 experts at a time; thread 0 then takes softmax / top-k / renorm /
+// EP remap exactly as moe_router_kernel (moe.hip).  E <= 64, 1024 threads, D <= 8192.
+struct NormRouter {
+  const float* wr;  // [E][D] fp32
+  int E, topk, renorm;
+  float scale;
+  int ep_base, ep_local;
+  int* ids;         // [T][topk]
+  float* wts;       // [T * topk]
+};
+
+template <int IT>
+__global__ __launch_bounds__(1024) void add_norm_router_kernel(float* __restrict__ residual, Src add, int has_add,
+                                                               const float* __restrict__ w,
+                                                               const float* __restrict__ b, bf16* __restrict__ out,
+                                                               int D, float eps, int mode, NormRouter R) {
+  constexpr int NT = 1024, NWV = NT / 64;
+  __shared__ float red[NWV];
+  __shared__ float rl[NWV][8];
+  __shared__ float lg[64];
+  const int t = blockIdx.x;
+  const int nv = D >> 2;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float* rrow = residual + (long)t * D;
+  float v[IT][4];
+  float4 ww[IT], bb[IT];
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int c = min(threadIdx.x + i * NT, nv - 1);
+    ww[i] = *(const float4*)(w + 4 * c);
+    bb[i] = b ? *(const float4*)(b + 4 * c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 r = *(const float4*)(rrow + 4 * c);
+    v[i][0] = r.x; v[i][1] = r.y; v[i][2] = r.z; v[i][3] = r.w;
+    if (has_add) {
+      float a[4];
+      load4(add, (long)t * D + 4 * c, 4 * c, a);
+      v[i][0] += a[0]; v[i][1] += a[1]; v[i][2] += a[2]; v[i][3] += a[3];
+    }
+  }
+  float s1 = 0.f;
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int c = threadIdx.x + i * NT;
+    if (c < nv) {
+      if (has_add) *(float4*)(rrow + 4 * c) = make_float4(v[i][0], v[i][1], v[i][2], v[i][3]);
+      s1 += (mode == 0) ? (v[i][0] * v[i][0] + v[i][1] * v[i][1] + v[i][2] * v[i][2] + v[i][3] * v[i][3])
+                        : (v[i][0] + v[i][1] + v[i][2] + v[i][3]);
+    }
+  }
+  float mean = 0.f, rstd;
+  if (mode == 0) {
+    rstd = rsqrtf(block_sum<NT>(s1, red) / (float)D + eps);
+  } else {
+    mean = block_sum<NT>(s1, red) / (float)D;
+    float s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      const int c = threadIdx.x + i * NT;
+      if (c < nv) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { const float d = v[i][j] - mean; s2 += d * d; }
+      }
+    }
+    rstd = rsqrtf(block_sum<NT>(s2, red) / (float)D + eps);
+  }
+  float xb[IT][4];
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int c = threadIdx.x + i * NT;
+    const float o[4] = {(v[i][0] - mean) * rstd * ww[i].x + bb[i].x, (v[i][1] - mean) * rstd * ww[i].y + bb[i].y,
+                        (v[i][2] - mean) * rstd * ww[i].z + bb[i].z, (v[i][3] - mean) * rstd * ww[i].w + bb[i].w};
+    const bf16x4 ob = {(bf16)o[0], (bf16)o[1], (bf16)o[2], (bf16)o[3]};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) xb[i][j] = (c < nv) ? (float)ob[j] : 0.f;
+    if (c < nv) *(bf16x4*)(out + (long)t * D + 4 * c) = ob;
+  }
+  // router logits, 8 experts per round: per-thread partial dots -> wave sums -> block sums
+  for (int e0 = 0; e0 < R.E; e0 += 8) {
+    float p[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      p[u] = 0.f;
+      const int e = min(e0 + u, R.E - 1);  // clamped: loads never branch (extra rows unused)
+#pragma unroll
+      for (int i = 0; i < IT; ++i) {
+        const int c = min(threadIdx.x + i * NT, nv - 1);
+        const float4 wv = *(const float4*)(R.wr + (size_t)e * D + 4 * c);
+        p[u] += xb[i][0] * wv.x + xb[i][1] * wv.y + xb[i][2] * wv.z + xb[i][3] * wv.w;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) p[u] += __shfl_xor(p[u], o, 64);
+    if (lane == 0) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) rl[wave][u] = p[u];
+    }
+    __syncthreads();
+    if (threadIdx.x < 8 && e0 + (int)threadIdx.x < R.E) {
+      float sacc = 0.f;
+#pragma unroll
+      for (int wv = 0; wv < NWV; ++wv) sacc += rl[wv][threadIdx.x];
+      lg[e0 + threadIdx.x] = sacc;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x != 0) return;
+  float mx = -INFINITY;
+  for (int e = 0; e < R.E; ++e) mx = fmaxf(mx, lg[e]);
+  float z = 0.0f;
+  for (int e = 0; e < R.E; ++e) {
+    lg[e] = __expf(lg[e] - mx);
+    z += lg[e];
+  }
+  const float inv = 1.0f / z;
+  unsigned long long taken = 0ull;  // E <= 64
+  float sel[16];
+  int sid[16];
+  float sum = 0.0f;
+  for (int k = 0; k < R.topk; ++k) {
+    int best = -1;
+    float bv = -1.0f;
+    for (int e = 0; e < R.E; ++e) {
+      if ((taken >> e) & 1ull) continue;
+      if (lg[e] > bv) { bv = lg[e]; best = e; }
+    }
+    taken |= 1ull << best;
+    sid[k] = best;
+    sel[k] = bv * inv;
+    sum += sel[k];
+  }
+  for (int k = 0; k < R.topk; ++k) {
+    const float wv = (R.renorm ? sel[k] / sum : sel[k]) * R.scale;
+    const int loc = sid[k] - R.ep_base;
+    R.ids[t * R.topk + k] = (loc >= 0 && loc < R.ep_local) ? loc : R.ep_local;
+    R.wts[t * R.topk + k] = wv;
+  }
+}
+
+// ------------------------------------------------------------------------------------
 // RoPE on q,k + append k,v into the paged cache.
 // qkv row layout: [Hq*Dh | Hkv*Dh | Hkv*Dh].  K cache [num_blocks][Hkv][BS][Dh], V cache transposed
 // in groups of 8 keys: [num_blocks][Hkv][BS/8][Dh][8] (bf16, see attention.hip).
@@ -462,6 +606,26 @@ extern "C" int la_add_norm(void* residual, const void* add_p, long add_slab, int
     default: return -1;
   }
 #undef LA_NORM_CASE
+  return (int)hipGetLastError();
+}
+
+// add_norm (RMS / LayerNorm, always writing the bf16 row) + the MoE router of every row; -1 when
+// the shape is outside the fused kernel (caller runs add_norm + la_moe_router)
+extern "C" int la_add_norm_router(void* residual, const void* add_p, long add_slab, int add_S, const void* add_bias,
+                                  int has_add, const void* w, const void* b, void* out, int T, int D, float eps,
+                                  int mode, const float* wr, int E, int topk, int renorm, float scale, int ep_base,
+                                  int ep_local, int* ids, float* wts, void* stream) {
+  if ((D & 3) || D > 1024 * 4 * 2 || T < 1 || !out || !wr || !ids || !wts || E < 1 || E > 64 || topk < 1 ||
+      topk > 16 || topk > E)
+    return -1;
+  Src s{add_p, add_slab, add_S, (const float*)add_bias};
+  la::NormRouter R{wr, E, topk, renorm, scale, ep_base, ep_local, ids, wts};
+  if ((D / 4 + 1023) / 1024 == 1)
+    hipLaunchKernelGGL((la::add_norm_router_kernel<1>), dim3(T), dim3(1024), 0, (hipStream_t)stream, (float*)residual,
+                       s, has_add, (const float*)w, (const float*)b, (bf16*)out, D, eps, mode, R);
+  else
+    hipLaunchKernelGGL((la::add_norm_router_kernel<2>), dim3(T), dim3(1024), 0, (hipStream_t)stream, (float*)residual,
+                       s, has_add, (const float*)w, (const float*)b, (bf16*)out, D, eps, mode, R);
   return (int)hipGetLastError();
 }
 

@@ -912,3 +912,28 @@ def test_gemv_in_kernel_split_reduction(M, monkeypatch):
         g.replay()
         torch.cuda.synchronize()
         assert torch.equal(ops.reduce(gp), got)
+
+
+@pytest.mark.parametrize("T,E,topk,mode,renorm,ep", [(1, 8, 2, 0, True, False), (2, 8, 2, 0, True, True),
+                                                      (37, 60, 4, 0, False, False), (5, 16, 2, 1, True, False)])
+def test_add_norm_router_matches_unfused(T, E, topk, mode, renorm, ep):
+    """add_norm_router (one launch) == add_norm + moe_router: identical bf16 rows and residual,
+    identical expert ids, routing weights to fp32 rounding (block-order sums of the logits)."""
+    g = torch.Generator(device="cpu").manual_seed(T * 100 + E)
+    D = 4096
+    res0 = torch.randn(T, D, generator=g).to(DEV)
+    slabs = torch.randn(3, T, D, generator=g).to(DEV) * 0.5
+    w = (1.0 + 0.1 * torch.randn(D, generator=g)).to(DEV)
+    b = (0.1 * torch.randn(D, generator=g)).to(DEV) if mode == 1 else None
+    router = (torch.randn(E, D, generator=g) * 0.05).to(DEV)
+    base, local = (E // 2, E // 2) if ep else (0, 0)
+    ra, rb = res0.clone(), res0.clone()
+    xa = ops.add_norm(ra, ops.Partial(slabs), w, b, 1e-5, mode)
+    ida, wa = ops.moe_router(xa, router, topk, renorm, 1.0, base, local)
+    fused = ops.add_norm_router(rb, ops.Partial(slabs), w, b, 1e-5, mode, router, topk, renorm, 1.0, base, local)
+    assert fused is not None
+    xb, idb, wb = fused
+    torch.cuda.synchronize()
+    assert torch.equal(ra, rb) and torch.equal(xa, xb)
+    assert torch.equal(ida, idb)
+    assert torch.allclose(wa, wb, rtol=1e-5, atol=1e-6)
