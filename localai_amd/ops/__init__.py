@@ -54,6 +54,7 @@ def lib():
             "la_gemv_variant": [I],
             "la_moe_tune": [I, I],
             "la_dec_one_part": [I],
+            "la_moe_gemv_variant": [I],
             "la_gather_rows": [P, P, LNG, P, P, LNG, P],
             "la_qgemv_dp4_rope": [I, P, P, P, I, P, I, P, P, P, I, I, I, P, P, P, I, P],
             "la_qgemv_dp4_norm": [I, P, P, P, I, I, I, P, I, LNG, P, P, LNG, I, P, P, F, P, P],
@@ -125,6 +126,8 @@ def lib():
         if mt:
             a, b = (int(v) for v in mt.split(","))
             _check(L.la_moe_tune(a, b), "la_moe_tune")
+        if os.environ.get("LOCALAI_AMD_MOE_GEMV_VAR") and hasattr(L, "la_moe_gemv_variant"):
+            _check(L.la_moe_gemv_variant(int(os.environ["LOCALAI_AMD_MOE_GEMV_VAR"])), "la_moe_gemv_variant")
         if os.environ.get("LOCALAI_AMD_DEC_ONE_PART") and hasattr(L, "la_dec_one_part"):
             _check(L.la_dec_one_part(int(os.environ["LOCALAI_AMD_DEC_ONE_PART"])), "la_dec_one_part")
         _LIB = L

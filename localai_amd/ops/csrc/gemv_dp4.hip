@@ -972,6 +972,7 @@ static inline size_t gv_lds_bytes(int MT, int kper) {
   return (size_t)MT * kper + (size_t)MT * (kper >> 4) * 4 + (size_t)MT * (kper >> 5) * 4;
 }
 
+static int g_moe_gv_var = 5;  // moe_gemv_kernel variant (la_moe_gemv_variant)
 static int g_gv_variant = 5;  // non-temporal weight loads, x staged first, one 8-row slot per wave (fastest overall)
 
 template <int MT, int FA, int FB>
@@ -1186,17 +1187,38 @@ extern "C" int la_moe_gemv(int fmt, int down, const void* qws, int N, int K, int
   const size_t lds = gv_lds_bytes(1, kper);
   if (lds > 64 * 1024) return -3;
   GVAct act{(const float*)act_p, act_slab, act_S, nullptr, act_mode, K};
-  constexpr int V = 5;  // non-temporal weights, x staged first, one 8-row slot per wave
-  const int rows = 32 * gv_rs<V>();
-  dim3 grid((N + rows - 1) / rows, splits, T * topk);
+  // variant (la_moe_gemv_variant): 5 = non-temporal weights, x staged first, one 8-row slot per
+  // wave (default); 21 = + 4-deep weight ring (whole groups of 4 super-blocks only); 1 / 9 = two /
+  // four 8-row slots per wave
+  int var = g_moe_gv_var;
+  if ((var & 16) && ((kper >> 8) % 4)) var &= ~16;
   hipStream_t st = (hipStream_t)stream;
-#define MG(F) hipLaunchKernelGGL((moe_gemv_kernel<F, V>), grid, dim3(GV_THREADS), lds, st, (const QW*)qws, ids, \
-                                 E_local, topk, (const bf16*)X, ldx, act, wts, down, kper, (float*)out, ldo, slab)
-  if (fmt == FMT_Q4_K) MG(FMT_Q4_K);
-  else if (fmt == FMT_Q6_K) MG(FMT_Q6_K);
-  else MG(FMT_Q8_0);
+#define MG(F, V)                                                                                              \
+  {                                                                                                           \
+    const int rows = 32 * gv_rs<V>();                                                                         \
+    dim3 grid((N + rows - 1) / rows, splits, T * topk);                                                       \
+    hipLaunchKernelGGL((moe_gemv_kernel<F, V>), grid, dim3(GV_THREADS), lds, st, (const QW*)qws, ids, E_local, \
+                       topk, (const bf16*)X, ldx, act, wts, down, kper, (float*)out, ldo, slab);              \
+  }
+#define MGV(F)                        \
+  switch (var) {                      \
+    case 1: MG(F, 1) break;           \
+    case 9: MG(F, 9) break;           \
+    case 21: MG(F, 21) break;         \
+    default: MG(F, 5) break;          \
+  }
+  if (fmt == FMT_Q4_K) MGV(FMT_Q4_K)
+  else if (fmt == FMT_Q6_K) MGV(FMT_Q6_K)
+  else MGV(FMT_Q8_0)
+#undef MGV
 #undef MG
   return (int)hipGetLastError();
+}
+
+extern "C" int la_moe_gemv_variant(int v) {
+  if (v != 1 && v != 5 && v != 9 && v != 21) return -1;
+  la::g_moe_gv_var = v;
+  return 0;
 }
 
 // Tuning hook: select the kernel variant (bit 0 non-temporal loads, bit 1 early weight prefetch).
