@@ -972,7 +972,9 @@ static inline size_t gv_lds_bytes(int MT, int kper) {
   return (size_t)MT * kper + (size_t)MT * (kper >> 4) * 4 + (size_t)MT * (kper >> 5) * 4;
 }
 
-static int g_moe_gv_var = 5;  // moe_gemv_kernel variant (la_moe_gemv_variant)
+// moe_gemv_kernel variant (la_moe_gemv_variant): 1 = two 8-row slots per wave -- Mixtral C=1 312.8 /
+// 313.2 vs 306.4 tok/s with variant 5, C=2 413.3 / 412.8 vs 404.0 (profiles/r5_logs/r5_mv2_*.log)
+static int g_moe_gv_var = 1;
 static int g_gv_variant = 5;  // non-temporal weight loads, x staged first, one 8-row slot per wave (fastest overall)
 
 template <int MT, int FA, int FB>
@@ -1187,9 +1189,9 @@ extern "C" int la_moe_gemv(int fmt, int down, const void* qws, int N, int K, int
   const size_t lds = gv_lds_bytes(1, kper);
   if (lds > 64 * 1024) return -3;
   GVAct act{(const float*)act_p, act_slab, act_S, nullptr, act_mode, K};
-  // variant (la_moe_gemv_variant): 5 = non-temporal weights, x staged first, one 8-row slot per
-  // wave (default); 21 = + 4-deep weight ring (whole groups of 4 super-blocks only); 1 / 9 = two /
-  // four 8-row slots per wave
+  // variant (la_moe_gemv_variant): 1 = non-temporal weights, x staged first, two 8-row slots per
+  // wave (default); 5 = one slot; 21 = one slot + 4-deep weight ring (whole groups of 4
+  // super-blocks only); 9 = four slots
   int var = g_moe_gv_var;
   if ((var & 16) && ((kper >> 8) % 4)) var &= ~16;
   hipStream_t st = (hipStream_t)stream;
@@ -1202,10 +1204,10 @@ extern "C" int la_moe_gemv(int fmt, int down, const void* qws, int N, int K, int
   }
 #define MGV(F)                        \
   switch (var) {                      \
-    case 1: MG(F, 1) break;           \
     case 9: MG(F, 9) break;           \
     case 21: MG(F, 21) break;         \
-    default: MG(F, 5) break;          \
+    case 5: MG(F, 5) break;           \
+    default: MG(F, 1) break;          \
   }
   if (fmt == FMT_Q4_K) MGV(FMT_Q4_K)
   else if (fmt == FMT_Q6_K) MGV(FMT_Q6_K)
