@@ -363,6 +363,12 @@ class Scheduler {
       chunks.push_back({id, cached, n});
       budget -= n;
     }
+    // A deferred (prefill-only) step that found no prefill it can actually run -- the waiting
+    // head does not fit the KV pool -- must not come back empty: nothing would decode, so no
+    // block would ever be freed and the engine would spin until the prefill-first cap expired.
+    // The deferred pass mutated nothing (no decode reservations, no allocation), so plan again
+    // with decode.
+    if (defer_decode && chunks.empty() && preempted.empty()) return schedule(lookahead, false);
 
     // ---- 3. pack device inputs
     py::dict out;

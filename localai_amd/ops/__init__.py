@@ -98,6 +98,9 @@ def lib():
             "la_attn_dense": [P, LNG, P, LNG, P, LNG, P, LNG, P, I, P, I, I, I, F, P],
             "la_gemm_pp2": [I, P, P, P, I, I, P, P, P, I, I, P, I, I, I, P, I, LNG, I, P],
             "la_gemm_pp_glu": [I, P, P, P, I, P, P, P, I, I, I, P, I, I, P, I, I, P],
+            "la_bsgemm": [I, P, P, P, I, I, P, I, I, I, P, I, LNG, I, I, P],
+            "la_bsgemm2": [I, P, P, P, I, I, P, P, P, I, I, P, I, I, I, P, I, LNG, I, I, P],
+            "la_bsgemm_glu": [I, P, P, P, I, P, P, P, I, I, I, P, I, I, P, I, I, I, P],
             "la_decode_advance": [P, P, P, P, P, P, I, I, I, P, I, P, P, P],
             "la_img_resample_h": [P, I, I, P, I, P, P, I, P],
             "la_img_resample_v_tiles": [P, I, I, P, P, I, I, I, I, I, I, I, P, P, P, P, P],
@@ -850,6 +853,55 @@ def _run_q32(x, ws, S, out, Ntot, var):
         _check(lib().la_qgemm32(w.fmt, p0, p1, g, w.N, w.K, x.data_ptr(), K, M, S, out.data_ptr() + col * esz, Ntot,
                                 0 if bf else M * Ntot, int(bf), var, _stream()), "la_qgemm32")
         col += w.N
+
+
+# Shared-dequant-image GEMM (gemm_bs.hip): variant id -> (BM, BN).  Each weight column is
+# dequantised once per workgroup into an LDS image all four waves read; X arrives by full-line
+# loads through a private per-wave LDS transpose.  Decode batches (M 65..256) and prefill chunks.
+BS_TILES = {0: (256, 128), 1: (128, 128), 2: (256, 256), 3: (256, 128)}
+BS_FMTS = (FMT_Q4_K, FMT_Q6_K, FMT_Q8_0, FMT_BF16)
+BS = os.environ.get("LOCALAI_AMD_BS", "1") == "1"
+
+
+def bs_ok(ws: Sequence[QWeight]) -> bool:
+    """Can gemm_bs.hip run these weights (one launch per weight, or one for a Q4_K/Q6_K pair)."""
+    return BS and all(w.fmt in BS_FMTS and w.K % 256 == 0 and w.N % 4 == 0 and w.planes[0] is not None
+                      for w in ws)
+
+
+def _bs_grid(M: int, N: int, var: int) -> int:
+    bm, bn = BS_TILES[var]
+    return -(-M // bm) * -(-N // bn)
+
+
+def _run_bs(x, ws, S, out, Ntot, var):
+    """out: fp32 slabs [S, M, Ntot], or a bf16 [M, Ntot] matrix (S == 1).  A Q4_K/Q6_K pair (q|k +
+    v) runs as ONE launch (la_bsgemm2)."""
+    M, K = x.shape
+    bf = out.dtype == torch.bfloat16
+    esz = 2 if bf else 4
+    slab = 0 if bf else M * Ntot
+    if len(ws) == 2 and (ws[0].fmt, ws[1].fmt) in _TILE2_PAIRS:
+        a0, a1, ag = ws[0].tile_planes()
+        b0, b1, bg = ws[1].tile_planes()
+        _check(lib().la_bsgemm2(ws[0].fmt, a0, a1, ag, ws[0].N, ws[1].fmt, b0, b1, bg, ws[1].N, K, x.data_ptr(), K,
+                                M, S, out.data_ptr(), Ntot, slab, int(bf), var, _stream()), "la_bsgemm2")
+        return
+    col = 0
+    for w in ws:
+        p0, p1, g = w.tile_planes()
+        _check(lib().la_bsgemm(w.fmt, p0, p1, g, w.N, w.K, x.data_ptr(), K, M, S, out.data_ptr() + col * esz, Ntot,
+                               slab, int(bf), var, _stream()), "la_bsgemm")
+        col += w.N
+
+
+def _run_bs_glu(x, pair, F: int, mode: int, var: int, out) -> None:
+    M, K = x.shape
+    wa, oa, wb, ob = pair
+    a0, a1, ag = wa.tile_planes()
+    b0, b1, bg = wb.tile_planes()
+    _check(lib().la_bsgemm_glu(wa.fmt, a0, a1, ag, oa, b0, b1, bg, ob, F, K, x.data_ptr(), K, M, out.data_ptr(), F,
+                               mode, var, _stream()), "la_bsgemm_glu")
 
 
 # Prefill GEMM (gemm_pp.hip): 256 x 256 ping-pong MFMA tiles with the GGUF dequantisation in the

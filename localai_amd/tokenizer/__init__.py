@@ -130,22 +130,34 @@ class Tokenizer:
     _WORD_CACHE_SIZE = 1 << 17
 
     def _bpe_fast(self, s: str) -> List[int]:
+        """Encode through the per-pre-token cache.  The output is built from a local map filled
+        before any eviction, so a concurrent or size-triggered clear() of the shared cache (other
+        gateway threads share this tokenizer) can never drop an entry this call still needs."""
         words = self._pre_re.findall(s)
         cache = self._word_cache
-        miss = [w for w in words if w not in cache]
+        got: Dict[str, tuple] = {}
+        miss: List[str] = []
+        for w in words:
+            if w in got:
+                continue
+            hit = cache.get(w)
+            if hit is None:
+                miss.append(w)
+                got[w] = ()
+            else:
+                got[w] = hit
         if miss:
-            uniq = list(dict.fromkeys(miss))
-            enc = self._hf_words.encode(uniq, is_pretokenized=True, add_special_tokens=False)
-            per: List[List[int]] = [[] for _ in uniq]
-            for t, w in zip(enc.ids, enc.word_ids):
-                per[w].append(t)
-            if len(cache) + len(uniq) > self._WORD_CACHE_SIZE:
+            enc = self._hf_words.encode(miss, is_pretokenized=True, add_special_tokens=False)
+            per: List[List[int]] = [[] for _ in miss]
+            for t, wi in zip(enc.ids, enc.word_ids):
+                per[wi].append(t)
+            if len(cache) + len(miss) > self._WORD_CACHE_SIZE:
                 cache.clear()
-            for w, p in zip(uniq, per):
-                cache[w] = tuple(p)
+            for w, p in zip(miss, per):
+                got[w] = cache[w] = tuple(p)
         out: List[int] = []
         for w in words:
-            out.extend(cache[w])
+            out.extend(got[w])
         return out
 
     def _piece_bytes(self, i: int) -> bytes:

@@ -17,6 +17,9 @@ for f in sorted(glob.glob(os.path.join(d, "counters*.csv"))):
             if not name or val is None:
                 continue
             short = k.split("(")[0][:70]
+            g = row.get("Grid_Size") or row.get("Grid-Size")
+            if g:
+                short += f" [grid {g}]"
             acc[short][name].append(float(val))
 names = sorted({n for v in acc.values() for n in v})
 print("| kernel | " + " | ".join(names) + " |")

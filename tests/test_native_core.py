@@ -81,6 +81,21 @@ def test_scheduler_preempts_youngest_when_out_of_blocks():
     assert 2 in pre  # the younger sequence is evicted and later recomputed
 
 
+def test_scheduler_deferred_step_decodes_when_waiting_prompt_does_not_fit():
+    """Burst prefill-first mode (defer_decode) with a KV pool too small for the waiting prompt: the
+    step must fall back to decoding the running rows (which frees blocks as they finish) instead
+    of returning an empty plan forever."""
+    s = core.Scheduler(4, 4, 8, 64, 256, False, 0)
+    s.add(1, [1, 2, 3], 3)          # 1 block
+    d = s.schedule()
+    assert list(d["p_ids"]) == [1]
+    s.append(1, 9)
+    s.add(2, list(range(20)), 2)    # needs 5 blocks: never fits while seq 1 holds one
+    d = s.schedule(1, True)
+    assert list(d["d_ids"]) == [1], "deferred step came back empty"
+    assert len(d["p_ids"]) == 0
+
+
 def _vocab():
     pieces = [b"", b"Hel", b"lo", b" wor", b"ld", b"<|eot|>", b"\xe2\x82", b"\xac", b"STOP", b"x"]
     return core.Vocab(pieces)

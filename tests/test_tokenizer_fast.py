@@ -31,3 +31,21 @@ def test_fast_bpe_matches_library_pipeline(preset, tmp_path):
     for t in texts[:200]:
         a = tok.encode(t, add_bos=False)
         assert a == tok.encode(t, add_bos=False)
+
+
+def test_fast_bpe_survives_cache_eviction(tmp_path, monkeypatch):
+    """A prompt that mixes cached and new pre-tokens right when the cache overflows (the size
+    check clears it) still encodes: hits are copied out before any eviction."""
+    p = synth.write_model(str(tmp_path / "t.gguf"), "tiny-llama", n_vocab=128256, tokenizer="llama3")
+    tok = Tokenizer.from_gguf(GGUFReader(p))
+    if tok.model != "gpt2" or tok._pre_re is None:
+        pytest.skip("no fast BPE path")
+    monkeypatch.setattr(type(tok), "_WORD_CACHE_SIZE", 4)
+    ref = lambda t: tok._hf.encode(t, add_special_tokens=False).ids  # noqa: E731
+    assert tok._bpe_fast("alpha beta") == ref("alpha beta")       # 2 words cached
+    # two hits + three misses: 2 + 3 > 4 clears the cache between the lookup and the output
+    t = "alpha beta gamma delta epsilon"
+    assert tok._bpe_fast(t) == ref(t)
+    # concurrent clear from another thread between calls
+    tok._word_cache.clear()
+    assert tok._bpe_fast(t) == ref(t)
