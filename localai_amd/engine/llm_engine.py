@@ -217,8 +217,15 @@ class LLMEngine:
             # persistent bf16 copy up front, so a decode batch of 65-256 rows never re-dequantises
             # them into scratch inside its graph (2 B/weight written + read back every step)
             self._materialize_bf16(only_non_tile=ops.TILE_GEMM)
-            self._prefill_bf16_copies()
         num_blocks = self._num_kv_blocks()
+        if self.tp.world > 1:
+            # the schedulers are replicated: every rank must admit and preempt exactly as rank 0
+            # does, so the KV pool is the smallest any rank can hold (each rank sized it from its
+            # own free memory)
+            import torch.distributed as dist
+            nb = torch.tensor([num_blocks], dtype=torch.int64)
+            dist.all_reduce(nb, op=dist.ReduceOp.MIN, group=self.ctrl)
+            num_blocks = int(nb.item())
         if faults.hit("kv_alloc"):
             raise faults.InjectedFault("hipMalloc failed for the KV cache (injected fault): out of memory")
         self.kv = self.model.new_kv_cache(num_blocks, bs)
@@ -317,52 +324,6 @@ class LLMEngine:
         if self.device.type == "cuda":
             torch.cuda.synchronize(self.device)
         log.info("materialised %.2f GB of bf16 weight copies", need / 2**30)
-
-    # Resident bf16 copies of the dense projections for the prefill GEMMs (hipBLASLt reads them in
-    # place instead of each prefill chunk dequantising every weight into scratch: 2 B/weight written
-    # and read back per chunk, ~5 % of a chunk's GEMM time).  The decode GEMMs keep reading the
-    # quantised planes.  "auto": only when the copies take at most PREFILL_BF16_FRAC of what is left
-    # for the KV cache after the cache the config asks for (Llama-3-8B: 15 GB of 288 GB).
-    PREFILL_BF16 = os.environ.get("LOCALAI_AMD_PREFILL_BF16", "auto")
-    PREFILL_BF16_FRAC = 0.5
-    # the experts of a sparse MoE too (their prefill runs per-expert library GEMMs over the routed
-    # rows, models/decoder._moe_dense_prefill).  Off by default: Mixtral-8x7B HTTP C=256 measured
-    # 9791 / 9841 / 10068 tok/s with the copies vs 9602 / 10022 without (p50 TTFT 984 / 900 / 990
-    # vs 1008 / 878 ms) -- within box noise, for 84 GB more device memory (r5_mxe_*.log)
-    PREFILL_BF16_EXPERTS = os.environ.get("LOCALAI_AMD_PREFILL_BF16_EXPERTS", "0") == "1"
-
-    def _prefill_bf16_copies(self):
-        if self.PREFILL_BF16 == "never" or not ops.TILE_GEMM or ops.PREFILL_GEMM != "blas":
-            return
-        m = self.model
-        groups = []
-        for L in m.layers:
-            grps = [L.qkv, L.gate_up, [L.wo]] + ([[L.down]] if L.down is not None else [])
-            if L.experts and self.PREFILL_BF16_EXPERTS:
-                for gu, d in L.experts:
-                    grps += [list(gu), [d]]
-            for grp in grps:
-                if grp and all(w is not None and w.tile_ok for w in grp) and any(w.bf16 is None for w in grp):
-                    groups.append(grp)
-        need = sum(w.N * w.K * 2 for grp in groups for w in grp if w.bf16 is None and w.fmt != ops.FMT_BF16)
-        if not need:
-            return
-        if self.PREFILL_BF16 == "auto":
-            free, total = torch.cuda.mem_get_info(self.device)
-            free += torch.cuda.memory_reserved(self.device) - torch.cuda.memory_allocated(self.device)
-            budget = int(free - (1.0 - self.cfg.gpu_memory_utilization) * total) - (4 << 30)
-            left = budget - self._kv_blocks_wanted() * self._kv_block_bytes()
-            if need > self.PREFILL_BF16_FRAC * left:
-                log.info("prefill bf16 copies skipped: %.1f GB needed, %.1f GB left after the KV cache",
-                         need / 2**30, max(0, left) / 2**30)
-                return
-        for grp in groups:
-            for w in grp:
-                w.materialize_bf16()
-            if len(grp) > 1:
-                ops.fuse_bf16(grp)
-        torch.cuda.synchronize(self.device)
-        log.info("prefill bf16 copies: %.1f GB resident", need / 2**30)
 
     def _kv_block_bytes(self) -> int:
         return 2 * self.hp.n_layer * self.model.Hkv * self.cfg.block_size * self.model.Dh * 2

@@ -1021,6 +1021,12 @@ def _autotune_mid(x, ws, key, Ntot):
             for S in sorted({1, max(1, base // 2), base, base * 2}):
                 if S <= min(8, K // 256) and _tile_split_ok(K, S):
                     cands.append(("q32", S, v))
+    if bs_ok(ws) and (len(ws) == 1 or (len(ws) == 2 and (ws[0].fmt, ws[1].fmt) in _TILE2_PAIRS)):
+        for v in ((0, 1, 3) if M > 128 else (1,)):
+            base = max(1, round(256 / _bs_grid(M, N, v)))
+            for S in sorted({1, max(1, base // 2), base, base * 2}):
+                if S <= min(8, K // 256) and _tile_split_ok(K, S):
+                    cands.append(("bs", S, v))
     if not cands or os.environ.get("LOCALAI_AMD_BLAS_CANDIDATE") == "1" or not TILE_GEMM:
         cands.append(("blas", 0, 0))
     if not TILE_GEMM:
@@ -1033,6 +1039,8 @@ def _autotune_mid(x, ws, key, Ntot):
             fn = lambda: _run_blas(x, ws, Ntot)  # noqa: E731
         elif kind == "tile":
             fn = lambda S=S, t=t: _run_tile(x, ws, S, outs[S], Ntot, t)  # noqa: E731
+        elif kind == "bs":
+            fn = lambda S=S, t=t: _run_bs(x, ws, S, outs[S], Ntot, t)  # noqa: E731
         else:
             fn = lambda S=S, t=t: _run_q32(x, ws, S, outs[S], Ntot, t)  # noqa: E731
         fn()
@@ -1080,9 +1088,9 @@ def linear_multi(x: torch.Tensor, ws: Sequence[QWeight], bias: Optional[torch.Te
     use_skinny = (M <= SKINNY_MAX_M and skinny_ok) if force is None else force == "skinny"
     tile_ok = TILE_GEMM and all(w.tile_ok for w in ws)
     S, tile, kind = 0, 0, None
-    if force is not None and force.startswith("q32:"):
-        _, v, s_ = force.split(":")
-        tile, S, kind = int(v), int(s_), "q32"
+    if force is not None and (force.startswith("q32:") or force.startswith("bs:")):
+        kind, v, s_ = force.split(":")
+        tile, S = int(v), int(s_)
     elif force is not None and force.startswith("tile"):
         # "tile" (heuristic) or "tile:<id>:<S>"
         parts = force.split(":")
@@ -1098,7 +1106,7 @@ def linear_multi(x: torch.Tensor, ws: Sequence[QWeight], bias: Optional[torch.Te
         if choice is None and tile_ok:
             t, s_ = pick_tile(M, [w.N for w in ws], K)
             choice = ("tile", s_, t)
-        if choice is not None and choice[0] in ("tile", "q32"):
+        if choice is not None and choice[0] in ("tile", "q32", "bs"):
             kind, S, tile = choice
     elif force is None and not use_skinny and tile_ok and PREFILL_GEMM == "tile":
         tile, S = pick_tile(M, [w.N for w in ws], K)   # prefill: heuristic, never tuned inline
@@ -1109,12 +1117,12 @@ def linear_multi(x: torch.Tensor, ws: Sequence[QWeight], bias: Optional[torch.Te
         S, kind = pp_splits(M, Ntot, K), "pp"
         while S > 1 and not pp_ok(ws, K, S):
             S //= 2
-    if kind in ("tile", "q32", "pp") and S == 1 and out_slabs is None:
+    if kind in ("tile", "q32", "pp", "bs") and S == 1 and out_slabs is None:
         y = torch.empty(M, Ntot, dtype=torch.bfloat16, device=x.device)
         if kind == "pp":
             _run_pp(x, ws, 1, y, Ntot)
         else:
-            (_run_tile if kind == "tile" else _run_q32)(x, ws, 1, y, Ntot, tile)
+            {"tile": _run_tile, "q32": _run_q32, "bs": _run_bs}[kind](x, ws, 1, y, Ntot, tile)
         return Partial(y, bias)
     if S:
         out = out_slabs
@@ -1124,6 +1132,8 @@ def linear_multi(x: torch.Tensor, ws: Sequence[QWeight], bias: Optional[torch.Te
             _run_tile(x, ws, S, out, Ntot, tile)
         elif kind == "pp":
             _run_pp(x, ws, S, out, Ntot)
+        elif kind == "bs":
+            _run_bs(x, ws, S, out, Ntot, tile)
         else:
             _run_q32(x, ws, S, out, Ntot, tile)
         return Partial(out, bias)
@@ -1175,9 +1185,12 @@ def _glu_pair(ws: Sequence[QWeight], F: int):
 
 
 def _run_glu(x: torch.Tensor, pair, F: int, mode: int, tile: int, out: torch.Tensor) -> None:
-    """tile < 100: gemm_q.hip tile id; 100 + v: gemm_q32.hip variant v."""
+    """tile < 100: gemm_q.hip tile id; 100 + v: gemm_q32.hip variant v; 200 + v: gemm_bs.hip variant v."""
     M, K = x.shape
     wa, oa, wb, ob = pair
+    if tile >= 200:
+        _run_bs_glu(x, pair, F, mode, tile - 200, out)
+        return
     a0, a1, ag = wa.tile_planes()
     b0, b1, bg = wb.tile_planes()
     if tile >= 100:
@@ -1239,6 +1252,8 @@ def glu_linear(x: torch.Tensor, ws: Sequence[QWeight], F: int, mode: int,
             # (128-row tiles at M > 128 -- 107 / 105, two row tiles to fill the chip -- were timed
             # and never won: r5_glu_bench.log)
             cands += [109, 108, 104] if M > 128 else [109, 108, 107]
+        if bs_ok([pair[0], pair[2]]) and pair[0].fmt == pair[2].fmt and F % 4 == 0:
+            cands += [200, 203] if M > 128 else [201]
         for t in cands:
             tt = _time_cold(lambda t=t: _run_glu(x, pair, F, mode, t, out))
             if tt < best_t:

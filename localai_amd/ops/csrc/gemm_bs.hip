@@ -235,6 +235,66 @@ struct BsGlu {
 
 LA_DEV float bs_gelu_tanh(float x) { return 0.5f * x * (1.f + tanhf(0.7978845608f * (x + 0.044715f * x * x * x))); }
 
+// Epilogue straight from the accumulators: lane (m = c32, hh) of block (cb, mb) holds columns
+// n = 32cb + 8g + 4hh + e (g = reg >> 2, e = reg & 3) of row 32mb + c32 of the wave's rows.
+template <class C, int MODE>
+LA_DEV void bs_epilogue(const bsf32x16 (&acc)[C::NCB][C::MB], const QW& w, int mt, int nt, int split, int M,
+                        float* __restrict__ out, bf16* __restrict__ outb, int ldo, long slab, const BsGlu& glu) {
+  constexpr int RM = C::RM, MB = C::MB, NCB = C::NCB;
+  const int lane = threadIdx.x & 63, c32 = lane & 31, hh = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int mrow0 = mt * C::BM + wave * RM + c32;
+  if constexpr (MODE == 1) {
+    const int j0 = nt * (C::BN / 2);
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) {
+      const int m = mrow0 + 32 * mb;
+      if (m >= M) continue;
+#pragma unroll
+      for (int cb = 0; cb < NCB / 2; ++cb)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int j = j0 + 32 * cb + 8 * g + 4 * hh;
+          bf16x4 hv;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float gv = acc[cb][mb][4 * g + e], uv = acc[cb + NCB / 2][mb][4 * g + e];
+            hv[e] = (bf16)((glu.act == 0 ? silu(gv) : bs_gelu_tanh(gv)) * uv);
+          }
+          if (j < glu.F) *(bf16x4*)(outb + (size_t)m * ldo + j) = hv;  // F % 4 == 0
+        }
+    }
+  } else {
+    const int n0 = nt * C::BN;
+    constexpr bool BFO = MODE == 2;  // bf16 [M][ldo] output, else fp32 slab `split`
+    float* o = BFO ? nullptr : out + (size_t)split * slab;
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) {
+      const int m = mrow0 + 32 * mb;
+      if (m >= M) continue;
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int n = n0 + 32 * cb + 8 * g + 4 * hh;
+          const f32x4 v{acc[cb][mb][4 * g], acc[cb][mb][4 * g + 1], acc[cb][mb][4 * g + 2], acc[cb][mb][4 * g + 3]};
+          if (n < w.N) {  // N % 4 == 0
+            if constexpr (BFO) {
+              bf16x4 bv;
+              bv[0] = (bf16)v[0];
+              bv[1] = (bf16)v[1];
+              bv[2] = (bf16)v[2];
+              bv[3] = (bf16)v[3];
+              *(bf16x4*)(outb + (size_t)m * ldo + n) = bv;
+            } else {
+              *(f32x4*)(o + (size_t)m * ldo + n) = v;
+            }
+          }
+        }
+    }
+  }
+}
+
 // One (M tile, N tile, K split) of a plain (MODE 0) or GLU (MODE 1) GEMM.
 template <int FMT, class C, int MODE, int ABL = 0>
 LA_DEV void bs_tile(uint8_t* __restrict__ lds, const QW& w, int mt, int nt, int split, const bf16* __restrict__ X,
@@ -423,6 +483,7 @@ LA_DEV void bs_tile(uint8_t* __restrict__ lds, const QW& w, int mt, int nt, int 
       constexpr int s = decltype(s_)::value;
       read_a(af[(s + 1) & 1], xcur, std::integral_constant<int, s + 1>{});
       read_b(bf[(s + 1) & 1], bcur, s + 1);
+      fence();  // the next sub-step's fragment reads issue BEFORE this sub-step's MFMAs
       if constexpr (s == 0) load_w(P_, t + D);
       load_x(P_, t + D, s * XL / 4, (s + 1) * XL / 4);
       // this sub-step's share of the next step's work: dequant pieces + X image writes
@@ -451,6 +512,7 @@ LA_DEV void bs_tile(uint8_t* __restrict__ lds, const QW& w, int mt, int nt, int 
     load_x(P_, t + D, 3 * XL / 4, XL);
     read_a(af[0], xnxt, I0{});
     read_b(bf[0], bnxt, 0);
+    fence();
     mfmas(af[1], bf[1]);
     fence();
   };
@@ -468,58 +530,198 @@ LA_DEV void bs_tile(uint8_t* __restrict__ lds, const QW& w, int mt, int nt, int 
   if constexpr (D > 3)
     if (t + 2 < nk) step(I2{}, t + 2);
 
-  // ---- epilogue straight from the accumulators: lane (m = c32, hh) of block (cb, mb) holds
-  // columns n = 32cb + 8g + 4hh + e (g = reg >> 2, e = reg & 3) of row 32mb + c32
-  const int mrow0 = mt * C::BM + wave * RM + c32;
-  if constexpr (MODE == 1) {
-    const int j0 = nt * (C::BN / 2);
+  bs_epilogue<C, MODE>(acc, w, mt, nt, split, M, out, outb, ldo, slab, glu);
+}
+
+// The same tile with X in the BLOCKED layout Xb[ceil(M/32)][K/8][32 rows][8] bf16 (16-B chunk
+// (row r, k-chunk c) at ((r/32 * K/8 + c) * 32 + r%32) * 16 bytes): an A fragment (32 rows x 8 k
+// per lane half) is then two 512-B contiguous runs, so every X load is a full-line load straight
+// into the fragment registers -- no private LDS transpose (its ds_write pass was most of the LDS
+// write traffic), and X loads need no LDS space at all.  The producer kernels write this layout.
+template <int FMT, class C, int MODE, int ABL = 0>
+LA_DEV void bs_tile_xb(uint8_t* __restrict__ lds, const QW& w, int mt, int nt, int split, const bf16* __restrict__ Xb,
+                       int M, int per_split, float* __restrict__ out, bf16* __restrict__ outb, int ldo, long slab,
+                       const BsGlu& glu) {
+  using F = BsF<FMT>;
+  constexpr int RM = C::RM, CBW = C::CBW, MB = C::MB, NCB = C::NCB, BIMG = C::BIMG, D = C::D;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int KS = w.K >> 6;
+  const int k0 = split * per_split;
+  const int nk = min(KS, k0 + per_split) - k0;
+  if (nk <= 0) return;
+  const int kl = k0 + nk - 1;
+  const int c32 = lane & 31, hh = lane >> 5;
+
+  typename F::Ptr wp[CBW];
 #pragma unroll
-    for (int mb = 0; mb < MB; ++mb) {
-      const int m = mrow0 + 32 * mb;
-      if (m >= M) continue;
-#pragma unroll
-      for (int cb = 0; cb < NCB / 2; ++cb)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int j = j0 + 32 * cb + 8 * g + 4 * hh;
-          bf16x4 hv;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float gv = acc[cb][mb][4 * g + e], uv = acc[cb + NCB / 2][mb][4 * g + e];
-            hv[e] = (bf16)((glu.act == 0 ? silu(gv) : bs_gelu_tanh(gv)) * uv);
-          }
-          if (j < glu.F) *(bf16x4*)(outb + (size_t)m * ldo + j) = hv;  // F % 4 == 0
-        }
-    }
-  } else {
-    const int n0 = nt * C::BN;
-    constexpr bool BFO = MODE == 2;  // bf16 [M][ldo] output, else fp32 slab `split`
-    float* o = BFO ? nullptr : out + (size_t)split * slab;
-#pragma unroll
-    for (int mb = 0; mb < MB; ++mb) {
-      const int m = mrow0 + 32 * mb;
-      if (m >= M) continue;
-#pragma unroll
-      for (int cb = 0; cb < NCB; ++cb)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int n = n0 + 32 * cb + 8 * g + 4 * hh;
-          const f32x4 v{acc[cb][mb][4 * g], acc[cb][mb][4 * g + 1], acc[cb][mb][4 * g + 2], acc[cb][mb][4 * g + 3]};
-          if (n < w.N) {  // N % 4 == 0
-            if constexpr (BFO) {
-              bf16x4 bv;
-              bv[0] = (bf16)v[0];
-              bv[1] = (bf16)v[1];
-              bv[2] = (bf16)v[2];
-              bv[3] = (bf16)v[3];
-              *(bf16x4*)(outb + (size_t)m * ldo + n) = bv;
-            } else {
-              *(f32x4*)(o + (size_t)m * ldo + n) = v;
-            }
-          }
-        }
+  for (int i = 0; i < CBW; ++i) {
+    const int cb = wave * CBW + i;
+    if constexpr (MODE == 1) {
+      const bool up = cb >= NCB / 2;
+      const int j = nt * (C::BN / 2) + (up ? cb - NCB / 2 : cb) * 32 + c32;
+      const QW& q = up ? glu.up : w;
+      wp[i] = F::ptr(q, (up ? glu.ob : glu.oa) + min(j, glu.F - 1), hh);
+    } else {
+      const int n = min(nt * C::BN + cb * 32 + c32, w.N - 1);
+      wp[i] = F::ptr(w, n, hh);
+      if constexpr ((ABL & 16384) && FMT == FMT_Q4_K) {
+        // probe: codes repacked [N/32][K/64][32 cols][32 B] (one K-step of 32 columns = 1 KiB)
+        wp[i].q = w.p0 + ((size_t)(n >> 5) * (w.K >> 6) * 32 + (n & 31)) * 32 + 16 * hh;
+      }
     }
   }
+  // A-fragment pointers: row block mb of this wave (clamped into the allocated blocks), lane row
+  // c32, run hh; + 8 * (chunk of K-step ks, sub-step s) * 32 elements
+  const int nmb = (M + 31) >> 5;
+  const bf16* xp[MB];
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) {
+    const int b = min((mt * C::BM + wave * RM) / 32 + mb, nmb - 1);
+    xp[mb] = Xb + ((size_t)b * (w.K >> 3) * 32 + (size_t)(F::RUN / 8) * hh * 32 + c32) * 8;
+  }
+  uint8_t* bimg = lds;  // [3][4 s][NCB][64 lanes][16 B]
+
+  typename F::Raw wr[D][CBW];
+  bf16x8 xr[D][MB][4];  // A fragments of D K-steps
+  auto load_w = [&](auto P_, int t) {
+    constexpr int P = decltype(P_)::value;
+    const int ks = min(k0 + t, kl);
+    if constexpr (ABL & 8) return;
+#pragma unroll
+    for (int i = 0; i < CBW; ++i) {
+      if constexpr ((ABL & 16384) && FMT == FMT_Q4_K) {
+        wr[P][i].q = *(const u32x4*)(wp[i].q + 1024 * ks);
+        wr[P][i].s = *(const u32x2*)(wp[i].s + 128 * ks);
+      } else {
+        F::load(wr[P][i], wp[i], ks);
+      }
+    }
+  };
+  auto load_x = [&](auto P_, int t, auto s_) {
+    constexpr int P = decltype(P_)::value, s = decltype(s_)::value;
+    const int c0 = F::xk(min(k0 + t, kl)) >> 3;  // first 8-k chunk of run 0
+    if constexpr (ABL & 4) return;
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) xr[P][mb][s] = *(const bf16x8*)(xp[mb] + (size_t)(c0 + s) * 256);
+  };
+  auto fence = [&]() {
+    if constexpr (!(ABL & 1024)) __builtin_amdgcn_sched_barrier(0);
+  };
+  auto deq_piece = [&](auto P_, auto p_, uint8_t* img) {
+    constexpr int P = decltype(P_)::value, p = decltype(p_)::value;
+#pragma unroll
+    for (int i = 0; i < CBW; ++i) {
+      const int cb = wave * CBW + i;
+      const bf16x8 v = F::template deq<p>(wr[P][i], hh);
+      const int s = F::S(p, hh), run = F::R(p, hh);
+      *(bf16x8*)(img + ((s * NCB + cb) * 64 + c32 + 32 * run) * 16) = v;
+    }
+  };
+
+  bsf32x16 acc[NCB][MB];
+#pragma unroll
+  for (int a = 0; a < NCB; ++a)
+#pragma unroll
+    for (int b = 0; b < MB; ++b)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[a][b][i] = 0.f;
+
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using I3 = std::integral_constant<int, 3>;
+  auto load_x_all = [&](auto P_, int t) {
+    load_x(P_, t, I0{});
+    load_x(P_, t, I1{});
+    load_x(P_, t, I2{});
+    load_x(P_, t, I3{});
+  };
+  load_w(I0{}, 0);
+  load_x_all(I0{}, 0);
+  load_w(I1{}, 1);
+  load_x_all(I1{}, 1);
+  if constexpr (D > 2) {
+    load_w(I2{}, 2);
+    load_x_all(I2{}, 2);
+  }
+  if constexpr (D > 3) {
+    load_w(I3{}, 3);
+    load_x_all(I3{}, 3);
+  }
+  deq_piece(I0{}, I0{}, bimg);
+  deq_piece(I0{}, I1{}, bimg);
+  deq_piece(I0{}, I2{}, bimg);
+  deq_piece(I0{}, I3{}, bimg);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+
+  bf16x8 bf[2][NCB];
+  auto read_b = [&](bf16x8 (&dst)[NCB], const uint8_t* img, int s) {
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb) dst[cb] = *(const bf16x8*)(img + ((s * NCB + cb) * 64 + lane) * 16);
+  };
+  auto mfmas = [&](auto P_, auto s_, const bf16x8 (&b)[NCB]) {
+    constexpr int P = decltype(P_)::value, s = decltype(s_)::value;
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb) {
+        acc[cb][mb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[cb], xr[P][mb][s], acc[cb][mb], 0, 0, 0);
+      }
+  };
+  read_b(bf[0], bimg, 0);
+
+  auto step = [&](auto P_, int t) {
+    constexpr int P = decltype(P_)::value;
+    using NX = std::integral_constant<int, (P + 1) % D>;
+    const int ib = t % 3;
+    const uint8_t* bcur = bimg + ib * BIMG;
+    uint8_t* bnxt = bimg + ((ib + 1) % 3) * BIMG;
+    auto sub = [&](auto s_) {
+      constexpr int s = decltype(s_)::value;
+      read_b(bf[(s + 1) & 1], bcur, s + 1);
+      fence();  // the next sub-step's fragment reads issue BEFORE this sub-step's MFMAs
+      if constexpr (s == 0) load_w(P_, t + D);
+      if constexpr (s == 0) {
+        deq_piece(NX{}, I0{}, bnxt);
+        deq_piece(NX{}, I1{}, bnxt);
+      } else if constexpr (s == 1) {
+        deq_piece(NX{}, I2{}, bnxt);
+      } else {
+        deq_piece(NX{}, I3{}, bnxt);
+      }
+      mfmas(P_, s_, bf[s & 1]);
+      load_x(P_, t + D, s_);  // this sub-step's A fragments are consumed: refill for step t + D
+      fence();
+    };
+    sub(I0{});
+    sub(I1{});
+    sub(I2{});
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if constexpr (!(ABL & 16)) __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    read_b(bf[0], bnxt, 0);
+    fence();
+    mfmas(P_, I3{}, bf[1]);
+    load_x(P_, t + D, I3{});
+    fence();
+  };
+
+  int t = 0;
+  for (; t + D <= nk; t += D) {
+    step(I0{}, t);
+    step(I1{}, t + 1);
+    if constexpr (D > 2) step(I2{}, t + 2);
+    if constexpr (D > 3) step(I3{}, t + 3);
+  }
+  if (t < nk) step(I0{}, t);
+  if constexpr (D > 2)
+    if (t + 1 < nk) step(I1{}, t + 1);
+  if constexpr (D > 3)
+    if (t + 2 < nk) step(I2{}, t + 2);
+  bs_epilogue<C, MODE>(acc, w, mt, nt, split, M, out, outb, ldo, slab, glu);
 }
 
 // Tile id -> (n tile fastest, then m tile, then split).  Blocks are dealt round-robin over the 8
@@ -547,13 +749,17 @@ template <int ABL>
 __global__ __launch_bounds__(256, 1) void bsgemm_probe_kernel(QW w, const bf16* __restrict__ X, int ldx, int M,
                                                                int m_tiles, int n_tiles, int real,
                                                                bf16* __restrict__ outb) {
-  using C = BsCfg<64, 1, (ABL & 256) ? 4 : 3>;
-  constexpr int AB = ABL & ~256;
+  using C = BsCfg<64, (ABL & 512) ? 2 : 1, (ABL & 512) ? 2 : (ABL & 256) ? 4 : 3>;
+  constexpr int AB = ABL & ~(256 | 512);
   __shared__ __attribute__((aligned(1024))) uint8_t lds[C::LDS];
   if ((int)blockIdx.x >= real) return;
   const int tile = bs_tile_id(real);
-  bs_tile<FMT_Q4_K, C, 2, AB>(lds, w, tile / n_tiles, tile % n_tiles, 0, X, ldx, M, w.K >> 6, nullptr, outb,
-                                      w.N, 0, BsGlu{});
+  if constexpr (ABL & 8192)
+    bs_tile_xb<FMT_Q4_K, C, 2, (AB & ~8192)>(lds, w, tile / n_tiles, tile % n_tiles, 0, X, M, w.K >> 6, nullptr, outb,
+                                             w.N, 0, BsGlu{});
+  else
+    bs_tile<FMT_Q4_K, C, 2, AB>(lds, w, tile / n_tiles, tile % n_tiles, 0, X, ldx, M, w.K >> 6, nullptr, outb, w.N,
+                                0, BsGlu{});
 }
 
 // Two weights of one fused output (Q4_K q|k beside a Q6_K v): segment B's tiles follow A's.
@@ -743,9 +949,9 @@ extern "C" int la_bsgemm_glu(int fmt, const void* pa0, const void* pa1, const vo
 extern "C" int la_bsgemm_probe(int abl, const void* p0, const void* gsc, int N, int K, const void* X, int ldx, int M,
                                void* out, void* stream) {
   using namespace la;
-  using C = BsCfg<64, 1>;
+  const int BN = (abl & 512) ? 256 : 128;
   QW w{(const uint8_t*)p0, nullptr, (const uint8_t*)gsc, nullptr, N, K};
-  const int m_tiles = (M + C::BM - 1) / C::BM, n_tiles = (N + C::BN - 1) / C::BN, real = m_tiles * n_tiles;
+  const int m_tiles = (M + 255) / 256, n_tiles = (N + BN - 1) / BN, real = m_tiles * n_tiles;
   hipStream_t st = (hipStream_t)stream;
 #define BS_P(A)                                                                                          \
   case A:                                                                                                \
@@ -755,7 +961,8 @@ extern "C" int la_bsgemm_probe(int abl, const void* p0, const void* gsc, int N, 
   switch (abl) {
     BS_P(0) BS_P(1) BS_P(2) BS_P(4) BS_P(8) BS_P(12) BS_P(16) BS_P(32) BS_P(64) BS_P(128) BS_P(192) BS_P(254)
     BS_P(6) BS_P(14) BS_P(46) BS_P(17) BS_P(256) BS_P(260) BS_P(264) BS_P(272) BS_P(1024)
-    BS_P(1280) BS_P(2048) BS_P(2304)
+    BS_P(1280) BS_P(2048) BS_P(2304) BS_P(8192) BS_P(8448) BS_P(8704) BS_P(512) BS_P(8196) BS_P(8200)
+    BS_P(8208) BS_P(24576) BS_P(25088) BS_P(24580)
     default: return -1;
   }
 #undef BS_P

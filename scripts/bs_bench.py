@@ -138,14 +138,29 @@ def ablate(ms):
     p0, _, g = w.tile_planes()
     for M in ms:
         xp = (torch.randn(M, K + 64, device=DEV) * 0.5).to(torch.bfloat16)
+        xb = xp[:, :K].contiguous().view(M // 32, 32, K // 8, 8).permute(0, 2, 1, 3).contiguous()
         out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
         line = []
-        for abl, ldx in ((0, K), (2048, K), (256, K), (2304, K), (260, K), (264, K), (272, K), (4, K), (8, K),
-                         (12, K), (16, K), (1, K), (254, K)):
-            def fn(abl=abl, ldx=ldx):
-                rc = L.la_bsgemm_probe(abl, p0, g, N, K, xp.data_ptr(), ldx, M, out.data_ptr(), ops._stream())
+        ref = None
+        # codes repacked [N/32][K/64][32][32 B] for the 16384 probes
+        qb = w.planes[0].view(N // 32, 32, K // 64, 32).permute(0, 2, 1, 3).contiguous()
+        for abl, ldx in ((0, K + 64), (512, K + 64), (8192, 0), (8704, 0), (24576, 0), (25088, 0), (24580, 0), (8196, 0),
+                         (8200, 0), (8208, 0), (254, K + 64)):
+            src = xb if abl & 8192 else xp
+            def fn(abl=abl, ldx=ldx, src=src):
+                rc = L.la_bsgemm_probe(abl, qb.data_ptr() if abl & 16384 else p0, g, N, K, src.data_ptr(), ldx, M,
+                                       out.data_ptr(), ops._stream())
                 assert rc == 0, rc
-            line.append("abl%d%s %.0f" % (abl, "p" if ldx != K else "", timeit(fn)))
+            tt = timeit(fn)
+            if abl in (0, 256, 512, 8192, 8448, 8704, 24576, 25088):
+                fn()
+                torch.cuda.synchronize()
+                if ref is None:
+                    ref = out.float().clone()
+                err = (out.float() - ref).abs().max().item()
+                line.append("abl%d %.0f (diff %.2g)" % (abl, tt, err))
+            else:
+                line.append("abl%d %.0f" % (abl, tt))
         print(f"ablate M={M}: " + ", ".join(line), flush=True)
 
 

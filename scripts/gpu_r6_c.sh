@@ -1,0 +1,2 @@
+export PYTHONUNBUFFERED=1
+timeout -k 10 300 python -u scripts/bs_bench.py --abl --m 8192 256 > gpurun_out/r6c_abl.log 2>&1; cat gpurun_out/r6c_abl.log
