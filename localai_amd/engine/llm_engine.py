@@ -253,6 +253,7 @@ class LLMEngine:
         # tensor parallelism, all-greedy batches: graphs whose sampler is the distributed argmax
         # (TPInfo.argmax_cols) -- no full-vocabulary all-gather, no RCCL call in the graph
         self._graphs_tpg: Dict[int, tuple] = {}
+        self._graphs_tps: Dict[tuple, tuple] = {}   # (Bp, mirostat rows) -> distributed-sampler graph
         self.tracer = get_tracer()
         self._pcache = PromptCacheFiles()
         self._graph_pool = None
@@ -665,6 +666,7 @@ class LLMEngine:
             self._ar_err = 0
             self._graphs.clear()   # the captured decode graphs call the custom kernel
             self._graphs_tpg.clear()
+            self._graphs_tps.clear()
             self.tp.drop_custom_ar()
             raise CustomAllReduceTimeout("tensor-parallel custom all-reduce timed out on a late peer rank: the last "
                                          "step's results are invalid; the group continues on RCCL")
@@ -1049,6 +1051,25 @@ class LLMEngine:
                 rec = self.model.tp.all_gather_cols(rec)
             self._emit_run(reqs, hist, K, rec)
             return
+        if device_sampling and self._tp_sample_ok(reqs):
+            miro = any(r.params.mirostat == 2 for r in reqs)
+            g = self._graphs_tps.get((Bp, miro))
+            if g is None:
+                g = self._graphs_tps[(Bp, miro)] = self._capture(Bp, tp_sample=miro)
+            graph, st, _ = g
+            self._upload_step_inputs(st, reqs, Bp, tok, pos, slots, lens, bt, True)
+            for _ in range(K):
+                graph.replay()
+            hist = st["hist"][:K, :B].cpu().numpy()
+            if miro:
+                muh = st["mu"][:B].cpu().numpy()
+                for j, r in enumerate(reqs):
+                    r.mu = float(muh[j])
+            rec = st.get("rec")
+            if rec is not None:
+                rec = self.model.tp.all_gather_cols(rec)
+            self._emit_run(reqs, hist, K, rec)
+            return
         g = self._graphs.get(Bp)
         if g is None:
             g = self._graphs[Bp] = self._capture(Bp)
@@ -1324,10 +1345,32 @@ class LLMEngine:
                 return False
         return True
 
-    def _capture(self, Bp: int, tp_greedy: bool = False):
+    TP_SAMPLE = os.environ.get("LOCALAI_AMD_TP_SAMPLE", "1") == "1"
+
+    def _tp_sample_ok(self, reqs) -> bool:
+        """Tensor parallelism and every row within the distributed sampler's reach
+        (TPInfo.sample_cols): greedy, mirostat 2, or the standard chain with 1 <= top_k <=
+        TP_SAMPLE_C (tail-free / typical / top-p / min-p / temperature after it); penalties and
+        logit bias are applied to each rank's own columns.  LocalAI's defaults (temperature 0.9,
+        top-k 40, top-p 0.95, mirostat 2; core/config/backend_config.go:284-289) qualify.  Rows
+        outside (top_k 0 without mirostat, grammars, mirostat 1) keep the full-row gather."""
+        if self.tp.world < 2 or not self.TP_SAMPLE:
+            return False
+        for r in reqs:
+            p = r.params
+            if r.grammar is not None or p.mirostat == 1:
+                return False
+            if p.temperature > 0 and p.mirostat != 2 and not (1 <= p.top_k <= ops.TP_SAMPLE_C):
+                return False
+        return True
+
+    def _capture(self, Bp: int, tp_greedy: bool = False, tp_sample: Optional[bool] = None):
         """One hipGraph per padded batch size: forward + logit bias + sampler + advance.
         tp_greedy: this rank's vocabulary columns only, logit bias on them, and the exact
-        distributed argmax (TPInfo.argmax_cols) as the sampler."""
+        distributed argmax (TPInfo.argmax_cols) as the sampler.  tp_sample (True: with the
+        mirostat-2 phases): this rank's columns, bias + penalties on them, and the distributed
+        sampler (TPInfo.sample_cols)."""
+        tp_local = tp_greedy or tp_sample is not None
         dev = self.device
         MB = self.max_blocks
         cap = max(1, Bp * self.cfg.bias_capacity)
@@ -1371,11 +1414,13 @@ class LLMEngine:
         ws = ops.decode_workspace(Bp, self.model.Hq, self.model.Hkv, self.model.Dh, self.ctx, dev,
                                   self.cfg.block_size)
         bs = self.cfg.block_size
-        if tp_greedy:
+        if tp_local:
             vl = self.model.vocab_local
             st["tp_cols"] = (self.model.tp.rank * vl, vl)   # bias entries are translated to these columns
+        if tp_sample is not None:
+            st["tpsw"] = self.model.tp.sample_workspace(Bp, dev)
         if self.cfg.record_logits:
-            st["rec"] = torch.zeros(K, Bp, self.model.vocab_local if tp_greedy else self.model.hp.n_vocab,
+            st["rec"] = torch.zeros(K, Bp, self.model.vocab_local if tp_local else self.model.hp.n_vocab,
                                     dtype=torch.float32, device=dev)
 
         def body_tpg():
@@ -1384,6 +1429,20 @@ class LLMEngine:
                 st["rec"].index_copy_(0, st["step"][:1].long(), lg.float().unsqueeze(0))
             ops.logit_bias(lg, st["bias_rows"], st["bias_cols"], st["bias_vals"], st["bias_n"])
             st["next"].copy_(self.model.tp.argmax_cols(lg))
+            ops.decode_advance(st["next"], st["tokens"], st["pos"], st["lens"], st["slots"], st["bt"], bs,
+                               st["hist"], st["step"], st["prm"])
+            return lg
+
+        def body_tps():
+            lg = self.model.forward(fb, self.kv, attn_workspace=ws, local_logits=True)
+            if "rec" in st:
+                st["rec"].index_copy_(0, st["step"][:1].long(), lg.float().unsqueeze(0))
+            ops.logit_bias(lg, st["bias_rows"], st["bias_cols"], st["bias_vals"], st["bias_n"])
+            ops.penalties(lg, st["phist"], st["phl"], st["pen"], self.tokenizer.nl_id, st["pnl"],
+                          col0=st["tp_cols"][0])
+            self.model.tp.sample_cols(lg, st["prm_np"], st["prm"], st["mu"], st["next"], st["tpsw"],
+                                      mirostat=bool(tp_sample))
+            ops.penalty_push(st["next"], st["phist"], st["pcnt"], st["phl"], st["pcap"])
             ops.decode_advance(st["next"], st["tokens"], st["pos"], st["lens"], st["slots"], st["bt"], bs,
                                st["hist"], st["step"], st["prm"])
             return lg
@@ -1409,6 +1468,8 @@ class LLMEngine:
         s.wait_stream(torch.cuda.current_stream(dev))
         if tp_greedy:
             body = body_tpg  # noqa: F811
+        elif tp_sample is not None:
+            body = body_tps  # noqa: F811
         with torch.cuda.stream(s):
             for _ in range(2):  # warm up allocator / kernels outside the graph
                 body()

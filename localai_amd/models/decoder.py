@@ -135,6 +135,63 @@ class TPInfo:
         best = buf[..., 0].argmax(0, keepdim=True)                       # [1, B]: first max -> lowest rank
         return buf[..., 1].gather(0, best).squeeze(0).to(torch.int32)
 
+    def sample_workspace(self, B: int, device) -> dict:
+        """Exchange buffers of sample_cols for batches of B rows (allocated once per captured graph:
+        a replayed graph keeps using the same memory)."""
+        C, w = ops.TP_SAMPLE_C, self.world
+        f32 = dict(dtype=torch.float32, device=device)
+        return {"cand": torch.zeros(w, B, C, 2, **f32), "x1": torch.zeros(w, B, 3, **f32),
+                "x2": torch.zeros(w, B, **f32), "x3": torch.zeros(w, B, 2, **f32), "mu_tmp": torch.zeros(B, **f32),
+                "idx": torch.zeros(B, dtype=torch.int32, device=device)}
+
+    def _exchange(self, buf: torch.Tensor) -> None:
+        """Sum `buf` over the group, in place: every rank filled only its own slot, so the sum is
+        the concatenation of all slots.  The custom all-reduce when it takes the size (graph-
+        replayable, no RCCL call in a captured step), else the process group."""
+        if self.car is not None and self.car.supports(buf.view(-1)):
+            self.car.all_reduce(buf.view(-1))
+        else:
+            import torch.distributed as dist
+            dist.all_reduce(buf, group=self.group)
+
+    def sample_cols(self, t: torch.Tensor, prm_np, prm_dev: torch.Tensor, mu: torch.Tensor, out: torch.Tensor,
+                    ws: dict, mirostat: bool = True) -> torch.Tensor:
+        """The device sampler over vocabulary-parallel logits t [B, V / world] (this rank's columns,
+        bias and penalties applied), without gathering a row (ref: vLLM's TP sampling behind
+        backend/python/vllm/backend.py:102-103; SURVEY §2.9 distributed top-k):
+          * greedy and standard-chain rows (1 <= top_k <= TP_SAMPLE_C): every rank's top-C
+            candidates (value, id) -- together a superset of the global top-k, which is all the
+            chain after top-k looks at -- are exchanged in ONE sum all-reduce of [world, B, C, 2]
+            and the unchanged sampler kernel runs on the merged [B, world * C] rows (in global id
+            order, so its lowest-id tie breaks are the full row's); Philox stream as at TP=1;
+          * mirostat-2 rows: four phases with three [world, B, <=3] exchanges (local max / argmax /
+            sum-exp, kept mass per rank, the pick of the rank holding the draw), the mu update
+            computed alike on every rank.
+        Graph-capturable with the custom all-reduce (no RCCL call).  out: int32 [B] tokens."""
+        B, Vs = t.shape
+        base, w, C = self.rank * Vs, self.world, ops.TP_SAMPLE_C
+        cand = ws["cand"]
+        cand.zero_()
+        ops.tp_topc(t, C, base, cand[self.rank])
+        self._exchange(cand)
+        vals = cand[..., 0].permute(1, 0, 2).contiguous().view(B, w * C)   # unit column stride for the sampler
+        ids = cand[..., 1].permute(1, 0, 2).contiguous().view(B, w * C)
+        ops.sample(vals, prm_np, mu=ws["mu_tmp"], params_dev=prm_dev, out=ws["idx"])
+        out.copy_(ids.gather(1, ws["idx"].long().unsqueeze(1)).squeeze(1).to(torch.int32))
+        if mirostat:
+            x1, x2, x3 = ws["x1"], ws["x2"], ws["x3"]
+            x1.zero_()
+            x2.zero_()
+            x3.zero_()
+            ops.tp_mirostat(1, t, base, w, self.rank, prm_dev, mu, x1, x2, x3, x1[self.rank], None)
+            self._exchange(x1)
+            ops.tp_mirostat(2, t, base, w, self.rank, prm_dev, mu, x1, x2, x3, x2[self.rank], None)
+            self._exchange(x2)
+            ops.tp_mirostat(3, t, base, w, self.rank, prm_dev, mu, x1, x2, x3, x3[self.rank], None)
+            self._exchange(x3)
+            ops.tp_mirostat(4, t, base, w, self.rank, prm_dev, mu, x1, x2, x3, None, out)
+        return out
+
     def all_gather_cols(self, t: torch.Tensor) -> torch.Tensor:
         if self.world == 1:
             return t

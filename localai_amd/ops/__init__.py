@@ -74,6 +74,9 @@ def lib():
             "la_attn_prefill": [P, P, P, P, I, P, P, P, I, I, I, I, I, F, P, F, I, P],
             "la_sample": [P, LNG, I, I, P, P, P, P, P],
             "la_penalties": [P, LNG, I, P, I, P, P, I, P, P],
+            "la_penalties_cols": [P, LNG, I, P, I, P, P, I, P, I, I, P],
+            "la_tp_topc": [P, LNG, I, I, I, I, P, P],
+            "la_tp_mirostat": [I, P, LNG, I, I, I, I, I, P, P, P, P, P, P, P, P],
             "la_grammar_mask": [P, LNG, I, I, P, P, LNG, P],
             "la_grammar_advance": [P, P, P, I, I, P],
             "la_sample_row_bytes": [],
@@ -2190,10 +2193,13 @@ def grammar_advance(tok: torch.Tensor, slot: torch.Tensor, nxt: torch.Tensor) ->
 
 
 def penalties(logits: torch.Tensor, hist: torch.Tensor, hist_len: torch.Tensor, pen: torch.Tensor,
-              nl_token: int = -1, penalize_nl: Optional[torch.Tensor] = None):
-    """In-place repeat/frequency/presence penalties.  hist [B, L] i32 (-1 padded); pen [B,3]."""
+              nl_token: int = -1, penalize_nl: Optional[torch.Tensor] = None, col0: int = 0):
+    """In-place repeat/frequency/presence penalties.  hist [B, L] i32 (-1 padded); pen [B,3].
+    col0 > 0 or a narrower row: logits hold the vocabulary columns [col0, col0 + V) only (a
+    tensor-parallel shard); history tokens outside them are skipped."""
     B = logits.shape[0]
     if not logits.is_cuda:
+        V = logits.shape[1]
         for b in range(B):
             L = int(hist_len[b])
             rp, fp, pp = (float(x) for x in pen[b])
@@ -2203,17 +2209,40 @@ def penalties(logits: torch.Tensor, hist: torch.Tensor, hist_len: torch.Tensor, 
                     continue
                 if t == nl_token and penalize_nl is not None and not bool(penalize_nl[b]):
                     continue
+                if t < col0 or t - col0 >= V:
+                    continue
                 c = toks.count(t)
-                v = float(logits[b, t])
+                v = float(logits[b, t - col0])
                 if rp != 1:
                     v = v / rp if v > 0 else v * rp
                 v -= c * fp + (pp if c > 0 else 0)
-                logits[b, t] = v
+                logits[b, t - col0] = v
         return logits
-    _check(lib().la_penalties(logits.data_ptr(), logits.stride(0), B, hist.data_ptr(), hist.stride(0),
-                              hist_len.data_ptr(), pen.data_ptr(), nl_token, _ptr(penalize_nl), _stream()),
-           "la_penalties")
+    _check(lib().la_penalties_cols(logits.data_ptr(), logits.stride(0), B, hist.data_ptr(), hist.stride(0),
+                                   hist_len.data_ptr(), pen.data_ptr(), nl_token, _ptr(penalize_nl), col0,
+                                   logits.shape[1], _stream()), "la_penalties_cols")
     return logits
+
+
+# Tensor-parallel sampling over vocabulary shards (sampling.hip tp_* kernels; decoder.TPInfo.sample_cols)
+TP_SAMPLE_C = 64   # standard-chain candidates per rank and row: rows with 1 <= top_k <= TP_SAMPLE_C
+
+
+def tp_topc(logits: torch.Tensor, C: int, base: int, out: torch.Tensor) -> None:
+    """out [B, C, 2] f32 (this rank's slot of the exchange buffer): the C largest logits of each row
+    of the shard as (value, global id), in increasing id order."""
+    B, Vs = logits.shape
+    _check(lib().la_tp_topc(logits.data_ptr(), logits.stride(0), B, Vs, C, base, out.data_ptr(), _stream()),
+           "la_tp_topc")
+
+
+def tp_mirostat(phase: int, logits: torch.Tensor, base: int, world: int, rank: int, params_dev: torch.Tensor,
+                mu: torch.Tensor, x1: torch.Tensor, x2: torch.Tensor, x3: torch.Tensor, own: Optional[torch.Tensor],
+                out_tok: Optional[torch.Tensor]) -> None:
+    B, Vs = logits.shape
+    _check(lib().la_tp_mirostat(phase, logits.data_ptr(), logits.stride(0), B, Vs, base, world, rank,
+                                params_dev.data_ptr(), mu.data_ptr(), x1.data_ptr(), x2.data_ptr(), x3.data_ptr(),
+                                _ptr(own), _ptr(out_tok), _stream()), "la_tp_mirostat")
 
 
 def penalty_push(nxt: torch.Tensor, hist: torch.Tensor, cnt: torch.Tensor, hl: torch.Tensor,

@@ -483,7 +483,8 @@ __global__ __launch_bounds__(256) void penalties_kernel(float* __restrict__ logi
                                                         const int* __restrict__ hist, int hist_ld,
                                                         const int* __restrict__ hist_len,
                                                         const float* __restrict__ pen /* [B][3] */, int nl_token,
-                                                        const int* __restrict__ penalize_nl) {
+                                                        const int* __restrict__ penalize_nl, int col0 = 0,
+                                                        int ncols = 0x7fffffff) {
   const int b = blockIdx.x;
   const int L = hist_len[b];
   const float rp = pen[3 * b], fp = pen[3 * b + 1], pp = pen[3 * b + 2];
@@ -503,10 +504,11 @@ __global__ __launch_bounds__(256) void penalties_kernel(float* __restrict__ logi
     }
     if (!first) continue;
     if (t == nl_token && penalize_nl && !penalize_nl[b]) continue;
-    float l = row[t];
+    if (t < col0 || t - col0 >= ncols) continue;  // another rank's column
+    float l = row[t - col0];
     if (rp != 1.f) l = (l > 0.f) ? l / rp : l * rp;
     l -= (float)cnt * fp + (cnt > 0 ? pp : 0.f);
-    row[t] = l;
+    row[t - col0] = l;
   }
 }
 
@@ -522,6 +524,238 @@ __global__ void pen_push_kernel(const int* __restrict__ next, int B, int* __rest
   hist[(long)b * hist_ld + c % k] = next[b];
   cnt[b] = c + 1;
   len[b] = min(c + 1, k);
+}
+
+// ---------------------------------------------------------------- tensor-parallel sampling
+// Vocabulary-parallel logits: rank r holds columns [base, base + Vs) of every row.  Nothing here
+// gathers a full row; the ranks exchange per-row candidates / statistics through small fp32
+// buffers in which every rank writes only its own slot (the others are zero), so ONE sum
+// all-reduce -- the graph-replayable custom all-reduce -- is the exchange.
+
+// ascending sort of sh.cval/cidx[0..n) by token index (bitonic, pads at the end)
+LA_DEV void block_sort_idx(SmpShared& sh, int n) {
+  int P = 1;
+  while (P < n) P <<= 1;
+  for (int i = n + threadIdx.x; i < P; i += SMP_T) { sh.cval[i] = -INFINITY; sh.cidx[i] = 0x7fffffff; }
+  __syncthreads();
+  for (int k = 2; k <= P; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < P; i += SMP_T) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const bool asc = ((i & k) == 0);
+          const bool swap = asc ? (sh.cidx[i] > sh.cidx[ixj]) : (sh.cidx[i] < sh.cidx[ixj]);
+          if (swap) {
+            const float a = sh.cval[i]; sh.cval[i] = sh.cval[ixj]; sh.cval[ixj] = a;
+            const int t = sh.cidx[i]; sh.cidx[i] = sh.cidx[ixj]; sh.cidx[ixj] = t;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// Standard-chain candidates: the C largest logits of this rank's columns (ties: highest value,
+// then lowest id), written in increasing id order as (value, global id) pairs to out[b][C][2];
+// unused entries (-inf, 0).  Every rank's C >= top_k candidates together hold the global top-k,
+// and the chain after top-k (tail-free, typical, top-p, min-p, temperature, draw) sees only those.
+__global__ __launch_bounds__(SMP_T) void tp_topc_kernel(const float* __restrict__ logits, long ld, int Vs, int C,
+                                                        int base, float* __restrict__ out) {
+  __shared__ SmpShared sh;
+  const int b = blockIdx.x;
+  const float* row = logits + (long)b * ld;
+  float* o = out + (long)b * C * 2;
+  uint32_t key_c = 0;
+  if (C < Vs) key_c = radix_kth(row, Vs, C, sh);
+  if (threadIdx.x == 0) sh.count = 0;
+  __syncthreads();
+  row_foreach(row, Vs, [&](float v, int i) {
+    if (C >= Vs || fkey(v) >= key_c) {
+      const int slot = atomicAdd(&sh.count, 1);
+      if (slot < CAP) { sh.cval[slot] = v; sh.cidx[slot] = i; }
+    }
+  });
+  __syncthreads();
+  int n = min(sh.count, CAP);
+  __syncthreads();
+  if (n > C) {  // ties at the C-th value: keep the lowest ids
+    block_sort_desc(sh, n);
+    n = C;
+  }
+  block_sort_idx(sh, n);
+  for (int j = threadIdx.x; j < C; j += SMP_T) {
+    o[2 * j] = j < n ? sh.cval[j] : -INFINITY;
+    o[2 * j + 1] = j < n ? (float)(base + sh.cidx[j]) : 0.f;
+  }
+}
+
+// Mirostat 2 over vocabulary shards, four phases with a sum-exchange between each (x1, x2, x3:
+// [world][B][.] buffers, this rank's slot written): the same arithmetic as sample_kernel's
+// mirostat branch (temperature, keep e >= 2^-mu * Z or the argmax, renormalise, draw with the
+// row's Philox uniform, mu update), with the sums taken per rank and combined in rank order.
+// Rows without mirostat 2 are skipped by every phase.
+LA_DEV bool tp_miro_row(const SampleRow& P) { return P.mirostat == 2 && P.temp > 0.f; }
+
+// phase 1: local max, its (lowest) global id and Z_r = sum exp((v - m_r) / T)
+__global__ __launch_bounds__(SMP_T) void tp_miro1_kernel(const float* __restrict__ logits, long ld, int Vs,
+                                                         int base, const SampleRow* __restrict__ params,
+                                                         float* __restrict__ x1) {
+  __shared__ SmpShared sh;
+  const int b = blockIdx.x;
+  const SampleRow P = params[b];
+  if (!tp_miro_row(P)) return;
+  const float* row = logits + (long)b * ld;
+  float mv = -INFINITY;
+  int mi = 0x7fffffff;
+  row_foreach(row, Vs, [&](float v, int i) {
+    if (v > mv || (v == mv && i < mi)) { mv = v; mi = i; }
+  });
+  block_argmax(mv, mi, sh);
+  const float invT = 1.f / P.temp;
+  float z = 0.f;
+  row_foreach(row, Vs, [&](float v, int) { z += __expf((v - mv) * invT); });
+  z = block_sum<SMP_T>(z, sh.fred);
+  if (threadIdx.x == 0) {
+    x1[3 * b] = mv;
+    x1[3 * b + 1] = (float)(base + mi);
+    x1[3 * b + 2] = z;
+  }
+}
+
+struct TpMiro {
+  float M, g, Z, thr, invT;
+};
+
+LA_DEV TpMiro tp_miro_global(const float* X1, int world, int B, int b, float temp, float mu) {
+  TpMiro t;
+  t.invT = 1.f / temp;
+  t.M = -INFINITY;
+  t.g = 3.0e38f;
+  for (int r = 0; r < world; ++r) {
+    const float m = X1[((long)r * B + b) * 3], id = X1[((long)r * B + b) * 3 + 1];
+    if (m > t.M || (m == t.M && id < t.g)) { t.M = m; t.g = id; }
+  }
+  t.Z = 0.f;
+  for (int r = 0; r < world; ++r) {
+    const float* x = X1 + ((long)r * B + b) * 3;
+    if (x[0] > -INFINITY) t.Z += x[2] * __expf((x[0] - t.M) * t.invT);
+  }
+  t.thr = exp2f(-mu) * t.Z;
+  return t;
+}
+
+// phase 2: W_r = sum over this rank's kept tokens of e = exp((v - M) / T)
+__global__ __launch_bounds__(SMP_T) void tp_miro2_kernel(const float* __restrict__ logits, long ld, int Vs,
+                                                         int base, const SampleRow* __restrict__ params,
+                                                         const float* __restrict__ mu, const float* __restrict__ X1,
+                                                         int world, int B, float* __restrict__ x2) {
+  __shared__ SmpShared sh;
+  const int b = blockIdx.x;
+  const SampleRow P = params[b];
+  if (!tp_miro_row(P)) return;
+  const TpMiro t = tp_miro_global(X1, world, B, b, P.temp, mu[b]);
+  const float* row = logits + (long)b * ld;
+  const int gl = (int)t.g - base;  // the global argmax's local index (outside [0, Vs) elsewhere)
+  float w = 0.f;
+  row_foreach(row, Vs, [&](float v, int i) {
+    const float e = __expf((v - t.M) * t.invT);
+    if (e >= t.thr || i == gl) w += e;
+  });
+  w = block_sum<SMP_T>(w, sh.fred);
+  if (threadIdx.x == 0) x2[b] = w;
+}
+
+// phase 3: the rank whose kept mass holds the draw picks the token by an ordered scan
+__global__ __launch_bounds__(SMP_T) void tp_miro3_kernel(const float* __restrict__ logits, long ld, int Vs,
+                                                         int base, const SampleRow* __restrict__ params,
+                                                         const float* __restrict__ mu, const float* __restrict__ X1,
+                                                         const float* __restrict__ X2, int world, int rank, int B,
+                                                         float* __restrict__ x3) {
+  __shared__ SmpShared sh;
+  const int b = blockIdx.x;
+  const SampleRow P = params[b];
+  if (!tp_miro_row(P)) return;
+  const TpMiro t = tp_miro_global(X1, world, B, b, P.temp, mu[b]);
+  float zk = 0.f;
+  for (int r = 0; r < world; ++r) zk += X2[(long)r * B + b];
+  uint32_t rnd[4];
+  philox(P.seed, P.counter, rnd);
+  const float u01 = ((rnd[0] >> 8) + 0.5f) * (1.0f / 16777216.0f);
+  const float target = u01 * zk;
+  int rs = -1, last = -1;
+  float acc0 = 0.f, run = 0.f;
+  for (int r = 0; r < world; ++r) {
+    const float w = X2[(long)r * B + b];
+    if (w > 0.f) last = r;
+    if (rs < 0 && w > 0.f && target < run + w) { rs = r; acc0 = run; }
+    run += w;
+  }
+  if (rs < 0) {  // rounding put the draw past the last mass: the last rank with mass takes it
+    rs = last;
+    acc0 = 0.f;
+    for (int r = 0; r < last; ++r) acc0 += X2[(long)r * B + b];
+  }
+  if (rs != rank) return;
+  const float* row = logits + (long)b * ld;
+  const int gl = (int)t.g - base;
+  const int C = (Vs + SMP_T - 1) / SMP_T;
+  const int lo = threadIdx.x * C, hi = min(Vs, lo + C);
+  float part = 0.f;
+  int lastk = -1;
+  chunk_foreach(row, lo, hi, [&](float v, int i) {
+    const float e = __expf((v - t.M) * t.invT);
+    if (e >= t.thr || i == gl) { part += e; lastk = i; }
+    return true;
+  });
+  if (threadIdx.x == 0) {
+    sh.sel = -1;
+    sh.count = -1;
+  }
+  float tot;
+  float acc = acc0 + block_excl_scan(part, sh, &tot);  // (synchronises: the inits above are visible)
+  if (target >= acc && target < acc + part) {
+    chunk_foreach(row, lo, hi, [&](float v, int i) {
+      const float e = __expf((v - t.M) * t.invT);
+      if (!(e >= t.thr || i == gl)) return true;
+      acc += e;
+      if (target < acc) { sh.sel = i; return false; }
+      return true;
+    });
+  }
+  __syncthreads();
+  // no thread claimed it (rounding): the rank's last kept token
+  int lk = lastk;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) lk = max(lk, __shfl_xor(lk, o, 64));
+  if ((threadIdx.x & 63) == 0) atomicMax(&sh.count, lk);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int s = sh.sel >= 0 ? sh.sel : sh.count;
+    if (s >= 0) {
+      x3[2 * b] = (float)(base + s + 1);
+      x3[2 * b + 1] = __expf((row[s] - t.M) * t.invT);
+    }
+  }
+}
+
+// phase 4: every rank takes the picked token, its probability and the mu update
+__global__ void tp_miro4_kernel(const SampleRow* __restrict__ params, float* __restrict__ mu,
+                                const float* __restrict__ X2, const float* __restrict__ X3, int world, int B,
+                                int* __restrict__ out_tok) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const SampleRow P = params[b];
+  if (!tp_miro_row(P)) return;
+  float zk = 0.f, id = 0.f, es = 0.f;
+  for (int r = 0; r < world; ++r) {
+    zk += X2[(long)r * B + b];
+    id += X3[((long)r * B + b) * 2];
+    es += X3[((long)r * B + b) * 2 + 1];
+  }
+  const int tok = (int)id - 1;
+  out_tok[b] = tok;
+  if (tok >= 0 && zk > 0.f && es > 0.f) mu[b] = mu[b] - P.eta * (-log2f(es / zk) - P.tau);
 }
 
 }  // namespace la
@@ -556,8 +790,51 @@ extern "C" int la_grammar_advance(const int* tok, int* slot, const short* next, 
 extern "C" int la_penalties(float* logits, long ld, int B, const int* hist, int hist_ld, const int* hist_len,
                             const float* pen, int nl_token, const int* penalize_nl, void* stream) {
   hipLaunchKernelGGL(la::penalties_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, logits, ld, hist, hist_ld,
-                     hist_len, pen, nl_token, penalize_nl);
+                     hist_len, pen, nl_token, penalize_nl, 0, 0x7fffffff);
   return (int)hipGetLastError();
 }
 
 extern "C" int la_sample_row_bytes() { return (int)sizeof(la::SampleRow); }
+
+// Penalties on a vocabulary shard: history tokens outside [col0, col0 + ncols) are skipped and the
+// rest index logits[t - col0] (tensor-parallel rows hold only their columns).
+extern "C" int la_penalties_cols(float* logits, long ld, int B, const int* hist, int hist_ld, const int* hist_len,
+                                 const float* pen, int nl_token, const int* penalize_nl, int col0, int ncols,
+                                 void* stream) {
+  hipLaunchKernelGGL(la::penalties_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, logits, ld, hist, hist_ld,
+                     hist_len, pen, nl_token, penalize_nl, col0, ncols);
+  return (int)hipGetLastError();
+}
+
+extern "C" int la_tp_topc(const float* logits, long ld, int B, int Vs, int C, int base, float* out, void* stream) {
+  if (C < 1 || C > 1024 || Vs < 1) return -1;
+  hipLaunchKernelGGL(la::tp_topc_kernel, dim3(B), dim3(la::SMP_T), 0, (hipStream_t)stream, logits, ld, Vs, C, base,
+                     out);
+  return (int)hipGetLastError();
+}
+
+// phase 1..4 of the vocabulary-parallel mirostat 2 sampler (see tp_miro*_kernel); x1/x2/x3 are the
+// exchange buffers [world][B][3 | 1 | 2] after their all-reduce (phase p writes its own slot of
+// the next one: own1 / own2 / own3 = this rank's slot).
+extern "C" int la_tp_mirostat(int phase, const float* logits, long ld, int B, int Vs, int base, int world, int rank,
+                              const void* params, float* mu, const float* x1, const float* x2, const float* x3,
+                              float* own, int* out_tok, void* stream) {
+  using namespace la;
+  hipStream_t st = (hipStream_t)stream;
+  const SampleRow* P = (const SampleRow*)params;
+  switch (phase) {
+    case 1: hipLaunchKernelGGL(tp_miro1_kernel, dim3(B), dim3(SMP_T), 0, st, logits, ld, Vs, base, P, own); break;
+    case 2:
+      hipLaunchKernelGGL(tp_miro2_kernel, dim3(B), dim3(SMP_T), 0, st, logits, ld, Vs, base, P, mu, x1, world, B, own);
+      break;
+    case 3:
+      hipLaunchKernelGGL(tp_miro3_kernel, dim3(B), dim3(SMP_T), 0, st, logits, ld, Vs, base, P, mu, x1, x2, world,
+                         rank, B, own);
+      break;
+    case 4:
+      hipLaunchKernelGGL(tp_miro4_kernel, dim3((B + 255) / 256), dim3(256), 0, st, P, mu, x2, x3, world, B, out_tok);
+      break;
+    default: return -1;
+  }
+  return (int)hipGetLastError();
+}

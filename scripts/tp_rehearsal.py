@@ -38,17 +38,31 @@ def main():
     eng = LLMEngine(EngineConfig(**cfg), tp=tp, ctrl_group=ctrl)
     prompts = ["tensor parallel on one gpu", "second prompt"]
     n_tok = 12
-    sp = lambda: SamplingParams(max_tokens=n_tok, temperature=0.0, ignore_eos=True)  # noqa: E731
+    sampling = os.environ.get("TP_REHEARSAL_SAMPLING", "0") == "1"
+    if sampling:
+        # LocalAI's default sampler (temperature 0.9, top-k 40, top-p 0.95) on the first prompt,
+        # mirostat 2 on the second, seeded: the TP run must draw the TP=1 tokens
+        prompts = ["tensor parallel on one gpu", "mirostat prompt", "penalised prompt"]
+        kws = [dict(temperature=0.9, top_k=40, top_p=0.95, seed=1234),
+               dict(temperature=0.9, mirostat=2, mirostat_tau=5.0, mirostat_eta=0.1, seed=99),
+               dict(temperature=0.8, top_k=20, repeat_penalty=1.3, seed=7)]
+        sps = iter([SamplingParams(max_tokens=n_tok, ignore_eos=True, **k) for k in kws * 2])
+        sp = lambda: next(sps)  # noqa: E731
+    else:
+        sp = lambda: SamplingParams(max_tokens=n_tok, temperature=0.0, ignore_eos=True)  # noqa: E731
     if rank == 0:
         outs = [eng.generate(p, sp()) for p in prompts]
         tpg_graphs = len(eng._graphs_tpg)
+        tps_graphs = len(eng._graphs_tps)
         eng.shutdown()
         single = LLMEngine(EngineConfig(**cfg))
         refs = [single.generate(p, sp()) for p in prompts]
         print("TP texts", [o["text"] for o in outs], "single", [r["text"] for r in refs], flush=True)
         assert all(o["completion_tokens"] == n_tok for o in outs)
-        if graphs:
+        if graphs and not sampling:
             assert tpg_graphs > 0, "greedy TP decode did not run the distributed-argmax graph"
+        if graphs and sampling:
+            assert tps_graphs > 0, "sampled TP decode did not run the distributed-sampler graph"
         worst_cos, worst_rel, total = 1.0, 0.0, 0
         for o, r in zip(outs, refs):
             a_ids, b_ids = o["token_ids"], r["token_ids"]
@@ -68,8 +82,9 @@ def main():
             assert rows >= MIN_ROWS, f"only {rows} rows share a prefix with TP=1"
             total += rows
         assert tp.car is not None and not tp.car.timed_out(), "custom all-reduce unavailable or timed out"
-        print(f"TP_ROWS world={world} graphs={graphs} rows={total} worst_cos={worst_cos:.6f} "
-              f"worst_rel={worst_rel:.2e}", flush=True)
+        same = sum(int(o["token_ids"] == r["token_ids"]) for o, r in zip(outs, refs))
+        print(f"TP_ROWS world={world} graphs={graphs} sampling={sampling} rows={total} worst_cos={worst_cos:.6f} "
+              f"worst_rel={worst_rel:.2e} identical_streams={same}/{len(outs)}", flush=True)
         print("TP_OK", flush=True)
     else:
         eng.run_follower()
