@@ -63,6 +63,11 @@ def parse():
     ap.add_argument("--decode-steps", type=int, default=int(os.environ.get("BENCH_DECODE_STEPS", 0)),
                     help="device decode steps per host round trip (0: engine default)")
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--arrival-rate", type=float, default=float(os.environ.get("BENCH_ARRIVAL_RATE", 0)),
+                    help="open-loop Poisson arrivals at this many requests/s (HTTP mode) instead of "
+                         "synchronised waves; reports tok/s, p50/p99 TTFT and p50/p99 inter-token latency")
+    ap.add_argument("--requests", type=int, default=int(os.environ.get("BENCH_REQUESTS", 0)),
+                    help="requests of the open-loop run (default: concurrency x steps)")
     ap.add_argument("--server", default=os.environ.get("BENCH_SERVER", "native"), choices=["native", "uvicorn"])
     ap.add_argument("--clients", type=int, default=int(os.environ.get("BENCH_CLIENTS", 4)),
                     help="load-generator processes (separate from the server process)")
@@ -255,12 +260,16 @@ def main():
 
     for w in range(args.warmup):
         wave(-1 - w)
+    if args.arrival_rate > 0 and args.mode == "http" and n_rep == 1 and rank == 0:
+        return open_loop(args, eng, runner, msgs)
     sync()
     lbarrier()
     sync()
     t0 = time.perf_counter()
     ttfts, tokens = [], 0
     ev0 = getattr(runner, "events", None)
+    for k in ("merged", "bad", "short", "split", "tail"):   # counters at the start of the timed waves
+        setattr(runner, f"_{k}0", getattr(runner, k, 0))
     for s_ in range(args.steps):
         tt, nt = wave(s_)
         ttfts += tt
@@ -273,11 +282,21 @@ def main():
     # fixes every request at max_tokens, and each generated token with non-empty text arrives as
     # its own SSE event (counted by the clients on the wire)
     stream_check = None
+    stream_bad = False
     if ev0 is not None:
+        # per request, on the wire: every chunk carries the running usage, so the events plus the
+        # tokens whose text arrived inside a later event (held-back partial UTF-8) must add up to
+        # the reported count, and each request must report exactly max_tokens (ignore_eos)
         expect = args.steps * len(msgs) * args.max_tokens
         events = runner.events - ev0
-        stream_check = {"expected_tokens": expect, "reported_tokens": tokens, "streamed_events": events}
-        if tokens != expect or events < 0.9 * tokens:
+        merged = getattr(runner, "merged", 0) - getattr(runner, "_merged0", 0)
+        d = {k: getattr(runner, k, 0) - getattr(runner, f"_{k}0", 0) for k in ("bad", "short", "split", "tail")}
+        stream_check = {"expected_tokens": expect, "reported_tokens": tokens, "streamed_events": events,
+                        "merged_tokens": merged, "split_events": d["split"], "tail_tokens": d["tail"],
+                        "bad_streams": d["bad"], "short_requests": d["short"]}
+        stream_bad = (tokens != expect or events - d["split"] + merged + d["tail"] != tokens or d["bad"]
+                      or d["short"])
+        if stream_bad:
             print(f"bench: stream check FAILED {stream_check}", file=sys.stderr, flush=True)
 
     all_ttft, tot_tokens, max_el = ttfts, tokens, elapsed
@@ -328,6 +347,8 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    if stream_bad:
+        sys.exit(3)
 
 
 def gateway_dp(args, eng, loadgen, rank, world, ctl, t_gen, t_load, t_capture):
@@ -378,6 +399,8 @@ def gateway_dp(args, eng, loadgen, rank, world, ctl, t_gen, t_load, t_capture):
     t0 = time.perf_counter()
     ttfts, tokens = [], 0
     ev0 = getattr(runner, "events", None)
+    for k in ("merged", "bad", "short", "split", "tail"):   # counters at the start of the timed waves
+        setattr(runner, f"_{k}0", getattr(runner, k, 0))
     for s_ in range(args.steps):
         tt, nt = wave(s_)
         ttfts += tt
@@ -447,6 +470,39 @@ class EngineRunner:
         pass
 
 
+def open_loop(args, eng, runner, msgs):
+    """Open-loop serving measurement: requests arrive as a Poisson process at args.arrival_rate
+    (seeded), each with its own prompt; tokens/s over the whole run, TTFT and per-token
+    inter-token-latency percentiles (SURVEY §3.2 TTFT; the reference streams one SSE event per
+    token, core/http/endpoints/openai/chat.go:463-508)."""
+    import numpy as np
+    n = args.requests or args.concurrency * max(1, args.steps)
+    rng = np.random.default_rng(20261018)
+    offs = np.cumsum(rng.exponential(1.0 / args.arrival_rate, size=n)).tolist()
+    contents = [f"(arrival {i}) " + msgs[i % len(msgs)] for i in range(n)]
+    t0 = time.perf_counter()
+    ttft, tokens = runner.wave(contents, offsets=offs)
+    el = time.perf_counter() - t0
+    w = runner.lg.last_wire
+    gaps = sorted(w["gaps_ms"])
+    out = {"metric": "open-loop Poisson arrivals, streamed /v1/chat/completions", "rate_rps": args.arrival_rate,
+           "requests": n, "tokens_per_s": round(tokens / el, 1), "elapsed_s": round(el, 2),
+           "p50_ttft_ms": round(percentile(ttft, 50) * 1e3, 1), "p99_ttft_ms": round(percentile(ttft, 99) * 1e3, 1),
+           "p50_itl_ms": round(percentile(gaps, 50), 2) if gaps else None,
+           "p99_itl_ms": round(percentile(gaps, 99), 2) if gaps else None,
+           "stream_check": {"reported_tokens": tokens, "expected_tokens": n * args.max_tokens,
+                            "streamed_events": w["events"], "merged_tokens": w["merged"],
+                            "split_events": w["split"], "tail_tokens": w["tail"], "bad_streams": w["bad"]},
+           "heuristics": {"admission_window_ms": float(os.environ.get("LOCALAI_AMD_ADMIT_WINDOW_MS",
+                                                                      eng.cfg.admission_window_ms)),
+                          "prefill_first_ms": float(os.environ.get("LOCALAI_AMD_PREFILL_FIRST_MS",
+                                                                   eng.cfg.prefill_first_ms))},
+           "config": {"model": MODEL_NAMES.get(args.preset, args.preset), "prompt_tokens": args.prompt_len,
+                      "max_tokens": args.max_tokens}}
+    print(json.dumps(out), flush=True)
+    runner.close()
+
+
 class HttpRunner:
     """Real gateway over HTTP: the FastAPI app on the native server (or uvicorn), driven by
     out-of-process aiohttp SSE clients."""
@@ -480,10 +536,16 @@ class HttpRunner:
         self.lg = loadgen
         self.url = f"http://127.0.0.1:{self.port}/v1/chat/completions"
 
-    def wave(self, contents):
+    def wave(self, contents, offsets=None):
         r = self.lg.wave(self.url, self.model_name, contents, self.args.max_tokens,
-                         extra={"temperature": 0, "ignore_eos": True, "mirostat": 0})
+                         extra={"temperature": 0, "ignore_eos": True, "mirostat": 0}, offsets=offsets)
         self.events = getattr(self, "events", 0) + getattr(self.lg, "last_events", 0)
+        w = getattr(self.lg, "last_wire", None) or {}
+        for k in ("merged", "bad", "split", "tail"):
+            setattr(self, k, getattr(self, k, 0) + w.get(k, 0))
+        # ignore_eos: every request must stream exactly max_tokens
+        self.short = getattr(self, "short", 0) + sum(1 for v in getattr(self.lg, "last_per", [])
+                                                      if v != self.args.max_tokens)
         return r
 
     def replica_stats(self):

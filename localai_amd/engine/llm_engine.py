@@ -94,6 +94,13 @@ class EngineConfig:
     # batch; a running stream (rows past their first token) keeps prefill and decode mixed.
     # 2 s covers a Mixtral-8x7B C=256 burst (r5_k2_mx_*.log); 0 disables
     prefill_first_ms: float = 2000.0
+    # ... where a burst is the requests of an idle -> busy transition plus every later arrival
+    # within burst_gap_ms of the burst's previous one (a synchronised client wave lands 0.3 ms
+    # apart; open-loop arrivals at 90 req/s average 11 ms apart and never form a long burst)
+    burst_gap_ms: float = 5.0
+    # while new prompts wait or are mid-prefill, a decode run holds at most this many ms of device
+    # steps (their admission waits for the run); 0: one step per round trip
+    admit_budget_ms: float = 25.0
     draft_model: str = ""             # speculative decoding: draft LM GGUF (engine/speculative.DraftModel)
     quantization: str = ""            # HF checkpoints: load-time quantisation (bnb_4bit / bnb_8bit / ...)
     draft_max_seqs: int = 16          # draft-model KV cache capacity in sequences of context_size
@@ -128,6 +135,7 @@ class Request:
     stream: object = None
     arrival: float = field(default_factory=time.perf_counter)
     first_token_t: float = 0.0
+    burst: bool = False      # member of the burst that woke the engine (_defer_decode)
     done: bool = False
     n_prompt: int = 0
     n_gen: int = 0
@@ -249,6 +257,8 @@ class LLMEngine:
         self._wake = threading.Event()
         # diagnostics (bench.py BENCH_ARRIVALS=1): perf_counter of every add_request and, per idle ->
         # busy transition, (time the admission window closed, requests waiting then)
+        self._burst_last = 0.0    # arrival time of the current burst's latest member (_defer_decode)
+        self._step_ms = 8.0       # EMA of one device decode step (_lookahead's admission budget)
         self.arrival_log: Optional[list] = None
         self.admit_log: Optional[list] = None
         self._thread: Optional[threading.Thread] = None
@@ -508,12 +518,15 @@ class LLMEngine:
             if not worked:
                 self._wake.wait(0.05)
                 self._wake.clear()
-                if self.cfg.admission_window_ms > 0 and not self.requests and not self._inbox.empty():
+                if self._admit_window_ms() > 0 and not self.requests and not self._inbox.empty():
                     self._admit_burst()
+
+    def _admit_window_ms(self) -> float:
+        return float(os.environ.get("LOCALAI_AMD_ADMIT_WINDOW_MS", self.cfg.admission_window_ms))
 
     def _admit_burst(self):
         """Idle -> busy: let a burst of arrivals land before scheduling (see EngineConfig)."""
-        t_end = time.perf_counter() + self.cfg.admission_window_ms / 1e3
+        t_end = time.perf_counter() + self._admit_window_ms() / 1e3
         quiet = self.cfg.admission_quiet_ms / 1e3
         close = int(os.environ.get("LOCALAI_AMD_ADMIT_TOKENS", self.cfg.admission_close_tokens))
         if close < 0:
@@ -610,6 +623,8 @@ class LLMEngine:
                     self._run_decode(plan, K)
             t1 = time.perf_counter()
             self.metrics["decode_s"] += t1 - t0
+            # per-device-step time of decode runs (EMA), for the admission budget of _lookahead
+            self._step_ms = 0.8 * self._step_ms + 0.2 * (t1 - t0) * 1e3 / max(1, K)
             if tr is not None:
                 tr.complete("decode", t0, t1, batch=len(d_ids), device_steps=K)
             did = True
@@ -749,6 +764,14 @@ class LLMEngine:
             n = self._pcache.ensure_loaded(self, r.params.prompt_cache_path)
             if n:
                 log.info("prompt cache %s: %d tokens of KV restored", r.params.prompt_cache_path, n)
+        # burst membership (_defer_decode): the requests of an idle -> busy transition, and then
+        # each one that arrived within burst_gap_ms of the burst's previous member
+        if not self.requests:
+            r.burst = True
+        elif self._burst_last > 0 and r.arrival - self._burst_last <= self.cfg.burst_gap_ms / 1e3:
+            r.burst = True
+        if r.burst:
+            self._burst_last = max(self._burst_last, r.arrival)
         self.requests[r.id] = r
         max_new = r.params.max_tokens if r.params.max_tokens > 0 else self.ctx
         self.sched.add(r.id, r.prompt, max_new)
@@ -888,16 +911,19 @@ class LLMEngine:
     k1_reasons: "collections.Counter"   # why a decode step ran one device step (diagnostics)
 
     def _defer_decode(self) -> bool:
-        """EngineConfig.prefill_first_ms: True while a burst is being prefilled (the native
-        scheduler then plans prefill only, when any prefill work is left)."""
+        """EngineConfig.prefill_first_ms: True while the burst that woke an idle engine is being
+        prefilled (the native scheduler then plans prefill only, when any prefill work is left).
+        Only members of that burst (EngineConfig.burst_gap_ms) keep it going: under steady open-
+        loop arrivals a later request never extends the deferral, so the burst's rows start
+        decoding as soon as the burst itself is prefilled (profiles/r6_arrivals.md)."""
         ms = float(os.environ.get("LOCALAI_AMD_PREFILL_FIRST_MS", self.cfg.prefill_first_ms))
         if ms <= 0 or self.tp.world > 1:
             return False
         oldest = None
-        pending = self.sched.num_waiting > 0
+        pending = False
         for r in self.requests.values():
             if r.n_gen == 0:
-                pending = True
+                pending = pending or r.burst
             elif r.n_gen > 1 or not r.first_token_t:
                 return False  # a decoding stream: keep it moving
             elif oldest is None or r.first_token_t < oldest:
@@ -913,17 +939,31 @@ class LLMEngine:
             return 1
         s = self.sched
         why = self.k1_reasons
+        # new prompts waiting or mid-prefill: they are admitted at the next host round trip, so a
+        # run is capped at admit_budget_ms of device steps (one step at the old default of 0):
+        # under steady open-loop arrivals some prompt is nearly always waiting, and one device step
+        # per round trip left the batch host-bound (profiles/r6_arrivals.md)
+        budget = float(os.environ.get("LOCALAI_AMD_ADMIT_BUDGET_MS", self.cfg.admit_budget_ms))
+        k_admit = max(1, min(K, int(budget / max(self._step_ms, 0.5)))) if budget > 0 else 1
         if s.num_waiting > 0 and s.num_running < self.cfg.max_num_seqs:
             why["admit"] += 1
-            return 1  # admit new prompts promptly
+            if k_admit <= 1:
+                return 1  # admit new prompts promptly
+            K = k_admit
         if len(self.requests) >= self.cfg.wide_batch and s.num_waiting == 0:
             K = max(K, self.cfg.decode_steps_wide)
         rem_tok, rem_ctx = 1, K
         riders = cons = unsure = 0
         for r in self.requests.values():
-            if r.n_gen == 0 or self._needs_host_sampler(r):
-                why["prefill" if r.n_gen == 0 else "host_sampler"] += 1
-                return 1  # prefill in flight, or a host-side sampler feature
+            if self._needs_host_sampler(r):
+                why["host_sampler"] += 1
+                return 1  # a host-side sampler feature
+            if r.n_gen == 0:
+                if k_admit <= 1:
+                    why["prefill"] += 1
+                    return 1  # prefill in flight
+                K = min(K, k_admit)
+                continue
             if r.grammar is not None and not self._grammar_ready(r):
                 if not self._grammar_slot_cached(r):
                     why["grammar_no_mask"] += 1

@@ -37,9 +37,10 @@ TP_OVERLAP_ROWS = int(os.environ.get("LOCALAI_AMD_TP_OVERLAP_ROWS", "1024"))
 TP_OVERLAP_CHUNKS = int(os.environ.get("LOCALAI_AMD_TP_OVERLAP_CHUNKS", "4"))
 # MoE decode batches route with the fused router kernel (moe.hip); =1 falls back to the torch ops
 FUSED_ROUTER_OFF = os.environ.get("LOCALAI_AMD_FUSED_ROUTER_OFF", "0") == "1"
-# prefill chunks of at least this many tokens run each expert as a dense GEMM over its gathered
-# rows (~T * topk / E rows: the library / tile prefill path, weights dequantised once per expert)
-# instead of the decode-shaped grouped kernel, which streams an expert's weights once per 64 rows
+# prefill chunks of at least this many tokens whose experts the grouped bs tile cannot run
+# (ops.moe_bs_ok: formats / shapes) run each expert as a dense GEMM over its gathered rows (~T *
+# topk / E rows: the library prefill path, weights dequantised once per expert, one host read of
+# the grouping) instead of the decode-shaped grouped kernel, which streams weights once per 64 rows
 MOE_DENSE_MIN_T = int(os.environ.get("LOCALAI_AMD_MOE_DENSE_MIN_T", "1024"))
 
 _ACT = {"swiglu": ops.ACT_SWIGLU, "gelu": ops.ACT_GELU, "geglu": ops.ACT_GEGLU}
@@ -620,7 +621,8 @@ class DecoderModel:
         T = xn.shape[0]
         El, base = self.E_local, self.ep_base
         if (L.moe_gu is not None and xn.is_cuda and not FUSED_ROUTER_OFF and L.experts is not None
-                and T >= MOE_DENSE_MIN_T and not torch.cuda.is_current_stream_capturing()):
+                and T >= MOE_DENSE_MIN_T and not torch.cuda.is_current_stream_capturing()
+                and not ops.moe_bs_ok(L.moe_gu, L.moe_down, T)):
             return self._moe_dense_prefill(L, xn, routed)
         if L.moe_gu is not None and xn.is_cuda and not FUSED_ROUTER_OFF:
             # any batch: one fused router launch (softmax, top-k, renorm, EP remap) feeds the
@@ -639,7 +641,12 @@ class DecoderModel:
                     d = ops.Partial((ops.reduce(d) + self._shared_expert(L, xn)).unsqueeze(0))
                 return self._row_parallel_out(d, None)
             order, off = ops.moe_route(ids, El + 1 if self.ep else El)
-            if ops.moe32_ok(L.moe_gu, L.moe_down, T):
+            if ops.moe_bs_ok(L.moe_gu, L.moe_down, T):
+                # prefill chunks: the grouped shared-dequant-image tiles, 256 routed rows per weight
+                # stream, one launch per projection for any routing (no host read of `off`)
+                h = ops.moe_glu_bs(xn, L.moe_gu, order, off, k, T)
+                d = ops.moe_down_bs(h, L.moe_down, order, off, k, T, wts, zero=self.ep)
+            elif ops.moe32_ok(L.moe_gu, L.moe_down, T):
                 # wide batch: 32x32x16 grouped tiles, SwiGLU fused into the gate|up epilogue
                 h = ops.moe_glu32(xn, L.moe_gu, order, off, k, T)
                 d = ops.moe_down32(h, L.moe_down, order, off, k, T, wts, zero=self.ep)
@@ -868,12 +875,19 @@ class DecoderModel:
         dev = torch.device("cpu")
         t = torch.tensor(tokens, dtype=torch.long)
         Tn = len(tokens)
-        x = self.tok_embd.dequant_f32().to(dev)[t] if self.tok_embd.ref is not None else \
-            self.tok_embd.materialize_bf16().float().cpu()[t]
-        x = x * hp.embed_scale
+        # dequantised fp32 host copies are kept across calls (an oracle checks hundreds of rows;
+        # re-dequantising every weight per call dominated test_headline_path_against_fp32_oracle)
+        cache = self.__dict__.setdefault("_oracle_w", {})
 
         def deq(w):
-            return (w.ref if w.ref is not None else w.materialize_bf16().float()).cpu()
+            if w.ref is not None:
+                return w.ref.cpu()
+            if id(w) not in cache:
+                cache[id(w)] = (w, w.materialize_bf16().float().cpu())
+            return cache[id(w)][1]
+
+        x = self.tok_embd.dequant_f32().to(dev)[t] if self.tok_embd.ref is not None else deq(self.tok_embd)[t]
+        x = x * hp.embed_scale
 
         def norm(x, w, b):
             if self.norm_mode == 0:

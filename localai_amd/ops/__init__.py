@@ -97,13 +97,11 @@ def lib():
             "la_qgemm32_2": [I, P, P, P, I, I, P, P, P, I, I, P, I, I, I, P, I, LNG, I, I, P],
             "la_qgemm32_glu": [I, P, P, P, I, P, P, P, I, I, I, P, I, I, P, I, I, I, P],
             "la_qgemm32_probe": [I, I, P, P, I, I, P, I, I, P, P],
-            "la_gemm_pp": [I, P, P, P, I, I, P, I, I, I, P, I, LNG, I, P],
             "la_attn_dense": [P, LNG, P, LNG, P, LNG, P, LNG, P, I, P, I, I, I, F, P],
-            "la_gemm_pp2": [I, P, P, P, I, I, P, P, P, I, I, P, I, I, I, P, I, LNG, I, P],
-            "la_gemm_pp_glu": [I, P, P, P, I, P, P, P, I, I, I, P, I, I, P, I, I, P],
             "la_bsgemm": [I, P, P, P, I, I, P, I, I, I, P, I, LNG, I, I, P],
             "la_bsgemm2": [I, P, P, P, I, I, P, P, P, I, I, P, I, I, I, P, I, LNG, I, I, P],
             "la_bsgemm_glu": [I, P, P, P, I, P, P, P, I, I, I, P, I, I, P, I, I, I, P],
+            "la_bsmoe": [I, I, P, I, I, I, P, P, I, P, I, I, I, P, P, I, LNG, I, I, P],
             "la_decode_advance": [P, P, P, P, P, P, I, I, I, P, I, P, P, P],
             "la_img_resample_h": [P, I, I, P, I, P, P, I, P],
             "la_img_resample_v_tiles": [P, I, I, P, P, I, I, I, I, I, I, I, P, P, P, P, P],
@@ -132,8 +130,6 @@ def lib():
         if mt:
             a, b = (int(v) for v in mt.split(","))
             _check(L.la_moe_tune(a, b), "la_moe_tune")
-        if os.environ.get("LOCALAI_AMD_MOE_GEMV_VAR") and hasattr(L, "la_moe_gemv_variant"):
-            _check(L.la_moe_gemv_variant(int(os.environ["LOCALAI_AMD_MOE_GEMV_VAR"])), "la_moe_gemv_variant")
         if os.environ.get("LOCALAI_AMD_DEC_ONE_PART") and hasattr(L, "la_dec_one_part"):
             _check(L.la_dec_one_part(int(os.environ["LOCALAI_AMD_DEC_ONE_PART"])), "la_dec_one_part")
         _LIB = L
@@ -439,28 +435,11 @@ def _gemv_splits(ws, K: int, M: int) -> int:
     return S
 
 
-# split-K partials of the decode GEMV summed inside the kernel (gemv_dp4.hip gv_reduce): the
-# consumers -- add_norm, the next GEMV's activation / norm prologue -- read ONE slab.  Off: every
-# workgroup's agent-scope release writes back its XCD's L2 before the ticket, and at ~1000
-# workgroups per GEMV that costs more than the slab reads it saves -- engine C=1 260.9 vs 436.4
-# tok/s, C=2 304.5 vs 727.4 (gpurun_out/r5_c*_red.log vs *_nored.log)
-GEMV_REDUCE = os.environ.get("LOCALAI_AMD_GEMV_REDUCE", "0") == "1"
-_GV_TICKETS: dict = {}
-
-
-def _gv_tickets(dev: torch.device) -> torch.Tensor:
-    t = _GV_TICKETS.get(dev)
-    if t is None:
-        t = _GV_TICKETS[dev] = torch.zeros(int(lib().la_gv_max_tickets()), dtype=torch.int32, device=dev)
-    return t
-
-
 def gemv_dp4(x: Optional[torch.Tensor], ws: Sequence[QWeight], S: int, out: torch.Tensor,
-             act_src: Optional[Partial] = None, act_mode: int = 0, reduce_splits: bool = False) -> None:
+             act_src: Optional[Partial] = None, act_mode: int = 0) -> None:
     """out[S, M, sum(N)] = split-K partials of x @ [W0; W1; ...]^T from the int8-dot decode GEMV,
     up to 3 weights (mixed Q4_K / Q6_K, same K) per launch.  With act_src (fp32 gate|up slabs)
-    x = act(act_src) is formed inside the GEMV prologue instead of being read.  reduce_splits:
-    the S partials are summed in the kernel into out[0] (the result is out[:1])."""
+    x = act(act_src) is formed inside the GEMV prologue instead of being read."""
     M = out.shape[1]
     K = ws[0].K
     a = (None, 0, 0, None) if act_src is None else act_src.src_args()
@@ -482,10 +461,7 @@ def gemv_dp4(x: Optional[torch.Tensor], ws: Sequence[QWeight], S: int, out: torc
         Ns = (ctypes.c_int * n)(*[w.N for w in seg])
         args = (n, fmts, planes, Ns, K, None if x is None else x.data_ptr(), K, M, S, out.data_ptr() + col * 4,
                 Ntot, M * Ntot, a[0], a[1], a[2], a[3], act_mode)
-        if reduce_splits and S > 1:
-            _check(lib().la_qgemv_dp4_red(*args, _gv_tickets(out.device).data_ptr(), _stream()), "la_qgemv_dp4_red")
-        else:
-            _check(lib().la_qgemv_dp4(*args, _stream()), "la_qgemv_dp4")
+        _check(lib().la_qgemv_dp4(*args, _stream()), "la_qgemv_dp4")
         col += sum(w.N for w in seg)
 
 
@@ -783,9 +759,10 @@ GQ_TILES = {0: (256, 256), 1: (256, 128), 2: (128, 256), 3: (128, 128), 4: (256,
             10: (256, 256), 11: (256, 128), 13: (128, 128), 16: (256, 256), 17: (128, 256)}
 # LOCALAI_AMD_TILE_GEMM=0 restores the round-2 path (hipBLASLt on bf16 weight copies)
 TILE_GEMM = os.environ.get("LOCALAI_AMD_TILE_GEMM", "1") == "1"
-# M > MID_MAX_M (prefill chunks): "blas" = dequantise into a scratch buffer + library GEMM, "pp" =
-# gemm_pp.hip (in-kernel dequant, no bf16 copy), "tile" = gemm_q.hip.  "blas" stays the default:
-# it is still 1.0-1.4x faster than gemm_pp at M = 2048 / 8192 (profiles/r5_prefill_gemm.md)
+# M > MID_MAX_M (prefill chunks): "blas" = dequantise into a scratch buffer + library GEMM, "tile" =
+# gemm_q.hip.  "blas" stays the default: the in-kernel-dequant MFMA GEMMs (gemm_bs.hip, and round
+# 5's gemm_pp.hip before it) top out near 1.0 PF/s against hipBLASLt's 1.3 at M = 8192
+# (profiles/r6_gemm_bs.md, r5_prefill_gemm.md)
 PREFILL_GEMM = os.environ.get("LOCALAI_AMD_PREFILL_GEMM", "blas")
 
 
@@ -907,71 +884,6 @@ def _run_bs_glu(x, pair, F: int, mode: int, var: int, out) -> None:
                                mode, var, _stream()), "la_bsgemm_glu")
 
 
-# Prefill GEMM (gemm_pp.hip): 256 x 256 ping-pong MFMA tiles with the GGUF dequantisation in the
-# kernel (Q4_K, Q6_K, bf16 weights); no bf16 weight copy, no library GEMM.
-PP_FMTS = (FMT_Q4_K, FMT_Q6_K, FMT_BF16)
-
-
-def pp_ok(ws: Sequence[QWeight], K: int, S: int = 1) -> bool:
-    """Can gemm_pp.hip run these weights (one launch per weight, or one for a two-weight pair)."""
-    kt = K // 64
-    if K % 256 or kt % S or (kt // S) % 4:
-        return False
-    if not all(w.fmt in PP_FMTS and w.K == K and w.planes[0] is not None for w in ws):
-        return False
-    return len(ws) <= 2 or all(w.fmt == ws[0].fmt for w in ws)
-
-
-def pp_splits(M: int, Ntot: int, K: int) -> int:
-    """Split-K so the grid covers the 256 CUs at least once (prefill chunks of 1-2k rows on the
-    4096-wide projections); each split keeps an even number of 64-deep K-tiles."""
-    tiles = -(-M // 256) * -(-Ntot // 256)
-    kt = K // 64
-    S = 1
-    while tiles * S < 224 and kt % (2 * S) == 0 and (kt // (2 * S)) % 4 == 0 and kt // (2 * S) >= 16:
-        S *= 2
-    return S
-
-
-def _pp_planes(w: QWeight):
-    if w.fmt == FMT_BF16:
-        return _ptr(w.planes[0]), None, None
-    return w.tile_planes()
-
-
-def _run_pp(x, ws, S, out, Ntot):
-    """out: fp32 slabs [S, M, Ntot], or a bf16 [M, Ntot] matrix (S == 1).  Two weights of one
-    output run as ONE launch."""
-    M, K = x.shape
-    bf = out.dtype == torch.bfloat16
-    esz = 2 if bf else 4
-    slab = 0 if bf else M * Ntot
-    if len(ws) == 2 and (ws[0].fmt, ws[1].fmt) in _PP2_PAIRS:
-        a0, a1, ag = _pp_planes(ws[0])
-        b0, b1, bg = _pp_planes(ws[1])
-        _check(lib().la_gemm_pp2(ws[0].fmt, a0, a1, ag, ws[0].N, ws[1].fmt, b0, b1, bg, ws[1].N, K, x.data_ptr(), K,
-                                 M, S, out.data_ptr(), Ntot, slab, int(bf), _stream()), "la_gemm_pp2")
-        return
-    col = 0
-    for w in ws:
-        p0, p1, g = _pp_planes(w)
-        _check(lib().la_gemm_pp(w.fmt, p0, p1, g, w.N, K, x.data_ptr(), K, M, S, out.data_ptr() + col * esz, Ntot,
-                                slab, int(bf), _stream()), "la_gemm_pp")
-        col += w.N
-
-
-_PP2_PAIRS = {(FMT_Q4_K, FMT_Q6_K), (FMT_Q6_K, FMT_Q4_K), (FMT_Q4_K, FMT_Q4_K)}
-
-
-def _run_pp_glu(x, pair, F: int, mode: int, out) -> None:
-    M, K = x.shape
-    wa, oa, wb, ob = pair
-    a0, a1, ag = _pp_planes(wa)
-    b0, b1, bg = _pp_planes(wb)
-    _check(lib().la_gemm_pp_glu(wa.fmt, a0, a1, ag, oa, b0, b1, bg, ob, F, K, x.data_ptr(), K, M, out.data_ptr(), F,
-                                mode, _stream()), "la_gemm_pp_glu")
-
-
 def _q32_grid(M: int, N: int, var: int) -> int:
     bm, bn = Q32_TILES[var]
     return -(-M // bm) * -(-N // bn)
@@ -1004,7 +916,7 @@ def _autotune_mid(x, ws, key, Ntot):
     """Time the tile GEMM's (tile, split-K) candidates with COLD weights (caches flushed before
     every timed call, as in decode where each step streams the whole model once) and remember
     the winner.  A split variant is charged for the extra fp32 bytes its consumer reads (at
-    ~4 TB/s).  LOCALAI_AMD_BLAS_CANDIDATE=1 adds hipBLASLt on a bf16 copy (A/B only)."""
+    ~4 TB/s)."""
     M, K = x.shape
     N = max(w.N for w in ws)
     cands = []
@@ -1030,9 +942,7 @@ def _autotune_mid(x, ws, key, Ntot):
             for S in sorted({1, max(1, base // 2), base, base * 2}):
                 if S <= min(8, K // 256) and _tile_split_ok(K, S):
                     cands.append(("bs", S, v))
-    if not cands or os.environ.get("LOCALAI_AMD_BLAS_CANDIDATE") == "1" or not TILE_GEMM:
-        cands.append(("blas", 0, 0))
-    if not TILE_GEMM:
+    if not cands or not TILE_GEMM:
         cands = [("blas", 0, 0)]
     outs = {S: torch.empty(S, M, Ntot, dtype=torch.float32, device=x.device) for _, S, _ in cands if S > 1}
     outs[1] = torch.empty(M, Ntot, dtype=torch.bfloat16, device=x.device)   # S = 1: one bf16 matrix
@@ -1114,18 +1024,9 @@ def linear_multi(x: torch.Tensor, ws: Sequence[QWeight], bias: Optional[torch.Te
     elif force is None and not use_skinny and tile_ok and PREFILL_GEMM == "tile":
         tile, S = pick_tile(M, [w.N for w in ws], K)   # prefill: heuristic, never tuned inline
         kind = "tile"
-    elif (force == "pp" or (force is None and not use_skinny and M > MID_MAX_M and PREFILL_GEMM == "pp")) \
-            and pp_ok(ws, K) and (len(ws) == 1 or (len(ws) == 2 and (ws[0].fmt, ws[1].fmt) in _PP2_PAIRS)
-                                 or all(w.fmt == ws[0].fmt for w in ws)):
-        S, kind = pp_splits(M, Ntot, K), "pp"
-        while S > 1 and not pp_ok(ws, K, S):
-            S //= 2
-    if kind in ("tile", "q32", "pp", "bs") and S == 1 and out_slabs is None:
+    if kind in ("tile", "q32", "bs") and S == 1 and out_slabs is None:
         y = torch.empty(M, Ntot, dtype=torch.bfloat16, device=x.device)
-        if kind == "pp":
-            _run_pp(x, ws, 1, y, Ntot)
-        else:
-            {"tile": _run_tile, "q32": _run_q32, "bs": _run_bs}[kind](x, ws, 1, y, Ntot, tile)
+        {"tile": _run_tile, "q32": _run_q32, "bs": _run_bs}[kind](x, ws, 1, y, Ntot, tile)
         return Partial(y, bias)
     if S:
         out = out_slabs
@@ -1133,8 +1034,6 @@ def linear_multi(x: torch.Tensor, ws: Sequence[QWeight], bias: Optional[torch.Te
             out = torch.empty(S, M, Ntot, dtype=torch.float32, device=x.device)
         if kind == "tile":
             _run_tile(x, ws, S, out, Ntot, tile)
-        elif kind == "pp":
-            _run_pp(x, ws, S, out, Ntot)
         elif kind == "bs":
             _run_bs(x, ws, S, out, Ntot, tile)
         else:
@@ -1149,9 +1048,8 @@ def linear_multi(x: torch.Tensor, ws: Sequence[QWeight], bias: Optional[torch.Te
         out = out_slabs
         if out is None or out.shape != (S, M, Ntot):
             out = torch.empty(S, M, Ntot, dtype=torch.float32, device=x.device)
-        red = GEMV_REDUCE and S > 1 and out_slabs is None
-        gemv_dp4(x, ws, S, out, reduce_splits=red)
-        return Partial(out[:1] if red else out, bias)
+        gemv_dp4(x, ws, S, out)
+        return Partial(out, bias)
     if use_skinny:
         S = min(pick_splits(w.N, w.K, M) for w in ws)
         nsb = K // 256
@@ -1171,8 +1069,6 @@ def linear_multi(x: torch.Tensor, ws: Sequence[QWeight], bias: Optional[torch.Te
 
 
 GLU_FUSE = os.environ.get("LOCALAI_AMD_GLU_FUSE", "1") == "1"
-PP_GLU = os.environ.get("LOCALAI_AMD_PP_GLU", "0") == "1"   # prefill gate|up on gemm_pp.hip
-PP_GLU_MIN_M = 1024   # below ~4 row tiles the 256 x 256 grid leaves CUs idle
 _GLU_CHOICE: Dict[tuple, Optional[int]] = {}
 
 
@@ -1227,18 +1123,9 @@ def glu_linear(x: torch.Tensor, ws: Sequence[QWeight], F: int, mode: int,
     if not (GLU_FUSE and TILE_GEMM and x.is_cuda and bias is None and mode in GLU_ACTS):
         return None
     M, K = x.shape
-    if M > MID_MAX_M:
-        # prefill chunks: gemm_pp.hip's fused GLU (gate and up of one index share a 256-wide tile,
-        # the activation runs in the epilogue).  Opt-in (LOCALAI_AMD_PP_GLU=1): it is still ~1.3x
-        # slower than dequant + hipBLASLt + the activation kernel at M = 8192, and the engine
-        # A/B lost 30 ms of p50 TTFT with it (profiles/r5_prefill_gemm.md)
-        pair = _glu_pair(ws, F) if PP_GLU and M >= PP_GLU_MIN_M else None
-        if pair is None or pair[0].fmt != pair[2].fmt or not pp_ok([pair[0], pair[2]], K):
-            return None
-        out = torch.empty(M, F, dtype=torch.bfloat16, device=x.device)
-        _run_pp_glu(x, pair, F, mode, out)
-        return out
-    if M <= SKINNY_MAX_M:
+    if M > MID_MAX_M or M <= SKINNY_MAX_M:
+        # prefill chunks: dequant + hipBLASLt + the activation kernel beats every fused GLU tile
+        # at M >= 1024 (gemm_bs.hip's GLU mode included, profiles/r6_gemm_bs.md)
         return None
     pair = _glu_pair(ws, F)
     if pair is None:
@@ -1454,9 +1341,8 @@ def act_linear(src: Partial, F: int, mode: int, w: QWeight) -> Partial:
             and w.K == F and src.N == width):
         S = _gemv_splits([w], w.K, M)
         out = torch.empty(S, M, w.N, dtype=torch.float32, device=src.t.device)
-        red = GEMV_REDUCE and S > 1
-        gemv_dp4(None, [w], S, out, act_src=src, act_mode=mode, reduce_splits=red)
-        return Partial(out[:1] if red else out)
+        gemv_dp4(None, [w], S, out, act_src=src, act_mode=mode)
+        return Partial(out)
     return linear(act(src, F, mode), w)
 
 
@@ -2099,6 +1985,50 @@ def moe_down32(h: torch.Tensor, mw: "MoEWeights", order: torch.Tensor, off: torc
     _check(lib().la_moe32(mw.fmt, 2, mw.desc32().data_ptr(), mw.N, mw.K, mw.E, order.data_ptr(), off.data_ptr(), topk,
                           h.data_ptr(), h.shape[1], T, S, wts.data_ptr(), out.data_ptr(), mw.N, T * mw.N, 0, v,
                           _stream()), "la_moe32")
+    return Partial(out)
+
+
+# Grouped MoE on the shared-dequant-image tile (gemm_bs.hip bsmoe_kernel): every local expert's
+# routed rows in ONE launch per projection, 256-row tiles (an expert's weights stream once per 256
+# rows, not once per 64 as on moe32), grid sized for any routing -- no host read of the grouping.
+# Prefill chunks (T >= MOE_BS_MIN_T tokens); decode batches stay on moe32.
+MOE_BS = os.environ.get("LOCALAI_AMD_MOE_BS", "1") == "1"
+MOE_BS_MIN_T = int(os.environ.get("LOCALAI_AMD_MOE_BS_MIN_T", "512"))
+MOE_BS_VAR = int(os.environ.get("LOCALAI_AMD_MOE_BS_VAR", "0"))
+
+
+def moe_bs_ok(gu: "MoEWeights", down: "MoEWeights", T: int) -> bool:
+    """Can the gate|up / down pair of a layer run on la_bsmoe for a T-token chunk."""
+    return (MOE_BS and T >= MOE_BS_MIN_T and gu.desc is not None and down.desc is not None
+            and gu.fmt in _MOE32_FMTS and down.fmt in _MOE32_FMTS and gu.K % 256 == 0 and down.K % 256 == 0
+            and gu.N % 16 == 0 and down.N % 4 == 0 and down.K == gu.N // 2)
+
+
+def moe_glu_bs(x: torch.Tensor, mw: "MoEWeights", order: torch.Tensor, off: torch.Tensor, topk: int, T: int,
+               act: int = ACT_SWIGLU, var: Optional[int] = None) -> torch.Tensor:
+    """moe_glu32's contract on the bs tile: h [T*topk, F] bf16 in grouped row order."""
+    F = mw.N // 2
+    if x.dtype != torch.bfloat16 or not x.is_contiguous() or x.shape[1] != mw.K or x.shape[0] != T:
+        raise ValueError("moe_glu_bs: x must be contiguous bf16 [T, K]")
+    h = torch.empty(T * topk, F, dtype=torch.bfloat16, device=x.device)
+    a = {ACT_SWIGLU: 0, ACT_GEGLU: 3}[act]
+    _check(lib().la_bsmoe(mw.fmt, 1, mw.desc32().data_ptr(), F, mw.K, mw.E, order.data_ptr(), off.data_ptr(), topk,
+                          x.data_ptr(), x.shape[1], T, 1, None, h.data_ptr(), F, 0, a,
+                          MOE_BS_VAR if var is None else var, _stream()), "la_bsmoe")
+    return h
+
+
+def moe_down_bs(h: torch.Tensor, mw: "MoEWeights", order: torch.Tensor, off: torch.Tensor, topk: int, T: int,
+                wts: torch.Tensor, zero: bool = False, var: Optional[int] = None) -> Partial:
+    """moe_down32's contract on the bs tile: Partial [topk, T, N], slab `slot` row t = wts[pair] *
+    (h_pair Wd^T) of token t's slot-th pick."""
+    if h.dtype != torch.bfloat16 or not h.is_contiguous() or h.shape[1] != mw.K or h.shape[0] != T * topk:
+        raise ValueError("moe_down_bs: h must be contiguous bf16 [T*topk, K]")
+    alloc = torch.zeros if zero else torch.empty
+    out = alloc(topk, T, mw.N, dtype=torch.float32, device=h.device)
+    _check(lib().la_bsmoe(mw.fmt, 2, mw.desc32().data_ptr(), mw.N, mw.K, mw.E, order.data_ptr(), off.data_ptr(), topk,
+                          h.data_ptr(), h.shape[1], T, 1, wts.data_ptr(), out.data_ptr(), mw.N, T * mw.N, 0,
+                          MOE_BS_VAR if var is None else var, _stream()), "la_bsmoe")
     return Partial(out)
 
 

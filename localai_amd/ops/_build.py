@@ -28,7 +28,7 @@ def _torch_lib() -> str:
 
 # per-file hipcc flags: the prefill GEMM's dequant runs beside MFMAs, where the packed
 # v_pk_fma_f32 the SLP vectoriser forms issues slower than two scalar FMAs (profiles/r5_prefill_gemm.md)
-FILE_FLAGS = {"gemm_pp.hip": ["-fno-slp-vectorize"], "gemm_bs.hip": ["-fno-slp-vectorize"]}
+FILE_FLAGS = {"gemm_bs.hip": ["-fno-slp-vectorize"]}
 
 
 def _sources():

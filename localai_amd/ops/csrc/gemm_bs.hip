@@ -233,13 +233,24 @@ struct BsGlu {
   int oa, ob, F, act;
 };
 
+// Grouped MoE rows (bsmoe_kernel): `order` points at the expert's first grouped pair; pair p is
+// token p / topk's slot p % topk, weighted by wts[p].
+struct BsMoe {
+  const int* order;
+  int topk;
+  const float* wts;
+};
+
 LA_DEV float bs_gelu_tanh(float x) { return 0.5f * x * (1.f + tanhf(0.7978845608f * (x + 0.044715f * x * x * x))); }
 
 // Epilogue straight from the accumulators: lane (m = c32, hh) of block (cb, mb) holds columns
 // n = 32cb + 8g + 4hh + e (g = reg >> 2, e = reg & 3) of row 32mb + c32 of the wave's rows.
+// MODE 3 (grouped MoE down projection): row m is pair mo.order[m]; its routing-weighted fp32 row
+// goes to slab (split * topk + slot), row token.
 template <class C, int MODE>
 LA_DEV void bs_epilogue(const bsf32x16 (&acc)[C::NCB][C::MB], const QW& w, int mt, int nt, int split, int M,
-                        float* __restrict__ out, bf16* __restrict__ outb, int ldo, long slab, const BsGlu& glu) {
+                        float* __restrict__ out, bf16* __restrict__ outb, int ldo, long slab, const BsGlu& glu,
+                        const BsMoe& mo) {
   constexpr int RM = C::RM, MB = C::MB, NCB = C::NCB;
   const int lane = threadIdx.x & 63, c32 = lane & 31, hh = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -262,6 +273,25 @@ LA_DEV void bs_epilogue(const bsf32x16 (&acc)[C::NCB][C::MB], const QW& w, int m
             hv[e] = (bf16)((glu.act == 0 ? silu(gv) : bs_gelu_tanh(gv)) * uv);
           }
           if (j < glu.F) *(bf16x4*)(outb + (size_t)m * ldo + j) = hv;  // F % 4 == 0
+        }
+    }
+  } else if constexpr (MODE == 3) {
+    const int n0 = nt * C::BN;
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) {
+      const int m = mrow0 + 32 * mb;
+      if (m >= M) continue;
+      const int pair = mo.order[m], tok = pair / mo.topk, slot = pair - tok * mo.topk;
+      const float sc = mo.wts[pair];
+      float* o = out + (size_t)(split * mo.topk + slot) * slab + (size_t)tok * ldo;
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int n = n0 + 32 * cb + 8 * g + 4 * hh;
+          const f32x4 v{sc * acc[cb][mb][4 * g], sc * acc[cb][mb][4 * g + 1], sc * acc[cb][mb][4 * g + 2],
+                        sc * acc[cb][mb][4 * g + 3]};
+          if (n < w.N) *(f32x4*)(o + n) = v;  // N % 4 == 0
         }
     }
   } else {
@@ -295,11 +325,13 @@ LA_DEV void bs_epilogue(const bsf32x16 (&acc)[C::NCB][C::MB], const QW& w, int m
   }
 }
 
-// One (M tile, N tile, K split) of a plain (MODE 0) or GLU (MODE 1) GEMM.
-template <int FMT, class C, int MODE, int ABL = 0>
+// One (M tile, N tile, K split) of a plain (MODE 0 fp32 slabs / 2 bf16), GLU (MODE 1) or grouped
+// MoE down (MODE 3) GEMM.  GATHER: logical row m reads X row mo.order[m] / mo.topk (the token of a
+// grouped MoE pair).
+template <int FMT, class C, int MODE, int ABL = 0, int GATHER = 0>
 LA_DEV void bs_tile(uint8_t* __restrict__ lds, const QW& w, int mt, int nt, int split, const bf16* __restrict__ X,
                     int ldx, int M, int per_split, float* __restrict__ out, bf16* __restrict__ outb, int ldo,
-                    long slab, const BsGlu& glu) {
+                    long slab, const BsGlu& glu, const BsMoe& mo = BsMoe{}) {
   using F = BsF<FMT>;
   constexpr int RM = C::RM, CBW = C::CBW, MB = C::MB, NCB = C::NCB, XL = C::XL;
   constexpr int BIMG = C::BIMG, XIMG = C::XIMG;
@@ -333,7 +365,8 @@ LA_DEV void bs_tile(uint8_t* __restrict__ lds, const QW& w, int mt, int nt, int 
 #pragma unroll
   for (int i = 0; i < XL; ++i) {
     const int r = 8 * i + (lane >> 3), c = lane & 7;
-    const int m = min(mt * C::BM + wave * RM + r, M - 1);
+    int m = min(mt * C::BM + wave * RM + r, M - 1);
+    if constexpr (GATHER) m = mo.order[m] / mo.topk;
     xp[i] = X + (size_t)m * ldx + (c < 4 ? 8 * c : F::RUN + 8 * (c - 4));
     xw[i] = (uint32_t)(r * 8 + (c ^ ((r >> 1) & 7))) * 16;
   }
@@ -530,7 +563,7 @@ LA_DEV void bs_tile(uint8_t* __restrict__ lds, const QW& w, int mt, int nt, int 
   if constexpr (D > 3)
     if (t + 2 < nk) step(I2{}, t + 2);
 
-  bs_epilogue<C, MODE>(acc, w, mt, nt, split, M, out, outb, ldo, slab, glu);
+  bs_epilogue<C, MODE>(acc, w, mt, nt, split, M, out, outb, ldo, slab, glu, mo);
 }
 
 // The same tile with X in the BLOCKED layout Xb[ceil(M/32)][K/8][32 rows][8] bf16 (16-B chunk
@@ -721,7 +754,7 @@ LA_DEV void bs_tile_xb(uint8_t* __restrict__ lds, const QW& w, int mt, int nt, i
     if (t + 1 < nk) step(I1{}, t + 1);
   if constexpr (D > 3)
     if (t + 2 < nk) step(I2{}, t + 2);
-  bs_epilogue<C, MODE>(acc, w, mt, nt, split, M, out, outb, ldo, slab, glu);
+  bs_epilogue<C, MODE>(acc, w, mt, nt, split, M, out, outb, ldo, slab, glu, BsMoe{});
 }
 
 // Tile id -> (n tile fastest, then m tile, then split).  Blocks are dealt round-robin over the 8
@@ -793,6 +826,63 @@ __global__ __launch_bounds__(256, 1) void bsgemm_glu_kernel(QW wg, BsGlu glu, co
   bs_tile<FMT, C, 1>(lds, wg, mt, nt, 0, X, ldx, M, wg.K >> 6, nullptr, outb, ldo, 0, glu);
 }
 
+// Grouped MoE GEMM: every local expert's routed rows in ONE launch, no host read of the grouping.
+// The grid covers cmax = ceil(P / BM) + E row chunks (P = T * topk pairs), enough for any routing:
+// sum_e ceil(M_e / BM) <= P / BM + E.  Tile id -> (n tile fastest, row chunk, split); a workgroup
+// finds the expert of its chunk with a wave-wide prefix sum over the per-expert chunk counts (read
+// from off[], identical in every wave) and exits when the chunk is past the last expert's rows.
+//   MODE 1: gate|up of the expert (gate rows [0, F), up rows [F, 2F) of one weight), GLU fused, X
+//           rows gathered from the tokens -> bf16 h rows in grouped order (row off[e] + m)
+//   MODE 3: down projection of the grouped h rows -> routing-weighted fp32 rows scattered to slab
+//           (split * topk + slot), row token
+template <int FMT, class C, int MODE>
+__global__ __launch_bounds__(256, 1) void bsmoe_kernel(const QW* __restrict__ qws, const int* __restrict__ order,
+                                                        const int* __restrict__ off, int E, int topk,
+                                                        const bf16* __restrict__ X, int ldx, int cmax, int n_tiles,
+                                                        int per_split, int real, const float* __restrict__ wts,
+                                                        float* __restrict__ out, bf16* __restrict__ outb, int ldo,
+                                                        long slab, int F, int act) {
+  __shared__ __attribute__((aligned(1024))) uint8_t lds[C::LDS];
+  if ((int)blockIdx.x >= real) return;
+  const int tile = bs_tile_id(real);
+  const int nt = tile % n_tiles, r = tile / n_tiles, c = r % cmax, split = r / cmax;
+  const int lane = threadIdx.x & 63;
+  int e = -1, cl = 0, base = 0;
+  for (int e0 = 0; e0 < E; e0 += 64) {
+    const int ei = e0 + lane;
+    const int cnt = ei < E ? (off[ei + 1] - off[ei] + C::BM - 1) / C::BM : 0;
+    int inc = cnt;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int v = __shfl_up(inc, d);
+      if (lane >= d) inc += v;
+    }
+    const unsigned long long hit = __ballot(cnt > 0 && c >= base + inc - cnt && c < base + inc);
+    if (hit) {
+      const int l = __ffsll((long long)hit) - 1;
+      e = e0 + l;
+      cl = c - base - (__shfl(inc, l) - __shfl(cnt, l));
+      break;
+    }
+    base += __shfl(inc, 63);
+  }
+  e = __builtin_amdgcn_readfirstlane(e);
+  cl = __builtin_amdgcn_readfirstlane(cl);
+  if (e < 0) return;
+  const int o0 = off[e], Me = off[e + 1] - o0;
+  QW w = qws[e];
+  const BsMoe mo{order + o0, topk, wts};
+  if constexpr (MODE == 1) {
+    const BsGlu glu{w, 0, F, F, act};
+    w.N = F;
+    bs_tile<FMT, C, 1, 0, 1>(lds, w, cl, nt, 0, X, ldx, Me, w.K >> 6, nullptr, outb + (size_t)o0 * ldo, ldo, 0, glu,
+                             mo);
+  } else {
+    bs_tile<FMT, C, 3>(lds, w, cl, nt, split, X + (size_t)o0 * ldx, ldx, Me, per_split, out, nullptr, ldo, slab,
+                       BsGlu{}, mo);
+  }
+}
+
 // variant ids (ops/__init__.py BS_TILES): tile, rows per wave, column blocks per wave, ring depth
 //   0: 256 x 128 (RM 64, CBW 1, D 3)   1: 128 x 128 (RM 32, CBW 1, D 3; two workgroups per CU)
 //   2: 256 x 256 (RM 64, CBW 2, D 2)   3: 256 x 128 (RM 64, CBW 1, D 4)
@@ -852,6 +942,21 @@ static int bs_launch_glu(int var, const QW& wg, const BsGlu& glu, const bf16* X,
     const int real = m_tiles * n_tiles;
     hipLaunchKernelGGL((bsgemm_glu_kernel<FMT, C>), dim3(real), dim3(256), 0, st, wg, glu, X, ldx, M, m_tiles, n_tiles,
                        real, outb, ldo);
+  });
+}
+
+template <int FMT, int MODE>
+static int bsmoe_launch(int var, const QW* qws, int N, int K, int E, const int* order, const int* off, int topk,
+                        const bf16* X, int ldx, int P, int splits, const float* wts, float* out, bf16* outb, int ldo,
+                        long slab, int act, hipStream_t st) {
+  const int KS = K >> 6, per = (KS + splits - 1) / splits;
+  return bs_var(var, [&](auto c) {
+    using C = decltype(c);
+    const int cmax = (P + C::BM - 1) / C::BM + E;
+    const int n_tiles = MODE == 1 ? (N + C::BN / 2 - 1) / (C::BN / 2) : (N + C::BN - 1) / C::BN;
+    const int real = cmax * n_tiles * splits;
+    hipLaunchKernelGGL((bsmoe_kernel<FMT, C, MODE>), dim3(real), dim3(256), 0, st, qws, order, off, E, topk, X, ldx,
+                       cmax, n_tiles, per, real, wts, out, outb, ldo, slab, N, act);
   });
 }
 
@@ -939,6 +1044,48 @@ extern "C" int la_bsgemm_glu(int fmt, const void* pa0, const void* pa1, const vo
     case FMT_Q8_0: rc = bs_launch_glu<FMT_Q8_0>(var, wg, glu, x, ldx, M, o, ldo, st); break;
     default: rc = bs_launch_glu<FMT_BF16>(var, wg, glu, x, ldx, M, o, ldo, st); break;
   }
+  if (rc) return rc;
+  return (int)hipGetLastError();
+}
+
+// Grouped MoE GEMM (see bsmoe_kernel).  qws: device array of E QW descriptors {codes, aux,
+// blocked scale plane, -, N, K} (MoEWeights.desc32); order / off: the pair grouping of
+// la_moe_route (off[E] may be < P: pairs past it belong to no local expert); P = T * topk.
+//   mode 1: X [T][ldx] tokens -> out bf16 [P][ldo]; N = F (each expert weight holds 2F rows);
+//           splits must be 1; act 0 SwiGLU / 3 GeGLU
+//   mode 2: X [P][ldx] grouped h rows -> out fp32 [splits * topk][T][ldo] (stride slab), rows
+//           scaled by wts[pair]; rows of pairs of no local expert are left unwritten
+extern "C" int la_bsmoe(int fmt, int mode, const void* qws, int N, int K, int E, const int* order, const int* off,
+                        int topk, const void* X, int ldx, int T, int splits, const float* wts, void* out, int ldo,
+                        long slab, int act, int var, void* stream) {
+  using namespace la;
+  if (T < 1 || N < 1 || (N & 3) || E < 1 || (K & 255) || splits < 1 || ldo < N || ldx < K || (ldx & 7) || (ldo & 3) ||
+      topk < 1 || !qws || !order || !off)
+    return -1;
+  if (mode == 1 && (splits != 1 || (act != 0 && act != 3))) return -1;
+  if (mode == 2 && (!wts || slab < (long)T * ldo)) return -1;
+  if (mode != 1 && mode != 2) return -1;
+  if (fmt != FMT_Q4_K && fmt != FMT_Q6_K && fmt != FMT_Q8_0) return -2;
+  const int P = T * topk;
+  const int KS = K / 64, per = (KS + splits - 1) / splits;
+  if (per * (splits - 1) >= KS) return -1;
+  if ((long)P * ldx >= (1L << 31) || (long)P * ldo >= (1L << 31) || (long)(P / 32 + E) * (N / 32 + 1) * splits >= (1L << 31))
+    return -1;
+  hipStream_t st = (hipStream_t)stream;
+  const QW* q = (const QW*)qws;
+  const bf16* x = (const bf16*)X;
+  float* o = mode == 2 ? (float*)out : nullptr;
+  bf16* ob = mode == 1 ? (bf16*)out : nullptr;
+  int rc;
+#define BSMOE_F(F_)                                                                                                  \
+  rc = mode == 1 ? bsmoe_launch<F_, 1>(var, q, N, K, E, order, off, topk, x, ldx, P, 1, wts, o, ob, ldo, slab, act, st) \
+                 : bsmoe_launch<F_, 3>(var, q, N, K, E, order, off, topk, x, ldx, P, splits, wts, o, ob, ldo, slab, act, st);
+  switch (fmt) {
+    case FMT_Q4_K: BSMOE_F(FMT_Q4_K) break;
+    case FMT_Q6_K: BSMOE_F(FMT_Q6_K) break;
+    default: BSMOE_F(FMT_Q8_0) break;
+  }
+#undef BSMOE_F
   if (rc) return rc;
   return (int)hipGetLastError();
 }

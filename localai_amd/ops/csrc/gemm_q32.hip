@@ -25,10 +25,6 @@
 
 #include "qweight.h"
 
-#ifndef LA_Q32_FP8
-#define LA_Q32_FP8 0  // 1: Q4_K nibbles through v_cvt_pk_f32_fp8 -- measured neutral (r5_fp8_*.log): gate|up M=256 76.4 vs 76.3 us, engine C=256 25.09k vs 25.30k
-#endif
-
 namespace la {
 
 typedef float f32x16_t __attribute__((ext_vector_type(16)));
@@ -99,41 +95,15 @@ template <> struct Q32F<FMT_Q4_K> {
   LA_DEV static void load(const uint8_t* raw, const uint8_t* scl, int c, int h, int, St& st) {
     st.q = *(const u32x4*)(raw + c * 32 + 16 * (h ^ ((c >> 3) & 1)));
     const u32x2 s = *(const u32x2*)(scl + c * 8);  // f16 D0, -M0, D1, -M1 (la_gemm_scales)
-    // LA_Q32_FP8: a nibble byte q (0..15) read as OCP e4m3 is exactly q * 2^-9, so the scale
-    // carries the 2^9
-    st.D0 = h2f(s.x & 0xFFFFu) * (LA_Q32_FP8 ? 512.f : 1.f);
+    st.D0 = h2f(s.x & 0xFFFFu);
     st.M0 = h2f(s.x >> 16);
-    st.D1 = h2f(s.y & 0xFFFFu) * (LA_Q32_FP8 ? 512.f : 1.f);
+    st.D1 = h2f(s.y & 0xFFFFu);
     st.M1 = h2f(s.y >> 16);
   }
   template <int S>
   LA_DEV static bf16x8 deq(const St& st) {
     const uint32_t w0 = (S & 1) ? st.q.z : st.q.x, w1 = (S & 1) ? st.q.w : st.q.y;
     uint32_t lo, hi;
-#if LA_Q32_FP8
-    // two weights per v_cvt_pk_f32_fp8 (vs one v_cvt_f32_ubyte each): 2.25 VALU per weight
-    if constexpr (S < 2) {
-      asm("v_and_b32 %0, 0x0f0f0f0f, %1" : "=v"(lo) : "v"(w0));
-      asm("v_and_b32 %0, 0x0f0f0f0f, %1" : "=v"(hi) : "v"(w1));
-    } else {
-      asm("v_and_b32 %0, 0x0f0f0f0f, %1" : "=v"(lo) : "v"(w0 >> 4));
-      asm("v_and_b32 %0, 0x0f0f0f0f, %1" : "=v"(hi) : "v"(w1 >> 4));
-    }
-    typedef float f2 __attribute__((ext_vector_type(2)));
-    const float D = S < 2 ? st.D0 : st.D1, Mn = S < 2 ? st.M0 : st.M1;
-    const f2 a0 = __builtin_amdgcn_cvt_pk_f32_fp8((int)lo, false), a1 = __builtin_amdgcn_cvt_pk_f32_fp8((int)lo, true);
-    const f2 b0 = __builtin_amdgcn_cvt_pk_f32_fp8((int)hi, false), b1 = __builtin_amdgcn_cvt_pk_f32_fp8((int)hi, true);
-    bf16x8 r;
-    r[0] = (bf16)fmaf(D, a0.x, Mn);
-    r[1] = (bf16)fmaf(D, a0.y, Mn);
-    r[2] = (bf16)fmaf(D, a1.x, Mn);
-    r[3] = (bf16)fmaf(D, a1.y, Mn);
-    r[4] = (bf16)fmaf(D, b0.x, Mn);
-    r[5] = (bf16)fmaf(D, b0.y, Mn);
-    r[6] = (bf16)fmaf(D, b1.x, Mn);
-    r[7] = (bf16)fmaf(D, b1.y, Mn);
-    return r;
-#else
     // opaque masks: one v_cvt_f32_ubyteN per weight
     if constexpr (S < 2) {
       asm("v_and_b32 %0, 0x0f0f0f0f, %1" : "=v"(lo) : "v"(w0));
@@ -150,7 +120,6 @@ template <> struct Q32F<FMT_Q4_K> {
       r[b + 4] = (bf16)fmaf(D, (float)((hi >> (8 * b)) & 0xFFu), Mn);
     }
     return r;
-#endif
   }
 };
 

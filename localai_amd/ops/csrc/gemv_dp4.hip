@@ -47,10 +47,8 @@ struct GVArgs {
   int blk_end[GV_SEGS];  // exclusive prefix sum of row blocks
   int col0[GV_SEGS];     // first output column of each segment
   int nseg;
-  int* tickets;          // non-null: split-K partials reduced in the kernel (gv_reduce), one per row block
 };
 
-constexpr int GV_MAX_TICKETS = 8192;  // row blocks of one launch with an in-kernel split-K reduction
 
 LA_DEV int dot4(uint32_t a, uint32_t b, int c) { return __builtin_amdgcn_sdot4((int)a, (int)b, c, false); }
 
@@ -849,49 +847,6 @@ LA_DEV void gv_q8(const QW& w, int row0, const bf16* X, int ldx, const GVAct& ac
   gv_store<MT, RS>(acc, n, w.N, M, t, o, ldo, col0, rp);
 }
 
-// In-kernel split-K reduction: the last of the gridDim.y workgroups of a row block to finish
-// (agent-scope release / ticket / acquire, the attention kernel's partition-merge protocol) sums
-// the block's S partial rows into slab 0, so the consumer -- the next GEMV's activation or norm
-// prologue, add_norm -- reads one slab instead of S (each of ~1000 consumer workgroups re-read
-// all S before).  The ticket resets itself for the next launch / graph replay.
-template <int RS>
-LA_DEV void gv_reduce(const GVArgs& a, int seg, int blk, int row0, float* __restrict__ out, int ldo, long slab,
-                      int M) {
-  __shared__ int last;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    int* tk = a.tickets + blk;
-    const int prev = __hip_atomic_fetch_add(tk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = prev == (int)gridDim.y - 1;
-    if (last) {
-      *tk = 0;
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-  }
-  __syncthreads();
-  if (!last) return;
-  constexpr int NR = 32 * RS;
-  const int N = a.w[seg].N, S = gridDim.y;
-  for (int i = threadIdx.x; i < M * NR; i += GV_THREADS) {
-    const int m = i / NR, n = row0 + i % NR;
-    if (n >= N) continue;
-    const long idx = (long)m * ldo + a.col0[seg] + n;
-    float v[8], acc = 0.f;
-    for (int y0 = 0; y0 < S; y0 += 8) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = out[(long)min(y0 + j, S - 1) * slab + idx];
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (y0 + j < S) acc += v[j];
-    }
-    out[idx] = acc;
-  }
-}
-
 // Segments [0, nA) are format FA, [nA, nseg) format FB (a q|k + v fusion is (Q4_K, Q6_K)).
 // VAR bit 0: non-temporal weight loads; bit 1: weights requested before the x prologue.
 template <int MT, int FA, int FB, int VAR>
@@ -920,7 +875,6 @@ __global__ __launch_bounds__(GV_THREADS) void qgemv_dp4_kernel(GVArgs a, const b
     if constexpr (FB == FMT_Q4_K) gv_q4k<MT, NT, EARLY, RS, PD, NM>(a.w[seg], row0, X, ldx, act, M, kper, o, ldo, a.col0[seg], xq, bs, dx, rp);
     else gv_q6k<MT, NT, EARLY, RS, PD, NM>(a.w[seg], row0, X, ldx, act, M, kper, o, ldo, a.col0[seg], xq, bs, dx, rp);
   }
-  if (a.tickets && gridDim.y > 1) gv_reduce<RS>(a, seg, blk, row0, out, ldo, slab, M);
 }
 
 // MoE decode (1-2 tokens): the routed experts' projections as GEMVs on the int8-dot path.  One
@@ -972,9 +926,6 @@ static inline size_t gv_lds_bytes(int MT, int kper) {
   return (size_t)MT * kper + (size_t)MT * (kper >> 4) * 4 + (size_t)MT * (kper >> 5) * 4;
 }
 
-// moe_gemv_kernel variant (la_moe_gemv_variant): 1 = two 8-row slots per wave -- Mixtral C=1 312.8 /
-// 313.2 vs 306.4 tok/s with variant 5, C=2 413.3 / 412.8 vs 404.0 (profiles/r5_logs/r5_mv2_*.log)
-static int g_moe_gv_var = 1;
 static int g_gv_variant = 5;  // non-temporal weight loads, x staged first, one 8-row slot per wave (fastest overall)
 
 template <int MT, int FA, int FB>
@@ -1021,8 +972,7 @@ static int launch_gv_m(const GVArgs& a, int nblk, int K, const bf16* X, int ldx,
 static int qgemv_dp4_impl(int nseg, const int* fmts, const void* const* planes, const int* Ns, int K,
                           const void* X, int ldx, int M, int splits, void* out, int ldo, long slab,
                           const void* act_p, long act_slab, int act_S, const void* act_bias, int act_mode,
-                          void* stream, const la::GVRope& rp, const la::GVAct* norm = nullptr,
-                          int* tickets = nullptr) {
+                          void* stream, const la::GVRope& rp, const la::GVAct* norm = nullptr) {
   using namespace la;
   if (nseg < 1 || nseg > GV_SEGS || M < 1 || M > 4 || (K & 255) || splits < 1 || ((K >> 8) % splits) ||
       slab < (long)M * ldo)
@@ -1070,8 +1020,6 @@ static int qgemv_dp4_impl(int nseg, const int* fmts, const void* const* planes, 
   }
   a.nseg = nseg;
   if (ldo < col) return -1;
-  if (tickets && (nblk > la::GV_MAX_TICKETS || rp.q_out || norm)) return -1;
-  a.tickets = splits > 1 ? tickets : nullptr;
   // formats must form at most two runs: [FA ...][FB ...]
   int fa = a.fmt[0], fb = a.fmt[nseg - 1];
   for (int i = 0; i < nseg; ++i)
@@ -1091,20 +1039,6 @@ static int qgemv_dp4_impl(int nseg, const int* fmts, const void* const* planes, 
   if (rc) return rc;
   return (int)hipGetLastError();
 }
-
-// la_qgemv_dp4 with the split-K partials summed in the kernel into slab 0 (tickets: a zeroed int
-// array of >= GV_MAX_TICKETS entries, private to the stream; it is left zeroed).
-extern "C" int la_qgemv_dp4_red(int nseg, const int* fmts, const void* const* planes, const int* Ns, int K,
-                                const void* X, int ldx, int M, int splits, void* out, int ldo, long slab,
-                                const void* act_p, long act_slab, int act_S, const void* act_bias, int act_mode,
-                                void* tickets, void* stream) {
-  la::GVRope rp{};
-  if (!tickets) return -1;
-  return qgemv_dp4_impl(nseg, fmts, planes, Ns, K, X, ldx, M, splits, out, ldo, slab, act_p, act_slab, act_S,
-                        act_bias, act_mode, stream, rp, nullptr, (int*)tickets);
-}
-
-extern "C" int la_gv_max_tickets() { return la::GV_MAX_TICKETS; }
 
 extern "C" int la_qgemv_dp4(int nseg, const int* fmts, const void* const* planes, const int* Ns, int K,
                             const void* X, int ldx, int M, int splits, void* out, int ldo, long slab,
@@ -1189,38 +1123,20 @@ extern "C" int la_moe_gemv(int fmt, int down, const void* qws, int N, int K, int
   const size_t lds = gv_lds_bytes(1, kper);
   if (lds > 64 * 1024) return -3;
   GVAct act{(const float*)act_p, act_slab, act_S, nullptr, act_mode, K};
-  // variant (la_moe_gemv_variant): 1 = non-temporal weights, x staged first, two 8-row slots per
-  // wave (default); 5 = one slot; 21 = one slot + 4-deep weight ring (whole groups of 4
-  // super-blocks only); 9 = four slots
-  int var = g_moe_gv_var;
-  if ((var & 16) && ((kper >> 8) % 4)) var &= ~16;
   hipStream_t st = (hipStream_t)stream;
-#define MG(F, V)                                                                                              \
-  {                                                                                                           \
-    const int rows = 32 * gv_rs<V>();                                                                         \
-    dim3 grid((N + rows - 1) / rows, splits, T * topk);                                                       \
-    hipLaunchKernelGGL((moe_gemv_kernel<F, V>), grid, dim3(GV_THREADS), lds, st, (const QW*)qws, ids, E_local, \
-                       topk, (const bf16*)X, ldx, act, wts, down, kper, (float*)out, ldo, slab);              \
-  }
-#define MGV(F)                        \
-  switch (var) {                      \
-    case 9: MG(F, 9) break;           \
-    case 21: MG(F, 21) break;         \
-    case 5: MG(F, 5) break;           \
-    default: MG(F, 1) break;          \
-  }
-  if (fmt == FMT_Q4_K) MGV(FMT_Q4_K)
-  else if (fmt == FMT_Q6_K) MGV(FMT_Q6_K)
-  else MGV(FMT_Q8_0)
-#undef MGV
+  // variant 1: non-temporal weights, x staged first, two 8-row slots per wave -- Mixtral C=1 312.8 /
+  // 313.2 vs 306.4 tok/s with one slot, C=2 413.3 / 412.8 vs 404.0 (profiles/r5_logs/r5_mv2_*.log)
+  constexpr int V = 1;
+  const int rows = 32 * gv_rs<V>();
+  dim3 grid((N + rows - 1) / rows, splits, T * topk);
+#define MG(F)                                                                                                 \
+  hipLaunchKernelGGL((moe_gemv_kernel<F, V>), grid, dim3(GV_THREADS), lds, st, (const QW*)qws, ids, E_local,   \
+                     topk, (const bf16*)X, ldx, act, wts, down, kper, (float*)out, ldo, slab);
+  if (fmt == FMT_Q4_K) MG(FMT_Q4_K)
+  else if (fmt == FMT_Q6_K) MG(FMT_Q6_K)
+  else MG(FMT_Q8_0)
 #undef MG
   return (int)hipGetLastError();
-}
-
-extern "C" int la_moe_gemv_variant(int v) {
-  if (v != 1 && v != 5 && v != 9 && v != 21) return -1;
-  la::g_moe_gv_var = v;
-  return 0;
 }
 
 // Tuning hook: select the kernel variant (bit 0 non-temporal loads, bit 1 early weight prefetch).

@@ -62,3 +62,27 @@ def test_bench_gateway_data_parallel(tmp_path):
     served = out["config"]["replica_requests"]
     # warmup + timed wave of 8 requests each, spread over both replicas
     assert sum(served) == 16 and min(served) > 0
+
+
+def test_bench_http_stream_check_per_request(tmp_path):
+    """One HTTP replica: the stream check adds up events + merged (held-back) tokens to the
+    reported count per request and passes on a well-formed stream."""
+    out = _bench(tmp_path, "--mode", "http")
+    sc = out["stream_check"]
+    assert sc["reported_tokens"] == sc["expected_tokens"] == 4 * 8
+    assert (sc["streamed_events"] - sc["split_events"] + sc["merged_tokens"] + sc["tail_tokens"]
+            == sc["reported_tokens"]), sc
+    assert sc["bad_streams"] == 0 and sc["short_requests"] == 0
+
+
+def test_bench_open_loop_arrivals(tmp_path):
+    """--arrival-rate: open-loop Poisson arrivals over HTTP report tokens/s, TTFT and inter-token
+    latency percentiles, with the same wire accounting."""
+    out = _bench(tmp_path, "--mode", "http", "--arrival-rate", "50", "--requests", "6")
+    assert out["requests"] == 6 and out["tokens_per_s"] > 0
+    assert out["p99_ttft_ms"] >= out["p50_ttft_ms"] > 0
+    assert out["p99_itl_ms"] >= out["p50_itl_ms"] > 0
+    sc = out["stream_check"]
+    assert sc["reported_tokens"] == sc["expected_tokens"] == 6 * 8
+    assert (sc["streamed_events"] - sc["split_events"] + sc["merged_tokens"] + sc["tail_tokens"]
+            == sc["reported_tokens"]) and sc["bad_streams"] == 0
