@@ -278,7 +278,7 @@ class LLMEngine:
         self.k_log = collections.deque(maxlen=1024)  # (K, constrained rows, batch, waiting) per run, in order
         self.metrics = {"prompt_tokens": 0, "gen_tokens": 0, "steps": 0, "prefill_s": 0.0, "decode_s": 0.0,
                         "requests": 0, "spec_steps": 0, "spec_drafted": 0, "spec_accepted": 0,
-                        "grammar_runs": 0, "grammar_run_rows": 0, "grammar_run_tokens": 0}
+                        "grammar_runs": 0, "grammar_run_rows": 0, "grammar_run_tokens": 0, "grammar_drift": 0}
         self.last_request_stats: dict = {}
         self.busy = False
 
@@ -1238,6 +1238,7 @@ class LLMEngine:
         for j in grows:
             r, s = reqs[j], int(gslot[j])
             kept = []
+            followed = missed = False
             for i in range(K):
                 t = int(hist[i, j])
                 self._on_token(r, t, now, append=False)
@@ -1253,14 +1254,18 @@ class LLMEngine:
                     s2 = self._grammar_mask_slot(r, V, self.device)
                     if (s, t) not in gtrans and epoch == self._gepoch:
                         self._gtrans_learn(s, t, s2)
+                    missed = True
                     break
                 # a learned transition within this epoch names the state's slot exactly (the table
                 # was written from the real successor), so the host follows it without hashing the
                 # parse state per token; the slot's mask stays recently used
                 s = gtrans[(s, t)]
+                followed = True
                 k = skey.get(s)
                 if k is not None and k in cache:
                     cache.move_to_end(k)
+            if followed and not missed and not r.done and epoch == self._gepoch:
+                self._grammar_verify(r, s)   # s and r.grammar both stand after the run's last token
             if kept and not r.done:
                 # the device already wrote the KV of every kept token but the last (fed by the
                 # next step): hand them over as a run, like the plain rows' _emit_run -- appending
@@ -1707,6 +1712,22 @@ class LLMEngine:
             self._gdev.discard(k)
             if v is not None and v >= 0:
                 self._gtrans_in.get(v, set()).discard(k)
+
+    def _grammar_verify(self, r, s: int):
+        """Once per row and run: the slot the host reached by following learned transitions must
+        name the row's real parse state (one state hash per run, not per token).  A mismatch means
+        a state key mapped two parse states with different successors; the slot is evicted (every
+        transition into or out of it is forgotten) so later runs re-learn from real states."""
+        key = (r.params.grammar, r.grammar.key())
+        if self._gslot_key.get(s) == key:
+            return
+        self.metrics["grammar_drift"] += 1
+        log.warning("grammar run-ahead: learned slot %d does not name the row's parse state; evicting it", s)
+        old = self._gslot_key.get(s)
+        if old is not None and self._gmask_cache.get(old) == s:
+            del self._gmask_cache[old]
+            self._gslot_key.pop(s, None)
+            self._gslot_release(s)
 
     def _gtrans_learn(self, s: int, t: int, s2):
         """Record the transition (slot s, token t) -> s2 (a slot, -1 complete, None unmasked);

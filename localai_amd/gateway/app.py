@@ -77,10 +77,13 @@ class CSRFMiddleware:
 
     SAFE = frozenset({"GET", "HEAD", "OPTIONS", "TRACE"})
     COOKIE, HEADER, TTL = "csrf_", "x-csrf-token", 3600.0
+    MAX_TOKENS = 65536   # live-token cap: the least recently used token is dropped first
 
-    def __init__(self, app):
+    def __init__(self, app, max_tokens: Optional[int] = None):
+        from collections import OrderedDict
         self.app = app
-        self.tokens: dict = {}   # token -> expiry (monotonic seconds)
+        self.max_tokens = max_tokens or self.MAX_TOKENS
+        self.tokens: "OrderedDict[str, float]" = OrderedDict()   # token -> expiry, LRU order
 
     def _valid(self, tok: str, now: float) -> bool:
         exp = self.tokens.get(tok)
@@ -91,13 +94,16 @@ class CSRFMiddleware:
             return False
         return True
 
+    def _touch(self, tok: str, now: float):
+        self.tokens[tok] = now + self.TTL
+        self.tokens.move_to_end(tok)
+        while len(self.tokens) > self.max_tokens:   # bounded under unauthenticated GET floods
+            self.tokens.popitem(last=False)
+
     def _issue(self, now: float) -> str:
         import secrets
-        if len(self.tokens) > 4096:   # drop expired entries before growing further
-            for k in [k for k, e in self.tokens.items() if e < now]:
-                del self.tokens[k]
         tok = secrets.token_urlsafe(24)
-        self.tokens[tok] = now + self.TTL
+        self._touch(tok, now)
         return tok
 
     async def __call__(self, scope, receive, send):
@@ -112,7 +118,7 @@ class CSRFMiddleware:
                 return await Response("Forbidden", status_code=403)(scope, receive, send)
             return await self.app(scope, receive, send)
         tok = cookie if cookie and self._valid(cookie, now) else self._issue(now)
-        self.tokens[tok] = now + self.TTL   # a token in use is refreshed
+        self._touch(tok, now)   # a token in use is refreshed
         set_cookie = f"{self.COOKIE}={tok}; Path=/; Max-Age={int(self.TTL)}; SameSite=Lax".encode()
 
         async def send_wrap(msg):

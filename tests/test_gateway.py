@@ -415,3 +415,18 @@ def test_csrf_middleware(engine, tmp_path_factory):
     app2, _ = create_app_for_engine(engine, name="tiny", app_config=ac2)
     with TestClient(app2) as c:   # off by default
         assert c.post("/v1/tokenize", json=body).status_code == 200
+
+
+def test_csrf_token_store_is_bounded():
+    """A flood of cookieless GETs cannot grow the live-token store past its cap: the least
+    recently used token goes first, and a token in use is refreshed to the front."""
+    from localai_amd.gateway.app import CSRFMiddleware
+    mw = CSRFMiddleware(app=None, max_tokens=8)
+    keep = mw._issue(0.0)
+    for i in range(100):
+        mw._issue(float(i))
+        mw._touch(keep, float(i))   # the client that keeps using its token
+    assert len(mw.tokens) == 8
+    assert mw._valid(keep, 100.0)
+    assert not mw._valid("never-issued", 0.0)
+    assert not mw._valid(keep, 1e9)   # expired
