@@ -16,11 +16,13 @@ runtime is needed.  The voice's JSON config supplies the rest of piper's contrac
   text     one utterance per sentence, joined with 0.2 s of silence
 
 Phonemes: voices with phoneme_type "text" read the text's characters (NFD, lower-cased), exactly
-as piper does.  "espeak" voices need espeak-ng, which is not in this image: their input is read
-as IPA phonemes character by character (NFD) -- pass IPA for exact pronunciation; plain text
-gives the letters' IPA readings.  Parity with real piper voices is unpinned (no voice files or
-onnxruntime here); the graph executor itself is checked against transformers' VITS exported to
-ONNX (tests/test_piper.py).
+as piper does.  "espeak" voices (every rhasspy voice in the gallery) get their phonemes from
+models/g2p_en.py, a rule-based English front end that writes espeak-ng's en-us IPA (lexicon +
+letter-to-sound rules + stress), folded onto the voice's phoneme_id_map; espeak-ng itself is not
+in this image.  Text that already holds IPA letters is read as phonemes as given; voices whose
+espeak voice is not English read the text's characters.  Parity with real piper voices is
+unpinned (no voice files, espeak-ng or onnxruntime here); the graph executor itself is checked
+against transformers' VITS exported to ONNX (tests/test_piper.py).
 """
 from __future__ import annotations
 
@@ -36,6 +38,7 @@ import torch
 PAD, BOS, EOS = "_", "^", "$"
 SENTENCE_SILENCE = 0.2
 _SENT = re.compile(r"(?<=[.!?])\s+")
+_IPA_INPUT = re.compile("[\u0250-\u02af\u02c8\u02cc\u02d0\u00e6\u00f0\u03b8\u014b]")   # IPA letters / marks
 
 
 def config_path(onnx_path: str) -> Optional[str]:
@@ -74,17 +77,30 @@ class PiperVoice:
         self.runner = OnnxRunner(path, device, generator=self.generator)
 
     # ------------------------------------------------------------------ text -> ids
+    def _g2p(self) -> bool:
+        """English espeak voice: phonemise with the en-us front end."""
+        if self.phoneme_type != "espeak":
+            return False
+        lang = str(((self.cfg.get("espeak") or {}).get("voice")) or "en-us").lower()
+        return lang.startswith("en")
+
     def phonemes(self, text: str) -> List[List[str]]:
+        from . import g2p_en
         out = []
+        g2p = self._g2p()
         for sent in _SENT.split(text.strip()):
             if not sent:
                 continue
+            if g2p and not _IPA_INPUT.search(sent):
+                sent = g2p_en.phonemize(sent)
             s = unicodedata.normalize("NFD", sent)
             if self.phoneme_type == "text":
                 s = s.lower()
             ph: List[str] = []
             for c in s:
                 ph += self.phoneme_map.get(c, [c])
+            if g2p:
+                ph = g2p_en.fold(ph, self.id_map)
             out.append(ph)
         return out
 

@@ -144,3 +144,45 @@ def test_piper_voice_on_gpu_matches_cpu(voice):
     a = PiperVoice(path, "cpu").synthesize("the quick brown fox")
     b = PiperVoice(path, "cuda:0").synthesize("the quick brown fox")
     assert a.shape == b.shape and np.abs(a - b).max() < 1e-3
+
+
+# the symbol inventory of piper's espeak-ng voices (the keys of their phoneme_id_map)
+_ESPEAK_SYMBOLS = set("_^$ !'(),-.:;?abcdefhijklmnopqrstuvwxyzæçðøħŋœǀǁǂǃɐɑɒɓɔɕɖɗɘəɚɛɜɞɟɠɡɢɣɤɥɦɧɨɪɫɬɭɮɯɰɱɲɳɴɵɶɸɹɺɻɽɾʀʁʂʃʄʈʉʊʋʌʍʎʏʐʑʒʔʕʘʙʛʜʝʟʡʢʲˈˌːˑ˞βθχᵻⱱ0123456789\"#↓↑")
+
+
+def test_g2p_english_espeak_style():
+    """espeak-type piper voices (reference backend/go/tts/piper.go:20-49 phonemises through
+    espeak-ng) get en-us IPA from the rule-based front end: dictionary readings of common words,
+    letter-to-sound rules with stress and the en-us flap, numbers read out, and every emitted
+    phoneme inside the espeak voices' inventory.  Parity with espeak-ng itself is unpinned."""
+    from localai_amd.models.g2p_en import fold, phonemize
+    assert phonemize("Hello world!") == "həlˈoʊ wˈɜːld!"
+    assert phonemize("This is a test.") == "ðɪs ɪz ɐ tˈɛst."
+    rules = {"cat": "kˈæt", "phone": "fˈoʊn", "sing": "sˈɪŋ", "nation": "nˈeɪʃən", "school": "skˈuːl",
+             "night": "nˈaɪt", "jumped": "dʒˈʌmpt", "fishes": "fˈɪʃɪz", "better": "bˈɛɾɚ", "dogs": "dˈɑːɡz",
+             "information": "ɪnfɚmˈeɪʃən", "21": "twˈɛnti wˈʌn"}
+    for w, ipa in rules.items():
+        assert phonemize(w) == ipa, (w, phonemize(w))
+    text = ("The quick brown fox jumps over the lazy dog. She sells 42 sea shells by the sea shore; "
+            "LocalAI serves OpenAI-compatible requests & streams tokens (quickly)!")
+    ipa = phonemize(text)
+    assert set(ipa) <= _ESPEAK_SYMBOLS, set(ipa) - _ESPEAK_SYMBOLS
+    # a voice without r-coloured schwa or length marks gets them folded onto what it has
+    small = {"ə": [1], "ɹ": [2], "t": [3], "ˈ": [4], "b": [5], "ɛ": [6], "ɾ": [7]}
+    assert fold(list("bˈɛɾɚ"), small) == ["b", "ˈ", "ɛ", "ɾ", "ə", "ɹ"]
+    assert fold(list("tːɾ"), {"t": [1]}) == ["t", "t"]
+
+
+def test_piper_espeak_voice_uses_g2p(voice):
+    from localai_amd.models.g2p_en import fold, phonemize
+    from localai_amd.models.piper import PiperVoice
+    path, _ = voice
+    v = PiperVoice(path, "cpu")
+    v.phoneme_type = "espeak"
+    (ph,) = v.phonemes("hello world")
+    assert ph == fold(list(phonemize("hello world")), v.id_map)
+    (raw,) = v.phonemes("həlˈoʊ")   # IPA input is read as given
+    assert raw == fold(list("həlˈoʊ"), v.id_map)
+    v.cfg["espeak"] = {"voice": "de"}   # not English: characters as before
+    (de,) = v.phonemes("hallo")
+    assert de == list("hallo")
