@@ -49,12 +49,10 @@ def lib():
         sig = {
             "la_qgemm_skinny": [I, P, P, P, P, I, I, P, I, I, I, P, I, LNG, P],
             "la_qgemv_dp4": [I, P, P, P, I, P, I, I, I, P, I, LNG, P, LNG, I, P, I, P],
-            "la_qgemv_dp4_red": [I, P, P, P, I, P, I, I, I, P, I, LNG, P, LNG, I, P, I, P, P],
             "la_moe_gemv": [I, I, P, I, I, I, P, I, I, P, I, I, P, LNG, I, I, P, P, I, LNG, P],
             "la_gemv_variant": [I],
             "la_moe_tune": [I, I],
             "la_dec_one_part": [I],
-            "la_moe_gemv_variant": [I],
             "la_gather_rows": [P, P, LNG, P, P, LNG, P],
             "la_qgemv_dp4_rope": [I, P, P, P, I, P, I, P, P, P, I, I, I, P, P, P, I, P],
             "la_qgemv_dp4_norm": [I, P, P, P, I, I, I, P, I, LNG, P, P, LNG, I, P, P, F, P, P],
@@ -1917,13 +1915,14 @@ MOE32 = os.environ.get("LOCALAI_AMD_MOE32", "1") == "1"
 # T = 16 / 24 / 32: var 9 232 / 234 / 237 us vs 266 / 315 / 317; T = 8: 221 vs 212
 # (gpurun_out/r5_moe_small.log)
 MOE32_MIN_T = int(os.environ.get("LOCALAI_AMD_MOE32_MIN_T", "12"))
-MOE32_SMALL_T = 96     # below: var 9 (32-row tiles); from here: var 4
+MOE32_SMALL_T = 48     # below: var 9 (32-row tiles); from here: var 17 (64-row chunks, live row blocks)
+MOE32_LIVE_BIG_T = 192  # from here: var 15 (one 128-row chunk per expert at top-2 of 8)
 MOE32_VAR_GLU = int(os.environ.get("LOCALAI_AMD_MOE32_VAR_GLU", "-1"))     # -1: by batch
 MOE32_VAR_DOWN = int(os.environ.get("LOCALAI_AMD_MOE32_VAR_DOWN", "-1"))
 MOE32_SPLITS = int(os.environ.get("LOCALAI_AMD_MOE32_SPLITS", "0"))   # 0: picked from the tile count
 MOE32_TILES = {0: (64, 128), 1: (64, 128), 2: (64, 256), 3: (64, 256), 4: (64, 256), 5: (32, 128), 6: (128, 128),
                7: (64, 128), 8: (64, 128), 9: (32, 128), 10: (32, 256), 11: (64, 256), 12: (32, 256),
-               13: (64, 128), 14: (32, 256)}
+               13: (64, 128), 14: (32, 256), 15: (128, 256), 16: (128, 128), 17: (64, 256), 18: (128, 128)}
 _MOE32_FMTS = (FMT_Q4_K, FMT_Q6_K, FMT_Q8_0)
 
 
@@ -1953,9 +1952,13 @@ def moe_glu32(x: torch.Tensor, mw: "MoEWeights", order: torch.Tensor, off: torch
 def _moe32_var(env: int, T: int, fmt: int = FMT_Q4_K, down: bool = False) -> int:
     if env >= 0:
         return env
-    # (Q6_K down on var 8 timed 255 vs 281 us in isolation at T = 256 -- r5_moe_q6.log -- but the
-    # engine did not move: Mixtral C=256 8140 vs 8198 tok/s, r5_mx256_*.log)
-    return 9 if T < MOE32_SMALL_T else 4
+    # live-row-block variants (profiles/r6_moe_live.md, Mixtral-8x7B shapes, cold weights): T = 256
+    # var 15 (128-row chunks, 8 waves) glu 249 + down 119 us vs var 4's 315 + 170; T = 64 / 128
+    # var 17 (64-row chunks) 167 + 82 / 172 + 86 vs var 9's 166 + 91 / var 4's 180 + 91; below
+    # MOE32_SMALL_T var 9 (32-row tiles, 4 workgroups per CU) stays for the smallest batches
+    if T >= MOE32_LIVE_BIG_T:
+        return 15
+    return 9 if T < MOE32_SMALL_T else 17
 
 
 def _moe32_splits(mw: "MoEWeights", T: int, topk: int, var: int) -> int:

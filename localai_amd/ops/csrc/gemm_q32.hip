@@ -104,7 +104,9 @@ template <> struct Q32F<FMT_Q4_K> {
   LA_DEV static bf16x8 deq(const St& st) {
     const uint32_t w0 = (S & 1) ? st.q.z : st.q.x, w1 = (S & 1) ? st.q.w : st.q.y;
     uint32_t lo, hi;
-    // opaque masks: one v_cvt_f32_ubyteN per weight
+    // opaque masks: one v_cvt_f32_ubyteN per weight (a packed v_cvt_pk_f32_fp8 + v_pk_fma_f32 form,
+    // 1.75 VALU per weight, was no faster on moe32 / the C=256 step and miscomputed the 64-column
+    // variants: profiles/r6_moe_live.md)
     if constexpr (S < 2) {
       asm("v_and_b32 %0, 0x0f0f0f0f, %1" : "=v"(lo) : "v"(w0));
       asm("v_and_b32 %0, 0x0f0f0f0f, %1" : "=v"(hi) : "v"(w1));
@@ -268,7 +270,10 @@ LA_DEV float q32_gelu_tanh(float x) { return 0.5f * x * (1.f + tanhf(0.797884560
 
 // One (M tile, N tile, K split).  GLU: columns [0, BN/2) of the tile are gate rows, [BN/2, BN)
 // the matching up rows; no split.
-template <int FMT, int BM, int WN, int NS, bool GLU, int PIPE = 0, int NW_ = 4, int ABL = 0, int MOE = 0>
+// MBL (<= BM / 32): row blocks that hold rows of this tile; the MFMAs and A-fragment reads of the
+// blocks past it are not issued (grouped MoE tiles: an expert's last row chunk is often short).
+template <int FMT, int BM, int WN, int NS, bool GLU, int PIPE = 0, int NW_ = 4, int ABL = 0, int MOE = 0,
+          int MBL = BM / 32>
 LA_DEV void q32_tile(uint8_t* __restrict__ lds, const QW& w, int tile, const bf16* __restrict__ X, int ldx, int M,
                      int per_split, int m_tiles, int n_tiles, float* __restrict__ out, bf16* __restrict__ outb,
                      int ldo, long slab, const Q32Glu& glu, const Q32Moe& moe = Q32Moe{}) {
@@ -277,6 +282,7 @@ LA_DEV void q32_tile(uint8_t* __restrict__ lds, const QW& w, int tile, const bf1
   constexpr int NW = G::NW, BN = G::BN, MB = BM / 32, CB = WN / 32;
   constexpr int XB = G::XB, SLOT = G::SLOT, PX = G::PX, PR = G::PR, PS = G::PS, L = G::L;
   static_assert(WN % 32 == 0 && BM % 32 == 0 && PR * 1024 == G::RW && PS * 256 == G::SW, "geometry");
+  static_assert(MBL >= 1 && MBL <= MB, "live row blocks");
   static_assert(NS >= 2 && NS <= 8 && NS * SLOT <= 163840, "ring");
 
   const int mt_i = tile % m_tiles;
@@ -359,7 +365,7 @@ LA_DEV void q32_tile(uint8_t* __restrict__ lds, const QW& w, int tile, const bf1
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
-      for (int mb = 0; mb < MB; ++mb) {
+      for (int mb = 0; mb < MBL; ++mb) {
         if constexpr (ABL & 8) asm volatile("; probe: no A read" : "=v"(dst[s][mb]));
         else dst[s][mb] = *(const bf16x8*)(sl + mb * 4096 + aoff[s0 + s]);
       }
@@ -374,7 +380,7 @@ LA_DEV void q32_tile(uint8_t* __restrict__ lds, const QW& w, int tile, const bf1
   auto mm = [&](const bf16x8 (&a)[MB], const bf16x8 (&b)[CB]) {
     if constexpr (LA_SETPRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int mb = 0; mb < MB; ++mb)
+    for (int mb = 0; mb < MBL; ++mb)
 #pragma unroll
       for (int cb = 0; cb < CB; ++cb) {
         if constexpr (ABL & 1) asm volatile("; probe: no MFMA" ::"v"(a[mb]), "v"(b[cb]));
@@ -439,9 +445,9 @@ LA_DEV void q32_tile(uint8_t* __restrict__ lds, const QW& w, int tile, const bf1
     // between the MFMAs of the current one, and the LDS reads are threaded between MFMAs, so
     // neither the dequant VALU nor the read issue serialises with the matrix pipe.  The last
     // K-step is peeled so the loop body has no branch around MFMAs (the accumulators stay put).
-    constexpr int NM = MB * CB;                      // MFMAs per sub-step
+    constexpr int NM = MBL * CB;                     // MFMAs per sub-step
     constexpr int VPM = (24 * CB + NM - 1) / NM;     // dequant VALU per MFMA slot
-    constexpr int RPM = (2 * MB + NM - 1) / NM;      // LDS reads per MFMA slot
+    constexpr int RPM = (2 * MBL + NM - 1) / NM;     // LDS reads per MFMA slot
     bf16x8 b0[CB];
     deqs(b0, st, S0{});
     auto first_half = [&](int t, bf16x8 (&b2)[CB], bf16x8 (&b3)[CB]) {
@@ -743,10 +749,11 @@ static int q32_launch_glu(int var, const QW& wa, const Q32Glu& glu, const bf16* 
 // weight) with the GLU fused, bf16 h rows in grouped order (row off[e] + m); MODE 2: down
 // projection of the grouped h rows, routing-weighted fp32 output scattered to slab
 // (split * topk + slot) row token.  qws[e] = {codes, aux, blocked scale plane, -, N, K}.
-template <class C, int OCC_, int NS_ = 0>
+template <class C, int OCC_, int NS_ = 0, bool LIVE_ = false>
 struct MoeCfg : C {
   static constexpr int OCC = OCC_;  // workgroups per CU the register budget is sized for
   static constexpr int NS = NS_;    // ring slots (0: q32_ns, <= 4); up to 8 stages of weight bytes in flight
+  static constexpr bool LIVE = LIVE_;  // MFMAs of the chunk's live row blocks only (per-tile dispatch)
 };
 
 template <int FMT, class C, int MODE, int ABL = 0>
@@ -775,14 +782,33 @@ __global__ __launch_bounds__(C::NW * 64) __attribute__((amdgpu_waves_per_eu(C::N
   const int t2 = chunk + mte * (nt + n_tiles * split);
   QW w = qws[e];
   const Q32Moe mo{order + o0, topk, wts};
-  if constexpr (MODE == 1) {
-    const Q32Glu glu{w, 0, F, F, act};
-    w.N = F;
-    q32_tile<FMT, C::BM, C::WN, NS, true, C::PIPE, C::NW, ABL, 1>(lds, w, t2, X, ldx, Me, w.K >> 6, mte, n_tiles,
-                                                               nullptr, outb + (size_t)o0 * ldo, ldo, 0, glu, mo);
+  // row blocks of this chunk that hold rows: the tile runs only their MFMAs (wave-uniform)
+  const int live = min(C::BM / 32, (Me - chunk * C::BM + 31) / 32);
+  auto run = [&](auto mbl_) {
+    constexpr int MBL = decltype(mbl_)::value;
+    if constexpr (MODE == 1) {
+      const Q32Glu glu{w, 0, F, F, act};
+      QW wg = w;
+      wg.N = F;
+      q32_tile<FMT, C::BM, C::WN, NS, true, C::PIPE, C::NW, ABL, 1, MBL>(lds, wg, t2, X, ldx, Me, w.K >> 6, mte,
+                                                                        n_tiles, nullptr, outb + (size_t)o0 * ldo,
+                                                                        ldo, 0, glu, mo);
+    } else {
+      q32_tile<FMT, C::BM, C::WN, NS, false, C::PIPE, C::NW, ABL, 2, MBL>(lds, w, t2, X + (size_t)o0 * ldx, ldx, Me,
+                                                                         per_split, mte, n_tiles, out, nullptr, ldo,
+                                                                         slab, Q32Glu{}, mo);
+    }
+  };
+  if constexpr (C::LIVE && C::BM / 32 >= 4) {
+    if (live <= 1) run(std::integral_constant<int, 1>{});
+    else if (live == 2) run(std::integral_constant<int, 2>{});
+    else if (live == 3) run(std::integral_constant<int, 3>{});
+    else run(std::integral_constant<int, C::BM / 32>{});
+  } else if constexpr (C::LIVE && C::BM / 32 >= 2) {
+    if (live <= 1) run(std::integral_constant<int, 1>{});
+    else run(std::integral_constant<int, C::BM / 32>{});
   } else {
-    q32_tile<FMT, C::BM, C::WN, NS, false, C::PIPE, C::NW, ABL, 2>(lds, w, t2, X + (size_t)o0 * ldx, ldx, Me, per_split,
-                                                                mte, n_tiles, out, nullptr, ldo, slab, Q32Glu{}, mo);
+    run(std::integral_constant<int, C::BM / 32>{});
   }
 }
 
@@ -805,6 +831,12 @@ static int moe32_var(int var, Fn&& fn) {
     case 12: fn(MoeCfg<Q32Cfg<32, 64, 4, 0>, 2, 5>{}); break;
     case 13: fn(MoeCfg<Q32Cfg<64, 32, 4, 0>, 1, 8>{}); break;
     case 14: fn(MoeCfg<Q32Cfg<32, 64, 4, 0>, 1, 8>{}); break;
+    // live-row-block dispatch: one 96..128-row chunk per expert at decode batches, MFMAs of its
+    // live 32-row blocks only (an expert's weights dequantised once, not once per 64 rows)
+    case 15: fn(MoeCfg<Q32Cfg<128, 32, 8, 0>, 1, 0, true>{}); break;
+    case 16: fn(MoeCfg<Q32Cfg<128, 32, 4, 0>, 1, 0, true>{}); break;
+    case 17: fn(MoeCfg<Q32Cfg<64, 32, 8, 0>, 2, 0, true>{}); break;
+    case 18: fn(MoeCfg<Q32Cfg<128, 32, 4, 1>, 1, 0, true>{}); break;
     default: return -1;
   }
   return 0;

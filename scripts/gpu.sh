@@ -12,7 +12,9 @@
 #   final                      tests + smoke + bench twice (the round-end sequence)
 #   prof [bench.py args]       rocprofv3 --kernel-trace --stats over a short bench; stats copied
 #   pmc <driver.py>            counter passes over a launch driver (scripts/gpu_pmc_run.sh)
-#   arrivals [rates...]        open-loop Poisson arrivals (bench.py --arrival-rate), default 90 60
+#   arrivals [rates...]        open-loop Poisson arrivals (bench.py --arrival-rate), default 90 60,
+#                              burst heuristics on and off
+#   mixtral                    Mixtral-8x7B HTTP C=256 + engine C=1
 #   ab <ENV=val> [bench args]  the headline bench with and without one environment setting
 #   tp                         TP tests on one card (ranks share the GPU) + the sampling rehearsal
 #   gemm [bs_bench.py args]    decode / prefill GEMM microbenchmarks (scripts/bs_bench.py)
@@ -68,10 +70,25 @@ case $task in
   pmc)
     bash scripts/gpu_pmc_run.sh "$1" "$O" ;;
   arrivals)
+    # each rate with the burst heuristics (admission window, prefill-first) on, then off
     rates=${*:-90 60}
     for rate in $rates; do
-      run_bench "r$rate" --warmup 1 --arrival-rate "$rate" --requests $((rate * 10)) || exit 1
+      run_bench "r${rate}_on" --warmup 1 --arrival-rate "$rate" --requests $((rate * 10)) || exit 1
+      LOCALAI_AMD_ADMIT_WINDOW_MS=0 LOCALAI_AMD_PREFILL_FIRST_MS=0 \
+        run_bench "r${rate}_off" --warmup 1 --arrival-rate "$rate" --requests $((rate * 10)) || exit 1
     done ;;
+  mixtral)
+    # BASELINE config 4's model: HTTP C=256 (headline layout), engine C=1; extra args go to the
+    # C=256 run (e.g. an A/B setting through env)
+    run_bench mx_http --preset mixtral-8x7b --steps 2 --warmup 1 "$@" &&
+      run_bench mx_c1 --preset mixtral-8x7b --mode engine --concurrency 1 --steps 2 --warmup 1 ;;
+  mixtral_ab)
+    # Mixtral HTTP C=256 with the MoE variants pinned by one env setting, then the defaults
+    setting=$1
+    env $setting timeout -k 10 600 python -u bench.py --preset mixtral-8x7b --steps 2 --warmup 1 \
+      > "$O/mx_ab.log" 2> "$O/mx_ab.err"
+    rc=$?; echo "$setting rc=$rc"; tail -1 "$O/mx_ab.log"; [ $rc -ne 0 ] && exit $rc
+    run_bench mx_http --preset mixtral-8x7b --steps 2 --warmup 1 ;;
   ab)
     setting=$1
     shift

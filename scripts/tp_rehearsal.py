@@ -79,10 +79,15 @@ def main():
                 rows += 1
                 if a_ids[j] != b_ids[j]:
                     break  # the prefixes differ from here on
-            assert rows >= MIN_ROWS, f"only {rows} rows share a prefix with TP=1"
+            # a sampled stream may part at any draw whose uniform falls within the logits' rounding
+            # difference of a CDF boundary; the sampler itself is pinned on identical logits in
+            # tests/test_tp_sample_gpu.py, so here only the rows up to the parting are compared
+            assert rows >= (1 if sampling else MIN_ROWS), f"only {rows} rows share a prefix with TP=1"
             total += rows
         assert tp.car is not None and not tp.car.timed_out(), "custom all-reduce unavailable or timed out"
         same = sum(int(o["token_ids"] == r["token_ids"]) for o, r in zip(outs, refs))
+        if sampling:
+            assert same >= 1 and total >= MIN_ROWS * len(outs) // 2, (same, total)
         print(f"TP_ROWS world={world} graphs={graphs} sampling={sampling} rows={total} worst_cos={worst_cos:.6f} "
               f"worst_rel={worst_rel:.2e} identical_streams={same}/{len(outs)}", flush=True)
         print("TP_OK", flush=True)
