@@ -37,11 +37,14 @@ TP_OVERLAP_ROWS = int(os.environ.get("LOCALAI_AMD_TP_OVERLAP_ROWS", "1024"))
 TP_OVERLAP_CHUNKS = int(os.environ.get("LOCALAI_AMD_TP_OVERLAP_CHUNKS", "4"))
 # MoE decode batches route with the fused router kernel (moe.hip); =1 falls back to the torch ops
 FUSED_ROUTER_OFF = os.environ.get("LOCALAI_AMD_FUSED_ROUTER_OFF", "0") == "1"
-# prefill chunks of at least this many tokens whose experts the grouped bs tile cannot run
-# (ops.moe_bs_ok: formats / shapes) run each expert as a dense GEMM over its gathered rows (~T *
-# topk / E rows: the library prefill path, weights dequantised once per expert, one host read of
-# the grouping) instead of the decode-shaped grouped kernel, which streams weights once per 64 rows
-MOE_DENSE_MIN_T = int(os.environ.get("LOCALAI_AMD_MOE_DENSE_MIN_T", "1024"))
+# prefill chunks of at least this many tokens run each expert as a dense GEMM over its gathered
+# rows (~T * topk / E rows: weights dequantised once per expert + the library GEMM, one host read
+# of the grouping).  Below it every batch runs the grouped moe32 tiles (no host sync).  Measured
+# on Mixtral-8x7B shapes (profiles/r6_moe_live.md): T = 8192 dense 6.36 ms vs grouped moe32 7.42 /
+# bs 7.65; T = 4096 grouped moe32 3.53 ms vs dense 4.06; T = 1024 1.07 vs 1.85; HTTP C=256
+# 10.61 k tok/s / p50 TTFT 1128 ms with dense 8192-token chunks vs 10.14 k / 1245 ms on the
+# grouped bs tile
+MOE_DENSE_MIN_T = int(os.environ.get("LOCALAI_AMD_MOE_DENSE_MIN_T", "6144"))
 
 _ACT = {"swiglu": ops.ACT_SWIGLU, "gelu": ops.ACT_GELU, "geglu": ops.ACT_GEGLU}
 

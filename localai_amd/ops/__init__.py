@@ -1916,13 +1916,14 @@ MOE32 = os.environ.get("LOCALAI_AMD_MOE32", "1") == "1"
 # (gpurun_out/r5_moe_small.log)
 MOE32_MIN_T = int(os.environ.get("LOCALAI_AMD_MOE32_MIN_T", "12"))
 MOE32_SMALL_T = 48     # below: var 9 (32-row tiles); from here: var 17 (64-row chunks, live row blocks)
-MOE32_LIVE_BIG_T = 192  # from here: var 15 (one 128-row chunk per expert at top-2 of 8)
+MOE32_LIVE_BIG_T = 192  # from here: var 19 (one 128-row chunk per expert at top-2 of 8)
 MOE32_VAR_GLU = int(os.environ.get("LOCALAI_AMD_MOE32_VAR_GLU", "-1"))     # -1: by batch
 MOE32_VAR_DOWN = int(os.environ.get("LOCALAI_AMD_MOE32_VAR_DOWN", "-1"))
 MOE32_SPLITS = int(os.environ.get("LOCALAI_AMD_MOE32_SPLITS", "0"))   # 0: picked from the tile count
 MOE32_TILES = {0: (64, 128), 1: (64, 128), 2: (64, 256), 3: (64, 256), 4: (64, 256), 5: (32, 128), 6: (128, 128),
                7: (64, 128), 8: (64, 128), 9: (32, 128), 10: (32, 256), 11: (64, 256), 12: (32, 256),
-               13: (64, 128), 14: (32, 256), 15: (128, 256), 16: (128, 128), 17: (64, 256), 18: (128, 128)}
+               13: (64, 128), 14: (32, 256), 15: (128, 256), 16: (128, 128), 17: (64, 256), 18: (128, 128),
+               19: (128, 512), 20: (128, 256)}
 _MOE32_FMTS = (FMT_Q4_K, FMT_Q6_K, FMT_Q8_0)
 
 
@@ -1945,7 +1946,7 @@ def moe_glu32(x: torch.Tensor, mw: "MoEWeights", order: torch.Tensor, off: torch
     a = {ACT_SWIGLU: 0, ACT_GEGLU: 3}[act]
     _check(lib().la_moe32(mw.fmt, 1, mw.desc32().data_ptr(), F, mw.K, mw.E, order.data_ptr(), off.data_ptr(), topk,
                           x.data_ptr(), x.shape[1], T, 1, None, h.data_ptr(), F, 0, a,
-                          _moe32_var(MOE32_VAR_GLU, T) if var is None else var, _stream()), "la_moe32")
+                          _moe32_var(MOE32_VAR_GLU, T, mw.fmt) if var is None else var, _stream()), "la_moe32")
     return h
 
 
@@ -1953,11 +1954,13 @@ def _moe32_var(env: int, T: int, fmt: int = FMT_Q4_K, down: bool = False) -> int
     if env >= 0:
         return env
     # live-row-block variants (profiles/r6_moe_live.md, Mixtral-8x7B shapes, cold weights): T = 256
-    # var 15 (128-row chunks, 8 waves) glu 249 + down 119 us vs var 4's 315 + 170; T = 64 / 128
+    # var 19 (128-row chunks, 8 waves x 64 columns) glu 244 + down 118 us vs var 15's 280 + 131 on
+    # the same box and var 4's 315 + 170 on another; T = 64 / 128
     # var 17 (64-row chunks) 167 + 82 / 172 + 86 vs var 9's 166 + 91 / var 4's 180 + 91; below
     # MOE32_SMALL_T var 9 (32-row tiles, 4 workgroups per CU) stays for the smallest batches
     if T >= MOE32_LIVE_BIG_T:
-        return 15
+        # var 19's 64-column waves spill with Q6_K / Q8_0 fragments (the launcher maps them to 15)
+        return 19 if fmt == FMT_Q4_K else 15
     return 9 if T < MOE32_SMALL_T else 17
 
 
@@ -1995,7 +1998,9 @@ def moe_down32(h: torch.Tensor, mw: "MoEWeights", order: torch.Tensor, off: torc
 # routed rows in ONE launch per projection, 256-row tiles (an expert's weights stream once per 256
 # rows, not once per 64 as on moe32), grid sized for any routing -- no host read of the grouping.
 # Prefill chunks (T >= MOE_BS_MIN_T tokens); decode batches stay on moe32.
-MOE_BS = os.environ.get("LOCALAI_AMD_MOE_BS", "1") == "1"
+# opt-in: slower than both the grouped moe32 tiles and the dense per-expert path on Mixtral-8x7B
+# prefill chunks (profiles/r6_moe_live.md)
+MOE_BS = os.environ.get("LOCALAI_AMD_MOE_BS", "0") == "1"
 MOE_BS_MIN_T = int(os.environ.get("LOCALAI_AMD_MOE_BS_MIN_T", "512"))
 MOE_BS_VAR = int(os.environ.get("LOCALAI_AMD_MOE_BS_VAR", "0"))
 

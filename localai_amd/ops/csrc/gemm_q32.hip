@@ -813,7 +813,7 @@ __global__ __launch_bounds__(C::NW * 64) __attribute__((amdgpu_waves_per_eu(C::N
 }
 
 // MoE variant ids (ops/__init__.py MOE32_TILES): row tile x (waves x columns per wave), schedule
-template <class Fn>
+template <bool Q4, class Fn>
 static int moe32_var(int var, Fn&& fn) {
   switch (var) {
     case 0: fn(MoeCfg<Q32Cfg<64, 32, 4, 0>, 2>{}); break;
@@ -837,6 +837,10 @@ static int moe32_var(int var, Fn&& fn) {
     case 16: fn(MoeCfg<Q32Cfg<128, 32, 4, 0>, 1, 0, true>{}); break;
     case 17: fn(MoeCfg<Q32Cfg<64, 32, 8, 0>, 2, 0, true>{}); break;
     case 18: fn(MoeCfg<Q32Cfg<128, 32, 4, 1>, 1, 0, true>{}); break;
+    // 64 columns per wave: twice the weight bytes per ring stage against the same X stage (the
+    // 128-row X slab is most of a stage), so twice the weight bytes in flight per CU
+    case 19: if constexpr (Q4) fn(MoeCfg<Q32Cfg<128, 64, 8, 0>, 1, 0, true>{}); else return -1; break;
+    case 20: if constexpr (Q4) fn(MoeCfg<Q32Cfg<128, 64, 4, 0>, 1, 0, true>{}); else return -1; break;
     default: return -1;
   }
   return 0;
@@ -847,7 +851,10 @@ static int moe32_launch(int var, const QW* qws, int N, int K, int E, const int* 
                         const bf16* X, int ldx, int maxM, int splits, const float* wts, float* out, bf16* outb,
                         int ldo, long slab, int act, hipStream_t st) {
   const int KS = K >> 6, per = (KS + splits - 1) / splits;
-  return moe32_var(var, [&](auto c) {
+  // 64 columns per wave at 128 rows spill with Q6_K / Q8_0's larger fragment state: those formats
+  // take the 32-column form of the same chunking
+  if (FMT != FMT_Q4_K && (var == 19 || var == 20)) var -= 4;
+  return moe32_var<FMT == FMT_Q4_K>(var, [&](auto c) {
     using C = decltype(c);
     const int mch = (maxM + C::BM - 1) / C::BM;
     const int n_tiles = MODE == 1 ? (N + C::BN / 2 - 1) / (C::BN / 2) : (N + C::BN - 1) / C::BN;

@@ -124,10 +124,10 @@ def prefill(a, mg, md, E, topk, D, F):
             t2 = timeit(lambda: ops.moe_down_bs(h, md, order, off, topk, T, wts, var=v))
             print(f"T={T} bs var {v}: {t:.1f} us ({flops / t / 1e6:.0f} TF/s; glu {t1:.1f} + down {t2:.1f})  "
                   f"rel-L2 vs dense {rel:.2e}", flush=True)
-        v = 4
-        t = timeit(lambda: ops.moe_down32(ops.moe_glu32(x, mg, order, off, topk, T, var=v), md, order, off, topk, T,
-                                          wts, var=v))
-        print(f"T={T} moe32 var {v}: {t:.1f} us ({flops / t / 1e6:.0f} TF/s)", flush=True)
+        for v in (15, 19):
+            t = timeit(lambda: ops.moe_down32(ops.moe_glu32(x, mg, order, off, topk, T, var=v), md, order, off, topk,
+                                              T, wts, var=v))
+            print(f"T={T} moe32 var {v}: {t:.1f} us ({flops / t / 1e6:.0f} TF/s)", flush=True)
 
 
 if __name__ == "__main__":

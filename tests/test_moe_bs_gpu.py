@@ -87,10 +87,12 @@ def test_moe_bs_graph_replay_new_routing():
 
 
 def test_decoder_moe_prefill_bs_matches_dense(tmp_path, monkeypatch):
-    """A Mixtral-shaped layer on a prefill-sized chunk: the grouped bs path (one launch per
-    projection, no host sync) and the dense per-expert path agree."""
+    """A Mixtral-shaped layer on a prefill-sized chunk: the grouped bs path (opt-in, one launch per
+    projection, no host sync), the default grouped moe32 path below MOE_DENSE_MIN_T and the dense
+    per-expert path agree."""
     from localai_amd.engine.llm_engine import EngineConfig, LLMEngine
     from localai_amd.models import decoder, synth
+    monkeypatch.setattr(ops, "MOE_BS", True)
     p = str(tmp_path / "mx.gguf")
     synth.write_model(p, "tiny-mixtral")
     eng = LLMEngine(EngineConfig(model_path=p, device="cuda:0", context_size=512, max_num_seqs=4,
@@ -108,7 +110,13 @@ def test_decoder_moe_prefill_bs_matches_dense(tmp_path, monkeypatch):
     a = ops.reduce(m._moe(L, xn)).float()
     assert calls, "the grouped bs path did not run"
     monkeypatch.setattr(ops, "MOE_BS", False)
+    g32 = []
+    orig32 = ops.moe_glu32
+    monkeypatch.setattr(ops, "moe_glu32", lambda *a, **k: g32.append(1) or orig32(*a, **k))
+    c = ops.reduce(m._moe(L, xn)).float()   # T < MOE_DENSE_MIN_T: grouped moe32
+    assert g32, "the grouped moe32 path did not run"
     monkeypatch.setattr(decoder, "MOE_DENSE_MIN_T", 1)
     b = ops.reduce(m._moe(L, xn)).float()
-    rel = ((a - b).norm() / b.norm()).item()
-    assert rel < 1e-2, rel
+    for got in (a, c):
+        rel = ((got - b).norm() / b.norm()).item()
+        assert rel < 1e-2, rel
