@@ -45,6 +45,8 @@ from ..utils import faults
 from ..utils.trace import get_tracer, roctx
 
 log = logging.getLogger("localai_amd.engine")
+# multi-step decode runs stream each step's tokens as its event fires (LLMEngine._run_streamed)
+STREAM_STEPS = os.environ.get("LOCALAI_AMD_STREAM_STEPS", "1") == "1"
 
 
 @dataclass
@@ -1200,16 +1202,88 @@ class LLMEngine:
             graph.replay()
             self._sample_and_emit(ids, logits[:B])
             return
-        for _ in range(K):
-            graph.replay()
-        hist = st["hist"][:K, :B].cpu().numpy()  # the only sync per K steps
+        if K > 1 and STREAM_STEPS and st.get("rec") is None and self.device.type == "cuda":
+            self._run_streamed(graph, st, reqs, K)
+        else:
+            for _ in range(K):
+                graph.replay()
+            hist = st["hist"][:K, :B].cpu().numpy()  # the only sync per K steps
+            self._emit_run(reqs, hist, K, st.get("rec"))
         if any(r.params.mirostat == 2 for r in reqs):
             muh = st["mu"][:B].cpu().numpy()
             for j, r in enumerate(reqs):
                 r.mu = float(muh[j])
-        self._emit_run(reqs, hist, K, st.get("rec"))
 
     _REASONS = {1: ("stop", True), 2: ("stop", False), 3: ("length", True), 4: ("abort", True)}
+
+    def _run_streamed(self, graph, st, reqs: List[Request], K: int):
+        """A K-step device run whose tokens reach the clients step by step.  Every replay is
+        followed by an async copy of its token row into pinned host memory and an event; the host
+        emits step k (native detokenise / stop strings / SSE writes) as soon as that event fires,
+        while the device computes steps k+1.., so the run still costs one host round trip but
+        streams at the step interval: p99 inter-token latency is about one decode step instead of
+        K of them (profiles/r6_arrivals.md).  Request bookkeeping (scheduler run, finish) happens
+        once at the end of the run, as in _emit_run."""
+        B = len(reqs)
+        hist = st["hist"]
+        pin = st.get("hist_pin")
+        if pin is None or pin.shape != hist.shape:
+            pin = st["hist_pin"] = torch.empty(hist.shape, dtype=hist.dtype, pin_memory=True)
+            st["hist_ev"] = [torch.cuda.Event() for _ in range(hist.shape[0])]
+        evs = st["hist_ev"]
+        for k in range(K):
+            graph.replay()
+            pin[k].copy_(hist[k], non_blocking=True)
+            evs[k].record()
+        pn = pin.numpy()
+        stt = np.zeros((B, 5), dtype=np.int32)
+        for j, r in enumerate(reqs):
+            stt[j] = (r.n_gen, r.params.max_tokens, r.n_prompt, 1 if r.params.ignore_eos else 0, 0 if r.done else 1)
+        streams, sinks = [r.stream for r in reqs], [r.sink for r in reqs]
+        tot = np.zeros(B, dtype=np.int32)
+        why = np.zeros(B, dtype=np.int32)
+        for k in range(K):
+            evs[k].synchronize()   # releases the GIL while the device works on step k
+            n_acc, reason, texts = core.emit_run(np.ascontiguousarray(pn[k:k + 1, :B]), 1, B, streams, sinks, stt,
+                                                 self._eog_list, self.ctx)
+            n_acc = np.asarray(n_acc, dtype=np.int32)
+            reason = np.asarray(reason, dtype=np.int32)
+            first = np.nonzero((tot == 0) & (n_acc > 0))[0]
+            if len(first):
+                now = time.perf_counter()
+                for j in first:
+                    r = reqs[j]
+                    if r.first_token_t == 0.0 and not r.done:
+                        r.first_token_t = now
+                        if self.tracer is not None:
+                            self.tracer.instant("first_token", now, cat="request", tid=1, id=r.id,
+                                                correlation_id=r.params.correlation_id)
+            tot += n_acc
+            stt[:, 0] += n_acc
+            ended = (reason != 0) & (why == 0)
+            why[ended] = reason[ended]
+            stt[reason != 0, 4] = 0
+            for j, t in enumerate(texts):
+                if t and not reqs[j].done:
+                    reqs[j].callback(Event(text=t, token=-1))
+            if not stt[:, 4].any():
+                break   # every row has finished: the remaining steps carry nothing to emit
+        for j, r in enumerate(reqs):
+            n = int(tot[j])
+            if r.done or n == 0:
+                continue
+            r.n_gen += n
+            self.metrics["gen_tokens"] += n
+            if r.out_ids is not None:
+                r.out_ids.extend(int(t) for t in pn[:n, j])
+            rs = int(why[j])
+            if rs == 0:
+                self.sched.append_run(r.id, pn[:n, j].tolist())
+            else:
+                why_s, flush = self._REASONS[rs]
+                self._finish(r, why_s, flush=flush)
+        if not evs[K - 1].query():
+            evs[K - 1].synchronize()   # an early break: the run's last steps still finish first
 
     def _grammar_run(self, graph, st, reqs, grows, gslot, K: int, V: int):
         """K device steps with grammar rows masked in the graph: each row's mask slot follows the

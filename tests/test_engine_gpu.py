@@ -37,12 +37,16 @@ def _run(eng, prompts, **sp):
                                      ignore_eos=True),
                                 dict(max_tokens=12, temperature=1.0, mirostat=2, seed=3, ignore_eos=True)])
 def test_multistep_decode_matches_single_step(tiny_model_path, sp):
+    """K-step device runs (tokens streamed to the clients step by step from pinned copies,
+    LLMEngine._run_streamed) produce exactly the single-step token stream."""
     prompts = ["one", "two three", "four five six", "seven"]
     a = _run(_eng(tiny_model_path, 1), prompts, **sp)
-    b = _run(_eng(tiny_model_path, 8), prompts, **sp)
+    e8 = _eng(tiny_model_path, 8)
+    b = _run(e8, prompts, **sp)
     for x, y in zip(a, b):
         assert x[1] == y[1] == sp["max_tokens"]
         assert x[0] == y[0]
+    assert any("hist_pin" in g[1] for g in e8._graphs.values()), "the streamed run path did not run"
 
 
 def test_wide_batch_decode_steps_match_single_step(tiny_model_path):
