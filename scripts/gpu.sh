@@ -60,12 +60,18 @@ case $task in
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 &&
       run_bench bench1 && run_bench bench2 ;;
   prof)
+    # kernel trace of one timed wave (engine or HTTP per the bench args) -> summary.md: whole-run
+    # table, decode steady state per step and per (kernel, grid) (scripts/prof_summary.py)
     cd /tmp && export TMPDIR=/tmp
+    rm -rf /tmp/prof
     timeout -k 10 600 rocprofv3 --kernel-trace --stats -d /tmp/prof -o run --output-format csv -- \
-      python3 "$R/bench.py" --steps 5 --warmup 2 "$@" > "$R/$O/prof.log" 2>&1
+      python3 "$R/bench.py" --steps 1 --warmup 1 "$@" > "$R/$O/prof.log" 2>&1
     rc=$?
-    cp $(find /tmp/prof -name "*kernel_stats.csv" | head -1) "$R/$O/kernel_stats.csv" 2>/dev/null
-    tail -2 "$R/$O/prof.log"
+    cd "$R"
+    cp $(find /tmp/prof -name "*kernel_stats.csv" | head -1) "$O/kernel_stats.csv" 2>/dev/null
+    [ $rc -eq 0 ] && python3 scripts/prof_summary.py /tmp/prof "${PROF_TITLE:-kernel trace: bench.py $*}" \
+      --steady 32 --by-grid 32 > "$O/summary.md"
+    tail -2 "$O/prof.log"
     exit $rc ;;
   pmc)
     bash scripts/gpu_pmc_run.sh "$1" "$O" ;;
