@@ -236,7 +236,7 @@ def test_q32_two_segments_one_launch(var):
 
 
 @pytest.mark.parametrize("t", [GGMLType.Q4_K, GGMLType.Q6_K, GGMLType.Q8_0])
-@pytest.mark.parametrize("var", [0, 2, 4, 5, 7, 8, 9])
+@pytest.mark.parametrize("var", [0, 1, 2, 4, 5, 7, 8, 9])
 def test_q32_glu(t, var):
     """gate|up with SwiGLU / GeGLU in the q32 epilogue vs fp32 (two weights, and the halves of
     one fused [2F, K] weight)."""
