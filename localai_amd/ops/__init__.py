@@ -15,6 +15,7 @@ import functools
 import math
 import os
 import threading
+import warnings
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -190,7 +191,11 @@ class QWeight:
             fmt = {GGMLType.Q4_K: FMT_Q4_K, GGMLType.Q6_K: FMT_Q6_K, GGMLType.Q8_0: FMT_Q8_0}.get(t, FMT_BF16)
             return QWeight(fmt, N, K, (None, None, None, None), ref=ref)
         ref = torch.from_numpy(dequantize(raw, t, (N, K)).astype(np.float32)) if keep_ref else None
-        src = torch.from_numpy(np.ascontiguousarray(raw)).to(device, non_blocking=False)
+        with warnings.catch_warnings():
+            # raw is usually a read-only view of the mmapped GGUF; the host tensor is only read
+            # by the device copy, so wrap it without a host-side copy of the payload
+            warnings.filterwarnings("ignore", message="The given NumPy array is not writable")
+            src = torch.from_numpy(np.ascontiguousarray(raw)).to(device, non_blocking=False)
         if t == GGMLType.Q4_K and K % 256 == 0:
             b = src.view(N, K // 256, 144)
             qs = b[:, :, 16:].contiguous().view(N, K // 2)
